@@ -1,0 +1,245 @@
+// K6: paged decode attention (one query token per sequence), GQA, split-K.
+//
+// Grid (Hkv, B, S): one workgroup per (kv head, sequence, key split); 4 waves.
+// All G = Hq/Hkv query heads of a kv head are processed together so every K/V
+// byte is read from HBM exactly once per step (decode is KV-bandwidth bound).
+//
+// Per 16-key tile (bs is a multiple of 16; a tile never straddles a page):
+//   S^T[16 keys][16 heads] = K_tile . Q^T  on one MFMA chain
+//     v_mfma_f32_16x16x32_bf16, A = K rows (16 B contiguous per lane, loaded
+//     straight from the paged cache into the A-fragment layout: no LDS),
+//     B = Q^T (resident in registers, heads >= G zero-padded);
+//   online softmax per head: lane&15 is the head, its 16 keys sit in 4 regs x
+//     4 lane groups -> 2 xor-shuffles;
+//   O[h][d] += P[h][k] V[k][d] on the VALU: lane (g, c) owns 8 dims (16-B V
+//     loads) and KG key sub-groups; P goes through a 1 KiB wave-private LDS tile.
+// Waves stride over tiles; the 4 wave states (m, l, O) merge through LDS at the
+// end. With S > 1 each split writes (O/l, lse) and decode_combine reduces.
+#include "common.h"
+
+namespace xgk {
+
+template <int D, int G>
+struct DecodeCfg {
+  static constexpr int KK = D / 32;       // MFMA k-steps over the head dim
+  static constexpr int CPL = D / 8;       // lanes that cover one V row (8 dims each)
+  static constexpr int KG = 64 / CPL;     // key groups in the PV phase
+  static constexpr int KPG = 16 / KG;     // keys per group per tile
+  static constexpr int WAVES = 4;
+};
+
+template <int D, int G>
+__global__ void __launch_bounds__(256) decode_attn_kernel(
+    const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int bt_stride,
+    const int32_t* __restrict__ seq_lens, float* __restrict__ part_out, float* __restrict__ part_lse,
+    uint16_t* __restrict__ out, int64_t out_stride, int Hq, int Hkv, int bs, float scale, int num_splits) {
+  using C = DecodeCfg<D, G>;
+  const int kvh = blockIdx.x, b = blockIdx.y, split = blockIdx.z;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int L = seq_lens[b];
+  const int ntiles = (L + 15) >> 4;
+  const int tps = (ntiles + num_splits - 1) / num_splits;
+  const int t_begin = split * tps;
+  const int t_end = min(ntiles, t_begin + tps);
+
+  __shared__ float p_lds[C::WAVES][16][16];
+  __shared__ float alpha_lds[C::WAVES][16];
+  __shared__ float m_lds[C::WAVES][16], l_lds[C::WAVES][16];
+  __shared__ float o_lds[C::WAVES][G][D];
+
+  // ---- Q^T fragment: lane holds Q[head = lane&15][32kk + 8(lane>>4) + j]
+  const int qh = lane & 15;
+  bf16x8_t qf[C::KK];
+  {
+    const uint16_t* qp = q + static_cast<int64_t>(b) * q_stride + static_cast<int64_t>(kvh * G + qh) * D;
+#pragma unroll
+    for (int kk = 0; kk < C::KK; ++kk) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (qh < G) v = ld16(qp + kk * 32 + 8 * (lane >> 4));
+      qf[kk] = as_frag(v);
+    }
+  }
+
+  const int g = lane / C::CPL, c = lane % C::CPL;  // PV role: key group g, dims 8c..8c+7
+  float m = -INFINITY, l = 0.f;                    // per head (lane&15)
+  float acc[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[h][i] = 0.f;
+
+  const int32_t* bt = block_tables + static_cast<int64_t>(b) * bt_stride;
+  const int64_t head_stride = static_cast<int64_t>(bs) * D;  // one (page, kv head) run
+
+  for (int t = t_begin + wid; t < t_end; t += C::WAVES) {
+    const int key0 = t * 16;
+    const int page = bt[key0 / bs];
+    const int poff = key0 % bs;
+    const int64_t base = (static_cast<int64_t>(page) * Hkv + kvh) * head_stride + static_cast<int64_t>(poff) * D;
+    // issue all loads of the tile first (K fragment + this lane's V rows)
+    uint4 kf[C::KK];
+    const uint16_t* kp = kc + base + (lane & 15) * D + 8 * (lane >> 4);
+#pragma unroll
+    for (int kk = 0; kk < C::KK; ++kk) kf[kk] = ld16(kp + kk * 32);
+    uint4 vv[C::KPG];
+#pragma unroll
+    for (int i = 0; i < C::KPG; ++i) vv[i] = ld16(vc + base + (g * C::KPG + i) * D + c * 8);
+
+    f32x4_t s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < C::KK; ++kk) s = mfma16x16x32(as_frag(kf[kk]), qf[kk], s);
+
+    // s[r] = S[key = key0 + 4*(lane>>4) + r][head = lane&15]
+    float sv[4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = key0 + 4 * (lane >> 4) + r;
+      sv[r] = key < L ? s[r] * scale : -INFINITY;
+      mx = fmaxf(mx, sv[r]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m, mx);
+    const float alpha = __expf(m - m_new);  // m = -inf on the first tile -> 0
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sv[r] = __expf(sv[r] - m_new);
+      ps += sv[r];
+    }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * alpha + ps;
+    m = m_new;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p_lds[wid][4 * (lane >> 4) + r][lane & 15] = sv[r];
+    if (lane < 16) alpha_lds[wid][lane] = alpha;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      const float a = alpha_lds[wid][h];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[h][i] *= a;
+    }
+#pragma unroll
+    for (int i = 0; i < C::KPG; ++i) {
+      float vf[8];
+      unpack8(vv[i], vf);
+      const int kr = g * C::KPG + i;
+#pragma unroll
+      for (int h = 0; h < G; ++h) {
+        const float p = p_lds[wid][kr][h];
+#pragma unroll
+        for (int d = 0; d < 8; ++d) acc[h][d] += p * vf[d];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // ---- reduce PV partials over key groups (lanes with the same c)
+#pragma unroll
+  for (int h = 0; h < G; ++h)
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      float v = acc[h][d];
+#pragma unroll
+      for (int o = C::CPL; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+      acc[h][d] = v;
+    }
+  if (lane < 16) {
+    m_lds[wid][lane] = m;
+    l_lds[wid][lane] = l;
+  }
+  if (lane < C::CPL) {
+#pragma unroll
+    for (int h = 0; h < G; ++h)
+#pragma unroll
+      for (int d = 0; d < 8; ++d) o_lds[wid][h][c * 8 + d] = acc[h][d];
+  }
+  __syncthreads();
+
+  // ---- merge the 4 wave states; thread -> (head, dim)
+  for (int idx = threadIdx.x; idx < G * D; idx += blockDim.x) {
+    const int h = idx / D, d = idx % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < C::WAVES; ++w) M = fmaxf(M, m_lds[w][h]);
+    float Ls = 0.f, O = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int w = 0; w < C::WAVES; ++w) {
+        const float e = __expf(m_lds[w][h] - M);
+        Ls += l_lds[w][h] * e;
+        O += o_lds[w][h][d] * e;
+      }
+    }
+    const int qhead = kvh * G + h;
+    const float res = Ls > 0.f ? O / Ls : 0.f;
+    if (num_splits == 1) {
+      out[static_cast<int64_t>(b) * out_stride + static_cast<int64_t>(qhead) * D + d] = f2bf(res);
+    } else {
+      const int64_t pi = (static_cast<int64_t>(b) * Hq + qhead) * num_splits + split;
+      part_out[pi * D + d] = res;
+      if (d == 0) part_lse[pi] = Ls > 0.f ? M + __logf(Ls) : -INFINITY;
+    }
+  }
+}
+
+// Split-K reduction: out[b, h, :] = sum_s softmax(lse)_s * part_out[b, h, s, :]
+template <int D>
+__global__ void __launch_bounds__(D) decode_combine_kernel(const float* __restrict__ part_out,
+                                                           const float* __restrict__ part_lse,
+                                                           uint16_t* __restrict__ out, int64_t out_stride,
+                                                           int Hq, int num_splits) {
+  const int bh = blockIdx.x;
+  const int b = bh / Hq, h = bh % Hq;
+  const float* lse = part_lse + static_cast<int64_t>(bh) * num_splits;
+  float M = -INFINITY;
+  for (int s = 0; s < num_splits; ++s) M = fmaxf(M, lse[s]);
+  float den = 0.f, acc = 0.f;
+  if (M != -INFINITY) {
+    for (int s = 0; s < num_splits; ++s) {
+      const float w = __expf(lse[s] - M);
+      den += w;
+      acc += w * part_out[(static_cast<int64_t>(bh) * num_splits + s) * D + threadIdx.x];
+    }
+  }
+  out[static_cast<int64_t>(b) * out_stride + static_cast<int64_t>(h) * D + threadIdx.x] =
+      f2bf(den > 0.f ? acc / den : 0.f);
+}
+
+template <int D, int G>
+static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, const uint16_t* vc,
+                          const int32_t* bt, int bts, const int32_t* sl, float* po, float* pl, uint16_t* out,
+                          int64_t os, int B, int Hq, int Hkv, int bs, float scale, int S, hipStream_t st) {
+  hipLaunchKernelGGL((decode_attn_kernel<D, G>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt, bts, sl,
+                     po, pl, out, os, Hq, Hkv, bs, scale, S);
+  if (S > 1)
+    hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
+}
+
+// returns 0 on success, -1 for an unsupported (D, G) combination
+int decode_attention(const uint16_t* q, int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
+                     const int32_t* bt, int bt_stride, const int32_t* seq_lens, float* part_out, float* part_lse,
+                     uint16_t* out, int64_t out_stride, int B, int Hq, int Hkv, int D, int bs, float scale,
+                     int num_splits, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (bs % 16 != 0 || Hq % Hkv != 0) return -1;
+  const int G = Hq / Hkv;
+#define XGK_DEC(DD, GG)                                                                                  \
+  if (D == DD && G == GG) {                                                                              \
+    launch_decode<DD, GG>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, part_out, part_lse, out, out_stride, \
+                          B, Hq, Hkv, bs, scale, num_splits, st);                                       \
+    return 0;                                                                                            \
+  }
+  XGK_DEC(128, 1) XGK_DEC(128, 2) XGK_DEC(128, 4) XGK_DEC(128, 8) XGK_DEC(128, 16)
+  XGK_DEC(64, 1) XGK_DEC(64, 2) XGK_DEC(64, 4) XGK_DEC(64, 8)
+#undef XGK_DEC
+  return -1;
+}
+
+}  // namespace xgk

@@ -1,0 +1,158 @@
+// pybind11 entry points of xgserve._kernels. Every op takes raw device pointers
+// (tensor.data_ptr()) and the hipStream_t of the caller's current torch stream,
+// so launches are graph-capturable and there is no dependence on torch's C++ ABI.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+
+namespace xgk {
+void rmsnorm(const uint16_t*, const uint16_t*, uint16_t*, int, int, float, int64_t, int64_t, hipStream_t);
+void fused_add_rmsnorm(const uint16_t*, uint16_t*, const uint16_t*, uint16_t*, int, int, float, hipStream_t);
+void layernorm(const uint16_t*, const uint16_t*, const uint16_t*, uint16_t*, int, int, float, hipStream_t);
+void silu_and_mul(const uint16_t*, uint16_t*, int, int, hipStream_t);
+void gelu_tanh(const uint16_t*, uint16_t*, int64_t, hipStream_t);
+int rope_cache(uint16_t*, int64_t, const int32_t*, const float*, uint16_t*, uint16_t*, const int32_t*, int, int, int,
+               int, int, int, hipStream_t);
+int decode_attention(const uint16_t*, int64_t, const uint16_t*, const uint16_t*, const int32_t*, int, const int32_t*,
+                     float*, float*, uint16_t*, int64_t, int, int, int, int, int, float, int, hipStream_t);
+int prefill_attention(const uint16_t*, int64_t, const uint16_t*, const uint16_t*, const int32_t*, int, const int32_t*,
+                      const int32_t*, uint16_t*, int64_t, int, int, int, int, int, int, float, hipStream_t);
+void argmax_logprob(const void*, int, int64_t, int, int, int32_t*, float*, hipStream_t);
+void sample_tokens(const void*, int, int64_t, int, int, const float*, const float*, const int32_t*, const uint64_t*,
+                   uint64_t, int32_t*, float*, hipStream_t);
+void segment_sum(const uint16_t*, int, const int32_t*, const int32_t*, float*, int, hipStream_t);
+void moe_topk_softmax(const void*, int, int, int, int, int, float*, int32_t*, hipStream_t);
+void moe_align(const int32_t*, int, int, int, int, int32_t*, int32_t*, int32_t*, int32_t*, hipStream_t);
+void moe_grouped_gemm(const uint16_t*, const int32_t*, const uint16_t*, uint16_t*, const int32_t*, const int32_t*,
+                      int, int, int, int, int, int, hipStream_t);
+void moe_silu_mul_gather(const uint16_t*, uint16_t*, int, int, hipStream_t);
+void moe_combine(const uint16_t*, const int32_t*, const float*, uint16_t*, int, int, int, hipStream_t);
+}  // namespace xgk
+
+template <typename T>
+static T* P(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static void check(int rc, const char* what) {
+  if (rc != 0) throw std::invalid_argument(std::string(what) + ": unsupported shape/config");
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+PYBIND11_MODULE(_kernels, m) {
+  m.doc() = "xgserve hand-written CDNA4 (gfx950) HIP kernels";
+  m.attr("arch") = "gfx950";
+
+  m.def("rmsnorm", [](uintptr_t x, uintptr_t w, uintptr_t out, int T, int H, float eps, int64_t xs, int64_t os,
+                      uintptr_t st) {
+    if (H % 8) throw std::invalid_argument("rmsnorm: H % 8 != 0");
+    xgk::rmsnorm(P<const uint16_t>(x), P<const uint16_t>(w), P<uint16_t>(out), T, H, eps, xs, os, S(st));
+    check(0, "rmsnorm");
+  });
+  m.def("fused_add_rmsnorm", [](uintptr_t x, uintptr_t res, uintptr_t w, uintptr_t out, int T, int H, float eps,
+                                uintptr_t st) {
+    if (H % 8) throw std::invalid_argument("fused_add_rmsnorm: H % 8 != 0");
+    xgk::fused_add_rmsnorm(P<const uint16_t>(x), P<uint16_t>(res), P<const uint16_t>(w), P<uint16_t>(out), T, H,
+                           eps, S(st));
+    check(0, "fused_add_rmsnorm");
+  });
+  m.def("layernorm", [](uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t out, int T, int H, float eps,
+                        uintptr_t st) {
+    if (H % 8) throw std::invalid_argument("layernorm: H % 8 != 0");
+    xgk::layernorm(P<const uint16_t>(x), P<const uint16_t>(w), P<const uint16_t>(b), P<uint16_t>(out), T, H, eps,
+                   S(st));
+    check(0, "layernorm");
+  });
+  m.def("silu_and_mul", [](uintptr_t in, uintptr_t out, int T, int F, uintptr_t st) {
+    if (F % 8) throw std::invalid_argument("silu_and_mul: F % 8 != 0");
+    xgk::silu_and_mul(P<const uint16_t>(in), P<uint16_t>(out), T, F, S(st));
+    check(0, "silu_and_mul");
+  });
+  m.def("gelu_tanh", [](uintptr_t in, uintptr_t out, int64_t n, uintptr_t st) {
+    if (n % 8) throw std::invalid_argument("gelu_tanh: n % 8 != 0");
+    xgk::gelu_tanh(P<const uint16_t>(in), P<uint16_t>(out), n, S(st));
+    check(0, "gelu_tanh");
+  });
+  m.def("rope_cache", [](uintptr_t qkv, int64_t row_stride, uintptr_t pos, uintptr_t cs, uintptr_t kc, uintptr_t vc,
+                         uintptr_t slots, int T, int Hq, int Hkv, int D, int bs, int apply_rope, uintptr_t st) {
+    check(xgk::rope_cache(P<uint16_t>(qkv), row_stride, P<const int32_t>(pos), P<const float>(cs), P<uint16_t>(kc),
+                          P<uint16_t>(vc), P<const int32_t>(slots), T, Hq, Hkv, D, bs, apply_rope, S(st)),
+          "rope_cache");
+  });
+  m.def("decode_attention", [](uintptr_t q, int64_t qs, uintptr_t kc, uintptr_t vc, uintptr_t bt, int bts,
+                               uintptr_t sl, uintptr_t po, uintptr_t pl, uintptr_t out, int64_t os, int B, int Hq,
+                               int Hkv, int D, int bs, float scale, int splits, uintptr_t st) {
+    check(xgk::decode_attention(P<const uint16_t>(q), qs, P<const uint16_t>(kc), P<const uint16_t>(vc),
+                                P<const int32_t>(bt), bts, P<const int32_t>(sl), P<float>(po), P<float>(pl),
+                                P<uint16_t>(out), os, B, Hq, Hkv, D, bs, scale, splits, S(st)),
+          "decode_attention");
+  });
+  m.def("prefill_attention", [](uintptr_t q, int64_t qs, uintptr_t kc, uintptr_t vc, uintptr_t bt, int bts,
+                                uintptr_t qsl, uintptr_t sl, uintptr_t out, int64_t os, int ns, int maxq, int Hq,
+                                int Hkv, int D, int bs, float scale, uintptr_t st) {
+    check(xgk::prefill_attention(P<const uint16_t>(q), qs, P<const uint16_t>(kc), P<const uint16_t>(vc),
+                                 P<const int32_t>(bt), bts, P<const int32_t>(qsl), P<const int32_t>(sl),
+                                 P<uint16_t>(out), os, ns, maxq, Hq, Hkv, D, bs, scale, S(st)),
+          "prefill_attention");
+  });
+  m.def("argmax_logprob", [](uintptr_t logits, int is_f32, int64_t stride, int B, int V, uintptr_t tok, uintptr_t lp,
+                             uintptr_t st) {
+    xgk::argmax_logprob(P<const void>(logits), is_f32, stride, B, V, P<int32_t>(tok), P<float>(lp), S(st));
+    check(0, "argmax_logprob");
+  });
+  m.def("sample_tokens", [](uintptr_t logits, int is_f32, int64_t stride, int B, int V, uintptr_t temps,
+                            uintptr_t top_ps, uintptr_t top_ks, uintptr_t seeds, uint64_t step, uintptr_t tok,
+                            uintptr_t lp, uintptr_t st) {
+    xgk::sample_tokens(P<const void>(logits), is_f32, stride, B, V, P<const float>(temps), P<const float>(top_ps),
+                       P<const int32_t>(top_ks), P<const uint64_t>(seeds), step, P<int32_t>(tok), P<float>(lp), S(st));
+    check(0, "sample_tokens");
+  });
+  m.def("segment_sum", [](uintptr_t hidden, int H, uintptr_t cu, uintptr_t rows, uintptr_t out, int nseg,
+                          uintptr_t st) {
+    if (H % 8) throw std::invalid_argument("segment_sum: H % 8 != 0");
+    xgk::segment_sum(P<const uint16_t>(hidden), H, P<const int32_t>(cu), P<const int32_t>(rows), P<float>(out), nseg,
+                     S(st));
+    check(0, "segment_sum");
+  });
+  m.def("moe_topk_softmax", [](uintptr_t logits, int is_f32, int T, int E, int k, int renorm, uintptr_t w,
+                               uintptr_t ids, uintptr_t st) {
+    xgk::moe_topk_softmax(P<const void>(logits), is_f32, T, E, k, renorm, P<float>(w), P<int32_t>(ids), S(st));
+    check(0, "moe_topk_softmax");
+  });
+  m.def("moe_align", [](uintptr_t ids, int T, int k, int E, int block_m, uintptr_t sorted_rows,
+                        uintptr_t expert_offsets, uintptr_t tile_expert, uintptr_t dest, uintptr_t st) {
+    xgk::moe_align(P<const int32_t>(ids), T, k, E, block_m, P<int32_t>(sorted_rows), P<int32_t>(expert_offsets),
+                   P<int32_t>(tile_expert), P<int32_t>(dest), S(st));
+    check(0, "moe_align");
+  });
+  m.def("moe_grouped_gemm", [](uintptr_t x, uintptr_t rows, uintptr_t w, uintptr_t out, uintptr_t offs,
+                               uintptr_t tile_expert, int max_tiles, int N, int K, int gather, int x_rows,
+                               int num_experts, uintptr_t st) {
+    if (K % 64 || N % 64) throw std::invalid_argument("moe_grouped_gemm: N, K must be multiples of 64");
+    xgk::moe_grouped_gemm(P<const uint16_t>(x), P<const int32_t>(rows), P<const uint16_t>(w), P<uint16_t>(out),
+                          P<const int32_t>(offs), P<const int32_t>(tile_expert), max_tiles, N, K, gather, x_rows,
+                          num_experts, S(st));
+    check(0, "moe_grouped_gemm");
+  });
+  m.def("moe_silu_mul", [](uintptr_t in, uintptr_t out, int rows, int F, uintptr_t st) {
+    xgk::moe_silu_mul_gather(P<const uint16_t>(in), P<uint16_t>(out), rows, F, S(st));
+    check(0, "moe_silu_mul");
+  });
+  m.def("moe_combine", [](uintptr_t y, uintptr_t dest, uintptr_t w, uintptr_t out, int T, int k, int H,
+                          uintptr_t st) {
+    xgk::moe_combine(P<const uint16_t>(y), P<const int32_t>(dest), P<const float>(w), P<uint16_t>(out), T, k, H,
+                     S(st));
+    check(0, "moe_combine");
+  });
+  m.def("device_synchronize", []() {
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) throw std::runtime_error(hipGetErrorString(e));
+  });
+}
