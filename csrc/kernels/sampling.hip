@@ -174,8 +174,9 @@ __global__ void __launch_bounds__(1024) sample_kernel(const T* __restrict__ logi
 
   // pass 2: Gumbel-max draw over kept tokens
   const uint64_t seed = seeds ? seeds[blockIdx.x] : 0x9E3779B97F4A7C15ull;
+  // the stream depends only on (seed, step): rows that share a seed draw identically
   const uint32_t key = hash32(static_cast<uint32_t>(seed) ^ hash32(static_cast<uint32_t>(seed >> 32) + 0x85ebca6bU) ^
-                              hash32(static_cast<uint32_t>(step) * 0x27d4eb2fU + blockIdx.x));
+                              hash32(static_cast<uint32_t>(step) * 0x27d4eb2fU + 0x165667b1U));
   ArgLse a{-INFINITY, 0x7fffffff, -INFINITY, 0.f};
   for (int i = threadIdx.x; i < V; i += blockDim.x) {
     const float x = scalar_at<T>(row, i) * it;

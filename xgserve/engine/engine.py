@@ -1,0 +1,403 @@
+"""LLMEngine: one model replica (a TP group) with continuous batching.
+
+Per step: the C++ StepScheduler packs decode tokens + prefill chunks under a
+token budget (prefix-cache aware, preempting on KV exhaustion) -> the TP leader
+broadcasts the plan to its followers -> every rank runs the forward (HIP graph
+for pure decode) -> the leader samples, feeds tokens back to the scheduler and
+produces RequestOutputs (incremental text, stop strings, finish reasons,
+embeddings for prefill-only requests).
+
+This realises the reference's spec'd worker interface
+(`InferenceWorker::initialize/infer/shutdown/status/model_info`,
+design.md:335-342) at iteration granularity: `infer(batch)` returning N results
+(Property 21) is `generate()` on top of `step()`; per-request failures are
+isolated (Property 22) because a failing request is aborted alone.
+"""
+from __future__ import annotations
+
+import itertools
+import logging
+import math
+import os
+import threading
+import time
+from dataclasses import asdict, dataclass, field
+from typing import Dict, Iterable, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import _runtime as R
+from ..models import build_model, get_config
+from ..parallel import comm
+from ..parallel.state import get_state
+from .request import (FINISH_ABORT, FINISH_EMBED, FINISH_LENGTH, FINISH_NAMES, FINISH_STOP, FINISH_STOP_SEQ,
+                      EngineRequest, RequestOutput, RequestType, SamplingParams)
+from .runner import ModelRunner, SamplingRows
+from .tokenizer import IncrementalDetokenizer, load_tokenizer
+
+log = logging.getLogger("xgserve.engine")
+
+_MASK63 = (1 << 63) - 1
+
+
+def _mix(seed: int, n: int) -> int:
+    x = (seed * 6364136223846793005 + (n + 1) * 1442695040888963407) & _MASK63
+    x ^= x >> 29
+    return (x * 0xBF58476D1CE4E5B9) & _MASK63
+
+
+@dataclass
+class EngineConfig:
+    model: str = "llama3-8b"
+    checkpoint: Optional[str] = None
+    tp: int = 1
+    device: Optional[str] = None
+    dtype: Optional[str] = None
+    block_size: int = 16
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 8192
+    max_model_len: Optional[int] = None
+    gpu_memory_utilization: float = 0.90
+    num_blocks: Optional[int] = None
+    enable_prefix_cache: bool = True
+    chunked_prefill: bool = True
+    cache_threshold: float = 0.8
+    use_graphs: bool = True
+    graph_batch_sizes: Optional[List[int]] = None
+    seed: int = 0
+    moe_comm: str = "alltoall"
+    max_prefill_seqs: int = 1 << 30
+    # speculative decoding (Req 12)
+    draft_model: Optional[str] = None
+    num_speculative_tokens: int = 0
+
+    def resolved_device(self) -> torch.device:
+        if self.device:
+            return torch.device(self.device)
+        return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, model=None):
+        self.cfg = cfg
+        self.mcfg = get_config(cfg.checkpoint or cfg.model) if model is None else model.cfg
+        if cfg.checkpoint and model is None:
+            self.mcfg.name = cfg.model if cfg.model else self.mcfg.name
+        st = get_state()
+        self.tp_rank = st.tp_rank
+        self.is_driver = st.tp_rank == 0
+        device = cfg.resolved_device()
+        dtype = {"bfloat16": torch.bfloat16, "float32": torch.float32, "float16": torch.float16,
+                 None: None}[cfg.dtype]
+        t0 = time.time()
+        self.model = model if model is not None else build_model(self.mcfg, device=device, dtype=dtype,
+                                                                 checkpoint=cfg.checkpoint, seed=cfg.seed)
+        self.model.set_moe_comm(cfg.moe_comm)
+        self.load_time = time.time() - t0
+        self.device = self.model.device
+        self.max_model_len = min(cfg.max_model_len or self.mcfg.max_position, self.mcfg.max_position)
+        self.tokenizer = load_tokenizer(self.mcfg, cfg.checkpoint)
+        num_blocks = cfg.num_blocks or self._auto_num_blocks()
+        self.num_blocks = num_blocks
+        sc = R.SchedulerConfig()
+        sc.block_size = cfg.block_size
+        sc.num_blocks = num_blocks
+        sc.max_num_seqs = cfg.max_num_seqs
+        sc.max_num_batched_tokens = cfg.max_num_batched_tokens
+        sc.max_model_len = self.max_model_len
+        sc.enable_prefix_cache = cfg.enable_prefix_cache
+        sc.chunked_prefill = cfg.chunked_prefill
+        sc.cache_threshold = cfg.cache_threshold
+        sc.max_prefill_seqs = cfg.max_prefill_seqs
+        sc.eos_ids = list(self.mcfg.eos_token_ids)
+        self.sched = R.StepScheduler(sc)
+        self.runner = ModelRunner(self.model, block_size=cfg.block_size, num_blocks=num_blocks,
+                                  max_num_seqs=cfg.max_num_seqs, max_num_batched_tokens=cfg.max_num_batched_tokens,
+                                  max_model_len=self.max_model_len, use_graphs=cfg.use_graphs,
+                                  graph_batch_sizes=cfg.graph_batch_sizes, is_driver=self.is_driver)
+        self.runner.capture_graphs()
+        H = self.mcfg.hidden_size
+        self.embed_acc = torch.zeros(cfg.max_num_seqs, H, dtype=torch.float32, device=self.device)
+        self.requests: Dict[str, EngineRequest] = {}
+        self.by_seq: Dict[int, EngineRequest] = {}
+        self._seq_counter = itertools.count(1)
+        self._lock = threading.Lock()
+        self._pending_aborts: List[str] = []
+        self.step_count = 0
+        self.stats_counters = {"prompt_tokens": 0, "generation_tokens": 0, "steps": 0, "decode_steps": 0,
+                               "prefill_tokens_computed": 0, "requests_finished": 0, "preemptions": 0}
+        self.spec = None
+        if cfg.draft_model and cfg.num_speculative_tokens > 0:
+            from .spec_decode import SpeculativeDecoder
+            self.spec = SpeculativeDecoder(self, cfg.draft_model, cfg.num_speculative_tokens)
+        log.info("engine ready: model=%s tp=%d blocks=%d (%.1f GiB KV) load=%.1fs", self.mcfg.name, get_state().tp_size,
+                 num_blocks, self.runner.kv_bytes() / 2**30, self.load_time)
+
+    # ------------------------------------------------------------------ sizing
+    def _block_bytes(self) -> int:
+        m = self.mcfg
+        esz = torch.tensor([], dtype=self.model.dtype).element_size()
+        return 2 * m.num_layers * self.model.num_kv_heads_local * self.cfg.block_size * m.head_dim * esz
+
+    def _auto_num_blocks(self) -> int:
+        if self.device.type != "cuda":
+            return 512
+        torch.cuda.synchronize()
+        free, total = torch.cuda.mem_get_info()
+        m = self.mcfg
+        act = self.cfg.max_num_batched_tokens * (6 * m.hidden_size + 4 * m.intermediate_size // max(1, get_state().tp_size)) * 2
+        act += self.cfg.max_num_seqs * m.vocab_size * 8 + (2 << 30)
+        budget = free - (1.0 - self.cfg.gpu_memory_utilization) * total - act
+        n = int(max(64, budget // self._block_bytes()))
+        st = get_state()
+        if st.tp_size > 1:
+            t = torch.tensor([n], dtype=torch.int64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN, group=st.tp_cpu_group)
+            n = int(t.item())
+        return n
+
+    # ------------------------------------------------------------------ requests
+    def add_request(self, request_id: str, prompt_ids: Sequence[int], params: SamplingParams,
+                    priority: int = 1, kind: RequestType = RequestType.Generate, user_data=None) -> EngineRequest:
+        prompt_ids = [int(t) for t in prompt_ids]
+        if not prompt_ids:
+            raise ValueError("empty prompt")
+        max_tokens = params.max_tokens
+        if kind != RequestType.Embeddings:
+            max_tokens = min(max_tokens, self.max_model_len - len(prompt_ids))
+        if kind != RequestType.Embeddings and len(prompt_ids) >= self.max_model_len:
+            raise ValueError(f"prompt of {len(prompt_ids)} tokens exceeds max_model_len={self.max_model_len}")
+        if kind == RequestType.Embeddings and len(prompt_ids) > self.max_model_len:
+            raise ValueError(f"input of {len(prompt_ids)} tokens exceeds max_model_len={self.max_model_len}")
+        seq_id = next(self._seq_counter)
+        req = EngineRequest(request_id=request_id, seq_id=seq_id, prompt_ids=prompt_ids, params=params,
+                            priority=priority, kind=kind, user_data=user_data)
+        req.detok = IncrementalDetokenizer(self.tokenizer, params.stop)
+        if params.seed is None:
+            params.seed = (hash(request_id) ^ (seq_id * 0x9E3779B97F4A7C15)) & _MASK63
+        with self._lock:
+            ok = self.sched.add(seq_id, prompt_ids, max(0, max_tokens), priority, params.ignore_eos,
+                                kind == RequestType.Embeddings, params.stop_token_ids, params.min_tokens)
+            if not ok:
+                raise ValueError("scheduler rejected the request (duplicate id or too long)")
+            self.requests[request_id] = req
+            self.by_seq[seq_id] = req
+        self.stats_counters["prompt_tokens"] += len(prompt_ids)
+        if max_tokens <= 0 and kind != RequestType.Embeddings:
+            self.abort(request_id, reason=FINISH_LENGTH)
+        return req
+
+    def abort(self, request_id: str, reason: int = FINISH_ABORT) -> bool:
+        with self._lock:
+            req = self.requests.get(request_id)
+            if req is None or req.finished:
+                return False
+            self.sched.abort(req.seq_id)
+            self._finish(req, reason)
+            self._pending_aborts.append(request_id)
+        return True
+
+    def _finish(self, req: EngineRequest, reason: int):
+        req.finished = True
+        req.finish_reason = FINISH_NAMES.get(reason, "stop")
+        req.finish_time = time.monotonic()
+        self.requests.pop(req.request_id, None)
+        self.by_seq.pop(req.seq_id, None)
+        self.stats_counters["requests_finished"] += 1
+
+    def has_work(self) -> bool:
+        return self.sched.has_work() or bool(self._pending_aborts)
+
+    # ------------------------------------------------------------------ step
+    def _sampling_rows(self, plan) -> Optional[SamplingRows]:
+        if not self.is_driver:
+            return None
+        idx = plan["sample_seq_index"]
+        n = idx.shape[0]
+        if n == 0:
+            return None
+        sids = plan["seq_ids"][idx]
+        temps = np.empty(n, np.float32)
+        tps = np.empty(n, np.float32)
+        tks = np.empty(n, np.int32)
+        seeds = np.empty(n, np.int64)
+        for i, sid in enumerate(sids.tolist()):
+            r = self.by_seq.get(sid)
+            if r is None:
+                temps[i], tps[i], tks[i], seeds[i] = 0.0, 1.0, 0, 0
+                continue
+            p = r.params
+            temps[i], tps[i], tks[i] = p.temperature, p.top_p, p.top_k
+            seeds[i] = _mix(p.seed, len(r.output_ids))
+        return SamplingRows(temps, tps, tks, seeds)
+
+    def step(self) -> List[RequestOutput]:
+        outs: List[RequestOutput] = []
+        with self._lock:
+            for rid in self._pending_aborts:
+                outs.append(RequestOutput(rid, [], "", True, "abort"))
+            self._pending_aborts.clear()
+            if self.spec is not None:
+                self.spec.propose()
+            plan = self.sched.schedule()
+        st = get_state()
+        if st.tp_size > 1:
+            comm.tp_broadcast_object(("plan", plan), src=0)
+        if plan["num_tokens"] == 0:
+            return outs
+        samp = self._sampling_rows(plan)
+        if self.spec is not None and plan["num_seqs"] > plan["num_decodes"]:
+            return outs + self.spec.verify_step(plan, samp)
+        toks, lps, hidden = self.runner.execute(plan, samp)
+        self.step_count += 1
+        self.stats_counters["steps"] += 1
+        if plan["num_decodes"] == plan["num_seqs"]:
+            self.stats_counters["decode_steps"] += 1
+        self.stats_counters["prefill_tokens_computed"] += int(plan["num_tokens"]) - int(plan["num_decodes"])
+        if hidden is not None:
+            self._accumulate_embeddings(plan, hidden)
+        return outs + self._process(plan, toks, lps)
+
+    def _accumulate_embeddings(self, plan, hidden):
+        from .. import ops
+        emb = np.nonzero(plan["is_embed"])[0]
+        if emb.size == 0:
+            return
+        qsl = plan["query_start_loc"]
+        cu = []
+        rows = []
+        for i in emb.tolist():
+            cu.append((int(qsl[i]), int(qsl[i + 1])))
+            rows.append(int(plan["slots"][i]))
+        for (a, b), r in zip(cu, rows):
+            cut = torch.tensor([a, b], dtype=torch.int32, device=self.device)
+            rr = torch.tensor([r], dtype=torch.int32, device=self.device)
+            ops.segment_sum(hidden, cut, self.embed_acc, rr)
+
+    def _process(self, plan, toks, lps) -> List[RequestOutput]:
+        outs: List[RequestOutput] = []
+        ns = int(plan["num_seqs"])
+        seq_ids = plan["seq_ids"]
+        n_sample = int(plan["num_sample"])
+        counts = np.ones(n_sample, np.int32)
+        now = time.monotonic()
+        with self._lock:
+            finished = self.sched.update(toks if toks is not None else np.zeros(n_sample, np.int32), counts)
+            fin_map = {f[0]: f for f in finished}
+            if not self.is_driver:
+                return outs
+            self.stats_counters["generation_tokens"] += n_sample
+            sidx = plan["sample_seq_index"]
+            for j in range(n_sample):
+                sid = int(seq_ids[sidx[j]])
+                req = self.by_seq.get(sid)
+                if req is None:
+                    continue
+                tok = int(toks[j])
+                if req.first_token_time is None:
+                    req.first_token_time = now
+                req.output_ids.append(tok)
+                text = req.detok.add([tok])
+                f = fin_map.get(sid)
+                reason = None
+                if req.detok.stopped and f is None:
+                    self.sched.abort(sid)
+                    reason = FINISH_STOP_SEQ
+                elif f is not None:
+                    reason = f[1]
+                    req.cached_tokens = f[4]
+                    if not req.detok.stopped:
+                        text += req.detok.flush()
+                out = RequestOutput(req.request_id, [tok], text, reason is not None,
+                                    FINISH_NAMES.get(reason) if reason else None,
+                                    prompt_tokens=len(req.prompt_ids), completion_tokens=len(req.output_ids),
+                                    logprobs=[float(lps[j])] if (lps is not None and req.params.logprobs) else None)
+                if reason is not None:
+                    out.cached_tokens = req.cached_tokens
+                    self._finish(req, reason)
+                outs.append(out)
+            # prefill-only (embedding) completions
+            for sid, f in fin_map.items():
+                if f[1] != FINISH_EMBED:
+                    continue
+                req = self.by_seq.get(sid)
+                if req is None:
+                    continue
+                slot = None
+                for i in range(ns):
+                    if int(seq_ids[i]) == sid:
+                        slot = int(plan["slots"][i])
+                v = self.embed_acc[slot] / max(1, len(req.prompt_ids))
+                v = v / v.norm().clamp_min(1e-12)
+                emb = v.cpu().tolist()
+                self.embed_acc[slot].zero_()
+                outs.append(RequestOutput(req.request_id, [], "", True, "stop", prompt_tokens=len(req.prompt_ids),
+                                          completion_tokens=0, embedding=emb))
+                self._finish(req, FINISH_EMBED)
+        return outs
+
+    # ------------------------------------------------------------------ followers (TP > 1)
+    def follower_loop(self):
+        """Non-leader TP ranks: mirror the leader's steps until told to stop."""
+        while True:
+            kind, payload = comm.tp_broadcast_object(None, src=0)
+            if kind == "stop":
+                return
+            if kind == "plan":
+                plan = payload
+                if plan["num_tokens"]:
+                    self.runner.execute(plan, None)
+            elif kind == "spec":
+                self.spec.follower_step(payload)
+
+    def stop_followers(self):
+        if get_state().tp_size > 1 and self.is_driver:
+            comm.tp_broadcast_object(("stop", None), src=0)
+
+    # ------------------------------------------------------------------ helpers
+    def generate(self, prompts: List[List[int]], params: SamplingParams, max_steps: int = 1 << 30):
+        """Blocking batch generation (tests / offline use). Returns output id lists."""
+        import copy
+        rids = []
+        for i, p in enumerate(prompts):
+            rid = f"gen-{time.monotonic_ns()}-{i}"
+            self.add_request(rid, p, copy.deepcopy(params))
+            rids.append(rid)
+        results = {r: [] for r in rids}
+        done = set()
+        steps = 0
+        while len(done) < len(rids) and steps < max_steps:
+            for o in self.step():
+                if o.request_id in results:
+                    results[o.request_id].extend(o.new_token_ids)
+                    if o.finished:
+                        done.add(o.request_id)
+            steps += 1
+        return [results[r] for r in rids]
+
+    def kv_usage(self) -> float:
+        return self.sched.num_used_blocks() / max(1, self.sched.num_blocks())
+
+    def stats(self) -> dict:
+        cs = self.sched.cache_stats()
+        bb = self._block_bytes()
+        return {
+            "model": self.mcfg.name,
+            "waiting": self.sched.num_waiting(),
+            "running": self.sched.num_running(),
+            "kv_blocks_total": self.sched.num_blocks(),
+            "kv_blocks_used": self.sched.num_used_blocks(),
+            "kv_blocks_free": self.sched.num_free_blocks(),
+            "kv_usage": self.kv_usage(),
+            "memory_used": self.sched.num_used_blocks() * bb,
+            "memory_available": (self.sched.num_free_blocks() + self.sched.num_evictable_blocks()) * bb,
+            "memory_limit": int(self.sched.num_blocks() * bb * self.cfg.cache_threshold),
+            "cache": cs,
+            "preemptions": self.sched.total_preemptions(),
+            **self.stats_counters,
+        }
+
+    def clear_prefix_cache(self):
+        with self._lock:
+            self.sched.clear_prefix_cache()

@@ -1,0 +1,279 @@
+"""Model runner: step plan -> device metadata -> forward -> logits -> sampled tokens.
+
+* The paged KV cache is one zero-initialised HBM tensor [L, 2, NB, Hkv, bs, D]
+  (zero-init: stale pages can never inject NaN into masked lanes), sized from
+  the free HBM left after the weights (gpu_memory_utilization of 288 GB).
+* All per-step int32 metadata of an eager step is packed into ONE pinned host
+  buffer and moved with ONE async H2D copy.
+* Pure-decode steps replay a HIP graph captured per padded batch size; the
+  graph covers embedding -> all layers -> LM head -> sampling, so a decode step
+  is one graph launch + one small H2D + one D2H. Padding rows use slot -1
+  (no KV write) and seq_len 0 (no attention work).
+"""
+from __future__ import annotations
+
+import logging
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.base import AttnMeta
+from ..ops.attention import DecodeWorkspace
+
+log = logging.getLogger("xgserve.runner")
+
+
+@dataclass
+class SamplingRows:
+    """Per-row sampling parameters (host numpy arrays), aligned with logits rows."""
+    temps: np.ndarray
+    top_ps: np.ndarray
+    top_ks: np.ndarray
+    seeds: np.ndarray  # int64, already mixed with the step counter
+
+    @property
+    def all_greedy(self) -> bool:
+        return bool((self.temps <= 0).all())
+
+
+def _pinned(n: int, dtype) -> torch.Tensor:
+    t = torch.empty(n, dtype=dtype)
+    return t.pin_memory() if torch.cuda.is_available() else t
+
+
+class ModelRunner:
+    def __init__(self, model, *, block_size: int, num_blocks: int, max_num_seqs: int,
+                 max_num_batched_tokens: int, max_model_len: int, use_graphs: bool = True,
+                 graph_batch_sizes: Optional[List[int]] = None, is_driver: bool = True):
+        self.model = model
+        self.cfg = model.cfg
+        self.device = model.device
+        self.dtype = model.dtype
+        self.bs = block_size
+        self.num_blocks = num_blocks
+        self.max_num_seqs = max_num_seqs
+        self.max_tokens = max_num_batched_tokens
+        self.max_model_len = max_model_len
+        self.max_blocks_per_seq = (max_model_len + block_size - 1) // block_size + 1
+        self.is_driver = is_driver
+        cfg = self.cfg
+        self.Hkv = model.num_kv_heads_local
+        self.kv = torch.zeros(cfg.num_layers, 2, num_blocks, self.Hkv, block_size, cfg.head_dim,
+                              dtype=self.dtype, device=self.device)
+        self.kv_caches = [(self.kv[i, 0], self.kv[i, 1]) for i in range(cfg.num_layers)]
+        self.is_cuda = self.device.type == "cuda"
+        Hq_local = cfg.num_heads // model.tp
+        self.max_splits = 16
+        self.workspace = DecodeWorkspace(max(max_num_seqs, 1), Hq_local, cfg.head_dim, self.max_splits,
+                                         self.device) if self.is_cuda else None
+        # pinned staging for eager steps
+        cap = 8 * max_num_batched_tokens + 4 * max_num_seqs * (self.max_blocks_per_seq + 4) + 64
+        self.h_stage = _pinned(cap, torch.int32)
+        self.d_stage = torch.empty(cap, dtype=torch.int32, device=self.device)
+        self.h_tok = _pinned(max(max_num_batched_tokens, max_num_seqs), torch.int32)
+        self.h_lp = _pinned(max(max_num_batched_tokens, max_num_seqs), torch.float32)
+        # graphs
+        self.use_graphs = use_graphs and self.is_cuda
+        if graph_batch_sizes is None:
+            graph_batch_sizes = [1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 256]
+        self.graph_bs = sorted(b for b in graph_batch_sizes if b <= max_num_seqs)
+        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self._graph_pool = None
+        self._init_graph_buffers()
+
+    # ------------------------------------------------------------------ utils
+    def kv_bytes(self) -> int:
+        return self.kv.numel() * self.kv.element_size()
+
+    def decode_splits(self, bs: int) -> int:
+        wgs = max(1, bs * self.Hkv)
+        return int(max(1, min(self.max_splits, (512 + wgs - 1) // wgs)))
+
+    # ------------------------------------------------------------------ graph buffers
+    def _init_graph_buffers(self):
+        B = max(self.graph_bs) if self.graph_bs else 1
+        W = self.max_blocks_per_seq
+        self.g_B, self.g_W = B, W
+        # int32 region: ids | pos | slots | sl | bt ; sampling region separate
+        n = 4 * B + B * W
+        self.g_int = torch.zeros(n, dtype=torch.int32, device=self.device)
+        self.g_ids = self.g_int[0:B]
+        self.g_pos = self.g_int[B:2 * B]
+        self.g_slot = self.g_int[2 * B:3 * B]
+        self.g_sl = self.g_int[3 * B:4 * B]
+        self.g_bt = self.g_int[4 * B:4 * B + B * W].view(B, W)
+        self.h_int = _pinned(n, torch.int32)
+        self.g_temp = torch.zeros(B, dtype=torch.float32, device=self.device)
+        self.g_topp = torch.ones(B, dtype=torch.float32, device=self.device)
+        self.g_topk = torch.zeros(B, dtype=torch.int32, device=self.device)
+        self.g_seed = torch.zeros(B, dtype=torch.int64, device=self.device)
+        self.h_samp_f = _pinned(2 * B, torch.float32)
+        self.h_samp_i = _pinned(B, torch.int32)
+        self.h_samp_s = _pinned(B, torch.int64)
+        self.g_out_tok = torch.zeros(B, dtype=torch.int32, device=self.device)
+        self.g_out_lp = torch.zeros(B, dtype=torch.float32, device=self.device)
+        self.g_greedy_graph: Dict[int, bool] = {}
+
+    def _decode_body(self, bs: int, greedy: bool):
+        meta = AttnMeta(num_tokens=bs, num_decodes=bs, positions=self.g_pos[:bs], slot_mapping=self.g_slot[:bs],
+                        dec_block_tables=self.g_bt[:bs], dec_seq_lens=self.g_sl[:bs],
+                        num_splits=self.decode_splits(bs), workspace=self.workspace)
+        h = self.model(self.g_ids[:bs], meta, self.kv_caches)
+        logits = self.model.compute_logits(h)
+        if greedy:
+            ops.argmax_logprob(logits, self.g_out_tok[:bs], self.g_out_lp[:bs])
+        else:
+            tok, lp = ops.sample_tokens(logits, self.g_temp[:bs], self.g_topp[:bs], self.g_topk[:bs],
+                                        self.g_seed[:bs], step=0)
+            self.g_out_tok[:bs].copy_(tok)
+            self.g_out_lp[:bs].copy_(lp)
+
+    @torch.no_grad()
+    def capture_graphs(self):
+        if not self.use_graphs or not self.graph_bs:
+            return
+        torch.cuda.synchronize()
+        # neutral inputs: padding rows (no KV writes, no attention work)
+        self.g_slot.fill_(-1)
+        self.g_sl.fill_(0)
+        self.g_ids.fill_(0)
+        self.g_pos.fill_(0)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for bs in reversed(self.graph_bs):
+                for greedy in (True, False):
+                    for _ in range(2):
+                        self._decode_body(bs, greedy)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self._graph_pool = torch.cuda.graph_pool_handle()
+        for bs in reversed(self.graph_bs):
+            for greedy in (True, False):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self._graph_pool):
+                    self._decode_body(bs, greedy)
+                self.graphs[(bs, greedy)] = g
+        torch.cuda.synchronize()
+        log.info("captured %d decode graphs (batch sizes %s)", len(self.graphs), self.graph_bs)
+
+    def _graph_bucket(self, n: int) -> Optional[int]:
+        for b in self.graph_bs:
+            if b >= n:
+                return b
+        return None
+
+    # ------------------------------------------------------------------ execution
+    @torch.no_grad()
+    def execute(self, plan: dict, samp: Optional[SamplingRows]):
+        """Run one step. Returns (tokens np[int32], logprobs np[float32], hidden or None).
+        On non-driver TP ranks the returned arrays are None."""
+        T = int(plan["num_tokens"])
+        Nd = int(plan["num_decodes"])
+        ns = int(plan["num_seqs"])
+        if T == 0:
+            return None, None, None
+        need_hidden = bool(plan["is_embed"].any()) if ns else False
+        bucket = self._graph_bucket(Nd) if (Nd == ns and T == Nd and not need_hidden) else None
+        if bucket is not None and self.graphs:
+            return self._execute_graph(plan, samp, Nd, bucket)
+        return self._execute_eager(plan, samp, need_hidden)
+
+    def _execute_graph(self, plan, samp: Optional[SamplingRows], n: int, bs: int):
+        B, W = self.g_B, self.g_W
+        hi = self.h_int.numpy()
+        w = int(plan["bt_width"])
+        hi[0:n] = plan["input_ids"]
+        hi[n:bs] = 0
+        hi[B:B + n] = plan["positions"]
+        hi[B + n:B + bs] = 0
+        hi[2 * B:2 * B + n] = plan["slot_mapping"]
+        hi[2 * B + n:2 * B + bs] = -1
+        hi[3 * B:3 * B + n] = plan["seq_lens"]
+        hi[3 * B + n:3 * B + bs] = 0
+        bt = hi[4 * B:4 * B + bs * W].reshape(bs, W)
+        bt[:n, :w] = plan["block_tables"].reshape(n, w)
+        # copy ids..sl (4*B) and the first bs rows of bt
+        self.g_int[:4 * B].copy_(self.h_int[:4 * B], non_blocking=True)
+        self.g_int[4 * B:4 * B + bs * W].copy_(self.h_int[4 * B:4 * B + bs * W], non_blocking=True)
+        greedy = samp is None or samp.all_greedy
+        if not greedy:
+            f = self.h_samp_f.numpy()
+            f[:n] = samp.temps
+            f[B:B + n] = samp.top_ps
+            self.h_samp_i.numpy()[:n] = samp.top_ks
+            self.h_samp_s.numpy()[:n] = samp.seeds
+            self.g_temp[:n].copy_(self.h_samp_f[:n], non_blocking=True)
+            self.g_topp[:n].copy_(self.h_samp_f[B:B + n], non_blocking=True)
+            self.g_topk[:n].copy_(self.h_samp_i[:n], non_blocking=True)
+            self.g_seed[:n].copy_(self.h_samp_s[:n], non_blocking=True)
+        self.graphs[(bs, greedy)].replay()
+        if not self.is_driver:
+            return None, None, None
+        self.h_tok[:n].copy_(self.g_out_tok[:n], non_blocking=True)
+        self.h_lp[:n].copy_(self.g_out_lp[:n], non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        return self.h_tok[:n].numpy().copy(), self.h_lp[:n].numpy().copy(), None
+
+    def _execute_eager(self, plan, samp: Optional[SamplingRows], need_hidden: bool):
+        T = int(plan["num_tokens"])
+        Nd = int(plan["num_decodes"])
+        ns = int(plan["num_seqs"])
+        w = int(plan["bt_width"])
+        Np = ns - Nd
+        li = plan["logits_indices"]
+        S = li.shape[0]
+        qsl = plan["query_start_loc"]
+        parts = [plan["input_ids"], plan["positions"], plan["slot_mapping"],
+                 plan["block_tables"], plan["seq_lens"], (qsl[Nd:] - Nd).astype(np.int32), li]
+        sizes = [p.size for p in parts]
+        total = sum(sizes)
+        hs = self.h_stage.numpy()
+        off = 0
+        for p in parts:
+            hs[off:off + p.size] = p.reshape(-1)
+            off += p.size
+        if self.is_cuda:
+            self.d_stage[:total].copy_(self.h_stage[:total], non_blocking=True)
+            dev = self.d_stage
+        else:
+            dev = self.h_stage
+        o = np.cumsum([0] + sizes)
+        ids = dev[o[0]:o[1]]
+        pos = dev[o[1]:o[2]]
+        slots = dev[o[2]:o[3]]
+        bt = dev[o[3]:o[4]].view(ns, w)
+        sl = dev[o[4]:o[5]]
+        pre_qsl = dev[o[5]:o[6]]
+        lidx = dev[o[6]:o[7]]
+        meta = AttnMeta(num_tokens=T, num_decodes=Nd, positions=pos, slot_mapping=slots,
+                        dec_block_tables=bt[:Nd], dec_seq_lens=sl[:Nd],
+                        num_splits=self.decode_splits(Nd) if self.is_cuda else 1, workspace=self.workspace,
+                        pre_block_tables=bt[Nd:], pre_qsl=pre_qsl, pre_seq_lens=sl[Nd:],
+                        pre_max_q=int(plan["q_lens"][Nd:].max()) if Np > 0 else 0)
+        h = self.model(ids, meta, self.kv_caches)
+        if S == 0:
+            return np.zeros(0, np.int32), np.zeros(0, np.float32), (h if need_hidden else None)
+        logits = self.model.compute_logits(h.index_select(0, lidx.long()))
+        if not self.is_driver:
+            return None, None, (h if need_hidden else None)
+        if samp is None or samp.all_greedy:
+            tok, lp = ops.argmax_logprob(logits)
+        else:
+            dev_f = torch.from_numpy(np.stack([samp.temps, samp.top_ps]).astype(np.float32)).to(self.device)
+            topk = torch.from_numpy(samp.top_ks.astype(np.int32)).to(self.device)
+            seeds = torch.from_numpy(samp.seeds.astype(np.int64)).to(self.device)
+            gen = None
+            if not self.is_cuda:
+                gen = torch.Generator().manual_seed(int(samp.seeds[0]) & 0x7FFFFFFF)
+            tok, lp = ops.sample_tokens(logits, dev_f[0], dev_f[1], topk, seeds, step=0, generator=gen)
+        if self.is_cuda:
+            self.h_tok[:S].copy_(tok, non_blocking=True)
+            self.h_lp[:S].copy_(lp, non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            return self.h_tok[:S].numpy().copy(), self.h_lp[:S].numpy().copy(), (h if need_hidden else None)
+        return tok.numpy().astype(np.int32), lp.numpy().astype(np.float32), (h if need_hidden else None)

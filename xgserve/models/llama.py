@@ -1,0 +1,202 @@
+"""Llama-3 (8B / 70B / 3.2-1B) and Mixtral-8x7B decoders on the paged-KV engine.
+
+Tensor parallelism (Megatron layout, one process per GPU, RCCL/xGMI):
+  * fused QKV and gate_up projections are column-parallel (heads / FFN split),
+  * o_proj and down_proj are row-parallel followed by one all-reduce each,
+  * the LM head is vocab-parallel (logits all-gathered), the embedding is
+    replicated (2 GB for 70B -- negligible in 288 GB of HBM).
+Expert parallelism (Mixtral): EP == TP group, rank r owns experts
+[r*E/tp, (r+1)*E/tp). Two exchange modes:
+  * "alltoall" (default for tp > 1, BASELINE config 5): each rank routes its
+    token slice, dispatches (token, choice) rows to the expert owners with a
+    fixed-capacity all_to_all (graph-capturable: no host sync on counts),
+    runs its local experts as one grouped GEMM, returns rows with a second
+    all_to_all, combines, and all-gathers the slices;
+  * "allreduce": every rank runs its local experts on all tokens and one
+    all-reduce sums the partial outputs.
+Per layer the hot path is: fused_add_rmsnorm (K1) -> QKV GEMM -> rope+KV append
+(K2/K4) -> paged decode / varlen prefill attention (K6/K5) -> o GEMM -> AR ->
+fused_add_rmsnorm -> gate_up GEMM -> SiLU-gate (K3) -> down GEMM -> AR.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from ..parallel import comm
+from ..parallel.state import get_state
+from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
+from .config import ModelConfig
+
+
+def _p(t: torch.Tensor) -> nn.Parameter:
+    return nn.Parameter(t, requires_grad=False)
+
+
+class LlamaLayer(nn.Module):
+    def __init__(self, cfg: ModelConfig, tp: int, rank: int, device, dtype):
+        super().__init__()
+        self.cfg = cfg
+        self.tp, self.rank = tp, rank
+        Hq, Hkv = local_heads(cfg, tp)
+        D, H = cfg.head_dim, cfg.hidden_size
+        self.Hq, self.Hkv = Hq, Hkv
+        z = lambda *s: torch.empty(*s, device=device, dtype=dtype)  # noqa: E731
+        self.input_norm = _p(torch.ones(H, device=device, dtype=dtype))
+        self.post_norm = _p(torch.ones(H, device=device, dtype=dtype))
+        self.qkv = _p(z((Hq + 2 * Hkv) * D, H))
+        self.o = _p(z(H, Hq * D))
+        self.moe = cfg.arch == "mixtral"
+        if self.moe:
+            E = cfg.num_experts
+            if E % tp:
+                raise ValueError(f"{E} experts not divisible by ep={tp}")
+            self.E_local = E // tp
+            self.expert_offset = rank * self.E_local
+            self.router = _p(z(E, H))
+            self.w13 = _p(z(self.E_local, 2 * cfg.intermediate_size, H))
+            self.w2 = _p(z(self.E_local, H, cfg.intermediate_size))
+        else:
+            Fl = cfg.intermediate_size // tp
+            self.gate_up = _p(z(2 * Fl, H))
+            self.down = _p(z(H, Fl))
+        self.attn = PagedAttention(Hq, Hkv, D)
+        self.moe_comm = "allreduce"
+
+    # ------------------------------------------------------------------ MoE
+    def _moe_allreduce(self, h: torch.Tensor) -> torch.Tensor:
+        logits = F.linear(h, self.router)
+        w, ids = ops.moe_topk_softmax(logits, self.cfg.experts_per_token)
+        out = ops.fused_moe(h, self.w13, self.w2, w, ids, self.expert_offset)
+        return comm.tp_all_reduce(out)
+
+    def _moe_alltoall(self, h: torch.Tensor) -> torch.Tensor:
+        tp, r = self.tp, self.rank
+        T, H = h.shape
+        k = self.cfg.experts_per_token
+        per = (T + tp - 1) // tp
+        lo, hi = min(T, r * per), min(T, (r + 1) * per)
+        hs = h[lo:hi]
+        Ts = hi - lo
+        cap = per * k  # fixed per-destination capacity: no host sync on counts
+        send = torch.zeros(tp, cap, H, dtype=h.dtype, device=h.device)
+        send_eid = torch.full((tp, cap), -1, dtype=torch.int32, device=h.device)
+        slot_of_pair = None
+        if Ts > 0:
+            logits = F.linear(hs, self.router)
+            w, ids = ops.moe_topk_softmax(logits, k)
+            flat_ids = ids.reshape(-1).long()
+            dest = flat_ids // self.E_local                                     # [Ts*k]
+            onehot = F.one_hot(dest, tp).to(torch.int32)                        # [Ts*k, tp]
+            pos = (torch.cumsum(onehot, 0) - onehot).gather(1, dest[:, None])[:, 0]  # rank-local slot
+            slot_of_pair = dest * cap + pos
+            rows = torch.arange(Ts * k, device=h.device) // k
+            send.view(tp * cap, H).index_copy_(0, slot_of_pair, hs[rows])
+            send_eid.view(-1).index_copy_(0, slot_of_pair, (flat_ids - dest * self.E_local).to(torch.int32))
+        recv = comm.tp_all_to_all(send.view(tp * cap, H), [cap] * tp, [cap] * tp)
+        recv_eid = comm.tp_all_to_all(send_eid.view(tp * cap, 1), [cap] * tp, [cap] * tp).view(-1)
+        valid = recv_eid >= 0
+        ones = valid.to(torch.float32)[:, None]
+        eids = torch.where(valid, recv_eid, torch.zeros_like(recv_eid)).to(torch.int32)[:, None]
+        y = ops.fused_moe(recv, self.w13, self.w2, ones, eids, 0)
+        back = comm.tp_all_to_all(y, [cap] * tp, [cap] * tp)                     # [tp*cap, H] in send order
+        out_slice = torch.zeros(per, H, dtype=h.dtype, device=h.device)
+        if Ts > 0:
+            contrib = back[slot_of_pair].float() * w.reshape(-1, 1)
+            out_slice[:Ts] = contrib.view(Ts, k, H).sum(1).to(h.dtype)
+        full = comm.tp_all_gather_rows(out_slice)                               # [tp*per, H]
+        return full[:T].contiguous()
+
+    def mlp(self, h: torch.Tensor) -> torch.Tensor:
+        if self.moe:
+            if self.tp > 1 and self.moe_comm == "alltoall":
+                return self._moe_alltoall(h)
+            return self._moe_allreduce(h)
+        gu = F.linear(h, self.gate_up)
+        a = ops.silu_and_mul(gu)
+        return comm.tp_all_reduce(F.linear(a, self.down))
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor], meta: AttnMeta,
+                kv: Tuple[torch.Tensor, torch.Tensor], cos_sin: torch.Tensor):
+        eps = self.cfg.norm_eps
+        if residual is None:
+            residual = x
+            h = ops.rmsnorm(x, self.input_norm, eps)
+        else:
+            h, residual = ops.fused_add_rmsnorm(x, residual, self.input_norm, eps)
+        qkv = F.linear(h, self.qkv)
+        a = self.attn(qkv, meta, kv, cos_sin)
+        o = comm.tp_all_reduce(F.linear(a, self.o))
+        h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
+        return self.mlp(h), residual
+
+
+class LlamaForCausalLM(nn.Module):
+    def __init__(self, cfg: ModelConfig, device="cpu", dtype=torch.bfloat16, tp: Optional[int] = None,
+                 rank: Optional[int] = None):
+        super().__init__()
+        st = get_state()
+        self.cfg = cfg
+        self.tp = st.tp_size if tp is None else tp
+        self.rank = st.tp_rank if rank is None else rank
+        self.device = torch.device(device)
+        self.dtype = dtype
+        H, V = cfg.hidden_size, cfg.vocab_size
+        self.V_pad = (V + self.tp - 1) // self.tp * self.tp
+        self.embed = _p(torch.empty(V, H, device=device, dtype=dtype))
+        self.layers = nn.ModuleList([LlamaLayer(cfg, self.tp, self.rank, device, dtype)
+                                     for _ in range(cfg.num_layers)])
+        self.norm = _p(torch.ones(H, device=device, dtype=dtype))
+        self.lm_head = None if (cfg.tie_embeddings and self.tp == 1) else \
+            _p(torch.empty(self.V_pad // self.tp, H, device=device, dtype=dtype))
+        self.cos_sin = ops.build_cos_sin(cfg.head_dim, cfg.max_position, cfg.rope_theta, cfg.rope_scaling,
+                                         device=device)
+        self.num_kv_heads_local = self.layers[0].Hkv
+
+    def set_moe_comm(self, mode: str):
+        for l in self.layers:
+            l.moe_comm = mode
+
+    # ------------------------------------------------------------------ init
+    @torch.no_grad()
+    def random_init(self, seed: int = 0, std: float = 0.02):
+        g = torch.Generator(device=self.device).manual_seed(seed + 1000 * self.rank) \
+            if self.device.type == "cuda" else torch.Generator().manual_seed(seed + 1000 * self.rank)
+        for name, p in self.named_parameters():
+            if "norm" in name:
+                p.fill_(1.0)
+            else:
+                p.normal_(0.0, std, generator=g)
+        # replicated parameters must agree across TP ranks
+        ge = torch.Generator(device=self.device).manual_seed(seed) if self.device.type == "cuda" \
+            else torch.Generator().manual_seed(seed)
+        self.embed.normal_(0.0, std, generator=ge)
+        for l in self.layers:
+            if l.moe:
+                l.router.normal_(0.0, std, generator=ge)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, input_ids: torch.Tensor, meta: AttnMeta,
+                kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+        x = F.embedding(input_ids, self.embed)
+        residual = None
+        for i, layer in enumerate(self.layers):
+            x, residual = layer(x, residual, meta, kv_caches[i], self.cos_sin)
+        if residual is None:
+            return ops.rmsnorm(x, self.norm, self.cfg.norm_eps)
+        h, _ = ops.fused_add_rmsnorm(x, residual, self.norm, self.cfg.norm_eps)
+        return h
+
+    def compute_logits(self, h: torch.Tensor) -> torch.Tensor:
+        w = self.embed if self.lm_head is None else self.lm_head
+        logits = F.linear(h, w)
+        if self.tp > 1:
+            logits = comm.tp_all_gather_lastdim(logits)
+        return logits[:, :self.cfg.vocab_size]
+
+    def hidden_size(self) -> int:
+        return self.cfg.hidden_size

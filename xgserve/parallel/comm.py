@@ -1,0 +1,99 @@
+"""Collectives used on the model's hot path (TP all-reduce, vocab all-gather,
+EP all-to-all) over RCCL/xGMI, with the custom one-shot xGMI all-reduce
+(csrc/comm/custom_allreduce.hip) taking latency-bound decode messages when it
+has been registered for the TP group.
+
+Sizing notes for MI355X (7 xGMI links x ~153 GB/s per GPU, point-to-point):
+  * decode all-reduces are T*H*2 bytes (8B: 8 KiB/token) -> latency bound;
+    the one-shot kernel reads all peers' buffers concurrently over all 7 links
+    instead of RCCL's per-link-bound ring;
+  * prefill all-reduces (MBs) go to RCCL.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .state import get_state
+
+_CUSTOM_AR = None  # set by register_custom_allreduce()
+
+
+def register_custom_allreduce(ar) -> None:
+    global _CUSTOM_AR
+    _CUSTOM_AR = ar
+
+
+def custom_allreduce():
+    return _CUSTOM_AR
+
+
+def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
+    s = get_state()
+    if s.tp_size == 1:
+        return x
+    ar = _CUSTOM_AR
+    if ar is not None and ar.can_run(x):
+        return ar.all_reduce(x)
+    dist.all_reduce(x, group=s.tp_group)
+    return x
+
+
+def tp_all_gather_lastdim(x: torch.Tensor) -> torch.Tensor:
+    """[.., n] sharded over TP ranks -> [.., n*tp] (rank-major)."""
+    s = get_state()
+    if s.tp_size == 1:
+        return x
+    x = x.contiguous()
+    out = torch.empty((s.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x, group=s.tp_group)
+    return out.movedim(0, -2).reshape(*x.shape[:-1], s.tp_size * x.shape[-1])
+
+
+def tp_all_gather_rows(x: torch.Tensor) -> torch.Tensor:
+    """[n, ..] per rank -> [n*tp, ..] (rank-major rows)."""
+    s = get_state()
+    if s.tp_size == 1:
+        return x
+    x = x.contiguous()
+    out = torch.empty((s.tp_size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x, group=s.tp_group)
+    return out
+
+
+def tp_all_to_all(x: torch.Tensor, send_splits: List[int], recv_splits: List[int]) -> torch.Tensor:
+    s = get_state()
+    out = torch.empty((sum(recv_splits),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    if s.tp_size == 1:
+        out.copy_(x)
+        return out
+    dist.all_to_all_single(out, x.contiguous(), recv_splits, send_splits, group=s.tp_group)
+    return out
+
+
+def tp_exchange_counts(counts: torch.Tensor) -> torch.Tensor:
+    """counts[r] = rows this rank sends to rank r -> rows this rank receives from each r."""
+    s = get_state()
+    if s.tp_size == 1:
+        return counts.clone()
+    out = torch.empty_like(counts)
+    dist.all_to_all_single(out, counts.contiguous(), group=s.tp_group)
+    return out
+
+
+def tp_broadcast_object(obj, src: int = 0):
+    s = get_state()
+    if s.tp_size == 1:
+        return obj
+    lst = [obj]
+    g = s.tp_cpu_group if s.tp_cpu_group is not None else s.tp_group
+    src_global = dist.get_global_rank(g, src) if g is not None and g != dist.group.WORLD else src
+    dist.broadcast_object_list(lst, src=src_global, group=g)
+    return lst[0]
+
+
+def barrier() -> None:
+    if dist.is_initialized():
+        dist.barrier()
