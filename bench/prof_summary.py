@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 --kernel-trace CSV: per-kernel time in the steady-state
+window (the last --window-ms of the trace), GPU busy share, and the host gaps.
+
+  python bench/prof_summary.py gpurun_out/prof1/run_kernel_trace.csv --window-ms 600 > profiles/x.md
+"""
+import argparse
+import collections
+import csv
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--window-ms", type=float, default=600.0)
+    ap.add_argument("--top", type=int, default=25)
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    last = int(rows[-1]["End_Timestamp"])
+    win = [r for r in rows if int(r["Start_Timestamp"]) > last - a.window_ms * 1e6]
+    t0 = int(win[0]["Start_Timestamp"])
+    span = (last - t0) / 1e6
+    busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in win) / 1e6
+    agg = collections.defaultdict(lambda: [0, 0])
+    for r in win:
+        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        agg[r["Kernel_Name"]][0] += d
+        agg[r["Kernel_Name"]][1] += 1
+    gaps = []
+    prev = None
+    for r in win:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if prev is not None and s - prev > 200e3:
+            gaps.append((s - prev) / 1e3)
+        prev = e if prev is None else max(prev, e)
+    print(f"# Kernel profile (steady-state window: last {a.window_ms:.0f} ms of the trace)\n")
+    print(f"- window span: {span:.1f} ms, GPU busy: {busy:.1f} ms ({100 * busy / span:.1f}%)")
+    if gaps:
+        print(f"- host gaps > 200 us: {len(gaps)}, mean {sum(gaps) / len(gaps):.0f} us, total {sum(gaps) / 1e3:.1f} ms")
+    print("\n| kernel | calls | total ms | avg us | share |\n|---|---:|---:|---:|---:|")
+    for n, (d, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:a.top]:
+        short = n.split("(")[0][:90].replace("|", "/")
+        print(f"| `{short}` | {c} | {d / 1e6:.2f} | {d / c / 1e3:.1f} | {100 * d / 1e6 / busy:.1f}% |")
+
+
+if __name__ == "__main__":
+    main()
