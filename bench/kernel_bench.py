@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Micro-benchmarks of the hot kernels at Llama-3-8B decode/prefill shapes on one
+MI355X. Reports time and achieved HBM bandwidth (bytes the op must move)."""
+import argparse
+import json
+import math
+
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from xgserve import ops
+
+
+def timeit(fn, iters=50, warm=10):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1000.0  # us
+
+
+def paged(B, L, Hkv, D, bs, dev):
+    pages = (L + bs - 1) // bs
+    NB = B * pages + 16
+    kc = torch.randn(NB, Hkv, bs, D, device=dev).bfloat16()
+    vc = torch.randn(NB, Hkv, bs, D, device=dev).bfloat16()
+    bt = torch.randperm(NB, device=dev)[:B * pages].view(B, pages).int()
+    return kc, vc, bt
+
+
+def bench_decode(res, B, L, splits_list, Hq=32, Hkv=8, D=128, bs=16):
+    dev = "cuda"
+    kc, vc, bt = paged(B, L, Hkv, D, bs, dev)
+    q = torch.randn(B, Hq, D, device=dev).bfloat16()
+    sl = torch.full((B,), L, dtype=torch.int32, device=dev)
+    ws = ops.attention.DecodeWorkspace(B, Hq, D, 64, dev)
+    out = torch.empty(B, Hq, D, device=dev, dtype=torch.bfloat16)
+    nbytes = B * L * Hkv * D * 2 * 2
+    for s in splits_list:
+        us = timeit(lambda: ops.decode_attention(q, kc, vc, bt, sl, 1 / math.sqrt(D), s, ws, out))
+        res.append({"op": "decode_attention", "B": B, "L": L, "splits": s, "us": round(us, 2),
+                    "TB/s": round(nbytes / us / 1e6, 3)})
+
+
+def bench_prefill(res, T, Hq=32, Hkv=8, D=128, bs=16):
+    dev = "cuda"
+    kc, vc, bt = paged(1, T, Hkv, D, bs, dev)
+    q = torch.randn(T, Hq, D, device=dev).bfloat16()
+    qsl = torch.tensor([0, T], dtype=torch.int32, device=dev)
+    sl = torch.tensor([T], dtype=torch.int32, device=dev)
+    out = torch.empty(T, Hq, D, device=dev, dtype=torch.bfloat16)
+    us = timeit(lambda: ops.prefill_attention(q, kc, vc, bt, qsl, sl, T, 1 / math.sqrt(D), out), iters=20)
+    flops = 4 * Hq * D * T * T / 2
+    res.append({"op": "prefill_attention", "T": T, "us": round(us, 1), "TFLOP/s": round(flops / us / 1e6, 1)})
+
+
+def bench_gemm(res, M, N, K):
+    dev = "cuda"
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = torch.randn(N, K, device=dev).bfloat16()
+    us = timeit(lambda: torch.nn.functional.linear(x, w))
+    res.append({"op": "hipblaslt_linear", "M": M, "N": N, "K": K, "us": round(us, 2),
+                "TB/s(weights)": round(N * K * 2 / us / 1e6, 3)})
+    if hasattr(ops, "skinny_linear"):
+        y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        us2 = timeit(lambda: ops.skinny_linear(x, w, out=y))
+        res.append({"op": "xgk_skinny_linear", "M": M, "N": N, "K": K, "us": round(us2, 2),
+                    "TB/s(weights)": round(N * K * 2 / us2 / 1e6, 3)})
+
+
+def bench_small(res, T=64, H=4096, F=14336):
+    dev = "cuda"
+    x = torch.randn(T, H, device=dev).bfloat16()
+    r = torch.randn(T, H, device=dev).bfloat16()
+    w = torch.randn(H, device=dev).bfloat16()
+    res.append({"op": "fused_add_rmsnorm", "T": T, "us": round(timeit(lambda: ops.fused_add_rmsnorm(x, r, w, 1e-5)), 2)})
+    gu = torch.randn(T, 2 * F, device=dev).bfloat16()
+    res.append({"op": "silu_and_mul", "T": T, "us": round(timeit(lambda: ops.silu_and_mul(gu)), 2)})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--what", default="all")
+    a = ap.parse_args()
+    res = []
+    if a.what in ("all", "decode"):
+        bench_decode(res, 64, 800, [1, 2, 4])
+        bench_decode(res, 1, 1024, [1, 8, 16, 32])
+        bench_decode(res, 256, 2048, [1, 2])
+    if a.what in ("all", "prefill"):
+        for T in (512, 2048, 8192):
+            bench_prefill(res, T)
+    if a.what in ("all", "gemm"):
+        for (N, K) in ((6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)):
+            for M in (1, 64):
+                bench_gemm(res, M, N, K)
+    if a.what in ("all", "small"):
+        bench_small(res)
+    for r in res:
+        print(json.dumps(r))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,4 +1,4 @@
-// K6: paged decode attention (one query token per sequence), GQA, split-K.
+// K6: paged decode attention (one query token per sequence), GQA, split-K (v2: MFMA for both products).
 //
 // Grid (Hkv, B, S): one workgroup per (kv head, sequence, key split); 4 waves.
 // All G = Hq/Hkv query heads of a kv head are processed together so every K/V
@@ -21,13 +21,34 @@ namespace xgk {
 
 template <int D, int G>
 struct DecodeCfg {
-  static constexpr int KK = D / 32;       // MFMA k-steps over the head dim
-  static constexpr int CPL = D / 8;       // lanes that cover one V row (8 dims each)
-  static constexpr int KG = 64 / CPL;     // key groups in the PV phase
-  static constexpr int KPG = 16 / KG;     // keys per group per tile
+  static constexpr int KK = D / 32;        // 16x16x32 k-steps over the head dim (S^T)
+  static constexpr int MT = D / 16;        // 16-dim output tiles (O^T)
+  static constexpr int NCH = D / 8;        // 16-B chunks per key row
+  static constexpr int VLD = 16 * NCH / 64;  // 16-B V chunks per lane per tile
   static constexpr int WAVES = 4;
 };
 
+__device__ __forceinline__ f32x4_t mfma16x16x16(bf16x4_t a, bf16x4_t b, f32x4_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+#else
+  return c;
+#endif
+}
+
+template <int D>
+__device__ __forceinline__ int dswz(int row, int ch) {
+  return ch ^ (((row & 7) << 1) & (D / 8 - 1));
+}
+
+// Per 16-key tile and wave:
+//   S^T[16 keys][16 heads] = K . Q^T     4 x v_mfma_f32_16x16x32_bf16 (K frags straight from HBM)
+//   online softmax per head (lane&15 = head): 2 xor-shuffles per reduction,
+//     alpha is lane-local so the O rescale needs no broadcast
+//   O^T[d][h] += V^T . P^T               D/16 x v_mfma_f32_16x16x16_bf16; the S^T
+//     accumulators ARE the P^T B-fragment (k = 4(lane>>4)+r), V^T fragments come
+//     from a 4 KiB wave-private LDS tile via ds_read_b64_tr_b16
+//   the next tile's K and V loads are issued before the current tile's math.
 template <int D, int G>
 __global__ void __launch_bounds__(256) decode_attn_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
@@ -37,132 +58,119 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   using C = DecodeCfg<D, G>;
   const int kvh = blockIdx.x, b = blockIdx.y, split = blockIdx.z;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
   const int L = seq_lens[b];
   const int ntiles = (L + 15) >> 4;
   const int tps = (ntiles + num_splits - 1) / num_splits;
   const int t_begin = split * tps;
   const int t_end = min(ntiles, t_begin + tps);
 
-  __shared__ float p_lds[C::WAVES][16][16];
-  __shared__ float alpha_lds[C::WAVES][16];
+  __shared__ __attribute__((aligned(16))) uint16_t v_lds[C::WAVES][16 * D];
   __shared__ float m_lds[C::WAVES][16], l_lds[C::WAVES][16];
   __shared__ float o_lds[C::WAVES][G][D];
 
-  // ---- Q^T fragment: lane holds Q[head = lane&15][32kk + 8(lane>>4) + j]
-  const int qh = lane & 15;
+  // Q^T fragment: lane holds Q[head = li][32kk + 8g + j] (heads >= G are zero)
   bf16x8_t qf[C::KK];
   {
-    const uint16_t* qp = q + static_cast<int64_t>(b) * q_stride + static_cast<int64_t>(kvh * G + qh) * D;
+    const uint16_t* qp = q + static_cast<int64_t>(b) * q_stride + static_cast<int64_t>(kvh * G + li) * D;
 #pragma unroll
-    for (int kk = 0; kk < C::KK; ++kk) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (qh < G) v = ld16(qp + kk * 32 + 8 * (lane >> 4));
-      qf[kk] = as_frag(v);
-    }
+    for (int kk = 0; kk < C::KK; ++kk) qf[kk] = as_frag(li < G ? ld16(qp + kk * 32 + 8 * g) : make_uint4(0, 0, 0, 0));
   }
 
-  const int g = lane / C::CPL, c = lane % C::CPL;  // PV role: key group g, dims 8c..8c+7
-  float m = -INFINITY, l = 0.f;                    // per head (lane&15)
-  float acc[G][8];
+  float m = -INFINITY, l = 0.f;  // per head li
+  f32x4_t o[C::MT];
 #pragma unroll
-  for (int h = 0; h < G; ++h)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[h][i] = 0.f;
+  for (int mt = 0; mt < C::MT; ++mt) o[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int32_t* bt = block_tables + static_cast<int64_t>(b) * bt_stride;
-  const int64_t head_stride = static_cast<int64_t>(bs) * D;  // one (page, kv head) run
+  const int64_t head_stride = static_cast<int64_t>(bs) * D;
+  uint16_t* my_v = v_lds[wid];
 
-  for (int t = t_begin + wid; t < t_end; t += C::WAVES) {
+  uint4 kf[C::KK], vr[C::VLD];
+  auto load_tile = [&](int t) {
     const int key0 = t * 16;
     const int page = bt[key0 / bs];
-    const int poff = key0 % bs;
-    const int64_t base = (static_cast<int64_t>(page) * Hkv + kvh) * head_stride + static_cast<int64_t>(poff) * D;
-    // issue all loads of the tile first (K fragment + this lane's V rows)
-    uint4 kf[C::KK];
-    const uint16_t* kp = kc + base + (lane & 15) * D + 8 * (lane >> 4);
+    const int64_t base = (static_cast<int64_t>(page) * Hkv + kvh) * head_stride + static_cast<int64_t>(key0 % bs) * D;
+    const uint16_t* kp = kc + base + li * D + 8 * g;
 #pragma unroll
     for (int kk = 0; kk < C::KK; ++kk) kf[kk] = ld16(kp + kk * 32);
-    uint4 vv[C::KPG];
 #pragma unroll
-    for (int i = 0; i < C::KPG; ++i) vv[i] = ld16(vc + base + (g * C::KPG + i) * D + c * 8);
+    for (int i = 0; i < C::VLD; ++i) {
+      const int c = lane + 64 * i;  // chunk id in the 16 x NCH tile
+      vr[i] = ld16(vc + base + (c / C::NCH) * D + (c % C::NCH) * 8);
+    }
+  };
+
+  int t = t_begin + wid;
+  if (t < t_end) load_tile(t);
+  for (; t < t_end; t += C::WAVES) {
+    uint4 kcur[C::KK];
+#pragma unroll
+    for (int kk = 0; kk < C::KK; ++kk) kcur[kk] = kf[kk];
+    // stage this tile's V rows into the wave-private LDS image (swizzled)
+#pragma unroll
+    for (int i = 0; i < C::VLD; ++i) {
+      const int c = lane + 64 * i;
+      const int row = c / C::NCH, ch = c % C::NCH;
+      st16(my_v + row * D + dswz<D>(row, ch) * 8, vr[i]);
+    }
+    if (t + C::WAVES < t_end) load_tile(t + C::WAVES);  // prefetch: in flight during the math below
 
     f32x4_t s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kk = 0; kk < C::KK; ++kk) s = mfma16x16x32(as_frag(kf[kk]), qf[kk], s);
+    for (int kk = 0; kk < C::KK; ++kk) s = mfma16x16x32(as_frag(kcur[kk]), qf[kk], s);
 
-    // s[r] = S[key = key0 + 4*(lane>>4) + r][head = lane&15]
-    float sv[4];
+    // s[r] = S[key = 16t + 4g + r][head = li]
+    const int key0 = t * 16 + 4 * g;
     float mx = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int key = key0 + 4 * (lane >> 4) + r;
-      sv[r] = key < L ? s[r] * scale : -INFINITY;
-      mx = fmaxf(mx, sv[r]);
+      s[r] = key0 + r < L ? s[r] * scale : -INFINITY;
+      mx = fmaxf(mx, s[r]);
     }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m, mx);
-    const float alpha = __expf(m - m_new);  // m = -inf on the first tile -> 0
+    const float alpha = __expf(m - m_new);  // first tile: m = -inf -> 0
     float ps = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      sv[r] = __expf(sv[r] - m_new);
-      ps += sv[r];
+      s[r] = __expf(s[r] - m_new);
+      ps += s[r];
     }
     ps += __shfl_xor(ps, 16, 64);
     ps += __shfl_xor(ps, 32, 64);
     l = l * alpha + ps;
     m = m_new;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) p_lds[wid][4 * (lane >> 4) + r][lane & 15] = sv[r];
-    if (lane < 16) alpha_lds[wid][lane] = alpha;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-
-#pragma unroll
-    for (int h = 0; h < G; ++h) {
-      const float a = alpha_lds[wid][h];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[h][i] *= a;
+    bf16x4_t pf;
+    {
+      const uint32_t lo = pack2(s[0], s[1]), hi = pack2(s[2], s[3]);
+      pf = __builtin_bit_cast(bf16x4_t, make_uint2(lo, hi));
     }
+    // O^T += V^T P^T ; lane (g, li) tr-reads keys 4g..4g+3 of dims 16mt + li
 #pragma unroll
-    for (int i = 0; i < C::KPG; ++i) {
-      float vf[8];
-      unpack8(vv[i], vf);
-      const int kr = g * C::KPG + i;
+    for (int mt = 0; mt < C::MT; ++mt) {
 #pragma unroll
-      for (int h = 0; h < G; ++h) {
-        const float p = p_lds[wid][kr][h];
-#pragma unroll
-        for (int d = 0; d < 8; ++d) acc[h][d] += p * vf[d];
-      }
+      for (int r = 0; r < 4; ++r) o[mt][r] *= alpha;
+      const int row = 4 * g + (li >> 2);
+      const int col = mt * 16 + 4 * (li & 3);
+      const bf16x4_t vfrag = lds_read_tr16(my_v + row * D + dswz<D>(row, col >> 3) * 8 + (col & 7));
+      o[mt] = mfma16x16x16(vfrag, pf, o[mt]);
     }
-    __builtin_amdgcn_wave_barrier();
   }
 
-  // ---- reduce PV partials over key groups (lanes with the same c)
-#pragma unroll
-  for (int h = 0; h < G; ++h)
-#pragma unroll
-    for (int d = 0; d < 8; ++d) {
-      float v = acc[h][d];
-#pragma unroll
-      for (int o = C::CPL; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
-      acc[h][d] = v;
-    }
+  // ---- merge the 4 wave states: O^T[d = 16mt + 4g + r][h = li]
   if (lane < 16) {
     m_lds[wid][lane] = m;
     l_lds[wid][lane] = l;
   }
-  if (lane < C::CPL) {
+  if (li < G) {
 #pragma unroll
-    for (int h = 0; h < G; ++h)
+    for (int mt = 0; mt < C::MT; ++mt)
 #pragma unroll
-      for (int d = 0; d < 8; ++d) o_lds[wid][h][c * 8 + d] = acc[h][d];
+      for (int r = 0; r < 4; ++r) o_lds[wid][li][mt * 16 + 4 * g + r] = o[mt][r];
   }
   __syncthreads();
-
-  // ---- merge the 4 wave states; thread -> (head, dim)
   for (int idx = threadIdx.x; idx < G * D; idx += blockDim.x) {
     const int h = idx / D, d = idx % D;
     float M = -INFINITY;

@@ -121,6 +121,13 @@ class LLMEngine:
         self.embed_acc = torch.zeros(cfg.max_num_seqs, H, dtype=torch.float32, device=self.device)
         self.requests: Dict[str, EngineRequest] = {}
         self.by_seq: Dict[int, EngineRequest] = {}
+        ns = cfg.max_num_seqs
+        self.slot_owner = np.full(ns, -1, np.int64)
+        self.slot_req: List[Optional[EngineRequest]] = [None] * ns
+        self.slot_temp = np.zeros(ns, np.float32)
+        self.slot_topp = np.ones(ns, np.float32)
+        self.slot_topk = np.zeros(ns, np.int32)
+        self.slot_seed = np.zeros(ns, np.uint64)
         self._seq_counter = itertools.count(1)
         self._lock = threading.Lock()
         self._pending_aborts: List[str] = []
@@ -210,27 +217,44 @@ class LLMEngine:
         return self.sched.has_work() or bool(self._pending_aborts)
 
     # ------------------------------------------------------------------ step
+    def _bind_slots(self, plan) -> None:
+        """Per-slot parameter arrays: rebind only slots whose owner changed."""
+        slots, sids = plan["slots"], plan["seq_ids"]
+        stale = np.nonzero(self.slot_owner[slots] != sids)[0]
+        for i in stale.tolist():
+            s, sid = int(slots[i]), int(sids[i])
+            r = self.by_seq.get(sid)
+            self.slot_owner[s] = sid
+            self.slot_req[s] = r
+            if r is None:
+                self.slot_temp[s], self.slot_topp[s], self.slot_topk[s], self.slot_seed[s] = 0.0, 1.0, 0, 0
+                continue
+            p = r.params
+            self.slot_temp[s], self.slot_topp[s], self.slot_topk[s] = p.temperature, p.top_p, p.top_k
+            self.slot_seed[s] = np.uint64(p.seed & _MASK63)
+
     def _sampling_rows(self, plan) -> Optional[SamplingRows]:
         if not self.is_driver:
             return None
         idx = plan["sample_seq_index"]
-        n = idx.shape[0]
-        if n == 0:
+        if idx.shape[0] == 0:
             return None
-        sids = plan["seq_ids"][idx]
-        temps = np.empty(n, np.float32)
-        tps = np.empty(n, np.float32)
-        tks = np.empty(n, np.int32)
-        seeds = np.empty(n, np.int64)
-        for i, sid in enumerate(sids.tolist()):
-            r = self.by_seq.get(sid)
-            if r is None:
-                temps[i], tps[i], tks[i], seeds[i] = 0.0, 1.0, 0, 0
-                continue
-            p = r.params
-            temps[i], tps[i], tks[i] = p.temperature, p.top_p, p.top_k
-            seeds[i] = _mix(p.seed, len(r.output_ids))
-        return SamplingRows(temps, tps, tks, seeds)
+        slots = plan["slots"][idx]
+        temps = self.slot_temp[slots]
+        # counter-based per-request stream: mix(seed, #tokens generated so far)
+        n = np.array([len(self.slot_req[s].output_ids) if self.slot_req[s] is not None else 0
+                      for s in slots.tolist()], dtype=np.uint64) if not (temps <= 0).all() else None
+        if n is None:
+            seeds = self.slot_seed[slots].view(np.int64)
+        else:
+            with np.errstate(over="ignore"):
+                x = self.slot_seed[slots] * np.uint64(6364136223846793005) + (n + np.uint64(1)) * np.uint64(
+                    1442695040888963407)
+                x &= np.uint64(_MASK63)
+                x ^= x >> np.uint64(29)
+                x = (x * np.uint64(0xBF58476D1CE4E5B9)) & np.uint64(_MASK63)
+            seeds = x.view(np.int64)
+        return SamplingRows(temps, self.slot_topp[slots], self.slot_topk[slots], seeds)
 
     def step(self) -> List[RequestOutput]:
         outs: List[RequestOutput] = []
@@ -246,6 +270,8 @@ class LLMEngine:
             comm.tp_broadcast_object(("plan", plan), src=0)
         if plan["num_tokens"] == 0:
             return outs
+        if self.is_driver:
+            self._bind_slots(plan)
         samp = self._sampling_rows(plan)
         if self.spec is not None and plan["num_seqs"] > plan["num_decodes"]:
             return outs + self.spec.verify_step(plan, samp)

@@ -104,66 +104,86 @@ def load_tokenizer(cfg, checkpoint: Optional[str] = None) -> BaseTokenizer:
 
 
 class IncrementalDetokenizer:
-    """Emits only complete text: holds back trailing bytes of a partial UTF-8
-    character, and holds back a suffix that could still become a stop string."""
+    """O(new tokens) incremental detokenization.
+
+    * synthetic tokenizer: token bytes go through an incremental UTF-8 decoder
+      (partial characters are buffered until complete);
+    * HF tokenizers: the prefix/read-offset window scheme (decode only the last
+      few ids; hold output while it ends in a replacement char);
+    * stop strings: only the tail window is searched, and a suffix that could
+      still grow into a stop string is held back.
+    """
 
     def __init__(self, tok: BaseTokenizer, stop: Sequence[str] = ()):
+        import codecs
         self.tok = tok
         self.ids: List[int] = []
-        self.text = ""          # full decoded text so far (complete chars only)
+        self.text = ""          # decoded text so far (complete chars only)
         self.emitted = 0        # chars of self.text already handed out
         self.stop = [s for s in stop if s]
+        self.max_stop = max((len(s) for s in self.stop), default=0)
         self.stopped = False
+        self._synthetic = isinstance(tok, SyntheticTokenizer)
+        self._dec = codecs.getincrementaldecoder("utf-8")(errors="replace") if self._synthetic else None
+        self._eos = set(tok.eos_ids)
         self._prefix_off = 0
         self._read_off = 0
 
-    def _decode_new(self) -> str:
-        if isinstance(self.tok, SyntheticTokenizer):
-            raw = b"".join(self.tok.token_bytes(i) for i in self.ids)
-            try:
-                return raw.decode("utf-8")
-            except UnicodeDecodeError as e:
-                return raw[:e.start].decode("utf-8", errors="replace")
-        full = self.tok.decode(self.ids)
-        if full.endswith("�"):
-            full = full.rstrip("�")
-        return full
+    def _append(self, new_ids) -> None:
+        ids = [int(i) for i in new_ids if int(i) not in self._eos]
+        if not ids:
+            return
+        self.ids.extend(ids)
+        if self._synthetic:
+            tb = self.tok.token_bytes
+            self.text += self._dec.decode(b"".join(tb(i) for i in ids))
+            return
+        prefix = self.tok.decode(self.ids[self._prefix_off:self._read_off])
+        full = self.tok.decode(self.ids[self._prefix_off:])
+        if full.endswith("\ufffd"):
+            return  # wait for the rest of the character
+        if len(full) > len(prefix):
+            self.text += full[len(prefix):]
+        self._prefix_off = self._read_off
+        self._read_off = len(self.ids)
 
     def add(self, new_ids: Sequence[int]) -> str:
         """Append tokens; return newly available text (stop strings excluded)."""
         if self.stopped:
             return ""
-        self.ids.extend(int(i) for i in new_ids if int(i) not in self.tok.eos_ids)
-        self.text = self._decode_new()
-        if self.stop:
-            cut = None
-            for s in self.stop:
-                j = self.text.find(s, max(0, self.emitted - len(s)))
-                if j >= 0 and (cut is None or j < cut):
-                    cut = j
-            if cut is not None:
-                self.stopped = True
-                out = self.text[self.emitted:cut]
-                self.text = self.text[:cut]
-                self.emitted = cut
-                return out
-            hold = max(len(s) - 1 for s in self.stop)
-            safe = len(self.text)
-            for k in range(min(hold, len(self.text)), 0, -1):
-                tail = self.text[-k:]
-                if any(s.startswith(tail) for s in self.stop):
-                    safe = len(self.text) - k
-                    break
-            out = self.text[self.emitted:safe]
-            self.emitted = max(self.emitted, safe)
+        self._append(new_ids)
+        if not self.stop:
+            out = self.text[self.emitted:]
+            self.emitted = len(self.text)
             return out
-        out = self.text[self.emitted:]
-        self.emitted = len(self.text)
+        lo = max(0, self.emitted - self.max_stop)
+        cut = None
+        for st in self.stop:
+            j = self.text.find(st, lo)
+            if j >= 0 and (cut is None or j < cut):
+                cut = j
+        if cut is not None:
+            self.stopped = True
+            out = self.text[self.emitted:cut]
+            self.text = self.text[:cut]
+            self.emitted = cut
+            return out
+        safe = len(self.text)
+        for k in range(min(self.max_stop - 1, len(self.text)), 0, -1):
+            tail = self.text[-k:]
+            if any(st.startswith(tail) for st in self.stop):
+                safe = len(self.text) - k
+                break
+        safe = max(safe, self.emitted)
+        out = self.text[self.emitted:safe]
+        self.emitted = safe
         return out
 
     def flush(self) -> str:
         if self.stopped:
             return ""
+        if self._synthetic:
+            self.text += self._dec.decode(b"", final=True)
         out = self.text[self.emitted:]
         self.emitted = len(self.text)
         return out
