@@ -71,9 +71,10 @@ def bench_gemm(res, M, N, K):
     res.append({"op": "hipblaslt_linear", "M": M, "N": N, "K": K, "us": round(us, 2),
                 "TB/s(weights)": round(N * K * 2 / us / 1e6, 3)})
     if hasattr(ops, "skinny_linear"):
-        y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        us2 = timeit(lambda: ops.skinny_linear(x, w, out=y))
-        res.append({"op": "xgk_skinny_linear", "M": M, "N": N, "K": K, "us": round(us2, 2),
+        from xgserve.ops.linear import MODE_PARTIAL, choose_split
+        S = choose_split(M, N, K)
+        us2 = timeit(lambda: ops.skinny_linear(x, w, S, MODE_PARTIAL))
+        res.append({"op": "xgk_skinny_linear(partial)", "M": M, "N": N, "K": K, "S": S, "us": round(us2, 2),
                     "TB/s(weights)": round(N * K * 2 / us2 / 1e6, 3)})
 
 

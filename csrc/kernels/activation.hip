@@ -7,8 +7,11 @@
 
 namespace xgk {
 
+// interleave16 != 0: the row is laid out in blocks of 16 as [g0..g15 u0..u15 g16..]
+// (the layout the decode skinny GEMM's fused SiLU epilogue needs).
 __global__ void __launch_bounds__(256) silu_and_mul_kernel(const uint16_t* __restrict__ in,
-                                                           uint16_t* __restrict__ out, int T, int F) {
+                                                           uint16_t* __restrict__ out, int T, int F,
+                                                           int interleave16) {
   const int fc = F >> 3;  // chunks of 8 per row
   const int64_t total = static_cast<int64_t>(T) * fc;
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
@@ -16,9 +19,12 @@ __global__ void __launch_bounds__(256) silu_and_mul_kernel(const uint16_t* __res
     const int64_t t = i / fc;
     const int c = static_cast<int>(i - t * fc);
     const uint16_t* row = in + t * 2 * F;
+    const int f = c * 8;
+    const int gi = interleave16 ? (f >> 4) * 32 + (f & 15) : f;
+    const int ui = interleave16 ? gi + 16 : F + f;
     float g[8], u[8], o[8];
-    unpack8(ld16(row + c * 8), g);
-    unpack8(ld16(row + F + c * 8), u);
+    unpack8(ld16(row + gi), g);
+    unpack8(ld16(row + ui), u);
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = g[k] / (1.f + __expf(-g[k])) * u[k];
     st16(out + t * F + c * 8, pack8(o));
@@ -46,10 +52,10 @@ static int grid_for(int64_t work) {
   return static_cast<int>(g < 2048 ? (g > 0 ? g : 1) : 2048);
 }
 
-void silu_and_mul(const uint16_t* in, uint16_t* out, int T, int F, hipStream_t st) {
+void silu_and_mul(const uint16_t* in, uint16_t* out, int T, int F, int interleave16, hipStream_t st) {
   if (T <= 0) return;
   hipLaunchKernelGGL(silu_and_mul_kernel, dim3(grid_for(static_cast<int64_t>(T) * (F / 8))), dim3(256), 0,
-                     st, in, out, T, F);
+                     st, in, out, T, F, interleave16);
 }
 
 void gelu_tanh(const uint16_t* in, uint16_t* out, int64_t n, hipStream_t st) {

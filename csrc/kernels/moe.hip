@@ -237,9 +237,9 @@ void moe_combine(const uint16_t* y, const int32_t* dest, const float* w, uint16_
   hipLaunchKernelGGL(combine_kernel, dim3(T), dim3(256), 0, st, y, dest, w, out, k, H);
 }
 
-void silu_and_mul(const uint16_t* in, uint16_t* out, int T, int F, hipStream_t st);
+void silu_and_mul(const uint16_t* in, uint16_t* out, int T, int F, int interleave16, hipStream_t st);
 void moe_silu_mul_gather(const uint16_t* in, uint16_t* out, int rows, int F, hipStream_t st) {
-  silu_and_mul(in, out, rows, F, st);
+  silu_and_mul(in, out, rows, F, 0, st);
 }
 
 }  // namespace xgk

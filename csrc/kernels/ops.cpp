@@ -14,7 +14,13 @@ namespace xgk {
 void rmsnorm(const uint16_t*, const uint16_t*, uint16_t*, int, int, float, int64_t, int64_t, hipStream_t);
 void fused_add_rmsnorm(const uint16_t*, uint16_t*, const uint16_t*, uint16_t*, int, int, float, hipStream_t);
 void layernorm(const uint16_t*, const uint16_t*, const uint16_t*, uint16_t*, int, int, float, hipStream_t);
-void silu_and_mul(const uint16_t*, uint16_t*, int, int, hipStream_t);
+void silu_and_mul(const uint16_t*, uint16_t*, int, int, int, hipStream_t);
+int skinny_gemm(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, hipStream_t);
+int skinny_slab_kmax(int);
+void add_partials_rmsnorm(const float*, int, int, uint16_t*, const uint16_t*, uint16_t*, int, float, hipStream_t);
+void reduce_partials(const float*, int, int64_t, uint16_t*, hipStream_t);
+int rope_cache_partials(const float*, int, uint16_t*, int64_t, const int32_t*, const float*, uint16_t*, uint16_t*,
+                        const int32_t*, int, int, int, int, int, int, hipStream_t);
 void gelu_tanh(const uint16_t*, uint16_t*, int64_t, hipStream_t);
 int rope_cache(uint16_t*, int64_t, const int32_t*, const float*, uint16_t*, uint16_t*, const int32_t*, int, int, int,
                int, int, int, hipStream_t);
@@ -70,10 +76,38 @@ PYBIND11_MODULE(_kernels, m) {
                    S(st));
     check(0, "layernorm");
   });
-  m.def("silu_and_mul", [](uintptr_t in, uintptr_t out, int T, int F, uintptr_t st) {
+  m.def("silu_and_mul", [](uintptr_t in, uintptr_t out, int T, int F, int interleave16, uintptr_t st) {
     if (F % 8) throw std::invalid_argument("silu_and_mul: F % 8 != 0");
-    xgk::silu_and_mul(P<const uint16_t>(in), P<uint16_t>(out), T, F, S(st));
+    if (interleave16 && F % 16) throw std::invalid_argument("silu_and_mul: interleaved F % 16 != 0");
+    xgk::silu_and_mul(P<const uint16_t>(in), P<uint16_t>(out), T, F, interleave16, S(st));
     check(0, "silu_and_mul");
+  });
+  m.def("skinny_gemm", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int split_k,
+                          int mode, uintptr_t st) {
+    check(xgk::skinny_gemm(P<const uint16_t>(x), M, K, P<const uint16_t>(w), N, P<float>(part), P<uint16_t>(out),
+                           split_k, mode, S(st)),
+          "skinny_gemm");
+  });
+  m.def("skinny_slab_kmax", &xgk::skinny_slab_kmax);
+  m.def("add_partials_rmsnorm", [](uintptr_t part, int S_, int T, uintptr_t res, uintptr_t w, uintptr_t out, int H,
+                                   float eps, uintptr_t st) {
+    if (H % 8) throw std::invalid_argument("add_partials_rmsnorm: H % 8 != 0");
+    xgk::add_partials_rmsnorm(P<const float>(part), S_, T, P<uint16_t>(res), P<const uint16_t>(w), P<uint16_t>(out),
+                              H, eps, S(st));
+    check(0, "add_partials_rmsnorm");
+  });
+  m.def("reduce_partials", [](uintptr_t part, int S_, int64_t n, uintptr_t out, uintptr_t st) {
+    if (n % 4) throw std::invalid_argument("reduce_partials: n % 4 != 0");
+    xgk::reduce_partials(P<const float>(part), S_, n, P<uint16_t>(out), S(st));
+    check(0, "reduce_partials");
+  });
+  m.def("rope_cache_partials", [](uintptr_t part, int S_, uintptr_t q_out, int64_t q_stride, uintptr_t pos,
+                                  uintptr_t cs, uintptr_t kc, uintptr_t vc, uintptr_t slots, int T, int Hq, int Hkv,
+                                  int D, int bs, int apply_rope, uintptr_t st) {
+    check(xgk::rope_cache_partials(P<const float>(part), S_, P<uint16_t>(q_out), q_stride, P<const int32_t>(pos),
+                                   P<const float>(cs), P<uint16_t>(kc), P<uint16_t>(vc), P<const int32_t>(slots), T,
+                                   Hq, Hkv, D, bs, apply_rope, S(st)),
+          "rope_cache_partials");
   });
   m.def("gelu_tanh", [](uintptr_t in, uintptr_t out, int64_t n, uintptr_t st) {
     if (n % 8) throw std::invalid_argument("gelu_tanh: n % 8 != 0");

@@ -1,9 +1,11 @@
 // K2 + K4: rotary embedding fused with the paged KV-cache append.
 //
-// Input is the QKV GEMM output row [q (Hq*D) | k (Hkv*D) | v (Hkv*D)] of each
-// token. In one pass per token:
-//   * q is rotated in place (attention reads it straight from the QKV buffer,
-//     no copy);
+// Input is the QKV projection of each token, either as a bf16 row
+// [q (Hq*D) | k (Hkv*D) | v (Hkv*D)] or as the fp32 split-K partial sums of the
+// decode skinny GEMM ([S, T, (Hq+2Hkv)*D], reduced here in the prologue). In
+// one pass per token:
+//   * q is rotated and written to q_out (in place for the bf16 input, so
+//     attention reads it straight from the QKV buffer);
 //   * k is rotated and scattered into the paged K cache at slot_mapping[t];
 //   * v is scattered into the paged V cache.
 // Rotation is the Llama "rotate_half" form on (x[d], x[d+D/2]) pairs with a
@@ -11,14 +13,36 @@
 // trig on device). Every access is 16 B per lane: a work item is 8 pairs.
 // Cache layout: [num_blocks, Hkv, block_size, D] -- a (page, kv-head) is one
 // contiguous block_size*D run, which is what the attention kernels stream.
-// slot_mapping < 0 marks padding tokens (CUDA-graph-style padded decode batch)
-// that must not write the cache.
+// slot_mapping < 0 marks padding tokens (graph-padded decode batch) that must
+// not write the cache.
 #include "common.h"
 
 namespace xgk {
 
+struct QkvSrc {
+  const uint16_t* row_bf16;  // bf16 QKV buffer (or null)
+  int64_t row_stride;
+  const float* part;         // fp32 partials [S, T, width] (or null)
+  int S, T, width;
+
+  __device__ __forceinline__ void load8(int t, int col, float* f) const {
+    if (part) {
+      for (int i = 0; i < 8; ++i) f[i] = 0.f;
+      for (int s = 0; s < S; ++s) {
+        const float* p = part + (static_cast<int64_t>(s) * T + t) * width + col;
+        const float4 a = *reinterpret_cast<const float4*>(p);
+        const float4 b = *reinterpret_cast<const float4*>(p + 4);
+        f[0] += a.x; f[1] += a.y; f[2] += a.z; f[3] += a.w;
+        f[4] += b.x; f[5] += b.y; f[6] += b.z; f[7] += b.w;
+      }
+    } else {
+      unpack8(ld16(row_bf16 + static_cast<int64_t>(t) * row_stride + col), f);
+    }
+  }
+};
+
 template <int D>
-__global__ void __launch_bounds__(256) rope_cache_kernel(uint16_t* __restrict__ qkv, int64_t row_stride,
+__global__ void __launch_bounds__(256) rope_cache_kernel(QkvSrc src, uint16_t* __restrict__ q_out, int64_t q_stride,
                                                          const int32_t* __restrict__ positions,
                                                          const float* __restrict__ cos_sin,
                                                          uint16_t* __restrict__ k_cache,
@@ -29,7 +53,6 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(uint16_t* __restrict__ 
   constexpr int CPH = HALF / 8;  // rope work items per head
   constexpr int VPH = D / 8;     // copy work items per head
   const int t = blockIdx.x;
-  uint16_t* row = qkv + static_cast<int64_t>(t) * row_stride;
   const int slot = slot_mapping[t];
   const int64_t page = slot >= 0 ? slot / block_size : 0;
   const int off = slot >= 0 ? slot % block_size : 0;
@@ -37,13 +60,15 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(uint16_t* __restrict__ 
   const float* cs = cos_sin + static_cast<int64_t>(pos) * D;
   const int n_rope = (Hq + Hkv) * CPH;
   const int n_all = n_rope + Hkv * VPH;
+  const bool inplace_q = src.part == nullptr && q_out == src.row_bf16;
   for (int it = threadIdx.x; it < n_all; it += blockDim.x) {
     if (it < n_rope) {
       const int h = it / CPH, c = it % CPH;
-      uint16_t* base = row + h * D;
+      if (h >= Hq && slot < 0) continue;
+      if (h < Hq && inplace_q && !apply_rope) continue;
       float a[8], b[8];
-      unpack8(ld16(base + c * 8), a);
-      unpack8(ld16(base + HALF + c * 8), b);
+      src.load8(t, h * D + c * 8, a);
+      src.load8(t, h * D + HALF + c * 8, b);
       if (apply_rope) {
         const float4 c0 = *reinterpret_cast<const float4*>(cs + c * 8);
         const float4 c1 = *reinterpret_cast<const float4*>(cs + c * 8 + 4);
@@ -60,11 +85,10 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(uint16_t* __restrict__ 
       }
       const uint4 pa = pack8(a), pb = pack8(b);
       if (h < Hq) {
-        if (apply_rope) {
-          st16(base + c * 8, pa);
-          st16(base + HALF + c * 8, pb);
-        }
-      } else if (slot >= 0) {
+        uint16_t* qd = q_out + static_cast<int64_t>(t) * q_stride + h * D;
+        st16(qd + c * 8, pa);
+        st16(qd + HALF + c * 8, pb);
+      } else {
         const int kh = h - Hq;
         uint16_t* dst = k_cache + ((page * Hkv + kh) * block_size + off) * D;
         st16(dst + c * 8, pa);
@@ -73,30 +97,51 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(uint16_t* __restrict__ 
     } else if (slot >= 0) {
       const int j = it - n_rope;
       const int kh = j / VPH, c = j % VPH;
-      const uint16_t* src = row + (Hq + Hkv + kh) * D + c * 8;
       uint16_t* dst = v_cache + ((page * Hkv + kh) * block_size + off) * D + c * 8;
-      st16(dst, ld16(src));
+      if (src.part) {
+        float f[8];
+        src.load8(t, (Hq + Hkv + kh) * D + c * 8, f);
+        st16(dst, pack8(f));
+      } else {
+        st16(dst, ld16(src.row_bf16 + static_cast<int64_t>(t) * src.row_stride + (Hq + Hkv + kh) * D + c * 8));
+      }
     }
+  }
+}
+
+static int launch_rope(QkvSrc src, uint16_t* q_out, int64_t q_stride, const int32_t* positions, const float* cos_sin,
+                       uint16_t* k_cache, uint16_t* v_cache, const int32_t* slot_mapping, int T, int Hq, int Hkv,
+                       int D, int block_size, int apply_rope, hipStream_t st) {
+  if (T <= 0) return 0;
+  dim3 g(T), b(256);
+  switch (D) {
+    case 64:
+      hipLaunchKernelGGL(rope_cache_kernel<64>, g, b, 0, st, src, q_out, q_stride, positions, cos_sin, k_cache,
+                         v_cache, slot_mapping, Hq, Hkv, block_size, apply_rope);
+      return 0;
+    case 128:
+      hipLaunchKernelGGL(rope_cache_kernel<128>, g, b, 0, st, src, q_out, q_stride, positions, cos_sin, k_cache,
+                         v_cache, slot_mapping, Hq, Hkv, block_size, apply_rope);
+      return 0;
+    default:
+      return -1;
   }
 }
 
 int rope_cache(uint16_t* qkv, int64_t row_stride, const int32_t* positions, const float* cos_sin,
                uint16_t* k_cache, uint16_t* v_cache, const int32_t* slot_mapping, int T, int Hq, int Hkv,
                int D, int block_size, int apply_rope, hipStream_t st) {
-  if (T <= 0) return 0;
-  dim3 g(T), b(256);
-  switch (D) {
-    case 64:
-      hipLaunchKernelGGL(rope_cache_kernel<64>, g, b, 0, st, qkv, row_stride, positions, cos_sin, k_cache,
-                         v_cache, slot_mapping, Hq, Hkv, block_size, apply_rope);
-      return 0;
-    case 128:
-      hipLaunchKernelGGL(rope_cache_kernel<128>, g, b, 0, st, qkv, row_stride, positions, cos_sin, k_cache,
-                         v_cache, slot_mapping, Hq, Hkv, block_size, apply_rope);
-      return 0;
-    default:
-      return -1;
-  }
+  QkvSrc src{qkv, row_stride, nullptr, 0, 0, 0};
+  return launch_rope(src, qkv, row_stride, positions, cos_sin, k_cache, v_cache, slot_mapping, T, Hq, Hkv, D,
+                     block_size, apply_rope, st);
+}
+
+int rope_cache_partials(const float* part, int S, uint16_t* q_out, int64_t q_stride, const int32_t* positions,
+                        const float* cos_sin, uint16_t* k_cache, uint16_t* v_cache, const int32_t* slot_mapping,
+                        int T, int Hq, int Hkv, int D, int block_size, int apply_rope, hipStream_t st) {
+  QkvSrc src{nullptr, 0, part, S, T, (Hq + 2 * Hkv) * D};
+  return launch_rope(src, q_out, q_stride, positions, cos_sin, k_cache, v_cache, slot_mapping, T, Hq, Hkv, D,
+                     block_size, apply_rope, st);
 }
 
 }  // namespace xgk

@@ -1,0 +1,427 @@
+// Decode-regime projection GEMM: out[M, N] = x[M, K] . W[N, K]^T for M <= 128.
+//
+// At decode batch sizes the Llama projections are pure weight streams (W is
+// read once per step; x is <= 3.7 MB and L2-resident), so the kernel is built
+// for HBM bandwidth, not MFMA rate (cdna_hip_programming.md §5: "GEMV / M <= 16
+// decode weights: load straight to VGPRs, deep unroll, late vmcnt"):
+//   * workgroup = 4 waves = 32 output columns (two 16-wide MFMA n-tiles); the
+//     4 waves split the workgroup's K range, so every wave is an independent
+//     weight stream with no barrier in its main loop;
+//   * W rows go straight from HBM into v_mfma_f32_16x16x32_bf16 A fragments
+//     (16 B per lane), x rows are read as B fragments from L2 (rows >= M are
+//     clamped, their results discarded);
+//   * named A/B register stages (loop unrolled by two, no runtime-indexed
+//     register arrays) keep the next stage's loads in flight during the
+//     current stage's MFMAs;
+//   * one LDS reduction over the 4 waves at the end; split-K over gridDim.y
+//     writes fp32 partials [S, M, N] that the CONSUMING kernel reduces in its
+//     prologue (add_partials_rmsnorm / rope_cache_partials), so split-K costs no
+//     extra launch;
+//   * epilogue modes: bf16, fp32 partials, or SiLU-gate: with the block-16
+//     interleaved gate|up layout a workgroup's two n-tiles are the gate and up
+//     rows of the same 16 features -> silu(g)*u is written as [M, N/2].
+#include "common.h"
+
+namespace xgk {
+
+constexpr int SK_BN = 32;     // columns per workgroup
+constexpr int SK_WAVES = 4;
+
+enum SkinnyMode : int { SK_BF16 = 0, SK_PARTIAL = 1, SK_SILU = 2 };
+
+template <int MT, int KS>
+struct Stage {
+  uint4 w[KS][2];
+  uint4 x[KS][MT];
+};
+
+template <int MT, int KS>
+__device__ __forceinline__ void stage_load(Stage<MT, KS>& st, const uint16_t* w0, const uint16_t* w1,
+                                           const uint16_t* const* xr, int k) {
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    st.w[ks][0] = ld16(w0 + k + ks * 32);
+    st.w[ks][1] = ld16(w1 + k + ks * 32);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) st.x[ks][mt] = ld16(xr[mt] + k + ks * 32);
+  }
+}
+
+template <int MT, int KS>
+__device__ __forceinline__ void stage_mma(const Stage<MT, KS>& st, f32x4_t (&acc)[2][MT]) {
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = mfma16x16x32(as_frag(st.w[ks][nt]), as_frag(st.x[ks][mt]), acc[nt][mt]);
+}
+
+template <int MT, int KS>
+__global__ void __launch_bounds__(256) skinny_gemm_kernel(const uint16_t* __restrict__ x, int M, int K,
+                                                          const uint16_t* __restrict__ w, int N,
+                                                          float* __restrict__ part, uint16_t* __restrict__ out,
+                                                          int mode) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int n0 = blockIdx.x * SK_BN;
+  const int S = gridDim.y, s = blockIdx.y;
+  const int kwg = K / S;                 // K range of this workgroup
+  const int kw = kwg / SK_WAVES;         // K range of this wave
+  const int kb = s * kwg + wid * kw + 8 * g;
+
+  const uint16_t* w0 = w + static_cast<int64_t>(n0 + li) * K + kb;
+  const uint16_t* w1 = w + static_cast<int64_t>(n0 + 16 + li) * K + kb;
+  const uint16_t* xr[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int row = min(mt * 16 + li, M - 1);
+    xr[mt] = x + static_cast<int64_t>(row) * K + kb;
+  }
+
+  f32x4_t acc[2][MT];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int STEP = KS * 32;
+  const int nst = kw / STEP;             // stages per wave (host guarantees >= 1)
+  // Loads of stage i+1 are in flight while stage i is multiplied. The steady
+  // loop has no conditional loads (a conditional load makes hipcc merge
+  // waitcnt states conservatively and drain vmcnt(0) every iteration).
+  Stage<MT, KS> A, B;
+  stage_load(A, w0, w1, xr, 0);
+  int i = 0;
+  for (; i + 2 < nst; i += 2) {
+    stage_load(B, w0, w1, xr, (i + 1) * STEP);
+    stage_mma(A, acc);
+    stage_load(A, w0, w1, xr, (i + 2) * STEP);
+    stage_mma(B, acc);
+  }
+  if (i + 1 < nst) {
+    stage_load(B, w0, w1, xr, (i + 1) * STEP);
+    stage_mma(A, acc);
+    stage_mma(B, acc);
+  } else {
+    stage_mma(A, acc);
+  }
+
+  // ---- reduce the 4 waves' K slices through LDS
+  // acc[nt][mt][r] = out[m = 16mt + li][n = n0 + 16nt + 4g + r]
+  __shared__ float red[SK_WAVES - 1][2][MT][4][64];
+  if (wid > 0) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wid - 1][nt][mt][r][lane] = acc[nt][mt][r];
+  }
+  __syncthreads();
+  if (wid != 0) return;
+#pragma unroll
+  for (int ww = 0; ww < SK_WAVES - 1; ++ww)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[nt][mt][r] += red[ww][nt][mt][r][lane];
+
+  if (mode == SK_PARTIAL) {
+    float* pp = part + static_cast<int64_t>(s) * M * N;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = mt * 16 + li;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        *reinterpret_cast<float4*>(pp + static_cast<int64_t>(m) * N + n0 + nt * 16 + 4 * g) =
+            make_float4(acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]);
+    }
+  } else if (mode == SK_BF16) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = mt * 16 + li;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        uint2 v;
+        v.x = pack2(acc[nt][mt][0], acc[nt][mt][1]);
+        v.y = pack2(acc[nt][mt][2], acc[nt][mt][3]);
+        *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * N + n0 + nt * 16 + 4 * g) = v;
+      }
+    }
+  } else {  // SK_SILU: n-tile 0 = gate rows, n-tile 1 = up rows of features f0..f0+15
+    const int F = N / 2;
+    const int f0 = n0 / 2 + 4 * g;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = mt * 16 + li;
+      if (m >= M) continue;
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float gt = acc[0][mt][r];
+        o[r] = gt / (1.f + __expf(-gt)) * acc[1][mt][r];
+      }
+      uint2 v;
+      v.x = pack2(o[0], o[1]);
+      v.y = pack2(o[2], o[3]);
+      *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * F + f0) = v;
+    }
+  }
+}
+
+template <int MT, int KS>
+static void launch_skinny(dim3 grid, const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part,
+                          uint16_t* out, int mode, hipStream_t st) {
+  hipLaunchKernelGGL((skinny_gemm_kernel<MT, KS>), grid, dim3(256), 0, st, x, M, K, w, N, part, out, mode);
+}
+
+// ---------------------------------------------------------------------------
+// "Slab" variant for 16 < M <= 64: the workgroup's whole x slab
+// [16*MT rows][Ks = K/S] (<= 128 KiB) is loaded into LDS once (one barrier),
+// then each of the 4 waves streams its own 16 weight rows through an 8-deep
+// register ring (8 k-steps = 8 KiB per wave in flight) with x B-fragments
+// read from LDS: no barrier in the main loop, x read from L2 once per
+// workgroup instead of once per wave. Tile 64 columns; split-K partials.
+// ---------------------------------------------------------------------------
+constexpr int SL_RING = 8;
+
+template <int MT>
+__global__ void __launch_bounds__(256) skinny_slab_kernel(const uint16_t* __restrict__ x, int M, int K,
+                                                          const uint16_t* __restrict__ w, int N,
+                                                          float* __restrict__ part, uint16_t* __restrict__ out,
+                                                          int mode) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];  // [16*MT][Ks], 16-B chunks swizzled
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int n0 = blockIdx.x * 64;
+  const int S = gridDim.y, s = blockIdx.y;
+  const int Ks = K / S;
+  const int kb = s * Ks;
+  const int nch = Ks / 8;  // 16-B chunks per slab row
+  const uint16_t* wrow = w + static_cast<int64_t>(n0 + wid * 16 + li) * K + kb + 8 * g;
+
+  // W ring prologue first: its HBM latency overlaps the slab fill
+  uint4 r0, r1, r2, r3, r4, r5, r6, r7;
+  r0 = ld16(wrow + 0 * 32); r1 = ld16(wrow + 1 * 32); r2 = ld16(wrow + 2 * 32); r3 = ld16(wrow + 3 * 32);
+  r4 = ld16(wrow + 4 * 32); r5 = ld16(wrow + 5 * 32); r6 = ld16(wrow + 6 * 32); r7 = ld16(wrow + 7 * 32);
+
+  // slab fill (rows >= M are zero): 8 independent loads in flight per thread
+  // before their LDS stores -- a load->store loop would serialise L2 latencies.
+  const int total = 16 * MT * nch;
+  for (int p0 = 0; p0 < total; p0 += 256 * 8) {
+    uint4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = p0 + u * 256 + threadIdx.x;
+      const int row = p / nch, ch = p % nch;
+      const int rr = min(row, M - 1);
+      v[u] = p < total ? ld16(x + static_cast<int64_t>(rr) * K + kb + ch * 8) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = p0 + u * 256 + threadIdx.x;
+      if (p >= total) continue;
+      const int row = p / nch, ch = p % nch;
+      st16(xs + static_cast<int64_t>(row) * Ks + ((ch ^ (row & 15)) * 8), row < M ? v[u] : make_uint4(0, 0, 0, 0));
+    }
+  }
+  __syncthreads();
+
+  f32x4_t acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nks = Ks / 32;
+  auto step = [&](const uint4& wv, int ks) {
+    const bf16x8_t a = as_frag(wv);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int row = mt * 16 + li;
+      const int ch = ks * 4 + g;
+      const uint4 b = *reinterpret_cast<const uint4*>(xs + static_cast<int64_t>(row) * Ks + ((ch ^ (row & 15)) * 8));
+      acc[mt] = mfma16x16x32(a, as_frag(b), acc[mt]);
+    }
+  };
+#define SL_STEP(R, J)                                           \
+  {                                                             \
+    const int ks = base + J;                                    \
+    step(R, ks);                                                \
+    if (ks + SL_RING < nks) R = ld16(wrow + (ks + SL_RING) * 32); \
+  }
+  for (int base = 0; base < nks; base += SL_RING) {
+    SL_STEP(r0, 0) SL_STEP(r1, 1) SL_STEP(r2, 2) SL_STEP(r3, 3)
+    SL_STEP(r4, 4) SL_STEP(r5, 5) SL_STEP(r6, 6) SL_STEP(r7, 7)
+  }
+#undef SL_STEP
+
+  // acc[mt][r] = out[m = 16mt + li][n = n0 + 16wid + 4g + r]
+  if (mode == SK_PARTIAL) {
+    float* pp = part + static_cast<int64_t>(s) * M * N;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = mt * 16 + li;
+      if (m < M)
+        *reinterpret_cast<float4*>(pp + static_cast<int64_t>(m) * N + n0 + wid * 16 + 4 * g) =
+            make_float4(acc[mt][0], acc[mt][1], acc[mt][2], acc[mt][3]);
+    }
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = mt * 16 + li;
+      if (m >= M) continue;
+      uint2 v;
+      v.x = pack2(acc[mt][0], acc[mt][1]);
+      v.y = pack2(acc[mt][2], acc[mt][3]);
+      *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * N + n0 + wid * 16 + 4 * g) = v;
+    }
+  }
+}
+
+constexpr int SL_MAX_LDS = 128 * 1024;
+
+// 0 = launched, -1 = shape not supported by the slab kernel
+static int launch_slab(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out,
+                       int split_k, int mode, hipStream_t st) {
+  if (M <= 16 || M > 64 || N % 64 || mode == SK_SILU) return -1;
+  const int MT = M <= 32 ? 2 : 4;
+  const int Ks = K / split_k;
+  if (K % split_k || Ks % (32 * SL_RING)) return -1;
+  const size_t lds = static_cast<size_t>(16 * MT) * Ks * 2;
+  if (lds > SL_MAX_LDS) return -1;
+  dim3 grid(N / 64, split_k);
+  static bool attr_set = false;  // opt in to > 64 KiB dynamic LDS once (not a stream op: graph-safe)
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_slab_kernel<2>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, SL_MAX_LDS);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_slab_kernel<4>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, SL_MAX_LDS);
+    attr_set = true;
+  }
+  if (MT == 2)
+    hipLaunchKernelGGL(skinny_slab_kernel<2>, grid, dim3(256), lds, st, x, M, K, w, N, part, out, mode);
+  else
+    hipLaunchKernelGGL(skinny_slab_kernel<4>, grid, dim3(256), lds, st, x, M, K, w, N, part, out, mode);
+  return 0;
+}
+
+// Largest per-workgroup K slice the slab kernel can hold for M rows (0 = not applicable).
+int skinny_slab_kmax(int M) {
+  if (M <= 16 || M > 64) return 0;
+  const int MT = M <= 32 ? 2 : 4;
+  return SL_MAX_LDS / (16 * MT * 2);
+}
+
+// K must be a multiple of split_k * 4 waves * stage depth (KS*32); returns -1 otherwise.
+int skinny_gemm(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int split_k,
+                int mode, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (M > 128 || N % SK_BN || split_k <= 0) return -1;
+  if (mode != SK_PARTIAL && split_k != 1) return -1;
+  if (M > 16 && M <= 64 && launch_slab(x, M, K, w, N, part, out, split_k, mode, st) == 0) return 0;
+  const int MT = M <= 16 ? 1 : M <= 32 ? 2 : M <= 64 ? 4 : 8;
+  const int KS = MT >= 8 ? 1 : 2;
+  if (K % (split_k * SK_WAVES * KS * 32)) return -1;
+  dim3 grid(N / SK_BN, split_k);
+  switch (MT) {
+    case 1: launch_skinny<1, 2>(grid, x, M, K, w, N, part, out, mode, st); break;
+    case 2: launch_skinny<2, 2>(grid, x, M, K, w, N, part, out, mode, st); break;
+    case 4: launch_skinny<4, 2>(grid, x, M, K, w, N, part, out, mode, st); break;
+    default: launch_skinny<8, 1>(grid, x, M, K, w, N, part, out, mode, st); break;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Split-K consumers
+// ---------------------------------------------------------------------------
+// residual[t] += sum_s part[s, t]; out[t] = rmsnorm(residual[t]) * w
+template <int VPT>
+__global__ void __launch_bounds__(256) add_partials_rmsnorm_kernel(const float* __restrict__ part, int S, int T,
+                                                                   uint16_t* __restrict__ residual,
+                                                                   const uint16_t* __restrict__ w,
+                                                                   uint16_t* __restrict__ out, int H, float eps) {
+  __shared__ float red[8];
+  const int row = blockIdx.x;
+  const int nchunk = H >> 3;
+  uint16_t* rr = residual + static_cast<int64_t>(row) * H;
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int c = threadIdx.x + k * blockDim.x;
+    if (c < nchunk) {
+      unpack8(ld16(rr + c * 8), v[k]);
+      for (int s = 0; s < S; ++s) {
+        const float* pp = part + (static_cast<int64_t>(s) * T + row) * H + c * 8;
+        const float4 a = *reinterpret_cast<const float4*>(pp);
+        const float4 b = *reinterpret_cast<const float4*>(pp + 4);
+        v[k][0] += a.x; v[k][1] += a.y; v[k][2] += a.z; v[k][3] += a.w;
+        v[k][4] += b.x; v[k][5] += b.y; v[k][6] += b.z; v[k][7] += b.w;
+      }
+      const uint4 pk = pack8(v[k]);
+      st16(rr + c * 8, pk);
+      unpack8(pk, v[k]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += v[k][i] * v[k][i];
+    }
+  }
+  ss = block_sum(ss, red);
+  const float inv = rsqrtf(ss / static_cast<float>(H) + eps);
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int c = threadIdx.x + k * blockDim.x;
+    if (c < nchunk) {
+      float wf[8], o[8];
+      unpack8(ld16(w + c * 8), wf);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = v[k][i] * inv * wf[i];
+      st16(out + static_cast<int64_t>(row) * H + c * 8, pack8(o));
+    }
+  }
+}
+
+void add_partials_rmsnorm(const float* part, int S, int T, uint16_t* residual, const uint16_t* w, uint16_t* out,
+                          int H, float eps, hipStream_t st) {
+  if (T <= 0) return;
+  const int nchunk = H / 8;
+  const int thr = nchunk >= 256 ? 256 : ((nchunk + 63) / 64) * 64;
+  int vpt = (nchunk + thr - 1) / thr;
+  vpt = vpt <= 1 ? 1 : vpt <= 2 ? 2 : vpt <= 4 ? 4 : 8;
+  dim3 g(T), b(thr);
+  switch (vpt) {
+    case 1: hipLaunchKernelGGL(add_partials_rmsnorm_kernel<1>, g, b, 0, st, part, S, T, residual, w, out, H, eps); break;
+    case 2: hipLaunchKernelGGL(add_partials_rmsnorm_kernel<2>, g, b, 0, st, part, S, T, residual, w, out, H, eps); break;
+    case 4: hipLaunchKernelGGL(add_partials_rmsnorm_kernel<4>, g, b, 0, st, part, S, T, residual, w, out, H, eps); break;
+    default: hipLaunchKernelGGL(add_partials_rmsnorm_kernel<8>, g, b, 0, st, part, S, T, residual, w, out, H, eps); break;
+  }
+}
+
+// out[t, :] = bf16(sum_s part[s, t, :])  (used when a collective needs the sum)
+__global__ void __launch_bounds__(256) reduce_partials_kernel(const float* __restrict__ part, int S, int64_t n,
+                                                              uint16_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n / 4;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    float4 a = reinterpret_cast<const float4*>(part)[i];
+    for (int s = 1; s < S; ++s) {
+      const float4 b = reinterpret_cast<const float4*>(part + s * n)[i];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    uint2 v;
+    v.x = pack2(a.x, a.y);
+    v.y = pack2(a.z, a.w);
+    reinterpret_cast<uint2*>(out)[i] = v;
+  }
+}
+
+void reduce_partials(const float* part, int S, int64_t n, uint16_t* out, hipStream_t st) {
+  if (n <= 0) return;
+  int64_t g = (n / 4 + 255) / 256;
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(g < 2048 ? g : 2048), dim3(256), 0, st, part, S, n, out);
+}
+
+}  // namespace xgk

@@ -60,6 +60,8 @@ class ModelRunner:
         self.max_model_len = max_model_len
         self.max_blocks_per_seq = (max_model_len + block_size - 1) // block_size + 1
         self.is_driver = is_driver
+        self.capture_logits = False  # tests: keep the last eager step's logits
+        self.last_logits = None
         cfg = self.cfg
         self.Hkv = model.num_kv_heads_local
         self.kv = torch.zeros(cfg.num_layers, 2, num_blocks, self.Hkv, block_size, cfg.head_dim,
@@ -72,8 +74,13 @@ class ModelRunner:
                                          self.device) if self.is_cuda else None
         # pinned staging for eager steps
         cap = 8 * max_num_batched_tokens + 4 * max_num_seqs * (self.max_blocks_per_seq + 4) + 64
-        self.h_stage = _pinned(cap, torch.int32)
-        self.d_stage = torch.empty(cap, dtype=torch.int32, device=self.device)
+        # two pinned host staging buffers + device twins: a step may return
+        # before its async H2D copy ran, so the next step must not overwrite the
+        # same host buffer until that copy's event has completed
+        self.h_stages = [_pinned(cap, torch.int32) for _ in range(2)]
+        self.d_stages = [torch.empty(cap, dtype=torch.int32, device=self.device) for _ in range(2)]
+        self.stage_events = [None, None]
+        self.stage_idx = 0
         self.h_tok = _pinned(max(max_num_batched_tokens, max_num_seqs), torch.int32)
         self.h_lp = _pinned(max(max_num_batched_tokens, max_num_seqs), torch.float32)
         # graphs
@@ -213,6 +220,8 @@ class ModelRunner:
             self.g_seed[:n].copy_(self.h_samp_s[:n], non_blocking=True)
         self.graphs[(bs, greedy)].replay()
         if not self.is_driver:
+            # no D2H to wait on: still drain before the pinned inputs get rewritten
+            torch.cuda.current_stream().synchronize()
             return None, None, None
         self.h_tok[:n].copy_(self.g_out_tok[:n], non_blocking=True)
         self.h_lp[:n].copy_(self.g_out_lp[:n], non_blocking=True)
@@ -232,16 +241,25 @@ class ModelRunner:
                  plan["block_tables"], plan["seq_lens"], (qsl[Nd:] - Nd).astype(np.int32), li]
         sizes = [p.size for p in parts]
         total = sum(sizes)
-        hs = self.h_stage.numpy()
+        si = self.stage_idx
+        self.stage_idx ^= 1
+        ev = self.stage_events[si]
+        if ev is not None:
+            ev.synchronize()  # the H2D copy that last read this host buffer has run
+        h_stage, d_stage = self.h_stages[si], self.d_stages[si]
+        hs = h_stage.numpy()
         off = 0
         for p in parts:
             hs[off:off + p.size] = p.reshape(-1)
             off += p.size
         if self.is_cuda:
-            self.d_stage[:total].copy_(self.h_stage[:total], non_blocking=True)
-            dev = self.d_stage
+            d_stage[:total].copy_(h_stage[:total], non_blocking=True)
+            if self.stage_events[si] is None:
+                self.stage_events[si] = torch.cuda.Event()
+            self.stage_events[si].record()
+            dev = d_stage
         else:
-            dev = self.h_stage
+            dev = h_stage
         o = np.cumsum([0] + sizes)
         ids = dev[o[0]:o[1]]
         pos = dev[o[1]:o[2]]
@@ -259,6 +277,8 @@ class ModelRunner:
         if S == 0:
             return np.zeros(0, np.int32), np.zeros(0, np.float32), (h if need_hidden else None)
         logits = self.model.compute_logits(h.index_select(0, lidx.long()))
+        if self.capture_logits:
+            self.last_logits = logits.float().cpu()
         if not self.is_driver:
             return None, None, (h if need_hidden else None)
         if samp is None or samp.all_greedy:

@@ -72,8 +72,23 @@ class PagedAttention:
         ops.rope_cache(qkv, meta.positions, cos_sin, kc, vc, meta.slot_mapping, self.Hq, self.Hkv, self.D,
                        self.use_rope)
         q = qkv[:, :self.Hq * self.D].view(T, self.Hq, self.D)
+        return self.attend(q, meta, kv, out)
+
+    def from_partials(self, pend, meta: AttnMeta, kv: Tuple[torch.Tensor, torch.Tensor],
+                      cos_sin: torch.Tensor) -> torch.Tensor:
+        """QKV as split-K partial sums (decode skinny GEMM): reduce + rope + KV append in one kernel."""
+        T = meta.num_tokens
+        q = torch.empty(T, self.Hq * self.D, dtype=torch.bfloat16, device=pend.part.device)
+        ops.rope_cache_partials(pend, q, meta.positions, cos_sin, kv[0], kv[1], meta.slot_mapping, self.Hq,
+                                self.Hkv, self.D, self.use_rope)
+        return self.attend(q.view(T, self.Hq, self.D), meta, kv)
+
+    def attend(self, q: torch.Tensor, meta: AttnMeta, kv: Tuple[torch.Tensor, torch.Tensor],
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        T = q.shape[0]
+        kc, vc = kv
         if out is None:
-            out = torch.empty(T, self.Hq, self.D, dtype=qkv.dtype, device=qkv.device)
+            out = torch.empty(T, self.Hq, self.D, dtype=q.dtype, device=q.device)
         nd = meta.num_decodes
         if nd > 0:
             ops.decode_attention(q[:nd], kc, vc, meta.dec_block_tables, meta.dec_seq_lens, self.scale,

@@ -29,8 +29,13 @@ import torch.nn.functional as F
 from .. import ops
 from ..parallel import comm
 from ..parallel.state import get_state
+from ..ops.linear import MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, pick_split, skinny_linear
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
 from .config import ModelConfig
+
+
+FAST_M_SMALL = 16   # tokens per step handled entirely by the streaming skinny GEMM
+FAST_M_SLAB = 64    # tokens per step for the O-projection slab kernel
 
 
 def _p(t: torch.Tensor) -> nn.Parameter:
@@ -66,6 +71,18 @@ class LlamaLayer(nn.Module):
             self.down = _p(z(H, Fl))
         self.attn = PagedAttention(Hq, Hkv, D)
         self.moe_comm = "allreduce"
+        # decode fast path: skinny split-K GEMMs whose partial sums are reduced by
+        # the consuming kernel (rope_cache / add+rmsnorm); SiLU fused in gate_up.
+        Nqkv = (Hq + 2 * Hkv) * D
+        self.split_qkv = pick_split(Nqkv, H)
+        self.split_o = pick_split(H, Hq * D)
+        dims_ok = (H % 256 == 0 and (Hq * D) % 256 == 0 and Nqkv % 64 == 0 and H % 64 == 0
+                   and self.split_qkv and self.split_o)
+        if not self.moe:
+            Fl = cfg.intermediate_size // tp
+            self.split_down = pick_split(H, Fl)
+            dims_ok = dims_ok and Fl % 256 == 0 and (2 * Fl) % 64 == 0 and self.split_down
+        self.fast_ok = bool(dims_ok) and torch.device(device).type == "cuda"
 
     # ------------------------------------------------------------------ MoE
     def _moe_allreduce(self, h: torch.Tensor) -> torch.Tensor:
@@ -117,10 +134,16 @@ class LlamaLayer(nn.Module):
                 return self._moe_alltoall(h)
             return self._moe_allreduce(h)
         gu = F.linear(h, self.gate_up)
-        a = ops.silu_and_mul(gu)
+        a = ops.silu_and_mul(gu, interleave16=True)
         return comm.tp_all_reduce(F.linear(a, self.down))
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor], meta: AttnMeta,
+    def _row_parallel_fast(self, a: torch.Tensor, w: torch.Tensor, split: int):
+        pend = skinny_linear(a, w, None, MODE_PARTIAL)
+        if self.tp == 1:
+            return pend  # reduced by the consumer's prologue
+        return comm.tp_all_reduce(pend.materialize())
+
+    def forward(self, x, residual: Optional[torch.Tensor], meta: AttnMeta,
                 kv: Tuple[torch.Tensor, torch.Tensor], cos_sin: torch.Tensor):
         eps = self.cfg.norm_eps
         if residual is None:
@@ -128,6 +151,27 @@ class LlamaLayer(nn.Module):
             h = ops.rmsnorm(x, self.input_norm, eps)
         else:
             h, residual = ops.fused_add_rmsnorm(x, residual, self.input_norm, eps)
+        T = meta.num_tokens
+        if self.fast_ok and T <= FAST_M_SMALL:
+            # M <= 16: every projection on the streaming skinny kernel (1.7x hipBLASLt
+            # on QKV/O at batch 1), split-K partials reduced by the consumers
+            pqkv = skinny_linear(h, self.qkv, None, MODE_PARTIAL)
+            a = self.attn.from_partials(pqkv, meta, kv, cos_sin)
+            o = self._row_parallel_fast(a, self.o, self.split_o)
+            h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
+            if self.moe:
+                return self.mlp(h), residual
+            act = skinny_linear(h, self.gate_up, mode=MODE_SILU)
+            return self._row_parallel_fast(act, self.down, self.split_down), residual
+        if self.fast_ok and T <= FAST_M_SLAB:
+            # 16 < M <= 64: measured per shape on MI355X -- only the O projection
+            # (N = H) is faster on the LDS-slab kernel; its split-K partials are
+            # reduced inside add+rmsnorm. QKV / gate_up / down stay on hipBLASLt.
+            qkv = F.linear(h, self.qkv)
+            a = self.attn(qkv, meta, kv, cos_sin)
+            o = self._row_parallel_fast(a, self.o, self.split_o)
+            h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
+            return self.mlp(h), residual
         qkv = F.linear(h, self.qkv)
         a = self.attn(qkv, meta, kv, cos_sin)
         o = comm.tp_all_reduce(F.linear(a, self.o))

@@ -16,6 +16,7 @@ from typing import Callable, Dict, Optional
 
 import torch
 
+from ..ops.linear import deinterleave_gate_up, interleave_gate_up
 from .base import kv_head_range
 from .config import ModelConfig, get_config
 from .gpt2 import GPT2ForCausalLM
@@ -135,7 +136,7 @@ def _load_llama(m, r: _Reader):
             Fl = cfg.intermediate_size // tp
             g = r.get(b + "mlp.gate_proj.weight", 0, rank * Fl, Fl)
             u = r.get(b + "mlp.up_proj.weight", 0, rank * Fl, Fl)
-            _copy(L.gate_up, torch.cat([g, u], 0), f"layer{i}.gate_up")
+            _copy(L.gate_up, interleave_gate_up(g, u), f"layer{i}.gate_up")
             _copy(L.down, r.get(b + "mlp.down_proj.weight", 1, rank * Fl, Fl), f"layer{i}.down")
 
 
@@ -212,8 +213,9 @@ def save_checkpoint(model, path: str) -> None:
                     t[eb + "w2.weight"] = L.w2[e]
             else:
                 Fd = cfg.intermediate_size
-                t[b + "mlp.gate_proj.weight"] = L.gate_up[:Fd]
-                t[b + "mlp.up_proj.weight"] = L.gate_up[Fd:]
+                gw, uw = deinterleave_gate_up(L.gate_up)
+                t[b + "mlp.gate_proj.weight"] = gw
+                t[b + "mlp.up_proj.weight"] = uw
                 t[b + "mlp.down_proj.weight"] = L.down
         hf = {"model_type": "mixtral" if cfg.arch == "mixtral" else "llama", "hidden_size": cfg.hidden_size,
               "num_hidden_layers": cfg.num_layers, "num_attention_heads": cfg.num_heads,

@@ -8,6 +8,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+from ..ops.linear import deinterleave_gate_up
 from ..ops.rope import build_cos_sin
 
 
@@ -78,9 +79,8 @@ def reference_logits(model, tokens) -> torch.Tensor:
                     out[t] += w[t, j] * ((F.silu(g[:Fd]) * g[Fd:]) @ L.w2[ei].float().t())
             x = x + out
         else:
-            Fd = L.gate_up.shape[0] // 2
-            g = h @ L.gate_up.float().t()
-            x = x + (F.silu(g[:, :Fd]) * g[:, Fd:]) @ L.down.float().t()
+            gw, uw = deinterleave_gate_up(L.gate_up)  # stored block-16 interleaved
+            x = x + (F.silu(h @ gw.float().t()) * (h @ uw.float().t())) @ L.down.float().t()
     x = rms(x, model.norm)
     w = model.embed if model.lm_head is None else model.lm_head[:cfg.vocab_size]
     return x @ w.float().t()

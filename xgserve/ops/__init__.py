@@ -6,7 +6,9 @@ Every GPU op here launches a hand-written kernel from csrc/kernels; the
 """
 from .norm import rmsnorm, fused_add_rmsnorm, layernorm, rmsnorm_ref, fused_add_rmsnorm_ref, layernorm_ref
 from .activation import silu_and_mul, gelu_tanh, silu_and_mul_ref, gelu_tanh_ref
-from .rope import RotaryCache, rope_cache, rope_cache_ref, build_cos_sin
+from .rope import RotaryCache, rope_cache, rope_cache_ref, build_cos_sin, rope_cache_partials
+from . import linear
+from .linear import skinny_linear, PendingSum
 from .attention import (decode_attention, prefill_attention, decode_attention_ref,
                         prefill_attention_ref, choose_num_splits)
 from .sampling import argmax_logprob, sample_tokens, argmax_logprob_ref, segment_sum

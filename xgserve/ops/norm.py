@@ -43,9 +43,18 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Te
     return out.view(*x.shape[:-1], H) if out.dim() == 2 and x.dim() != 2 else out
 
 
-def fused_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+def fused_add_rmsnorm(x, residual: torch.Tensor, w: torch.Tensor, eps: float,
                       out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """residual <- x + residual (in place); returns (rmsnorm(residual) * w, residual)."""
+    """residual <- x + residual (in place); returns (rmsnorm(residual) * w, residual).
+    `x` may be a PendingSum (split-K partials): they are reduced in the kernel prologue."""
+    from .linear import PendingSum
+    if isinstance(x, PendingSum):
+        S, T, H = x.part.shape
+        if out is None:
+            out = torch.empty(T, H, dtype=residual.dtype, device=residual.device)
+        kernels().add_partials_rmsnorm(x.part.data_ptr(), S, T, residual.data_ptr(), w.data_ptr(), out.data_ptr(),
+                                       H, float(eps), stream_ptr())
+        return out, residual
     if not use_native(x):
         y, r = fused_add_rmsnorm_ref(x, residual, w, eps)
         residual.copy_(r)

@@ -71,6 +71,18 @@ def rope_cache_ref(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Te
     v_cache[pages, :, offs] = v[valid].to(v_cache.dtype)
 
 
+def rope_cache_partials(pend, q_out: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
+                        k_cache: torch.Tensor, v_cache: torch.Tensor, slot_mapping: torch.Tensor, Hq: int, Hkv: int,
+                        D: int, apply_rope: bool = True) -> torch.Tensor:
+    """QKV given as split-K partial sums (PendingSum [S, T, (Hq+2Hkv)D]); q -> q_out [T, Hq*D]."""
+    S, T, W = pend.part.shape
+    assert W == (Hq + 2 * Hkv) * D and q_out.stride(-1) == 1
+    kernels().rope_cache_partials(pend.part.data_ptr(), S, q_out.data_ptr(), q_out.stride(0), positions.data_ptr(),
+                                  cos_sin.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), slot_mapping.data_ptr(),
+                                  T, Hq, Hkv, D, k_cache.shape[2], 1 if apply_rope else 0, stream_ptr())
+    return q_out
+
+
 def rope_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor,
                v_cache: torch.Tensor, slot_mapping: torch.Tensor, Hq: int, Hkv: int, D: int,
                apply_rope: bool = True) -> None:
