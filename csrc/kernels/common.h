@@ -36,6 +36,13 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 }
 
 __device__ __forceinline__ uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+// non-temporal 16-B load: for weights streamed once per step (guide: nt-weights)
+__device__ __forceinline__ uint4 ld16_nt(const void* p) {
+  const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
 __device__ __forceinline__ void st16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
 
 __device__ __forceinline__ void unpack8(uint4 v, float* f) {

@@ -188,7 +188,8 @@ static void launch_skinny(dim3 grid, const uint16_t* x, int M, int K, const uint
 // read from LDS: no barrier in the main loop, x read from L2 once per
 // workgroup instead of once per wave. Tile 64 columns; split-K partials.
 // ---------------------------------------------------------------------------
-constexpr int SL_RING = 8;
+constexpr int SL_NKS = 32;            // k-steps per workgroup slice
+constexpr int SL_KS = SL_NKS * 32;    // K slice per workgroup (fixed: K / split_k must equal it)
 
 template <int MT>
 __global__ void __launch_bounds__(256) skinny_slab_kernel(const uint16_t* __restrict__ x, int M, int K,
@@ -205,25 +206,27 @@ __global__ void __launch_bounds__(256) skinny_slab_kernel(const uint16_t* __rest
   const int nch = Ks / 8;  // 16-B chunks per slab row
   const uint16_t* wrow = w + static_cast<int64_t>(n0 + wid * 16 + li) * K + kb + 8 * g;
 
-  // W ring prologue first: its HBM latency overlaps the slab fill
-  uint4 r0, r1, r2, r3, r4, r5, r6, r7;
-  r0 = ld16(wrow + 0 * 32); r1 = ld16(wrow + 1 * 32); r2 = ld16(wrow + 2 * 32); r3 = ld16(wrow + 3 * 32);
-  r4 = ld16(wrow + 4 * 32); r5 = ld16(wrow + 5 * 32); r6 = ld16(wrow + 6 * 32); r7 = ld16(wrow + 7 * 32);
+  // The wave's ENTIRE weight slice (SL_NKS k-steps = 32 KiB per wave, 128 VGPRs)
+  // is requested before anything else: at one workgroup per CU the register
+  // file is there to hold it, and all of the HBM latency overlaps the slab fill.
+  uint4 wr[SL_NKS];
+#pragma unroll
+  for (int ks = 0; ks < SL_NKS; ++ks) wr[ks] = ld16_nt(wrow + ks * 32);
 
-  // slab fill (rows >= M are zero): 8 independent loads in flight per thread
+  // slab fill (rows >= M are zero): 16 independent loads in flight per thread
   // before their LDS stores -- a load->store loop would serialise L2 latencies.
   const int total = 16 * MT * nch;
-  for (int p0 = 0; p0 < total; p0 += 256 * 8) {
-    uint4 v[8];
+  for (int p0 = 0; p0 < total; p0 += 256 * 16) {
+    uint4 v[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const int p = p0 + u * 256 + threadIdx.x;
       const int row = p / nch, ch = p % nch;
       const int rr = min(row, M - 1);
       v[u] = p < total ? ld16(x + static_cast<int64_t>(rr) * K + kb + ch * 8) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const int p = p0 + u * 256 + threadIdx.x;
       if (p >= total) continue;
       const int row = p / nch, ch = p % nch;
@@ -236,9 +239,9 @@ __global__ void __launch_bounds__(256) skinny_slab_kernel(const uint16_t* __rest
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int nks = Ks / 32;
-  auto step = [&](const uint4& wv, int ks) {
-    const bf16x8_t a = as_frag(wv);
+#pragma unroll
+  for (int ks = 0; ks < SL_NKS; ++ks) {
+    const bf16x8_t a = as_frag(wr[ks]);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int row = mt * 16 + li;
@@ -246,18 +249,7 @@ __global__ void __launch_bounds__(256) skinny_slab_kernel(const uint16_t* __rest
       const uint4 b = *reinterpret_cast<const uint4*>(xs + static_cast<int64_t>(row) * Ks + ((ch ^ (row & 15)) * 8));
       acc[mt] = mfma16x16x32(a, as_frag(b), acc[mt]);
     }
-  };
-#define SL_STEP(R, J)                                           \
-  {                                                             \
-    const int ks = base + J;                                    \
-    step(R, ks);                                                \
-    if (ks + SL_RING < nks) R = ld16(wrow + (ks + SL_RING) * 32); \
   }
-  for (int base = 0; base < nks; base += SL_RING) {
-    SL_STEP(r0, 0) SL_STEP(r1, 1) SL_STEP(r2, 2) SL_STEP(r3, 3)
-    SL_STEP(r4, 4) SL_STEP(r5, 5) SL_STEP(r6, 6) SL_STEP(r7, 7)
-  }
-#undef SL_STEP
 
   // acc[mt][r] = out[m = 16mt + li][n = n0 + 16wid + 4g + r]
   if (mode == SK_PARTIAL) {
@@ -290,7 +282,7 @@ static int launch_slab(const uint16_t* x, int M, int K, const uint16_t* w, int N
   if (M <= 16 || M > 64 || N % 64 || mode == SK_SILU) return -1;
   const int MT = M <= 32 ? 2 : 4;
   const int Ks = K / split_k;
-  if (K % split_k || Ks % (32 * SL_RING)) return -1;
+  if (K % split_k || Ks != SL_KS) return -1;
   const size_t lds = static_cast<size_t>(16 * MT) * Ks * 2;
   if (lds > SL_MAX_LDS) return -1;
   dim3 grid(N / 64, split_k);
@@ -312,8 +304,7 @@ static int launch_slab(const uint16_t* x, int M, int K, const uint16_t* w, int N
 // Largest per-workgroup K slice the slab kernel can hold for M rows (0 = not applicable).
 int skinny_slab_kmax(int M) {
   if (M <= 16 || M > 64) return 0;
-  const int MT = M <= 32 ? 2 : 4;
-  return SL_MAX_LDS / (16 * MT * 2);
+  return SL_KS;  // the slab kernel takes exactly this K slice per workgroup
 }
 
 // K must be a multiple of split_k * 4 waves * stage depth (KS*32); returns -1 otherwise.

@@ -57,16 +57,8 @@ def choose_split(M: int, N: int, K: int, target_wgs: int = 256) -> int:
         kmax = _SLAB_KMAX.get(M)
         if kmax is None:
             kmax = _SLAB_KMAX[M] = kernels().skinny_slab_kmax(M)
-        nb = N // 64
-        best = None
-        for s in range(1, 65):
-            if K % s or (K // s) % 256 or K // s > kmax:
-                continue
-            best = s
-            if nb * s >= target_wgs:
-                break
-        if best:
-            return best
+        if K % kmax == 0:  # the slab kernel takes exactly kmax of K per workgroup
+            return K // kmax
     return pick_split(N, K, target_wgs)
 
 
