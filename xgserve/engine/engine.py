@@ -427,3 +427,10 @@ class LLMEngine:
     def clear_prefix_cache(self):
         with self._lock:
             self.sched.clear_prefix_cache()
+
+    def set_limits(self, max_num_seqs: int, max_num_batched_tokens: int):
+        """Runtime batch limits (degradation / hot reload), clamped to the sizes the
+        runner's buffers and graphs were built for."""
+        with self._lock:
+            self.sched.set_limits(max(1, min(max_num_seqs, self.cfg.max_num_seqs)),
+                                  max(1, min(max_num_batched_tokens, self.cfg.max_num_batched_tokens)))

@@ -47,8 +47,10 @@ def tp_all_gather_lastdim(x: torch.Tensor) -> torch.Tensor:
     if s.tp_size == 1:
         return x
     x = x.contiguous()
-    out = torch.empty((s.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+    # flat [tp*rows, ...] output (the layout every backend accepts), viewed as [tp, ...]
+    out = torch.empty((s.tp_size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     dist.all_gather_into_tensor(out, x, group=s.tp_group)
+    out = out.view((s.tp_size,) + tuple(x.shape))
     return out.movedim(0, -2).reshape(*x.shape[:-1], s.tp_size * x.shape[-1])
 
 

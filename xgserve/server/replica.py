@@ -1,0 +1,403 @@
+"""Model replicas: the spec's Inference Worker (Req 7, requirements.md:100-110;
+design.md:310-361) as an *engine loop* that owns one LLMEngine (a TP group).
+
+* `EngineLoop` -- the worker main loop: drains commands (add / abort /
+  set_limits / clear_cache / stop), runs `engine.step()` while there is work,
+  emits RequestOutputs and a heartbeat with engine stats every 0.5 s. A step
+  that raises is contained: HIP OOM -> flush the prefix cache and retry once
+  (Req 9.3), then fail only the requests that were in flight with
+  `out_of_memory`; any other exception fails the in-flight requests with
+  `inference_failed` (Property 22) and the loop keeps serving.
+* `InProcessReplica` -- engine + loop on a thread of the server process
+  (tp == 1; tests, CPU configs).
+* `ProcessReplica` -- one OS process per GPU (spawned, so HIP is initialised
+  fresh in each): rank 0 runs the EngineLoop and talks to the server over two
+  multiprocessing queues; ranks 1..tp-1 run `engine.follower_loop()` and
+  receive step plans over the TP group (design note SURVEY.md 3.3 A). Crash
+  detection = process liveness + heartbeat age (Req 7.4, 9.4).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import queue as pyqueue
+import threading
+import time
+import traceback
+from typing import Any, Callable, Dict, List, Optional
+
+log = logging.getLogger("xgserve.replica")
+
+HEARTBEAT_S = 0.5
+
+
+# ---------------------------------------------------------------------------
+# engine construction (runs inside the replica)
+# ---------------------------------------------------------------------------
+def engine_spec(worker, cache=None, spec=None, fault: Optional[dict] = None) -> dict:
+    """Plain-dict (picklable) description of one replica's engine. `fault` holds
+    MockEngine fault-injection knobs (crash_after_steps, eos_every)."""
+    dt = {"bf16": "bfloat16", "fp16": "float16", "fp32": "float32"}[worker.quantization]
+    return dict(mock=worker.mock, mock_latency_ms=worker.mock_latency_ms, model=worker.model,
+                checkpoint=worker.checkpoint, tp=worker.tp, device=worker.device, dtype=dt,
+                block_size=worker.block_size, max_num_seqs=worker.max_num_seqs,
+                max_num_batched_tokens=worker.max_num_batched_tokens, max_model_len=worker.max_model_len,
+                gpu_memory_utilization=worker.gpu_memory_utilization, num_blocks=worker.num_blocks,
+                use_graphs=worker.use_graphs, seed=worker.seed, moe_comm=worker.moe_comm,
+                enable_prefix_cache=True if cache is None else cache.enable_prefix_cache,
+                cache_threshold=0.8 if cache is None else cache.memory_threshold,
+                draft_model=None if spec is None else spec.draft_model,
+                num_speculative_tokens=0 if spec is None else spec.num_speculative_tokens,
+                min_acceptance_rate=0.5 if spec is None else spec.min_acceptance_rate,
+                fault=dict(fault or {}))
+
+
+def make_engine(spec: dict):
+    if spec.get("mock"):
+        from ..engine.mock import MockEngine
+        f = spec.get("fault") or {}
+        return MockEngine(model_name=spec.get("model") or "mock", step_latency_s=spec.get("mock_latency_ms", 0) / 1000.0,
+                          max_num_seqs=spec.get("max_num_seqs", 256), crash_after_steps=f.get("crash_after_steps"),
+                          eos_every=f.get("eos_every"))
+    from ..engine import EngineConfig, LLMEngine
+    keys = set(EngineConfig.__dataclass_fields__)
+    ec = EngineConfig(**{k: v for k, v in spec.items() if k in keys})
+    eng = LLMEngine(ec)
+    if eng.spec is not None:
+        eng.spec.min_acceptance_rate = spec.get("min_acceptance_rate", 0.5)
+    return eng
+
+
+def engine_info(engine) -> dict:
+    m = engine.mcfg
+    info = {"model": m.name, "vocab_size": m.vocab_size, "hidden_size": m.hidden_size,
+            "max_model_len": getattr(engine, "max_model_len", getattr(m, "max_position", 8192)),
+            "eos_token_ids": list(m.eos_token_ids), "num_blocks": getattr(engine, "num_blocks", 0)}
+    try:
+        bb = engine._block_bytes()
+        info["kv_bytes_per_token"] = bb // engine.cfg.block_size
+    except Exception:
+        info["kv_bytes_per_token"] = 1024
+    return info
+
+
+def _is_oom(e: BaseException) -> bool:
+    try:
+        import torch
+        if isinstance(e, torch.cuda.OutOfMemoryError):
+            return True
+    except Exception:
+        pass
+    return "out of memory" in str(e).lower()
+
+
+# ---------------------------------------------------------------------------
+# the worker main loop
+# ---------------------------------------------------------------------------
+class EngineLoop:
+    """Drives one engine. `emit(kind, payload)` is called from the loop thread
+    with kind in {"out", "hb", "fatal"}."""
+
+    def __init__(self, engine, emit: Callable[[str, Any], None]):
+        self.engine = engine
+        self.emit = emit
+        self._inbox: pyqueue.SimpleQueue = pyqueue.SimpleQueue()
+        self._wake = threading.Event()
+        self._stop = False
+        self.steps = 0
+        self.last_step_s = 0.0
+
+    def submit(self, cmd: tuple) -> None:
+        self._inbox.put(cmd)
+        self._wake.set()
+
+    def _drain(self, outs: list) -> None:
+        from ..engine.request import RequestOutput, RequestType, SamplingParams
+        while True:
+            try:
+                cmd = self._inbox.get_nowait()
+            except pyqueue.Empty:
+                return
+            op = cmd[0]
+            if op == "add":
+                _, rid, prompt_ids, params, prio, kind = cmd
+                try:
+                    self.engine.add_request(rid, prompt_ids, params, prio, RequestType(kind))
+                except Exception as e:  # per-request rejection, never fatal
+                    outs.append(RequestOutput(rid, [], "", True, "error", prompt_tokens=len(prompt_ids),
+                                              error=f"Inference failed: {e}", error_code="inference_failed"))
+            elif op == "abort":
+                self.engine.abort(cmd[1])
+            elif op == "limits":
+                self.engine.set_limits(cmd[1], cmd[2])
+            elif op == "clear_cache":
+                self.engine.clear_prefix_cache()
+            elif op == "hang":  # fault injection (tests)
+                self.engine.hang = True
+            elif op == "stop":
+                self._stop = True
+
+    def _fail_inflight(self, code: str, msg: str) -> list:
+        from ..engine.request import RequestOutput
+        outs = []
+        for rid in list(getattr(self.engine, "requests", {}).keys()):
+            self.engine.abort(rid)
+            outs.append(RequestOutput(rid, [], "", True, "error", error=msg, error_code=code))
+        return outs
+
+    def run(self) -> None:
+        last_hb = 0.0
+        while not self._stop:
+            outs: list = []
+            self._drain(outs)
+            if self._stop:
+                break
+            if self.engine.has_work():
+                t0 = time.perf_counter()
+                try:
+                    outs += self.engine.step()
+                except SystemExit:
+                    raise
+                except Exception as e:  # contain the failure to the in-flight requests
+                    if _is_oom(e):
+                        log.warning("OOM in engine step; flushing prefix cache and retrying")
+                        try:
+                            self.engine.clear_prefix_cache()
+                            outs += self.engine.step()
+                        except Exception as e2:
+                            outs += self._fail_inflight("out_of_memory", f"Out of memory: {e2}")
+                    else:
+                        log.error("engine step failed: %s\n%s", e, traceback.format_exc())
+                        outs += self._fail_inflight("inference_failed", f"Inference failed: {e}")
+                self.last_step_s = time.perf_counter() - t0
+                self.steps += 1
+            else:
+                self._wake.wait(0.02)
+                self._wake.clear()
+            if outs:
+                self.emit("out", outs)
+            now = time.monotonic()
+            if now - last_hb >= HEARTBEAT_S:
+                last_hb = now
+                st = self.engine.stats()
+                st["last_step_ms"] = 1000 * self.last_step_s
+                self.emit("hb", st)
+        try:
+            if hasattr(self.engine, "stop_followers"):
+                self.engine.stop_followers()
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------------------
+# replica handles (server side)
+# ---------------------------------------------------------------------------
+class Replica:
+    """Server-side handle. Outputs are delivered through `on_event(replica_id,
+    kind, payload)` on an arbitrary thread (the server hops onto its loop)."""
+
+    kind = "base"
+
+    def __init__(self, rid: int, spec: dict, on_event: Callable[[int, str, Any], None]):
+        self.id = rid
+        self.spec = spec
+        self.on_event = on_event
+        self.info: dict = {}
+        self.stats: dict = {}
+        self.last_hb = time.monotonic()
+        self.ready = threading.Event()
+        self.error: Optional[str] = None
+        self.inflight: Dict[str, Any] = {}
+        self.restarts = 0
+        self.draining = False
+
+    def _event(self, kind: str, payload: Any) -> None:
+        if kind == "hb":
+            self.last_hb = time.monotonic()
+            self.stats = payload
+        elif kind == "ready":
+            self.info = payload
+            self.last_hb = time.monotonic()
+            self.ready.set()
+            return
+        elif kind == "fatal":
+            self.error = payload
+            self.ready.set()
+        self.on_event(self.id, kind, payload)
+
+    def wait_ready(self, timeout: float) -> bool:
+        ok = self.ready.wait(timeout)
+        return ok and self.error is None
+
+    def submit(self, rid: str, prompt_ids: List[int], params, priority: int, kind: str) -> None:
+        self._send(("add", rid, list(prompt_ids), params, int(priority), kind))
+
+    def abort(self, rid: str) -> None:
+        self._send(("abort", rid))
+
+    def set_limits(self, max_num_seqs: int, max_num_batched_tokens: int) -> None:
+        self._send(("limits", int(max_num_seqs), int(max_num_batched_tokens)))
+
+    def clear_cache(self) -> None:
+        self._send(("clear_cache",))
+
+    def inject_hang(self) -> None:
+        self._send(("hang",))
+
+    def heartbeat_age(self) -> float:
+        return time.monotonic() - self.last_hb
+
+    # subclass API
+    def start(self) -> None: ...
+    def _send(self, cmd: tuple) -> None: ...
+    def is_alive(self) -> bool: ...
+    def shutdown(self, timeout: float = 10.0) -> None: ...
+
+
+class InProcessReplica(Replica):
+    kind = "thread"
+
+    def __init__(self, rid, spec, on_event, engine=None):
+        super().__init__(rid, spec, on_event)
+        self._engine = engine
+        self.loop: Optional[EngineLoop] = None
+        self.thread: Optional[threading.Thread] = None
+
+    def start(self) -> None:
+        def main():
+            try:
+                eng = self._engine if self._engine is not None else make_engine(self.spec)
+                self.engine = eng
+                self.loop = EngineLoop(eng, self._event)
+                self._event("ready", engine_info(eng))
+                self.loop.run()
+            except BaseException as e:  # noqa: BLE001 - report every death
+                log.error("replica %d died: %s", self.id, e)
+                self._event("fatal", f"{type(e).__name__}: {e}")
+
+        self.thread = threading.Thread(target=main, name=f"replica-{self.id}", daemon=True)
+        self.thread.start()
+
+    def _send(self, cmd):
+        if self.loop is not None:
+            self.loop.submit(cmd)
+
+    def is_alive(self) -> bool:
+        return self.thread is not None and self.thread.is_alive() and self.error is None
+
+    def shutdown(self, timeout: float = 10.0) -> None:
+        if self.loop is not None:
+            self.loop.submit(("stop",))
+        if self.thread is not None:
+            self.thread.join(timeout)
+
+
+def _worker_main(spec: dict, rank: int, env: dict, cmd_q, out_q) -> None:
+    """Entry point of a replica process (one per GPU)."""
+    os.environ.update(env)
+    logging.basicConfig(level=os.environ.get("XGS_LOG_LEVEL", "WARNING"),
+                        format=f"[replica {env.get('XGS_REPLICA', '?')} rank {rank}] %(levelname)s %(message)s")
+    try:
+        eng_spec = dict(spec)
+        if not spec.get("mock"):
+            from ..parallel.state import init_distributed
+            import torch
+            dev = None if not spec.get("device") else torch.device(spec["device"])
+            init_distributed(tp_size=spec.get("tp", 1), device=dev)
+        eng = make_engine(eng_spec)
+        if rank != 0:
+            eng.follower_loop()
+            return
+        loop = EngineLoop(eng, lambda k, p: out_q.put((k, p)))
+
+        def reader():
+            while True:
+                cmd = cmd_q.get()
+                loop.submit(cmd)
+                if cmd[0] == "stop":
+                    return
+
+        threading.Thread(target=reader, daemon=True).start()
+        out_q.put(("ready", engine_info(eng)))
+        loop.run()
+    except SystemExit as e:
+        out_q.put(("fatal", f"worker exited: {e}"))
+        raise
+    except BaseException as e:  # noqa: BLE001
+        out_q.put(("fatal", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
+        raise
+
+
+class ProcessReplica(Replica):
+    kind = "process"
+
+    def __init__(self, rid, spec, on_event, gpus: Optional[List[int]] = None, master_port: int = 0):
+        super().__init__(rid, spec, on_event)
+        tp = spec.get("tp", 1)
+        self.gpus = gpus if gpus is not None else list(range(rid * tp, rid * tp + tp))
+        self.master_port = master_port or _free_port()
+        self.procs: list = []
+        self.cmd_q = None
+        self.out_q = None
+        self._reader: Optional[threading.Thread] = None
+
+    def start(self) -> None:
+        import multiprocessing as mp
+        ctx = mp.get_context("spawn")
+        self.cmd_q, self.out_q = ctx.Queue(), ctx.Queue()
+        tp = self.spec.get("tp", 1)
+        self.procs = []
+        for k in range(tp):
+            env = {"RANK": str(k), "WORLD_SIZE": str(tp), "LOCAL_RANK": str(self.gpus[k]),
+                   "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(self.master_port), "XGS_REPLICA": str(self.id),
+                   "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+            p = ctx.Process(target=_worker_main, args=(self.spec, k, env, self.cmd_q if k == 0 else None, self.out_q),
+                            daemon=True, name=f"xgs-r{self.id}-tp{k}")
+            p.start()
+            self.procs.append(p)
+
+        def reader():
+            while True:
+                try:
+                    kind, payload = self.out_q.get()
+                except (EOFError, OSError):
+                    return
+                self._event(kind, payload)
+                if kind == "fatal":
+                    return
+
+        self._reader = threading.Thread(target=reader, daemon=True, name=f"replica-{self.id}-reader")
+        self._reader.start()
+
+    def _send(self, cmd):
+        if self.cmd_q is not None:
+            try:
+                self.cmd_q.put(cmd)
+            except (ValueError, OSError):
+                pass
+
+    def is_alive(self) -> bool:
+        return bool(self.procs) and all(p.is_alive() for p in self.procs) and self.error is None
+
+    def shutdown(self, timeout: float = 10.0) -> None:
+        self._send(("stop",))
+        t_end = time.monotonic() + timeout
+        for p in self.procs:
+            p.join(max(0.1, t_end - time.monotonic()))
+        for p in self.procs:
+            if p.is_alive():
+                p.kill()
+                p.join(2.0)
+
+    def kill(self) -> None:
+        """Fault injection: hard-kill the replica's processes."""
+        for p in self.procs:
+            if p.is_alive():
+                p.kill()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
