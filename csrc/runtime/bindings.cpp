@@ -260,6 +260,8 @@ PYBIND11_MODULE(_runtime, m) {
       .def("total_preemptions", &StepScheduler::total_preemptions)
       .def("set_limits", &StepScheduler::set_limits)
       .def("clear_prefix_cache", &StepScheduler::clear_prefix_cache)
+      .def("cached_prefix", &StepScheduler::cached_prefix)
+      .def("install_prefix", &StepScheduler::install_prefix)
       .def("seq_info",
            [](const StepScheduler& s, int64_t id) -> py::object {
              const Sequence* q = s.get(id);

@@ -26,6 +26,36 @@ void StepScheduler::set_limits(int max_num_seqs, int max_num_batched_tokens) {
 
 int StepScheduler::num_used_blocks() const { return alloc_.num_blocks() - alloc_.num_free(); }
 
+std::vector<int> StepScheduler::cached_prefix(const std::vector<int32_t>& tokens) {
+  return cache_.match(tokens.data(), static_cast<int>(tokens.size()), static_cast<int>(tokens.size()), false);
+}
+
+std::vector<int> StepScheduler::install_prefix(const std::vector<int32_t>& tokens, int n_pages) {
+  const int bs = cfg_.block_size;
+  n_pages = std::min<int>(n_pages, static_cast<int>(tokens.size()) / bs);
+  std::vector<int> have = cached_prefix(tokens);
+  const int before = std::min<int>(static_cast<int>(have.size()), n_pages);
+  have.resize(before);
+  std::vector<int> fresh;
+  for (int i = before; i < n_pages; ++i) {
+    int b = alloc_.alloc();
+    if (b < 0 && cache_.evict(1) > 0) b = alloc_.alloc();
+    if (b < 0) {
+      for (int f : fresh) alloc_.decref(f);
+      return {};
+    }
+    fresh.push_back(b);
+    have.push_back(b);
+  }
+  cache_.insert(tokens.data(), n_pages * bs, have.data(), n_pages);
+  for (int f : fresh) alloc_.decref(f);  // the cache now holds the only reference
+  std::vector<int> out;
+  out.reserve(have.size() + 1);
+  out.push_back(before);
+  out.insert(out.end(), have.begin(), have.end());
+  return out;
+}
+
 const Sequence* StepScheduler::get(int64_t id) const {
   auto it = seqs_.find(id);
   return it == seqs_.end() ? nullptr : it->second.get();

@@ -128,6 +128,12 @@ class StepScheduler {
   int64_t total_preemptions() const { return total_preemptions_; }
   void set_limits(int max_num_seqs, int max_num_batched_tokens);
   void clear_prefix_cache() { cache_.clear(); }
+  // KV export/import (cache entry serialisation, design.md:400-401):
+  // pages currently caching the page-aligned prefix of tokens (no stats, no incref)
+  std::vector<int> cached_prefix(const std::vector<int32_t>& tokens);
+  // make the first n_pages pages of tokens resident in the prefix cache; returns
+  // {#pages that were already cached, page ids...}. Empty on allocation failure.
+  std::vector<int> install_prefix(const std::vector<int32_t>& tokens, int n_pages);
 
  private:
   bool ensure_blocks(Sequence& s, int total_tokens);

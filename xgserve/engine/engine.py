@@ -428,6 +428,35 @@ class LLMEngine:
         with self._lock:
             self.sched.clear_prefix_cache()
 
+    def export_prefix(self, tokens: Sequence[int]):
+        """CacheEntry for the longest cached page-aligned prefix of `tokens` (this rank's KV shard)."""
+        from .kv_io import CacheEntry
+        with self._lock:
+            blocks = self.sched.cached_prefix([int(t) for t in tokens])
+            idx = torch.tensor(blocks, dtype=torch.long, device=self.device)
+            kv = self.runner.kv.index_select(2, idx).cpu()
+        n = len(blocks) * self.cfg.block_size
+        return CacheEntry([int(t) for t in tokens[:n]], kv, n, self.mcfg.name, self.cfg.block_size, self.tp_rank)
+
+    def import_prefix(self, entry) -> int:
+        """Install a CacheEntry into the prefix cache; returns #pages newly written."""
+        if entry.block_size != self.cfg.block_size:
+            raise ValueError(f"entry block_size {entry.block_size} != engine {self.cfg.block_size}")
+        want = tuple(self.runner.kv.shape[:2]) + (entry.kv.shape[2],) + tuple(self.runner.kv.shape[3:])
+        if tuple(entry.kv.shape) != want:
+            raise ValueError(f"entry KV shape {tuple(entry.kv.shape)} does not match this engine {want}")
+        n_pages = entry.kv.shape[2]
+        with self._lock:
+            res = self.sched.install_prefix([int(t) for t in entry.key], n_pages)
+            if not res:
+                raise MemoryError("no free KV pages to import the entry")
+            before, blocks = res[0], res[1:]
+            if len(blocks) > before:
+                idx = torch.tensor(blocks[before:], dtype=torch.long, device=self.device)
+                src = entry.kv[:, :, before:len(blocks)].to(self.device, self.runner.kv.dtype)
+                self.runner.kv.index_copy_(2, idx, src)
+        return len(blocks) - before
+
     def set_limits(self, max_num_seqs: int, max_num_batched_tokens: int):
         """Runtime batch limits (degradation / hot reload), clamped to the sizes the
         runner's buffers and graphs were built for."""

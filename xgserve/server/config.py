@@ -212,26 +212,50 @@ HOT_RELOADABLE = {
 }
 
 
+def _base_type(typ) -> tuple:
+    """(base type name, optional) for a dataclass field annotation (a string under
+    `from __future__ import annotations`)."""
+    tname = typ if isinstance(typ, str) else getattr(typ, "__name__", str(typ))
+    tname = tname.replace("typing.", "")
+    optional = tname.startswith("Optional[")
+    if optional:
+        tname = tname[len("Optional["):-1]
+    return tname, optional
+
+
 def _coerce(value: Any, typ) -> Any:
-    t = typ if isinstance(typ, type) else None
-    tname = str(typ)
+    base, optional = _base_type(typ)
+    if value is None:
+        if optional:
+            return None
+        raise ValueError("null is not allowed")
     if isinstance(value, str):
         s = value.strip()
-        if s.lower() in ("none", "null") and "Optional" in tname:
+        if optional and s.lower() in ("none", "null"):
             return None
-        if t is bool or "bool" in tname:
+        if base == "bool":
             if s.lower() in ("1", "true", "yes", "on"):
                 return True
             if s.lower() in ("0", "false", "no", "off"):
                 return False
             raise ValueError(f"not a boolean: {value!r}")
-        if t is int or tname.startswith("typing.Optional[int]") or tname == "Optional[int]":
+        if base == "int":
             return int(s)
-        if t is float or "float" in tname:
+        if base == "float":
             return float(s)
         return s
-    if (t is float or "float" in tname) and isinstance(value, int) and not isinstance(value, bool):
+    if base == "bool" and not isinstance(value, bool):
+        raise ValueError(f"not a boolean: {value!r}")
+    if base == "int" and (isinstance(value, bool) or not isinstance(value, int)):
+        if isinstance(value, float) and value.is_integer():
+            return int(value)
+        raise ValueError(f"not an integer: {value!r}")
+    if base == "float":
+        if isinstance(value, bool) or not isinstance(value, (int, float)):
+            raise ValueError(f"not a number: {value!r}")
         return float(value)
+    if base == "str" and not isinstance(value, str):
+        return str(value)
     return value
 
 
