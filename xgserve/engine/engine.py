@@ -71,6 +71,7 @@ class EngineConfig:
     # speculative decoding (Req 12)
     draft_model: Optional[str] = None
     num_speculative_tokens: int = 0
+    spec_min_acceptance_rate: float = 0.5
 
     def resolved_device(self) -> torch.device:
         if self.device:
@@ -137,7 +138,8 @@ class LLMEngine:
         self.spec = None
         if cfg.draft_model and cfg.num_speculative_tokens > 0:
             from .spec_decode import SpeculativeDecoder
-            self.spec = SpeculativeDecoder(self, cfg.draft_model, cfg.num_speculative_tokens)
+            self.spec = SpeculativeDecoder(self, cfg.draft_model, cfg.num_speculative_tokens,
+                                           cfg.spec_min_acceptance_rate)
         log.info("engine ready: model=%s tp=%d blocks=%d (%.1f GiB KV) load=%.1fs", self.mcfg.name, get_state().tp_size,
                  num_blocks, self.runner.kv_bytes() / 2**30, self.load_time)
 
@@ -273,9 +275,11 @@ class LLMEngine:
         if self.is_driver:
             self._bind_slots(plan)
         samp = self._sampling_rows(plan)
-        if self.spec is not None and plan["num_seqs"] > plan["num_decodes"]:
-            return outs + self.spec.verify_step(plan, samp)
-        toks, lps, hidden = self.runner.execute(plan, samp)
+        counts = None
+        if self.spec is not None and self.is_driver and plan["num_seqs"] > plan["num_decodes"]:
+            toks, lps, hidden, counts = self.spec.verify_execute(plan, samp)
+        else:
+            toks, lps, hidden = self.runner.execute(plan, samp)
         self.step_count += 1
         self.stats_counters["steps"] += 1
         if plan["num_decodes"] == plan["num_seqs"]:
@@ -283,7 +287,7 @@ class LLMEngine:
         self.stats_counters["prefill_tokens_computed"] += int(plan["num_tokens"]) - int(plan["num_decodes"])
         if hidden is not None:
             self._accumulate_embeddings(plan, hidden)
-        return outs + self._process(plan, toks, lps)
+        return outs + self._process(plan, toks, lps, counts)
 
     def _accumulate_embeddings(self, plan, hidden):
         from .. import ops
@@ -301,31 +305,42 @@ class LLMEngine:
             rr = torch.tensor([r], dtype=torch.int32, device=self.device)
             ops.segment_sum(hidden, cut, self.embed_acc, rr)
 
-    def _process(self, plan, toks, lps) -> List[RequestOutput]:
+    def _process(self, plan, toks, lps, counts=None) -> List[RequestOutput]:
+        """Apply sampled tokens. `counts[j]` tokens belong to sampled sequence j
+        (1 for plain decode; accepted drafts + 1 after a speculative verify)."""
         outs: List[RequestOutput] = []
         ns = int(plan["num_seqs"])
         seq_ids = plan["seq_ids"]
         n_sample = int(plan["num_sample"])
-        counts = np.ones(n_sample, np.int32)
+        if counts is None:
+            counts = np.ones(n_sample, np.int32)
         now = time.monotonic()
         with self._lock:
-            finished = self.sched.update(toks if toks is not None else np.zeros(n_sample, np.int32), counts)
+            finished = self.sched.update(toks if toks is not None else np.zeros(int(counts.sum()), np.int32),
+                                         counts)
             fin_map = {f[0]: f for f in finished}
             if not self.is_driver:
                 return outs
-            self.stats_counters["generation_tokens"] += n_sample
+            self.stats_counters["generation_tokens"] += int(counts.sum())
             sidx = plan["sample_seq_index"]
+            k = 0
             for j in range(n_sample):
+                c = int(counts[j])
                 sid = int(seq_ids[sidx[j]])
                 req = self.by_seq.get(sid)
                 if req is None:
+                    k += c
                     continue
-                tok = int(toks[j])
+                f = fin_map.get(sid)
+                # the scheduler stops appending at the first stop condition inside an accepted run
+                take = c if f is None else max(1, min(c, f[3] - len(req.output_ids)))
+                new = [int(t) for t in toks[k:k + take]]
+                new_lps = [float(x) for x in lps[k:k + take]] if (lps is not None and req.params.logprobs) else None
+                k += c
                 if req.first_token_time is None:
                     req.first_token_time = now
-                req.output_ids.append(tok)
-                text = req.detok.add([tok])
-                f = fin_map.get(sid)
+                req.output_ids.extend(new)
+                text = req.detok.add(new)
                 reason = None
                 if req.detok.stopped and f is None:
                     self.sched.abort(sid)
@@ -335,10 +350,10 @@ class LLMEngine:
                     req.cached_tokens = f[4]
                     if not req.detok.stopped:
                         text += req.detok.flush()
-                out = RequestOutput(req.request_id, [tok], text, reason is not None,
+                out = RequestOutput(req.request_id, new, text, reason is not None,
                                     FINISH_NAMES.get(reason) if reason else None,
                                     prompt_tokens=len(req.prompt_ids), completion_tokens=len(req.output_ids),
-                                    logprobs=[float(lps[j])] if (lps is not None and req.params.logprobs) else None)
+                                    logprobs=new_lps)
                 if reason is not None:
                     out.cached_tokens = req.cached_tokens
                     self._finish(req, reason)
@@ -374,8 +389,6 @@ class LLMEngine:
                 plan = payload
                 if plan["num_tokens"]:
                     self.runner.execute(plan, None)
-            elif kind == "spec":
-                self.spec.follower_step(payload)
 
     def stop_followers(self):
         if get_state().tp_size > 1 and self.is_driver:
@@ -422,6 +435,7 @@ class LLMEngine:
             "cache": cs,
             "preemptions": self.sched.total_preemptions(),
             **self.stats_counters,
+            **({"speculative": self.spec.stats()} if self.spec is not None else {}),
         }
 
     def clear_prefix_cache(self):

@@ -86,6 +86,8 @@ register(ModelConfig("gpt2", "gpt2", 768, 12, 12, 12, 64, 3072, 50257, 1024, 0.0
 # tiny variants for CPU / unit tests (same code paths, small dims)
 register(ModelConfig("llama-tiny", "llama", 256, 2, 4, 2, 64, 512, 512, 1024, 10000.0,
                      bos_token_id=1, eos_token_ids=[2]))
+register(ModelConfig("llama-tiny-draft", "llama", 128, 1, 2, 1, 64, 256, 512, 1024, 10000.0,
+                     bos_token_id=1, eos_token_ids=[2]))
 register(ModelConfig("llama-tiny-gqa8", "llama", 512, 2, 8, 8, 64, 1024, 512, 1024, 10000.0,
                      bos_token_id=1, eos_token_ids=[2]))
 register(ModelConfig("mixtral-tiny", "mixtral", 256, 2, 4, 2, 64, 256, 512, 1024, 1000000.0,

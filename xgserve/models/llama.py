@@ -84,12 +84,16 @@ class LlamaLayer(nn.Module):
             dims_ok = dims_ok and Fl % 256 == 0 and (2 * Fl) % 64 == 0 and self.split_down
         self.fast_ok = bool(dims_ok) and torch.device(device).type == "cuda"
 
+    def _ar(self, x: torch.Tensor) -> torch.Tensor:
+        # keyed on the layer's own TP degree: a TP=1 draft model may live in a TP>1 process
+        return x if self.tp == 1 else comm.tp_all_reduce(x)
+
     # ------------------------------------------------------------------ MoE
     def _moe_allreduce(self, h: torch.Tensor) -> torch.Tensor:
         logits = F.linear(h, self.router)
         w, ids = ops.moe_topk_softmax(logits, self.cfg.experts_per_token)
         out = ops.fused_moe(h, self.w13, self.w2, w, ids, self.expert_offset)
-        return comm.tp_all_reduce(out)
+        return self._ar(out)
 
     def _moe_alltoall(self, h: torch.Tensor) -> torch.Tensor:
         tp, r = self.tp, self.rank
@@ -135,13 +139,13 @@ class LlamaLayer(nn.Module):
             return self._moe_allreduce(h)
         gu = F.linear(h, self.gate_up)
         a = ops.silu_and_mul(gu, interleave16=True)
-        return comm.tp_all_reduce(F.linear(a, self.down))
+        return self._ar(F.linear(a, self.down))
 
     def _row_parallel_fast(self, a: torch.Tensor, w: torch.Tensor, split: int):
         pend = skinny_linear(a, w, None, MODE_PARTIAL)
         if self.tp == 1:
             return pend  # reduced by the consumer's prologue
-        return comm.tp_all_reduce(pend.materialize())
+        return self._ar(pend.materialize())
 
     def forward(self, x, residual: Optional[torch.Tensor], meta: AttnMeta,
                 kv: Tuple[torch.Tensor, torch.Tensor], cos_sin: torch.Tensor):
@@ -174,7 +178,7 @@ class LlamaLayer(nn.Module):
             return self.mlp(h), residual
         qkv = F.linear(h, self.qkv)
         a = self.attn(qkv, meta, kv, cos_sin)
-        o = comm.tp_all_reduce(F.linear(a, self.o))
+        o = self._ar(F.linear(a, self.o))
         h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
         return self.mlp(h), residual
 

@@ -140,6 +140,11 @@ class MetricsCollector:
             self.spec_proposed += proposed
             self.spec_accepted += accepted
 
+    def set_spec_totals(self, proposed: int, accepted: int):
+        """Absolute draft-token counters (summed over replicas' heartbeats)."""
+        with self._lock:
+            self.spec_proposed, self.spec_accepted = proposed, accepted
+
     # ---- snapshot (design.md:480-491) -------------------------------------
     def snapshot(self) -> dict:
         with self._lock:

@@ -532,6 +532,10 @@ class InferenceServer:
     def check_health(self) -> None:
         hb_timeout = self.cfg.scheduler.heartbeat_timeout_s
         healthy = self._healthy_ids()
+        specs = [r.stats.get("speculative") for r in self.replicas.values() if r.stats.get("speculative")]
+        if specs:
+            self.metrics.set_spec_totals(sum(x["draft_tokens_proposed"] for x in specs),
+                                         sum(x["draft_tokens_accepted"] for x in specs))
         for rid in list(self.routable):
             r = self.replicas.get(rid)
             if r is None:

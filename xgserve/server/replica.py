@@ -62,10 +62,8 @@ def make_engine(spec: dict):
     from ..engine import EngineConfig, LLMEngine
     keys = set(EngineConfig.__dataclass_fields__)
     ec = EngineConfig(**{k: v for k, v in spec.items() if k in keys})
-    eng = LLMEngine(ec)
-    if eng.spec is not None:
-        eng.spec.min_acceptance_rate = spec.get("min_acceptance_rate", 0.5)
-    return eng
+    ec.spec_min_acceptance_rate = spec.get("min_acceptance_rate", 0.5)
+    return LLMEngine(ec)
 
 
 def engine_info(engine) -> dict:
