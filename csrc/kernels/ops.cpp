@@ -7,6 +7,9 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <vector>
+#include <cstring>
+#include <pybind11/stl.h>
 
 namespace py = pybind11;
 
@@ -38,6 +41,16 @@ void moe_grouped_gemm(const uint16_t*, const int32_t*, const uint16_t*, uint16_t
                       int, int, int, int, int, int, hipStream_t);
 void moe_silu_mul_gather(const uint16_t*, uint16_t*, int, int, hipStream_t);
 void moe_combine(const uint16_t*, const int32_t*, const float*, uint16_t*, int, int, int, hipStream_t);
+int custom_allreduce(const void*, void*, int64_t, int64_t, const uintptr_t*, const uintptr_t*, int, int, uint32_t*,
+                     hipStream_t);
+int car_max_blocks();
+int car_chunk();
+int car_max_ranks();
+int car_alloc_uncached(int64_t, void**);
+int car_ipc_handle(void*, hipIpcMemHandle_t*);
+int car_ipc_open(const hipIpcMemHandle_t*, void**);
+int car_ipc_close(void*);
+int car_free(void*);
 }  // namespace xgk
 
 template <typename T>
@@ -188,5 +201,37 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("device_synchronize", []() {
     hipError_t e = hipDeviceSynchronize();
     if (e != hipSuccess) throw std::runtime_error(hipGetErrorString(e));
+  });
+
+  // ---- custom one-shot xGMI all-reduce (csrc/comm/custom_allreduce.hip)
+  m.def("car_limits", []() { return py::make_tuple(xgk::car_max_ranks(), xgk::car_max_blocks(), xgk::car_chunk()); });
+  m.def("car_alloc_uncached", [](int64_t bytes) {
+    void* p = nullptr;
+    if (xgk::car_alloc_uncached(bytes, &p)) throw std::runtime_error("car_alloc_uncached failed");
+    return reinterpret_cast<uintptr_t>(p);
+  });
+  m.def("car_ipc_handle", [](uintptr_t ptr) {
+    hipIpcMemHandle_t h;
+    if (xgk::car_ipc_handle(reinterpret_cast<void*>(ptr), &h)) throw std::runtime_error("hipIpcGetMemHandle failed");
+    return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  });
+  m.def("car_ipc_open", [](py::bytes handle) {
+    std::string s = handle;
+    if (s.size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("bad IPC handle size");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, s.data(), sizeof(h));
+    void* p = nullptr;
+    if (xgk::car_ipc_open(&h, &p)) throw std::runtime_error("hipIpcOpenMemHandle failed");
+    return reinterpret_cast<uintptr_t>(p);
+  });
+  m.def("car_ipc_close", [](uintptr_t p) { return xgk::car_ipc_close(reinterpret_cast<void*>(p)) == 0; });
+  m.def("car_free", [](uintptr_t p) { return xgk::car_free(reinterpret_cast<void*>(p)) == 0; });
+  m.def("custom_allreduce", [](uintptr_t in, uintptr_t out, int64_t nbytes, int64_t slot_bytes,
+                               std::vector<uintptr_t> data, std::vector<uintptr_t> sig, int rank, uintptr_t gens,
+                               uintptr_t st) {
+    if (data.size() != sig.size()) throw std::invalid_argument("custom_allreduce: pointer lists differ in size");
+    check(xgk::custom_allreduce(P<void>(in), P<void>(out), nbytes, slot_bytes, data.data(), sig.data(), rank,
+                                static_cast<int>(data.size()), P<uint32_t>(gens), S(st)),
+          "custom_allreduce");
   });
 }

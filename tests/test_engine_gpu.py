@@ -115,3 +115,50 @@ def test_embeddings_request(llama_small):
     v = torch.tensor(emb)
     assert v.shape[0] == llama_small.cfg.hidden_size
     assert abs(float(v.norm()) - 1.0) < 1e-3
+
+
+def test_speculative_self_draft_on_gpu(llama_small):
+    """Draft == target weights on the GPU (graphs on): nearly every draft token is
+    accepted and the output tracks plain greedy decoding (bf16 verify rows go
+    through the prefill kernel, plain decode through the decode kernel, so a rare
+    near-tie may flip late tokens)."""
+    prompts = [[128000] + list(range(300 + 13 * i, 340 + 13 * i)) for i in range(4)]
+    sp = SamplingParams(max_tokens=16, temperature=0.0, ignore_eos=True)
+    want = _engine(llama_small).generate(prompts, sp)
+    eng = _engine(llama_small, draft_model=llama_small, num_speculative_tokens=3)
+    got = eng.generate(prompts, sp)
+    st = eng.stats()["speculative"]
+    assert st["acceptance_rate"] > 0.8, st
+    agree = sum(a[:8] == b[:8] for a, b in zip(got, want))
+    assert agree >= 3, (got, want)
+
+
+def test_http_server_with_gpu_engine(llama_small):
+    """The HTTP layer over a real HIP engine replica (in-process)."""
+    import asyncio
+    import json
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from _server_util import run_with_client
+    from xgserve.server.config import load_config
+    eng = _engine(llama_small)
+    cfg = load_config(env={}, overrides={"worker": {"model": "llama3-8b", "in_process": True}})
+
+    async def fn(c, srv):
+        rs = await asyncio.gather(*[c.post("/generate", data=json.dumps(
+            {"prompt": f"hello {i}", "max_tokens": 8, "temperature": 0.0, "ignore_eos": True})) for i in range(4)])
+        for r in rs:
+            d = await r.json()
+            assert r.status == 200, d
+            assert d["usage"]["completion_tokens"] == 8
+        r = await c.post("/generate", data=json.dumps({"prompt": "stream me", "max_tokens": 5, "stream": True,
+                                                       "ignore_eos": True}))
+        body = await r.read()
+        assert b'"type":"done"' in body
+        r = await c.post("/embeddings", data=json.dumps({"input": ["a", "bb"]}))
+        d = await r.json()
+        assert r.status == 200 and len(d["data"][0]["embedding"]) == 4096
+        return True
+
+    assert run_with_client(cfg, fn, engine=eng, timeout=300)

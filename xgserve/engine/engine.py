@@ -96,6 +96,8 @@ class LLMEngine:
                                                                  checkpoint=cfg.checkpoint, seed=cfg.seed)
         self.model.set_moe_comm(cfg.moe_comm)
         self.load_time = time.time() - t0
+        from ..parallel.custom_ar import maybe_enable
+        self.custom_ar = maybe_enable(st, self.model.device)  # one-shot xGMI all-reduce for TP decode
         self.device = self.model.device
         self.max_model_len = min(cfg.max_model_len or self.mcfg.max_position, self.mcfg.max_position)
         self.tokenizer = load_tokenizer(self.mcfg, cfg.checkpoint)

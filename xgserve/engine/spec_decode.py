@@ -66,11 +66,14 @@ class SpeculativeDecoder:
         self.seqs: Dict[int, _DraftSeq] = {}
         if not self.enabled:
             return
-        dcfg = get_config(draft_model)
+        if isinstance(draft_model, str):
+            dcfg = get_config(draft_model)
+            self.model = build_model(dcfg, device=engine.device, dtype=engine.model.dtype, seed=engine.cfg.seed,
+                                     tp=1, rank=0)
+        else:  # a pre-built TP=1 model (tests, or a draft sharing memory with something else)
+            self.model, dcfg = draft_model, draft_model.cfg
         if dcfg.vocab_size != engine.mcfg.vocab_size:
             raise ValueError(f"draft vocab {dcfg.vocab_size} != target vocab {engine.mcfg.vocab_size}")
-        self.model = build_model(dcfg, device=engine.device, dtype=engine.model.dtype, seed=engine.cfg.seed,
-                                 tp=1, rank=0)
         ec = engine.cfg
         bs = ec.block_size
         per_seq = (engine.max_model_len + bs - 1) // bs + 1
