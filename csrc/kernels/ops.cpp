@@ -20,6 +20,7 @@ void layernorm(const uint16_t*, const uint16_t*, const uint16_t*, uint16_t*, int
 void silu_and_mul(const uint16_t*, uint16_t*, int, int, int, hipStream_t);
 int skinny_gemm(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, hipStream_t);
 int skinny_slab_kmax(int);
+int gemm_m64(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 void add_partials_rmsnorm(const float*, int, int, uint16_t*, const uint16_t*, uint16_t*, int, float, hipStream_t);
 void reduce_partials(const float*, int, int64_t, uint16_t*, hipStream_t);
 int rope_cache_partials(const float*, int, uint16_t*, int64_t, const int32_t*, const float*, uint16_t*, uint16_t*,
@@ -233,5 +234,12 @@ PYBIND11_MODULE(_kernels, m) {
     check(xgk::custom_allreduce(P<void>(in), P<void>(out), nbytes, slot_bytes, data.data(), sig.data(), rank,
                                 static_cast<int>(data.size()), P<uint32_t>(gens), S(st)),
           "custom_allreduce");
+  });
+
+  m.def("gemm_m64", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
+                       int mode, int nw, int variant, uintptr_t st) {
+    check(xgk::gemm_m64(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode, nw,
+                        variant, S(st)),
+          "gemm_m64");
   });
 }

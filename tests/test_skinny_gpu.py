@@ -100,3 +100,44 @@ def test_rope_cache_partials_matches_bf16_path():
     torch.testing.assert_close(q.float(), qkv[:, :Hq * D].float(), atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(kc1.float(), kc2.float(), atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(vc1.float(), vc2.float(), atol=3e-2, rtol=2e-2)
+
+
+# ---------------------------------------------------------------- gemm_m64 (16 < M <= 64)
+@pytest.mark.parametrize("M", [17, 24, 32, 33, 48, 63, 64])
+@pytest.mark.parametrize("N,K,nw,S", [(6144, 4096, 1, 4), (4096, 4096, 1, 4), (4096, 14336, 1, 4),
+                                      (4096, 14336, 2, 1), (1024, 512, 1, 2), (768, 256, 1, 1)])
+def test_gemm_m64_partial(M, N, K, nw, S):
+    from xgserve.ops.linear import m64_linear
+    if N % (64 * nw) or K % (S * 256):
+        pytest.skip("shape not tileable")
+    x, w = rnd(M, K), rnd(N, K, scale=0.02)
+    pend = m64_linear(x, w, MODE_PARTIAL, split_k=S, nw=nw)
+    ref = x.float() @ w.float().t()
+    assert pend.part.shape == (S, M, N)
+    assert rel_err(pend.part.sum(0), ref) < 1e-5
+    assert rel_err(pend.materialize(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("M", [17, 40, 64])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_gemm_m64_variants_and_modes(M, variant):
+    from xgserve.ops.linear import m64_linear
+    F_, H = 1024, 512
+    x = rnd(M, H)
+    g, u = rnd(F_, H, scale=0.05), rnd(F_, H, scale=0.05)
+    w = interleave_gate_up(g, u)
+    got = m64_linear(x, w, MODE_SILU, variant=variant)
+    ref = torch.nn.functional.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
+    assert got.shape == (M, F_)
+    assert rel_err(got, ref) < 1e-2
+    w2 = rnd(2048, H, scale=0.02)
+    got2 = m64_linear(x, w2, MODE_BF16, variant=variant)
+    assert rel_err(got2, x.float() @ w2.float().t()) < 1e-2
+
+
+def test_gemm_m64_rejects_bad_shapes():
+    from xgserve.ops.linear import m64_linear
+    with pytest.raises(ValueError):
+        m64_linear(rnd(8, 256), rnd(256, 256), MODE_PARTIAL)   # M <= 16: not this kernel
+    with pytest.raises(ValueError):
+        m64_linear(rnd(32, 200), rnd(256, 200), MODE_PARTIAL)  # K % 256

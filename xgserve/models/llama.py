@@ -29,7 +29,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..parallel import comm
 from ..parallel.state import get_state
-from ..ops.linear import MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, pick_split, skinny_linear
+from ..ops.linear import MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, m64_linear, m64_plan, pick_split, skinny_linear
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
 from .config import ModelConfig
 
@@ -83,6 +83,13 @@ class LlamaLayer(nn.Module):
             self.split_down = pick_split(H, Fl)
             dims_ok = dims_ok and Fl % 256 == 0 and (2 * Fl) % 64 == 0 and self.split_down
         self.fast_ok = bool(dims_ok) and torch.device(device).type == "cuda"
+        # 16 < M <= 64: gemm_m64 for QKV / O / down (split-K partials into the consumers),
+        # and the fused SiLU-gate gate_up above M = 32 (measured: bench/gemm_bench.py)
+        self.m64_ok = self.fast_ok and all(
+            m64_plan(64, n, k, MODE_PARTIAL) is not None
+            for n, k in ((Nqkv, H), (H, Hq * D)) + (() if self.moe else ((H, cfg.intermediate_size // tp),)))
+        self.m64_silu_ok = self.m64_ok and not self.moe and m64_plan(64, 2 * (cfg.intermediate_size // tp), H,
+                                                                     MODE_SILU) is not None
 
     def _ar(self, x: torch.Tensor) -> torch.Tensor:
         # keyed on the layer's own TP degree: a TP=1 draft model may live in a TP>1 process
@@ -167,6 +174,21 @@ class LlamaLayer(nn.Module):
                 return self.mlp(h), residual
             act = skinny_linear(h, self.gate_up, mode=MODE_SILU)
             return self._row_parallel_fast(act, self.down, self.split_down), residual
+        if self.m64_ok and T <= FAST_M_SLAB:
+            pqkv = m64_linear(h, self.qkv, MODE_PARTIAL)
+            a = self.attn.from_partials(pqkv, meta, kv, cos_sin)
+            o = m64_linear(a, self.o, MODE_PARTIAL)
+            if self.tp > 1:
+                o = self._ar(o.materialize())
+            h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
+            if self.moe:
+                return self.mlp(h), residual
+            if self.m64_silu_ok and T > 32:
+                act = m64_linear(h, self.gate_up, MODE_SILU)
+            else:
+                act = ops.silu_and_mul(F.linear(h, self.gate_up), interleave16=True)
+            d = m64_linear(act, self.down, MODE_PARTIAL)
+            return (d if self.tp == 1 else self._ar(d.materialize())), residual
         if self.fast_ok and T <= FAST_M_SLAB:
             # 16 < M <= 64: measured per shape on MI355X -- only the O projection
             # (N = H) is faster on the LDS-slab kernel; its split-K partials are
