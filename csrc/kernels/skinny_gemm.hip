@@ -331,7 +331,9 @@ int skinny_gemm(const uint16_t* x, int M, int K, const uint16_t* w, int N, float
 // Split-K consumers
 // ---------------------------------------------------------------------------
 // residual[t] += sum_s part[s, t]; out[t] = rmsnorm(residual[t]) * w
-template <int VPT>
+// SP > 0: compile-time partial count (every load of a chunk issued before the
+// adds); SP == 0: runtime S.
+template <int VPT, int SP>
 __global__ void __launch_bounds__(256) add_partials_rmsnorm_kernel(const float* __restrict__ part, int S, int T,
                                                                    uint16_t* __restrict__ residual,
                                                                    const uint16_t* __restrict__ w,
@@ -347,12 +349,27 @@ __global__ void __launch_bounds__(256) add_partials_rmsnorm_kernel(const float* 
     const int c = threadIdx.x + k * blockDim.x;
     if (c < nchunk) {
       unpack8(ld16(rr + c * 8), v[k]);
-      for (int s = 0; s < S; ++s) {
-        const float* pp = part + (static_cast<int64_t>(s) * T + row) * H + c * 8;
-        const float4 a = *reinterpret_cast<const float4*>(pp);
-        const float4 b = *reinterpret_cast<const float4*>(pp + 4);
-        v[k][0] += a.x; v[k][1] += a.y; v[k][2] += a.z; v[k][3] += a.w;
-        v[k][4] += b.x; v[k][5] += b.y; v[k][6] += b.z; v[k][7] += b.w;
+      if constexpr (SP > 0) {
+        float4 a[SP], b[SP];
+#pragma unroll
+        for (int s = 0; s < SP; ++s) {
+          const float* pp = part + (static_cast<int64_t>(s) * T + row) * H + c * 8;
+          a[s] = *reinterpret_cast<const float4*>(pp);
+          b[s] = *reinterpret_cast<const float4*>(pp + 4);
+        }
+#pragma unroll
+        for (int s = 0; s < SP; ++s) {
+          v[k][0] += a[s].x; v[k][1] += a[s].y; v[k][2] += a[s].z; v[k][3] += a[s].w;
+          v[k][4] += b[s].x; v[k][5] += b[s].y; v[k][6] += b[s].z; v[k][7] += b[s].w;
+        }
+      } else {
+        for (int s = 0; s < S; ++s) {
+          const float* pp = part + (static_cast<int64_t>(s) * T + row) * H + c * 8;
+          const float4 a = *reinterpret_cast<const float4*>(pp);
+          const float4 b = *reinterpret_cast<const float4*>(pp + 4);
+          v[k][0] += a.x; v[k][1] += a.y; v[k][2] += a.z; v[k][3] += a.w;
+          v[k][4] += b.x; v[k][5] += b.y; v[k][6] += b.z; v[k][7] += b.w;
+        }
       }
       const uint4 pk = pack8(v[k]);
       st16(rr + c * 8, pk);
@@ -384,12 +401,22 @@ void add_partials_rmsnorm(const float* part, int S, int T, uint16_t* residual, c
   int vpt = (nchunk + thr - 1) / thr;
   vpt = vpt <= 1 ? 1 : vpt <= 2 ? 2 : vpt <= 4 ? 4 : 8;
   dim3 g(T), b(thr);
+#define XGK_APR(V, SPV) hipLaunchKernelGGL((add_partials_rmsnorm_kernel<V, SPV>), g, b, 0, st, part, S, T, residual, \
+                                           w, out, H, eps)
+#define XGK_APR_S(V)            \
+  if (S == 1) XGK_APR(V, 1);    \
+  else if (S == 2) XGK_APR(V, 2); \
+  else if (S == 4) XGK_APR(V, 4); \
+  else if (S == 8) XGK_APR(V, 8); \
+  else XGK_APR(V, 0);
   switch (vpt) {
-    case 1: hipLaunchKernelGGL(add_partials_rmsnorm_kernel<1>, g, b, 0, st, part, S, T, residual, w, out, H, eps); break;
-    case 2: hipLaunchKernelGGL(add_partials_rmsnorm_kernel<2>, g, b, 0, st, part, S, T, residual, w, out, H, eps); break;
-    case 4: hipLaunchKernelGGL(add_partials_rmsnorm_kernel<4>, g, b, 0, st, part, S, T, residual, w, out, H, eps); break;
-    default: hipLaunchKernelGGL(add_partials_rmsnorm_kernel<8>, g, b, 0, st, part, S, T, residual, w, out, H, eps); break;
+    case 1: XGK_APR_S(1); break;
+    case 2: XGK_APR_S(2); break;
+    case 4: XGK_APR_S(4); break;
+    default: XGK_APR_S(8); break;
   }
+#undef XGK_APR_S
+#undef XGK_APR
 }
 
 // out[t, :] = bf16(sum_s part[s, t, :])  (used when a collective needs the sum)

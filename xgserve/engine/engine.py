@@ -72,6 +72,9 @@ class EngineConfig:
     draft_model: Optional[str] = None
     num_speculative_tokens: int = 0
     spec_min_acceptance_rate: float = 0.5
+    # detokenise / build step N's outputs while step N+1 runs on the GPU (first
+    # tokens are still emitted at once, so TTFT is unchanged)
+    overlap_outputs: bool = True
 
     def resolved_device(self) -> torch.device:
         if self.device:
@@ -131,6 +134,8 @@ class LLMEngine:
         self.slot_topp = np.ones(ns, np.float32)
         self.slot_topk = np.zeros(ns, np.int32)
         self.slot_seed = np.zeros(ns, np.uint64)
+        self.slot_ngen = np.zeros(ns, np.int64)  # tokens generated by the slot's owner (sampling counter)
+        self._deferred = None  # (plan, toks, lps, counts, fin_map) awaiting detokenisation
         self._seq_counter = itertools.count(1)
         self._lock = threading.Lock()
         self._pending_aborts: List[str] = []
@@ -218,7 +223,7 @@ class LLMEngine:
         self.stats_counters["requests_finished"] += 1
 
     def has_work(self) -> bool:
-        return self.sched.has_work() or bool(self._pending_aborts)
+        return self.sched.has_work() or bool(self._pending_aborts) or self._deferred is not None
 
     # ------------------------------------------------------------------ step
     def _bind_slots(self, plan) -> None:
@@ -230,6 +235,7 @@ class LLMEngine:
             r = self.by_seq.get(sid)
             self.slot_owner[s] = sid
             self.slot_req[s] = r
+            self.slot_ngen[s] = len(r.output_ids) if r is not None else 0
             if r is None:
                 self.slot_temp[s], self.slot_topp[s], self.slot_topk[s], self.slot_seed[s] = 0.0, 1.0, 0, 0
                 continue
@@ -246,8 +252,7 @@ class LLMEngine:
         slots = plan["slots"][idx]
         temps = self.slot_temp[slots]
         # counter-based per-request stream: mix(seed, #tokens generated so far)
-        n = np.array([len(self.slot_req[s].output_ids) if self.slot_req[s] is not None else 0
-                      for s in slots.tolist()], dtype=np.uint64) if not (temps <= 0).all() else None
+        n = self.slot_ngen[slots].astype(np.uint64) if not (temps <= 0).all() else None
         if n is None:
             seeds = self.slot_seed[slots].view(np.int64)
         else:
@@ -267,13 +272,14 @@ class LLMEngine:
                 outs.append(RequestOutput(rid, [], "", True, "abort"))
             self._pending_aborts.clear()
             if self.spec is not None:
+                outs += self._flush_deferred()  # the draft needs every request's tokens
                 self.spec.propose()
             plan = self.sched.schedule()
         st = get_state()
         if st.tp_size > 1:
             comm.tp_broadcast_object(("plan", plan), src=0)
         if plan["num_tokens"] == 0:
-            return outs
+            return outs + self._flush_deferred()
         if self.is_driver:
             self._bind_slots(plan)
         samp = self._sampling_rows(plan)
@@ -281,7 +287,9 @@ class LLMEngine:
         if self.spec is not None and self.is_driver and plan["num_seqs"] > plan["num_decodes"]:
             toks, lps, hidden, counts = self.spec.verify_execute(plan, samp)
         else:
-            toks, lps, hidden = self.runner.execute(plan, samp)
+            handle = self.runner.launch(plan, samp)
+            outs += self._flush_deferred()  # previous step's outputs, while this one runs
+            toks, lps, hidden = self.runner.wait(handle)
         self.step_count += 1
         self.stats_counters["steps"] += 1
         if plan["num_decodes"] == plan["num_seqs"]:
@@ -289,7 +297,25 @@ class LLMEngine:
         self.stats_counters["prefill_tokens_computed"] += int(plan["num_tokens"]) - int(plan["num_decodes"])
         if hidden is not None:
             self._accumulate_embeddings(plan, hidden)
-        return outs + self._process(plan, toks, lps, counts)
+        n_sample = int(plan["num_sample"])
+        if counts is None:
+            counts = np.ones(n_sample, np.int32)
+        fin_map = self._apply(plan, toks, counts)
+        if not self.is_driver:
+            return outs
+        first_tokens = bool(plan["is_prefill"][plan["sample_seq_index"]].any()) if n_sample else False
+        if self.cfg.overlap_outputs and self.spec is None and not first_tokens and not fin_map:
+            self._deferred = (plan, toks, lps, counts, fin_map)
+            return outs
+        with self._lock:
+            return outs + self._emit(plan, toks, lps, counts, fin_map)
+
+    def _flush_deferred(self) -> List[RequestOutput]:
+        d, self._deferred = self._deferred, None
+        if d is None:
+            return []
+        with self._lock:
+            return self._emit(*d)
 
     def _accumulate_embeddings(self, plan, hidden):
         from .. import ops
@@ -308,76 +334,88 @@ class LLMEngine:
             ops.segment_sum(hidden, cut, self.embed_acc, rr)
 
     def _process(self, plan, toks, lps, counts=None) -> List[RequestOutput]:
-        """Apply sampled tokens. `counts[j]` tokens belong to sampled sequence j
-        (1 for plain decode; accepted drafts + 1 after a speculative verify)."""
+        """Apply + emit in one go (tests / callers that run the runner themselves)."""
+        if counts is None:
+            counts = np.ones(int(plan["num_sample"]), np.int32)
+        fin_map = self._apply(plan, toks, counts)
+        if not self.is_driver:
+            return []
+        with self._lock:
+            return self._emit(plan, toks, lps, counts, fin_map)
+
+    def _apply(self, plan, toks, counts) -> dict:
+        """Feed sampled tokens to the C++ scheduler (stop checks, page publishing):
+        the part the next schedule() depends on. `counts[j]` tokens belong to
+        sampled sequence j (1 for plain decode; accepted drafts + 1 after a verify)."""
+        with self._lock:
+            finished = self.sched.update(toks if toks is not None else np.zeros(int(counts.sum()), np.int32),
+                                         counts)
+        if self.is_driver and counts.size:
+            np.add.at(self.slot_ngen, plan["slots"][plan["sample_seq_index"]], counts)
+        self.stats_counters["generation_tokens"] += int(counts.sum())
+        return {f[0]: f for f in finished}
+
+    def _emit(self, plan, toks, lps, counts, fin_map) -> List[RequestOutput]:
+        """Per-request host work of a step: detokenise, stop strings, RequestOutputs."""
         outs: List[RequestOutput] = []
         ns = int(plan["num_seqs"])
         seq_ids = plan["seq_ids"]
         n_sample = int(plan["num_sample"])
-        if counts is None:
-            counts = np.ones(n_sample, np.int32)
         now = time.monotonic()
-        with self._lock:
-            finished = self.sched.update(toks if toks is not None else np.zeros(int(counts.sum()), np.int32),
-                                         counts)
-            fin_map = {f[0]: f for f in finished}
-            if not self.is_driver:
-                return outs
-            self.stats_counters["generation_tokens"] += int(counts.sum())
-            sidx = plan["sample_seq_index"]
-            k = 0
-            for j in range(n_sample):
-                c = int(counts[j])
-                sid = int(seq_ids[sidx[j]])
-                req = self.by_seq.get(sid)
-                if req is None:
-                    k += c
-                    continue
-                f = fin_map.get(sid)
-                # the scheduler stops appending at the first stop condition inside an accepted run
-                take = c if f is None else max(1, min(c, f[3] - len(req.output_ids)))
-                new = [int(t) for t in toks[k:k + take]]
-                new_lps = [float(x) for x in lps[k:k + take]] if (lps is not None and req.params.logprobs) else None
+        sidx = plan["sample_seq_index"]
+        k = 0
+        for j in range(n_sample):
+            c = int(counts[j])
+            sid = int(seq_ids[sidx[j]])
+            req = self.by_seq.get(sid)
+            if req is None:
                 k += c
-                if req.first_token_time is None:
-                    req.first_token_time = now
-                req.output_ids.extend(new)
-                text = req.detok.add(new)
-                reason = None
-                if req.detok.stopped and f is None:
-                    self.sched.abort(sid)
-                    reason = FINISH_STOP_SEQ
-                elif f is not None:
-                    reason = f[1]
-                    req.cached_tokens = f[4]
-                    if not req.detok.stopped:
-                        text += req.detok.flush()
-                out = RequestOutput(req.request_id, new, text, reason is not None,
-                                    FINISH_NAMES.get(reason) if reason else None,
-                                    prompt_tokens=len(req.prompt_ids), completion_tokens=len(req.output_ids),
-                                    logprobs=new_lps)
-                if reason is not None:
-                    out.cached_tokens = req.cached_tokens
-                    self._finish(req, reason)
-                outs.append(out)
-            # prefill-only (embedding) completions
-            for sid, f in fin_map.items():
-                if f[1] != FINISH_EMBED:
-                    continue
-                req = self.by_seq.get(sid)
-                if req is None:
-                    continue
-                slot = None
-                for i in range(ns):
-                    if int(seq_ids[i]) == sid:
-                        slot = int(plan["slots"][i])
-                v = self.embed_acc[slot] / max(1, len(req.prompt_ids))
-                v = v / v.norm().clamp_min(1e-12)
-                emb = v.cpu().tolist()
-                self.embed_acc[slot].zero_()
-                outs.append(RequestOutput(req.request_id, [], "", True, "stop", prompt_tokens=len(req.prompt_ids),
-                                          completion_tokens=0, embedding=emb))
-                self._finish(req, FINISH_EMBED)
+                continue
+            f = fin_map.get(sid)
+            # the scheduler stops appending at the first stop condition inside an accepted run
+            take = c if f is None else max(1, min(c, f[3] - len(req.output_ids)))
+            new = [int(t) for t in toks[k:k + take]]
+            new_lps = [float(x) for x in lps[k:k + take]] if (lps is not None and req.params.logprobs) else None
+            k += c
+            if req.first_token_time is None:
+                req.first_token_time = now
+            req.output_ids.extend(new)
+            text = req.detok.add(new)
+            reason = None
+            if req.detok.stopped and f is None:
+                self.sched.abort(sid)
+                reason = FINISH_STOP_SEQ
+            elif f is not None:
+                reason = f[1]
+                req.cached_tokens = f[4]
+                if not req.detok.stopped:
+                    text += req.detok.flush()
+            out = RequestOutput(req.request_id, new, text, reason is not None,
+                                FINISH_NAMES.get(reason) if reason else None,
+                                prompt_tokens=len(req.prompt_ids), completion_tokens=len(req.output_ids),
+                                logprobs=new_lps)
+            if reason is not None:
+                out.cached_tokens = req.cached_tokens
+                self._finish(req, reason)
+            outs.append(out)
+        # prefill-only (embedding) completions
+        for sid, f in fin_map.items():
+            if f[1] != FINISH_EMBED:
+                continue
+            req = self.by_seq.get(sid)
+            if req is None:
+                continue
+            slot = None
+            for i in range(ns):
+                if int(seq_ids[i]) == sid:
+                    slot = int(plan["slots"][i])
+            v = self.embed_acc[slot] / max(1, len(req.prompt_ids))
+            v = v / v.norm().clamp_min(1e-12)
+            emb = v.cpu().tolist()
+            self.embed_acc[slot].zero_()
+            outs.append(RequestOutput(req.request_id, [], "", True, "stop", prompt_tokens=len(req.prompt_ids),
+                                      completion_tokens=0, embedding=emb))
+            self._finish(req, FINISH_EMBED)
         return outs
 
     # ------------------------------------------------------------------ followers (TP > 1)

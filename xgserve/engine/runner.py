@@ -179,16 +179,32 @@ class ModelRunner:
     def execute(self, plan: dict, samp: Optional[SamplingRows]):
         """Run one step. Returns (tokens np[int32], logprobs np[float32], hidden or None).
         On non-driver TP ranks the returned arrays are None."""
+        return self.wait(self.launch(plan, samp))
+
+    @torch.no_grad()
+    def launch(self, plan: dict, samp: Optional[SamplingRows]):
+        """Enqueue one step (inputs H2D, forward, sampling, tokens D2H) without
+        waiting for it; `wait(handle)` returns what `execute` returns. The host
+        can do other work (previous step's detokenisation) while the GPU runs."""
         T = int(plan["num_tokens"])
         Nd = int(plan["num_decodes"])
         ns = int(plan["num_seqs"])
         if T == 0:
-            return None, None, None
+            return (0, None, (None, None, None))
         need_hidden = bool(plan["is_embed"].any()) if ns else False
         bucket = self._graph_bucket(Nd) if (Nd == ns and T == Nd and not need_hidden) else None
         if bucket is not None and self.graphs:
             return self._execute_graph(plan, samp, Nd, bucket)
         return self._execute_eager(plan, samp, need_hidden)
+
+    def wait(self, handle):
+        n, hidden, ready = handle
+        if ready is not None:
+            return ready
+        torch.cuda.current_stream().synchronize()
+        if not self.is_driver:
+            return None, None, hidden
+        return self.h_tok[:n].numpy().copy(), self.h_lp[:n].numpy().copy(), hidden
 
     def _execute_graph(self, plan, samp: Optional[SamplingRows], n: int, bs: int):
         B, W = self.g_B, self.g_W
@@ -220,13 +236,11 @@ class ModelRunner:
             self.g_seed[:n].copy_(self.h_samp_s[:n], non_blocking=True)
         self.graphs[(bs, greedy)].replay()
         if not self.is_driver:
-            # no D2H to wait on: still drain before the pinned inputs get rewritten
-            torch.cuda.current_stream().synchronize()
-            return None, None, None
+            # no D2H to wait on; wait() still drains before the pinned inputs get rewritten
+            return (n, None, None)
         self.h_tok[:n].copy_(self.g_out_tok[:n], non_blocking=True)
         self.h_lp[:n].copy_(self.g_out_lp[:n], non_blocking=True)
-        torch.cuda.current_stream().synchronize()
-        return self.h_tok[:n].numpy().copy(), self.h_lp[:n].numpy().copy(), None
+        return (n, None, None)
 
     def _execute_eager(self, plan, samp: Optional[SamplingRows], need_hidden: bool):
         T = int(plan["num_tokens"])
@@ -274,13 +288,14 @@ class ModelRunner:
                         pre_block_tables=bt[Nd:], pre_qsl=pre_qsl, pre_seq_lens=sl[Nd:],
                         pre_max_q=int(plan["q_lens"][Nd:].max()) if Np > 0 else 0)
         h = self.model(ids, meta, self.kv_caches)
+        hid = h if need_hidden else None
         if S == 0:
-            return np.zeros(0, np.int32), np.zeros(0, np.float32), (h if need_hidden else None)
+            return (0, hid, (np.zeros(0, np.int32), np.zeros(0, np.float32), hid))
         logits = self.model.compute_logits(h.index_select(0, lidx.long()))
         if self.capture_logits:
             self.last_logits = logits.float().cpu()
         if not self.is_driver:
-            return None, None, (h if need_hidden else None)
+            return (S, hid, None) if self.is_cuda else (S, hid, (None, None, hid))
         if samp is None or samp.all_greedy:
             tok, lp = ops.argmax_logprob(logits)
         else:
@@ -294,6 +309,5 @@ class ModelRunner:
         if self.is_cuda:
             self.h_tok[:S].copy_(tok, non_blocking=True)
             self.h_lp[:S].copy_(lp, non_blocking=True)
-            torch.cuda.current_stream().synchronize()
-            return self.h_tok[:S].numpy().copy(), self.h_lp[:S].numpy().copy(), (h if need_hidden else None)
-        return tok.numpy().astype(np.int32), lp.numpy().astype(np.float32), (h if need_hidden else None)
+            return (S, hid, None)
+        return (S, hid, (tok.numpy().astype(np.int32), lp.numpy().astype(np.float32), hid))
