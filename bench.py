@@ -1,25 +1,29 @@
 #!/usr/bin/env python3
 """Headline benchmark: whole-node output tokens/s (+ p50 TTFT) of Llama-3-8B
 serving with continuous batching (BASELINE.json config 3: 64 concurrent
-synthetic requests per GPU), one DP replica per GPU.
+synthetic requests per replica), one DP replica per GPU by default.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--concurrency 64]
                   [--prompt-len 512] [--output-len 256] [--model llama3-8b]
+                  [--tp 1]
 
-For N > 1 launch one rank per GPU (torch.distributed.run); ranks are
-independent replicas (weak scaling: per-GPU work is fixed) and only meet at the
-timing barriers. A "step" is one engine iteration (scheduler + forward of the
-packed decode/prefill batch + sampling), the unit the engine serves in.
-Weights are random-init bf16 of the full architecture, prompts are synthetic
-token ids; finished requests are immediately replaced so the concurrency stays
-at --concurrency. Rank 0 prints ONE JSON line.
+For N > 1 launch one rank per GPU (torch.distributed.run). With --tp 1 the
+ranks are independent replicas (weak scaling: per-GPU work is fixed) that only
+meet at the timing barriers. With --tp T the N ranks form N/T tensor-parallel
+replicas (the other BASELINE configs: Llama-3-70B TP=8, Mixtral 8x7B TP=2):
+the TP leader of each replica drives its engine and the followers mirror the
+leader's step plans (RCCL/xGMI collectives + the custom one-shot all-reduce).
+A "step" is one engine iteration (scheduler + forward of the packed
+decode/prefill batch + sampling). Weights are random-init bf16 of the full
+architecture, prompts are synthetic token ids; finished requests are
+immediately replaced so the concurrency stays at --concurrency. Rank 0 prints
+ONE JSON line (value = whole-job output tokens/s).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
-import random
 import sys
 import time
 
@@ -32,13 +36,14 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--model", default="llama3-8b")
-    ap.add_argument("--concurrency", type=int, default=64)
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree per replica")
+    ap.add_argument("--concurrency", type=int, default=64, help="concurrent requests per replica")
     ap.add_argument("--prompt-len", type=int, default=512)
     ap.add_argument("--output-len", type=int, default=256)
     ap.add_argument("--max-batched-tokens", type=int, default=8192)
+    ap.add_argument("--moe-comm", default="alltoall", choices=["alltoall", "allreduce"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
-    ap.add_argument("--profile-steps", type=int, default=0, help="(debug) torch.profiler over N timed steps")
     return ap.parse_args()
 
 
@@ -51,19 +56,32 @@ def main():
     from xgserve.engine import EngineConfig, LLMEngine, SamplingParams
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    st = init_distributed(tp_size=1)
+    st = init_distributed(tp_size=a.tp)
     rank = st.rank
+    dp = world // a.tp
     dev = torch.device("cuda", torch.cuda.current_device())
     max_len = a.prompt_len + 2 * a.output_len + 16
-    ecfg = EngineConfig(model=a.model, device=str(dev), max_num_seqs=max(64, a.concurrency),
+    ecfg = EngineConfig(model=a.model, device=str(dev), tp=a.tp, max_num_seqs=max(64, a.concurrency),
                         max_num_batched_tokens=a.max_batched_tokens, max_model_len=max_len,
-                        use_graphs=not a.no_graphs, enable_prefix_cache=not a.no_prefix_cache,
+                        use_graphs=not a.no_graphs, enable_prefix_cache=not a.no_prefix_cache, moe_comm=a.moe_comm,
                         graph_batch_sizes=[b for b in [1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128]
-                                           if b <= max(64, a.concurrency)], seed=rank)
+                                           if b <= max(64, a.concurrency)], seed=st.dp_rank)
     eng = LLMEngine(ecfg)
-    V = eng.mcfg.vocab_size
-    rng = random.Random(1234 + rank)
+    leader = st.tp_rank == 0
+    # timing collectives run among the TP leaders only (followers sit in follower_loop)
+    leaders = [r for r in range(world) if r % a.tp == 0]
+    lgroup = None
+    if world > 1:
+        lgroup = dist.group.WORLD if a.tp == 1 else dist.new_group(leaders)
+    cpu_group = dist.new_group(leaders, backend="gloo") if world > 1 else None
+    if not leader:
+        eng.follower_loop()
+        dist.barrier()
+        dist.destroy_process_group()
+        return 0
 
+    V = eng.mcfg.vocab_size
+    rng = np.random.default_rng(1234 + st.dp_rank)
     counter = [0]
     arrival = {}
     first_tok = {}
@@ -72,7 +90,7 @@ def main():
         rid = f"r{rank}-{counter[0]}"
         counter[0] += 1
         # random token prompts: no accidental prefix sharing across requests
-        prompt = [rng.randrange(10, V - 10) for _ in range(a.prompt_len)]
+        prompt = rng.integers(10, V - 10, size=a.prompt_len).tolist()
         eng.add_request(rid, prompt, SamplingParams(max_tokens=max_tokens, temperature=0.0, ignore_eos=True))
         arrival[rid] = time.perf_counter()
 
@@ -96,9 +114,11 @@ def main():
     for _ in range(a.warmup):
         run_step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    if lgroup is not None:
+        dist.barrier(group=lgroup)
     torch.cuda.synchronize()
+    if os.environ.get("XGS_STEP_TIMING"):
+        eng.enable_step_timing()
     t_start_wall = time.perf_counter()
     tokens = 0
     first_before = set(first_tok)
@@ -106,24 +126,24 @@ def main():
         tokens += run_step()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start_wall
-    if world > 1:
-        dist.barrier()
+    if lgroup is not None:
+        dist.barrier(group=lgroup)
     torch.cuda.synchronize()
     ttfts = [first_tok[r] - arrival[r] for r in first_tok if r not in first_before]
     p50_local = float(np.median(ttfts)) if ttfts else float("nan")
 
-    t = torch.tensor([elapsed, float(tokens), p50_local], dtype=torch.float64, device=dev)
-    if world > 1:
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = t.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed, tokens, p50 = mx[0].item(), sm[1].item(), sm[2].item() / world
+    t = torch.tensor([elapsed, float(tokens), p50_local], dtype=torch.float64)
+    if cpu_group is not None:
+        mx, sm = t.clone(), t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=cpu_group)
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM, group=cpu_group)
+        elapsed, tokens, p50 = mx[0].item(), sm[1].item(), sm[2].item() / len(leaders)
     else:
         p50 = p50_local
     if rank == 0:
         value = tokens / elapsed
         st_ = eng.stats()
+        par = f"dp{dp}" if a.tp == 1 else (f"tp{a.tp}" if dp == 1 else f"dp{dp}xtp{a.tp}")
         print(json.dumps({
             "metric": "output_tokens_per_sec",
             "value": round(value, 2),
@@ -138,17 +158,22 @@ def main():
             "dtype": "bf16",
             "data": "synthetic (random-token prompts, random-init weights)",
             "ttft_p50_ms": round(1000 * p50, 2) if p50 == p50 else None,
-            "config": {"model": a.model, "global_batch": a.concurrency * world,
+            "config": {"model": a.model, "global_batch": a.concurrency * dp,
                        "seq_len": a.prompt_len + a.output_len, "prompt_len": a.prompt_len,
-                       "output_len": a.output_len, "parallelism": f"dp{world}",
-                       "concurrency_per_gpu": a.concurrency},
+                       "output_len": a.output_len, "parallelism": par,
+                       "concurrency_per_replica": a.concurrency},
             "detail": {"preemptions": st_["preemptions"], "kv_blocks": st_["kv_blocks_total"],
-                       "decode_steps_total": st_["decode_steps"], "steps_total": st_["steps"]},
+                       "decode_steps_total": st_["decode_steps"], "steps_total": st_["steps"],
+                       **({"host_ms_per_step": {k: round(1000 * v / a.steps, 4)
+                                                for k, v in eng.step_timing().items()}}
+                          if eng._timing is not None else {})},
         }), flush=True)
+    eng.stop_followers()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -136,6 +136,7 @@ class LLMEngine:
         self.slot_seed = np.zeros(ns, np.uint64)
         self.slot_ngen = np.zeros(ns, np.int64)  # tokens generated by the slot's owner (sampling counter)
         self._deferred = None  # (plan, toks, lps, counts, fin_map) awaiting detokenisation
+        self._timing = None
         self._seq_counter = itertools.count(1)
         self._lock = threading.Lock()
         self._pending_aborts: List[str] = []
@@ -266,7 +267,22 @@ class LLMEngine:
         return SamplingRows(temps, self.slot_topp[slots], self.slot_topk[slots], seeds)
 
     def step(self) -> List[RequestOutput]:
+        if self._timing is None:
+            return self._step()
+        t0 = time.perf_counter()
+        out = self._step()
+        self._timing["step"] += time.perf_counter() - t0
+        return out
+
+    def _tick(self, phase: str, t0: float) -> float:
+        t1 = time.perf_counter()
+        if self._timing is not None:
+            self._timing[phase] += t1 - t0
+        return t1
+
+    def _step(self) -> List[RequestOutput]:
         outs: List[RequestOutput] = []
+        t = time.perf_counter()
         with self._lock:
             for rid in self._pending_aborts:
                 outs.append(RequestOutput(rid, [], "", True, "abort"))
@@ -275,6 +291,7 @@ class LLMEngine:
                 outs += self._flush_deferred()  # the draft needs every request's tokens
                 self.spec.propose()
             plan = self.sched.schedule()
+        t = self._tick("schedule", t)
         st = get_state()
         if st.tp_size > 1:
             comm.tp_broadcast_object(("plan", plan), src=0)
@@ -283,13 +300,17 @@ class LLMEngine:
         if self.is_driver:
             self._bind_slots(plan)
         samp = self._sampling_rows(plan)
+        t = self._tick("prepare", t)
         counts = None
         if self.spec is not None and self.is_driver and plan["num_seqs"] > plan["num_decodes"]:
             toks, lps, hidden, counts = self.spec.verify_execute(plan, samp)
         else:
             handle = self.runner.launch(plan, samp)
+            t = self._tick("launch", t)
             outs += self._flush_deferred()  # previous step's outputs, while this one runs
+            t = self._tick("emit_overlapped", t)
             toks, lps, hidden = self.runner.wait(handle)
+            t = self._tick("wait_gpu", t)
         self.step_count += 1
         self.stats_counters["steps"] += 1
         if plan["num_decodes"] == plan["num_seqs"]:
@@ -301,6 +322,7 @@ class LLMEngine:
         if counts is None:
             counts = np.ones(n_sample, np.int32)
         fin_map = self._apply(plan, toks, counts)
+        t = self._tick("apply", t)
         if not self.is_driver:
             return outs
         first_tokens = bool(plan["is_prefill"][plan["sample_seq_index"]].any()) if n_sample else False
@@ -308,7 +330,17 @@ class LLMEngine:
             self._deferred = (plan, toks, lps, counts, fin_map)
             return outs
         with self._lock:
-            return outs + self._emit(plan, toks, lps, counts, fin_map)
+            outs += self._emit(plan, toks, lps, counts, fin_map)
+        self._tick("emit_blocking", t)
+        return outs
+
+    def enable_step_timing(self, on: bool = True) -> None:
+        """Accumulate host time per step phase (bench / profiling)."""
+        import collections
+        self._timing = collections.defaultdict(float) if on else None
+
+    def step_timing(self) -> dict:
+        return dict(self._timing or {})
 
     def _flush_deferred(self) -> List[RequestOutput]:
         d, self._deferred = self._deferred, None
