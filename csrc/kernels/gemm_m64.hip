@@ -207,6 +207,131 @@ __global__ void __launch_bounds__(256, 2) gemm_m64_kernel(const uint16_t* __rest
   }
 }
 
+// ---------------------------------------------------------------------------
+// Grouped (MoE) form. W is [E, N, K]; x rows come through the block-64 padded
+// expert-sorted layout of moe_align (rows[p] = source row of padded row p, -1 =
+// pad; offs[E + 1] = padded segment offsets; rows == nullptr: x is already in
+// that layout). One workgroup per (column tile, k-split, expert) loops over the
+// expert's 64-row tiles, so each column tile of an expert's weights leaves HBM
+// once per step and later row tiles (prefill) re-read it from L2 / MALL.
+// Output rows are padded positions: out / part have P = offs[E] rows.
+template <int NW>
+__global__ void __launch_bounds__(256, 2) gemm_m64_grouped_kernel(const uint16_t* __restrict__ x,
+                                                                  const int32_t* __restrict__ rows,
+                                                                  const int32_t* __restrict__ offs, int K,
+                                                                  const uint16_t* __restrict__ w, int N, int P,
+                                                                  float* __restrict__ part,
+                                                                  uint16_t* __restrict__ out, int mode) {
+  constexpr int MT = 4, XP = 8;
+  __shared__ uint4 xs[2][64 * 32];
+  const int e = blockIdx.z;
+  const int p0 = offs[e], p1 = offs[e + 1];
+  if (p1 <= p0) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int S = gridDim.y, s = blockIdx.y;
+  const int kws = K / S;
+  const int k0 = s * kws;
+  const int nchunks = kws / GM_KC;
+  const int nbase = blockIdx.x * (64 * NW) + wid * (16 * NW);
+  const uint16_t* we = w + static_cast<int64_t>(e) * N * K;
+  const uint16_t* wp[NW];
+#pragma unroll
+  for (int nt = 0; nt < NW; ++nt) wp[nt] = we + static_cast<int64_t>(nbase + 16 * nt + li) * K + k0 + 8 * g;
+
+  for (int rt = p0; rt < p1; rt += 64) {
+    if (rt != p0) __syncthreads();  // the previous tile's last chunk may still be read from xs
+    const int first = rows ? rows[rt] : rt;  // a tile is never all padding
+    const uint16_t* xp[XP];
+    int xi[XP];
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+      const int q = tid + 256 * i, r = q >> 5, c = q & 31;
+      int src = rows ? rows[rt + r] : rt + r;
+      if (src < 0) src = first;
+      xp[i] = x + static_cast<int64_t>(src) * K + k0 + 8 * c;
+      xi[i] = gm_slot(r, c);
+    }
+    uint4 X[XP];
+    GmW<NW> A;
+#pragma unroll
+    for (int i = 0; i < XP; ++i) X[i] = ld16(xp[i]);
+#pragma unroll
+    for (int t = 0; t < GM_STEPS; ++t)
+#pragma unroll
+      for (int nt = 0; nt < NW; ++nt) A.w[t][nt] = ld16(wp[nt] + 32 * t);
+#pragma unroll
+    for (int i = 0; i < XP; ++i) xs[0][xi[i]] = X[i];
+    __syncthreads();
+    f32x4_t acc[NW][MT];
+#pragma unroll
+    for (int nt = 0; nt < NW; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    int c = 0;
+    for (; c + 1 < nchunks; ++c)
+      gm_chunk<MT, NW, true, true, false>(A, X, acc, xs[c & 1], xs[(c + 1) & 1], wp, xp, xi, (c + 1) * GM_KC,
+                                          (c + 1) * GM_KC, li, g);
+    gm_chunk<MT, NW, false, false, false>(A, X, acc, xs[c & 1], xs[(c + 1) & 1], wp, xp, xi, 0, 0, li, g);
+
+    if (mode == GM_PARTIAL) {
+      float* pp = part + static_cast<int64_t>(s) * P * N;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = rt + 16 * mt + li;
+#pragma unroll
+        for (int nt = 0; nt < NW; ++nt)
+          *reinterpret_cast<float4*>(pp + static_cast<int64_t>(m) * N + nbase + 16 * nt + 4 * g) =
+              make_float4(acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]);
+      }
+    } else if (mode == GM_BF16) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = rt + 16 * mt + li;
+#pragma unroll
+        for (int nt = 0; nt < NW; ++nt) {
+          uint2 v;
+          v.x = pack2(acc[nt][mt][0], acc[nt][mt][1]);
+          v.y = pack2(acc[nt][mt][2], acc[nt][mt][3]);
+          *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * N + nbase + 16 * nt + 4 * g) = v;
+        }
+      }
+    } else if (NW == 2) {  // GM_SILU on the block-16 interleaved gate|up rows of the expert
+      const int F = N / 2, f0 = nbase / 2 + 4 * g;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = rt + 16 * mt + li;
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gt = acc[0][mt][r];
+          o[r] = gt / (1.f + __expf(-gt)) * acc[NW - 1][mt][r];
+        }
+        uint2 v;
+        v.x = pack2(o[0], o[1]);
+        v.y = pack2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * F + f0) = v;
+      }
+    }
+  }
+}
+
+int moe_gemm_m64(const uint16_t* x, const int32_t* rows, const int32_t* offs, int E, int K, const uint16_t* w, int N,
+                 int P, float* part, uint16_t* out, int S, int mode, int nw, hipStream_t st) {
+  if (E < 1 || P < 0 || P % 64 || S < 1 || (nw != 1 && nw != 2)) return 1;
+  if (K % (S * GM_KC) || N % (64 * nw)) return 1;
+  if (mode == GM_SILU && (nw != 2 || S != 1)) return 1;
+  if (mode == GM_PARTIAL && part == nullptr) return 1;
+  if (mode != GM_PARTIAL && out == nullptr) return 1;
+  if (P == 0) return 0;
+  const dim3 grid(N / (64 * nw), S, E);
+  if (nw == 1)
+    hipLaunchKernelGGL(gemm_m64_grouped_kernel<1>, grid, dim3(256), 0, st, x, rows, offs, K, w, N, P, part, out, mode);
+  else
+    hipLaunchKernelGGL(gemm_m64_grouped_kernel<2>, grid, dim3(256), 0, st, x, rows, offs, K, w, N, P, part, out, mode);
+  return 0;
+}
+
 template <int MT, int NW>
 static void launch_gm(int tiles, int S, const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part,
                       uint16_t* out, int mode, int variant, hipStream_t st) {

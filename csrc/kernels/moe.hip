@@ -5,18 +5,14 @@
 //                      (== softmax-then-renormalise, Mixtral semantics) or the
 //                      plain softmax probabilities when renorm == 0.
 //   moe_align        : one workgroup builds the expert-sorted, block_m-padded
-//                      row layout: sorted_rows[p] = token of padded row p (-1 =
-//                      pad), expert_offsets[E+1], tile_expert[tile], dest[t*k+j]
-//                      = padded row of (token t, choice j).
-//   moe_grouped_gemm : out[p, :] = x[rows[p], :] @ W[e(p)]^T for every expert
-//                      at once (W stored [E, N, K], the nn.Linear layout). A
-//                      64x64 tile per workgroup: the gathered 64-row x slab is
-//                      staged in LDS (XOR-swizzled, shared by the 4 waves), each
-//                      wave streams its own 16 weight rows straight into MFMA
-//                      B fragments (weights are read once: GEMV-regime rule),
-//                      v_mfma_f32_16x16x32_bf16, next-chunk loads issued before
-//                      the current chunk's MFMAs.
-//   moe_combine      : out[t] = sum_j w[t, j] * y[dest[t*k + j]].
+//                      row layout for this rank's experts: sorted_rows[p] =
+//                      token of padded row p (-1 = pad), expert_offsets[E+1],
+//                      dest[t*k+j] = padded row of (token t, choice j) or -1
+//                      when the expert lives on another EP rank.
+//   (the grouped expert GEMMs are gemm_m64_grouped in gemm_m64.hip: W [E, N, K]
+//    streamed once per step per column tile, fused SiLU-gate on w13)
+//   moe_combine      : out[t] = sum_j w[t, j] * y[dest[t*k + j]], y bf16 or
+//                      fp32 split-K partials of the w2 GEMM.
 #include "common.h"
 
 namespace xgk {
@@ -72,17 +68,23 @@ void moe_topk_softmax(const void* logits, int is_f32, int T, int E, int k, int r
 }
 
 // ---------------------------------------------------------------- layout
-// sorted_rows must hold T*k + E*(block_m-1) entries; tile_expert the same / block_m.
+// Expert-parallel aware: a pair (t, j) whose global expert ids[t*k+j] is outside
+// [expert_offset, expert_offset + E) belongs to another rank: dest = -1, not placed.
+// sorted_rows holds cap = T*k + E*(block_m-1) rounded up to block_m entries (-1 = pad);
+// offsets[E+1] are block_m-padded segment starts; dest[t*k+j] = padded row of the pair.
 __global__ void __launch_bounds__(1024) align_kernel(const int32_t* __restrict__ ids, int n_pairs, int k, int E,
-                                                     int block_m, int32_t* __restrict__ sorted_rows,
-                                                     int32_t* __restrict__ offsets, int32_t* __restrict__ tile_expert,
-                                                     int32_t* __restrict__ dest, int cap) {
+                                                     int expert_offset, int block_m, int32_t* __restrict__ sorted_rows,
+                                                     int32_t* __restrict__ offsets, int32_t* __restrict__ dest,
+                                                     int cap) {
   __shared__ int cnt[256];
   __shared__ int off[257];
   __shared__ int fill[256];
   for (int e = threadIdx.x; e < E; e += blockDim.x) { cnt[e] = 0; fill[e] = 0; }
   __syncthreads();
-  for (int i = threadIdx.x; i < n_pairs; i += blockDim.x) atomicAdd(&cnt[ids[i]], 1);
+  for (int i = threadIdx.x; i < n_pairs; i += blockDim.x) {
+    const int e = ids[i] - expert_offset;
+    if (e >= 0 && e < E) atomicAdd(&cnt[e], 1);
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     off[0] = 0;
@@ -90,140 +92,60 @@ __global__ void __launch_bounds__(1024) align_kernel(const int32_t* __restrict__
   }
   __syncthreads();
   for (int e = threadIdx.x; e <= E; e += blockDim.x) offsets[e] = off[e];
-  const int total = off[E];
   for (int p = threadIdx.x; p < cap; p += blockDim.x) sorted_rows[p] = -1;
-  const int ntile_cap = cap / block_m;
-  for (int tl = threadIdx.x; tl < ntile_cap; tl += blockDim.x) {
-    const int p = tl * block_m;
-    int e = -1;
-    if (p < total)
-      for (int x = 0; x < E; ++x)
-        if (p >= off[x] && p < off[x + 1]) { e = x; break; }
-    tile_expert[tl] = e;
-  }
   __syncthreads();
   for (int i = threadIdx.x; i < n_pairs; i += blockDim.x) {
-    const int e = ids[i];
+    const int e = ids[i] - expert_offset;
+    if (e < 0 || e >= E) {
+      dest[i] = -1;
+      continue;
+    }
     const int pos = off[e] + atomicAdd(&fill[e], 1);
     sorted_rows[pos] = i / k;
     dest[i] = pos;
   }
 }
 
-void moe_align(const int32_t* ids, int T, int k, int E, int block_m, int32_t* sorted_rows, int32_t* offsets,
-               int32_t* tile_expert, int32_t* dest, hipStream_t st) {
-  const int cap = T * k + E * (block_m - 1);
-  hipLaunchKernelGGL(align_kernel, dim3(1), dim3(1024), 0, st, ids, T * k, k, E, block_m, sorted_rows, offsets,
-                     tile_expert, dest, cap);
-}
-
-// ---------------------------------------------------------------- grouped GEMM
-// tile 64 rows x 64 cols, K chunk 64. x rows gathered through rows[] when gather.
-constexpr int GG_BM = 64, GG_BN = 64, GG_BK = 64;
-
-__global__ void __launch_bounds__(256) grouped_gemm_kernel(const uint16_t* __restrict__ x,
-                                                           const int32_t* __restrict__ rows,
-                                                           const uint16_t* __restrict__ w, uint16_t* __restrict__ out,
-                                                           const int32_t* __restrict__ tile_expert, int N, int K,
-                                                           int gather) {
-  const int tile = blockIdx.x;
-  const int e = tile_expert[tile];
-  if (e < 0) return;
-  const int n0 = blockIdx.y * GG_BN;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  __shared__ __attribute__((aligned(16))) uint16_t xs[GG_BM * GG_BK];  // 8 KiB, [row][8 chunks] swizzled
-
-  // staging role: 256 threads x 2 chunks of 16 B = 64 rows x 64 k
-  int src_row[2];
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int ci = threadIdx.x + it * 256;
-    const int r = ci >> 3;
-    const int p = tile * GG_BM + r;
-    src_row[it] = gather ? rows[p] : p;
-  }
-  const uint16_t* wrow = w + (static_cast<int64_t>(e) * N + n0 + wid * 16 + li) * K;
-
-  uint4 xr[2], wr[2];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int ci = threadIdx.x + it * 256;
-      const int ch = ci & 7;
-      xr[it] = src_row[it] >= 0 ? ld16(x + static_cast<int64_t>(src_row[it]) * K + k0 + ch * 8) : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) wr[ks] = ld16(wrow + k0 + ks * 32 + 8 * g);
-  };
-  auto lstore = [&]() {
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int ci = threadIdx.x + it * 256;
-      const int r = ci >> 3, ch = ci & 7;
-      st16(xs + r * GG_BK + ((ch ^ (r & 7)) * 8), xr[it]);
-    }
-  };
-
-  f32x4_t acc[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  gload(0);
-  for (int k0 = 0; k0 < K; k0 += GG_BK) {
-    __syncthreads();
-    lstore();
-    const uint4 wcur0 = wr[0], wcur1 = wr[1];
-    __syncthreads();
-    if (k0 + GG_BK < K) gload(k0 + GG_BK);
-    // out^T tile for this wave: C[n = 16wid + li][m] ... we compute C = X . W^T with
-    // A = X rows (from LDS), B = W^T (lane holds W[n = li][k = 8g + j])
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8_t bfrag = as_frag(ks == 0 ? wcur0 : wcur1);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const int r = mt * 16 + li;
-        const int ch = ks * 4 + g;
-        const uint4 a = *reinterpret_cast<const uint4*>(xs + r * GG_BK + ((ch ^ (r & 7)) * 8));
-        acc[mt] = mfma16x16x32(as_frag(a), bfrag, acc[mt]);
-      }
-    }
-  }
-  // C layout: acc[mt][r] = out[row = 16mt + 4g + r][col = 16wid + li]
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int p = tile * GG_BM + mt * 16 + 4 * g + r;
-      out[static_cast<int64_t>(p) * N + n0 + wid * 16 + li] = f2bf(acc[mt][r]);
-    }
-}
-
-void moe_grouped_gemm(const uint16_t* x, const int32_t* rows, const uint16_t* w, uint16_t* out, const int32_t* offs,
-                      const int32_t* tile_expert, int max_tiles, int N, int K, int gather, int x_rows,
-                      int num_experts, hipStream_t st) {
-  (void)offs;
-  (void)x_rows;
-  (void)num_experts;
-  if (max_tiles <= 0) return;
-  hipLaunchKernelGGL(grouped_gemm_kernel, dim3(max_tiles, N / GG_BN), dim3(256), 0, st, x, rows, w, out, tile_expert,
-                     N, K, gather);
+void moe_align(const int32_t* ids, int T, int k, int E, int expert_offset, int block_m, int32_t* sorted_rows,
+               int32_t* offsets, int32_t* dest, hipStream_t st) {
+  int cap = T * k + E * (block_m - 1);
+  cap = (cap + block_m - 1) / block_m * block_m;
+  hipLaunchKernelGGL(align_kernel, dim3(1), dim3(1024), 0, st, ids, T * k, k, E, expert_offset, block_m, sorted_rows,
+                     offsets, dest, cap);
 }
 
 // ---------------------------------------------------------------- combine
-__global__ void __launch_bounds__(256) combine_kernel(const uint16_t* __restrict__ y, const int32_t* __restrict__ dest,
-                                                      const float* __restrict__ w, uint16_t* __restrict__ out, int k,
-                                                      int H) {
+// out[t] = sum_j w[t, j] * sum_s part[s][dest[t*k + j]]   (dest < 0: another rank's expert)
+// y is either bf16 [P, H] (S == 0) or fp32 split-K partials [S, P, H].
+template <int SP>
+__global__ void __launch_bounds__(256) combine_kernel(const void* __restrict__ y, int S, int P,
+                                                      const int32_t* __restrict__ dest, const float* __restrict__ w,
+                                                      uint16_t* __restrict__ out, int k, int H) {
   const int t = blockIdx.x;
   for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int j = 0; j < k; ++j) {
       const int p = dest[t * k + j];
+      if (p < 0) continue;
       const float wt = w[t * k + j];
-      if (wt == 0.f) continue;  // dropped (non-local) choice: its row may be unwritten
       float f[8];
-      unpack8(ld16(y + static_cast<int64_t>(p) * H + c * 8), f);
+      if constexpr (SP == 0) {
+        unpack8(ld16(static_cast<const uint16_t*>(y) + static_cast<int64_t>(p) * H + c * 8), f);
+      } else {
+        float4 a[SP], b[SP];
+#pragma unroll
+        for (int s = 0; s < SP; ++s) {
+          const float* q = static_cast<const float*>(y) + (static_cast<int64_t>(s) * P + p) * H + c * 8;
+          a[s] = *reinterpret_cast<const float4*>(q);
+          b[s] = *reinterpret_cast<const float4*>(q + 4);
+        }
+        for (int i = 0; i < 8; ++i) f[i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < SP; ++s) {
+          f[0] += a[s].x; f[1] += a[s].y; f[2] += a[s].z; f[3] += a[s].w;
+          f[4] += b[s].x; f[5] += b[s].y; f[6] += b[s].z; f[7] += b[s].w;
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] += wt * f[i];
     }
@@ -231,15 +153,19 @@ __global__ void __launch_bounds__(256) combine_kernel(const uint16_t* __restrict
   }
 }
 
-void moe_combine(const uint16_t* y, const int32_t* dest, const float* w, uint16_t* out, int T, int k, int H,
-                 hipStream_t st) {
-  if (T <= 0) return;
-  hipLaunchKernelGGL(combine_kernel, dim3(T), dim3(256), 0, st, y, dest, w, out, k, H);
+int moe_combine(const void* y, int S, int P, const int32_t* dest, const float* w, uint16_t* out, int T, int k, int H,
+                hipStream_t st) {
+  if (T <= 0) return 0;
+  if (H % 8) return 1;
+  const dim3 g(T), b(256);
+  switch (S) {
+    case 0: hipLaunchKernelGGL(combine_kernel<0>, g, b, 0, st, y, S, P, dest, w, out, k, H); return 0;
+    case 1: hipLaunchKernelGGL(combine_kernel<1>, g, b, 0, st, y, S, P, dest, w, out, k, H); return 0;
+    case 2: hipLaunchKernelGGL(combine_kernel<2>, g, b, 0, st, y, S, P, dest, w, out, k, H); return 0;
+    case 4: hipLaunchKernelGGL(combine_kernel<4>, g, b, 0, st, y, S, P, dest, w, out, k, H); return 0;
+    default: return 1;
+  }
 }
 
-void silu_and_mul(const uint16_t* in, uint16_t* out, int T, int F, int interleave16, hipStream_t st);
-void moe_silu_mul_gather(const uint16_t* in, uint16_t* out, int rows, int F, hipStream_t st) {
-  silu_and_mul(in, out, rows, F, 0, st);
-}
 
 }  // namespace xgk

@@ -37,11 +37,10 @@ void sample_tokens(const void*, int, int64_t, int, int, const float*, const floa
                    uint64_t, int32_t*, float*, hipStream_t);
 void segment_sum(const uint16_t*, int, const int32_t*, const int32_t*, float*, int, hipStream_t);
 void moe_topk_softmax(const void*, int, int, int, int, int, float*, int32_t*, hipStream_t);
-void moe_align(const int32_t*, int, int, int, int, int32_t*, int32_t*, int32_t*, int32_t*, hipStream_t);
-void moe_grouped_gemm(const uint16_t*, const int32_t*, const uint16_t*, uint16_t*, const int32_t*, const int32_t*,
-                      int, int, int, int, int, int, hipStream_t);
-void moe_silu_mul_gather(const uint16_t*, uint16_t*, int, int, hipStream_t);
-void moe_combine(const uint16_t*, const int32_t*, const float*, uint16_t*, int, int, int, hipStream_t);
+void moe_align(const int32_t*, int, int, int, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
+int moe_combine(const void*, int, int, const int32_t*, const float*, uint16_t*, int, int, int, hipStream_t);
+int moe_gemm_m64(const uint16_t*, const int32_t*, const int32_t*, int, int, const uint16_t*, int, int, float*,
+                 uint16_t*, int, int, int, hipStream_t);
 int custom_allreduce(const void*, void*, int64_t, int64_t, const uintptr_t*, const uintptr_t*, int, int, uint32_t*,
                      hipStream_t);
 int car_max_blocks();
@@ -174,30 +173,24 @@ PYBIND11_MODULE(_kernels, m) {
     xgk::moe_topk_softmax(P<const void>(logits), is_f32, T, E, k, renorm, P<float>(w), P<int32_t>(ids), S(st));
     check(0, "moe_topk_softmax");
   });
-  m.def("moe_align", [](uintptr_t ids, int T, int k, int E, int block_m, uintptr_t sorted_rows,
-                        uintptr_t expert_offsets, uintptr_t tile_expert, uintptr_t dest, uintptr_t st) {
-    xgk::moe_align(P<const int32_t>(ids), T, k, E, block_m, P<int32_t>(sorted_rows), P<int32_t>(expert_offsets),
-                   P<int32_t>(tile_expert), P<int32_t>(dest), S(st));
+  m.def("moe_align", [](uintptr_t ids, int T, int k, int E, int expert_offset, int block_m, uintptr_t sorted_rows,
+                        uintptr_t expert_offsets, uintptr_t dest, uintptr_t st) {
+    if (E < 1 || E > 256) throw std::invalid_argument("moe_align: 1 <= E <= 256");
+    xgk::moe_align(P<const int32_t>(ids), T, k, E, expert_offset, block_m, P<int32_t>(sorted_rows),
+                   P<int32_t>(expert_offsets), P<int32_t>(dest), S(st));
     check(0, "moe_align");
   });
-  m.def("moe_grouped_gemm", [](uintptr_t x, uintptr_t rows, uintptr_t w, uintptr_t out, uintptr_t offs,
-                               uintptr_t tile_expert, int max_tiles, int N, int K, int gather, int x_rows,
-                               int num_experts, uintptr_t st) {
-    if (K % 64 || N % 64) throw std::invalid_argument("moe_grouped_gemm: N, K must be multiples of 64");
-    xgk::moe_grouped_gemm(P<const uint16_t>(x), P<const int32_t>(rows), P<const uint16_t>(w), P<uint16_t>(out),
-                          P<const int32_t>(offs), P<const int32_t>(tile_expert), max_tiles, N, K, gather, x_rows,
-                          num_experts, S(st));
-    check(0, "moe_grouped_gemm");
+  m.def("moe_gemm_m64", [](uintptr_t x, uintptr_t rows, uintptr_t offs, int E, int K, uintptr_t w, int N, int P_,
+                           uintptr_t part, uintptr_t out, int splits, int mode, int nw, uintptr_t st) {
+    check(xgk::moe_gemm_m64(P<const uint16_t>(x), P<const int32_t>(rows), P<const int32_t>(offs), E, K,
+                            P<const uint16_t>(w), N, P_, P<float>(part), P<uint16_t>(out), splits, mode, nw, S(st)),
+          "moe_gemm_m64");
   });
-  m.def("moe_silu_mul", [](uintptr_t in, uintptr_t out, int rows, int F, uintptr_t st) {
-    xgk::moe_silu_mul_gather(P<const uint16_t>(in), P<uint16_t>(out), rows, F, S(st));
-    check(0, "moe_silu_mul");
-  });
-  m.def("moe_combine", [](uintptr_t y, uintptr_t dest, uintptr_t w, uintptr_t out, int T, int k, int H,
-                          uintptr_t st) {
-    xgk::moe_combine(P<const uint16_t>(y), P<const int32_t>(dest), P<const float>(w), P<uint16_t>(out), T, k, H,
-                     S(st));
-    check(0, "moe_combine");
+  m.def("moe_combine", [](uintptr_t y, int splits, int P_, uintptr_t dest, uintptr_t w, uintptr_t out, int T, int k,
+                          int H, uintptr_t st) {
+    check(xgk::moe_combine(P<const void>(y), splits, P_, P<const int32_t>(dest), P<const float>(w), P<uint16_t>(out),
+                           T, k, H, S(st)),
+          "moe_combine");
   });
   m.def("device_synchronize", []() {
     hipError_t e = hipDeviceSynchronize();

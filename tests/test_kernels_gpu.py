@@ -215,10 +215,17 @@ def test_segment_sum():
     torch.testing.assert_close(out, ref, atol=1e-2, rtol=1e-3)
 
 
-@pytest.mark.parametrize("T,E,k,H,F", [(1, 8, 2, 512, 256), (37, 8, 2, 1024, 512), (200, 8, 2, 4096, 1792)])
+def _w13(E, F, H):
+    """per-expert block-16 interleaved gate|up rows (the serving layout)."""
+    from xgserve.ops.linear import interleave_gate_up
+    return torch.stack([interleave_gate_up(rnd(F, H, scale=0.05), rnd(F, H, scale=0.05)) for _ in range(E)])
+
+
+@pytest.mark.parametrize("T,E,k,H,F", [(1, 8, 2, 512, 256), (2, 8, 2, 1024, 512), (37, 8, 2, 1024, 512),
+                                       (64, 8, 2, 4096, 1792), (200, 8, 2, 4096, 1792)])
 def test_fused_moe(T, E, k, H, F):
     x = rnd(T, H)
-    w13 = rnd(E, 2 * F, H, scale=0.05)
+    w13 = _w13(E, F, H)
     w2 = rnd(E, H, F, scale=0.05)
     logits = rnd(T, E, dtype=torch.float32)
     w, ids = ops.moe_topk_softmax(logits, k)
@@ -234,7 +241,7 @@ def test_fused_moe(T, E, k, H, F):
 def test_fused_moe_expert_parallel_shard():
     T, E, k, H, F = 50, 8, 2, 512, 256
     x = rnd(T, H)
-    w13 = rnd(E, 2 * F, H, scale=0.05)
+    w13 = _w13(E, F, H)
     w2 = rnd(E, H, F, scale=0.05)
     w, ids = ops.moe_topk_softmax(rnd(T, E, dtype=torch.float32), k)
     full = ops.moe_forward_ref(x.cpu(), w13.cpu(), w2.cpu(), w.cpu(), ids.cpu()).float()

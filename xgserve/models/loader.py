@@ -130,7 +130,7 @@ def _load_llama(m, r: _Reader):
             for el in range(L.E_local):
                 e = L.expert_offset + el
                 eb = b + f"block_sparse_moe.experts.{e}."
-                L.w13.data[el].copy_(torch.cat([r.get(eb + "w1.weight"), r.get(eb + "w3.weight")], 0).to(L.w13.dtype))
+                L.w13.data[el].copy_(interleave_gate_up(r.get(eb + "w1.weight"), r.get(eb + "w3.weight")).to(L.w13.dtype))
                 L.w2.data[el].copy_(r.get(eb + "w2.weight").to(L.w2.dtype))
         else:
             Fl = cfg.intermediate_size // tp
@@ -208,8 +208,7 @@ def save_checkpoint(model, path: str) -> None:
                 t[b + "block_sparse_moe.gate.weight"] = L.router
                 for e in range(cfg.num_experts):
                     eb = b + f"block_sparse_moe.experts.{e}."
-                    t[eb + "w1.weight"] = L.w13[e, :Fd]
-                    t[eb + "w3.weight"] = L.w13[e, Fd:]
+                    t[eb + "w1.weight"], t[eb + "w3.weight"] = deinterleave_gate_up(L.w13[e])
                     t[eb + "w2.weight"] = L.w2[e]
             else:
                 Fd = cfg.intermediate_size

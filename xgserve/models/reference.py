@@ -75,8 +75,9 @@ def reference_logits(model, tokens) -> torch.Tensor:
             for t in range(T):
                 for j in range(cfg.experts_per_token):
                     ei = int(e[t, j])
-                    g = h[t] @ L.w13[ei].float().t()
-                    out[t] += w[t, j] * ((F.silu(g[:Fd]) * g[Fd:]) @ L.w2[ei].float().t())
+                    gw, uw = deinterleave_gate_up(L.w13[ei])  # block-16 interleaved per expert
+                    a = F.silu(h[t] @ gw.float().t()) * (h[t] @ uw.float().t())
+                    out[t] += w[t, j] * (a @ L.w2[ei].float().t())
             x = x + out
         else:
             gw, uw = deinterleave_gate_up(L.gate_up)  # stored block-16 interleaved

@@ -28,46 +28,28 @@ def moe_topk_softmax(router_logits: torch.Tensor, k: int, renorm: bool = True) -
     return w, ids
 
 
-def moe_align(ids: torch.Tensor, num_experts: int, block_m: int = BLOCK_M):
-    """-> (sorted_rows [cap], expert_offsets [E+1], tile_expert [cap/block_m], dest [T*k])"""
+def moe_align(ids: torch.Tensor, num_experts: int, expert_offset: int = 0, block_m: int = BLOCK_M):
+    """Expert-sorted, block_m-padded layout of this rank's experts
+    [expert_offset, expert_offset + num_experts). -> (sorted_rows [cap] (-1 = pad),
+    expert_offsets [E+1], dest [T*k] (padded row of each pair, -1 = another rank's expert))."""
     T, k = ids.shape
     cap = T * k + num_experts * (block_m - 1)
     cap = (cap + block_m - 1) // block_m * block_m
     dev = ids.device
     sorted_rows = torch.empty(cap, dtype=torch.int32, device=dev)
     offs = torch.empty(num_experts + 1, dtype=torch.int32, device=dev)
-    tile_expert = torch.empty(cap // block_m, dtype=torch.int32, device=dev)
     dest = torch.empty(T * k, dtype=torch.int32, device=dev)
-    kernels().moe_align(ids.data_ptr(), T, k, num_experts, block_m, sorted_rows.data_ptr(), offs.data_ptr(),
-                        tile_expert.data_ptr(), dest.data_ptr(), stream_ptr())
-    return sorted_rows, offs, tile_expert, dest
-
-
-def moe_grouped_gemm(x: torch.Tensor, rows: Optional[torch.Tensor], w: torch.Tensor, tile_expert: torch.Tensor,
-                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out[p] = x[rows[p]] @ w[e(p)]^T for padded expert-sorted rows p. w: [E, N, K]."""
-    E, N, K = w.shape
-    n_tiles = tile_expert.shape[0]
-    P = n_tiles * BLOCK_M
-    if out is None:
-        out = torch.zeros(P, N, dtype=x.dtype, device=x.device)
-    kernels().moe_grouped_gemm(x.data_ptr(), rows.data_ptr() if rows is not None else 0, w.data_ptr(),
-                               out.data_ptr(), 0, tile_expert.data_ptr(), n_tiles, N, K, 1 if rows is not None else 0,
-                               x.shape[0], E, stream_ptr())
-    return out
-
-
-def moe_combine(y: torch.Tensor, dest: torch.Tensor, weights: torch.Tensor, T: int, k: int) -> torch.Tensor:
-    H = y.shape[1]
-    out = torch.empty(T, H, dtype=y.dtype, device=y.device)
-    kernels().moe_combine(y.data_ptr(), dest.data_ptr(), weights.data_ptr(), out.data_ptr(), T, k, H, stream_ptr())
-    return out
+    kernels().moe_align(ids.contiguous().data_ptr(), T, k, num_experts, expert_offset, block_m, sorted_rows.data_ptr(),
+                        offs.data_ptr(), dest.data_ptr(), stream_ptr())
+    return sorted_rows, offs, dest
 
 
 def moe_forward_ref(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
                     topk_ids: torch.Tensor, expert_offset: int = 0) -> torch.Tensor:
-    """fp32 reference. w13: [E_local, 2F, H], w2: [E_local, H, F]; experts outside
+    """fp32 reference. w13: [E_local, 2F, H] block-16 interleaved gate|up rows
+    (ops.linear.interleave_gate_up per expert), w2: [E_local, H, F]; experts outside
     [expert_offset, expert_offset+E_local) contribute nothing."""
+    from .linear import deinterleave_gate_up
     T, H = x.shape
     E = w13.shape[0]
     out = torch.zeros(T, H, dtype=torch.float32, device=x.device)
@@ -79,9 +61,8 @@ def moe_forward_ref(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w
         if tok.numel() == 0:
             continue
         wt = (topk_w * mask).sum(-1)[tok]
-        h = xf[tok] @ w13[e].float().t()
-        F = h.shape[1] // 2
-        a = torch.nn.functional.silu(h[:, :F]) * h[:, F:]
+        g, u = deinterleave_gate_up(w13[e])
+        a = torch.nn.functional.silu(xf[tok] @ g.float().t()) * (xf[tok] @ u.float().t())
         a = a.to(x.dtype).float()
         y = a @ w2[e].float().t()
         out[tok] += wt[:, None] * y
@@ -91,20 +72,28 @@ def moe_forward_ref(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w
 def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
               topk_ids: torch.Tensor, expert_offset: int = 0) -> torch.Tensor:
     """Local-expert MoE FFN: sum_j w_j * FFN_{e_j}(x) over choices owned locally
-    (ids in [expert_offset, expert_offset + E_local)); others are skipped."""
+    (ids in [expert_offset, expert_offset + E_local)); others contribute nothing.
+
+    align (one tiny kernel) -> grouped gemm_m64 on w13 with the SiLU-gate fused
+    (x gathered through the sorted rows) -> grouped gemm_m64 on w2 (split-K
+    partials when few experts are active) -> combine (weights, partial sums)."""
     if not use_native(x):
         return moe_forward_ref(x, w13, w2, topk_w, topk_ids, expert_offset)
     T, k = topk_ids.shape
-    E = w13.shape[0]
-    local = topk_ids - expert_offset
-    in_range = (local >= 0) & (local < E)
-    # out-of-range choices are routed to a dummy expert id E (dropped tiles) with weight 0
-    ids = torch.where(in_range, local, torch.full_like(local, E)).to(torch.int32).contiguous()
-    wts = torch.where(in_range, topk_w, torch.zeros_like(topk_w)).float().contiguous()
-    sorted_rows, offs, tile_expert, dest = moe_align(ids, E + 1)
-    # tiles of the dummy expert are skipped by the GEMM (tile_expert == E -> mark -1)
-    tile_expert = torch.where(tile_expert >= E, torch.full_like(tile_expert, -1), tile_expert)
-    h = moe_grouped_gemm(x.contiguous(), sorted_rows, w13, tile_expert)
-    a = silu_and_mul(h)
-    y = moe_grouped_gemm(a, None, w2, tile_expert)
-    return moe_combine(y, dest, wts, T, k)
+    E, F2, H = w13.shape
+    F = F2 // 2
+    sorted_rows, offs, dest = moe_align(topk_ids, E, expert_offset)
+    P = sorted_rows.shape[0]
+    act = torch.empty(P, F, dtype=x.dtype, device=x.device)
+    kn = kernels()
+    kn.moe_gemm_m64(x.contiguous().data_ptr(), sorted_rows.data_ptr(), offs.data_ptr(), E, H, w13.data_ptr(), F2, P,
+                    0, act.data_ptr(), 1, 2, 2, stream_ptr())
+    # w2 has only H/64 column tiles per expert: split K while few experts are active
+    S = 2 if (T * k <= 8 and F % 512 == 0) else 1
+    part = torch.empty(S, P, H, dtype=torch.float32, device=x.device)
+    kn.moe_gemm_m64(act.data_ptr(), 0, offs.data_ptr(), E, F, w2.data_ptr(), H, P, part.data_ptr(), 0, S, 1, 1,
+                    stream_ptr())
+    out = torch.empty(T, H, dtype=x.dtype, device=x.device)
+    kn.moe_combine(part.data_ptr(), S, P, dest.data_ptr(), topk_w.float().contiguous().data_ptr(), out.data_ptr(), T,
+                   k, H, stream_ptr())
+    return out
