@@ -67,6 +67,83 @@ void moe_topk_softmax(const void* logits, int is_f32, int T, int E, int k, int r
                        ids);
 }
 
+// Router GEMV + softmax + top-k in one launch (replaces a tiny hipBLASLt GEMM and
+// the topk kernel on the decode path): one workgroup per token, each thread dots
+// 8-element chunks of the hidden row with all EM (>= E) router rows in fp32,
+// block reduction, then lane 0 selects the top k (softmax over all E, optionally
+// renormalised over the chosen k: Mixtral semantics).
+template <int EM>
+__global__ void __launch_bounds__(256) route_kernel(const uint16_t* __restrict__ h, const uint16_t* __restrict__ wr,
+                                                    int H, int E, int k, int renorm, float* __restrict__ w,
+                                                    int32_t* __restrict__ ids) {
+  __shared__ float red[4][EM];
+  const int t = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float acc[EM];
+#pragma unroll
+  for (int e = 0; e < EM; ++e) acc[e] = 0.f;
+  const uint16_t* hr = h + static_cast<int64_t>(t) * H;
+  for (int c = threadIdx.x; c < H / 8; c += 256) {
+    float x[8];
+    unpack8(ld16(hr + c * 8), x);
+#pragma unroll
+    for (int e = 0; e < EM; ++e) {
+      if (e >= E) break;
+      float r[8];
+      unpack8(ld16(wr + static_cast<int64_t>(e) * H + c * 8), r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[e] += x[i] * r[i];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EM; ++e) {
+    const float v = wave_sum(acc[e]);
+    if (lane == 0) red[wid][e] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  float v[EM];
+  float mx = -INFINITY;
+  for (int e = 0; e < E; ++e) {
+    v[e] = red[0][e] + red[1][e] + red[2][e] + red[3][e];
+    mx = fmaxf(mx, v[e]);
+  }
+  float den = 0.f;
+  for (int e = 0; e < E; ++e) den += __expf(v[e] - mx);
+  unsigned long long used = 0;
+  float sel[16];
+  int sid[16];
+  float ssum = 0.f;
+  for (int j = 0; j < k; ++j) {
+    int best = -1;
+    float bv = -INFINITY;
+    for (int e = 0; e < E; ++e)
+      if (!((used >> e) & 1ull) && (best < 0 || v[e] > bv)) { best = e; bv = v[e]; }
+    used |= 1ull << best;
+    sid[j] = best;
+    sel[j] = __expf(bv - mx) / den;
+    ssum += sel[j];
+  }
+  for (int j = 0; j < k; ++j) {
+    w[static_cast<int64_t>(t) * k + j] = renorm ? sel[j] / ssum : sel[j];
+    ids[static_cast<int64_t>(t) * k + j] = sid[j];
+  }
+}
+
+int moe_route(const uint16_t* h, const uint16_t* wr, int T, int H, int E, int k, int renorm, float* w, int32_t* ids,
+              hipStream_t st) {
+  if (T <= 0) return 0;
+  if (H % 8 || E < 1 || E > 64 || k < 1 || k > 16 || k > E) return 1;
+  const dim3 g(T), b(256);
+  if (E <= 8)
+    hipLaunchKernelGGL(route_kernel<8>, g, b, 0, st, h, wr, H, E, k, renorm, w, ids);
+  else if (E <= 16)
+    hipLaunchKernelGGL(route_kernel<16>, g, b, 0, st, h, wr, H, E, k, renorm, w, ids);
+  else
+    hipLaunchKernelGGL(route_kernel<64>, g, b, 0, st, h, wr, H, E, k, renorm, w, ids);
+  return 0;
+}
+
 // ---------------------------------------------------------------- layout
 // Expert-parallel aware: a pair (t, j) whose global expert ids[t*k+j] is outside
 // [expert_offset, expert_offset + E) belongs to another rank: dest = -1, not placed.

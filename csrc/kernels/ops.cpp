@@ -39,6 +39,7 @@ void segment_sum(const uint16_t*, int, const int32_t*, const int32_t*, float*, i
 void moe_topk_softmax(const void*, int, int, int, int, int, float*, int32_t*, hipStream_t);
 void moe_align(const int32_t*, int, int, int, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
 int moe_combine(const void*, int, int, const int32_t*, const float*, uint16_t*, int, int, int, hipStream_t);
+int moe_route(const uint16_t*, const uint16_t*, int, int, int, int, int, float*, int32_t*, hipStream_t);
 int moe_gemm_m64(const uint16_t*, const int32_t*, const int32_t*, int, int, const uint16_t*, int, int, float*,
                  uint16_t*, int, int, int, hipStream_t);
 int custom_allreduce(const void*, void*, int64_t, int64_t, const uintptr_t*, const uintptr_t*, int, int, uint32_t*,
@@ -185,6 +186,12 @@ PYBIND11_MODULE(_kernels, m) {
     check(xgk::moe_gemm_m64(P<const uint16_t>(x), P<const int32_t>(rows), P<const int32_t>(offs), E, K,
                             P<const uint16_t>(w), N, P_, P<float>(part), P<uint16_t>(out), splits, mode, nw, S(st)),
           "moe_gemm_m64");
+  });
+  m.def("moe_route", [](uintptr_t h, uintptr_t wr, int T, int H, int E, int k, int renorm, uintptr_t w, uintptr_t ids,
+                        uintptr_t st) {
+    check(xgk::moe_route(P<const uint16_t>(h), P<const uint16_t>(wr), T, H, E, k, renorm, P<float>(w),
+                         P<int32_t>(ids), S(st)),
+          "moe_route");
   });
   m.def("moe_combine", [](uintptr_t y, int splits, int P_, uintptr_t dest, uintptr_t w, uintptr_t out, int T, int k,
                           int H, uintptr_t st) {

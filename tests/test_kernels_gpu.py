@@ -248,3 +248,14 @@ def test_fused_moe_expert_parallel_shard():
     half0 = ops.fused_moe(x, w13[:4].contiguous(), w2[:4].contiguous(), w, ids, expert_offset=0).cpu().float()
     half1 = ops.fused_moe(x, w13[4:].contiguous(), w2[4:].contiguous(), w, ids, expert_offset=4).cpu().float()
     torch.testing.assert_close(half0 + half1, full, atol=4e-2, rtol=4e-2)
+
+
+@pytest.mark.parametrize("T,E,k,H", [(1, 8, 2, 4096), (64, 8, 2, 4096), (5, 16, 4, 512), (3, 64, 6, 1024)])
+def test_moe_route_matches_fp32(T, E, k, H):
+    h = rnd(T, H)
+    router = rnd(E, H, scale=0.05)
+    w, ids = ops.moe_route(h, router, k)
+    logits = h.float() @ router.float().t()
+    rw, rids = ops.moe_topk_softmax(logits.cpu(), k)
+    assert torch.equal(ids.cpu().long().sort(-1).values, rids.long().sort(-1).values)
+    torch.testing.assert_close(w.cpu().sort(-1).values, rw.sort(-1).values, atol=1e-4, rtol=1e-4)

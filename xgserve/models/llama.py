@@ -97,8 +97,7 @@ class LlamaLayer(nn.Module):
 
     # ------------------------------------------------------------------ MoE
     def _moe_allreduce(self, h: torch.Tensor) -> torch.Tensor:
-        logits = F.linear(h, self.router)
-        w, ids = ops.moe_topk_softmax(logits, self.cfg.experts_per_token)
+        w, ids = ops.moe_route(h, self.router, self.cfg.experts_per_token)
         out = ops.fused_moe(h, self.w13, self.w2, w, ids, self.expert_offset)
         return self._ar(out)
 
@@ -115,8 +114,7 @@ class LlamaLayer(nn.Module):
         send_eid = torch.full((tp, cap), -1, dtype=torch.int32, device=h.device)
         slot_of_pair = None
         if Ts > 0:
-            logits = F.linear(hs, self.router)
-            w, ids = ops.moe_topk_softmax(logits, k)
+            w, ids = ops.moe_route(hs, self.router, k)
             flat_ids = ids.reshape(-1).long()
             dest = flat_ids // self.E_local                                     # [Ts*k]
             onehot = F.one_hot(dest, tp).to(torch.int32)                        # [Ts*k, tp]

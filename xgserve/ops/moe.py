@@ -28,6 +28,20 @@ def moe_topk_softmax(router_logits: torch.Tensor, k: int, renorm: bool = True) -
     return w, ids
 
 
+def moe_route(h: torch.Tensor, router: torch.Tensor, k: int, renorm: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Router logits (fp32) + softmax + top-k in one kernel: h [T, H] bf16, router [E, H] bf16."""
+    if not use_native(h):
+        return moe_topk_softmax(h.float() @ router.float().t(), k, renorm)
+    T, H = h.shape
+    E = router.shape[0]
+    w = torch.empty(T, k, dtype=torch.float32, device=h.device)
+    ids = torch.empty(T, k, dtype=torch.int32, device=h.device)
+    hc = h.contiguous()
+    kernels().moe_route(hc.data_ptr(), router.data_ptr(), T, H, E, k, 1 if renorm else 0, w.data_ptr(),
+                        ids.data_ptr(), stream_ptr())
+    return w, ids
+
+
 def moe_align(ids: torch.Tensor, num_experts: int, expert_offset: int = 0, block_m: int = BLOCK_M):
     """Expert-sorted, block_m-padded layout of this rank's experts
     [expert_offset, expert_offset + num_experts). -> (sorted_rows [cap] (-1 = pad),
@@ -89,7 +103,11 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     kn.moe_gemm_m64(x.contiguous().data_ptr(), sorted_rows.data_ptr(), offs.data_ptr(), E, H, w13.data_ptr(), F2, P,
                     0, act.data_ptr(), 1, 2, 2, stream_ptr())
     # w2 has only H/64 column tiles per expert: split K while few experts are active
-    S = 2 if (T * k <= 8 and F % 512 == 0) else 1
+    S = 1
+    for sk in ((4, 2) if T * k <= 4 else (2,) if T * k <= 16 else ()):
+        if F % (sk * 256) == 0:
+            S = sk
+            break
     part = torch.empty(S, P, H, dtype=torch.float32, device=x.device)
     kn.moe_gemm_m64(act.data_ptr(), 0, offs.data_ptr(), E, F, w2.data_ptr(), H, P, part.data_ptr(), 0, S, 1, 1,
                     stream_ptr())
