@@ -38,7 +38,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, nargs="+", default=[32, 64])
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
-    ap.add_argument("--variants", type=int, nargs="+", default=[0, 1, 2, 3])
+    ap.add_argument("--variants", type=int, nargs="+", default=[2, 4])
     a = ap.parse_args()
     kernels()
     dev = "cuda"

@@ -1,0 +1,218 @@
+// gemm_m64 with LDS-DMA (global_load_lds_dwordx4) staging for BOTH operands.
+//
+// Same contract as gemm_m64 (16 < M <= 64, out = x . W^T, split-K partials /
+// bf16 / fused SiLU-gate), different load path: the register-ring kernel feeds
+// W to the MFMAs as fragment-shaped loads (16 rows x 64 B per wave instruction),
+// which keeps the texture-address path busy at ~4 TB/s chip-wide; here every
+// wave instruction moves 4 rows x 256 B (full lines) straight into LDS:
+//   * K chunk = 128 (256 B per row); 3 LDS slots, 2 chunks in flight;
+//   * W: each wave DMAs its own 16*NW rows into a wave-private region of the
+//     slot; x: the 4 waves DMA 64 rows x 256 B (4 instructions each);
+//   * LDS images are lane-linear (DMA writes base + lane*16) with the 16-B
+//     granule XOR-swizzle (granule ^ (row & 15)) applied on the GLOBAL source
+//     address, and undone on the ds_read_b128 fragment reads (conflict-free);
+//   * one raw s_barrier per chunk after a COUNTED vmcnt (the next chunk stays in
+//     flight across it), never __syncthreads (its fence would drain the DMA
+//     queue); WAR: a slot is re-filled only after the barrier that follows its
+//     last reads (cdna_hip_programming.md §5 "Pipelining across barriers").
+#include "common.h"
+
+namespace xgk {
+
+constexpr int GG_KC = 128;              // k per chunk (one slot)
+constexpr int GG_SLOTS = 3;
+constexpr int GG_XBYTES = 64 * 256;     // x rows x bytes per chunk
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+// The DMA is issued from inline asm so that hipcc's waitcnt pass does not see it:
+// with the builtin it serialises the DMAs of different slots (vmcnt(0) between
+// them and before every fragment read). Completion is then tracked ONLY by the
+// explicit counted waits below; "memory" keeps the compiler from moving LDS
+// reads across them.
+__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)(lds_base))));
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off"
+      :
+      : "v"(src), "s"(lds)
+      : "memory", "m0");
+#endif
+}
+
+// s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14; expcnt, lgkmcnt left at max)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#endif
+}
+
+__device__ __forceinline__ void raw_barrier() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_barrier" ::: "memory");
+#endif
+}
+
+enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2 };
+
+template <int NW>
+__global__ void __launch_bounds__(256, 1) gemm_m64g_kernel(const uint16_t* __restrict__ x, int M, int K,
+                                                           const uint16_t* __restrict__ w, int N,
+                                                           float* __restrict__ part, uint16_t* __restrict__ out,
+                                                           int mode) {
+  constexpr int MT = 4;
+  constexpr int WROWS = 16 * NW;                 // weight rows per wave
+  constexpr int WBYTES = WROWS * 256;            // per wave per slot
+  constexpr int SLOT = GG_XBYTES + 4 * WBYTES;   // bytes per slot
+  constexpr int G = NW * 4 + 4;                  // DMA instructions per wave per chunk
+  // one __shared__ object per slot, every slot index a compile-time constant: the
+  // compiler then proves a fragment read of slot A cannot alias the DMAs still in
+  // flight into slots B / C and keeps them in flight (with one runtime-indexed
+  // array it waits vmcnt(0) before every read)
+  __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
+  __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
+  __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int S = gridDim.y, s = blockIdx.y;
+  const int kws = K / S;
+  const int k0 = s * kws;
+  const int nchunks = kws / GG_KC;
+  const int nbase = blockIdx.x * (64 * NW) + wid * WROWS;
+
+  // DMA source rows / granules for this lane (fixed over the k loop)
+  const int dr = lane >> 4, dj = lane & 15;      // row within a 4-row instruction, granule
+  const uint16_t* wsrc[NW * 4];
+#pragma unroll
+  for (int i = 0; i < NW * 4; ++i) {
+    const int r = 4 * i + dr;                    // local weight row 0..WROWS-1
+    wsrc[i] = w + static_cast<int64_t>(nbase + r) * K + k0 + 8 * (dj ^ (r & 15));
+  }
+  const uint16_t* xsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 16 * wid + 4 * i + dr;         // x row 0..63
+    xsrc[i] = x + static_cast<int64_t>(min(r, M - 1)) * K + k0 + 8 * (dj ^ (r & 15));
+  }
+
+  auto issue = [&](uint8_t* slot, int c) {
+    const int kk = c * GG_KC;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kk, slot + (16 * wid + 4 * i) * 256);
+#pragma unroll
+    for (int i = 0; i < NW * 4; ++i) glds16(wsrc[i] + kk, slot + GG_XBYTES + wid * WBYTES + i * 1024);
+  };
+
+  f32x4_t acc[NW][MT];
+#pragma unroll
+  for (int nt = 0; nt < NW; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](const uint8_t* slot) {
+    const uint8_t* xs = slot;
+    const uint8_t* ws = slot + GG_XBYTES + wid * WBYTES;
+#pragma unroll
+    for (int t = 0; t < GG_KC / 32; ++t) {
+      const int phys = (4 * t + g) ^ li;    // swizzled granule of (row with row&15 == li, logical granule 4t+g)
+      uint4 b[MT], a[NW];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) b[mt] = *reinterpret_cast<const uint4*>(xs + (16 * mt + li) * 256 + phys * 16);
+#pragma unroll
+      for (int nt = 0; nt < NW; ++nt) a[nt] = *reinterpret_cast<const uint4*>(ws + (16 * nt + li) * 256 + phys * 16);
+#pragma unroll
+      for (int nt = 0; nt < NW; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = mfma16x16x32(as_frag(a[nt]), as_frag(b[mt]), acc[nt][mt]);
+    }
+  };
+
+  // chunk c lives in slot c % 3; per chunk: counted wait (chunk c+1 stays in
+  // flight), barrier, DMA chunk c+2 into the slot freed by that barrier, compute c
+  auto step = [&](uint8_t* cur, uint8_t* nxt2, int c) {
+    if (c + 1 < nchunks) wait_vmcnt<G>();
+    else wait_vmcnt<0>();
+    raw_barrier();
+    if (c + 2 < nchunks) issue(nxt2, c + 2);
+    compute(cur);
+  };
+
+  issue(lds0, 0);
+  if (nchunks > 1) issue(lds1, 1);
+  int c = 0;
+  for (; c + 3 <= nchunks; c += 3) {
+    step(lds0, lds2, c);
+    step(lds1, lds0, c + 1);
+    step(lds2, lds1, c + 2);
+  }
+  if (c < nchunks) step(lds0, lds2, c);
+  if (c + 1 < nchunks) step(lds1, lds0, c + 1);
+
+  // acc[nt][mt][r] = out[m = 16 mt + li][n = nbase + 16 nt + 4 g + r]
+  if (mode == GG_PARTIAL) {
+    float* pp = part + static_cast<int64_t>(s) * M * N;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = 16 * mt + li;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < NW; ++nt)
+        *reinterpret_cast<float4*>(pp + static_cast<int64_t>(m) * N + nbase + 16 * nt + 4 * g) =
+            make_float4(acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]);
+    }
+  } else if (mode == GG_BF16) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = 16 * mt + li;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < NW; ++nt) {
+        uint2 v;
+        v.x = pack2(acc[nt][mt][0], acc[nt][mt][1]);
+        v.y = pack2(acc[nt][mt][2], acc[nt][mt][3]);
+        *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * N + nbase + 16 * nt + 4 * g) = v;
+      }
+    }
+  } else if (NW == 2) {
+    const int F = N / 2, f0 = nbase / 2 + 4 * g;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = 16 * mt + li;
+      if (m >= M) continue;
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float gt = acc[0][mt][r];
+        o[r] = gt / (1.f + __expf(-gt)) * acc[NW - 1][mt][r];
+      }
+      uint2 v;
+      v.x = pack2(o[0], o[1]);
+      v.y = pack2(o[2], o[3]);
+      *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * F + f0) = v;
+    }
+  }
+}
+
+int gemm_m64g(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
+              int nw, hipStream_t st) {
+  if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2)) return 1;
+  if (K % (S * GG_KC) || N % (64 * nw)) return 1;
+  if (mode == GG_SILU && (nw != 2 || S != 1)) return 1;
+  if (mode == GG_PARTIAL && part == nullptr) return 1;
+  if (mode != GG_PARTIAL && out == nullptr) return 1;
+  const dim3 grid(N / (64 * nw), S);
+  if (nw == 1)
+    hipLaunchKernelGGL(gemm_m64g_kernel<1>, grid, dim3(256), 0, st, x, M, K, w, N, part, out, mode);
+  else
+    hipLaunchKernelGGL(gemm_m64g_kernel<2>, grid, dim3(256), 0, st, x, M, K, w, N, part, out, mode);
+  return 0;
+}
+
+}  // namespace xgk

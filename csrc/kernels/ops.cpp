@@ -21,6 +21,7 @@ void silu_and_mul(const uint16_t*, uint16_t*, int, int, int, hipStream_t);
 int skinny_gemm(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, hipStream_t);
 int skinny_slab_kmax(int);
 int gemm_m64(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
+int gemm_m64g(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, hipStream_t);
 void add_partials_rmsnorm(const float*, int, int, uint16_t*, const uint16_t*, uint16_t*, int, float, hipStream_t);
 void reduce_partials(const float*, int, int64_t, uint16_t*, hipStream_t);
 int rope_cache_partials(const float*, int, uint16_t*, int64_t, const int32_t*, const float*, uint16_t*, uint16_t*,
@@ -186,6 +187,12 @@ PYBIND11_MODULE(_kernels, m) {
     check(xgk::moe_gemm_m64(P<const uint16_t>(x), P<const int32_t>(rows), P<const int32_t>(offs), E, K,
                             P<const uint16_t>(w), N, P_, P<float>(part), P<uint16_t>(out), splits, mode, nw, S(st)),
           "moe_gemm_m64");
+  });
+  m.def("gemm_m64g", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
+                        int mode, int nw, uintptr_t st) {
+    check(xgk::gemm_m64g(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode, nw,
+                         S(st)),
+          "gemm_m64g");
   });
   m.def("moe_route", [](uintptr_t h, uintptr_t wr, int T, int H, int E, int k, int renorm, uintptr_t w, uintptr_t ids,
                         uintptr_t st) {

@@ -83,8 +83,8 @@ class LlamaLayer(nn.Module):
             self.split_down = pick_split(H, Fl)
             dims_ok = dims_ok and Fl % 256 == 0 and (2 * Fl) % 64 == 0 and self.split_down
         self.fast_ok = bool(dims_ok) and torch.device(device).type == "cuda"
-        # 16 < M <= 64: gemm_m64 for QKV / O / down (split-K partials into the consumers),
-        # and the fused SiLU-gate gate_up above M = 32 (measured: bench/gemm_bench.py)
+        # 16 < M <= 64: gemm_m64g for QKV / O / down (split-K partials into the consumers)
+        # and the fused SiLU-gate gate_up (measured: bench/gemm_bench.py)
         self.m64_ok = self.fast_ok and all(
             m64_plan(64, n, k, MODE_PARTIAL) is not None
             for n, k in ((Nqkv, H), (H, Hq * D)) + (() if self.moe else ((H, cfg.intermediate_size // tp),)))
@@ -181,7 +181,7 @@ class LlamaLayer(nn.Module):
             h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
             if self.moe:
                 return self.mlp(h), residual
-            if self.m64_silu_ok and T > 32:
+            if self.m64_silu_ok:
                 act = m64_linear(h, self.gate_up, MODE_SILU)
             else:
                 act = ops.silu_and_mul(F.linear(h, self.gate_up), interleave16=True)

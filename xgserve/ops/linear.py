@@ -87,30 +87,28 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, split_k: Optional[int] = Non
     return out
 
 
-def m64_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL, target_wgs: int = 224):
-    """(nw, split_k) for gemm_m64, or None if the shape is unsupported. 128-column tiles
-    when there are enough of them, else 64; split-K until ~one workgroup per CU
-    (bf16 / SiLU epilogues need the full K sum: split 1)."""
+def m64_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL):
+    """(nw, split_k) for gemm_m64 / gemm_m64g, or None if unsupported. Measured on
+    MI355X (bench/gemm_bench.py, profiles/r1_gemm_*): split-K 4 whenever K allows
+    (the partials are reduced by the consumer kernel for free), 128-column tiles
+    once they give >= 192 workgroups, else 64; bf16 / SiLU epilogues need split 1."""
     if not (16 < M <= 64) or K % 256:
         return None
     if mode == MODE_SILU:
         return (2, 1) if N % 128 == 0 else None
-    nw = 2 if (N % 128 == 0 and N // 128 >= 192) else 1
+    if mode == MODE_BF16:
+        nw = 2 if N % 128 == 0 else 1
+        return (nw, 1) if N % (64 * nw) == 0 else None
+    S = next(s for s in (4, 2, 1) if K % (s * 256) == 0)
+    nw = 2 if (N % 128 == 0 and (N // 128) * S >= 192) else 1
     if N % (64 * nw):
         return None
-    if mode == MODE_BF16:
-        return nw, 1
-    tiles, S = N // (64 * nw), 1
-    for sk in (1, 2, 4, 8, 16):
-        if K % (sk * 256):
-            break
-        S = sk
-        if tiles * sk >= target_wgs:
-            break
     return nw, S
 
 
-M64_VARIANT = 2  # bit0: two W chunks in flight; bit1: default cache policy for W (else non-temporal)
+# 4: LDS-DMA staging (gemm_m64g.hip, fastest on every measured shape); 0-3: register-ring gemm_m64
+# (bit0: two W chunks in flight; bit1: default cache policy for W, else non-temporal)
+M64_VARIANT = 4
 
 
 def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split_k: Optional[int] = None,
@@ -124,16 +122,22 @@ def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split
         raise ValueError(f"gemm_m64: unsupported shape M={M} N={N} K={K} mode={mode}")
     nw = nw or plan[0]
     S = split_k or plan[1]
+    var = M64_VARIANT if variant is None else variant
+    k = kernels()
     if mode == MODE_PARTIAL:
         part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
-        kernels().gemm_m64(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw,
-                           M64_VARIANT if variant is None else variant, stream_ptr())
+        if var == 4:  # LDS-DMA staging (gemm_m64g.hip)
+            k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, stream_ptr())
+        else:
+            k.gemm_m64(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, var, stream_ptr())
         return PendingSum(part, S)
     ncol = N // 2 if mode == MODE_SILU else N
     if out is None:
         out = torch.empty(M, ncol, dtype=torch.bfloat16, device=x.device)
-    kernels().gemm_m64(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw,
-                       M64_VARIANT if variant is None else variant, stream_ptr())
+    if var == 4:
+        k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, stream_ptr())
+    else:
+        k.gemm_m64(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, var, stream_ptr())
     return out
 
 
