@@ -200,6 +200,166 @@ __global__ void __launch_bounds__(256, 1) gemm_m64g_kernel(const uint16_t* __res
   }
 }
 
+// Grouped (MoE) form of the same pipeline: W [E, N, K]; x rows gathered through
+// the block-64 padded expert-sorted layout (rows[p] = source row, -1 = pad;
+// rows == nullptr: x already in padded layout); offs[E+1] padded segment starts.
+// One workgroup per (column tile, k-split, expert) loops over the expert's
+// 64-row tiles (the same weight column tile is re-read from L2/MALL, not HBM).
+template <int NW>
+__global__ void __launch_bounds__(256, 1) gemm_m64g_grouped_kernel(const uint16_t* __restrict__ x,
+                                                                   const int32_t* __restrict__ rows,
+                                                                   const int32_t* __restrict__ offs, int K,
+                                                                   const uint16_t* __restrict__ w, int N, int P,
+                                                                   float* __restrict__ part,
+                                                                   uint16_t* __restrict__ out, int mode) {
+  constexpr int MT = 4;
+  constexpr int WROWS = 16 * NW;
+  constexpr int WBYTES = WROWS * 256;
+  constexpr int SLOT = GG_XBYTES + 4 * WBYTES;
+  constexpr int G = NW * 4 + 4;
+  __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
+  __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
+  __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
+
+  const int e = blockIdx.z;
+  const int p0 = offs[e], p1 = offs[e + 1];
+  if (p1 <= p0) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int S = gridDim.y, s = blockIdx.y;
+  const int kws = K / S;
+  const int k0 = s * kws;
+  const int nchunks = kws / GG_KC;
+  const int nbase = blockIdx.x * (64 * NW) + wid * WROWS;
+  const int dr = lane >> 4, dj = lane & 15;
+  const uint16_t* we = w + static_cast<int64_t>(e) * N * K;
+  const uint16_t* wsrc[NW * 4];
+#pragma unroll
+  for (int i = 0; i < NW * 4; ++i) {
+    const int r = 4 * i + dr;
+    wsrc[i] = we + static_cast<int64_t>(nbase + r) * K + k0 + 8 * (dj ^ (r & 15));
+  }
+
+  for (int rt = p0; rt < p1; rt += 64) {
+    if (rt != p0) raw_barrier();  // the previous tile's last slot may still be read
+    const int first = rows ? rows[rt] : rt;
+    const uint16_t* xsrc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 16 * wid + 4 * i + dr;
+      int src = rows ? rows[rt + r] : rt + r;
+      if (src < 0) src = first;
+      xsrc[i] = x + static_cast<int64_t>(src) * K + k0 + 8 * (dj ^ (r & 15));
+    }
+    auto issue = [&](uint8_t* slot, int c) {
+      const int kk = c * GG_KC;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kk, slot + (16 * wid + 4 * i) * 256);
+#pragma unroll
+      for (int i = 0; i < NW * 4; ++i) glds16(wsrc[i] + kk, slot + GG_XBYTES + wid * WBYTES + i * 1024);
+    };
+    f32x4_t acc[NW][MT];
+#pragma unroll
+    for (int nt = 0; nt < NW; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](const uint8_t* slot) {
+      const uint8_t* xs = slot;
+      const uint8_t* ws = slot + GG_XBYTES + wid * WBYTES;
+#pragma unroll
+      for (int t = 0; t < GG_KC / 32; ++t) {
+        const int phys = (4 * t + g) ^ li;
+        uint4 b[MT], a[NW];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          b[mt] = *reinterpret_cast<const uint4*>(xs + (16 * mt + li) * 256 + phys * 16);
+#pragma unroll
+        for (int nt = 0; nt < NW; ++nt)
+          a[nt] = *reinterpret_cast<const uint4*>(ws + (16 * nt + li) * 256 + phys * 16);
+#pragma unroll
+        for (int nt = 0; nt < NW; ++nt)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = mfma16x16x32(as_frag(a[nt]), as_frag(b[mt]), acc[nt][mt]);
+      }
+    };
+    auto step = [&](uint8_t* cur, uint8_t* nxt2, int c) {
+      if (c + 1 < nchunks) wait_vmcnt<G>();
+      else wait_vmcnt<0>();
+      raw_barrier();
+      if (c + 2 < nchunks) issue(nxt2, c + 2);
+      compute(cur);
+    };
+    issue(lds0, 0);
+    if (nchunks > 1) issue(lds1, 1);
+    int c = 0;
+    for (; c + 3 <= nchunks; c += 3) {
+      step(lds0, lds2, c);
+      step(lds1, lds0, c + 1);
+      step(lds2, lds1, c + 2);
+    }
+    if (c < nchunks) step(lds0, lds2, c);
+    if (c + 1 < nchunks) step(lds1, lds0, c + 1);
+
+    if (mode == GG_PARTIAL) {
+      float* pp = part + static_cast<int64_t>(s) * P * N;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = rt + 16 * mt + li;
+#pragma unroll
+        for (int nt = 0; nt < NW; ++nt)
+          *reinterpret_cast<float4*>(pp + static_cast<int64_t>(m) * N + nbase + 16 * nt + 4 * g) =
+              make_float4(acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]);
+      }
+    } else if (mode == GG_BF16) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = rt + 16 * mt + li;
+#pragma unroll
+        for (int nt = 0; nt < NW; ++nt) {
+          uint2 v;
+          v.x = pack2(acc[nt][mt][0], acc[nt][mt][1]);
+          v.y = pack2(acc[nt][mt][2], acc[nt][mt][3]);
+          *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * N + nbase + 16 * nt + 4 * g) = v;
+        }
+      }
+    } else if (NW == 2) {
+      const int F = N / 2, f0 = nbase / 2 + 4 * g;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = rt + 16 * mt + li;
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gt = acc[0][mt][r];
+          o[r] = gt / (1.f + __expf(-gt)) * acc[NW - 1][mt][r];
+        }
+        uint2 v;
+        v.x = pack2(o[0], o[1]);
+        v.y = pack2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * F + f0) = v;
+      }
+    }
+  }
+}
+
+int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, int E, int K, const uint16_t* w, int N,
+                  int P, float* part, uint16_t* out, int S, int mode, int nw, hipStream_t st) {
+  if (E < 1 || P < 0 || P % 64 || S < 1 || (nw != 1 && nw != 2)) return 1;
+  if (K % (S * GG_KC) || N % (64 * nw)) return 1;
+  if (mode == GG_SILU && (nw != 2 || S != 1)) return 1;
+  if (mode == GG_PARTIAL && part == nullptr) return 1;
+  if (mode != GG_PARTIAL && out == nullptr) return 1;
+  if (P == 0) return 0;
+  const dim3 grid(N / (64 * nw), S, E);
+  if (nw == 1)
+    hipLaunchKernelGGL(gemm_m64g_grouped_kernel<1>, grid, dim3(256), 0, st, x, rows, offs, K, w, N, P, part, out,
+                       mode);
+  else
+    hipLaunchKernelGGL(gemm_m64g_grouped_kernel<2>, grid, dim3(256), 0, st, x, rows, offs, K, w, N, P, part, out,
+                       mode);
+  return 0;
+}
+
 int gemm_m64g(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
               int nw, hipStream_t st) {
   if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2)) return 1;

@@ -259,3 +259,22 @@ def test_moe_route_matches_fp32(T, E, k, H):
     rw, rids = ops.moe_topk_softmax(logits.cpu(), k)
     assert torch.equal(ids.cpu().long().sort(-1).values, rids.long().sort(-1).values)
     torch.testing.assert_close(w.cpu().sort(-1).values, rw.sort(-1).values, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("glds", [True, False])
+@pytest.mark.parametrize("T", [1, 3, 64, 150])
+def test_fused_moe_both_pipelines(T, glds):
+    from xgserve.ops import moe as M
+    E, k, H, F = 8, 2, 1024, 512
+    x = rnd(T, H)
+    w13 = _w13(E, F, H)
+    w2 = rnd(E, H, F, scale=0.05)
+    w, ids = ops.moe_topk_softmax(rnd(T, E, dtype=torch.float32), k)
+    old = M.MOE_GLDS
+    M.MOE_GLDS = glds
+    try:
+        out = ops.fused_moe(x, w13, w2, w, ids)
+    finally:
+        M.MOE_GLDS = old
+    ref = ops.moe_forward_ref(x.cpu(), w13.cpu(), w2.cpu(), w.cpu(), ids.cpu()).float()
+    torch.testing.assert_close(out.cpu().float(), ref, atol=2e-2 * ref.std().item(), rtol=2e-2)

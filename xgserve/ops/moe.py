@@ -9,6 +9,7 @@ from ._native import kernels, stream_ptr, use_native
 from .activation import silu_and_mul
 
 BLOCK_M = 64
+MOE_GLDS = True  # expert GEMMs on the LDS-DMA pipeline (gemm_m64g.hip); False: register-ring gemm_m64
 
 
 def moe_topk_softmax(router_logits: torch.Tensor, k: int, renorm: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -100,8 +101,9 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     P = sorted_rows.shape[0]
     act = torch.empty(P, F, dtype=x.dtype, device=x.device)
     kn = kernels()
-    kn.moe_gemm_m64(x.contiguous().data_ptr(), sorted_rows.data_ptr(), offs.data_ptr(), E, H, w13.data_ptr(), F2, P,
-                    0, act.data_ptr(), 1, 2, 2, stream_ptr())
+    gemm = kn.moe_gemm_m64g if MOE_GLDS else kn.moe_gemm_m64
+    gemm(x.contiguous().data_ptr(), sorted_rows.data_ptr(), offs.data_ptr(), E, H, w13.data_ptr(), F2, P, 0,
+         act.data_ptr(), 1, 2, 2, stream_ptr())
     # w2 has only H/64 column tiles per expert: split K while few experts are active
     S = 1
     for sk in ((4, 2) if T * k <= 4 else (2,) if T * k <= 16 else ()):
@@ -109,8 +111,7 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
             S = sk
             break
     part = torch.empty(S, P, H, dtype=torch.float32, device=x.device)
-    kn.moe_gemm_m64(act.data_ptr(), 0, offs.data_ptr(), E, F, w2.data_ptr(), H, P, part.data_ptr(), 0, S, 1, 1,
-                    stream_ptr())
+    gemm(act.data_ptr(), 0, offs.data_ptr(), E, F, w2.data_ptr(), H, P, part.data_ptr(), 0, S, 1, 1, stream_ptr())
     out = torch.empty(T, H, dtype=x.dtype, device=x.device)
     kn.moe_combine(part.data_ptr(), S, P, dest.data_ptr(), topk_w.float().contiguous().data_ptr(), out.data_ptr(), T,
                    k, H, stream_ptr())
