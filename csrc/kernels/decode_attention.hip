@@ -54,7 +54,8 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int bt_stride,
     const int32_t* __restrict__ seq_lens, float* __restrict__ part_out, float* __restrict__ part_lse,
-    uint16_t* __restrict__ out, int64_t out_stride, int Hq, int Hkv, int bs, float scale, int num_splits) {
+    uint16_t* __restrict__ out, int64_t out_stride, int Hq, int Hkv, int bs, float scale, int num_splits,
+    int* __restrict__ counters) {
   using C = DecodeCfg<D, G>;
   const int kvh = blockIdx.x, b = blockIdx.y, split = blockIdx.z;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -195,6 +196,43 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
       if (d == 0) part_lse[pi] = Ls > 0.f ? M + __logf(Ls) : -INFINITY;
     }
   }
+  if (num_splits == 1 || counters == nullptr) return;
+  // In-launch split-K combine: the last split of (b, kv head) to arrive merges all
+  // splits' (O, lse) for its G query heads (cdna_hip_programming.md §5 "In-launch
+  // split-K reduction": agent-scope release before the ticket, acquire after it).
+  __shared__ int am_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* cnt = counters + b * Hkv + kvh;
+    const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    am_last = prev == num_splits - 1;
+    if (am_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      *cnt = 0;  // re-armed for the next launch (graph replays included)
+    }
+  }
+  __syncthreads();
+  if (!am_last) return;
+  for (int idx = threadIdx.x; idx < G * D; idx += blockDim.x) {
+    const int qhead = kvh * G + idx / D, d = idx % D;
+    const int64_t bh = static_cast<int64_t>(b) * Hq + qhead;
+    const float* lse = part_lse + bh * num_splits;
+    float M = -INFINITY;
+    for (int s2 = 0; s2 < num_splits; ++s2) M = fmaxf(M, lse[s2]);
+    float den = 0.f, acc = 0.f;
+    if (M != -INFINITY) {
+      for (int s2 = 0; s2 < num_splits; ++s2) {
+        const float wgt = __expf(lse[s2] - M);
+        den += wgt;
+        acc += wgt * part_out[(bh * num_splits + s2) * D + d];
+      }
+    }
+    out[static_cast<int64_t>(b) * out_stride + static_cast<int64_t>(qhead) * D + d] = f2bf(den > 0.f ? acc / den : 0.f);
+  }
 }
 
 // Split-K reduction: out[b, h, :] = sum_s softmax(lse)_s * part_out[b, h, s, :]
@@ -223,10 +261,11 @@ __global__ void __launch_bounds__(D) decode_combine_kernel(const float* __restri
 template <int D, int G>
 static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, const uint16_t* vc,
                           const int32_t* bt, int bts, const int32_t* sl, float* po, float* pl, uint16_t* out,
-                          int64_t os, int B, int Hq, int Hkv, int bs, float scale, int S, hipStream_t st) {
+                          int64_t os, int B, int Hq, int Hkv, int bs, float scale, int S, int* counters,
+                          hipStream_t st) {
   hipLaunchKernelGGL((decode_attn_kernel<D, G>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt, bts, sl,
-                     po, pl, out, os, Hq, Hkv, bs, scale, S);
-  if (S > 1)
+                     po, pl, out, os, Hq, Hkv, bs, scale, S, counters);
+  if (S > 1 && counters == nullptr)
     hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
 }
 
@@ -234,14 +273,14 @@ static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, con
 int decode_attention(const uint16_t* q, int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
                      const int32_t* bt, int bt_stride, const int32_t* seq_lens, float* part_out, float* part_lse,
                      uint16_t* out, int64_t out_stride, int B, int Hq, int Hkv, int D, int bs, float scale,
-                     int num_splits, hipStream_t st) {
+                     int num_splits, int* counters, hipStream_t st) {
   if (B <= 0) return 0;
   if (bs % 16 != 0 || Hq % Hkv != 0) return -1;
   const int G = Hq / Hkv;
 #define XGK_DEC(DD, GG)                                                                                  \
   if (D == DD && G == GG) {                                                                              \
     launch_decode<DD, GG>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, part_out, part_lse, out, out_stride, \
-                          B, Hq, Hkv, bs, scale, num_splits, st);                                       \
+                          B, Hq, Hkv, bs, scale, num_splits, counters, st);                             \
     return 0;                                                                                            \
   }
   XGK_DEC(128, 1) XGK_DEC(128, 2) XGK_DEC(128, 4) XGK_DEC(128, 8) XGK_DEC(128, 16)

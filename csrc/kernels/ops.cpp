@@ -32,7 +32,7 @@ void gelu_tanh(const uint16_t*, uint16_t*, int64_t, hipStream_t);
 int rope_cache(uint16_t*, int64_t, const int32_t*, const float*, uint16_t*, uint16_t*, const int32_t*, int, int, int,
                int, int, int, hipStream_t);
 int decode_attention(const uint16_t*, int64_t, const uint16_t*, const uint16_t*, const int32_t*, int, const int32_t*,
-                     float*, float*, uint16_t*, int64_t, int, int, int, int, int, float, int, hipStream_t);
+                     float*, float*, uint16_t*, int64_t, int, int, int, int, int, float, int, int*, hipStream_t);
 int prefill_attention(const uint16_t*, int64_t, const uint16_t*, const uint16_t*, const int32_t*, int, const int32_t*,
                       const int32_t*, uint16_t*, int64_t, int, int, int, int, int, int, float, hipStream_t);
 void argmax_logprob(const void*, int, int64_t, int, int, int32_t*, float*, hipStream_t);
@@ -139,10 +139,10 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("decode_attention", [](uintptr_t q, int64_t qs, uintptr_t kc, uintptr_t vc, uintptr_t bt, int bts,
                                uintptr_t sl, uintptr_t po, uintptr_t pl, uintptr_t out, int64_t os, int B, int Hq,
-                               int Hkv, int D, int bs, float scale, int splits, uintptr_t st) {
+                               int Hkv, int D, int bs, float scale, int splits, uintptr_t counters, uintptr_t st) {
     check(xgk::decode_attention(P<const uint16_t>(q), qs, P<const uint16_t>(kc), P<const uint16_t>(vc),
                                 P<const int32_t>(bt), bts, P<const int32_t>(sl), P<float>(po), P<float>(pl),
-                                P<uint16_t>(out), os, B, Hq, Hkv, D, bs, scale, splits, S(st)),
+                                P<uint16_t>(out), os, B, Hq, Hkv, D, bs, scale, splits, P<int>(counters), S(st)),
           "decode_attention");
   });
   m.def("prefill_attention", [](uintptr_t q, int64_t qs, uintptr_t kc, uintptr_t vc, uintptr_t bt, int bts,

@@ -278,3 +278,27 @@ def test_fused_moe_both_pipelines(T, glds):
         M.MOE_GLDS = old
     ref = ops.moe_forward_ref(x.cpu(), w13.cpu(), w2.cpu(), w.cpu(), ids.cpu()).float()
     torch.testing.assert_close(out.cpu().float(), ref, atol=2e-2 * ref.std().item(), rtol=2e-2)
+
+
+@pytest.mark.parametrize("in_kernel", [True, False])
+def test_decode_attention_split_combine_rearms(in_kernel):
+    """The in-launch combine's arrival tickets re-arm: repeated launches on one
+    workspace (as graph replays do) stay correct; also the two-launch fallback."""
+    from xgserve.ops import attention as A
+    Hq, Hkv, D, bs = 32, 8, 128, 16
+    lens = [700, 33, 1, 256]
+    kc, vc, bt = _paged(lens, Hkv, D, bs)
+    B = len(lens)
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    ws = A.DecodeWorkspace(B, Hq, D, 16, DEV)
+    old = A.IN_KERNEL_COMBINE
+    A.IN_KERNEL_COMBINE = in_kernel
+    try:
+        for it, splits in enumerate((16, 16, 5, 16)):
+            q = rnd(B, Hq, D)
+            out = ops.decode_attention(q, kc, vc, bt, sl, 0.088, num_splits=splits, workspace=ws)
+            ref = ops.decode_attention_ref(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), sl.cpu(), 0.088)
+            torch.testing.assert_close(out.cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
+    finally:
+        A.IN_KERNEL_COMBINE = old
+    assert int(ws.counters.abs().sum()) == 0

@@ -8,6 +8,8 @@ import torch
 
 from ._native import kernels, stream_ptr, use_native
 
+IN_KERNEL_COMBINE = True  # split-K decode: last-arriving split merges (no combine launch)
+
 
 def choose_num_splits(batch: int, num_kv_heads: int, max_seq_len: int, num_cus: int = 256) -> int:
     """Split-K factor so the decode grid has >= ~2 workgroups per CU, but every
@@ -77,6 +79,9 @@ class DecodeWorkspace:
         self.part_out = torch.empty(max_batch * num_q_heads * max_splits * head_dim, dtype=torch.float32,
                                     device=device)
         self.part_lse = torch.empty(max_batch * num_q_heads * max_splits, dtype=torch.float32, device=device)
+        # arrival tickets of the in-launch split combine ([B, Hkv] <= [B, Hq]); the last
+        # split of each (sequence, kv head) re-zeroes its ticket
+        self.counters = torch.zeros(max_batch * num_q_heads, dtype=torch.int32, device=device)
         self.max_splits = max_splits
 
 
@@ -102,12 +107,13 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         if workspace is None or workspace.max_splits < num_splits or workspace.part_lse.numel() < B * Hq * num_splits:
             workspace = DecodeWorkspace(B, Hq, D, num_splits, q.device)
         po, pl = workspace.part_out.data_ptr(), workspace.part_lse.data_ptr()
+        cnt = workspace.counters.data_ptr() if IN_KERNEL_COMBINE else 0
     else:
-        po = pl = 0
+        po = pl = cnt = 0
     kernels().decode_attention(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                block_tables.data_ptr(), block_tables.stride(0), seq_lens.data_ptr(), po, pl,
                                out.data_ptr(), out.stride(0), B, Hq, Hkv, D, bs, float(scale), int(num_splits),
-                               stream_ptr())
+                               cnt, stream_ptr())
     return out
 
 
