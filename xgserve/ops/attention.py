@@ -8,7 +8,10 @@ import torch
 
 from ._native import kernels, stream_ptr, use_native
 
-IN_KERNEL_COMBINE = True  # split-K decode: last-arriving split merges (no combine launch)
+# split-K decode: the last-arriving split merges in-launch instead of a combine launch.
+# Measured slower on MI355X (8B batch 1: 4.14 vs 3.89 ms/step; c64 -2.5%): the serial merge
+# on the tail workgroup costs more than the ~4 us launch boundary it saves. Kept switchable.
+IN_KERNEL_COMBINE = False
 
 
 def choose_num_splits(batch: int, num_kv_heads: int, max_seq_len: int, num_cus: int = 256) -> int:
