@@ -7,6 +7,7 @@
 #include "queue.h"
 #include "router.h"
 #include "scheduler.h"
+#include "shm_channel.h"
 #include "validator.h"
 
 namespace py = pybind11;
@@ -320,4 +321,33 @@ PYBIND11_MODULE(_runtime, m) {
         }
         return out;
       });
+
+  py::class_<ShmChannel>(m, "ShmChannel")
+      .def(py::init<const std::string&, uint64_t, int, bool>(), py::arg("name"),
+           py::arg("capacity"), py::arg("num_readers"), py::arg("create"))
+      .def("publish",
+           [](ShmChannel& c, py::bytes b, double timeout_s) {
+             std::string_view v = b;
+             py::gil_scoped_release nogil;
+             return c.publish(v.data(), v.size(), timeout_s);
+           },
+           py::arg("data"), py::arg("timeout_s") = -1.0)
+      .def("receive",
+           [](ShmChannel& c, int rank, double timeout_s) -> py::object {
+             int64_t n;
+             {
+               py::gil_scoped_release nogil;
+               n = c.wait_message(rank, timeout_s);
+             }
+             if (n < 0) return py::none();
+             PyObject* b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)n);
+             if (!b) throw py::error_already_set();
+             c.consume(rank, PyBytes_AS_STRING(b));
+             return py::reinterpret_steal<py::object>(b);
+           },
+           py::arg("rank"), py::arg("timeout_s") = -1.0)
+      .def_property_readonly("capacity", &ShmChannel::capacity)
+      .def_property_readonly("seq", &ShmChannel::seq)
+      .def_property_readonly("name", &ShmChannel::name)
+      .def("unlink", &ShmChannel::unlink);
 }

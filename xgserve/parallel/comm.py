@@ -11,6 +11,7 @@ Sizing notes for MI355X (7 xGMI links x ~153 GB/s per GPU, point-to-point):
 """
 from __future__ import annotations
 
+import pickle
 from typing import List, Optional
 
 import torch
@@ -85,10 +86,31 @@ def tp_exchange_counts(counts: torch.Tensor) -> torch.Tensor:
     return out
 
 
+PLAN_TIMEOUT_S = 600.0
+
+
 def tp_broadcast_object(obj, src: int = 0):
+    """Leader -> followers object broadcast. Uses the shared-memory plan channel
+    when the group has one (one memcpy + an atomic, no TCP round trip); an object
+    larger than the channel travels over gloo, announced by an empty message."""
     s = get_state()
     if s.tp_size == 1:
         return obj
+    ch = s.plan_channel
+    if ch is not None and src == 0:
+        if s.tp_rank == 0:
+            data = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+            big = len(data) > ch.capacity
+            if not ch.publish(b"" if big else data, PLAN_TIMEOUT_S):
+                raise RuntimeError("TP follower did not consume the previous plan (dead rank?)")
+            if not big:
+                return obj
+        else:
+            data = None
+            while data is None:
+                data = ch.receive(s.tp_rank - 1, PLAN_TIMEOUT_S)
+            if data:
+                return pickle.loads(data)
     lst = [obj]
     g = s.tp_cpu_group if s.tp_cpu_group is not None else s.tp_group
     src_global = dist.get_global_rank(g, src) if g is not None and g != dist.group.WORLD else src

@@ -31,6 +31,7 @@ class ParallelState:
     tp_cpu_group: Optional[object] = None
     backend: str = "none"
     device: torch.device = torch.device("cpu")
+    plan_channel: Optional[object] = None  # _runtime.ShmChannel (TP leader writes, followers read)
 
     @property
     def ep_size(self) -> int:
@@ -98,11 +99,63 @@ def init_distributed(tp_size: int = 1, backend: Optional[str] = None, device: Op
     s = ParallelState(world_size=world, rank=rank, tp_size=tp_size, tp_rank=my.index(rank),
                       dp_size=world // tp_size, dp_rank=rank // tp_size, tp_group=tp_group,
                       tp_cpu_group=tp_cpu, backend=backend, device=device)
+    if tp_size > 1:
+        s.plan_channel = _open_plan_channel(s, my)
     set_state(s)
     return s
 
 
+PLAN_CHANNEL_BYTES = 32 << 20  # sparse: only the pages a plan touches are ever backed
+
+
+def _open_plan_channel(s: ParallelState, ranks):
+    """Per-step plan broadcast over POSIX shared memory.
+
+    The TP leader creates the segment, the name travels once over the gloo
+    group, every follower maps it, and the leader unlinks the name as soon as
+    all ranks hold a mapping, so a crashed group leaves nothing in /dev/shm.
+    TP groups are always node-local (one process per GPU of one node).
+    Disabled with XGS_SHM_PLAN=0 (plans then go over gloo)."""
+    if os.environ.get("XGS_SHM_PLAN", "1") == "0":
+        return None
+    try:
+        from .. import _runtime as R
+    except ImportError:
+        return None
+    g = s.tp_cpu_group
+    src = ranks[0]
+    ch, err = None, None
+    if s.tp_rank == 0:
+        name = f"xgs_plan_{os.getpid()}_{s.dp_rank}_{os.environ.get('MASTER_PORT', '0')}"
+        try:
+            ch = R.ShmChannel(name, PLAN_CHANNEL_BYTES, s.tp_size - 1, True)
+        except Exception as e:  # noqa: BLE001 - fall back to gloo below
+            name, err = None, e
+        box = [name]
+    else:
+        box = [None]
+    dist.broadcast_object_list(box, src=src, group=g)
+    name = box[0]
+    ok = 1
+    if name is not None and s.tp_rank != 0:
+        try:
+            ch = R.ShmChannel(name, 0, s.tp_size - 1, False)
+        except Exception as e:  # noqa: BLE001
+            ch, ok, err = None, 0, e
+    flag = torch.tensor([ok if name is not None else 0], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=g)
+    if s.tp_rank == 0 and ch is not None:
+        ch.unlink()
+    if not int(flag.item()):
+        if err is not None:
+            import logging
+            logging.getLogger("xgserve").warning("shm plan channel unavailable (%s); using gloo", err)
+        return None
+    return ch
+
+
 def destroy_distributed() -> None:
+    _STATE.plan_channel = None
     if dist.is_initialized():
         dist.destroy_process_group()
     set_state(ParallelState())
