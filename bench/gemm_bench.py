@@ -54,6 +54,13 @@ def main():
             us = timeit([lambda w=w: F.linear(x, w) for w in ws])
             rows.append(("hipblaslt", us, None))
             mode = L.MODE_SILU if name == "gate_up" else (L.MODE_BF16 if name == "lm_head" else L.MODE_PARTIAL)
+            if M <= 16:
+                for S in ((1,) if mode != L.MODE_PARTIAL else (1, 2, 4, 7, 8, 14, 16)):
+                    if K % (S * 256) or (mode == L.MODE_PARTIAL and N % 64):
+                        continue
+                    fn = lambda w, S=S: L.skinny_linear(x, w, S, mode)  # noqa: E731
+                    us3 = timeit([lambda w=w, fn=fn: fn(w) for w in ws])
+                    rows.append((f"skinny(S={S},mode={mode})", us3, None))
             plan = L.m64_plan(M, N, K, mode)
             if plan is not None:
                 for nw in ((1, 2) if mode == L.MODE_PARTIAL and N % 128 == 0 else (plan[0],)):
