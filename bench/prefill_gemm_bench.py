@@ -24,13 +24,22 @@ def timeit(fn, iters=20, warm=5):
 
 
 def main():
-    Ms = [int(m) for m in sys.argv[1:]] or [512, 575, 576, 640, 768, 1024, 2048, 4096]
+    args = sys.argv[1:]
+    tag = "hipblaslt"
+    if args and args[0] == "--tunable":  # PyTorch TunableOp: benchmark rocBLAS + hipBLASLt solutions per shape
+        args = args[1:]
+        tag = "tunableop"
+        torch.cuda.tunable.enable(True)
+        torch.cuda.tunable.tuning_enable(True)
+        torch.cuda.tunable.set_max_tuning_duration(200)
+        torch.cuda.tunable.set_filename(os.environ.get("TUNABLE_FILE", "/tmp/tunableop.csv"))
+    Ms = [int(m) for m in args] or [512, 575, 576, 640, 768, 1024, 2048, 4096]
     for name, (N, K) in SHAPES.items():
         w = (torch.randn(N, K, device="cuda") * 0.02).bfloat16()
         for M in Ms:
             x = torch.randn(M, K, device="cuda").bfloat16()
             us = timeit(lambda: F.linear(x, w))
-            print(json.dumps({"shape": name, "M": M, "us": round(us, 2), "TFLOP/s": round(2 * M * N * K / us / 1e6, 1)}),
+            print(json.dumps({"op": tag, "shape": name, "M": M, "us": round(us, 2), "TFLOP/s": round(2 * M * N * K / us / 1e6, 1)}),
                   flush=True)
 
 

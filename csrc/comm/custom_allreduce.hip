@@ -23,6 +23,17 @@
 // hence finished reading generation g-2 (the previous user of slot s).
 // Buffers and signals are allocated uncached (hipDeviceMallocUncached) so peer
 // reads never see stale cache lines; flags use system-scope atomics.
+// Two-shot variant (car2_kernel) for larger messages (prefill, 512 KiB..32 MiB at
+// TP >= 4): the message is split into W rank shards; block b of every rank
+//   1. stages chunk b of every shard into its IPC slot, signals phase 0
+//   2. reduces chunk b of its OWN shard over all ranks (rank order), writes the
+//      result to its output and back into its own slot, signals phase 1
+//   3. copies chunk b of every other shard (already reduced by its owner)
+// so each xGMI link carries ~2n/W bytes instead of n (one-shot), and every rank
+// ends with the same bits (each shard is reduced exactly once). It has its own
+// slots, signal arrays and generation counters, so the one-shot and two-shot
+// paths never share a buffer region (the double-buffering argument above holds
+// per block index within each path).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -106,6 +117,84 @@ __global__ void __launch_bounds__(CAR_THREADS) car_kernel(const uint8_t* __restr
   if (t == 0) gens[b] = gen;
 }
 
+template <typename T>
+__device__ __forceinline__ void car_signal_wait(const CarPtrs& p, int phase, int rank, int world, int b,
+                                                uint32_t gen, uint32_t* timeouts) {
+  const int t = threadIdx.x;
+  __threadfence_system();
+  __syncthreads();
+  const int64_t ph = static_cast<int64_t>(phase) * CAR_MAX_RANKS * CAR_MAX_BLOCKS;
+  if (t < world && t != rank)
+    __hip_atomic_store(p.sig[t] + ph + rank * CAR_MAX_BLOCKS + b, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t < world && t != rank) {
+    const uint32_t* f = p.sig[rank] + ph + t * CAR_MAX_BLOCKS + b;
+    uint32_t spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 24)) {
+        atomicAdd(timeouts, 1u);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __threadfence_system();
+}
+
+template <typename T>
+__global__ void __launch_bounds__(CAR_THREADS) car2_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                           int64_t nbytes, int64_t shard, int64_t slot_bytes,
+                                                           CarPtrs p, int rank, int world,
+                                                           uint32_t* __restrict__ gens) {
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;
+  const uint32_t gen = gens[b] + 1;
+  const int64_t slot_off = (gen & 1) * slot_bytes;
+  const int64_t cbase = static_cast<int64_t>(b) * CAR_CHUNK;
+  uint8_t* mine = p.data[rank] + slot_off;
+  // 1. stage chunk b of every shard (loads first, then stores: W*4 x 16 B in flight)
+  for (int s = 0; s < world; ++s) {
+    uint4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t o = cbase + (static_cast<int64_t>(i) * CAR_THREADS + t) * 16;
+      const int64_t g = s * shard + o;
+      if (o < shard && g < nbytes) v[i] = ld16(in + g);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t o = cbase + (static_cast<int64_t>(i) * CAR_THREADS + t) * 16;
+      const int64_t g = s * shard + o;
+      if (o < shard && g < nbytes) st16(mine + g, v[i]);
+    }
+  }
+  car_signal_wait<T>(p, 0, rank, world, b, gen, gens + CAR_MAX_BLOCKS);
+  // 2. reduce my shard's chunk b in rank order
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t o = cbase + (static_cast<int64_t>(i) * CAR_THREADS + t) * 16;
+    const int64_t g = rank * shard + o;
+    if (o >= shard || g >= nbytes) continue;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < world; ++r) acc8<T>(a, ld16_nt(p.data[r] + slot_off + g));
+    const uint4 y = pack8(a);
+    st16(out + g, y);
+    st16(mine + g, y);
+  }
+  car_signal_wait<T>(p, 1, rank, world, b, gen, gens + CAR_MAX_BLOCKS);
+  // 3. gather every other shard's chunk b from its owner
+  for (int s = 0; s < world; ++s) {
+    if (s == rank) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t o = cbase + (static_cast<int64_t>(i) * CAR_THREADS + t) * 16;
+      const int64_t g = s * shard + o;
+      if (o < shard && g < nbytes) st16(out + g, ld16_nt(p.data[s] + slot_off + g));
+    }
+  }
+  if (t == 0) gens[b] = gen;
+}
+
 int car_max_blocks() { return CAR_MAX_BLOCKS; }
 int car_chunk() { return CAR_CHUNK; }
 int car_max_ranks() { return CAR_MAX_RANKS; }
@@ -125,6 +214,25 @@ int custom_allreduce(const void* in, void* out, int64_t nbytes, int64_t slot_byt
   hipLaunchKernelGGL(car_kernel<uint16_t>, dim3(static_cast<unsigned>(blocks)), dim3(CAR_THREADS), 0, st,
                      static_cast<const uint8_t*>(in), static_cast<uint8_t*>(out), nbytes, slot_bytes, p, rank, world,
                      gens);
+  return 0;
+}
+
+// Two-shot: the signal arrays passed here hold 2 phases x [CAR_MAX_RANKS][CAR_MAX_BLOCKS].
+int custom_allreduce_2shot(const void* in, void* out, int64_t nbytes, int64_t slot_bytes, const uintptr_t* data_ptrs,
+                           const uintptr_t* sig_ptrs, int rank, int world, uint32_t* gens, hipStream_t st) {
+  if (world < 2 || world > CAR_MAX_RANKS || rank < 0 || rank >= world) return 1;
+  if (nbytes <= 0 || nbytes % 16 || nbytes > slot_bytes) return 1;
+  const int64_t shard = ((nbytes + world - 1) / world + 15) / 16 * 16;
+  const int64_t blocks = (shard + CAR_CHUNK - 1) / CAR_CHUNK;
+  if (blocks > CAR_MAX_BLOCKS) return 1;
+  CarPtrs p{};
+  for (int r = 0; r < world; ++r) {
+    p.data[r] = reinterpret_cast<uint8_t*>(data_ptrs[r]);
+    p.sig[r] = reinterpret_cast<uint32_t*>(sig_ptrs[r]);
+  }
+  hipLaunchKernelGGL(car2_kernel<uint16_t>, dim3(static_cast<unsigned>(blocks)), dim3(CAR_THREADS), 0, st,
+                     static_cast<const uint8_t*>(in), static_cast<uint8_t*>(out), nbytes, shard, slot_bytes, p, rank,
+                     world, gens);
   return 0;
 }
 

@@ -47,6 +47,8 @@ int moe_gemm_m64(const uint16_t*, const int32_t*, const int32_t*, int, int, cons
                  uint16_t*, int, int, int, hipStream_t);
 int custom_allreduce(const void*, void*, int64_t, int64_t, const uintptr_t*, const uintptr_t*, int, int, uint32_t*,
                      hipStream_t);
+int custom_allreduce_2shot(const void*, void*, int64_t, int64_t, const uintptr_t*, const uintptr_t*, int, int,
+                           uint32_t*, hipStream_t);
 int car_max_blocks();
 int car_chunk();
 int car_max_ranks();
@@ -249,6 +251,14 @@ PYBIND11_MODULE(_kernels, m) {
     check(xgk::custom_allreduce(P<void>(in), P<void>(out), nbytes, slot_bytes, data.data(), sig.data(), rank,
                                 static_cast<int>(data.size()), P<uint32_t>(gens), S(st)),
           "custom_allreduce");
+  });
+  m.def("custom_allreduce_2shot", [](uintptr_t in, uintptr_t out, int64_t nbytes, int64_t slot_bytes,
+                                     std::vector<uintptr_t> data, std::vector<uintptr_t> sig, int rank,
+                                     uintptr_t gens, uintptr_t st) {
+    if (data.size() != sig.size()) throw std::invalid_argument("custom_allreduce_2shot: pointer lists differ");
+    check(xgk::custom_allreduce_2shot(P<void>(in), P<void>(out), nbytes, slot_bytes, data.data(), sig.data(), rank,
+                                      static_cast<int>(data.size()), P<uint32_t>(gens), S(st)),
+          "custom_allreduce_2shot");
   });
 
   m.def("gemm_m64", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,

@@ -16,16 +16,16 @@ def _port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, two_shot_min=None):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
     import torch.distributed as dist
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
         from xgserve.parallel.custom_ar import CustomAllReduce
-        ar = CustomAllReduce(rank, world, torch.device("cuda:0"))
+        ar = CustomAllReduce(rank, world, torch.device("cuda:0"), two_shot_min=two_shot_min)
         errs = []
-        for n in (8, 512, 4096, 8192, 65536, 1 << 20, 2 << 20):  # elements (bf16)
+        for n in (8, 512, 4096, 8192, 24584, 65536, 1 << 20, 2 << 20, 6 << 20):  # elements (bf16)
             for it in range(3):
                 g = torch.Generator().manual_seed(1000 * it + n)
                 xs = [torch.randn(n, generator=g).bfloat16() for _ in range(world)]
@@ -61,12 +61,15 @@ def _worker(rank, world, port, q):
         q.put((rank, [repr(e)], -1))
 
 
-def test_custom_allreduce_two_ranks_one_gpu():
+@pytest.mark.parametrize("world,two_shot_min", [(2, None), (2, 0), (4, None), (4, 0)])
+def test_custom_allreduce_one_gpu(world, two_shot_min):
+    """world ranks share the GPU; two_shot_min=0 forces the two-shot kernel for
+    every size, None is the production choice (one-shot small, two-shot large at 4 ranks)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, two_shot_min)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=240) for _ in ps]

@@ -228,7 +228,7 @@ def test_hot_reload_config():
 
 
 def test_model_hot_swap_drains_old():
-    """Properties 28/29: in-flight requests finish on the old model; new ones see the new model."""
+    """Property 28: in-flight requests finish on the old model; new ones see the new model."""
     cfg = mock_config(worker={"mock_latency_ms": 5.0})
 
     async def fn(c, srv):
@@ -252,6 +252,7 @@ def test_model_hot_swap_drains_old():
 
 
 def test_hot_swap_failure_keeps_old_model():
+    """Property 29: a failed swap leaves the original model serving without interruption."""
     async def fn(c, srv):
         r = await c.post("/admin/model", data=json.dumps({"model": "no-such-model", "mock": False}))
         assert r.status in (400, 500)
