@@ -137,6 +137,8 @@ class LLMEngine:
         self.slot_ngen = np.zeros(ns, np.int64)  # tokens generated by the slot's owner (sampling counter)
         self._deferred = None  # (plan, toks, lps, counts, fin_map) awaiting detokenisation
         self._timing = None
+        self._tprof = None  # torch.profiler state (XGS_TORCH_PROFILE)
+        self._tprof_left = 0
         self._seq_counter = itertools.count(1)
         self._lock = threading.Lock()
         self._pending_aborts: List[str] = []
@@ -266,7 +268,38 @@ class LLMEngine:
             seeds = x.view(np.int64)
         return SamplingRows(temps, self.slot_topp[slots], self.slot_topk[slots], seeds)
 
+    def _torch_profile_tick(self) -> None:
+        """XGS_TORCH_PROFILE=N: record the next N steps with torch.profiler (CPU +
+        HIP activity via roctracer) and write a Chrome trace to
+        $XGS_TORCH_PROFILE_DIR (default ./gpurun_out) when done."""
+        prof = self._tprof
+        if prof is None:
+            n = int(os.environ.get("XGS_TORCH_PROFILE", "0") or 0)
+            if n <= 0:
+                self._tprof = False
+                return
+            acts = [torch.profiler.ProfilerActivity.CPU]
+            if self.device.type == "cuda":
+                acts.append(torch.profiler.ProfilerActivity.CUDA)
+            prof = torch.profiler.profile(activities=acts, record_shapes=False)
+            prof.__enter__()
+            self._tprof, self._tprof_left = prof, n
+            return
+        if prof is False:
+            return
+        self._tprof_left -= 1
+        if self._tprof_left <= 0:
+            prof.__exit__(None, None, None)
+            out = os.environ.get("XGS_TORCH_PROFILE_DIR", "gpurun_out")
+            os.makedirs(out, exist_ok=True)
+            path = os.path.join(out, f"torch_trace_rank{get_state().rank}_{os.getpid()}.json")
+            prof.export_chrome_trace(path)
+            log.info("torch.profiler trace written to %s", path)
+            self._tprof = False
+
     def step(self) -> List[RequestOutput]:
+        if self._tprof is not False:
+            self._torch_profile_tick()
         if self._timing is None:
             return self._step()
         t0 = time.perf_counter()

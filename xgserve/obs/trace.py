@@ -6,7 +6,7 @@ stream). Finished spans go to an in-memory ring (served at /debug/traces) and,
 when XGS_TRACE_FILE is set, are appended as JSON lines -- the OpenTelemetry
 span shape (trace_id, span_id, parent_span_id, name, start/end ns, attributes)
 so an OTel collector can ingest the file. Kernel-level profiling is
-rocprofv3 (see bench/profile.sh); `XGS_TORCH_PROFILE=N` wraps N engine steps in
+rocprofv3 (bench/profile.sh: kernel table + step-gap analysis); `XGS_TORCH_PROFILE=N` wraps N engine steps in
 torch.profiler.
 """
 from __future__ import annotations
