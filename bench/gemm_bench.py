@@ -17,7 +17,11 @@ from xgserve.ops import linear as L  # noqa: E402
 from xgserve.ops._native import kernels  # noqa: E402
 
 SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
-          "lm_head": (128256, 4096)}
+          "lm_head": (128256, 4096),
+          # Llama-3-70B (TP1 / TP8) and Llama-3-8B TP2 shards
+          "qkv70": (10240, 8192), "o70": (8192, 8192), "gate_up70": (57344, 8192), "down70": (8192, 28672),
+          "qkv70t8": (1280, 8192), "o70t8": (8192, 1024), "gate_up70t8": (7168, 8192), "down70t8": (8192, 3584),
+          "qkv8t2": (3072, 4096), "o8t2": (4096, 2048), "gate_up8t2": (14336, 4096), "down8t2": (4096, 7168)}
 
 
 def timeit(fns, iters=30, warm=5):
@@ -39,8 +43,12 @@ def main():
     ap.add_argument("--M", type=int, nargs="+", default=[32, 64])
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
     ap.add_argument("--variants", type=int, nargs="+", default=[2, 4])
+    ap.add_argument("--m64g-sweep", action="store_true",
+                    help="sweep gemm_m64g (nw, split, cfg) configurations instead of the shoot-out")
     a = ap.parse_args()
     kernels()
+    if a.m64g_sweep:
+        return m64g_sweep(a)
     dev = "cuda"
     for name in a.shapes:
         N, K = SHAPES[name]
@@ -53,7 +61,7 @@ def main():
             rows = []
             us = timeit([lambda w=w: F.linear(x, w) for w in ws])
             rows.append(("hipblaslt", us, None))
-            mode = L.MODE_SILU if name == "gate_up" else (L.MODE_BF16 if name == "lm_head" else L.MODE_PARTIAL)
+            mode = L.MODE_SILU if name.startswith("gate_up") else (L.MODE_BF16 if name == "lm_head" else L.MODE_PARTIAL)
             if M <= 16:
                 for S in ((1,) if mode != L.MODE_PARTIAL else (1, 2, 4, 7, 8, 14, 16)):
                     if K % (S * 256) or (mode == L.MODE_PARTIAL and N % 64):
@@ -88,6 +96,54 @@ def main():
             for op, t, err in rows:
                 print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "op": op, "us": round(t, 2),
                                   "TB/s": round(nbytes / t / 1e6, 3), "rel_err": err}), flush=True)
+        del ws
+        torch.cuda.empty_cache()
+
+
+def m64g_sweep(a):
+    """Every valid gemm_m64g configuration per shape (cold weights); prints the
+    checked-correct ones, fastest first."""
+    k = kernels()
+    waves = {c: (2 if c >= 4 else 4) for c in range(7)}
+    kcs = {c: (64 if c in (2, 3, 4, 5) else 128) for c in range(7)}
+    for name in a.shapes:
+        N, K = SHAPES[name]
+        nbytes = N * K * 2
+        copies = max(2, min(8, (1 << 30) // nbytes + 1))
+        ws = [(torch.randn(N, K, device="cuda") * 0.02).bfloat16() for _ in range(copies)]
+        mode = L.MODE_SILU if name.startswith("gate_up") else (L.MODE_BF16 if name == "lm_head" else L.MODE_PARTIAL)
+        for M in a.M:
+            x = torch.randn(M, K, device="cuda").bfloat16()
+            if mode == L.MODE_SILU:
+                g, u = L.deinterleave_gate_up(ws[0])
+                want = F.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
+            else:
+                want = x.float() @ ws[0].float().t()
+            rows = []
+            for cfg in range(7):
+                for nw in ((2,) if mode == L.MODE_SILU else (1, 2)):
+                    for S in ((1,) if mode != L.MODE_PARTIAL else (1, 2, 4, 8)):
+                        cols = 16 * nw * waves[cfg]
+                        if N % cols or K % (S * kcs[cfg]):
+                            continue
+                        part = torch.empty(S, M, N, dtype=torch.float32, device="cuda")
+                        out = torch.empty(M, N // 2 if mode == L.MODE_SILU else N, dtype=torch.bfloat16,
+                                          device="cuda")
+
+                        def fn(w, nw=nw, S=S, cfg=cfg, part=part, out=out):
+                            k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N,
+                                        part.data_ptr() if mode == L.MODE_PARTIAL else 0,
+                                        out.data_ptr() if mode != L.MODE_PARTIAL else 0, S, mode, nw, cfg,
+                                        torch.cuda.current_stream().cuda_stream)
+                        us = timeit([lambda w=w, fn=fn: fn(w) for w in ws])
+                        fn(ws[0])
+                        y = part.sum(0) if mode == L.MODE_PARTIAL else out.float()
+                        err = float((y - want).norm() / want.norm())
+                        rows.append((us, nw, S, cfg, err))
+            for us, nw, S, cfg, err in sorted(rows):
+                print(json.dumps({"shape": name, "M": M, "op": f"m64g(nw={nw},S={S},cfg={cfg})", "us": round(us, 2),
+                                  "TB/s": round(nbytes / us / 1e6, 3), "wgs": N // (16 * nw * waves[cfg]) * S,
+                                  "rel_err": round(err, 6)}), flush=True)
         del ws
         torch.cuda.empty_cache()
 

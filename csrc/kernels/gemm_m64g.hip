@@ -45,6 +45,20 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
 #endif
 }
 
+__device__ __forceinline__ void glds16_nt(const void* src, void* lds_base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)(lds_base))));
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off nt"
+      :
+      : "v"(src), "s"(lds)
+      : "memory", "m0");
+#endif
+}
+
 // s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14; expcnt, lgkmcnt left at max)
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -61,20 +75,29 @@ __device__ __forceinline__ void raw_barrier() {
 
 enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2 };
 
-template <int NW>
-__global__ void __launch_bounds__(256, 1) gemm_m64g_kernel(const uint16_t* __restrict__ x, int M, int K,
-                                                           const uint16_t* __restrict__ w, int N,
-                                                           float* __restrict__ part, uint16_t* __restrict__ out,
-                                                           int mode) {
+// Dense kernel, parametrised for the decode shapes (bench/gemm_bench.py picks):
+//   NW  16-column MFMA tiles per wave (2 = 32 columns; required by the SiLU epilogue)
+//   WV  waves per workgroup (4 or 2): fewer waves = more, smaller workgroups, so a
+//       short N still puts a workgroup on every CU
+//   KC  k per chunk (128: 256-B rows, 1 workgroup/CU; 64: 128-B rows, 2-3 per CU)
+//   NT  non-temporal weight DMA (streamed once; keeps x resident in L2)
+template <int NW, int WV, int KC, bool NT>
+__global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* __restrict__ x, int M, int K,
+                                                               const uint16_t* __restrict__ w, int N,
+                                                               float* __restrict__ part, uint16_t* __restrict__ out,
+                                                               int mode) {
   constexpr int MT = 4;
+  constexpr int RB = KC * 2;                     // bytes per LDS row
+  constexpr int GPR = KC / 8;                    // 16-B granules per row
+  constexpr int RPI = 1024 / RB;                 // rows per DMA instruction (64 lanes x 16 B)
+  constexpr int XBYTES = 64 * RB;
+  constexpr int XI = 64 / RPI / WV;              // x DMA instructions per wave per chunk
   constexpr int WROWS = 16 * NW;                 // weight rows per wave
-  constexpr int WBYTES = WROWS * 256;            // per wave per slot
-  constexpr int SLOT = GG_XBYTES + 4 * WBYTES;   // bytes per slot
-  constexpr int G = NW * 4 + 4;                  // DMA instructions per wave per chunk
-  // one __shared__ object per slot, every slot index a compile-time constant: the
-  // compiler then proves a fragment read of slot A cannot alias the DMAs still in
-  // flight into slots B / C and keeps them in flight (with one runtime-indexed
-  // array it waits vmcnt(0) before every read)
+  constexpr int WI = WROWS / RPI;                // weight DMA instructions per wave per chunk
+  constexpr int WBYTES = WROWS * RB;             // per wave per slot
+  constexpr int SLOT = XBYTES + WV * WBYTES;
+  constexpr int G = XI + WI;
+  static_assert(XI >= 1 && WI >= 1 && 64 % (RPI * WV) == 0, "bad m64g geometry");
   __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
@@ -84,30 +107,32 @@ __global__ void __launch_bounds__(256, 1) gemm_m64g_kernel(const uint16_t* __res
   const int S = gridDim.y, s = blockIdx.y;
   const int kws = K / S;
   const int k0 = s * kws;
-  const int nchunks = kws / GG_KC;
-  const int nbase = blockIdx.x * (64 * NW) + wid * WROWS;
+  const int nchunks = kws / KC;
+  const int nbase = blockIdx.x * (16 * NW * WV) + wid * WROWS;
 
-  // DMA source rows / granules for this lane (fixed over the k loop)
-  const int dr = lane >> 4, dj = lane & 15;      // row within a 4-row instruction, granule
-  const uint16_t* wsrc[NW * 4];
+  const int dr = lane / GPR, dj = lane % GPR;    // row within a DMA instruction, granule
+  const uint16_t* wsrc[WI];
 #pragma unroll
-  for (int i = 0; i < NW * 4; ++i) {
-    const int r = 4 * i + dr;                    // local weight row 0..WROWS-1
-    wsrc[i] = w + static_cast<int64_t>(nbase + r) * K + k0 + 8 * (dj ^ (r & 15));
+  for (int i = 0; i < WI; ++i) {
+    const int r = RPI * i + dr;
+    wsrc[i] = w + static_cast<int64_t>(nbase + r) * K + k0 + 8 * (dj ^ (r & (GPR - 1)));
   }
-  const uint16_t* xsrc[4];
+  const uint16_t* xsrc[XI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = 16 * wid + 4 * i + dr;         // x row 0..63
-    xsrc[i] = x + static_cast<int64_t>(min(r, M - 1)) * K + k0 + 8 * (dj ^ (r & 15));
+  for (int i = 0; i < XI; ++i) {
+    const int r = RPI * (wid * XI + i) + dr;     // x row 0..63
+    xsrc[i] = x + static_cast<int64_t>(min(r, M - 1)) * K + k0 + 8 * (dj ^ (r & (GPR - 1)));
   }
 
   auto issue = [&](uint8_t* slot, int c) {
-    const int kk = c * GG_KC;
+    const int kk = c * KC;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kk, slot + (16 * wid + 4 * i) * 256);
+    for (int i = 0; i < XI; ++i) glds16(xsrc[i] + kk, slot + RPI * (wid * XI + i) * RB);
 #pragma unroll
-    for (int i = 0; i < NW * 4; ++i) glds16(wsrc[i] + kk, slot + GG_XBYTES + wid * WBYTES + i * 1024);
+    for (int i = 0; i < WI; ++i) {
+      if constexpr (NT) glds16_nt(wsrc[i] + kk, slot + XBYTES + wid * WBYTES + i * 1024);
+      else glds16(wsrc[i] + kk, slot + XBYTES + wid * WBYTES + i * 1024);
+    }
   };
 
   f32x4_t acc[NW][MT];
@@ -118,15 +143,15 @@ __global__ void __launch_bounds__(256, 1) gemm_m64g_kernel(const uint16_t* __res
 
   auto compute = [&](const uint8_t* slot) {
     const uint8_t* xs = slot;
-    const uint8_t* ws = slot + GG_XBYTES + wid * WBYTES;
+    const uint8_t* ws = slot + XBYTES + wid * WBYTES;
 #pragma unroll
-    for (int t = 0; t < GG_KC / 32; ++t) {
-      const int phys = (4 * t + g) ^ li;    // swizzled granule of (row with row&15 == li, logical granule 4t+g)
+    for (int t = 0; t < KC / 32; ++t) {
+      const int phys = (4 * t + g) ^ (li & (GPR - 1));
       uint4 b[MT], a[NW];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) b[mt] = *reinterpret_cast<const uint4*>(xs + (16 * mt + li) * 256 + phys * 16);
+      for (int mt = 0; mt < MT; ++mt) b[mt] = *reinterpret_cast<const uint4*>(xs + (16 * mt + li) * RB + phys * 16);
 #pragma unroll
-      for (int nt = 0; nt < NW; ++nt) a[nt] = *reinterpret_cast<const uint4*>(ws + (16 * nt + li) * 256 + phys * 16);
+      for (int nt = 0; nt < NW; ++nt) a[nt] = *reinterpret_cast<const uint4*>(ws + (16 * nt + li) * RB + phys * 16);
 #pragma unroll
       for (int nt = 0; nt < NW; ++nt)
 #pragma unroll
@@ -360,18 +385,37 @@ int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, i
   return 0;
 }
 
+// cfg: 0 = (4 waves, KC 128), 1 = (4, 128, nt), 2 = (4, 64), 3 = (4, 64, nt),
+//      4 = (2, 64), 5 = (2, 64, nt), 6 = (2, 128, nt)
+template <int NW>
+static void launch_m64g(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N,
+                        float* part, uint16_t* out, int mode) {
+  switch (cfg) {
+    case 1: hipLaunchKernelGGL((gemm_m64g_kernel<NW, 4, 128, true>), grid, dim3(256), 0, st, x, M, K, w, N, part, out, mode); break;
+    case 2: hipLaunchKernelGGL((gemm_m64g_kernel<NW, 4, 64, false>), grid, dim3(256), 0, st, x, M, K, w, N, part, out, mode); break;
+    case 3: hipLaunchKernelGGL((gemm_m64g_kernel<NW, 4, 64, true>), grid, dim3(256), 0, st, x, M, K, w, N, part, out, mode); break;
+    case 4: hipLaunchKernelGGL((gemm_m64g_kernel<NW, 2, 64, false>), grid, dim3(128), 0, st, x, M, K, w, N, part, out, mode); break;
+    case 5: hipLaunchKernelGGL((gemm_m64g_kernel<NW, 2, 64, true>), grid, dim3(128), 0, st, x, M, K, w, N, part, out, mode); break;
+    case 6: hipLaunchKernelGGL((gemm_m64g_kernel<NW, 2, 128, true>), grid, dim3(128), 0, st, x, M, K, w, N, part, out, mode); break;
+    default: hipLaunchKernelGGL((gemm_m64g_kernel<NW, 4, 128, false>), grid, dim3(256), 0, st, x, M, K, w, N, part, out, mode); break;
+  }
+}
+
+int m64g_cfg_waves(int cfg) { return cfg >= 4 ? 2 : 4; }
+int m64g_cfg_kc(int cfg) { return (cfg == 2 || cfg == 3 || cfg == 4 || cfg == 5) ? 64 : 128; }
+
 int gemm_m64g(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
-              int nw, hipStream_t st) {
-  if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2)) return 1;
-  if (K % (S * GG_KC) || N % (64 * nw)) return 1;
+              int nw, int cfg, hipStream_t st) {
+  if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 6) return 1;
+  const int wv = m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
+  const int cols = 16 * nw * wv;
+  if (K % (S * kc) || N % cols) return 1;
   if (mode == GG_SILU && (nw != 2 || S != 1)) return 1;
   if (mode == GG_PARTIAL && part == nullptr) return 1;
   if (mode != GG_PARTIAL && out == nullptr) return 1;
-  const dim3 grid(N / (64 * nw), S);
-  if (nw == 1)
-    hipLaunchKernelGGL(gemm_m64g_kernel<1>, grid, dim3(256), 0, st, x, M, K, w, N, part, out, mode);
-  else
-    hipLaunchKernelGGL(gemm_m64g_kernel<2>, grid, dim3(256), 0, st, x, M, K, w, N, part, out, mode);
+  const dim3 grid(N / cols, S);
+  if (nw == 1) launch_m64g<1>(cfg, grid, st, x, M, K, w, N, part, out, mode);
+  else launch_m64g<2>(cfg, grid, st, x, M, K, w, N, part, out, mode);
   return 0;
 }
 

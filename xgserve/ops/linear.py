@@ -89,23 +89,67 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, split_k: Optional[int] = Non
     return out
 
 
+# gemm_m64g launch configurations (csrc/kernels/gemm_m64g.hip launch_m64g):
+# cfg -> (waves per workgroup, k chunk, non-temporal weight DMA)
+M64G_CFGS = {0: (4, 128, False), 1: (4, 128, True), 2: (4, 64, False), 3: (4, 64, True),
+             4: (2, 64, False), 5: (2, 64, True), 6: (2, 128, True)}
+
+# Measured on MI355X with cold weights (bench/gemm_bench.py --m64g-sweep,
+# profiles/r1_m64g_sweep.jsonl): (N, K, mode) -> {M bucket: (nw, split_k, cfg)}.
+# Bucket 64 serves 40 < M <= 64, bucket 32 serves 16 < M <= 40 (falls back to 64).
+_M64_TUNED = {
+    # Llama-3-8B / Mixtral attention, TP1
+    (6144, 4096, MODE_PARTIAL): {64: (2, 4, 3), 32: (2, 8, 5)},
+    (4096, 4096, MODE_PARTIAL): {64: (1, 4, 0), 32: (1, 4, 0)},
+    (28672, 4096, MODE_SILU): {64: (2, 1, 1), 32: (2, 1, 5)},
+    (4096, 14336, MODE_PARTIAL): {64: (2, 8, 3), 32: (1, 4, 1)},
+    # Llama-3-8B TP2 shards
+    (3072, 4096, MODE_PARTIAL): {64: (1, 8, 2)},
+    (4096, 2048, MODE_PARTIAL): {64: (1, 4, 5)},
+    (14336, 4096, MODE_SILU): {64: (2, 1, 6)},
+    (4096, 7168, MODE_PARTIAL): {64: (2, 8, 3)},
+    # Llama-3-70B TP1
+    (10240, 8192, MODE_PARTIAL): {64: (2, 2, 1)},
+    (8192, 8192, MODE_PARTIAL): {64: (2, 8, 3)},
+    (57344, 8192, MODE_SILU): {64: (2, 1, 3)},
+    (8192, 28672, MODE_PARTIAL): {64: (2, 4, 3)},
+    # Llama-3-70B TP8 shards
+    (1280, 8192, MODE_PARTIAL): {64: (1, 8, 0)},
+    (8192, 1024, MODE_PARTIAL): {64: (2, 4, 2)},
+    (7168, 8192, MODE_SILU): {64: (2, 1, 6)},
+    (8192, 3584, MODE_PARTIAL): {64: (1, 2, 1)},
+}
+
+
+def _m64_valid(N: int, K: int, mode: int, nw: int, S: int, cfg: int) -> bool:
+    wv, kc, _ = M64G_CFGS[cfg]
+    if N % (16 * nw * wv) or K % (S * kc):
+        return False
+    return not (mode == MODE_SILU and (nw != 2 or S != 1)) and not (mode == MODE_BF16 and S != 1)
+
+
 def m64_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL):
-    """(nw, split_k) for gemm_m64 / gemm_m64g, or None if unsupported. Measured on
-    MI355X (bench/gemm_bench.py, profiles/r1_gemm_*): split-K 4 whenever K allows
-    (the partials are reduced by the consumer kernel for free), 128-column tiles
-    once they give >= 192 workgroups, else 64; bf16 / SiLU epilogues need split 1."""
+    """(nw, split_k, cfg) for gemm_m64g, or None if unsupported. Measured shapes come
+    from _M64_TUNED; otherwise split-K 4 whenever K allows (the partials are reduced
+    by the consumer kernel for free), 128-column tiles once they give >= 192
+    workgroups, else 64; bf16 / SiLU epilogues need split 1 (SiLU: nt weight DMA)."""
     if not (16 < M <= 64) or K % 256:
         return None
+    t = _M64_TUNED.get((N, K, mode))
+    if t is not None:
+        p = t.get(32) if (M <= 40 and 32 in t) else t.get(64)
+        if p is not None and _m64_valid(N, K, mode, *p):
+            return p
     if mode == MODE_SILU:
-        return (2, 1) if N % 128 == 0 else None
+        return (2, 1, 1) if N % 128 == 0 else None
     if mode == MODE_BF16:
         nw = 2 if N % 128 == 0 else 1
-        return (nw, 1) if N % (64 * nw) == 0 else None
+        return (nw, 1, 0) if N % (64 * nw) == 0 else None
     S = next(s for s in (4, 2, 1) if K % (s * 256) == 0)
     nw = 2 if (N % 128 == 0 and (N // 128) * S >= 192) else 1
     if N % (64 * nw):
         return None
-    return nw, S
+    return nw, S, 0
 
 
 # 4: LDS-DMA staging (gemm_m64g.hip, fastest on every measured shape); 0-3: register-ring gemm_m64
@@ -114,7 +158,8 @@ M64_VARIANT = 4
 
 
 def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split_k: Optional[int] = None,
-               nw: Optional[int] = None, out: Optional[torch.Tensor] = None, variant: Optional[int] = None):
+               nw: Optional[int] = None, out: Optional[torch.Tensor] = None, variant: Optional[int] = None,
+               cfg: Optional[int] = None):
     """gemm_m64 (csrc/kernels/gemm_m64.hip) for 16 < M <= 64: bf16 [M, N], PendingSum
     (MODE_PARTIAL) or silu(gate)*up [M, N/2] (MODE_SILU, interleaved gate|up weight)."""
     M, K = x.shape
@@ -122,14 +167,21 @@ def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split
     plan = m64_plan(M, N, K, mode)
     if plan is None:
         raise ValueError(f"gemm_m64: unsupported shape M={M} N={N} K={K} mode={mode}")
-    nw = nw or plan[0]
-    S = split_k or plan[1]
+    if nw is None and split_k is None and cfg is None:
+        nw, S, cfg = plan
+    else:
+        nw = nw or plan[0]
+        S = split_k or plan[1]
+        cfg = plan[2] if cfg is None else cfg
+        if not _m64_valid(N, K, mode, nw, S, cfg):
+            cfg = 0
     var = M64_VARIANT if variant is None else variant
     k = kernels()
     if mode == MODE_PARTIAL:
         part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
         if var == 4:  # LDS-DMA staging (gemm_m64g.hip)
-            k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, stream_ptr())
+            k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg,
+                        stream_ptr())
         else:
             k.gemm_m64(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, var, stream_ptr())
         return PendingSum(part, S)
@@ -137,7 +189,7 @@ def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split
     if out is None:
         out = torch.empty(M, ncol, dtype=torch.bfloat16, device=x.device)
     if var == 4:
-        k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, stream_ptr())
+        k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, cfg, stream_ptr())
     else:
         k.gemm_m64(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, var, stream_ptr())
     return out
