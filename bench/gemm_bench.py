@@ -43,12 +43,16 @@ def main():
     ap.add_argument("--M", type=int, nargs="+", default=[32, 64])
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
     ap.add_argument("--variants", type=int, nargs="+", default=[2, 4])
+    ap.add_argument("--moe-sweep", action="store_true",
+                    help="sweep the grouped (MoE) gemm_m64g configurations at Mixtral decode shapes")
     ap.add_argument("--m64g-sweep", action="store_true",
                     help="sweep gemm_m64g (nw, split, cfg) configurations instead of the shoot-out")
     a = ap.parse_args()
     kernels()
     if a.m64g_sweep:
         return m64g_sweep(a)
+    if a.moe_sweep:
+        return moe_sweep(a)
     dev = "cuda"
     for name in a.shapes:
         N, K = SHAPES[name]
@@ -146,6 +150,49 @@ def m64g_sweep(a):
                                   "rel_err": round(err, 6)}), flush=True)
         del ws
         torch.cuda.empty_cache()
+
+
+def moe_sweep(a):
+    """Mixtral-8x7B expert GEMMs at decode batch sizes a.M (top-2 of 8, random routing),
+    every grouped gemm_m64g configuration, cold weights (2 copies of all experts)."""
+    from xgserve.ops import moe as MO
+    k = kernels()
+    E, H, F = 8, 4096, 14336
+    copies = 2
+    w13s = [(torch.randn(E, 2 * F, H, device="cuda") * 0.02).bfloat16() for _ in range(copies)]
+    w2s = [(torch.randn(E, H, F, device="cuda") * 0.02).bfloat16() for _ in range(copies)]
+    st = torch.cuda.current_stream().cuda_stream
+    for T in a.M:
+        g = torch.Generator(device="cuda").manual_seed(T)
+        ids = torch.stack([torch.randperm(E, generator=g, device="cuda")[:2] for _ in range(T)]).int()
+        x = torch.randn(T, H, device="cuda").bfloat16()
+        rows, offs, dest = MO.moe_align(ids, E, 0)
+        P = rows.shape[0]
+        act = torch.empty(P, F, dtype=torch.bfloat16, device="cuda")
+        res = []
+        for cfg in range(7):
+            wv = 2 if cfg >= 4 else 4
+            if (2 * F) % (32 * wv):
+                continue
+            fn = lambda w, cfg=cfg: k.moe_gemm_m64g(x.data_ptr(), rows.data_ptr(), offs.data_ptr(), E, H, w.data_ptr(),
+                                                     2 * F, P, 0, act.data_ptr(), 1, 2, 2, cfg, st)  # noqa: E731
+            res.append(("w13", timeit([lambda w=w, fn=fn: fn(w) for w in w13s]), 2, 1, cfg))
+        for cfg in range(7):
+            wv = 2 if cfg >= 4 else 4
+            kc = 64 if cfg in (2, 3, 4, 5) else 128
+            for nw in (1, 2):
+                for S in (1, 2, 4, 8):
+                    if H % (16 * nw * wv) or F % (S * kc):
+                        continue
+                    part = torch.empty(S, P, H, dtype=torch.float32, device="cuda")
+                    fn = lambda w, cfg=cfg, nw=nw, S=S, part=part: k.moe_gemm_m64g(  # noqa: E731
+                        act.data_ptr(), 0, offs.data_ptr(), E, F, w.data_ptr(), H, P, part.data_ptr(), 0, S, 1, nw, cfg,
+                        st)
+                    res.append(("w2", timeit([lambda w=w, fn=fn: fn(w) for w in w2s]), nw, S, cfg))
+        for name in ("w13", "w2"):
+            for us, nw, S, cfg in sorted((r[1], r[2], r[3], r[4]) for r in res if r[0] == name)[:8]:
+                print(json.dumps({"moe": name, "T": T, "P": P, "nw": nw, "S": S, "cfg": cfg, "us": round(us, 2)}),
+                      flush=True)
 
 
 if __name__ == "__main__":

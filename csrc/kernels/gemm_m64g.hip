@@ -230,18 +230,25 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
 // rows == nullptr: x already in padded layout); offs[E+1] padded segment starts.
 // One workgroup per (column tile, k-split, expert) loops over the expert's
 // 64-row tiles (the same weight column tile is re-read from L2/MALL, not HBM).
-template <int NW>
-__global__ void __launch_bounds__(256, 1) gemm_m64g_grouped_kernel(const uint16_t* __restrict__ x,
-                                                                   const int32_t* __restrict__ rows,
-                                                                   const int32_t* __restrict__ offs, int K,
-                                                                   const uint16_t* __restrict__ w, int N, int P,
-                                                                   float* __restrict__ part,
-                                                                   uint16_t* __restrict__ out, int mode) {
+template <int NW, int WV, int KC, bool NT>
+__global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uint16_t* __restrict__ x,
+                                                                       const int32_t* __restrict__ rows,
+                                                                       const int32_t* __restrict__ offs, int K,
+                                                                       const uint16_t* __restrict__ w, int N, int P,
+                                                                       float* __restrict__ part,
+                                                                       uint16_t* __restrict__ out, int mode) {
   constexpr int MT = 4;
+  constexpr int RB = KC * 2;
+  constexpr int GPR = KC / 8;
+  constexpr int RPI = 1024 / RB;
+  constexpr int XBYTES = 64 * RB;
+  constexpr int XI = 64 / RPI / WV;
   constexpr int WROWS = 16 * NW;
-  constexpr int WBYTES = WROWS * 256;
-  constexpr int SLOT = GG_XBYTES + 4 * WBYTES;
-  constexpr int G = NW * 4 + 4;
+  constexpr int WI = WROWS / RPI;
+  constexpr int WBYTES = WROWS * RB;
+  constexpr int SLOT = XBYTES + WV * WBYTES;
+  constexpr int G = XI + WI;
+  static_assert(XI >= 1 && WI >= 1 && 64 % (RPI * WV) == 0, "bad m64g geometry");
   __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
@@ -254,57 +261,65 @@ __global__ void __launch_bounds__(256, 1) gemm_m64g_grouped_kernel(const uint16_
   const int S = gridDim.y, s = blockIdx.y;
   const int kws = K / S;
   const int k0 = s * kws;
-  const int nchunks = kws / GG_KC;
-  const int nbase = blockIdx.x * (64 * NW) + wid * WROWS;
-  const int dr = lane >> 4, dj = lane & 15;
+  const int nchunks = kws / KC;
+  const int nbase = blockIdx.x * (16 * NW * WV) + wid * WROWS;
+  const int dr = lane / GPR, dj = lane % GPR;
   const uint16_t* we = w + static_cast<int64_t>(e) * N * K;
-  const uint16_t* wsrc[NW * 4];
+  const uint16_t* wsrc[WI];
 #pragma unroll
-  for (int i = 0; i < NW * 4; ++i) {
-    const int r = 4 * i + dr;
-    wsrc[i] = we + static_cast<int64_t>(nbase + r) * K + k0 + 8 * (dj ^ (r & 15));
+  for (int i = 0; i < WI; ++i) {
+    const int r = RPI * i + dr;
+    wsrc[i] = we + static_cast<int64_t>(nbase + r) * K + k0 + 8 * (dj ^ (r & (GPR - 1)));
   }
+  // non-temporal weight loads only when each expert's column tile is read once
+  // (one 64-row tile); with several row tiles the re-reads should hit L2/MALL
+  const bool nt = NT && (p1 - p0) <= 64;
 
   for (int rt = p0; rt < p1; rt += 64) {
     if (rt != p0) raw_barrier();  // the previous tile's last slot may still be read
     const int first = rows ? rows[rt] : rt;
-    const uint16_t* xsrc[4];
+    const uint16_t* xsrc[XI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 16 * wid + 4 * i + dr;
+    for (int i = 0; i < XI; ++i) {
+      const int r = RPI * (wid * XI + i) + dr;
       int src = rows ? rows[rt + r] : rt + r;
       if (src < 0) src = first;
-      xsrc[i] = x + static_cast<int64_t>(src) * K + k0 + 8 * (dj ^ (r & 15));
+      xsrc[i] = x + static_cast<int64_t>(src) * K + k0 + 8 * (dj ^ (r & (GPR - 1)));
     }
     auto issue = [&](uint8_t* slot, int c) {
-      const int kk = c * GG_KC;
+      const int kk = c * KC;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kk, slot + (16 * wid + 4 * i) * 256);
+      for (int i = 0; i < XI; ++i) glds16(xsrc[i] + kk, slot + RPI * (wid * XI + i) * RB);
+      if (nt) {
 #pragma unroll
-      for (int i = 0; i < NW * 4; ++i) glds16(wsrc[i] + kk, slot + GG_XBYTES + wid * WBYTES + i * 1024);
+        for (int i = 0; i < WI; ++i) glds16_nt(wsrc[i] + kk, slot + XBYTES + wid * WBYTES + i * 1024);
+      } else {
+#pragma unroll
+        for (int i = 0; i < WI; ++i) glds16(wsrc[i] + kk, slot + XBYTES + wid * WBYTES + i * 1024);
+      }
     };
     f32x4_t acc[NW][MT];
 #pragma unroll
-    for (int nt = 0; nt < NW; ++nt)
+    for (int nt_ = 0; nt_ < NW; ++nt_)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int mt = 0; mt < MT; ++mt) acc[nt_][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     auto compute = [&](const uint8_t* slot) {
       const uint8_t* xs = slot;
-      const uint8_t* ws = slot + GG_XBYTES + wid * WBYTES;
+      const uint8_t* ws = slot + XBYTES + wid * WBYTES;
 #pragma unroll
-      for (int t = 0; t < GG_KC / 32; ++t) {
-        const int phys = (4 * t + g) ^ li;
+      for (int t = 0; t < KC / 32; ++t) {
+        const int phys = (4 * t + g) ^ (li & (GPR - 1));
         uint4 b[MT], a[NW];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
-          b[mt] = *reinterpret_cast<const uint4*>(xs + (16 * mt + li) * 256 + phys * 16);
+          b[mt] = *reinterpret_cast<const uint4*>(xs + (16 * mt + li) * RB + phys * 16);
 #pragma unroll
-        for (int nt = 0; nt < NW; ++nt)
-          a[nt] = *reinterpret_cast<const uint4*>(ws + (16 * nt + li) * 256 + phys * 16);
+        for (int nt_ = 0; nt_ < NW; ++nt_)
+          a[nt_] = *reinterpret_cast<const uint4*>(ws + (16 * nt_ + li) * RB + phys * 16);
 #pragma unroll
-        for (int nt = 0; nt < NW; ++nt)
+        for (int nt_ = 0; nt_ < NW; ++nt_)
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = mfma16x16x32(as_frag(a[nt]), as_frag(b[mt]), acc[nt][mt]);
+          for (int mt = 0; mt < MT; ++mt) acc[nt_][mt] = mfma16x16x32(as_frag(a[nt_]), as_frag(b[mt]), acc[nt_][mt]);
       }
     };
     auto step = [&](uint8_t* cur, uint8_t* nxt2, int c) {
@@ -331,20 +346,20 @@ __global__ void __launch_bounds__(256, 1) gemm_m64g_grouped_kernel(const uint16_
       for (int mt = 0; mt < MT; ++mt) {
         const int m = rt + 16 * mt + li;
 #pragma unroll
-        for (int nt = 0; nt < NW; ++nt)
-          *reinterpret_cast<float4*>(pp + static_cast<int64_t>(m) * N + nbase + 16 * nt + 4 * g) =
-              make_float4(acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]);
+        for (int nt_ = 0; nt_ < NW; ++nt_)
+          *reinterpret_cast<float4*>(pp + static_cast<int64_t>(m) * N + nbase + 16 * nt_ + 4 * g) =
+              make_float4(acc[nt_][mt][0], acc[nt_][mt][1], acc[nt_][mt][2], acc[nt_][mt][3]);
       }
     } else if (mode == GG_BF16) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int m = rt + 16 * mt + li;
 #pragma unroll
-        for (int nt = 0; nt < NW; ++nt) {
+        for (int nt_ = 0; nt_ < NW; ++nt_) {
           uint2 v;
-          v.x = pack2(acc[nt][mt][0], acc[nt][mt][1]);
-          v.y = pack2(acc[nt][mt][2], acc[nt][mt][3]);
-          *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * N + nbase + 16 * nt + 4 * g) = v;
+          v.x = pack2(acc[nt_][mt][0], acc[nt_][mt][1]);
+          v.y = pack2(acc[nt_][mt][2], acc[nt_][mt][3]);
+          *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * N + nbase + 16 * nt_ + 4 * g) = v;
         }
       }
     } else if (NW == 2) {
@@ -367,21 +382,40 @@ __global__ void __launch_bounds__(256, 1) gemm_m64g_grouped_kernel(const uint16_
   }
 }
 
+template <int NW>
+static void launch_m64g_grouped(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, const int32_t* rows,
+                                const int32_t* offs, int K, const uint16_t* w, int N, int P, float* part,
+                                uint16_t* out, int mode) {
+#define XGK_GRP(WV, KC, NT)                                                                                    \
+  hipLaunchKernelGGL((gemm_m64g_grouped_kernel<NW, WV, KC, NT>), grid, dim3(64 * WV), 0, st, x, rows, offs, K, w, \
+                     N, P, part, out, mode)
+  switch (cfg) {
+    case 1: XGK_GRP(4, 128, true); break;
+    case 2: XGK_GRP(4, 64, false); break;
+    case 3: XGK_GRP(4, 64, true); break;
+    case 4: XGK_GRP(2, 64, false); break;
+    case 5: XGK_GRP(2, 64, true); break;
+    case 6: XGK_GRP(2, 128, true); break;
+    default: XGK_GRP(4, 128, false); break;
+  }
+#undef XGK_GRP
+}
+
+int m64g_cfg_waves(int cfg);
+int m64g_cfg_kc(int cfg);
+
 int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, int E, int K, const uint16_t* w, int N,
-                  int P, float* part, uint16_t* out, int S, int mode, int nw, hipStream_t st) {
-  if (E < 1 || P < 0 || P % 64 || S < 1 || (nw != 1 && nw != 2)) return 1;
-  if (K % (S * GG_KC) || N % (64 * nw)) return 1;
+                  int P, float* part, uint16_t* out, int S, int mode, int nw, int cfg, hipStream_t st) {
+  if (E < 1 || P < 0 || P % 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 6) return 1;
+  const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
+  if (K % (S * kc) || N % cols) return 1;
   if (mode == GG_SILU && (nw != 2 || S != 1)) return 1;
   if (mode == GG_PARTIAL && part == nullptr) return 1;
   if (mode != GG_PARTIAL && out == nullptr) return 1;
   if (P == 0) return 0;
-  const dim3 grid(N / (64 * nw), S, E);
-  if (nw == 1)
-    hipLaunchKernelGGL(gemm_m64g_grouped_kernel<1>, grid, dim3(256), 0, st, x, rows, offs, K, w, N, P, part, out,
-                       mode);
-  else
-    hipLaunchKernelGGL(gemm_m64g_grouped_kernel<2>, grid, dim3(256), 0, st, x, rows, offs, K, w, N, P, part, out,
-                       mode);
+  const dim3 grid(N / cols, S, E);
+  if (nw == 1) launch_m64g_grouped<1>(cfg, grid, st, x, rows, offs, K, w, N, P, part, out, mode);
+  else launch_m64g_grouped<2>(cfg, grid, st, x, rows, offs, K, w, N, P, part, out, mode);
   return 0;
 }
 

@@ -23,7 +23,7 @@ int skinny_slab_kmax(int);
 int gemm_m64(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 int gemm_m64g(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 int moe_gemm_m64g(const uint16_t*, const int32_t*, const int32_t*, int, int, const uint16_t*, int, int, float*,
-                  uint16_t*, int, int, int, hipStream_t);
+                  uint16_t*, int, int, int, int, hipStream_t);
 void add_partials_rmsnorm(const float*, int, int, uint16_t*, const uint16_t*, uint16_t*, int, float, hipStream_t);
 void reduce_partials(const float*, int, int64_t, uint16_t*, hipStream_t);
 int rope_cache_partials(const float*, int, uint16_t*, int64_t, const int32_t*, const float*, uint16_t*, uint16_t*,
@@ -199,9 +199,10 @@ PYBIND11_MODULE(_kernels, m) {
           "gemm_m64g");
   });
   m.def("moe_gemm_m64g", [](uintptr_t x, uintptr_t rows, uintptr_t offs, int E, int K, uintptr_t w, int N, int P_,
-                            uintptr_t part, uintptr_t out, int splits, int mode, int nw, uintptr_t st) {
+                            uintptr_t part, uintptr_t out, int splits, int mode, int nw, int cfg, uintptr_t st) {
     check(xgk::moe_gemm_m64g(P<const uint16_t>(x), P<const int32_t>(rows), P<const int32_t>(offs), E, K,
-                             P<const uint16_t>(w), N, P_, P<float>(part), P<uint16_t>(out), splits, mode, nw, S(st)),
+                             P<const uint16_t>(w), N, P_, P<float>(part), P<uint16_t>(out), splits, mode, nw, cfg,
+                             S(st)),
           "moe_gemm_m64g");
   });
   m.def("moe_route", [](uintptr_t h, uintptr_t wr, int T, int H, int E, int k, int renorm, uintptr_t w, uintptr_t ids,

@@ -10,6 +10,11 @@ from .activation import silu_and_mul
 
 BLOCK_M = 64
 MOE_GLDS = True  # expert GEMMs on the LDS-DMA pipeline (gemm_m64g.hip); False: register-ring gemm_m64
+# gemm_m64g launch configurations for the expert GEMMs (see ops/linear.py M64G_CFGS);
+# measured with bench/gemm_bench.py --moe-sweep
+# (Mixtral 8x7B, T = 1 / 32 / 64: w13 cfg 3 = 352 vs 384 us at T=64; w2 nw 2 + cfg 1 = 153 vs ~175 us)
+MOE_CFG_W13 = 3
+MOE_CFG_W2 = 1
 
 
 def moe_topk_softmax(router_logits: torch.Tensor, k: int, renorm: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -101,17 +106,27 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     P = sorted_rows.shape[0]
     act = torch.empty(P, F, dtype=x.dtype, device=x.device)
     kn = kernels()
-    gemm = kn.moe_gemm_m64g if MOE_GLDS else kn.moe_gemm_m64
+    if MOE_GLDS:
+        def gemm(*a, cfg=0):
+            kn.moe_gemm_m64g(*a[:-1], cfg, a[-1])
+    else:
+        def gemm(*a, cfg=0):
+            kn.moe_gemm_m64(*a)
+    cfg13 = MOE_CFG_W13 if (MOE_GLDS and H % (64 * 1) == 0 and F2 % 128 == 0) else 0
     gemm(x.contiguous().data_ptr(), sorted_rows.data_ptr(), offs.data_ptr(), E, H, w13.data_ptr(), F2, P, 0,
-         act.data_ptr(), 1, 2, 2, stream_ptr())
-    # w2 has only H/64 column tiles per expert: split K while few experts are active
+         act.data_ptr(), 1, 2, 2, stream_ptr(), cfg=cfg13)
+    # w2 has only H/128 column tiles per expert: split K while few experts are active
+    nw2 = 2 if H % 128 == 0 else 1
+    cfg2 = MOE_CFG_W2 if MOE_GLDS and nw2 == 2 else 0
+    kc2 = 128
     S = 1
     for sk in ((4, 2) if T * k <= 4 else (2,) if T * k <= 16 else ()):
-        if F % (sk * 256) == 0:
+        if F % (sk * kc2) == 0 and F % (sk * 256) == 0:
             S = sk
             break
     part = torch.empty(S, P, H, dtype=torch.float32, device=x.device)
-    gemm(act.data_ptr(), 0, offs.data_ptr(), E, F, w2.data_ptr(), H, P, part.data_ptr(), 0, S, 1, 1, stream_ptr())
+    gemm(act.data_ptr(), 0, offs.data_ptr(), E, F, w2.data_ptr(), H, P, part.data_ptr(), 0, S, 1, nw2, stream_ptr(),
+         cfg=cfg2)
     out = torch.empty(T, H, dtype=x.dtype, device=x.device)
     kn.moe_combine(part.data_ptr(), S, P, dest.data_ptr(), topk_w.float().contiguous().data_ptr(), out.data_ptr(), T,
                    k, H, stream_ptr())
