@@ -90,6 +90,11 @@ class LlamaLayer(nn.Module):
             for n, k in ((Nqkv, H), (H, Hq * D)) + (() if self.moe else ((H, cfg.intermediate_size // tp),)))
         self.m64_silu_ok = self.m64_ok and not self.moe and m64_plan(64, 2 * (cfg.intermediate_size // tp), H,
                                                                      MODE_SILU) is not None
+        # M <= 16 too, when every projection has a measured small-M plan
+        self.m64_small_ok = self.m64_ok and all(
+            m64_plan(1, n, k, MODE_PARTIAL) is not None
+            for n, k in ((Nqkv, H), (H, Hq * D)) + (() if self.moe else ((H, cfg.intermediate_size // tp),))) and (
+            self.moe or m64_plan(1, 2 * (cfg.intermediate_size // tp), H, MODE_SILU) is not None)
 
     def _ar(self, x: torch.Tensor) -> torch.Tensor:
         # keyed on the layer's own TP degree: a TP=1 draft model may live in a TP>1 process
@@ -161,7 +166,7 @@ class LlamaLayer(nn.Module):
         else:
             h, residual = ops.fused_add_rmsnorm(x, residual, self.input_norm, eps)
         T = meta.num_tokens
-        if self.fast_ok and T <= FAST_M_SMALL:
+        if self.fast_ok and T <= FAST_M_SMALL and not self.m64_small_ok:
             # M <= 16: every projection on the streaming skinny kernel (1.7x hipBLASLt
             # on QKV/O at batch 1), split-K partials reduced by the consumers
             pqkv = skinny_linear(h, self.qkv, None, MODE_PARTIAL)
@@ -173,6 +178,8 @@ class LlamaLayer(nn.Module):
             act = skinny_linear(h, self.gate_up, mode=MODE_SILU)
             return self._row_parallel_fast(act, self.down, self.split_down), residual
         if self.m64_ok and T <= FAST_M_SLAB:
+            # gemm_m64g (LDS-DMA weight streaming) for every projection: split-K partials
+            # go to the consumers (rope_cache / add+rmsnorm), SiLU-gate fused in gate_up
             pqkv = m64_linear(h, self.qkv, MODE_PARTIAL)
             a = self.attn.from_partials(pqkv, meta, kv, cos_sin)
             o = m64_linear(a, self.o, MODE_PARTIAL)

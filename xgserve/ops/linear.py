@@ -96,13 +96,16 @@ M64G_CFGS = {0: (4, 128, False), 1: (4, 128, True), 2: (4, 64, False), 3: (4, 64
 
 # Measured on MI355X with cold weights (bench/gemm_bench.py --m64g-sweep,
 # profiles/r1_m64g_sweep.jsonl): (N, K, mode) -> {M bucket: (nw, split_k, cfg)}.
-# Bucket 64 serves 40 < M <= 64, bucket 32 serves 16 < M <= 40 (falls back to 64).
+# Bucket 64 serves 40 < M <= 64, bucket 32 serves 16 < M <= 40 (falls back to 64),
+# bucket 16 serves M <= 16 -- only shapes that have one take gemm_m64g at M <= 16
+# (it beats the register-streaming skinny kernel there: 8B batch 1 QKV 12.3 -> 9.8 us,
+# down 22.9 -> 19.2 us); the rest keep the skinny kernel.
 _M64_TUNED = {
     # Llama-3-8B / Mixtral attention, TP1
-    (6144, 4096, MODE_PARTIAL): {64: (2, 4, 3), 32: (2, 8, 5)},
-    (4096, 4096, MODE_PARTIAL): {64: (1, 4, 0), 32: (1, 4, 0)},
-    (28672, 4096, MODE_SILU): {64: (2, 1, 1), 32: (2, 1, 5)},
-    (4096, 14336, MODE_PARTIAL): {64: (2, 8, 3), 32: (1, 4, 1)},
+    (6144, 4096, MODE_PARTIAL): {64: (2, 4, 3), 32: (2, 8, 5), 16: (2, 8, 5)},
+    (4096, 4096, MODE_PARTIAL): {64: (1, 4, 0), 32: (1, 4, 0), 16: (1, 4, 0)},
+    (28672, 4096, MODE_SILU): {64: (2, 1, 1), 32: (2, 1, 5), 16: (2, 1, 5)},
+    (4096, 14336, MODE_PARTIAL): {64: (2, 8, 3), 32: (1, 4, 1), 16: (1, 8, 3)},
     # Llama-3-8B TP2 shards
     (3072, 4096, MODE_PARTIAL): {64: (1, 8, 2)},
     (4096, 2048, MODE_PARTIAL): {64: (1, 4, 5)},
@@ -133,9 +136,12 @@ def m64_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL):
     from _M64_TUNED; otherwise split-K 4 whenever K allows (the partials are reduced
     by the consumer kernel for free), 128-column tiles once they give >= 192
     workgroups, else 64; bf16 / SiLU epilogues need split 1 (SiLU: nt weight DMA)."""
-    if not (16 < M <= 64) or K % 256:
+    if not (1 <= M <= 64) or K % 256:
         return None
     t = _M64_TUNED.get((N, K, mode))
+    if M <= 16:
+        p = t.get(16) if t is not None else None
+        return p if (p is not None and _m64_valid(N, K, mode, *p)) else None
     if t is not None:
         p = t.get(32) if (M <= 40 and 32 in t) else t.get(64)
         if p is not None and _m64_valid(N, K, mode, *p):
