@@ -11,10 +11,19 @@
 //     B = Q^T (resident in registers, heads >= G zero-padded);
 //   online softmax per head: lane&15 is the head, its 16 keys sit in 4 regs x
 //     4 lane groups -> 2 xor-shuffles;
-//   O[h][d] += P[h][k] V[k][d] on the VALU: lane (g, c) owns 8 dims (16-B V
-//     loads) and KG key sub-groups; P goes through a 1 KiB wave-private LDS tile.
+//   O^T += V^T P^T on v_mfma_f32_16x16x16_bf16, V^T fragments read transposed
+//     (ds_read_b64_tr_b16) from a wave-private LDS tile.
 // Waves stride over tiles; the 4 wave states (m, l, O) merge through LDS at the
 // end. With S > 1 each split writes (O/l, lse) and decode_combine reduces.
+//
+// Fused-QKV form (FQ; the dense decode layer, see gemm_m64g.hip): the QKV
+// projection arrives as fp32 split-K partials. Each workgroup's prologue reduces
+// the partials of ITS (sequence, kv head) -- the G query heads plus the k and v
+// head --, rotates q and k with the RoPE table and, in the split that owns the
+// sequence's last key, appends the new k/v row to the paged cache before its key
+// loop reads it (same workgroup: ordered by vmcnt(0) + barrier; no other
+// workgroup touches that row). This replaces rope_cache_partials and the q round
+// trip through HBM: one launch less per layer.
 #include "common.h"
 
 namespace xgk {
@@ -41,6 +50,87 @@ __device__ __forceinline__ int dswz(int row, int ch) {
   return ch ^ (((row & 7) << 1) & (D / 8 - 1));
 }
 
+// Fused-QKV operands (FQ instantiations only).
+struct QkvFuse {
+  const float* part;            // [S, B, (Hq + 2 Hkv) * D] fp32 QKV split-K partials; row b = sequence b
+  int S;
+  const int32_t* positions;     // [B]
+  const float* cos_sin;         // [max_pos, D] = [cos | sin], fp32
+  const int32_t* slot_mapping;  // [B]; < 0: padding row (no cache write)
+  uint16_t* k_cache;            // the kernel's kc / vc, writable
+  uint16_t* v_cache;
+  int apply_rope;
+};
+
+// f[0..4) = sum_s part[s * slab + off + 0..4): batches of 4 clamped loads issued
+// before the adds (a runtime trip count with one load per iteration would chain S
+// dependent L2 round trips); masked partials add exactly 0.
+__device__ __forceinline__ void sum_partials4(const float* __restrict__ part, int S, int64_t slab, int64_t off,
+                                              float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) f[i] = 0.f;
+  for (int s0 = 0; s0 < S; s0 += 4) {
+    float4 a[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const float4*>(part + min(s0 + i, S - 1) * slab + off);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float k = s0 + i < S ? 1.f : 0.f;
+      f[0] += k * a[i].x; f[1] += k * a[i].y; f[2] += k * a[i].z; f[3] += k * a[i].w;
+    }
+  }
+}
+
+__device__ __forceinline__ uint2 pack4(const float* f) { return make_uint2(pack2(f[0], f[1]), pack2(f[2], f[3])); }
+
+// Prologue of the fused form: q (G heads, rotated) -> q_lds [G][D] bf16; when this
+// split owns the last key and the row is real, the rotated k and the v row are
+// written to the paged cache at slot_mapping[b]. One work item = 4 rotation pairs
+// (or 4 v values): (G + 1) * D/8 + D/4 items spread over the 256 threads.
+template <int D, int G>
+__device__ __forceinline__ void decode_qkv_prologue(const QkvFuse& fq, int b, int kvh, int Hq, int Hkv, int bs,
+                                                     bool owns_last, uint16_t* q_lds) {
+  constexpr int HALF = D / 2, CPH = HALF / 4;  // rope work items (4 pairs each) per head
+  const int64_t width = static_cast<int64_t>(Hq + 2 * Hkv) * D;
+  const int64_t slab = static_cast<int64_t>(gridDim.y) * width;
+  const int64_t row = static_cast<int64_t>(b) * width;
+  const int slot = fq.slot_mapping[b];
+  const bool wkv = owns_last && slot >= 0;
+  const int64_t dst = wkv ? ((static_cast<int64_t>(slot / bs) * Hkv + kvh) * bs + slot % bs) * D : 0;
+  const float* cs = fq.cos_sin + static_cast<int64_t>(fq.positions[b]) * D;
+  const int n_rope = (G + 1) * CPH;
+  for (int it = threadIdx.x; it < n_rope + D / 4; it += blockDim.x) {
+    if (it < n_rope) {
+      const int hh = it / CPH, c = it % CPH;  // hh < G: query head kvh*G + hh; hh == G: the k head
+      if (hh == G && !wkv) continue;
+      const int64_t col = static_cast<int64_t>(hh < G ? kvh * G + hh : Hq + kvh) * D + c * 4;
+      float a[4], e[4];
+      sum_partials4(fq.part, fq.S, slab, row + col, a);
+      sum_partials4(fq.part, fq.S, slab, row + col + HALF, e);
+      if (fq.apply_rope) {
+        const float4 cv = *reinterpret_cast<const float4*>(cs + c * 4);
+        const float4 sv = *reinterpret_cast<const float4*>(cs + HALF + c * 4);
+        const float cc[4] = {cv.x, cv.y, cv.z, cv.w}, ss[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float x1 = a[i], x2 = e[i];
+          a[i] = x1 * cc[i] - x2 * ss[i];
+          e[i] = x2 * cc[i] + x1 * ss[i];
+        }
+      }
+      uint16_t* o = hh < G ? q_lds + hh * D : fq.k_cache + dst;
+      *reinterpret_cast<uint2*>(o + c * 4) = pack4(a);
+      *reinterpret_cast<uint2*>(o + HALF + c * 4) = pack4(e);
+    } else if (wkv) {
+      const int c = it - n_rope;
+      float f[4];
+      sum_partials4(fq.part, fq.S, slab, row + static_cast<int64_t>(Hq + Hkv + kvh) * D + c * 4, f);
+      *reinterpret_cast<uint2*>(fq.v_cache + dst + c * 4) = pack4(f);
+    }
+  }
+  if (wkv) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the cache row lands before any wave reads it
+}
+
 // Per 16-key tile and wave:
 //   S^T[16 keys][16 heads] = K . Q^T     4 x v_mfma_f32_16x16x32_bf16 (K frags straight from HBM)
 //   online softmax per head (lane&15 = head): 2 xor-shuffles per reduction,
@@ -49,13 +139,13 @@ __device__ __forceinline__ int dswz(int row, int ch) {
 //     accumulators ARE the P^T B-fragment (k = 4(lane>>4)+r), V^T fragments come
 //     from a 4 KiB wave-private LDS tile via ds_read_b64_tr_b16
 //   the next tile's K and V loads are issued before the current tile's math.
-template <int D, int G>
+// kc / vc are not __restrict__: the fused form writes the new row through fq.
+template <int D, int G, bool FQ>
 __global__ void __launch_bounds__(256) decode_attn_kernel(
-    const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
-    const uint16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int bt_stride,
-    const int32_t* __restrict__ seq_lens, float* __restrict__ part_out, float* __restrict__ part_lse,
-    uint16_t* __restrict__ out, int64_t out_stride, int Hq, int Hkv, int bs, float scale, int num_splits,
-    int* __restrict__ counters) {
+    const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
+    const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ seq_lens,
+    float* __restrict__ part_out, float* __restrict__ part_lse, uint16_t* __restrict__ out, int64_t out_stride,
+    int Hq, int Hkv, int bs, float scale, int num_splits, int* __restrict__ counters, QkvFuse fq) {
   using C = DecodeCfg<D, G>;
   const int kvh = blockIdx.x, b = blockIdx.y, split = blockIdx.z;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -69,10 +159,21 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   __shared__ __attribute__((aligned(16))) uint16_t v_lds[C::WAVES][16 * D];
   __shared__ float m_lds[C::WAVES][16], l_lds[C::WAVES][16];
   __shared__ float o_lds[C::WAVES][G][D];
+  __shared__ __attribute__((aligned(16))) uint16_t q_lds[FQ ? G * D : 8];
+
+  if constexpr (FQ) {
+    if (L > 0) decode_qkv_prologue<D, G>(fq, b, kvh, Hq, Hkv, bs, split == (ntiles - 1) / tps, q_lds);
+    __syncthreads();
+  }
 
   // Q^T fragment: lane holds Q[head = li][32kk + 8g + j] (heads >= G are zero)
   bf16x8_t qf[C::KK];
-  {
+  if constexpr (FQ) {
+    const uint16_t* qp = q_lds + (li < G ? li : 0) * D;
+#pragma unroll
+    for (int kk = 0; kk < C::KK; ++kk)
+      qf[kk] = as_frag(li < G ? *reinterpret_cast<const uint4*>(qp + kk * 32 + 8 * g) : make_uint4(0, 0, 0, 0));
+  } else {
     const uint16_t* qp = q + static_cast<int64_t>(b) * q_stride + static_cast<int64_t>(kvh * G + li) * D;
 #pragma unroll
     for (int kk = 0; kk < C::KK; ++kk) qf[kk] = as_frag(li < G ? ld16(qp + kk * 32 + 8 * g) : make_uint4(0, 0, 0, 0));
@@ -280,13 +381,13 @@ __global__ void __launch_bounds__(D) decode_combine_kernel(const float* __restri
       f2bf(den > 0.f ? acc / den : 0.f);
 }
 
-template <int D, int G>
+template <int D, int G, bool FQ>
 static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, const uint16_t* vc,
                           const int32_t* bt, int bts, const int32_t* sl, float* po, float* pl, uint16_t* out,
                           int64_t os, int B, int Hq, int Hkv, int bs, float scale, int S, int* counters,
-                          hipStream_t st) {
-  hipLaunchKernelGGL((decode_attn_kernel<D, G>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt, bts, sl,
-                     po, pl, out, os, Hq, Hkv, bs, scale, S, counters);
+                          const QkvFuse& fq, hipStream_t st) {
+  hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt, bts, sl,
+                     po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq);
   if (S > 1 && counters == nullptr)
     hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
 }
@@ -299,15 +400,38 @@ int decode_attention(const uint16_t* q, int64_t q_stride, const uint16_t* kc, co
   if (B <= 0) return 0;
   if (bs % 16 != 0 || Hq % Hkv != 0) return -1;
   const int G = Hq / Hkv;
+  const QkvFuse nofuse{nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
 #define XGK_DEC(DD, GG)                                                                                  \
   if (D == DD && G == GG) {                                                                              \
-    launch_decode<DD, GG>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, part_out, part_lse, out, out_stride, \
-                          B, Hq, Hkv, bs, scale, num_splits, counters, st);                             \
+    launch_decode<DD, GG, false>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, part_out, part_lse, out,  \
+                                 out_stride, B, Hq, Hkv, bs, scale, num_splits, counters, nofuse, st);   \
     return 0;                                                                                            \
   }
   XGK_DEC(128, 1) XGK_DEC(128, 2) XGK_DEC(128, 4) XGK_DEC(128, 8) XGK_DEC(128, 16)
   XGK_DEC(64, 1) XGK_DEC(64, 2) XGK_DEC(64, 4) XGK_DEC(64, 8)
 #undef XGK_DEC
+  return -1;
+}
+
+// Fused-QKV decode attention (D = 128): part = QKV split-K partials [S_qkv, B, (Hq+2Hkv)*128].
+int decode_attention_fq(const float* part, int S_qkv, const int32_t* positions, const float* cos_sin,
+                        const int32_t* slots, uint16_t* kc, uint16_t* vc, const int32_t* bt, int bt_stride,
+                        const int32_t* seq_lens, float* part_out, float* part_lse, uint16_t* out,
+                        int64_t out_stride, int B, int Hq, int Hkv, int D, int bs, float scale, int num_splits,
+                        int apply_rope, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (part == nullptr || S_qkv < 1 || bs % 16 != 0 || Hq % Hkv != 0 || D != 128 || num_splits < 1) return -1;
+  if (num_splits > 1 && (part_out == nullptr || part_lse == nullptr)) return -1;
+  const QkvFuse fq{part, S_qkv, positions, cos_sin, slots, kc, vc, apply_rope};
+  const int G = Hq / Hkv;
+#define XGK_DECF(GG)                                                                                         \
+  if (G == GG) {                                                                                             \
+    launch_decode<128, GG, true>(nullptr, 0, kc, vc, bt, bt_stride, seq_lens, part_out, part_lse, out,       \
+                                 out_stride, B, Hq, Hkv, bs, scale, num_splits, nullptr, fq, st);            \
+    return 0;                                                                                                \
+  }
+  XGK_DECF(1) XGK_DECF(2) XGK_DECF(4) XGK_DECF(8)
+#undef XGK_DECF
   return -1;
 }
 

@@ -15,65 +15,133 @@
 //     flight across it), never __syncthreads (its fence would drain the DMA
 //     queue); WAR: a slot is re-filled only after the barrier that follows its
 //     last reads (cdna_hip_programming.md §5 "Pipelining across barriers").
-#include "common.h"
+//
+// Fused decode layer (M64Epi; dense Llama decode path, xgserve/models/llama.py):
+//   * the input RMSNorm as an epilogue row scale: x is the raw bf16 residual
+//     stream, the norm weight is folded into W at load time, and output row m is
+//     scaled by rsqrt(sum_sq[m] / K + eps) -- no normalised-activation kernel;
+//   * GG_RESID: the residual add + the next norm's statistics inside the same
+//     launch: write-through split-K slabs and an agent-scope arrival ticket per
+//     column tile whose last workgroup reduces the tile into the bf16 residual
+//     stream and the tile's per-row sum of squares; the consuming GEMM adds the
+//     per-tile sums in a fixed order (deterministic).
+//   * the statistics are loaded at kernel START (spread over the 16 lane groups x
+//     waves of a row, so each lane holds <= 8 values) and combined in the epilogue
+//     by xor-shuffles (+ one LDS step): their latency hides under the weight
+//     stream instead of extending the tail.
+#include "glds.h"
 
 namespace xgk {
 
-constexpr int GG_KC = 128;              // k per chunk (one slot)
-constexpr int GG_SLOTS = 3;
-constexpr int GG_XBYTES = 64 * 256;     // x rows x bytes per chunk
+enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2, GG_RESID = 3 };
 
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void glb_void_t;
+// Fused-decode epilogue operands (all null / 0 for a plain GEMM).
+//   ss_in / ss_n / ss_stride: RMSNorm statistics of the input rows as ss_n
+//           partial sums of squares per row, ss_in[j * ss_stride + m], added in a
+//           fixed order; output row m is scaled by rsqrt(sum / K + eps).
+//           ss_n <= 8: any M (lane group g of row m sums j = g, g + 4);
+//           8 < ss_n <= 64: M <= 16 only (wave w, group g sums j = 4w + g + 4 WV q, q < 8).
+//   GG_RESID: resid[m, n] += sum_s part[s, m, n] (bf16 residual stream, in place);
+//           ss_out[tile * M + m] = sum over the tile's columns of resid[m, n]^2
+//           (the next GEMM's ss_in with ss_n = gridDim.x). counters: gridDim.x tile
+//           tickets, zero before the first launch; every ticket winner re-zeroes
+//           its word, so each launch leaves them zero.
+struct M64Epi {
+  const float* ss_in;
+  int ss_n;
+  int ss_stride;
+  float eps;
+  uint16_t* resid;
+  float* ss_out;
+  int* counters;
+};
 
-// The DMA is issued from inline asm so that hipcc's waitcnt pass does not see it:
-// with the builtin it serialises the DMAs of different slots (vmcnt(0) between
-// them and before every fragment read). Completion is then tracked ONLY by the
-// explicit counted waits below; "memory" keeps the compiler from moving LDS
-// reads across them.
-__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const uint32_t lds = __builtin_amdgcn_readfirstlane(
-      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)(lds_base))));
-  asm volatile(
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %0, off"
-      :
-      : "v"(src), "s"(lds)
-      : "memory", "m0");
-#endif
+// Every wave drains its stores (write-through), then one relaxed agent-scope
+// ticket; returns in every thread whether this workgroup drew `last_value`. The
+// winner acquires (agent scope: drops this CU's stale L1 lines) before any of its
+// waves reads what the others published, and re-arms the word. `flag` is an LDS
+// word no wave touches concurrently (inside the staging array: ONE __shared__
+// object per kernel, guide §5 "Three .s-level traps" (a)).
+__device__ __forceinline__ bool agent_ticket(int* cnt, int last_value, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == last_value;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  const bool r = *flag != 0;
+  __syncthreads();
+  return r;
 }
 
-__device__ __forceinline__ void glds16_nt(const void* src, void* lds_base) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const uint32_t lds = __builtin_amdgcn_readfirstlane(
-      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)(lds_base))));
-  asm volatile(
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %0, off nt"
-      :
-      : "v"(src), "s"(lds)
-      : "memory", "m0");
-#endif
+// Reduction of one column tile [tile*COLS, +COLS) x [0, M): the S fp32 slabs + the
+// bf16 residual -> new residual and the tile's per-row sum of squares. The threads
+// of one row are C4 = COLS/4 consecutive lanes of one wave (row sum = xor butterfly
+// over them); every lane runs every butterfly.
+template <int COLS, int NTHR>
+__device__ __forceinline__ void m64g_resid_reduce(const float* __restrict__ part, int S, int M, int N, int tile,
+                                                  const M64Epi& epi) {
+  constexpr int C4 = COLS / 4;
+  static_assert(64 % C4 == 0 && NTHR % C4 == 0, "row groups must not straddle waves");
+  const int tid = threadIdx.x;
+  const int n0 = tile * COLS;
+  const int64_t slab = static_cast<int64_t>(M) * N;
+  for (int base = 0; base < M * C4; base += NTHR) {
+    const int idx = base + tid;
+    const bool ok = idx < M * C4;
+    const int m = ok ? idx / C4 : 0, c = idx % C4;
+    const int64_t off = static_cast<int64_t>(m) * N + n0 + 4 * c;
+    float y[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < S; s0 += 4) {
+      float4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)  // clamped unconditional loads, masked after (no branch per load)
+        v[i] = *reinterpret_cast<const float4*>(part + min(s0 + i, S - 1) * slab + off);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float k = s0 + i < S ? 1.f : 0.f;
+        y[0] += k * v[i].x;
+        y[1] += k * v[i].y;
+        y[2] += k * v[i].z;
+        y[3] += k * v[i].w;
+      }
+    }
+    float sq = 0.f;
+    if (ok) {
+      const uint2 r = *reinterpret_cast<const uint2*>(epi.resid + off);
+      y[0] += __uint_as_float(r.x << 16);
+      y[1] += __uint_as_float(r.x & 0xFFFF0000u);
+      y[2] += __uint_as_float(r.y << 16);
+      y[3] += __uint_as_float(r.y & 0xFFFF0000u);
+      uint2 o;
+      o.x = pack2(y[0], y[1]);
+      o.y = pack2(y[2], y[3]);
+      *reinterpret_cast<uint2*>(epi.resid + off) = o;
+      // the residual stream is bf16: the norm statistics use the rounded values
+      const float r0 = __uint_as_float(o.x << 16), r1 = __uint_as_float(o.x & 0xFFFF0000u);
+      const float r2 = __uint_as_float(o.y << 16), r3 = __uint_as_float(o.y & 0xFFFF0000u);
+      sq = r0 * r0 + r1 * r1 + r2 * r2 + r3 * r3;
+    }
+#pragma unroll
+    for (int o = C4 / 2; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+    if (ok && c == 0) epi.ss_out[tile * M + m] = sq;
+  }
 }
 
-// s_waitcnt vmcnt(N) (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14; expcnt, lgkmcnt left at max)
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-#endif
+// GG_RESID tail: tile ticket -> the last arriver reduces the tile.
+template <int COLS, int NTHR>
+__device__ __forceinline__ void m64g_resid_tail(const float* __restrict__ part, int S, int M, int N,
+                                                const M64Epi& epi, int* flag) {
+  if (S > 1 && !agent_ticket(epi.counters + blockIdx.x, S - 1, flag)) return;
+  m64g_resid_reduce<COLS, NTHR>(part, S, M, N, blockIdx.x, epi);
 }
-
-__device__ __forceinline__ void raw_barrier() {
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm volatile("s_barrier" ::: "memory");
-#endif
-}
-
-enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2 };
 
 // Dense kernel, parametrised for the decode shapes (bench/gemm_bench.py picks):
 //   NW  16-column MFMA tiles per wave (2 = 32 columns; required by the SiLU epilogue)
@@ -85,7 +153,7 @@ template <int NW, int WV, int KC, bool NT>
 __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* __restrict__ x, int M, int K,
                                                                const uint16_t* __restrict__ w, int N,
                                                                float* __restrict__ part, uint16_t* __restrict__ out,
-                                                               int mode) {
+                                                               int mode, M64Epi epi) {
   constexpr int MT = 4;
   constexpr int RB = KC * 2;                     // bytes per LDS row
   constexpr int GPR = KC / 8;                    // 16-B granules per row
@@ -169,6 +237,20 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
     compute(cur);
   };
 
+  // RMSNorm statistics of the input rows, loaded before the weight stream starts
+  // (clamped unconditional loads, masked when combined; held in 8 registers)
+  const bool has_ss = epi.ss_in != nullptr;
+  const bool wide_ss = has_ss && epi.ss_n > 8;  // per-tile sums (M <= 16): spread over waves too
+  float ssv[8];
+  if (has_ss) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int mt = wide_ss ? 0 : i >> 1, q = wide_ss ? i : i & 1;
+      const int j = wide_ss ? 4 * wid + g + 4 * WV * q : g + 4 * q;
+      ssv[i] = epi.ss_in[min(j, epi.ss_n - 1) * epi.ss_stride + min(16 * mt + li, M - 1)];
+    }
+  }
+
   issue(lds0, 0);
   if (nchunks > 1) issue(lds1, 1);
   int c = 0;
@@ -180,18 +262,59 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   if (c < nchunks) step(lds0, lds2, c);
   if (c + 1 < nchunks) step(lds1, lds0, c + 1);
 
+  if (has_ss) {  // input RMSNorm as a row scale of the (linear) output
+    float tot[MT];
+    if (!wide_ss) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        float v = (g < epi.ss_n ? ssv[2 * mt] : 0.f) + (g + 4 < epi.ss_n ? ssv[2 * mt + 1] : 0.f);
+        v += __shfl_xor(v, 16, 64);
+        tot[mt] = v + __shfl_xor(v, 32, 64);
+      }
+    } else {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v += 4 * wid + g + 4 * WV * q < epi.ss_n ? ssv[q] : 0.f;
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      float* red = reinterpret_cast<float*>(lds0);
+      __syncthreads();  // all waves are past their last slot read (no DMA in flight)
+      if (g == 0) red[wid * 16 + li] = v;
+      __syncthreads();
+      float t = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < WV; ++w2) t += red[w2 * 16 + li];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) tot[mt] = t;  // M <= 16: only rows of mt 0 are real
+      __syncthreads();  // red is re-used as the GG_RESID ticket flag below
+    }
+    const float inv_k = 1.f / static_cast<float>(K);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const float sc = rsqrtf(tot[mt] * inv_k + epi.eps);
+#pragma unroll
+      for (int nt = 0; nt < NW; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[nt][mt][r] *= sc;
+    }
+  }
+
   // acc[nt][mt][r] = out[m = 16 mt + li][n = nbase + 16 nt + 4 g + r]
-  if (mode == GG_PARTIAL) {
+  if (mode == GG_PARTIAL || mode == GG_RESID) {
     float* pp = part + static_cast<int64_t>(s) * M * N;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int m = 16 * mt + li;
       if (m >= M) continue;
 #pragma unroll
-      for (int nt = 0; nt < NW; ++nt)
-        *reinterpret_cast<float4*>(pp + static_cast<int64_t>(m) * N + nbase + 16 * nt + 4 * g) =
-            make_float4(acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]);
+      for (int nt = 0; nt < NW; ++nt) {
+        float* dst = pp + static_cast<int64_t>(m) * N + nbase + 16 * nt + 4 * g;
+        if (mode == GG_RESID) st16_sc1(dst, acc[nt][mt]);
+        else *reinterpret_cast<float4*>(dst) = make_float4(acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]);
+      }
     }
+    if (mode == GG_RESID)
+      m64g_resid_tail<16 * NW * WV, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0));
   } else if (mode == GG_BF16) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -407,6 +530,7 @@ int m64g_cfg_kc(int cfg);
 int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, int E, int K, const uint16_t* w, int N,
                   int P, float* part, uint16_t* out, int S, int mode, int nw, int cfg, hipStream_t st) {
   if (E < 1 || P < 0 || P % 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 6) return 1;
+  if (mode != GG_BF16 && mode != GG_PARTIAL && mode != GG_SILU) return 1;
   const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
   if (K % (S * kc) || N % cols) return 1;
   if (mode == GG_SILU && (nw != 2 || S != 1)) return 1;
@@ -423,33 +547,65 @@ int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, i
 //      4 = (2, 64), 5 = (2, 64, nt), 6 = (2, 128, nt)
 template <int NW>
 static void launch_m64g(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N,
-                        float* part, uint16_t* out, int mode) {
+                        float* part, uint16_t* out, int mode, const M64Epi& epi) {
+#define XGK_M64G(WV, KC, NT)                                                                                     \
+  hipLaunchKernelGGL((gemm_m64g_kernel<NW, WV, KC, NT>), grid, dim3(64 * WV), 0, st, x, M, K, w, N, part, out, \
+                     mode, epi)
   switch (cfg) {
-    case 1: hipLaunchKernelGGL((gemm_m64g_kernel<NW, 4, 128, true>), grid, dim3(256), 0, st, x, M, K, w, N, part, out, mode); break;
-    case 2: hipLaunchKernelGGL((gemm_m64g_kernel<NW, 4, 64, false>), grid, dim3(256), 0, st, x, M, K, w, N, part, out, mode); break;
-    case 3: hipLaunchKernelGGL((gemm_m64g_kernel<NW, 4, 64, true>), grid, dim3(256), 0, st, x, M, K, w, N, part, out, mode); break;
-    case 4: hipLaunchKernelGGL((gemm_m64g_kernel<NW, 2, 64, false>), grid, dim3(128), 0, st, x, M, K, w, N, part, out, mode); break;
-    case 5: hipLaunchKernelGGL((gemm_m64g_kernel<NW, 2, 64, true>), grid, dim3(128), 0, st, x, M, K, w, N, part, out, mode); break;
-    case 6: hipLaunchKernelGGL((gemm_m64g_kernel<NW, 2, 128, true>), grid, dim3(128), 0, st, x, M, K, w, N, part, out, mode); break;
-    default: hipLaunchKernelGGL((gemm_m64g_kernel<NW, 4, 128, false>), grid, dim3(256), 0, st, x, M, K, w, N, part, out, mode); break;
+    case 1: XGK_M64G(4, 128, true); break;
+    case 2: XGK_M64G(4, 64, false); break;
+    case 3: XGK_M64G(4, 64, true); break;
+    case 4: XGK_M64G(2, 64, false); break;
+    case 5: XGK_M64G(2, 64, true); break;
+    case 6: XGK_M64G(2, 128, true); break;
+    default: XGK_M64G(4, 128, false); break;
   }
+#undef XGK_M64G
 }
 
 int m64g_cfg_waves(int cfg) { return cfg >= 4 ? 2 : 4; }
 int m64g_cfg_kc(int cfg) { return (cfg == 2 || cfg == 3 || cfg == 4 || cfg == 5) ? 64 : 128; }
 
-int gemm_m64g(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
-              int nw, int cfg, hipStream_t st) {
+// Host-side shape / operand checks shared by both entry points (0 = valid).
+static int m64g_check(int M, int K, int N, const float* part, const uint16_t* out, int S, int mode, int nw, int cfg,
+                      const M64Epi& epi) {
   if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 6) return 1;
-  const int wv = m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
-  const int cols = 16 * nw * wv;
+  if (mode < GG_BF16 || mode > GG_RESID) return 1;
+  const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
   if (K % (S * kc) || N % cols) return 1;
   if (mode == GG_SILU && (nw != 2 || S != 1)) return 1;
-  if (mode == GG_PARTIAL && part == nullptr) return 1;
-  if (mode != GG_PARTIAL && out == nullptr) return 1;
-  const dim3 grid(N / cols, S);
-  if (nw == 1) launch_m64g<1>(cfg, grid, st, x, M, K, w, N, part, out, mode);
-  else launch_m64g<2>(cfg, grid, st, x, M, K, w, N, part, out, mode);
+  if (mode == GG_BF16 && S != 1) return 1;
+  if ((mode == GG_PARTIAL || mode == GG_RESID) && part == nullptr) return 1;
+  if ((mode == GG_BF16 || mode == GG_SILU) && out == nullptr) return 1;
+  if (mode == GG_RESID && (epi.resid == nullptr || epi.ss_out == nullptr || epi.counters == nullptr)) return 1;
+  if (epi.ss_in != nullptr && (epi.ss_n < 1 || epi.ss_n > 64 || epi.ss_stride < M || (epi.ss_n > 8 && M > 16)))
+    return 1;
+  return 0;
+}
+
+static void m64g_launch(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S,
+                        int mode, int nw, int cfg, const M64Epi& epi, hipStream_t st) {
+  const dim3 grid(N / (16 * nw * m64g_cfg_waves(cfg)), S);
+  if (nw == 1) launch_m64g<1>(cfg, grid, st, x, M, K, w, N, part, out, mode, epi);
+  else launch_m64g<2>(cfg, grid, st, x, M, K, w, N, part, out, mode, epi);
+}
+
+int gemm_m64g(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
+              int nw, int cfg, hipStream_t st) {
+  const M64Epi epi{nullptr, 0, 0, 0.f, nullptr, nullptr, nullptr};
+  if (mode == GG_RESID || m64g_check(M, K, N, part, out, S, mode, nw, cfg, epi)) return 1;
+  m64g_launch(x, M, K, w, N, part, out, S, mode, nw, cfg, epi, st);
+  return 0;
+}
+
+// Fused-decode entry: the row-scaled input norm (ss_in) and/or the GG_RESID
+// epilogue; ss_out holds (N / cols) * M floats, counters N / cols ints.
+int gemm_m64g_ex(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S,
+                 int mode, int nw, int cfg, const float* ss_in, int ss_n, int ss_stride, float eps, uint16_t* resid,
+                 float* ss_out, int* counters, hipStream_t st) {
+  const M64Epi epi{ss_in, ss_n, ss_stride, eps, resid, ss_out, counters};
+  if (m64g_check(M, K, N, part, out, S, mode, nw, cfg, epi)) return 1;
+  m64g_launch(x, M, K, w, N, part, out, S, mode, nw, cfg, epi, st);
   return 0;
 }
 

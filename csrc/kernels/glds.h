@@ -1,0 +1,72 @@
+// LDS-DMA pipeline helpers shared by the MFMA GEMMs (gemm_m64g.hip, gemm_tile.hip):
+//   * global_load_lds_dwordx4 issued from inline asm -- hipcc's waitcnt pass does
+//     not see it (with the builtin it serialises the DMAs of different slots:
+//     vmcnt(0) between them and before every fragment read), so completion is
+//     tracked ONLY by the explicit counted waits; "memory" keeps the compiler
+//     from moving LDS reads across them. M0 is written in the same statement
+//     that reads it (cdna_hip_programming.md §5.7);
+//   * counted s_waitcnt vmcnt(N) and a raw s_barrier (never __syncthreads inside
+//     a pipelined loop: its fence drains the DMA queue);
+//   * the write-through (sc1) 16-B store of in-launch hand-offs (Guideline 16 R1).
+#pragma once
+
+#include "common.h"
+
+namespace xgk {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)(lds_base))));
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off"
+      :
+      : "v"(src), "s"(lds)
+      : "memory", "m0");
+#endif
+}
+
+// non-temporal weight stream (read once per step: keeps the activations in L2)
+__device__ __forceinline__ void glds16_nt(const void* src, void* lds_base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)(lds_base))));
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off nt"
+      :
+      : "v"(src), "s"(lds)
+      : "memory", "m0");
+#endif
+}
+
+// s_waitcnt vmcnt(N) (expcnt, lgkmcnt left at max)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#endif
+}
+
+__device__ __forceinline__ void raw_barrier() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_barrier" ::: "memory");
+#endif
+}
+
+// Write-through (sc1) 16-B store: visible chip-wide once the storing wave's vmcnt
+// drains, so a hand-off ticket after it needs no release fence. Not counted by
+// hipcc: the caller's explicit vmcnt(0) covers it; s_nop 1 keeps the next
+// instruction from overwriting the data registers before the store reads them.
+__device__ __forceinline__ void st16_sc1(float* p, f32x4_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+#endif
+}
+
+}  // namespace xgk

@@ -139,6 +139,27 @@ void fused_add_rmsnorm(const uint16_t* x, uint16_t* res, const uint16_t* w, uint
   if (T > 0) launch_rms<true>(x, res, w, out, T, H, eps, H, H, st);
 }
 
+// Per-row sum of squares (fp32) of bf16 [T, H] rows: the RMSNorm statistic the
+// fused decode GEMMs apply as an epilogue row scale (layer 0's input).
+__global__ void __launch_bounds__(256) row_sumsq_kernel(const uint16_t* __restrict__ x, float* __restrict__ ss,
+                                                        int H) {
+  __shared__ float red[8];
+  const uint16_t* xr = x + static_cast<int64_t>(blockIdx.x) * H;
+  float s = 0.f;
+  for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
+    float v[8];
+    unpack8(ld16(xr + c * 8), v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[i] * v[i];
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) ss[blockIdx.x] = s;
+}
+
+void row_sumsq(const uint16_t* x, int T, int H, float* ss, hipStream_t st) {
+  if (T > 0) hipLaunchKernelGGL(row_sumsq_kernel, dim3(T), dim3(256), 0, st, x, ss, H);
+}
+
 void layernorm(const uint16_t* x, const uint16_t* w, const uint16_t* b, uint16_t* out, int T, int H,
                float eps, hipStream_t st) {
   if (T <= 0) return;

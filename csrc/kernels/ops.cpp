@@ -22,6 +22,13 @@ int skinny_gemm(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_
 int skinny_slab_kmax(int);
 int gemm_m64(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 int gemm_m64g(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
+int gemm_m64g_ex(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, const float*,
+                 int, int, float, uint16_t*, float*, int*, hipStream_t);
+void add_partials_resid(const float*, int, int, uint16_t*, float*, int, hipStream_t);
+void row_sumsq(const uint16_t*, int, int, float*, hipStream_t);
+int decode_attention_fq(const float*, int, const int32_t*, const float*, const int32_t*, uint16_t*, uint16_t*,
+                        const int32_t*, int, const int32_t*, float*, float*, uint16_t*, int64_t, int, int, int, int,
+                        int, float, int, int, hipStream_t);
 int moe_gemm_m64g(const uint16_t*, const int32_t*, const int32_t*, int, int, const uint16_t*, int, int, float*,
                   uint16_t*, int, int, int, int, hipStream_t);
 void add_partials_rmsnorm(const float*, int, int, uint16_t*, const uint16_t*, uint16_t*, int, float, hipStream_t);
@@ -197,6 +204,36 @@ PYBIND11_MODULE(_kernels, m) {
     check(xgk::gemm_m64g(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode, nw,
                          cfg, S(st)),
           "gemm_m64g");
+  });
+  // ---- fused decode layer (gemm_m64g.hip epilogues, decode_attention.hip FQ prologue)
+  m.def("gemm_m64g_ex", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
+                           int mode, int nw, int cfg, uintptr_t ss_in, int ss_n, int ss_stride, float eps,
+                           uintptr_t resid, uintptr_t ss_out, uintptr_t counters, uintptr_t st) {
+    check(xgk::gemm_m64g_ex(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode,
+                            nw, cfg, P<const float>(ss_in), ss_n, ss_stride, eps, P<uint16_t>(resid),
+                            P<float>(ss_out), P<int>(counters), S(st)),
+          "gemm_m64g_ex");
+  });
+  m.def("add_partials_resid", [](uintptr_t part, int S_, int T, uintptr_t res, uintptr_t ss_part, int H,
+                                 uintptr_t st) {
+    if (H % 1024) throw std::invalid_argument("add_partials_resid: H % 1024 != 0");
+    xgk::add_partials_resid(P<const float>(part), S_, T, P<uint16_t>(res), P<float>(ss_part), H, S(st));
+    check(0, "add_partials_resid");
+  });
+  m.def("row_sumsq", [](uintptr_t x, int T, int H, uintptr_t ss, uintptr_t st) {
+    if (H % 8) throw std::invalid_argument("row_sumsq: H % 8 != 0");
+    xgk::row_sumsq(P<const uint16_t>(x), T, H, P<float>(ss), S(st));
+    check(0, "row_sumsq");
+  });
+  m.def("decode_attention_fq", [](uintptr_t part, int S_, uintptr_t pos, uintptr_t cs, uintptr_t slots, uintptr_t kc,
+                                  uintptr_t vc, uintptr_t bt, int bts, uintptr_t sl, uintptr_t po, uintptr_t pl,
+                                  uintptr_t out, int64_t os, int B, int Hq, int Hkv, int D, int bs, float scale,
+                                  int splits, int apply_rope, uintptr_t st) {
+    check(xgk::decode_attention_fq(P<const float>(part), S_, P<const int32_t>(pos), P<const float>(cs),
+                                   P<const int32_t>(slots), P<uint16_t>(kc), P<uint16_t>(vc), P<const int32_t>(bt),
+                                   bts, P<const int32_t>(sl), P<float>(po), P<float>(pl), P<uint16_t>(out), os, B, Hq,
+                                   Hkv, D, bs, scale, splits, apply_rope, S(st)),
+          "decode_attention_fq");
   });
   m.def("moe_gemm_m64g", [](uintptr_t x, uintptr_t rows, uintptr_t offs, int E, int K, uintptr_t w, int N, int P_,
                             uintptr_t part, uintptr_t out, int splits, int mode, int nw, int cfg, uintptr_t st) {

@@ -419,6 +419,68 @@ void add_partials_rmsnorm(const float* part, int S, int T, uint16_t* residual, c
 #undef XGK_APR
 }
 
+// Fused decode layer, large split-K slabs (M ~ 64 decode): residual[t] +=
+// sum_s part[s, t] (bf16, in place) and the new residual's sums of squares per
+// 1024-column chunk, ss_part[chunk * T + t]; the next GEMM adds the H/1024 chunk
+// sums in order (deterministic) and applies the RMSNorm as a row scale. One
+// 128-thread workgroup per (row, chunk): 8 columns per lane, every partial load
+// issued before the adds; 4-8x the workgroups of add_partials_rmsnorm.
+template <int SP>
+__global__ void __launch_bounds__(128) add_partials_resid_kernel(const float* __restrict__ part, int S, int T,
+                                                                  uint16_t* __restrict__ residual,
+                                                                  float* __restrict__ ss_part, int H) {
+  __shared__ float red[8];
+  const int t = blockIdx.x, chunk = blockIdx.y;
+  const int col = (chunk * 128 + threadIdx.x) * 8;
+  uint16_t* rr = residual + static_cast<int64_t>(t) * H + col;
+  float v[8];
+  unpack8(ld16(rr), v);
+  if constexpr (SP > 0) {
+    float4 a[SP], b[SP];
+#pragma unroll
+    for (int s = 0; s < SP; ++s) {
+      const float* pp = part + (static_cast<int64_t>(s) * T + t) * H + col;
+      a[s] = *reinterpret_cast<const float4*>(pp);
+      b[s] = *reinterpret_cast<const float4*>(pp + 4);
+    }
+#pragma unroll
+    for (int s = 0; s < SP; ++s) {
+      v[0] += a[s].x; v[1] += a[s].y; v[2] += a[s].z; v[3] += a[s].w;
+      v[4] += b[s].x; v[5] += b[s].y; v[6] += b[s].z; v[7] += b[s].w;
+    }
+  } else {
+    for (int s = 0; s < S; ++s) {
+      const float* pp = part + (static_cast<int64_t>(s) * T + t) * H + col;
+      const float4 a = *reinterpret_cast<const float4*>(pp);
+      const float4 b = *reinterpret_cast<const float4*>(pp + 4);
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+      v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+  }
+  const uint4 pk = pack8(v);
+  st16(rr, pk);
+  unpack8(pk, v);  // statistics of the rounded (stored) residual
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ss += v[i] * v[i];
+  ss = block_sum(ss, red);
+  if (threadIdx.x == 0) ss_part[static_cast<int64_t>(chunk) * T + t] = ss;
+}
+
+void add_partials_resid(const float* part, int S, int T, uint16_t* residual, float* ss_part, int H,
+                        hipStream_t st) {
+  if (T <= 0) return;
+  const dim3 g(T, H / 1024);
+#define XGK_APRS(SPV) \
+  hipLaunchKernelGGL((add_partials_resid_kernel<SPV>), g, dim3(128), 0, st, part, S, T, residual, ss_part, H)
+  if (S == 1) XGK_APRS(1);
+  else if (S == 2) XGK_APRS(2);
+  else if (S == 4) XGK_APRS(4);
+  else if (S == 8) XGK_APRS(8);
+  else XGK_APRS(0);
+#undef XGK_APRS
+}
+
 // out[t, :] = bf16(sum_s part[s, t, :])  (used when a collective needs the sum)
 __global__ void __launch_bounds__(256) reduce_partials_kernel(const float* __restrict__ part, int S, int64_t n,
                                                               uint16_t* __restrict__ out) {

@@ -1,0 +1,163 @@
+"""Fused decode layer on the MI355X: gemm_m64g's RMSNorm row-scale and residual
+(GG_RESID) epilogues, the fused QKV -> RoPE -> KV-append attention prologue, and
+the fused model path -- each against a plain fp32 PyTorch reference (or the
+unfused kernel chain that is itself checked against fp32 elsewhere)."""
+import math
+from dataclasses import replace
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from xgserve import ops
+from xgserve.ops import _native
+from xgserve.ops import linear as lin
+from xgserve.ops.linear import (MODE_PARTIAL, MODE_SILU, PendingSum, ResidWorkspace, RowStats, interleave_gate_up,
+                                m64_norm_linear, m64_resid_linear)
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _k():
+    _native.kernels()  # fail loudly: the HIP library must be the one that runs
+    torch.manual_seed(0)
+
+
+def rnd(*s, scale=1.0):
+    return (torch.randn(*s, device=DEV) * scale).bfloat16()
+
+
+def rel_err(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-6))
+
+
+@pytest.mark.parametrize("M,n_parts", [(1, 1), (5, 4), (16, 8), (24, 1), (64, 4), (64, 8), (1, 64), (9, 64),
+                                        (16, 32)])
+def test_norm_linear_row_scale(M, n_parts):
+    K = 4096
+    x = rnd(M, K)
+    sq = x.float() ** 2
+    st = RowStats(sq.view(M, n_parts, -1).sum(-1).t().contiguous(), n_parts, M)
+    h = x.float() * torch.rsqrt(sq.sum(-1, keepdim=True) / K + 1e-5)
+    w = rnd(6144, K, scale=0.02)
+    pend = m64_norm_linear(x, w, MODE_PARTIAL, st, 1e-5)
+    assert rel_err(pend.part.sum(0), h @ w.float().t()) < 2e-3
+    g, u = rnd(14336, K, scale=0.02), rnd(14336, K, scale=0.02)
+    y = m64_norm_linear(x, interleave_gate_up(g, u), MODE_SILU, st, 1e-5)
+    ref = F.silu(h @ g.float().t()) * (h @ u.float().t())
+    assert rel_err(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 14336)])
+@pytest.mark.parametrize("inlaunch", [True, False])
+def test_resid_linear(M, N, K, inlaunch, monkeypatch):
+    monkeypatch.setattr(lin, "RESID_INLAUNCH_MAX_BYTES", (1 << 30) if inlaunch else 0)
+    x, w, r0 = rnd(M, K), rnd(N, K, scale=0.02), rnd(M, N)
+    ws = ResidWorkspace(4, 64, N, DEV)
+    ref = (r0.float() + x.float() @ w.float().t()).bfloat16().float()
+    runs = []
+    for _ in range(3):  # the tickets are re-armed by their winners: repeated launches stay exact
+        r = r0.clone()
+        st = m64_resid_linear(x, w, r, ws, 1, 1e-5)
+        torch.testing.assert_close(r.float(), ref, atol=3e-2, rtol=2e-2)
+        ss = st.ss.reshape(-1)[: st.n * st.stride].view(st.n, st.stride)[:, :M].sum(0)
+        assert st.n == (64 if inlaunch and M <= 16 else N // 1024)
+        assert rel_err(ss, (r.float() ** 2).sum(-1)) < 1e-5
+        runs.append((r.clone(), ss.clone()))
+    assert all(torch.equal(runs[0][0], a) and torch.equal(runs[0][1], b) for a, b in runs)  # deterministic
+    assert int(ws.counters.abs().sum()) == 0
+
+
+def _paged(lens, Hkv, D, bs, extra_pages=8):
+    pages_per = [(L + bs - 1) // bs for L in lens]
+    NB = sum(pages_per) + extra_pages
+    kc = rnd(NB, Hkv, bs, D)
+    vc = rnd(NB, Hkv, bs, D)
+    perm = torch.randperm(NB).tolist()
+    bt = torch.zeros(len(lens), max(pages_per), dtype=torch.int32)
+    i = 0
+    for s, n in enumerate(pages_per):
+        bt[s, :n] = torch.tensor(perm[i:i + n])
+        i += n
+    return kc, vc, bt.to(DEV)
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 8)])
+@pytest.mark.parametrize("S", [1, 4, 8])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_decode_attention_fused_prologue(Hq, Hkv, S, splits):
+    D, bs = 128, 16
+    lens = [1, 17, 300, 64, 0, 129]  # row 4: a graph padding row (no KV write, no attention)
+    kc, vc, bt = _paged([max(1, L) for L in lens], Hkv, D, bs)
+    B = len(lens)
+    part = torch.randn(S, B, (Hq + 2 * Hkv) * D, device=DEV) * 0.3
+    pos = torch.tensor([max(0, L - 1) for L in lens], dtype=torch.int32, device=DEV)
+    slots = torch.tensor([int(bt[b, (L - 1) // bs]) * bs + (L - 1) % bs if L > 0 else -1
+                          for b, L in enumerate(lens)], dtype=torch.int32, device=DEV)
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    cs = ops.build_cos_sin(D, 4096, 500000.0, device=DEV)
+    scale = 1.0 / math.sqrt(D)
+    kc1, vc1, kc2, vc2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
+    out = ops.decode_attention_fused(PendingSum(part, S), pos, slots, cs, kc1, vc1, bt, sl, Hq, scale, splits)
+    # reference: the unfused chain (rope_cache_partials -> fp32 attention reference)
+    q = torch.empty(B, Hq * D, dtype=torch.bfloat16, device=DEV)
+    ops.rope_cache_partials(PendingSum(part, S), q, pos, cs, kc2, vc2, slots, Hq, Hkv, D)
+    ref = ops.decode_attention_ref(q.view(B, Hq, D).cpu(), kc2.cpu(), vc2.cpu(), bt.cpu(), sl.cpu(), scale)
+    torch.testing.assert_close(out.view(B, Hq, D).cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(kc1.float(), kc2.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(vc1.float(), vc2.float(), atol=0, rtol=0)
+    assert out[4].float().abs().max().item() == 0.0
+
+
+@pytest.fixture(scope="module")
+def llama_small():
+    from xgserve.models import build_model, get_config
+    cfg = replace(get_config("llama3-8b"), num_layers=2, name="llama3-8b-2l")
+    return build_model(cfg, device="cuda:0", seed=3)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_decode_step_logits_match_reference(llama_small, fused, monkeypatch):
+    """One eager pure-decode step through the fused (or unfused) layer chain vs the
+    dense fp32 reference forward with the same weights."""
+    import xgserve.models.llama as ll
+    from xgserve.engine import EngineConfig, LLMEngine, SamplingParams
+    from xgserve.models.reference import reference_logits
+    monkeypatch.setattr(ll, "FUSED_DECODE", fused)
+    assert llama_small._fused_ok and llama_small.norms_folded
+    eng = LLMEngine(EngineConfig(model=llama_small.cfg.name, device="cuda:0", num_blocks=256, max_num_seqs=8,
+                                 max_num_batched_tokens=1024, max_model_len=512, use_graphs=False),
+                    model=llama_small)
+    eng.runner.capture_logits = True
+    prompt = [128000] + list(range(700, 790))
+    eng.add_request("d", prompt, SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True))
+    toks = []
+    while eng.has_work():
+        for o in eng.step():
+            toks += o.new_token_ids
+    assert len(toks) == 2
+    got = eng.runner.last_logits[-1]
+    ref = reference_logits(llama_small, prompt + toks[:1])[-1].float().cpu()
+    assert float((got - ref).norm() / ref.norm()) < 2e-2
+
+
+def test_fused_batch_decode_matches_unfused(llama_small, monkeypatch):
+    """A 5-sequence greedy decode (graphs on): the first decode token of every
+    sequence from the fused chain matches the unfused chain's (bf16 rounding order
+    differs, so one near-tie flip is tolerated)."""
+    import xgserve.models.llama as ll
+    from xgserve.engine import EngineConfig, LLMEngine, SamplingParams
+    prompts = [[128000] + list(range(1200 + 9 * i, 1260 + 4 * i)) for i in range(5)]
+    sp = SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True)
+    outs = {}
+    for fused in (True, False):
+        monkeypatch.setattr(ll, "FUSED_DECODE", fused)
+        eng = LLMEngine(EngineConfig(model=llama_small.cfg.name, device="cuda:0", num_blocks=256, max_num_seqs=8,
+                                     max_num_batched_tokens=1024, max_model_len=512, graph_batch_sizes=[1, 2, 4, 8]),
+                        model=llama_small)
+        outs[fused] = eng.generate(prompts, sp)
+    agree = sum(a[1] == b[1] for a, b in zip(outs[True], outs[False]))
+    assert agree >= 4, outs

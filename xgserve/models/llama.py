@@ -20,6 +20,7 @@ fused_add_rmsnorm -> gate_up GEMM -> SiLU-gate (K3) -> down GEMM -> AR.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -29,13 +30,31 @@ import torch.nn.functional as F
 from .. import ops
 from ..parallel import comm
 from ..parallel.state import get_state
-from ..ops.linear import MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, m64_linear, m64_plan, pick_split, skinny_linear
+from ..ops.linear import (MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, ResidWorkspace, RowStats, m64_linear,
+                          m64_norm_linear, m64_plan, m64_resid_linear, pick_split, skinny_linear)
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
 from .config import ModelConfig
 
 
 FAST_M_SMALL = 16   # tokens per step handled entirely by the streaming skinny GEMM
 FAST_M_SLAB = 64    # tokens per step for the O-projection slab kernel
+# Fused decode layer (dense Llama, TP=1, pure-decode steps of <= 64 tokens): the
+# RMSNorms become GEMM epilogue row scales (norm weights folded into W), the
+# residual adds + norm statistics run inside the O / down GEMM launches and the
+# QKV reduce + RoPE + KV append inside the attention prologue: 4 GEMM launches +
+# 1 attention launch per layer instead of 9. XGS_FUSED_DECODE=0 restores the
+# unfused chain (A/B measurements, tests).
+FUSED_DECODE = os.environ.get("XGS_FUSED_DECODE", "1") != "0"
+
+
+@torch.no_grad()
+def _fold_norm(w: torch.Tensor, norm: torch.Tensor) -> None:
+    """W[:, k] *= norm[k] (one bf16 rounding), norm <- 1: rmsnorm(x, g) @ W^T ==
+    rmsnorm(x, 1) @ (W diag(g))^T exactly in real arithmetic."""
+    if bool((norm == 1).all()):
+        return
+    w.copy_((w.float() * norm.float()[None, :]).to(w.dtype))
+    norm.fill_(1.0)
 
 
 def _p(t: torch.Tensor) -> nn.Parameter:
@@ -209,6 +228,21 @@ class LlamaLayer(nn.Module):
         h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
         return self.mlp(h), residual
 
+    def forward_fused(self, resid: torch.Tensor, stats: RowStats, meta: AttnMeta,
+                      kv: Tuple[torch.Tensor, torch.Tensor], cos_sin: torch.Tensor, ws: ResidWorkspace,
+                      site: int) -> RowStats:
+        """Fused decode layer: QKV GEMM (input norm as a row scale) -> attention (QKV
+        reduce + RoPE + KV append in its prologue) -> O GEMM (+ residual, + post-norm
+        statistics) -> gate_up GEMM (post-norm row scale, SiLU-gate) -> down GEMM
+        (+ residual, + next statistics). `resid` (bf16 [T, H]) is updated in place;
+        returns the statistics of the new residual for the next layer."""
+        eps = self.cfg.norm_eps
+        pqkv = m64_norm_linear(resid, self.qkv, MODE_PARTIAL, stats, eps)
+        a = self.attn.fused_decode(pqkv, meta, kv, cos_sin)
+        st = m64_resid_linear(a, self.o, resid, ws, site, eps)
+        act = m64_norm_linear(resid, self.gate_up, MODE_SILU, st, eps)
+        return m64_resid_linear(act, self.down, resid, ws, site + 1, eps)
+
 
 class LlamaForCausalLM(nn.Module):
     def __init__(self, cfg: ModelConfig, device="cpu", dtype=torch.bfloat16, tp: Optional[int] = None,
@@ -231,6 +265,41 @@ class LlamaForCausalLM(nn.Module):
         self.cos_sin = ops.build_cos_sin(cfg.head_dim, cfg.max_position, cfg.rope_theta, cfg.rope_scaling,
                                          device=device)
         self.num_kv_heads_local = self.layers[0].Hkv
+        l0 = self.layers[0]
+        self.norms_folded = False
+        self._fused_ok = (self.tp == 1 and self.device.type == "cuda" and not l0.moe and l0.m64_ok
+                          and l0.m64_silu_ok and cfg.head_dim == 128 and l0.Hq % l0.Hkv == 0
+                          and l0.Hq // l0.Hkv in (1, 2, 4, 8) and H % 1024 == 0 and H // 1024 <= 8)
+        self._fused_small_ok = self._fused_ok and l0.m64_small_ok
+        self._fused_ws = ResidWorkspace(2 * cfg.num_layers + 1, FAST_M_SLAB, H, device) if self._fused_ok else None
+
+    @torch.no_grad()
+    def fold_norms(self):
+        """Fold every RMSNorm weight into the input columns of the projection that
+        consumes it and reset the norm to 1, so the decode GEMMs can apply the norm
+        as a per-row epilogue scale of the raw residual stream. Exact in real
+        arithmetic: every other path (prefill, TP, the fp32 reference) computes the
+        same function. MoE post-attention norms stay (router and experts read them)."""
+        for l in self.layers:
+            _fold_norm(l.qkv, l.input_norm)
+            if not l.moe:
+                _fold_norm(l.gate_up, l.post_norm)
+        self.norms_folded = True
+
+    def fused_decode_ok(self, meta: AttnMeta) -> bool:
+        T = meta.num_tokens
+        if not (FUSED_DECODE and self._fused_ok and self.norms_folded) or T != meta.num_decodes or not 0 < T <= 64:
+            return False
+        return T > FAST_M_SMALL or self._fused_small_ok
+
+    def _forward_fused(self, input_ids: torch.Tensor, meta: AttnMeta,
+                       kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+        ws = self._fused_ws
+        resid = F.embedding(input_ids, self.embed)
+        st = RowStats(ops.row_sumsq(resid, ws.ss[0]), 1, meta.num_tokens)
+        for i, layer in enumerate(self.layers):
+            st = layer.forward_fused(resid, st, meta, kv_caches[i], self.cos_sin, ws, 2 * i + 1)
+        return ops.rmsnorm(resid, self.norm, self.cfg.norm_eps)
 
     def set_moe_comm(self, mode: str):
         for l in self.layers:
@@ -257,6 +326,8 @@ class LlamaForCausalLM(nn.Module):
     # ------------------------------------------------------------------ forward
     def forward(self, input_ids: torch.Tensor, meta: AttnMeta,
                 kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+        if self.fused_decode_ok(meta):
+            return self._forward_fused(input_ids, meta, kv_caches)
         x = F.embedding(input_ids, self.embed)
         residual = None
         for i, layer in enumerate(self.layers):

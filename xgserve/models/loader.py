@@ -37,6 +37,8 @@ def build_model(cfg: ModelConfig, device="cpu", dtype: Optional[torch.dtype] = N
         load_checkpoint(m, checkpoint)
     else:
         m.random_init(seed)
+    if hasattr(m, "fold_norms"):
+        m.fold_norms()  # RMSNorm weights into the projections (fused decode layer)
     m.eval()
     return m
 

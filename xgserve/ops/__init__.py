@@ -4,22 +4,22 @@ and PyTorch reference implementations (CPU tensors, tests).
 Every GPU op here launches a hand-written kernel from csrc/kernels; the
 `*_ref` functions are the fp32 PyTorch references the kernel tests compare to.
 """
-from .norm import rmsnorm, fused_add_rmsnorm, layernorm, rmsnorm_ref, fused_add_rmsnorm_ref, layernorm_ref
+from .norm import rmsnorm, fused_add_rmsnorm, layernorm, rmsnorm_ref, fused_add_rmsnorm_ref, layernorm_ref, row_sumsq
 from .activation import silu_and_mul, gelu_tanh, silu_and_mul_ref, gelu_tanh_ref
 from .rope import RotaryCache, rope_cache, rope_cache_ref, build_cos_sin, rope_cache_partials
 from . import linear
 from .linear import skinny_linear, PendingSum
-from .attention import (decode_attention, prefill_attention, decode_attention_ref,
+from .attention import (decode_attention, decode_attention_fused, prefill_attention, decode_attention_ref,
                         prefill_attention_ref, choose_num_splits)
 from .sampling import argmax_logprob, sample_tokens, argmax_logprob_ref, segment_sum
 from .moe import moe_topk_softmax, moe_route, moe_align, moe_forward_ref, fused_moe
 from ._native import available as native_available
 
 __all__ = [
-    "rmsnorm", "fused_add_rmsnorm", "layernorm", "rmsnorm_ref", "fused_add_rmsnorm_ref", "layernorm_ref",
+    "rmsnorm", "fused_add_rmsnorm", "layernorm", "row_sumsq", "rmsnorm_ref", "fused_add_rmsnorm_ref", "layernorm_ref",
     "silu_and_mul", "gelu_tanh", "silu_and_mul_ref", "gelu_tanh_ref",
     "RotaryCache", "rope_cache", "rope_cache_ref", "build_cos_sin",
-    "decode_attention", "prefill_attention", "decode_attention_ref", "prefill_attention_ref", "choose_num_splits",
+    "decode_attention", "decode_attention_fused", "prefill_attention", "decode_attention_ref", "prefill_attention_ref", "choose_num_splits",
     "argmax_logprob", "sample_tokens", "argmax_logprob_ref", "segment_sum",
     "moe_topk_softmax", "moe_route", "moe_align", "moe_forward_ref", "fused_moe",
     "native_available",

@@ -120,6 +120,36 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     return out
 
 
+def decode_attention_fused(pend, positions: torch.Tensor, slot_mapping: torch.Tensor, cos_sin: torch.Tensor,
+                           k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
+                           seq_lens: torch.Tensor, num_heads: int, scale: float, num_splits: int = 1,
+                           workspace: Optional[DecodeWorkspace] = None, apply_rope: bool = True,
+                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Paged decode attention on the QKV projection's split-K partials (PendingSum
+    [S, B, (Hq + 2 Hkv) D]): each workgroup's prologue reduces its (sequence, kv
+    head) slice, applies RoPE and appends the new K/V row to the cache -- the work
+    of rope_cache_partials without its launch or the q round trip. -> [B, Hq * D]."""
+    S, B, W = pend.part.shape
+    Hkv, bs, D = k_cache.shape[1], k_cache.shape[2], k_cache.shape[3]
+    Hq = num_heads
+    assert W == (Hq + 2 * Hkv) * D and pend.part.is_contiguous()
+    assert block_tables.dtype == torch.int32 and seq_lens.dtype == torch.int32 and block_tables.stride(1) == 1
+    assert positions.dtype == torch.int32 and slot_mapping.dtype == torch.int32 and cos_sin.dtype == torch.float32
+    if out is None:
+        out = torch.empty(B, Hq * D, dtype=torch.bfloat16, device=pend.part.device)
+    po = pl = 0
+    if num_splits > 1:
+        if workspace is None or workspace.max_splits < num_splits or workspace.part_lse.numel() < B * Hq * num_splits:
+            workspace = DecodeWorkspace(B, Hq, D, num_splits, pend.part.device)
+        po, pl = workspace.part_out.data_ptr(), workspace.part_lse.data_ptr()
+    kernels().decode_attention_fq(pend.part.data_ptr(), S, positions.data_ptr(), cos_sin.data_ptr(),
+                                  slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                  block_tables.data_ptr(), block_tables.stride(0), seq_lens.data_ptr(), po, pl,
+                                  out.data_ptr(), out.stride(0), B, Hq, Hkv, D, bs, float(scale), int(num_splits),
+                                  1 if apply_rope else 0, stream_ptr())
+    return out
+
+
 def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                       query_start_loc: torch.Tensor, seq_lens: torch.Tensor, max_q_len: int, scale: float,
                       out: Optional[torch.Tensor] = None) -> torch.Tensor:

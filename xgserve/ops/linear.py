@@ -201,6 +201,92 @@ def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split
     return out
 
 
+# ---------------------------------------------------------------------------- fused decode layer
+MODE_RESID = 3
+# GG_RESID (residual add + next-norm statistics inside the GEMM launch) reduces a
+# column tile in-launch while its split-K slab (S x M x columns fp32) is at most
+# this many bytes -- the tile's last arriver reads it serially (~1 us per 16 KB,
+# cdna_hip_programming.md §5); larger slabs (M ~ 64) go through the wide
+# add_partials_resid kernel instead.
+RESID_INLAUNCH_MAX_BYTES = 32 << 10
+
+
+@dataclass
+class RowStats:
+    """RMSNorm statistics of the rows of a residual stream: `n` partial sums of
+    squares per row at ss[j * stride + m], added in order by the consuming GEMM."""
+    ss: torch.Tensor
+    n: int
+    stride: int
+
+
+class ResidWorkspace:
+    """Scratch of the fused decode layer, sized once per model (graph-capture safe).
+    Statistics site 0 is the embedding; sites 2i+1 / 2i+2 follow layer i's
+    attention / MLP residual adds."""
+
+    MAX_TILES = 64  # per-tile statistics a consumer can combine (ss_n <= 64, M <= 16)
+    IN_LAUNCH_MAX_M = 16
+
+    def __init__(self, n_sites: int, max_m: int, H: int, device):
+        self.max_m = max_m
+        rows = max(self.MAX_TILES * self.IN_LAUNCH_MAX_M, max(1, H // 1024) * max_m)
+        self.ss = torch.zeros(n_sites, rows, dtype=torch.float32, device=device)
+        # arrival tickets: zero here, and every ticket winner re-arms its word
+        self.counters = torch.zeros(n_sites, self.MAX_TILES, dtype=torch.int32, device=device)
+
+
+def m64_norm_linear(x: torch.Tensor, w: torch.Tensor, mode: int, stats: RowStats, eps: float,
+                    out: Optional[torch.Tensor] = None):
+    """gemm_m64g on the raw residual stream x with its RMSNorm applied as a per-row
+    epilogue scale rsqrt(sum_sq / K + eps) (norm weight folded into w): PendingSum
+    (MODE_PARTIAL) or bf16 silu(gate) * up (MODE_SILU)."""
+    M, K = x.shape
+    N = w.shape[0]
+    plan = m64_plan(M, N, K, mode)
+    if plan is None:
+        raise ValueError(f"gemm_m64g: unsupported shape M={M} N={N} K={K} mode={mode}")
+    nw, S, cfg = plan
+    k = kernels()
+    st = (stats.ss.data_ptr(), stats.n, stats.stride, float(eps))
+    if mode == MODE_PARTIAL:
+        part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+        k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg, *st,
+                       0, 0, 0, stream_ptr())
+        return PendingSum(part, S)
+    if out is None:
+        out = torch.empty(M, N // 2 if mode == MODE_SILU else N, dtype=torch.bfloat16, device=x.device)
+    k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, cfg, *st, 0, 0, 0,
+                   stream_ptr())
+    return out
+
+
+def m64_resid_linear(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace, site: int,
+                     eps: float) -> RowStats:
+    """resid += x . w^T (bf16 residual stream, in place) on gemm_m64g; returns the
+    new residual's RMSNorm statistics. Small split-K slabs are reduced inside the
+    GEMM launch (GG_RESID), large ones by the wide add_partials_resid kernel."""
+    M, K = x.shape
+    N = w.shape[0]
+    plan = m64_plan(M, N, K, MODE_PARTIAL)
+    if plan is None or N % 1024 or tuple(resid.shape) != (M, N):
+        raise ValueError(f"gemm_m64g resid: unsupported shape M={M} N={N} K={K}")
+    nw, S, cfg = plan
+    k = kernels()
+    part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+    ss = ws.ss[site]
+    cols = 16 * nw * M64G_CFGS[cfg][0]
+    ntiles = N // cols
+    if (S * M * cols * 4 <= RESID_INLAUNCH_MAX_BYTES and ntiles <= ws.MAX_TILES
+            and M <= ws.IN_LAUNCH_MAX_M):
+        k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_RESID, nw, cfg, 0, 0, 0,
+                       float(eps), resid.data_ptr(), ss.data_ptr(), ws.counters[site].data_ptr(), stream_ptr())
+        return RowStats(ss, ntiles, M)  # one partial sum per column tile
+    k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg, stream_ptr())
+    k.add_partials_resid(part.data_ptr(), S, M, resid.data_ptr(), ss.data_ptr(), N, stream_ptr())
+    return RowStats(ss, N // 1024, M)  # one partial sum per 1024-column chunk
+
+
 def interleave_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
     """[F, H] x2 -> [2F, H] in blocks of 16 rows: g0..g15 u0..u15 g16.. (F % 16 == 0)."""
     F, H = gate.shape

@@ -72,6 +72,18 @@ def fused_add_rmsnorm(x, residual: torch.Tensor, w: torch.Tensor, eps: float,
     return out, residual
 
 
+def row_sumsq(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out.view(-1)[t] = sum_k x[t, k]^2 (fp32) for bf16 rows [T, H]: the RMSNorm
+    statistic the fused decode GEMMs apply as an epilogue row scale."""
+    T, H = x.shape
+    if not use_native(x):
+        out.view(-1)[:T] = x.float().pow(2).sum(-1)
+        return out
+    assert x.is_contiguous() and x.dtype == torch.bfloat16 and out.dtype == torch.float32
+    kernels().row_sumsq(x.data_ptr(), T, H, out.data_ptr(), stream_ptr())
+    return out
+
+
 def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> torch.Tensor:
     if not use_native(x):
         return layernorm_ref(x, w, b, eps)
