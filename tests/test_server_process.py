@@ -83,12 +83,19 @@ def test_process_replica_crash_restart():
     assert run_with_client(cfg, fn, timeout=120)
 
 
-@pytest.mark.parametrize("model,moe_comm", [("llama-tiny-gqa8", "alltoall"), ("mixtral-tiny", "alltoall"),
-                                            ("mixtral-tiny", "allreduce")])
-def test_tp2_process_replica_gloo_matches_tp1(tmp_path, model, moe_comm):
+@pytest.mark.parametrize("model,moe_comm,overlap", [("llama-tiny-gqa8", "alltoall", False),
+                                                    ("llama-tiny-gqa8", "alltoall", True),
+                                                    ("mixtral-tiny", "alltoall", False),
+                                                    ("mixtral-tiny", "allreduce", False)])
+def test_tp2_process_replica_gloo_matches_tp1(tmp_path, monkeypatch, model, moe_comm, overlap):
     """TP=2 (two processes over gloo; leader broadcasts step plans; Mixtral
     experts split 4+4 with all-to-all or all-reduce combine) serving HTTP gives
-    the same greedy text as a TP=1 engine on the same safetensors checkpoint."""
+    the same greedy text as a TP=1 engine on the same safetensors checkpoint.
+    `overlap`: every step takes the chunk-pipelined all-reduce path
+    (LlamaLayer._forward_tp_overlap, 3 token chunks, async all-reduces)."""
+    if overlap:  # read by the replica processes at import
+        monkeypatch.setenv("XGS_TP_OVERLAP_MIN_TOKENS", "1")
+        monkeypatch.setenv("XGS_TP_OVERLAP_CHUNKS", "3")
     import torch
     from xgserve.engine import EngineConfig, LLMEngine, SamplingParams
     from xgserve.models import build_model, get_config, save_checkpoint

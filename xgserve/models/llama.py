@@ -45,6 +45,12 @@ FAST_M_SLAB = 64    # tokens per step for the O-projection slab kernel
 # 1 attention launch per layer instead of 9. XGS_FUSED_DECODE=0 restores the
 # unfused chain (A/B measurements, tests).
 FUSED_DECODE = os.environ.get("XGS_FUSED_DECODE", "1") != "0"
+# TP > 1 prefill-sized steps: the row-parallel all-reduces are pipelined over this
+# many token chunks and overlapped with the next chunk's GEMMs (RCCL stream); a
+# 2k-token 8B step moves 16 MiB per all-reduce -- ~100 us on 7 xGMI links, a
+# GEMM-sized share of the layer. XGS_TP_OVERLAP_CHUNKS=1 disables it.
+TP_OVERLAP_CHUNKS = int(os.environ.get("XGS_TP_OVERLAP_CHUNKS", "2"))
+TP_OVERLAP_MIN_TOKENS = int(os.environ.get("XGS_TP_OVERLAP_MIN_TOKENS", "256"))
 
 
 @torch.no_grad()
@@ -224,9 +230,42 @@ class LlamaLayer(nn.Module):
             return self.mlp(h), residual
         qkv = F.linear(h, self.qkv)
         a = self.attn(qkv, meta, kv, cos_sin)
+        if self.tp > 1 and not self.moe and T >= TP_OVERLAP_MIN_TOKENS and TP_OVERLAP_CHUNKS > 1:
+            return self._forward_tp_overlap(a, residual)
         o = self._ar(F.linear(a, self.o))
         h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
         return self.mlp(h), residual
+
+    def _forward_tp_overlap(self, a: torch.Tensor, residual: torch.Tensor):
+        """Row-parallel half of a TP layer for prefill-sized steps, pipelined over
+        token chunks so every all-reduce runs (on RCCL's stream) under the GEMMs of
+        the following chunk: O GEMM(c) -> AR(c) async; then per chunk: wait AR(c)
+        -> add + post-norm -> gate_up -> SiLU-gate -> down(c) -> AR(c) async. Only
+        the last chunk's down all-reduce is exposed. Everything after attention is
+        per-token, so the chunked result equals the unchunked one exactly."""
+        T, H = residual.shape
+        eps = self.cfg.norm_eps
+        n = TP_OVERLAP_CHUNKS
+        step = (T + n - 1) // n
+        if step > 64:
+            step = (step + 63) // 64 * 64  # GEMM-friendly row blocks
+        bounds = [(lo, min(T, lo + step)) for lo in range(0, T, step)]
+        o = torch.empty(T, H, dtype=a.dtype, device=a.device)
+        works = []
+        for lo, hi in bounds:
+            torch.mm(a[lo:hi], self.o.t(), out=o[lo:hi])
+            works.append(comm.tp_all_reduce_async(o[lo:hi]))
+        d = torch.empty(T, H, dtype=a.dtype, device=a.device)
+        dworks = []
+        for (lo, hi), w in zip(bounds, works):
+            w.wait()
+            hc, _ = ops.fused_add_rmsnorm(o[lo:hi], residual[lo:hi], self.post_norm, eps)
+            act = ops.silu_and_mul(F.linear(hc, self.gate_up), interleave16=True)
+            torch.mm(act, self.down.t(), out=d[lo:hi])
+            dworks.append(comm.tp_all_reduce_async(d[lo:hi]))
+        for w in dworks:
+            w.wait()
+        return d, residual
 
     def forward_fused(self, resid: torch.Tensor, stats: RowStats, meta: AttnMeta,
                       kv: Tuple[torch.Tensor, torch.Tensor], cos_sin: torch.Tensor, ws: ResidWorkspace,

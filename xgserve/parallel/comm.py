@@ -42,6 +42,23 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+class _Done:
+    def wait(self):
+        return True
+
+
+def tp_all_reduce_async(x: torch.Tensor):
+    """In-place all-reduce of x over the TP group without blocking the compute
+    stream: RCCL runs it on its own stream behind an event on the current one;
+    `.wait()` on the returned handle makes the current stream (not the host)
+    wait for it. Used to overlap prefill-sized all-reduces with the GEMMs of the
+    next token chunk (LlamaLayer._forward_tp_overlap)."""
+    s = get_state()
+    if s.tp_size == 1:
+        return _Done()
+    return dist.all_reduce(x, group=s.tp_group, async_op=True)
+
+
 def tp_all_gather_lastdim(x: torch.Tensor) -> torch.Tensor:
     """[.., n] sharded over TP ranks -> [.., n*tp] (rank-major)."""
     s = get_state()
