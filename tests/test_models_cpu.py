@@ -32,3 +32,16 @@ def test_fold_norms_keeps_moe_post_norm():
     m.fold_norms()
     assert all(bool((layer.post_norm == 1.5).all()) for layer in m.layers)  # router + experts read it
     torch.testing.assert_close(reference_logits(m, toks), before, atol=1e-4, rtol=1e-4)
+
+
+def test_engine_rejects_out_of_vocab_prompt_ids():
+    """An id outside the embedding table must never reach the GPU gather."""
+    import pytest
+    from xgserve.engine import EngineConfig, LLMEngine, SamplingParams
+    eng = LLMEngine(EngineConfig(model="llama-tiny", device="cpu", dtype="float32", num_blocks=32, max_num_seqs=2,
+                                 max_num_batched_tokens=64, use_graphs=False))
+    V = eng.mcfg.vocab_size
+    for bad in ([1, V], [-1, 2]):
+        with pytest.raises(ValueError, match="token ids"):
+            eng.add_request("x", bad, SamplingParams(max_tokens=2))
+    eng.add_request("ok", [1, V - 1], SamplingParams(max_tokens=2))

@@ -118,9 +118,14 @@ class LLMEngine:
         sc.max_prefill_seqs = cfg.max_prefill_seqs
         sc.eos_ids = list(self.mcfg.eos_token_ids)
         self.sched = R.StepScheduler(sc)
+        # decode graphs capture the TP collectives: RCCL (and the IPC all-reduce) can be
+        # captured into a HIP graph, gloo (CPU-staged) cannot -> eager decode there
+        use_graphs = cfg.use_graphs and (st.tp_size == 1 or st.backend == "nccl")
+        if cfg.use_graphs and not use_graphs:
+            log.info("TP over %s: decode graphs disabled (collectives not capturable)", st.backend)
         self.runner = ModelRunner(self.model, block_size=cfg.block_size, num_blocks=num_blocks,
                                   max_num_seqs=cfg.max_num_seqs, max_num_batched_tokens=cfg.max_num_batched_tokens,
-                                  max_model_len=self.max_model_len, use_graphs=cfg.use_graphs,
+                                  max_model_len=self.max_model_len, use_graphs=use_graphs,
                                   graph_batch_sizes=cfg.graph_batch_sizes, is_driver=self.is_driver)
         self.runner.capture_graphs()
         H = self.mcfg.hidden_size
@@ -182,6 +187,10 @@ class LLMEngine:
         prompt_ids = [int(t) for t in prompt_ids]
         if not prompt_ids:
             raise ValueError("empty prompt")
+        V = self.mcfg.vocab_size
+        if min(prompt_ids) < 0 or max(prompt_ids) >= V:
+            # an id outside the embedding table would be an out-of-bounds gather on the GPU
+            raise ValueError(f"prompt token ids must be in [0, {V}), got [{min(prompt_ids)}, {max(prompt_ids)}]")
         max_tokens = params.max_tokens
         if kind != RequestType.Embeddings:
             max_tokens = min(max_tokens, self.max_model_len - len(prompt_ids))
