@@ -29,6 +29,8 @@
 //     waves of a row, so each lane holds <= 8 values) and combined in the epilogue
 //     by xor-shuffles (+ one LDS step): their latency hides under the weight
 //     stream instead of extending the tail.
+#include <cstdlib>
+
 #include "glds.h"
 
 namespace xgk {
@@ -149,23 +151,25 @@ __device__ __forceinline__ void m64g_resid_tail(const float* __restrict__ part, 
 //       short N still puts a workgroup on every CU
 //   KC  k per chunk (128: 256-B rows, 1 workgroup/CU; 64: 128-B rows, 2-3 per CU)
 //   NT  non-temporal weight DMA (streamed once; keeps x resident in L2)
-template <int NW, int WV, int KC, bool NT>
+//   MT  16-row x tiles (4: 16 < M <= 64; 1: M <= 16 -- a quarter of the x DMA and
+//       LDS per chunk, so the weight stream owns the load path at batch 1)
+template <int NW, int WV, int KC, bool NT, int MT>
 __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* __restrict__ x, int M, int K,
                                                                const uint16_t* __restrict__ w, int N,
                                                                float* __restrict__ part, uint16_t* __restrict__ out,
                                                                int mode, M64Epi epi) {
-  constexpr int MT = 4;
   constexpr int RB = KC * 2;                     // bytes per LDS row
   constexpr int GPR = KC / 8;                    // 16-B granules per row
   constexpr int RPI = 1024 / RB;                 // rows per DMA instruction (64 lanes x 16 B)
-  constexpr int XBYTES = 64 * RB;
-  constexpr int XI = 64 / RPI / WV;              // x DMA instructions per wave per chunk
+  constexpr int XROWS = 16 * MT;
+  constexpr int XBYTES = XROWS * RB;
+  constexpr int XI = XROWS / RPI / WV;           // x DMA instructions per wave per chunk
   constexpr int WROWS = 16 * NW;                 // weight rows per wave
   constexpr int WI = WROWS / RPI;                // weight DMA instructions per wave per chunk
   constexpr int WBYTES = WROWS * RB;             // per wave per slot
   constexpr int SLOT = XBYTES + WV * WBYTES;
   constexpr int G = XI + WI;
-  static_assert(XI >= 1 && WI >= 1 && 64 % (RPI * WV) == 0, "bad m64g geometry");
+  static_assert(XI >= 1 && WI >= 1 && XROWS % (RPI * WV) == 0, "bad m64g geometry");
   __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
@@ -188,7 +192,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   const uint16_t* xsrc[XI];
 #pragma unroll
   for (int i = 0; i < XI; ++i) {
-    const int r = RPI * (wid * XI + i) + dr;     // x row 0..63
+    const int r = RPI * (wid * XI + i) + dr;     // x row 0..XROWS-1
     xsrc[i] = x + static_cast<int64_t>(min(r, M - 1)) * K + k0 + 8 * (dj ^ (r & (GPR - 1)));
   }
 
@@ -245,6 +249,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   if (has_ss) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+      if (!wide_ss && (i >> 1) >= MT) break;
       const int mt = wide_ss ? 0 : i >> 1, q = wide_ss ? i : i & 1;
       const int j = wide_ss ? 4 * wid + g + 4 * WV * q : g + 4 * q;
       ssv[i] = epi.ss_in[min(j, epi.ss_n - 1) * epi.ss_stride + min(16 * mt + li, M - 1)];
@@ -545,22 +550,44 @@ int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, i
 
 // cfg: 0 = (4 waves, KC 128), 1 = (4, 128, nt), 2 = (4, 64), 3 = (4, 64, nt),
 //      4 = (2, 64), 5 = (2, 64, nt), 6 = (2, 128, nt)
+// M <= 16 takes the one-x-tile kernel (MT = 1) except for the 4-wave KC-64 configs,
+// whose 16 x rows would be less than one DMA instruction per wave.
+// XGS_M64G_MT1=0 keeps MT = 4 everywhere (A/B).
+static bool m64g_mt1_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("XGS_M64G_MT1");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 template <int NW>
 static void launch_m64g(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N,
                         float* part, uint16_t* out, int mode, const M64Epi& epi) {
-#define XGK_M64G(WV, KC, NT)                                                                                     \
-  hipLaunchKernelGGL((gemm_m64g_kernel<NW, WV, KC, NT>), grid, dim3(64 * WV), 0, st, x, M, K, w, N, part, out, \
+  const bool mt1 = M <= 16 && cfg != 2 && cfg != 3 && m64g_mt1_enabled();
+#define XGK_M64G(WV, KC, NT)                                                                                         \
+  do {                                                                                                               \
+    if (mt1)                                                                                                         \
+      hipLaunchKernelGGL((gemm_m64g_kernel<NW, WV, KC, NT, 1>), grid, dim3(64 * WV), 0, st, x, M, K, w, N, part, out, \
+                         mode, epi);                                                                                 \
+    else                                                                                                             \
+      hipLaunchKernelGGL((gemm_m64g_kernel<NW, WV, KC, NT, 4>), grid, dim3(64 * WV), 0, st, x, M, K, w, N, part, out, \
+                         mode, epi);                                                                                 \
+  } while (0)
+#define XGK_M64G4(WV, KC, NT)                                                                                      \
+  hipLaunchKernelGGL((gemm_m64g_kernel<NW, WV, KC, NT, 4>), grid, dim3(64 * WV), 0, st, x, M, K, w, N, part, out, \
                      mode, epi)
   switch (cfg) {
     case 1: XGK_M64G(4, 128, true); break;
-    case 2: XGK_M64G(4, 64, false); break;
-    case 3: XGK_M64G(4, 64, true); break;
+    case 2: XGK_M64G4(4, 64, false); break;
+    case 3: XGK_M64G4(4, 64, true); break;
     case 4: XGK_M64G(2, 64, false); break;
     case 5: XGK_M64G(2, 64, true); break;
     case 6: XGK_M64G(2, 128, true); break;
     default: XGK_M64G(4, 128, false); break;
   }
 #undef XGK_M64G
+#undef XGK_M64G4
 }
 
 int m64g_cfg_waves(int cfg) { return cfg >= 4 ? 2 : 4; }
