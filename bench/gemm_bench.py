@@ -21,7 +21,9 @@ SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "dow
           # Llama-3-70B (TP1 / TP8) and Llama-3-8B TP2 shards
           "qkv70": (10240, 8192), "o70": (8192, 8192), "gate_up70": (57344, 8192), "down70": (8192, 28672),
           "qkv70t8": (1280, 8192), "o70t8": (8192, 1024), "gate_up70t8": (7168, 8192), "down70t8": (8192, 3584),
-          "qkv8t2": (3072, 4096), "o8t2": (4096, 2048), "gate_up8t2": (14336, 4096), "down8t2": (4096, 7168)}
+          "qkv8t2": (3072, 4096), "o8t2": (4096, 2048), "gate_up8t2": (14336, 4096), "down8t2": (4096, 7168),
+          # gate_up shapes as plain split-K partial GEMMs (what a split SiLU epilogue would stream)
+          "gate_up_p": (28672, 4096), "gate_up70_p": (57344, 8192)}
 
 
 def timeit(fns, iters=30, warm=5):
@@ -65,7 +67,7 @@ def main():
             rows = []
             us = timeit([lambda w=w: F.linear(x, w) for w in ws])
             rows.append(("hipblaslt", us, None))
-            mode = L.MODE_SILU if name.startswith("gate_up") else (L.MODE_BF16 if name == "lm_head" else L.MODE_PARTIAL)
+            mode = L.MODE_SILU if name.startswith("gate_up") and not name.endswith("_p") else (L.MODE_BF16 if name == "lm_head" else L.MODE_PARTIAL)
             if M <= 16:
                 for S in ((1,) if mode != L.MODE_PARTIAL else (1, 2, 4, 7, 8, 14, 16)):
                     if K % (S * 256) or (mode == L.MODE_PARTIAL and N % 64):
@@ -115,7 +117,7 @@ def m64g_sweep(a):
         nbytes = N * K * 2
         copies = max(2, min(8, (1 << 30) // nbytes + 1))
         ws = [(torch.randn(N, K, device="cuda") * 0.02).bfloat16() for _ in range(copies)]
-        mode = L.MODE_SILU if name.startswith("gate_up") else (L.MODE_BF16 if name == "lm_head" else L.MODE_PARTIAL)
+        mode = L.MODE_SILU if name.startswith("gate_up") and not name.endswith("_p") else (L.MODE_BF16 if name == "lm_head" else L.MODE_PARTIAL)
         for M in a.M:
             x = torch.randn(M, K, device="cuda").bfloat16()
             if mode == L.MODE_SILU:

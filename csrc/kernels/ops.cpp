@@ -46,6 +46,7 @@ void argmax_logprob(const void*, int, int64_t, int, int, int32_t*, float*, hipSt
 void sample_tokens(const void*, int, int64_t, int, int, const float*, const float*, const int32_t*, const uint64_t*,
                    uint64_t, int32_t*, float*, hipStream_t);
 void segment_sum(const uint16_t*, int, const int32_t*, const int32_t*, float*, int, hipStream_t);
+void subst_tokens(int32_t*, const int32_t*, const int32_t*, int, hipStream_t);
 void moe_topk_softmax(const void*, int, int, int, int, int, float*, int32_t*, hipStream_t);
 void moe_align(const int32_t*, int, int, int, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
 int moe_combine(const void*, int, int, const int32_t*, const float*, uint16_t*, int, int, int, hipStream_t);
@@ -173,6 +174,10 @@ PYBIND11_MODULE(_kernels, m) {
     xgk::sample_tokens(P<const void>(logits), is_f32, stride, B, V, P<const float>(temps), P<const float>(top_ps),
                        P<const int32_t>(top_ks), P<const uint64_t>(seeds), step, P<int32_t>(tok), P<float>(lp), S(st));
     check(0, "sample_tokens");
+  });
+  m.def("subst_tokens", [](uintptr_t ids, uintptr_t src, uintptr_t prev, int n, uintptr_t st) {
+    xgk::subst_tokens(P<int32_t>(ids), P<const int32_t>(src), P<const int32_t>(prev), n, S(st));
+    check(0, "subst_tokens");
   });
   m.def("segment_sum", [](uintptr_t hidden, int H, uintptr_t cu, uintptr_t rows, uintptr_t out, int nseg,
                           uintptr_t st) {

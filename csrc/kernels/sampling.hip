@@ -262,4 +262,21 @@ void segment_sum(const uint16_t* hidden, int H, const int32_t* cu, const int32_t
   hipLaunchKernelGGL(segment_sum_kernel, dim3(S, gy), dim3(256), 0, st, hidden, H, cu, out_rows, out);
 }
 
+// Asynchronous scheduling: a step planned before the previous one finished has
+// placeholder ids for its decode rows; ids[i] <- prev[src[i]] (the previous step's
+// sampled token of that sequence) where src[i] >= 0. Runs first inside the decode
+// graph (src all -1 on ordinary steps: a no-op).
+__global__ void __launch_bounds__(256) subst_tokens_kernel(int32_t* __restrict__ ids, const int32_t* __restrict__ src,
+                                                           const int32_t* __restrict__ prev, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int s = src[i];
+    if (s >= 0) ids[i] = prev[s];
+  }
+}
+
+void subst_tokens(int32_t* ids, const int32_t* src, const int32_t* prev, int n, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(subst_tokens_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ids, src, prev, n);
+}
+
 }  // namespace xgk

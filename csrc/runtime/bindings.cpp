@@ -251,6 +251,17 @@ PYBIND11_MODULE(_runtime, m) {
                                          f.num_cached));
              return out;
            })
+      .def("lookahead", &StepScheduler::lookahead, py::arg("across_length_finish") = false)
+      .def("commit",
+           [](StepScheduler& s, py::array_t<int32_t, py::array::c_style | py::array::forcecast> tok) {
+             auto fin = s.commit(tok.data(), static_cast<int>(tok.size()));
+             py::list out;
+             for (const auto& f : fin)
+               out.append(py::make_tuple(f.id, static_cast<int>(f.reason), f.prompt_len, f.num_generated,
+                                         f.num_cached));
+             return out;
+           })
+      .def("num_inflight", &StepScheduler::num_inflight)
       .def("num_waiting", &StepScheduler::num_waiting)
       .def("num_running", &StepScheduler::num_running)
       .def("has_work", &StepScheduler::has_work)

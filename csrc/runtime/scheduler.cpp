@@ -145,10 +145,17 @@ bool StepScheduler::abort(int64_t id) {
     waiting_.erase(std::remove(waiting_.begin(), waiting_.end(), s), waiting_.end());
     release(*s, false);
   }
-  for (auto& p : plan_seqs_)
-    if (p == s) p = nullptr;
+  forget(s);
   seqs_.erase(it);
   return true;
+}
+
+void StepScheduler::forget(Sequence* s) {
+  for (auto& p : plan_seqs_)
+    if (p == s) p = nullptr;
+  for (auto& r : inflight_)
+    for (auto& p : r.seqs)
+      if (p == s) p = nullptr;
 }
 
 bool StepScheduler::set_draft(int64_t id, const std::vector<int32_t>& draft) {
@@ -270,6 +277,7 @@ const StepPlan& StepScheduler::schedule() {
   while (!waiting_.empty() && budget > 0 && static_cast<int>(running_.size()) < cfg_.max_num_seqs &&
          n_prefill < cfg_.max_prefill_seqs) {
     Sequence* s = waiting_.front();
+    if (s->tokens.back() == kPlaceholder) break;  // preempted by a lookahead plan: wait for commit()
     int matched_pages = 0;
     if (cfg_.enable_prefix_cache && s->blocks.empty() && s->num_computed == 0) {
       const int n = static_cast<int>(s->tokens.size());
@@ -342,6 +350,7 @@ int StepScheduler::check_stop(Sequence& s) {
 std::vector<FinishedSeq> StepScheduler::update(const int32_t* tokens, const int32_t* counts,
                                                int num_sample) {
   std::vector<FinishedSeq> done;
+  if (!inflight_.empty()) throw std::logic_error("update: lookahead plans must be committed first");
   if (num_sample != plan_.num_sample) throw std::invalid_argument("update: num_sample mismatch");
   int k = 0, si = 0;
   std::vector<Sequence*> finished;
@@ -379,8 +388,77 @@ std::vector<FinishedSeq> StepScheduler::update(const int32_t* tokens, const int3
     s->status = SeqStatus::Finished;
     running_.erase(std::remove(running_.begin(), running_.end(), s), running_.end());
     done.push_back(FinishedSeq{s->id, s->finish, s->prompt_len, s->num_generated(), s->num_cached});
-    for (auto& p : plan_seqs_)
-      if (p == s) p = nullptr;
+    forget(s);
+    seqs_.erase(s->id);
+  }
+  return done;
+}
+
+bool StepScheduler::lookahead(bool across_length_finish) {
+  const StepPlan& p = plan_;
+  if (p.num_seqs == 0 || p.num_decodes != p.num_seqs || p.num_sample != p.num_seqs) return false;
+  for (int i = 0; i < p.num_seqs; ++i) {
+    const Sequence* s = plan_seqs_[i];
+    if (s == nullptr) continue;
+    if (!s->draft.empty()) return false;
+    // a row that reaches its length limit with this token frees its slot at commit;
+    // planning the next step synchronously lets a waiting request take it at once
+    // (admission latency = TTFT) instead of one step later
+    if (!across_length_finish && s->status == SeqStatus::Running &&
+        (s->num_generated() + 1 >= s->max_tokens ||
+         static_cast<int>(s->tokens.size()) + 1 >= cfg_.max_model_len))
+      return false;
+  }
+  Inflight r;
+  r.seqs.reserve(p.num_seqs);
+  r.pos.reserve(p.num_seqs);
+  for (int i = 0; i < p.num_seqs; ++i) {
+    Sequence* s = plan_seqs_[i];
+    r.seqs.push_back(s);
+    if (s == nullptr || s->status != SeqStatus::Running) {
+      r.pos.push_back(-1);
+      continue;
+    }
+    r.pos.push_back(static_cast<int>(s->tokens.size()));
+    s->tokens.push_back(kPlaceholder);
+    s->num_computed = static_cast<int>(s->tokens.size()) - 1;
+  }
+  inflight_.push_back(std::move(r));
+  for (auto& q : plan_seqs_) q = nullptr;  // the plan is now owned by the record
+  return true;
+}
+
+std::vector<FinishedSeq> StepScheduler::commit(const int32_t* tokens, int num_sample) {
+  if (inflight_.empty()) throw std::logic_error("commit: no lookahead plan in flight");
+  Inflight r = std::move(inflight_.front());
+  inflight_.pop_front();
+  if (num_sample != static_cast<int>(r.seqs.size())) throw std::invalid_argument("commit: num_sample mismatch");
+  std::vector<Sequence*> finished;
+  for (int i = 0; i < num_sample; ++i) {
+    Sequence* s = r.seqs[i];
+    const int pos = r.pos[i];
+    if (s == nullptr || pos < 0 || s->status == SeqStatus::Finished) continue;
+    if (pos != static_cast<int>(s->tokens.size()) - 1 || s->tokens[pos] != kPlaceholder)
+      throw std::logic_error("commit: placeholder bookkeeping out of order");
+    s->tokens[pos] = tokens[i];
+    int reason = check_stop(*s);
+    if (reason) {
+      s->finish = static_cast<SeqFinish>(reason);
+      finished.push_back(s);
+    }
+  }
+  std::vector<FinishedSeq> done;
+  for (Sequence* s : finished) {
+    if (s->status == SeqStatus::Running) {
+      release(*s, /*publish=*/true);
+      running_.erase(std::remove(running_.begin(), running_.end(), s), running_.end());
+    } else {  // preempted by the lookahead schedule(): waiting, holds no pages
+      waiting_.erase(std::remove(waiting_.begin(), waiting_.end(), s), waiting_.end());
+      release(*s, false);
+    }
+    s->status = SeqStatus::Finished;
+    done.push_back(FinishedSeq{s->id, s->finish, s->prompt_len, s->num_generated(), s->num_cached});
+    forget(s);
     seqs_.erase(s->id);
   }
   return done;

@@ -113,6 +113,21 @@ class StepScheduler {
   // many belong to sampled sequence i (1 for plain decode). Returns finished.
   std::vector<FinishedSeq> update(const int32_t* tokens, const int32_t* counts, int num_sample);
 
+  // Asynchronous scheduling (one step of lookahead): for a plan of plain decode
+  // rows whose tokens are still being sampled on the GPU, append a placeholder
+  // token (kPlaceholder) to every sequence so schedule() can plan the NEXT step
+  // before this one finishes -- the runner substitutes the placeholders on the
+  // device from this step's sampled-token buffer. commit() later resolves the
+  // oldest lookahead plan with its real tokens (one per row, plan order) and runs
+  // the stop checks; a sequence that stopped there may already be in the next
+  // plan, whose row for it is then ignored. Returns false (and does nothing) if
+  // the current plan is not a pure-decode plan, or (unless across_length_finish)
+  // if a row of it reaches its length limit (so its freed slot is refilled at once).
+  static constexpr int32_t kPlaceholder = -1;
+  bool lookahead(bool across_length_finish = false);
+  std::vector<FinishedSeq> commit(const int32_t* tokens, int num_sample);
+  int num_inflight() const { return static_cast<int>(inflight_.size()); }
+
   // queries
   int num_waiting() const { return static_cast<int>(waiting_.size()); }
   int num_running() const { return static_cast<int>(running_.size()); }
@@ -142,6 +157,13 @@ class StepScheduler {
   void insert_waiting(Sequence* s);
   void emit(Sequence& s, int q_len, bool prefill, bool sample);
   int check_stop(Sequence& s);
+  void forget(Sequence* s);  // drop s from the plan / lookahead records
+
+  struct Inflight {
+    std::vector<Sequence*> seqs;  // plan order (every row samples)
+    std::vector<int> pos;         // index of the placeholder in seqs[i]->tokens, -1 = none
+  };
+  std::deque<Inflight> inflight_;
 
   SchedulerConfig cfg_;
   BlockAllocator alloc_;

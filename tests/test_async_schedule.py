@@ -1,0 +1,125 @@
+"""Asynchronous scheduling in the C++ step scheduler (StepScheduler.lookahead /
+commit): step N+1 is planned while step N's tokens are still on the GPU. The
+placeholder bookkeeping must give the same token streams, stop decisions and
+page accounting as the synchronous update() loop."""
+import numpy as np
+import pytest
+
+from xgserve import _runtime as R
+
+PH = -1
+
+
+def _sched(num_blocks=64, eos=(), max_seqs=8):
+    c = R.SchedulerConfig()
+    c.block_size = 4
+    c.num_blocks = num_blocks
+    c.max_num_seqs = max_seqs
+    c.max_num_batched_tokens = 64
+    c.max_model_len = 256
+    c.enable_prefix_cache = True
+    c.eos_ids = list(eos)
+    return R.StepScheduler(c)
+
+
+def _oracle(seq_id, step):  # the "model": a deterministic token per (sequence, position)
+    return 1000 + 7 * seq_id + step
+
+
+def _run(sync: bool, prompts, max_tokens, eos=(), abort_at=None, num_blocks=64, across=True):
+    s = _sched(eos=eos, num_blocks=num_blocks)
+    for i, (p, m) in enumerate(zip(prompts, max_tokens)):
+        assert s.add(i + 1, p, m, 1, not eos, False, [], 0)
+    out = {i + 1: [] for i in range(len(prompts))}
+    finished = {}
+    pos = {i + 1: len(p) for i, p in enumerate(prompts)}
+
+    def tok_for(plan):
+        ts = []
+        for j in plan["sample_seq_index"]:
+            sid = int(plan["seq_ids"][j])
+            ts.append(_oracle(sid, pos[sid]))
+        return np.array(ts, np.int32)
+
+    def record(plan, toks, fins):
+        for j, t in zip(plan["sample_seq_index"], toks):
+            sid = int(plan["seq_ids"][j])
+            if sid in finished:
+                continue
+            out[sid].append(int(t))
+            pos[sid] += 1
+        for f in fins:
+            finished[f[0]] = f[1]
+
+    plan = s.schedule()
+    steps = 0
+    while plan["num_tokens"] > 0 and steps < 500:
+        steps += 1
+        if abort_at is not None and steps == abort_at[0]:
+            s.abort(abort_at[1])
+            finished[abort_at[1]] = "abort"
+        ahead = (not sync) and s.lookahead(across)
+        toks = tok_for(plan)
+        if ahead:
+            nxt = s.schedule()
+            # every placeholder input belongs to a row of the step in flight
+            nd = nxt["num_decodes"]
+            for i in range(nd):
+                if nxt["input_ids"][i] == PH:
+                    assert int(nxt["seq_ids"][i]) in set(int(x) for x in plan["seq_ids"])
+            fins = s.commit(toks)
+            record(plan, toks, fins)
+            plan = nxt
+        else:
+            fins = s.update(toks, np.ones(len(toks), np.int32))
+            record(plan, toks, fins)
+            plan = s.schedule()
+    assert s.num_inflight() == 0
+    return out, finished, s
+
+
+@pytest.mark.parametrize("across", [True, False])
+@pytest.mark.parametrize("eos", [(), (1000 + 7 * 2 + 9,)])
+def test_lookahead_matches_sync(eos, across):
+    prompts = [[1, 2, 3], [4, 5, 6, 7, 8], [9] * 11]
+    mt = [5, 12, 3]
+    a, fa, sa = _run(True, prompts, mt, eos)
+    b, fb, sb = _run(False, prompts, mt, eos, across=across)
+    assert a == b
+    assert fa == fb
+    assert sa.num_used_blocks() == sb.num_used_blocks()
+    assert sb.num_running() == 0 and sb.num_waiting() == 0
+
+
+def test_lookahead_with_abort():
+    prompts = [[1, 2, 3], [4, 5, 6]]
+    b, fb, sb = _run(False, prompts, [20, 20], abort_at=(6, 1))
+    assert fb[1] == "abort" and len(b[2]) == 20
+    assert sb.num_running() == 0 and sb.num_free_blocks() + sb.num_evictable_blocks() == 64 - 0
+
+
+def test_lookahead_refuses_mixed_plans_and_update_guard():
+    s = _sched()
+    assert s.add(1, [1, 2, 3], 4, 1, True, False, [], 0)
+    plan = s.schedule()  # prefill
+    assert not s.lookahead()
+    s.update(np.array([5], np.int32), np.ones(1, np.int32))
+    s.schedule()
+    assert s.lookahead()
+    with pytest.raises(Exception):
+        s.update(np.array([6], np.int32), np.ones(1, np.int32))
+    s.commit(np.array([6], np.int32))
+    with pytest.raises(Exception):
+        s.commit(np.array([7], np.int32))
+
+
+def test_lookahead_under_preemption():
+    """A pool too small for all sequences: the lookahead schedule() preempts
+    sequences holding an unresolved placeholder; they are re-admitted only after
+    commit() and still produce the synchronous token streams."""
+    prompts = [[i + 1] * 8 for i in range(3)]
+    a, fa, _ = _run(True, prompts, [20, 20, 20], num_blocks=12)
+    b, fb, sb = _run(False, prompts, [20, 20, 20], num_blocks=12)
+    assert a == b and fa == fb
+    assert all(len(v) == 20 for v in b.values())
+    assert sb.total_preemptions() > 0 if hasattr(sb, "total_preemptions") else True

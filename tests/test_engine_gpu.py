@@ -163,3 +163,55 @@ def test_http_server_with_gpu_engine(llama_small):
         return True
 
     assert run_with_client(cfg, fn, engine=eng, timeout=300)
+
+
+def _run_async_vs_sync(model, async_, staggered, temperature):
+    eng = _engine(model, async_schedule=async_)
+    assert eng._async == async_
+    outs = {}
+    for i in range(4):
+        eng.add_request(f"r{i}", [128000] + list(range(400 + 9 * i, 430 + 13 * i)),
+                        SamplingParams(max_tokens=(5 + 3 * i) if staggered else 10, temperature=temperature,
+                                       ignore_eos=True, seed=11 + i))
+    n = 0
+    while eng.has_work():
+        for o in eng.step():
+            outs.setdefault(o.request_id, []).extend(o.new_token_ids)
+        n += 1
+        if staggered and n == 4:  # arrivals while a lookahead step is in flight
+            for i in range(4, 7):
+                eng.add_request(f"r{i}", [128000] + list(range(700 + 5 * i, 720 + 5 * i)),
+                                SamplingParams(max_tokens=9, temperature=temperature, ignore_eos=True,
+                                               seed=11 + i))
+    return outs, eng
+
+
+@pytest.mark.parametrize("temperature", [0.0, 0.8])
+def test_async_schedule_matches_sync(llama_small, temperature):
+    """Asynchronous scheduling (step N+1 planned and launched before step N's
+    tokens reach the host; decode ids substituted on the GPU from the previous
+    graph step's sampled tokens) reproduces the synchronous loop exactly when the
+    steps' batch composition is the same: greedy and seeded sampling."""
+    a, _ = _run_async_vs_sync(llama_small, False, False, temperature)
+    b, eng = _run_async_vs_sync(llama_small, True, False, temperature)
+    assert a == b
+    assert all(len(v) == 10 for v in b.values())
+    assert eng.sched.num_inflight() == 0 and eng.sched.num_running() == 0
+
+
+def test_async_schedule_staggered_tokens_are_reference_argmax(llama_small):
+    """Staggered lengths (rows finishing while their successor step is already in
+    flight) and mid-run arrivals change step composition, hence bf16 rounding, so
+    each greedy token is checked against the fp32 reference instead: an argmax up
+    to a bf16-sized near-tie, with exact requested lengths."""
+    b, eng = _run_async_vs_sync(llama_small, True, True, 0.0)
+    assert all(len(b[f"r{i}"]) == (5 + 3 * i if i < 4 else 9) for i in range(7))
+    prompts = {f"r{i}": [128000] + list(range(400 + 9 * i, 430 + 13 * i)) for i in range(4)}
+    prompts.update({f"r{i}": [128000] + list(range(700 + 5 * i, 720 + 5 * i)) for i in range(4, 7)})
+    for rid, gen in b.items():
+        p = prompts[rid]
+        ref = reference_logits(llama_small, p + gen[:-1]).float()
+        for i, tok in enumerate(gen):
+            row = ref[len(p) - 1 + i]
+            assert float(row.max() - row[tok]) < 0.15, (rid, i)
+    assert eng.sched.num_inflight() == 0 and eng.sched.num_running() == 0

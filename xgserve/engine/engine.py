@@ -75,6 +75,11 @@ class EngineConfig:
     # detokenise / build step N's outputs while step N+1 runs on the GPU (first
     # tokens are still emitted at once, so TTFT is unchanged)
     overlap_outputs: bool = True
+    # asynchronous scheduling: plan + launch step N+1 (its decode ids substituted on
+    # the GPU from step N's sampled tokens) before step N's tokens reach the host,
+    # so the host's per-step work (commit, schedule, metadata, launch) overlaps the
+    # GPU instead of sitting between steps. TP=1, no speculation, graph decode steps.
+    async_schedule: bool = True
 
     def resolved_device(self) -> torch.device:
         if self.device:
@@ -155,6 +160,10 @@ class LLMEngine:
             from .spec_decode import SpeculativeDecoder
             self.spec = SpeculativeDecoder(self, cfg.draft_model, cfg.num_speculative_tokens,
                                            cfg.spec_min_acceptance_rate)
+        self._inflight = None  # (plan, handle): launched by the previous step() (async scheduling)
+        self._async = (cfg.async_schedule and os.environ.get("XGS_ASYNC_SCHED", "1") != "0"
+                       and self.device.type == "cuda" and get_state().tp_size == 1 and self.spec is None
+                       and bool(self.runner.graphs))
         log.info("engine ready: model=%s tp=%d blocks=%d (%.1f GiB KV) load=%.1fs", self.mcfg.name, get_state().tp_size,
                  num_blocks, self.runner.kv_bytes() / 2**30, self.load_time)
 
@@ -235,7 +244,8 @@ class LLMEngine:
         self.stats_counters["requests_finished"] += 1
 
     def has_work(self) -> bool:
-        return self.sched.has_work() or bool(self._pending_aborts) or self._deferred is not None
+        return (self.sched.has_work() or bool(self._pending_aborts) or self._deferred is not None
+                or self._inflight is not None)
 
     # ------------------------------------------------------------------ step
     def _bind_slots(self, plan) -> None:
@@ -322,7 +332,82 @@ class LLMEngine:
             self._timing[phase] += t1 - t0
         return t1
 
+    @staticmethod
+    def _lookahead_src(prev: dict, nxt: dict) -> Optional[np.ndarray]:
+        """Per decode row of `nxt`: the row of `prev` (a pure-decode graph step, one
+        sampled token per row) whose token is this row's placeholder input, -1 if the
+        row has a real id. None if no row needs one."""
+        nd = int(nxt["num_decodes"])
+        ids = nxt["input_ids"][:nd]
+        need = ids == -1  # StepScheduler::kPlaceholder
+        if not need.any():
+            return None
+        pids, cids = prev["seq_ids"], nxt["seq_ids"][:nd]
+        sorter = np.argsort(pids, kind="stable")
+        k = np.clip(np.searchsorted(pids, cids, sorter=sorter), 0, len(pids) - 1)
+        j = sorter[k]
+        hit = pids[j] == cids
+        if not hit[need].all():  # an unresolved id would be an out-of-range embedding gather
+            raise RuntimeError("async scheduling: placeholder without a producing row")
+        return np.where(need, j, -1).astype(np.int32)
+
+    def _step_async(self) -> List[RequestOutput]:
+        """One step of the pipelined loop: retire the step launched by the previous
+        call (or launch one now), but first plan and launch its successor when it is
+        a pure-decode graph step -- the GPU always has the next step queued."""
+        outs: List[RequestOutput] = []
+        t = time.perf_counter()
+        with self._lock:
+            for rid in self._pending_aborts:
+                outs.append(RequestOutput(rid, [], "", True, "abort"))
+            self._pending_aborts.clear()
+        cur, self._inflight = self._inflight, None
+        if cur is None:
+            with self._lock:
+                plan = self.sched.schedule()
+            t = self._tick("schedule", t)
+            if plan["num_tokens"] == 0:
+                return outs + self._flush_deferred()
+            self._bind_slots(plan)
+            samp = self._sampling_rows(plan)
+            t = self._tick("prepare", t)
+            handle = self.runner.launch(plan, samp)
+            t = self._tick("launch", t)
+        else:
+            plan, handle = cur
+        ahead = False
+        if self.runner.launched_as_graph(handle):
+            with self._lock:
+                ahead = self.sched.lookahead()
+                nplan = self.sched.schedule() if ahead else None
+            t = self._tick("schedule", t)
+            if ahead:
+                # the next step's sampling seeds count the token this step produces
+                np.add.at(self.slot_ngen, plan["slots"][plan["sample_seq_index"]], 1)
+                if nplan["num_tokens"] > 0:
+                    self._bind_slots(nplan)
+                    nsamp = self._sampling_rows(nplan)
+                    src = self._lookahead_src(plan, nplan)
+                    self._inflight = (nplan, self.runner.launch(nplan, nsamp, src=src))
+                t = self._tick("launch", t)
+        outs += self._flush_deferred()  # previous step's outputs, while the GPU runs
+        t = self._tick("emit_overlapped", t)
+        toks, lps, hidden = self.runner.wait(handle)
+        t = self._tick("wait_gpu", t)
+        n_sample = int(plan["num_sample"])
+        counts = np.ones(n_sample, np.int32)
+        if ahead:
+            with self._lock:
+                finished = self.sched.commit(toks)
+            self.stats_counters["generation_tokens"] += n_sample
+            fin_map = {f[0]: f for f in finished}
+        else:
+            fin_map = None
+        return outs + self._finish_step(plan, toks, lps, hidden, counts, fin_map, t)
+
     def _step(self) -> List[RequestOutput]:
+        if self._async:
+            return self._step_async()
         outs: List[RequestOutput] = []
         t = time.perf_counter()
         with self._lock:
@@ -353,6 +438,14 @@ class LLMEngine:
             t = self._tick("emit_overlapped", t)
             toks, lps, hidden = self.runner.wait(handle)
             t = self._tick("wait_gpu", t)
+        if counts is None:
+            counts = np.ones(int(plan["num_sample"]), np.int32)
+        return outs + self._finish_step(plan, toks, lps, hidden, counts, None, t)
+
+    def _finish_step(self, plan, toks, lps, hidden, counts, fin_map, t) -> List[RequestOutput]:
+        """Bookkeeping after a step's tokens are on the host: stats, embeddings, the
+        scheduler update (unless an async commit already did it: fin_map given),
+        and output emission (deferred to the next step when nothing finished)."""
         self.step_count += 1
         self.stats_counters["steps"] += 1
         if plan["num_decodes"] == plan["num_seqs"]:
@@ -361,18 +454,17 @@ class LLMEngine:
         if hidden is not None:
             self._accumulate_embeddings(plan, hidden)
         n_sample = int(plan["num_sample"])
-        if counts is None:
-            counts = np.ones(n_sample, np.int32)
-        fin_map = self._apply(plan, toks, counts)
+        if fin_map is None:
+            fin_map = self._apply(plan, toks, counts)
         t = self._tick("apply", t)
         if not self.is_driver:
-            return outs
+            return []
         first_tokens = bool(plan["is_prefill"][plan["sample_seq_index"]].any()) if n_sample else False
         if self.cfg.overlap_outputs and self.spec is None and not first_tokens and not fin_map:
             self._deferred = (plan, toks, lps, counts, fin_map)
-            return outs
+            return []
         with self._lock:
-            outs += self._emit(plan, toks, lps, counts, fin_map)
+            outs = self._emit(plan, toks, lps, counts, fin_map)
         self._tick("emit_blocking", t)
         return outs
 

@@ -81,8 +81,12 @@ class ModelRunner:
         self.d_stages = [torch.empty(cap, dtype=torch.int32, device=self.device) for _ in range(2)]
         self.stage_events = [None, None]
         self.stage_idx = 0
-        self.h_tok = _pinned(max(max_num_batched_tokens, max_num_seqs), torch.int32)
-        self.h_lp = _pinned(max(max_num_batched_tokens, max_num_seqs), torch.float32)
+        # sampled tokens / logprobs D2H: two pinned buffers + an event each, so a step
+        # launched before the previous one was waited on never overwrites its results
+        nt = max(max_num_batched_tokens, max_num_seqs)
+        self.h_toks = [_pinned(nt, torch.int32) for _ in range(2)]
+        self.h_lps = [_pinned(nt, torch.float32) for _ in range(2)]
+        self.out_idx = 0
         # graphs
         self.use_graphs = use_graphs and self.is_cuda
         if graph_batch_sizes is None:
@@ -105,27 +109,35 @@ class ModelRunner:
         B = max(self.graph_bs) if self.graph_bs else 1
         W = self.max_blocks_per_seq
         self.g_B, self.g_W = B, W
-        # int32 region: ids | pos | slots | sl | bt ; sampling region separate
-        n = 4 * B + B * W
+        # int32 region: ids | pos | slots | sl | src | bt ; sampling region separate.
+        # src[i] >= 0: row i's input id is the previous graph step's sampled token
+        # g_out_tok[src[i]] (asynchronous scheduling), substituted inside the graph
+        n = 5 * B + B * W
         self.g_int = torch.zeros(n, dtype=torch.int32, device=self.device)
         self.g_ids = self.g_int[0:B]
         self.g_pos = self.g_int[B:2 * B]
         self.g_slot = self.g_int[2 * B:3 * B]
         self.g_sl = self.g_int[3 * B:4 * B]
-        self.g_bt = self.g_int[4 * B:4 * B + B * W].view(B, W)
-        self.h_int = _pinned(n, torch.int32)
+        self.g_src = self.g_int[4 * B:5 * B]
+        self.g_bt = self.g_int[5 * B:5 * B + B * W].view(B, W)
         self.g_temp = torch.zeros(B, dtype=torch.float32, device=self.device)
         self.g_topp = torch.ones(B, dtype=torch.float32, device=self.device)
         self.g_topk = torch.zeros(B, dtype=torch.int32, device=self.device)
         self.g_seed = torch.zeros(B, dtype=torch.int64, device=self.device)
-        self.h_samp_f = _pinned(2 * B, torch.float32)
-        self.h_samp_i = _pinned(B, torch.int32)
-        self.h_samp_s = _pinned(B, torch.int64)
+        # two sets of pinned host inputs (event-guarded): the next step's inputs can be
+        # written while this step's H2D copies are still queued behind the GPU
+        self.h_ints = [_pinned(n, torch.int32) for _ in range(2)]
+        self.h_samp_fs = [_pinned(2 * B, torch.float32) for _ in range(2)]
+        self.h_samp_is = [_pinned(B, torch.int32) for _ in range(2)]
+        self.h_samp_ss = [_pinned(B, torch.int64) for _ in range(2)]
+        self.g_stage_events = [None, None]
+        self.g_stage_idx = 0
         self.g_out_tok = torch.zeros(B, dtype=torch.int32, device=self.device)
         self.g_out_lp = torch.zeros(B, dtype=torch.float32, device=self.device)
         self.g_greedy_graph: Dict[int, bool] = {}
 
     def _decode_body(self, bs: int, greedy: bool):
+        ops.subst_tokens(self.g_ids[:bs], self.g_src[:bs], self.g_out_tok)
         meta = AttnMeta(num_tokens=bs, num_decodes=bs, positions=self.g_pos[:bs], slot_mapping=self.g_slot[:bs],
                         dec_block_tables=self.g_bt[:bs], dec_seq_lens=self.g_sl[:bs],
                         num_splits=self.decode_splits(bs), workspace=self.workspace)
@@ -146,6 +158,7 @@ class ModelRunner:
         torch.cuda.synchronize()
         # neutral inputs: padding rows (no KV writes, no attention work)
         self.g_slot.fill_(-1)
+        self.g_src.fill_(-1)
         self.g_sl.fill_(0)
         self.g_ids.fill_(0)
         self.g_pos.fill_(0)
@@ -182,33 +195,57 @@ class ModelRunner:
         return self.wait(self.launch(plan, samp))
 
     @torch.no_grad()
-    def launch(self, plan: dict, samp: Optional[SamplingRows]):
+    def launch(self, plan: dict, samp: Optional[SamplingRows], src: Optional[np.ndarray] = None):
         """Enqueue one step (inputs H2D, forward, sampling, tokens D2H) without
         waiting for it; `wait(handle)` returns what `execute` returns. The host
-        can do other work (previous step's detokenisation) while the GPU runs."""
+        can do other work (previous step's detokenisation, planning the next step)
+        while the GPU runs. `src` (asynchronous scheduling): per decode row, the
+        row of the previous GRAPH step whose sampled token is this row's input
+        (-1: the plan's own id)."""
         T = int(plan["num_tokens"])
         Nd = int(plan["num_decodes"])
         ns = int(plan["num_seqs"])
         if T == 0:
-            return (0, None, (None, None, None))
+            return (0, None, (None, None, None), None)
         need_hidden = bool(plan["is_embed"].any()) if ns else False
         bucket = self._graph_bucket(Nd) if (Nd == ns and T == Nd and not need_hidden) else None
         if bucket is not None and self.graphs:
-            return self._execute_graph(plan, samp, Nd, bucket)
-        return self._execute_eager(plan, samp, need_hidden)
+            return self._execute_graph(plan, samp, Nd, bucket, src)
+        return self._execute_eager(plan, samp, need_hidden, src)
+
+    def launched_as_graph(self, handle) -> bool:
+        """True if the step wrote its sampled tokens to g_out_tok (a graph step)."""
+        return len(handle) > 4 and handle[4]
+
+    def _record_out(self, n: int, tok: torch.Tensor, lp: torch.Tensor, hidden, graph: bool):
+        """Tokens / logprobs D2H into the next of the two pinned buffers + an event."""
+        i = self.out_idx
+        self.out_idx ^= 1
+        self.h_toks[i][:n].copy_(tok[:n], non_blocking=True)
+        self.h_lps[i][:n].copy_(lp[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return (n, hidden, None, (i, ev), graph)
 
     def wait(self, handle):
-        n, hidden, ready = handle
+        n, hidden, ready, out = handle[:4]
         if ready is not None:
             return ready
-        torch.cuda.current_stream().synchronize()
-        if not self.is_driver:
+        if out is None:
+            torch.cuda.current_stream().synchronize()
             return None, None, hidden
-        return self.h_tok[:n].numpy().copy(), self.h_lp[:n].numpy().copy(), hidden
+        i, ev = out
+        ev.synchronize()  # this step only: a step queued behind it keeps running
+        return self.h_toks[i][:n].numpy().copy(), self.h_lps[i][:n].numpy().copy(), hidden
 
-    def _execute_graph(self, plan, samp: Optional[SamplingRows], n: int, bs: int):
+    def _execute_graph(self, plan, samp: Optional[SamplingRows], n: int, bs: int, src: Optional[np.ndarray]):
         B, W = self.g_B, self.g_W
-        hi = self.h_int.numpy()
+        si = self.g_stage_idx
+        self.g_stage_idx ^= 1
+        if self.g_stage_events[si] is not None:
+            self.g_stage_events[si].synchronize()  # the H2D copies that last read this set have run
+        h_int = self.h_ints[si]
+        hi = h_int.numpy()
         w = int(plan["bt_width"])
         hi[0:n] = plan["input_ids"]
         hi[n:bs] = 0
@@ -218,31 +255,36 @@ class ModelRunner:
         hi[2 * B + n:2 * B + bs] = -1
         hi[3 * B:3 * B + n] = plan["seq_lens"]
         hi[3 * B + n:3 * B + bs] = 0
-        bt = hi[4 * B:4 * B + bs * W].reshape(bs, W)
+        hi[4 * B:4 * B + bs] = -1
+        if src is not None:
+            hi[4 * B:4 * B + n] = src
+        bt = hi[5 * B:5 * B + bs * W].reshape(bs, W)
         bt[:n, :w] = plan["block_tables"].reshape(n, w)
-        # copy ids..sl (4*B) and the first bs rows of bt
-        self.g_int[:4 * B].copy_(self.h_int[:4 * B], non_blocking=True)
-        self.g_int[4 * B:4 * B + bs * W].copy_(self.h_int[4 * B:4 * B + bs * W], non_blocking=True)
+        # copy ids..src (5*B) and the first bs rows of bt
+        self.g_int[:5 * B].copy_(h_int[:5 * B], non_blocking=True)
+        self.g_int[5 * B:5 * B + bs * W].copy_(h_int[5 * B:5 * B + bs * W], non_blocking=True)
         greedy = samp is None or samp.all_greedy
         if not greedy:
-            f = self.h_samp_f.numpy()
+            hf, hsi, hss = self.h_samp_fs[si], self.h_samp_is[si], self.h_samp_ss[si]
+            f = hf.numpy()
             f[:n] = samp.temps
             f[B:B + n] = samp.top_ps
-            self.h_samp_i.numpy()[:n] = samp.top_ks
-            self.h_samp_s.numpy()[:n] = samp.seeds
-            self.g_temp[:n].copy_(self.h_samp_f[:n], non_blocking=True)
-            self.g_topp[:n].copy_(self.h_samp_f[B:B + n], non_blocking=True)
-            self.g_topk[:n].copy_(self.h_samp_i[:n], non_blocking=True)
-            self.g_seed[:n].copy_(self.h_samp_s[:n], non_blocking=True)
+            hsi.numpy()[:n] = samp.top_ks
+            hss.numpy()[:n] = samp.seeds
+            self.g_temp[:n].copy_(hf[:n], non_blocking=True)
+            self.g_topp[:n].copy_(hf[B:B + n], non_blocking=True)
+            self.g_topk[:n].copy_(hsi[:n], non_blocking=True)
+            self.g_seed[:n].copy_(hss[:n], non_blocking=True)
+        ev = self.g_stage_events[si] or torch.cuda.Event()
+        ev.record()
+        self.g_stage_events[si] = ev
         self.graphs[(bs, greedy)].replay()
         if not self.is_driver:
             # no D2H to wait on; wait() still drains before the pinned inputs get rewritten
-            return (n, None, None)
-        self.h_tok[:n].copy_(self.g_out_tok[:n], non_blocking=True)
-        self.h_lp[:n].copy_(self.g_out_lp[:n], non_blocking=True)
-        return (n, None, None)
+            return (n, None, None, None, True)
+        return self._record_out(n, self.g_out_tok, self.g_out_lp, None, True)
 
-    def _execute_eager(self, plan, samp: Optional[SamplingRows], need_hidden: bool):
+    def _execute_eager(self, plan, samp: Optional[SamplingRows], need_hidden: bool, src: Optional[np.ndarray]):
         T = int(plan["num_tokens"])
         Nd = int(plan["num_decodes"])
         ns = int(plan["num_seqs"])
@@ -282,6 +324,9 @@ class ModelRunner:
         sl = dev[o[4]:o[5]]
         pre_qsl = dev[o[5]:o[6]]
         lidx = dev[o[6]:o[7]]
+        if src is not None:  # decode rows first: their ids from the previous graph step
+            d_src = torch.from_numpy(np.ascontiguousarray(src, dtype=np.int32)).to(self.device, non_blocking=False)
+            ops.subst_tokens(ids[:src.shape[0]], d_src, self.g_out_tok)
         meta = AttnMeta(num_tokens=T, num_decodes=Nd, positions=pos, slot_mapping=slots,
                         dec_block_tables=bt[:Nd], dec_seq_lens=sl[:Nd],
                         num_splits=self.decode_splits(Nd) if self.is_cuda else 1, workspace=self.workspace,
@@ -290,12 +335,12 @@ class ModelRunner:
         h = self.model(ids, meta, self.kv_caches)
         hid = h if need_hidden else None
         if S == 0:
-            return (0, hid, (np.zeros(0, np.int32), np.zeros(0, np.float32), hid))
+            return (0, hid, (np.zeros(0, np.int32), np.zeros(0, np.float32), hid), None)
         logits = self.model.compute_logits(h.index_select(0, lidx.long()))
         if self.capture_logits:
             self.last_logits = logits.float().cpu()
         if not self.is_driver:
-            return (S, hid, None) if self.is_cuda else (S, hid, (None, None, hid))
+            return (S, hid, None, None) if self.is_cuda else (S, hid, (None, None, hid), None)
         if samp is None or samp.all_greedy:
             tok, lp = ops.argmax_logprob(logits)
         else:
@@ -307,7 +352,5 @@ class ModelRunner:
                 gen = torch.Generator().manual_seed(int(samp.seeds[0]) & 0x7FFFFFFF)
             tok, lp = ops.sample_tokens(logits, dev_f[0], dev_f[1], topk, seeds, step=0, generator=gen)
         if self.is_cuda:
-            self.h_tok[:S].copy_(tok, non_blocking=True)
-            self.h_lp[:S].copy_(lp, non_blocking=True)
-            return (S, hid, None)
-        return (S, hid, (tok.numpy().astype(np.int32), lp.numpy().astype(np.float32), hid))
+            return self._record_out(S, tok, lp, hid, False)
+        return (S, hid, (tok.numpy().astype(np.int32), lp.numpy().astype(np.float32), hid), None)

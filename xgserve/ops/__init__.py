@@ -11,7 +11,7 @@ from . import linear
 from .linear import skinny_linear, PendingSum
 from .attention import (decode_attention, decode_attention_fused, prefill_attention, decode_attention_ref,
                         prefill_attention_ref, choose_num_splits)
-from .sampling import argmax_logprob, sample_tokens, argmax_logprob_ref, segment_sum
+from .sampling import argmax_logprob, sample_tokens, argmax_logprob_ref, segment_sum, subst_tokens
 from .moe import moe_topk_softmax, moe_route, moe_align, moe_forward_ref, fused_moe
 from ._native import available as native_available
 
@@ -20,7 +20,7 @@ __all__ = [
     "silu_and_mul", "gelu_tanh", "silu_and_mul_ref", "gelu_tanh_ref",
     "RotaryCache", "rope_cache", "rope_cache_ref", "build_cos_sin",
     "decode_attention", "decode_attention_fused", "prefill_attention", "decode_attention_ref", "prefill_attention_ref", "choose_num_splits",
-    "argmax_logprob", "sample_tokens", "argmax_logprob_ref", "segment_sum",
+    "argmax_logprob", "sample_tokens", "argmax_logprob_ref", "segment_sum", "subst_tokens",
     "moe_topk_softmax", "moe_route", "moe_align", "moe_forward_ref", "fused_moe",
     "native_available",
 ]

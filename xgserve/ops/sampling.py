@@ -94,3 +94,17 @@ def segment_sum(hidden: torch.Tensor, cu: torch.Tensor, out: torch.Tensor,
     H = hidden.shape[-1]
     kernels().segment_sum(hidden.data_ptr(), H, cu.data_ptr(), ptr(out_rows), out.data_ptr(), S, stream_ptr())
     return out
+
+
+def subst_tokens(ids: torch.Tensor, src: torch.Tensor, prev: torch.Tensor) -> torch.Tensor:
+    """ids[i] <- prev[src[i]] where src[i] >= 0 (int32, in place): the decode rows of
+    a step planned before the previous step's tokens reached the host."""
+    n = ids.shape[0]
+    assert ids.dtype == src.dtype == prev.dtype == torch.int32 and src.shape[0] >= n
+    if not use_native(ids):
+        s = src[:n].long()
+        m = s >= 0
+        ids[m] = prev[s[m]]
+        return ids
+    kernels().subst_tokens(ids.data_ptr(), src.data_ptr(), prev.data_ptr(), n, stream_ptr())
+    return ids
