@@ -95,7 +95,7 @@ M64G_CFGS = {0: (4, 128, False), 1: (4, 128, True), 2: (4, 64, False), 3: (4, 64
              4: (2, 64, False), 5: (2, 64, True), 6: (2, 128, True)}
 
 # Measured on MI355X with cold weights (bench/gemm_bench.py --m64g-sweep,
-# profiles/r1_m64g_sweep.jsonl): (N, K, mode) -> {M bucket: (nw, split_k, cfg)}.
+# profiles/r1_m64g_sweep.jsonl; bucket 16 re-swept with the MT=1 kernel: r1_m64g_mt1_sweep.jsonl): (N, K, mode) -> {M bucket: (nw, split_k, cfg)}.
 # Bucket 64 serves 40 < M <= 64, bucket 32 serves 16 < M <= 40 (falls back to 64),
 # bucket 16 serves M <= 16 -- only shapes that have one take gemm_m64g at M <= 16
 # (it beats the register-streaming skinny kernel there: 8B batch 1 QKV 12.3 -> 9.8 us,
@@ -103,19 +103,19 @@ M64G_CFGS = {0: (4, 128, False), 1: (4, 128, True), 2: (4, 64, False), 3: (4, 64
 _M64_TUNED = {
     # Llama-3-8B / Mixtral attention, TP1
     (6144, 4096, MODE_PARTIAL): {64: (2, 4, 3), 32: (2, 8, 5), 16: (2, 8, 5)},
-    (4096, 4096, MODE_PARTIAL): {64: (1, 4, 0), 32: (1, 4, 0), 16: (1, 4, 0)},
-    (28672, 4096, MODE_SILU): {64: (2, 1, 1), 32: (2, 1, 5), 16: (2, 1, 5)},
-    (4096, 14336, MODE_PARTIAL): {64: (2, 8, 3), 32: (1, 4, 1), 16: (1, 8, 3)},
+    (4096, 4096, MODE_PARTIAL): {64: (1, 4, 0), 32: (1, 4, 0), 16: (2, 4, 4)},
+    (28672, 4096, MODE_SILU): {64: (2, 1, 1), 32: (2, 1, 5), 16: (2, 1, 6)},
+    (4096, 14336, MODE_PARTIAL): {64: (2, 8, 3), 32: (1, 4, 1), 16: (2, 4, 6)},
     # Llama-3-8B TP2 shards
     (3072, 4096, MODE_PARTIAL): {64: (1, 8, 2)},
     (4096, 2048, MODE_PARTIAL): {64: (1, 4, 5)},
     (14336, 4096, MODE_SILU): {64: (2, 1, 6)},
     (4096, 7168, MODE_PARTIAL): {64: (2, 8, 3)},
     # Llama-3-70B TP1
-    (10240, 8192, MODE_PARTIAL): {64: (2, 2, 1)},
-    (8192, 8192, MODE_PARTIAL): {64: (2, 8, 3)},
-    (57344, 8192, MODE_SILU): {64: (2, 1, 3)},
-    (8192, 28672, MODE_PARTIAL): {64: (2, 4, 3)},
+    (10240, 8192, MODE_PARTIAL): {64: (2, 2, 1), 16: (2, 8, 5)},
+    (8192, 8192, MODE_PARTIAL): {64: (2, 8, 3), 16: (2, 8, 1)},
+    (57344, 8192, MODE_SILU): {64: (2, 1, 3), 16: (2, 1, 5)},
+    (8192, 28672, MODE_PARTIAL): {64: (2, 4, 3), 16: (2, 4, 5)},
     # Llama-3-70B TP8 shards
     (1280, 8192, MODE_PARTIAL): {64: (1, 8, 0)},
     (8192, 1024, MODE_PARTIAL): {64: (2, 4, 2)},
