@@ -24,6 +24,9 @@
 // loop reads it (same workgroup: ordered by vmcnt(0) + barrier; no other
 // workgroup touches that row). This replaces rope_cache_partials and the q round
 // trip through HBM: one launch less per layer.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace xgk {
@@ -145,14 +148,16 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ seq_lens,
     float* __restrict__ part_out, float* __restrict__ part_lse, uint16_t* __restrict__ out, int64_t out_stride,
-    int Hq, int Hkv, int bs, float scale, int num_splits, int* __restrict__ counters, QkvFuse fq) {
+    int Hq, int Hkv, int bs, float scale, int num_splits, int* __restrict__ counters, QkvFuse fq, int min_tps) {
   using C = DecodeCfg<D, G>;
   const int kvh = blockIdx.x, b = blockIdx.y, split = blockIdx.z;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int L = seq_lens[b];
   const int ntiles = (L + 15) >> 4;
-  const int tps = (ntiles + num_splits - 1) / num_splits;
+  // tiles per split: an even share, but at least min_tps, so short sequences leave
+  // their trailing splits empty (they publish lse = -inf) and long ones spread out
+  const int tps = max(min_tps, (ntiles + num_splits - 1) / num_splits);
   const int t_begin = split * tps;
   const int t_end = min(ntiles, t_begin + tps);
 
@@ -188,8 +193,11 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   const int64_t head_stride = static_cast<int64_t>(bs) * D;
   uint16_t* my_v = v_lds[wid];
 
-  uint4 kf[C::KK], vr[C::VLD];
-  auto load_tile = [&](int t) {
+  // two register tiles per wave (K fragments + V rows): tile t+W and t+2W are in
+  // flight while tile t is processed (one tile of lookahead left HBM idle between
+  // a wave's tiles at 64 concurrent sequences)
+  uint4 kfA[C::KK], vrA[C::VLD], kfB[C::KK], vrB[C::VLD];
+  auto load_tile = [&](int t, uint4 (&kf)[C::KK], uint4 (&vr)[C::VLD]) {
     const int key0 = t * 16;
     const int page = bt[key0 / bs];
     const int64_t base = (static_cast<int64_t>(page) * Hkv + kvh) * head_stride + static_cast<int64_t>(key0 % bs) * D;
@@ -203,9 +211,7 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     }
   };
 
-  int t = t_begin + wid;
-  if (t < t_end) load_tile(t);
-  for (; t < t_end; t += C::WAVES) {
+  auto process = [&](int t, uint4 (&kf)[C::KK], uint4 (&vr)[C::VLD]) {
     uint4 kcur[C::KK];
 #pragma unroll
     for (int kk = 0; kk < C::KK; ++kk) kcur[kk] = kf[kk];
@@ -216,7 +222,7 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
       const int row = c / C::NCH, ch = c % C::NCH;
       st16(my_v + row * D + dswz<D>(row, ch) * 8, vr[i]);
     }
-    if (t + C::WAVES < t_end) load_tile(t + C::WAVES);  // prefetch: in flight during the math below
+    if (t + 2 * C::WAVES < t_end) load_tile(t + 2 * C::WAVES, kf, vr);  // refill this register tile
 
     f32x4_t s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -259,6 +265,15 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
       const bf16x4_t vfrag = lds_read_tr16(my_v + row * D + dswz<D>(row, col >> 3) * 8 + (col & 7));
       o[mt] = mfma16x16x16(vfrag, pf, o[mt]);
     }
+  };
+
+  int t = t_begin + wid;
+  if (t < t_end) load_tile(t, kfA, vrA);
+  if (t + C::WAVES < t_end) load_tile(t + C::WAVES, kfB, vrB);
+  for (; t < t_end; t += 2 * C::WAVES) {
+    process(t, kfA, vrA);
+    if (t + C::WAVES >= t_end) break;
+    process(t + C::WAVES, kfB, vrB);
   }
 
   // ---- merge the 4 wave states: O^T[d = 16mt + 4g + r][h = li]
@@ -381,13 +396,22 @@ __global__ void __launch_bounds__(D) decode_combine_kernel(const float* __restri
       f2bf(den > 0.f ? acc / den : 0.f);
 }
 
+// XGS_DECODE_MIN_SPLIT_TILES: minimum 16-key tiles per split (default 1 = even split).
+static int decode_min_split_tiles() {
+  static const int v = [] {
+    const char* e = std::getenv("XGS_DECODE_MIN_SPLIT_TILES");
+    return e ? std::max(1, std::atoi(e)) : 1;
+  }();
+  return v;
+}
+
 template <int D, int G, bool FQ>
 static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, const uint16_t* vc,
                           const int32_t* bt, int bts, const int32_t* sl, float* po, float* pl, uint16_t* out,
                           int64_t os, int B, int Hq, int Hkv, int bs, float scale, int S, int* counters,
                           const QkvFuse& fq, hipStream_t st) {
   hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt, bts, sl,
-                     po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq);
+                     po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq, S > 1 ? decode_min_split_tiles() : 1);
   if (S > 1 && counters == nullptr)
     hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
 }

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -100,9 +101,12 @@ class ModelRunner:
     def kv_bytes(self) -> int:
         return self.kv.numel() * self.kv.element_size()
 
+    DECODE_SPLIT_WGS = int(os.environ.get("XGS_DECODE_SPLIT_WGS", "512"))
+
     def decode_splits(self, bs: int) -> int:
         wgs = max(1, bs * self.Hkv)
-        return int(max(1, min(self.max_splits, (512 + wgs - 1) // wgs)))
+        target = self.DECODE_SPLIT_WGS
+        return int(max(1, min(self.max_splits, (target + wgs - 1) // wgs)))
 
     # ------------------------------------------------------------------ graph buffers
     def _init_graph_buffers(self):
