@@ -23,10 +23,12 @@ def main():
     span = (last - t0) / 1e6
     busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in win) / 1e6
     agg = collections.defaultdict(lambda: [0, 0])
+    durs = collections.defaultdict(list)
     for r in win:
         d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         agg[r["Kernel_Name"]][0] += d
         agg[r["Kernel_Name"]][1] += 1
+        durs[r["Kernel_Name"]].append(d)
     gaps = []
     prev = None
     for r in win:
@@ -38,10 +40,14 @@ def main():
     print(f"- window span: {span:.1f} ms, GPU busy: {busy:.1f} ms ({100 * busy / span:.1f}%)")
     if gaps:
         print(f"- host gaps > 200 us: {len(gaps)}, mean {sum(gaps) / len(gaps):.0f} us, total {sum(gaps) / 1e3:.1f} ms")
-    print("\n| kernel | calls | total ms | avg us | share |\n|---|---:|---:|---:|---:|")
+    # median / max per call separate the steady decode launches from the (rarer,
+    # larger) mixed prefill launches of the same kernel
+    print("\n| kernel | calls | total ms | avg us | median us | max us | share |\n|---|---:|---:|---:|---:|---:|---:|")
     for n, (d, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:a.top]:
         short = n.split("(")[0][:90].replace("|", "/")
-        print(f"| `{short}` | {c} | {d / 1e6:.2f} | {d / c / 1e3:.1f} | {100 * d / 1e6 / busy:.1f}% |")
+        v = sorted(durs[n])
+        med, mx = v[len(v) // 2] / 1e3, v[-1] / 1e3
+        print(f"| `{short}` | {c} | {d / 1e6:.2f} | {d / c / 1e3:.1f} | {med:.1f} | {mx:.1f} | {100 * d / 1e6 / busy:.1f}% |")
 
 
 if __name__ == "__main__":

@@ -356,14 +356,20 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
 // Grouped (MoE) form of the same pipeline: W [E, N, K]; x rows gathered through
 // the block-64 padded expert-sorted layout (rows[p] = source row, -1 = pad;
 // rows == nullptr: x already in padded layout); offs[E+1] padded segment starts.
-// One workgroup per (column tile, k-split, expert) loops over the expert's
-// 64-row tiles (the same weight column tile is re-read from L2/MALL, not HBM).
+// Grid (column tiles, k-splits, P / 64 row tiles): one workgroup per row tile, so
+// an expert's row tiles run concurrently -- the column tiles of one row tile
+// (N / cols <= a few hundred) are fewer than the resident workgroups, so the
+// next row tiles of the same weight tile are in flight together and re-read it
+// from L2/MALL (a per-expert loop over row tiles serialised them). The column
+// tile stays the fastest dimension: consecutive workgroups spread over the 8 XCDs
+// (row-tile-fastest put a batch-1 step's two active experts on 2 XCDs). Row tiles
+// past the last expert's segment (capacity padding) exit at once.
 template <int NW, int WV, int KC, bool NT>
 __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uint16_t* __restrict__ x,
                                                                        const int32_t* __restrict__ rows,
-                                                                       const int32_t* __restrict__ offs, int K,
-                                                                       const uint16_t* __restrict__ w, int N, int P,
-                                                                       float* __restrict__ part,
+                                                                       const int32_t* __restrict__ offs, int E,
+                                                                       int K, const uint16_t* __restrict__ w, int N,
+                                                                       int P, float* __restrict__ part,
                                                                        uint16_t* __restrict__ out, int mode) {
   constexpr int MT = 4;
   constexpr int RB = KC * 2;
@@ -381,9 +387,12 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
   __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
 
-  const int e = blockIdx.z;
+  const int rt0 = blockIdx.z * 64;
+  int e = -1;
+  for (int i = 0; i < E; ++i)
+    if (rt0 >= offs[i] && rt0 < offs[i + 1]) e = i;
+  if (e < 0) return;  // capacity padding past the last segment
   const int p0 = offs[e], p1 = offs[e + 1];
-  if (p1 <= p0) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int S = gridDim.y, s = blockIdx.y;
@@ -403,8 +412,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
   // (one 64-row tile); with several row tiles the re-reads should hit L2/MALL
   const bool nt = NT && (p1 - p0) <= 64;
 
-  for (int rt = p0; rt < p1; rt += 64) {
-    if (rt != p0) raw_barrier();  // the previous tile's last slot may still be read
+  {
+    const int rt = rt0;
     const int first = rows ? rows[rt] : rt;
     const uint16_t* xsrc[XI];
 #pragma unroll
@@ -512,11 +521,11 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
 
 template <int NW>
 static void launch_m64g_grouped(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, const int32_t* rows,
-                                const int32_t* offs, int K, const uint16_t* w, int N, int P, float* part,
+                                const int32_t* offs, int E, int K, const uint16_t* w, int N, int P, float* part,
                                 uint16_t* out, int mode) {
 #define XGK_GRP(WV, KC, NT)                                                                                    \
-  hipLaunchKernelGGL((gemm_m64g_grouped_kernel<NW, WV, KC, NT>), grid, dim3(64 * WV), 0, st, x, rows, offs, K, w, \
-                     N, P, part, out, mode)
+  hipLaunchKernelGGL((gemm_m64g_grouped_kernel<NW, WV, KC, NT>), grid, dim3(64 * WV), 0, st, x, rows, offs, E, K, \
+                     w, N, P, part, out, mode)
   switch (cfg) {
     case 1: XGK_GRP(4, 128, true); break;
     case 2: XGK_GRP(4, 64, false); break;
@@ -542,9 +551,9 @@ int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, i
   if (mode == GG_PARTIAL && part == nullptr) return 1;
   if (mode != GG_PARTIAL && out == nullptr) return 1;
   if (P == 0) return 0;
-  const dim3 grid(N / cols, S, E);
-  if (nw == 1) launch_m64g_grouped<1>(cfg, grid, st, x, rows, offs, K, w, N, P, part, out, mode);
-  else launch_m64g_grouped<2>(cfg, grid, st, x, rows, offs, K, w, N, P, part, out, mode);
+  const dim3 grid(N / cols, S, P / 64);
+  if (nw == 1) launch_m64g_grouped<1>(cfg, grid, st, x, rows, offs, E, K, w, N, P, part, out, mode);
+  else launch_m64g_grouped<2>(cfg, grid, st, x, rows, offs, E, K, w, N, P, part, out, mode);
   return 0;
 }
 

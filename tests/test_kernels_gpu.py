@@ -263,8 +263,9 @@ def test_moe_route_matches_fp32(T, E, k, H):
 
 @pytest.mark.parametrize("glds", [True, False])
 @pytest.mark.parametrize("T", [1, 3, 64, 150])
-def test_fused_moe_both_pipelines(T, glds):
+def test_fused_moe_both_pipelines(T, glds, monkeypatch):
     from xgserve.ops import moe as M
+    monkeypatch.setattr(M, "MOE_DENSE_MIN_PAIRS", 1 << 30)  # the grouped pipelines at every T
     E, k, H, F = 8, 2, 1024, 512
     x = rnd(T, H)
     w13 = _w13(E, F, H)
@@ -302,3 +303,27 @@ def test_decode_attention_split_combine_rearms(in_kernel):
     finally:
         A.IN_KERNEL_COMBINE = old
     assert int(ws.counters.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("T,offset", [(300, 0), (300, 4), (1100, 0)])
+def test_fused_moe_prefill_per_expert_path(T, offset, monkeypatch):
+    """Prefill-sized MoE (per-expert hipBLASLt path) vs the fp32 reference and vs the
+    grouped m64g path on the same routing, incl. an expert-parallel shard."""
+    from xgserve.ops import moe as MO
+    E, k, H, F = 8, 2, 1024, 512
+    El = 4 if offset else E
+    x = rnd(T, H)
+    w13 = _w13(El, F, H)
+    w2 = rnd(El, H, F, scale=0.05)
+    logits = rnd(T, E, dtype=torch.float32)
+    w, ids = ops.moe_topk_softmax(logits, k)
+    monkeypatch.setattr(MO, "MOE_DENSE_MIN_PAIRS", 1)
+    dense = ops.fused_moe(x, w13, w2, w, ids, offset)
+    monkeypatch.setattr(MO, "MOE_DENSE_MIN_PAIRS", 1 << 30)
+    grouped = ops.fused_moe(x, w13, w2, w, ids, offset)
+    ref = ops.moe_forward_ref(x.cpu(), w13.cpu(), w2.cpu(), w.cpu(), ids.cpu(), offset).float()
+    # the hipBLASLt path rounds gate and up to bf16 before the SiLU-gate (the grouped
+    # kernel applies it to fp32 accumulators): one extra bf16 rounding
+    tol = 3e-2 * ref.std().item()
+    torch.testing.assert_close(dense.cpu().float(), ref, atol=tol, rtol=3e-2)
+    torch.testing.assert_close(dense.float(), grouped.float(), atol=tol, rtol=3e-2)

@@ -15,6 +15,14 @@ MOE_GLDS = True  # expert GEMMs on the LDS-DMA pipeline (gemm_m64g.hip); False: 
 # (Mixtral 8x7B, T = 1 / 32 / 64: w13 cfg 3 = 352 vs 384 us at T=64; w2 nw 2 + cfg 1 = 153 vs ~175 us)
 MOE_CFG_W13 = 3
 MOE_CFG_W2 = 1
+# Optional prefill MoE path (>= this many (token, expert) pairs, eager steps only):
+# read the expert offsets to the host (one small sync) and run each expert's rows
+# as two hipBLASLt GEMMs around the SiLU-gate kernel. Off by default: measured on
+# Mixtral 64-concurrent the grouped m64g kernel (one workgroup per 64-row tile,
+# an expert's tiles sharing its weight stream through L2/MALL) is faster
+# (2,680 vs 2,638 tok/s); XGS_MOE_DENSE_MIN_PAIRS=256 turns it on.
+import os as _os
+MOE_DENSE_MIN_PAIRS = int(_os.environ.get("XGS_MOE_DENSE_MIN_PAIRS", str(1 << 30)))
 
 
 def moe_topk_softmax(router_logits: torch.Tensor, k: int, renorm: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -104,6 +112,8 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     F = F2 // 2
     sorted_rows, offs, dest = moe_align(topk_ids, E, expert_offset)
     P = sorted_rows.shape[0]
+    if T * k >= MOE_DENSE_MIN_PAIRS and not torch.cuda.is_current_stream_capturing():
+        return _moe_per_expert(x, w13, w2, topk_w, sorted_rows, offs, dest, T, k)
     act = torch.empty(P, F, dtype=x.dtype, device=x.device)
     kn = kernels()
     if MOE_GLDS:
@@ -130,4 +140,25 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     out = torch.empty(T, H, dtype=x.dtype, device=x.device)
     kn.moe_combine(part.data_ptr(), S, P, dest.data_ptr(), topk_w.float().contiguous().data_ptr(), out.data_ptr(), T,
                    k, H, stream_ptr())
+    return out
+
+
+def _moe_per_expert(x, w13, w2, topk_w, sorted_rows, offs, dest, T, k):
+    """Prefill-sized MoE: per active expert, its padded row segment (rows gathered
+    from x; pad rows read row 0 and are never combined) -> hipBLASLt gate_up ->
+    SiLU-gate -> hipBLASLt down -> fp32 slab row segment -> the same combine."""
+    E, F2, H = w13.shape
+    P = sorted_rows.shape[0]
+    o = offs.tolist()  # host sync: E + 1 ints
+    xs = x.index_select(0, sorted_rows.clamp(min=0).long())
+    part = torch.empty(1, P, H, dtype=torch.float32, device=x.device)
+    for e in range(E):
+        a, b = o[e], o[e + 1]
+        if b <= a:
+            continue
+        act = silu_and_mul(torch.mm(xs[a:b], w13[e].t()), interleave16=True)
+        part[0, a:b].copy_(torch.mm(act, w2[e].t()))
+    out = torch.empty(T, H, dtype=x.dtype, device=x.device)
+    kernels().moe_combine(part.data_ptr(), 1, P, dest.data_ptr(), topk_w.float().contiguous().data_ptr(),
+                          out.data_ptr(), T, k, H, stream_ptr())
     return out
