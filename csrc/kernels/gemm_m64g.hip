@@ -364,25 +364,25 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
 // tile stays the fastest dimension: consecutive workgroups spread over the 8 XCDs
 // (row-tile-fastest put a batch-1 step's two active experts on 2 XCDs). Row tiles
 // past the last expert's segment (capacity padding) exit at once.
-template <int NW, int WV, int KC, bool NT>
+template <int NW, int WV, int KC, bool NT, int MT>
 __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uint16_t* __restrict__ x,
                                                                        const int32_t* __restrict__ rows,
                                                                        const int32_t* __restrict__ offs, int E,
                                                                        int K, const uint16_t* __restrict__ w, int N,
                                                                        int P, float* __restrict__ part,
                                                                        uint16_t* __restrict__ out, int mode) {
-  constexpr int MT = 4;
   constexpr int RB = KC * 2;
   constexpr int GPR = KC / 8;
   constexpr int RPI = 1024 / RB;
-  constexpr int XBYTES = 64 * RB;
-  constexpr int XI = 64 / RPI / WV;
+  constexpr int XROWS = 16 * MT;  // MT = 1: <= 16 real rows per expert (batch <= 8 at top-2)
+  constexpr int XBYTES = XROWS * RB;
+  constexpr int XI = XROWS / RPI / WV;
   constexpr int WROWS = 16 * NW;
   constexpr int WI = WROWS / RPI;
   constexpr int WBYTES = WROWS * RB;
   constexpr int SLOT = XBYTES + WV * WBYTES;
   constexpr int G = XI + WI;
-  static_assert(XI >= 1 && WI >= 1 && 64 % (RPI * WV) == 0, "bad m64g geometry");
+  static_assert(XI >= 1 && WI >= 1 && XROWS % (RPI * WV) == 0, "bad m64g geometry");
   __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
@@ -519,46 +519,6 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
   }
 }
 
-template <int NW>
-static void launch_m64g_grouped(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, const int32_t* rows,
-                                const int32_t* offs, int E, int K, const uint16_t* w, int N, int P, float* part,
-                                uint16_t* out, int mode) {
-#define XGK_GRP(WV, KC, NT)                                                                                    \
-  hipLaunchKernelGGL((gemm_m64g_grouped_kernel<NW, WV, KC, NT>), grid, dim3(64 * WV), 0, st, x, rows, offs, E, K, \
-                     w, N, P, part, out, mode)
-  switch (cfg) {
-    case 1: XGK_GRP(4, 128, true); break;
-    case 2: XGK_GRP(4, 64, false); break;
-    case 3: XGK_GRP(4, 64, true); break;
-    case 4: XGK_GRP(2, 64, false); break;
-    case 5: XGK_GRP(2, 64, true); break;
-    case 6: XGK_GRP(2, 128, true); break;
-    default: XGK_GRP(4, 128, false); break;
-  }
-#undef XGK_GRP
-}
-
-int m64g_cfg_waves(int cfg);
-int m64g_cfg_kc(int cfg);
-
-int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, int E, int K, const uint16_t* w, int N,
-                  int P, float* part, uint16_t* out, int S, int mode, int nw, int cfg, hipStream_t st) {
-  if (E < 1 || P < 0 || P % 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 6) return 1;
-  if (mode != GG_BF16 && mode != GG_PARTIAL && mode != GG_SILU) return 1;
-  const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
-  if (K % (S * kc) || N % cols) return 1;
-  if (mode == GG_SILU && (nw != 2 || S != 1)) return 1;
-  if (mode == GG_PARTIAL && part == nullptr) return 1;
-  if (mode != GG_PARTIAL && out == nullptr) return 1;
-  if (P == 0) return 0;
-  const dim3 grid(N / cols, S, P / 64);
-  if (nw == 1) launch_m64g_grouped<1>(cfg, grid, st, x, rows, offs, E, K, w, N, P, part, out, mode);
-  else launch_m64g_grouped<2>(cfg, grid, st, x, rows, offs, E, K, w, N, P, part, out, mode);
-  return 0;
-}
-
-// cfg: 0 = (4 waves, KC 128), 1 = (4, 128, nt), 2 = (4, 64), 3 = (4, 64, nt),
-//      4 = (2, 64), 5 = (2, 64, nt), 6 = (2, 128, nt)
 // M <= 16 takes the one-x-tile kernel (MT = 1) except for the 4-wave KC-64 configs,
 // whose 16 x rows would be less than one DMA instruction per wave.
 // XGS_M64G_MT1=0 keeps MT = 4 everywhere (A/B).
@@ -570,6 +530,56 @@ static bool m64g_mt1_enabled() {
   return on;
 }
 
+template <int NW>
+static void launch_m64g_grouped(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, const int32_t* rows,
+                                const int32_t* offs, int E, int K, const uint16_t* w, int N, int P, float* part,
+                                uint16_t* out, int mode, bool mt1) {
+#define XGK_GRP_MT(WV, KC, NT, MT)                                                                              \
+  hipLaunchKernelGGL((gemm_m64g_grouped_kernel<NW, WV, KC, NT, MT>), grid, dim3(64 * WV), 0, st, x, rows, offs, E, \
+                     K, w, N, P, part, out, mode)
+#define XGK_GRP(WV, KC, NT)              \
+  do {                                   \
+    if (mt1) XGK_GRP_MT(WV, KC, NT, 1);  \
+    else XGK_GRP_MT(WV, KC, NT, 4);      \
+  } while (0)
+  // the 4-wave KC-64 configs have < 1 x DMA instruction per wave at 16 rows: MT = 4
+  switch (cfg) {
+    case 1: XGK_GRP(4, 128, true); break;
+    case 2: XGK_GRP_MT(4, 64, false, 4); break;
+    case 3: XGK_GRP_MT(4, 64, true, 4); break;
+    case 4: XGK_GRP(2, 64, false); break;
+    case 5: XGK_GRP(2, 64, true); break;
+    case 6: XGK_GRP(2, 128, true); break;
+    default: XGK_GRP(4, 128, false); break;
+  }
+#undef XGK_GRP
+#undef XGK_GRP_MT
+}
+
+int m64g_cfg_waves(int cfg);
+int m64g_cfg_kc(int cfg);
+
+// max_rows: a bound on the real rows of any expert (<= 16 selects the one-x-tile
+// kernel; rows 16..63 of each padded tile are then left unwritten -- pads only).
+int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, int E, int K, const uint16_t* w, int N,
+                  int P, float* part, uint16_t* out, int S, int mode, int nw, int cfg, int max_rows, hipStream_t st) {
+  if (E < 1 || P < 0 || P % 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 6) return 1;
+  if (mode != GG_BF16 && mode != GG_PARTIAL && mode != GG_SILU) return 1;
+  const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
+  if (K % (S * kc) || N % cols) return 1;
+  if (mode == GG_SILU && (nw != 2 || S != 1)) return 1;
+  if (mode == GG_PARTIAL && part == nullptr) return 1;
+  if (mode != GG_PARTIAL && out == nullptr) return 1;
+  if (P == 0) return 0;
+  const dim3 grid(N / cols, S, P / 64);
+  const bool mt1 = max_rows <= 16 && cfg != 2 && cfg != 3 && m64g_mt1_enabled();
+  if (nw == 1) launch_m64g_grouped<1>(cfg, grid, st, x, rows, offs, E, K, w, N, P, part, out, mode, mt1);
+  else launch_m64g_grouped<2>(cfg, grid, st, x, rows, offs, E, K, w, N, P, part, out, mode, mt1);
+  return 0;
+}
+
+// cfg: 0 = (4 waves, KC 128), 1 = (4, 128, nt), 2 = (4, 64), 3 = (4, 64, nt),
+//      4 = (2, 64), 5 = (2, 64, nt), 6 = (2, 128, nt)
 template <int NW>
 static void launch_m64g(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N,
                         float* part, uint16_t* out, int mode, const M64Epi& epi) {

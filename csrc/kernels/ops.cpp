@@ -30,7 +30,7 @@ int decode_attention_fq(const float*, int, const int32_t*, const float*, const i
                         const int32_t*, int, const int32_t*, float*, float*, uint16_t*, int64_t, int, int, int, int,
                         int, float, int, int, hipStream_t);
 int moe_gemm_m64g(const uint16_t*, const int32_t*, const int32_t*, int, int, const uint16_t*, int, int, float*,
-                  uint16_t*, int, int, int, int, hipStream_t);
+                  uint16_t*, int, int, int, int, int, hipStream_t);
 void add_partials_rmsnorm(const float*, int, int, uint16_t*, const uint16_t*, uint16_t*, int, float, hipStream_t);
 void reduce_partials(const float*, int, int64_t, uint16_t*, hipStream_t);
 int rope_cache_partials(const float*, int, uint16_t*, int64_t, const int32_t*, const float*, uint16_t*, uint16_t*,
@@ -244,8 +244,17 @@ PYBIND11_MODULE(_kernels, m) {
                             uintptr_t part, uintptr_t out, int splits, int mode, int nw, int cfg, uintptr_t st) {
     check(xgk::moe_gemm_m64g(P<const uint16_t>(x), P<const int32_t>(rows), P<const int32_t>(offs), E, K,
                              P<const uint16_t>(w), N, P_, P<float>(part), P<uint16_t>(out), splits, mode, nw, cfg,
-                             S(st)),
+                             64, S(st)),
           "moe_gemm_m64g");
+  });
+  // same, with a host-known bound on the real rows of any expert (<= 16: one-x-tile kernel)
+  m.def("moe_gemm_m64g_rows", [](uintptr_t x, uintptr_t rows, uintptr_t offs, int E, int K, uintptr_t w, int N, int P_,
+                                 uintptr_t part, uintptr_t out, int splits, int mode, int nw, int cfg, int max_rows,
+                                 uintptr_t st) {
+    check(xgk::moe_gemm_m64g(P<const uint16_t>(x), P<const int32_t>(rows), P<const int32_t>(offs), E, K,
+                             P<const uint16_t>(w), N, P_, P<float>(part), P<uint16_t>(out), splits, mode, nw, cfg,
+                             max_rows, S(st)),
+          "moe_gemm_m64g_rows");
   });
   m.def("moe_route", [](uintptr_t h, uintptr_t wr, int T, int H, int E, int k, int renorm, uintptr_t w, uintptr_t ids,
                         uintptr_t st) {

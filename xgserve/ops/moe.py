@@ -117,8 +117,10 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     act = torch.empty(P, F, dtype=x.dtype, device=x.device)
     kn = kernels()
     if MOE_GLDS:
+        max_rows = T * k  # no expert holds more rows than (token, choice) pairs
+
         def gemm(*a, cfg=0):
-            kn.moe_gemm_m64g(*a[:-1], cfg, a[-1])
+            kn.moe_gemm_m64g_rows(*a[:-1], cfg, max_rows, a[-1])
     else:
         def gemm(*a, cfg=0):
             kn.moe_gemm_m64(*a)
