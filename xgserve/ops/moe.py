@@ -12,8 +12,9 @@ BLOCK_M = 64
 MOE_GLDS = True  # expert GEMMs on the LDS-DMA pipeline (gemm_m64g.hip); False: register-ring gemm_m64
 # gemm_m64g launch configurations for the expert GEMMs (see ops/linear.py M64G_CFGS);
 # measured with bench/gemm_bench.py --moe-sweep
-# (Mixtral 8x7B, T = 1 / 32 / 64: w13 cfg 3 = 352 vs 384 us at T=64; w2 nw 2 + cfg 1 = 153 vs ~175 us)
-MOE_CFG_W13 = 3
+# (Mixtral 8x7B; profiles/r1_moe_sweep_v2.jsonl, per-row-tile grid + MT=1: w13 cfg 5 = 324 us at
+# T=64 (cfg 3: 338), 81 us at T=1; w2 nw 2 + cfg 1 = 153 us at T=64)
+MOE_CFG_W13 = 5  # (2 waves, KC 64, nt): best at T = 1..64 with the per-row-tile grid (bench --moe-sweep)
 MOE_CFG_W2 = 1
 # Optional prefill MoE path (>= this many (token, expert) pairs, eager steps only):
 # read the expert offsets to the host (one small sync) and run each expert's rows
