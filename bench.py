@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--max-batched-tokens", type=int, default=8192)
     ap.add_argument("--moe-comm", default="alltoall", choices=["alltoall", "allreduce"])
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--weight-dtype", default=None, choices=["fp8"],
+                    help="fp8: E4M3 weight copies for batch <= 16 decode (not the bf16 headline)")
     ap.add_argument("--no-prefix-cache", action="store_true")
     return ap.parse_args()
 
@@ -64,6 +66,7 @@ def main():
     ecfg = EngineConfig(model=a.model, device=str(dev), tp=a.tp, max_num_seqs=max(64, a.concurrency),
                         max_num_batched_tokens=a.max_batched_tokens, max_model_len=max_len,
                         use_graphs=not a.no_graphs, enable_prefix_cache=not a.no_prefix_cache, moe_comm=a.moe_comm,
+                        weight_dtype=a.weight_dtype,
                         graph_batch_sizes=[b for b in [1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128]
                                            if b <= max(64, a.concurrency)], seed=st.dp_rank)
     eng = LLMEngine(ecfg)
@@ -155,7 +158,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if a.weight_dtype is None else "bf16 activations, fp8 (E4M3) decode weights",
             "data": "synthetic (random-token prompts, random-init weights)",
             "ttft_p50_ms": round(1000 * p50, 2) if p50 == p50 else None,
             "config": {"model": a.model, "global_batch": a.concurrency * dp,

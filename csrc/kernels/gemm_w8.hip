@@ -1,0 +1,208 @@
+// Decode GEMM with FP8 weights (OCP E4M3, one fp32 scale per output channel) and
+// bf16 activations: out = x . (diag(s) W8)^T for M <= 16 (batch <= 16 decode).
+//
+// Weight-only FP8 halves the bytes of a bandwidth-bound decode step. The weights
+// stream through the same LDS-DMA pipeline as gemm_m64g (3 slots, 2 chunks in
+// flight, counted vmcnt + raw barrier, non-temporal weight DMA); each A fragment is
+// read as 8 fp8 bytes and widened to bf16 in registers with v_cvt_scalef32_pk_bf16_fp8
+// (exact: every E4M3 value is representable in bf16), then the bf16 MFMA
+// (16x16x32) runs as in the bf16 kernel. The per-channel scale is applied to the
+// fp32 accumulators in the epilogue. Activations stay bf16 (no activation
+// quantisation): the accuracy is that of the rounded weights alone.
+//
+//   weights [N, K] uint8 (E4M3), scale [N] fp32; x [M, K] bf16 (M <= 16).
+//   LDS: x rows 2*KC bytes, weight rows KC bytes, 16-B granules XOR-swizzled by
+//   row on the GLOBAL source address (DMA writes are lane-linear).
+//   modes: W8_PARTIAL -> fp32 split-K partials [S, M, N] (reduced by the consumer
+//   kernel, like gemm_m64g's); W8_SILU -> bf16 silu(gate) * up from block-16
+//   interleaved gate|up rows (split 1).
+#include "glds.h"
+
+namespace xgk {
+
+enum : int { W8_PARTIAL = 1, W8_SILU = 2 };
+
+// 8 E4M3 bytes (k order) -> bf16x8 A fragment
+__device__ __forceinline__ bf16x8_t fp8x8_to_bf16(uint2 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const auto a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.x, 1.0f, false);
+  const auto b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.x, 1.0f, true);
+  const auto c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.y, 1.0f, false);
+  const auto d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.y, 1.0f, true);
+  return as_frag(make_uint4(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
+                            __builtin_bit_cast(uint32_t, c), __builtin_bit_cast(uint32_t, d)));
+#else
+  return bf16x8_t{};
+#endif
+}
+
+//   NW  16-column MFMA tiles per wave (SiLU needs 2: one gate + one up tile)
+//   WV  waves per workgroup
+//   KC  k per chunk (fp8 row = KC bytes, bf16 x row = 2 KC bytes)
+template <int NW, int WV, int KC>
+__global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __restrict__ x, int M, int K,
+                                                             const uint8_t* __restrict__ w,
+                                                             const float* __restrict__ wscale, int N,
+                                                             float* __restrict__ part, uint16_t* __restrict__ out,
+                                                             int mode) {
+  constexpr int XRB = KC * 2, WRB = KC;          // bytes per LDS row
+  constexpr int XG = XRB / 16, WG = WRB / 16;    // 16-B granules per row
+  constexpr int XRPI = 1024 / XRB, WRPI = 1024 / WRB;  // rows per DMA instruction
+  constexpr int XBYTES = 16 * XRB;
+  constexpr int XI = 16 / XRPI / WV;             // x DMA instructions per wave per chunk
+  constexpr int WROWS = 16 * NW;
+  constexpr int WI = WROWS / WRPI;               // weight DMA instructions per wave per chunk
+  constexpr int WBYTES = WROWS * WRB;
+  constexpr int SLOT = XBYTES + WV * WBYTES;
+  constexpr int G = XI + WI;
+  static_assert(XI >= 1 && WI >= 1 && 16 % (XRPI * WV) == 0 && WROWS % WRPI == 0, "bad w8 geometry");
+  __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
+  __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
+  __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int S = gridDim.y, s = blockIdx.y;
+  const int kws = K / S;
+  const int k0 = s * kws;
+  const int nchunks = kws / KC;
+  const int nbase = blockIdx.x * (16 * NW * WV) + wid * WROWS;
+
+  const uint8_t* wsrc[WI];
+  {
+    const int dr = lane / WG, dj = lane % WG;
+#pragma unroll
+    for (int i = 0; i < WI; ++i) {
+      const int r = WRPI * i + dr;
+      wsrc[i] = w + static_cast<int64_t>(nbase + r) * K + k0 + 16 * (dj ^ (r & (WG - 1)));
+    }
+  }
+  const uint16_t* xsrc[XI];
+  {
+    const int dr = lane / XG, dj = lane % XG;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int r = XRPI * (wid * XI + i) + dr;  // x row 0..15
+      xsrc[i] = x + static_cast<int64_t>(min(r, M - 1)) * K + k0 + 8 * (dj ^ (r & (XG - 1)));
+    }
+  }
+
+  auto issue = [&](uint8_t* slot, int c) {
+    const int kk = c * KC;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) glds16(xsrc[i] + kk, slot + XRPI * (wid * XI + i) * XRB);
+#pragma unroll
+    for (int i = 0; i < WI; ++i) glds16_nt(wsrc[i] + kk, slot + XBYTES + wid * WBYTES + i * 1024);
+  };
+
+  f32x4_t acc[NW];
+#pragma unroll
+  for (int nt = 0; nt < NW; ++nt) acc[nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](const uint8_t* slot) {
+    const uint8_t* xs = slot;
+    const uint8_t* ws = slot + XBYTES + wid * WBYTES;
+#pragma unroll
+    for (int t = 0; t < KC / 32; ++t) {
+      // x (B operand): row li, k = 32t + 8g.. -> bf16 granule 4t + g
+      const uint4 b = *reinterpret_cast<const uint4*>(xs + li * XRB + (((4 * t + g) ^ (li & (XG - 1))) * 16));
+#pragma unroll
+      for (int nt = 0; nt < NW; ++nt) {
+        // W (A operand): row 16 nt + li, k = 32t + 8g.. -> fp8 granule 2t + g/2, byte (g & 1) * 8
+        const int row = 16 * nt + li;
+        const uint2 a8 = *reinterpret_cast<const uint2*>(ws + row * WRB +
+                                                         (((2 * t + (g >> 1)) ^ (row & (WG - 1))) * 16) +
+                                                         (g & 1) * 8);
+        acc[nt] = mfma16x16x32(fp8x8_to_bf16(a8), as_frag(b), acc[nt]);
+      }
+    }
+  };
+
+  auto step = [&](uint8_t* cur, uint8_t* nxt2, int c) {
+    if (c + 1 < nchunks) wait_vmcnt<G>();
+    else wait_vmcnt<0>();
+    raw_barrier();
+    if (c + 2 < nchunks) issue(nxt2, c + 2);
+    compute(cur);
+  };
+
+  issue(lds0, 0);
+  if (nchunks > 1) issue(lds1, 1);
+  int c = 0;
+  for (; c + 3 <= nchunks; c += 3) {
+    step(lds0, lds2, c);
+    step(lds1, lds0, c + 1);
+    step(lds2, lds1, c + 2);
+  }
+  if (c < nchunks) step(lds0, lds2, c);
+  if (c + 1 < nchunks) step(lds1, lds0, c + 1);
+
+  // acc[nt][r] = out[m = li][n = nbase + 16 nt + 4 g + r] / scale[n]
+#pragma unroll
+  for (int nt = 0; nt < NW; ++nt) {
+    const float4 sc = *reinterpret_cast<const float4*>(wscale + nbase + 16 * nt + 4 * g);
+    acc[nt][0] *= sc.x;
+    acc[nt][1] *= sc.y;
+    acc[nt][2] *= sc.z;
+    acc[nt][3] *= sc.w;
+  }
+  const int m = li;
+  if (m >= M) return;
+  if (mode == W8_PARTIAL) {
+    float* pp = part + static_cast<int64_t>(s) * M * N + static_cast<int64_t>(m) * N;
+#pragma unroll
+    for (int nt = 0; nt < NW; ++nt)
+      *reinterpret_cast<float4*>(pp + nbase + 16 * nt + 4 * g) =
+          make_float4(acc[nt][0], acc[nt][1], acc[nt][2], acc[nt][3]);
+  } else if (NW == 2) {
+    const int F = N / 2, f0 = nbase / 2 + 4 * g;
+    float o[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float gt = acc[0][r];
+      o[r] = gt / (1.f + __expf(-gt)) * acc[NW - 1][r];
+    }
+    uint2 v;
+    v.x = pack2(o[0], o[1]);
+    v.y = pack2(o[2], o[3]);
+    *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * F + f0) = v;
+  }
+}
+
+// cfg: 0 = (NW 2, 4 waves, KC 128), 1 = (2, 2, 128), 2 = (1, 4, 128), 3 = (2, 2, 256), 4 = (2, 4, 256)
+static int w8_cfg_cols(int cfg) {
+  switch (cfg) {
+    case 0: return 128;
+    case 1: return 64;
+    case 2: return 64;
+    case 3: return 64;
+    case 4: return 128;
+    default: return 0;
+  }
+}
+static int w8_cfg_kc(int cfg) { return cfg >= 3 ? 256 : 128; }
+static int w8_cfg_nw(int cfg) { return cfg == 2 ? 1 : 2; }
+
+int gemm_w8(const uint16_t* x, int M, int K, const uint8_t* w, const float* scale, int N, float* part,
+            uint16_t* out, int S, int mode, int cfg, hipStream_t st) {
+  if (M < 1 || M > 16 || S < 1 || cfg < 0 || cfg > 4) return 1;
+  if (mode != W8_PARTIAL && mode != W8_SILU) return 1;
+  const int cols = w8_cfg_cols(cfg), kc = w8_cfg_kc(cfg);
+  if (N % cols || K % (S * kc)) return 1;
+  if (mode == W8_SILU && (w8_cfg_nw(cfg) != 2 || S != 1 || out == nullptr)) return 1;
+  if (mode == W8_PARTIAL && part == nullptr) return 1;
+  const dim3 grid(N / cols, S);
+#define XGK_W8(NW, WV, KC) \
+  hipLaunchKernelGGL((gemm_w8_kernel<NW, WV, KC>), grid, dim3(64 * WV), 0, st, x, M, K, w, scale, N, part, out, mode)
+  switch (cfg) {
+    case 0: XGK_W8(2, 4, 128); break;
+    case 1: XGK_W8(2, 2, 128); break;
+    case 2: XGK_W8(1, 4, 128); break;
+    case 3: XGK_W8(2, 2, 256); break;
+    default: XGK_W8(2, 4, 256); break;
+  }
+#undef XGK_W8
+  return 0;
+}
+
+}  // namespace xgk

@@ -47,6 +47,8 @@ void sample_tokens(const void*, int, int64_t, int, int, const float*, const floa
                    uint64_t, int32_t*, float*, hipStream_t);
 void segment_sum(const uint16_t*, int, const int32_t*, const int32_t*, float*, int, hipStream_t);
 void subst_tokens(int32_t*, const int32_t*, const int32_t*, int, hipStream_t);
+int gemm_w8(const uint16_t*, int, int, const uint8_t*, const float*, int, float*, uint16_t*, int, int, int,
+            hipStream_t);
 void moe_topk_softmax(const void*, int, int, int, int, int, float*, int32_t*, hipStream_t);
 void moe_align(const int32_t*, int, int, int, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
 int moe_combine(const void*, int, int, const int32_t*, const float*, uint16_t*, int, int, int, hipStream_t);
@@ -174,6 +176,12 @@ PYBIND11_MODULE(_kernels, m) {
     xgk::sample_tokens(P<const void>(logits), is_f32, stride, B, V, P<const float>(temps), P<const float>(top_ps),
                        P<const int32_t>(top_ks), P<const uint64_t>(seeds), step, P<int32_t>(tok), P<float>(lp), S(st));
     check(0, "sample_tokens");
+  });
+  m.def("gemm_w8", [](uintptr_t x, int M, int K, uintptr_t w, uintptr_t scale, int N, uintptr_t part, uintptr_t out,
+                      int splits, int mode, int cfg, uintptr_t st) {
+    check(xgk::gemm_w8(P<const uint16_t>(x), M, K, P<const uint8_t>(w), P<const float>(scale), N, P<float>(part),
+                       P<uint16_t>(out), splits, mode, cfg, S(st)),
+          "gemm_w8");
   });
   m.def("subst_tokens", [](uintptr_t ids, uintptr_t src, uintptr_t prev, int n, uintptr_t st) {
     xgk::subst_tokens(P<int32_t>(ids), P<const int32_t>(src), P<const int32_t>(prev), n, S(st));

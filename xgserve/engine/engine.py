@@ -80,6 +80,8 @@ class EngineConfig:
     # so the host's per-step work (commit, schedule, metadata, launch) overlaps the
     # GPU instead of sitting between steps. TP=1, no speculation, graph decode steps.
     async_schedule: bool = True
+    # "fp8": weight-only E4M3 copies for batch <= 16 decode (bf16 activations)
+    weight_dtype: Optional[str] = None
 
     def resolved_device(self) -> torch.device:
         if self.device:
@@ -101,7 +103,8 @@ class LLMEngine:
                  None: None}[cfg.dtype]
         t0 = time.time()
         self.model = model if model is not None else build_model(self.mcfg, device=device, dtype=dtype,
-                                                                 checkpoint=cfg.checkpoint, seed=cfg.seed)
+                                                                 checkpoint=cfg.checkpoint, seed=cfg.seed,
+                                                                 weight_dtype=cfg.weight_dtype)
         self.model.set_moe_comm(cfg.moe_comm)
         self.load_time = time.time() - t0
         from ..parallel.custom_ar import maybe_enable

@@ -30,8 +30,9 @@ import torch.nn.functional as F
 from .. import ops
 from ..parallel import comm
 from ..parallel.state import get_state
-from ..ops.linear import (MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, ResidWorkspace, RowStats, m64_linear,
-                          m64_norm_linear, m64_plan, m64_resid_linear, pick_split, skinny_linear)
+from ..ops.linear import (MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, W8_MAX_M, ResidWorkspace, RowStats, m64_linear,
+                          m64_norm_linear, m64_plan, m64_resid_linear, pick_split, quantize_fp8, skinny_linear,
+                          w8_linear, w8_plan)
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
 from .config import ModelConfig
 
@@ -116,6 +117,7 @@ class LlamaLayer(nn.Module):
         self.m64_silu_ok = self.m64_ok and not self.moe and m64_plan(64, 2 * (cfg.intermediate_size // tp), H,
                                                                      MODE_SILU) is not None
         # M <= 16 too, when every projection has a measured small-M plan
+        self.w8 = None  # FP8 weight copies for batch <= 16 decode (LlamaForCausalLM.quantize_fp8)
         self.m64_small_ok = self.m64_ok and all(
             m64_plan(1, n, k, MODE_PARTIAL) is not None
             for n, k in ((Nqkv, H), (H, Hq * D)) + (() if self.moe else ((H, cfg.intermediate_size // tp),))) and (
@@ -191,6 +193,19 @@ class LlamaLayer(nn.Module):
         else:
             h, residual = ops.fused_add_rmsnorm(x, residual, self.input_norm, eps)
         T = meta.num_tokens
+        if self.w8 is not None and T <= W8_MAX_M:
+            # FP8 weights (gemm_w8): half the weight bytes of the bf16 decode chain; the
+            # split-K partials go to the same consumers (rope_cache / add+rmsnorm)
+            q = self.w8
+            pqkv = w8_linear(h, *q["qkv"], MODE_PARTIAL)
+            a = self.attn.from_partials(pqkv, meta, kv, cos_sin)
+            o = w8_linear(a, *q["o"], MODE_PARTIAL)
+            if self.tp > 1:
+                o = self._ar(o.materialize())
+            h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
+            act = w8_linear(h, *q["gate_up"], MODE_SILU)
+            d = w8_linear(act, *q["down"], MODE_PARTIAL)
+            return (d if self.tp == 1 else self._ar(d.materialize())), residual
         if self.fast_ok and T <= FAST_M_SMALL and not self.m64_small_ok:
             # M <= 16: every projection on the streaming skinny kernel (1.7x hipBLASLt
             # on QKV/O at batch 1), split-K partials reduced by the consumers
@@ -306,6 +321,7 @@ class LlamaForCausalLM(nn.Module):
         self.num_kv_heads_local = self.layers[0].Hkv
         l0 = self.layers[0]
         self.norms_folded = False
+        self.weight_dtype = "bf16"
         self._fused_ok = (self.tp == 1 and self.device.type == "cuda" and not l0.moe and l0.m64_ok
                           and l0.m64_silu_ok and cfg.head_dim == 128 and l0.Hq % l0.Hkv == 0
                           and l0.Hq // l0.Hkv in (1, 2, 4, 8) and H % 1024 == 0 and H // 1024 <= 8)
@@ -324,6 +340,27 @@ class LlamaForCausalLM(nn.Module):
             if not l.moe:
                 _fold_norm(l.gate_up, l.post_norm)
         self.norms_folded = True
+
+    @torch.no_grad()
+    def quantize_fp8(self) -> bool:
+        """Weight-only FP8 for batch <= 16 decode: per dense layer, E4M3 copies of the
+        QKV / O / gate_up / down weights with per-output-channel scales (after the
+        RMSNorm folding). Prefill and larger batches keep the bf16 weights (MFMA-
+        bound there); the fused bf16 decode layer is disabled. Returns False (and
+        changes nothing) when a shape has no gemm_w8 plan or the model is MoE."""
+        if self.device.type != "cuda" or any(l.moe for l in self.layers):
+            return False
+        l0 = self.layers[0]
+        names = ("qkv", "o", "gate_up", "down")
+        for n in names:
+            w = getattr(l0, n)
+            if w8_plan(1, w.shape[0], w.shape[1], MODE_SILU if n == "gate_up" else MODE_PARTIAL) is None:
+                return False
+        for l in self.layers:
+            l.w8 = {n: quantize_fp8(getattr(l, n)) for n in names}
+        self._fused_ok = self._fused_small_ok = False
+        self.weight_dtype = "fp8"
+        return True
 
     def fused_decode_ok(self, meta: AttnMeta) -> bool:
         T = meta.num_tokens

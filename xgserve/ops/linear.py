@@ -297,3 +297,72 @@ def deinterleave_gate_up(w: torch.Tensor):
     F2, H = w.shape
     v = w.reshape(F2 // 32, 2, 16, H)
     return v[:, 0].reshape(F2 // 2, H), v[:, 1].reshape(F2 // 2, H)
+
+
+# ---------------------------------------------------------------------------- FP8 weights
+# Weight-only FP8 (OCP E4M3 + one fp32 scale per output channel) for batch <= 16
+# decode: csrc/kernels/gemm_w8.hip streams half the bytes of the bf16 kernels.
+W8_MAX_M = 16
+# cfg -> (columns per workgroup, k chunk)
+W8_CFGS = {0: (128, 128), 1: (64, 128), 2: (64, 128), 3: (64, 256), 4: (128, 256)}
+_W8_TUNED = {}  # (N, K, mode) -> (split_k, cfg), filled from bench/gemm_bench.py --w8-sweep
+
+
+def quantize_fp8(w: torch.Tensor):
+    """[N, K] -> (uint8 E4M3 codes [N, K], fp32 per-row scales [N]) with
+    scale = max|w_row| / 448 (the E4M3 finite maximum)."""
+    wf = w.float()
+    scale = (wf.abs().amax(dim=1) / 448.0).clamp_min(1e-12)
+    q = (wf / scale[:, None]).clamp(-448.0, 448.0).to(torch.float8_e4m3fn)
+    return q.view(torch.uint8).contiguous(), scale.contiguous()
+
+
+def dequantize_fp8(q: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    return q.view(torch.float8_e4m3fn).float() * scale.float()[:, None]
+
+
+def w8_plan(M: int, N: int, K: int, mode: int):
+    """(split_k, cfg) for gemm_w8, or None. SiLU needs split 1 and two 16-column
+    tiles per wave; otherwise the smallest split-K giving >= 256 workgroups."""
+    if not (1 <= M <= W8_MAX_M):
+        return None
+    t = _W8_TUNED.get((N, K, mode))
+    if t is not None:
+        return t
+    cfg = 1
+    cols, kc = W8_CFGS[cfg]
+    if N % cols or K % kc:
+        return None
+    if mode == MODE_SILU:
+        return 1, cfg
+    S = 1
+    for s in (1, 2, 4, 8, 16):
+        if K % (s * kc):
+            break
+        S = s
+        if (N // cols) * s >= 256:
+            break
+    return S, cfg
+
+
+def w8_linear(x: torch.Tensor, q: torch.Tensor, scale: torch.Tensor, mode: int = MODE_PARTIAL,
+              plan=None, out: Optional[torch.Tensor] = None):
+    """x [M <= 16, K] bf16 . (diag(scale) q)^T: PendingSum (MODE_PARTIAL) or bf16
+    silu(gate) * up [M, N/2] from block-16 interleaved gate|up rows (MODE_SILU)."""
+    M, K = x.shape
+    N = q.shape[0]
+    p = plan or w8_plan(M, N, K, mode)
+    if p is None or not x.is_contiguous() or q.dtype != torch.uint8 or scale.dtype != torch.float32:
+        raise ValueError(f"gemm_w8: unsupported M={M} N={N} K={K} mode={mode}")
+    S, cfg = p
+    k = kernels()
+    if mode == MODE_PARTIAL:
+        part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+        k.gemm_w8(x.data_ptr(), M, K, q.data_ptr(), scale.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, cfg,
+                  stream_ptr())
+        return PendingSum(part, S)
+    if out is None:
+        out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=x.device)
+    k.gemm_w8(x.data_ptr(), M, K, q.data_ptr(), scale.data_ptr(), N, 0, out.data_ptr(), 1, MODE_SILU, cfg,
+              stream_ptr())
+    return out
