@@ -47,12 +47,16 @@ def main():
     ap.add_argument("--variants", type=int, nargs="+", default=[2, 4])
     ap.add_argument("--moe-sweep", action="store_true",
                     help="sweep the grouped (MoE) gemm_m64g configurations at Mixtral decode shapes")
+    ap.add_argument("--w8-sweep", action="store_true",
+                    help="every gemm_w8 (fp8 weight) configuration per shape at M <= 16, cold weights")
     ap.add_argument("--m64g-sweep", action="store_true",
                     help="sweep gemm_m64g (nw, split, cfg) configurations instead of the shoot-out")
     a = ap.parse_args()
     kernels()
     if a.m64g_sweep:
         return m64g_sweep(a)
+    if a.w8_sweep:
+        return w8_sweep(a)
     if a.moe_sweep:
         return moe_sweep(a)
     dev = "cuda"
@@ -103,6 +107,44 @@ def main():
                 print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "op": op, "us": round(t, 2),
                                   "TB/s": round(nbytes / t / 1e6, 3), "rel_err": err}), flush=True)
         del ws
+        torch.cuda.empty_cache()
+
+
+def w8_sweep(a):
+    """gemm_w8 configurations (split-K x cfg) per shape, cold fp8 weights; prints the
+    checked-correct ones, fastest first (TB/s counts the fp8 weight bytes)."""
+    for name in a.shapes:
+        N, K = SHAPES[name]
+        nbytes = N * K
+        copies = max(2, min(8, (1 << 30) // nbytes + 1))
+        qs = [L.quantize_fp8(torch.randn(N, K, device="cuda") * 0.02) for _ in range(copies)]
+        mode = L.MODE_SILU if name.startswith("gate_up") and not name.endswith("_p") else L.MODE_PARTIAL
+        for M in a.M:
+            if M > L.W8_MAX_M:
+                continue
+            x = torch.randn(M, K, device="cuda").bfloat16()
+            wd = L.dequantize_fp8(*qs[0])
+            if mode == L.MODE_SILU:
+                g, u = L.deinterleave_gate_up(wd)
+                want = F.silu(x.float() @ g.t()) * (x.float() @ u.t())
+            else:
+                want = x.float() @ wd.t()
+            rows = []
+            for cfg, (cols, kc) in L.W8_CFGS.items():
+                for S in ((1,) if mode == L.MODE_SILU else (1, 2, 4, 8, 16)):
+                    if N % cols or K % (S * kc) or (mode == L.MODE_SILU and cfg == 2):
+                        continue
+
+                    def fn(q, S=S, cfg=cfg):
+                        return L.w8_linear(x, q[0], q[1], mode, plan=(S, cfg))
+                    us = timeit([lambda q=q, fn=fn: fn(q) for q in qs])
+                    y = fn(qs[0])
+                    y = y.part.sum(0) if mode == L.MODE_PARTIAL else y.float()
+                    rows.append((us, S, cfg, float((y - want).norm() / want.norm())))
+            for us, S, cfg, err in sorted(rows):
+                print(json.dumps({"shape": name, "M": M, "op": f"w8(S={S},cfg={cfg})", "us": round(us, 2),
+                                  "TB/s": round(nbytes / us / 1e6, 3), "rel_err": round(err, 6)}), flush=True)
+        del qs
         torch.cuda.empty_cache()
 
 

@@ -30,7 +30,8 @@ import torch.nn.functional as F
 from .. import ops
 from ..parallel import comm
 from ..parallel.state import get_state
-from ..ops.linear import (MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, W8_MAX_M, ResidWorkspace, RowStats, m64_linear,
+from ..ops.linear import (MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace, RowStats,
+                          m64_linear,
                           m64_norm_linear, m64_plan, m64_resid_linear, pick_split, quantize_fp8, skinny_linear,
                           w8_linear, w8_plan)
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
@@ -123,6 +124,14 @@ class LlamaLayer(nn.Module):
             for n, k in ((Nqkv, H), (H, Hq * D)) + (() if self.moe else ((H, cfg.intermediate_size // tp),))) and (
             self.moe or m64_plan(1, 2 * (cfg.intermediate_size // tp), H, MODE_SILU) is not None)
 
+    def _w8_or_m64(self, x: torch.Tensor, name: str, mode: int):
+        """One projection of the fp8 decode chain: the E4M3 copy when the layer has
+        one, else the bf16 weight on gemm_m64g (same PendingSum / SiLU outputs)."""
+        q = self.w8.get(name)
+        if q is not None:
+            return w8_linear(x, q[0], q[1], mode)
+        return m64_linear(x, getattr(self, name), mode)
+
     def _ar(self, x: torch.Tensor) -> torch.Tensor:
         # keyed on the layer's own TP degree: a TP=1 draft model may live in a TP>1 process
         return x if self.tp == 1 else comm.tp_all_reduce(x)
@@ -196,15 +205,14 @@ class LlamaLayer(nn.Module):
         if self.w8 is not None and T <= W8_MAX_M:
             # FP8 weights (gemm_w8): half the weight bytes of the bf16 decode chain; the
             # split-K partials go to the same consumers (rope_cache / add+rmsnorm)
-            q = self.w8
-            pqkv = w8_linear(h, *q["qkv"], MODE_PARTIAL)
+            pqkv = self._w8_or_m64(h, "qkv", MODE_PARTIAL)
             a = self.attn.from_partials(pqkv, meta, kv, cos_sin)
-            o = w8_linear(a, *q["o"], MODE_PARTIAL)
+            o = self._w8_or_m64(a, "o", MODE_PARTIAL)
             if self.tp > 1:
                 o = self._ar(o.materialize())
             h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
-            act = w8_linear(h, *q["gate_up"], MODE_SILU)
-            d = w8_linear(act, *q["down"], MODE_PARTIAL)
+            act = self._w8_or_m64(h, "gate_up", MODE_SILU)
+            d = self._w8_or_m64(act, "down", MODE_PARTIAL)
             return (d if self.tp == 1 else self._ar(d.materialize())), residual
         if self.fast_ok and T <= FAST_M_SMALL and not self.m64_small_ok:
             # M <= 16: every projection on the streaming skinny kernel (1.7x hipBLASLt
@@ -356,8 +364,14 @@ class LlamaForCausalLM(nn.Module):
             w = getattr(l0, n)
             if w8_plan(1, w.shape[0], w.shape[1], MODE_SILU if n == "gate_up" else MODE_PARTIAL) is None:
                 return False
+        def use_fp8(n):  # small projections stay bf16 where gemm_m64g has a plan
+            w = getattr(l0, n)
+            mode = MODE_SILU if n == "gate_up" else MODE_PARTIAL
+            return w.numel() >= W8_MIN_ELEMS or not (l0.m64_small_ok and
+                                                     m64_plan(1, w.shape[0], w.shape[1], mode) is not None)
+        chosen = [n for n in names if use_fp8(n)]
         for l in self.layers:
-            l.w8 = {n: quantize_fp8(getattr(l, n)) for n in names}
+            l.w8 = {n: quantize_fp8(getattr(l, n)) for n in chosen}
         self._fused_ok = self._fused_small_ok = False
         self.weight_dtype = "fp8"
         return True

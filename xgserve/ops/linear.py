@@ -305,7 +305,19 @@ def deinterleave_gate_up(w: torch.Tensor):
 W8_MAX_M = 16
 # cfg -> (columns per workgroup, k chunk)
 W8_CFGS = {0: (128, 128), 1: (64, 128), 2: (64, 128), 3: (64, 256), 4: (128, 256)}
-_W8_TUNED = {}  # (N, K, mode) -> (split_k, cfg), filled from bench/gemm_bench.py --w8-sweep
+# (N, K, mode) -> (split_k, cfg), measured at M = 1 / 16 with cold weights
+# (bench/gemm_bench.py --w8-sweep, profiles/r1_w8_sweep.jsonl)
+_W8_TUNED = {
+    (6144, 4096, MODE_PARTIAL): (4, 4), (4096, 4096, MODE_PARTIAL): (4, 4),
+    (28672, 4096, MODE_SILU): (1, 3), (4096, 14336, MODE_PARTIAL): (8, 2),
+    (10240, 8192, MODE_PARTIAL): (4, 2), (8192, 8192, MODE_PARTIAL): (4, 2),
+    (57344, 8192, MODE_SILU): (1, 3), (8192, 28672, MODE_PARTIAL): (4, 2),
+}
+# Projections below this many weight elements keep bf16 (gemm_m64g) in the fp8
+# decode chain. 0: in isolation the 8B QKV / O are latency-bound either way (fp8
+# 9.4 / 9.0 us vs bf16 9.5 / 7.3 us), but end to end all-fp8 measured faster
+# (8B batch 1: 387 vs 375 tok/s with QKV / O on bf16).
+W8_MIN_ELEMS = 0
 
 
 def quantize_fp8(w: torch.Tensor):
