@@ -31,13 +31,13 @@
 
 namespace xgk {
 
-template <int D, int G>
+template <int D, int G, int NWAVES = 4>
 struct DecodeCfg {
   static constexpr int KK = D / 32;        // 16x16x32 k-steps over the head dim (S^T)
   static constexpr int MT = D / 16;        // 16-dim output tiles (O^T)
   static constexpr int NCH = D / 8;        // 16-B chunks per key row
   static constexpr int VLD = 16 * NCH / 64;  // 16-B V chunks per lane per tile
-  static constexpr int WAVES = 4;
+  static constexpr int WAVES = NWAVES;
 };
 
 __device__ __forceinline__ f32x4_t mfma16x16x16(bf16x4_t a, bf16x4_t b, f32x4_t c) {
@@ -143,13 +143,13 @@ __device__ __forceinline__ void decode_qkv_prologue(const QkvFuse& fq, int b, in
 //     from a 4 KiB wave-private LDS tile via ds_read_b64_tr_b16
 //   the next tile's K and V loads are issued before the current tile's math.
 // kc / vc are not __restrict__: the fused form writes the new row through fq.
-template <int D, int G, bool FQ>
-__global__ void __launch_bounds__(256) decode_attn_kernel(
+template <int D, int G, bool FQ, int NWAVES = 4>
+__global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ seq_lens,
     float* __restrict__ part_out, float* __restrict__ part_lse, uint16_t* __restrict__ out, int64_t out_stride,
     int Hq, int Hkv, int bs, float scale, int num_splits, int* __restrict__ counters, QkvFuse fq, int min_tps) {
-  using C = DecodeCfg<D, G>;
+  using C = DecodeCfg<D, G, NWAVES>;
   const int kvh = blockIdx.x, b = blockIdx.y, split = blockIdx.z;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -396,6 +396,15 @@ __global__ void __launch_bounds__(D) decode_combine_kernel(const float* __restri
       f2bf(den > 0.f ? acc / den : 0.f);
 }
 
+// XGS_DECODE_ATTN_WAVES: 4 (default) or 8 waves per workgroup for the fused form (A/B).
+static int decode_attn_waves() {
+  static const int v = [] {
+    const char* e = std::getenv("XGS_DECODE_ATTN_WAVES");
+    return (e && std::atoi(e) == 8) ? 8 : 4;
+  }();
+  return v;
+}
+
 // XGS_DECODE_MIN_SPLIT_TILES: minimum 16-key tiles per split (default 1 = even split).
 static int decode_min_split_tiles() {
   static const int v = [] {
@@ -410,6 +419,10 @@ static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, con
                           const int32_t* bt, int bts, const int32_t* sl, float* po, float* pl, uint16_t* out,
                           int64_t os, int B, int Hq, int Hkv, int bs, float scale, int S, int* counters,
                           const QkvFuse& fq, hipStream_t st) {
+  if (FQ && decode_attn_waves() == 8)
+    hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, 8>), dim3(Hkv, B, S), dim3(512), 0, st, q, qs, kc, vc, bt, bts,
+                       sl, po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq, S > 1 ? decode_min_split_tiles() : 1);
+  else
   hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt, bts, sl,
                      po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq, S > 1 ? decode_min_split_tiles() : 1);
   if (S > 1 && counters == nullptr)
