@@ -132,7 +132,7 @@ def w8_sweep(a):
             rows = []
             for cfg, (cols, kc) in L.W8_CFGS.items():
                 for S in ((1,) if mode == L.MODE_SILU else (1, 2, 4, 8, 16)):
-                    if N % cols or K % (S * kc) or (mode == L.MODE_SILU and cfg == 2):
+                    if N % cols or K % (S * kc) or (mode == L.MODE_SILU and cfg == 2) or (M > 16 and cfg >= 3):
                         continue
 
                     def fn(q, S=S, cfg=cfg):

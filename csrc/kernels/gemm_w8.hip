@@ -1,5 +1,5 @@
 // Decode GEMM with FP8 weights (OCP E4M3, one fp32 scale per output channel) and
-// bf16 activations: out = x . (diag(s) W8)^T for M <= 16 (batch <= 16 decode).
+// bf16 activations: out = x . (diag(s) W8)^T for M <= 64 (decode batches).
 //
 // Weight-only FP8 halves the bytes of a bandwidth-bound decode step. The weights
 // stream through the same LDS-DMA pipeline as gemm_m64g (3 slots, 2 chunks in
@@ -10,7 +10,8 @@
 // fp32 accumulators in the epilogue. Activations stay bf16 (no activation
 // quantisation): the accuracy is that of the rounded weights alone.
 //
-//   weights [N, K] uint8 (E4M3), scale [N] fp32; x [M, K] bf16 (M <= 16).
+//   weights [N, K] uint8 (E4M3), scale [N] fp32; x [M, K] bf16 (M <= 64; MT = 1
+//   x tile of 16 rows for M <= 16, MT = 4 tiles for 16 < M <= 64, KC 128 only).
 //   LDS: x rows 2*KC bytes, weight rows KC bytes, 16-B granules XOR-swizzled by
 //   row on the GLOBAL source address (DMA writes are lane-linear).
 //   modes: W8_PARTIAL -> fp32 split-K partials [S, M, N] (reduced by the consumer
@@ -39,7 +40,7 @@ __device__ __forceinline__ bf16x8_t fp8x8_to_bf16(uint2 v) {
 //   NW  16-column MFMA tiles per wave (SiLU needs 2: one gate + one up tile)
 //   WV  waves per workgroup
 //   KC  k per chunk (fp8 row = KC bytes, bf16 x row = 2 KC bytes)
-template <int NW, int WV, int KC>
+template <int NW, int WV, int KC, int MT>
 __global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __restrict__ x, int M, int K,
                                                              const uint8_t* __restrict__ w,
                                                              const float* __restrict__ wscale, int N,
@@ -48,14 +49,15 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __r
   constexpr int XRB = KC * 2, WRB = KC;          // bytes per LDS row
   constexpr int XG = XRB / 16, WG = WRB / 16;    // 16-B granules per row
   constexpr int XRPI = 1024 / XRB, WRPI = 1024 / WRB;  // rows per DMA instruction
-  constexpr int XBYTES = 16 * XRB;
-  constexpr int XI = 16 / XRPI / WV;             // x DMA instructions per wave per chunk
+  constexpr int XROWS = 16 * MT;
+  constexpr int XBYTES = XROWS * XRB;
+  constexpr int XI = XROWS / XRPI / WV;          // x DMA instructions per wave per chunk
   constexpr int WROWS = 16 * NW;
   constexpr int WI = WROWS / WRPI;               // weight DMA instructions per wave per chunk
   constexpr int WBYTES = WROWS * WRB;
   constexpr int SLOT = XBYTES + WV * WBYTES;
   constexpr int G = XI + WI;
-  static_assert(XI >= 1 && WI >= 1 && 16 % (XRPI * WV) == 0 && WROWS % WRPI == 0, "bad w8 geometry");
+  static_assert(XI >= 1 && WI >= 1 && XROWS % (XRPI * WV) == 0 && WROWS % WRPI == 0, "bad w8 geometry");
   __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
@@ -82,7 +84,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __r
     const int dr = lane / XG, dj = lane % XG;
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-      const int r = XRPI * (wid * XI + i) + dr;  // x row 0..15
+      const int r = XRPI * (wid * XI + i) + dr;  // x row 0..XROWS-1
       xsrc[i] = x + static_cast<int64_t>(min(r, M - 1)) * K + k0 + 8 * (dj ^ (r & (XG - 1)));
     }
   }
@@ -95,17 +97,24 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __r
     for (int i = 0; i < WI; ++i) glds16_nt(wsrc[i] + kk, slot + XBYTES + wid * WBYTES + i * 1024);
   };
 
-  f32x4_t acc[NW];
+  f32x4_t acc[NW][MT];
 #pragma unroll
-  for (int nt = 0; nt < NW; ++nt) acc[nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int nt = 0; nt < NW; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](const uint8_t* slot) {
     const uint8_t* xs = slot;
     const uint8_t* ws = slot + XBYTES + wid * WBYTES;
 #pragma unroll
     for (int t = 0; t < KC / 32; ++t) {
-      // x (B operand): row li, k = 32t + 8g.. -> bf16 granule 4t + g
-      const uint4 b = *reinterpret_cast<const uint4*>(xs + li * XRB + (((4 * t + g) ^ (li & (XG - 1))) * 16));
+      // x (B operand): row 16 mt + li, k = 32t + 8g.. -> bf16 granule 4t + g
+      uint4 b[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int xr = 16 * mt + li;
+        b[mt] = *reinterpret_cast<const uint4*>(xs + xr * XRB + (((4 * t + g) ^ (xr & (XG - 1))) * 16));
+      }
 #pragma unroll
       for (int nt = 0; nt < NW; ++nt) {
         // W (A operand): row 16 nt + li, k = 32t + 8g.. -> fp8 granule 2t + g/2, byte (g & 1) * 8
@@ -113,7 +122,9 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __r
         const uint2 a8 = *reinterpret_cast<const uint2*>(ws + row * WRB +
                                                          (((2 * t + (g >> 1)) ^ (row & (WG - 1))) * 16) +
                                                          (g & 1) * 8);
-        acc[nt] = mfma16x16x32(fp8x8_to_bf16(a8), as_frag(b), acc[nt]);
+        const bf16x8_t a = fp8x8_to_bf16(a8);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = mfma16x16x32(a, as_frag(b[mt]), acc[nt][mt]);
       }
     }
   };
@@ -137,35 +148,41 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __r
   if (c < nchunks) step(lds0, lds2, c);
   if (c + 1 < nchunks) step(lds1, lds0, c + 1);
 
-  // acc[nt][r] = out[m = li][n = nbase + 16 nt + 4 g + r] / scale[n]
+  // acc[nt][mt][r] = out[m = 16 mt + li][n = nbase + 16 nt + 4 g + r] / scale[n]
 #pragma unroll
   for (int nt = 0; nt < NW; ++nt) {
     const float4 sc = *reinterpret_cast<const float4*>(wscale + nbase + 16 * nt + 4 * g);
-    acc[nt][0] *= sc.x;
-    acc[nt][1] *= sc.y;
-    acc[nt][2] *= sc.z;
-    acc[nt][3] *= sc.w;
-  }
-  const int m = li;
-  if (m >= M) return;
-  if (mode == W8_PARTIAL) {
-    float* pp = part + static_cast<int64_t>(s) * M * N + static_cast<int64_t>(m) * N;
 #pragma unroll
-    for (int nt = 0; nt < NW; ++nt)
-      *reinterpret_cast<float4*>(pp + nbase + 16 * nt + 4 * g) =
-          make_float4(acc[nt][0], acc[nt][1], acc[nt][2], acc[nt][3]);
-  } else if (NW == 2) {
-    const int F = N / 2, f0 = nbase / 2 + 4 * g;
-    float o[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float gt = acc[0][r];
-      o[r] = gt / (1.f + __expf(-gt)) * acc[NW - 1][r];
+    for (int mt = 0; mt < MT; ++mt) {
+      acc[nt][mt][0] *= sc.x;
+      acc[nt][mt][1] *= sc.y;
+      acc[nt][mt][2] *= sc.z;
+      acc[nt][mt][3] *= sc.w;
     }
-    uint2 v;
-    v.x = pack2(o[0], o[1]);
-    v.y = pack2(o[2], o[3]);
-    *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * F + f0) = v;
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = 16 * mt + li;
+    if (m >= M) continue;
+    if (mode == W8_PARTIAL) {
+      float* pp = part + static_cast<int64_t>(s) * M * N + static_cast<int64_t>(m) * N;
+#pragma unroll
+      for (int nt = 0; nt < NW; ++nt)
+        *reinterpret_cast<float4*>(pp + nbase + 16 * nt + 4 * g) =
+            make_float4(acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]);
+    } else if (NW == 2) {
+      const int F = N / 2, f0 = nbase / 2 + 4 * g;
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float gt = acc[0][mt][r];
+        o[r] = gt / (1.f + __expf(-gt)) * acc[NW - 1][mt][r];
+      }
+      uint2 v;
+      v.x = pack2(o[0], o[1]);
+      v.y = pack2(o[2], o[3]);
+      *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * F + f0) = v;
+    }
   }
 }
 
@@ -185,21 +202,24 @@ static int w8_cfg_nw(int cfg) { return cfg == 2 ? 1 : 2; }
 
 int gemm_w8(const uint16_t* x, int M, int K, const uint8_t* w, const float* scale, int N, float* part,
             uint16_t* out, int S, int mode, int cfg, hipStream_t st) {
-  if (M < 1 || M > 16 || S < 1 || cfg < 0 || cfg > 4) return 1;
+  if (M < 1 || M > 64 || S < 1 || cfg < 0 || cfg > 4) return 1;
+  if (M > 16 && cfg >= 3) return 1;  // KC 256 with four x tiles exceeds the LDS
   if (mode != W8_PARTIAL && mode != W8_SILU) return 1;
   const int cols = w8_cfg_cols(cfg), kc = w8_cfg_kc(cfg);
   if (N % cols || K % (S * kc)) return 1;
   if (mode == W8_SILU && (w8_cfg_nw(cfg) != 2 || S != 1 || out == nullptr)) return 1;
   if (mode == W8_PARTIAL && part == nullptr) return 1;
   const dim3 grid(N / cols, S);
-#define XGK_W8(NW, WV, KC) \
-  hipLaunchKernelGGL((gemm_w8_kernel<NW, WV, KC>), grid, dim3(64 * WV), 0, st, x, M, K, w, scale, N, part, out, mode)
+#define XGK_W8(NW, WV, KC, MT)                                                                               \
+  hipLaunchKernelGGL((gemm_w8_kernel<NW, WV, KC, MT>), grid, dim3(64 * WV), 0, st, x, M, K, w, scale, N, part, out, \
+                     mode)
+  const bool mt1 = M <= 16;
   switch (cfg) {
-    case 0: XGK_W8(2, 4, 128); break;
-    case 1: XGK_W8(2, 2, 128); break;
-    case 2: XGK_W8(1, 4, 128); break;
-    case 3: XGK_W8(2, 2, 256); break;
-    default: XGK_W8(2, 4, 256); break;
+    case 0: if (mt1) XGK_W8(2, 4, 128, 1); else XGK_W8(2, 4, 128, 4); break;
+    case 1: if (mt1) XGK_W8(2, 2, 128, 1); else XGK_W8(2, 2, 128, 4); break;
+    case 2: if (mt1) XGK_W8(1, 4, 128, 1); else XGK_W8(1, 4, 128, 4); break;
+    case 3: XGK_W8(2, 2, 256, 1); break;
+    default: XGK_W8(2, 4, 256, 1); break;
   }
 #undef XGK_W8
   return 0;

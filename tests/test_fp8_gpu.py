@@ -34,13 +34,13 @@ def test_quantize_roundtrip_cpu_semantics():
     assert float(d.abs().amax(1).sub(w.abs().amax(1)).abs().max()) < 1e-6  # row max maps to 448 exactly
 
 
-@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("M", [1, 5, 16, 17, 40, 64])
 @pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 4096), (4096, 14336), (1024, 512)])
 @pytest.mark.parametrize("cfg", sorted(W8_CFGS))
 @pytest.mark.parametrize("S", [1, 2, 4])
 def test_w8_partial(M, N, K, cfg, S):
     cols, kc = W8_CFGS[cfg]
-    if N % cols or K % (S * kc):
+    if N % cols or K % (S * kc) or (M > 16 and cfg >= 3):
         pytest.skip("shape not divisible for this configuration")
     x = torch.randn(M, K, device=DEV).bfloat16()
     q, s = quantize_fp8(torch.randn(N, K, device=DEV) * 0.02)
@@ -50,9 +50,11 @@ def test_w8_partial(M, N, K, cfg, S):
     assert rel_err(pend.part.sum(0), ref) < 2e-3
 
 
-@pytest.mark.parametrize("M", [1, 7, 16])
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
 @pytest.mark.parametrize("cfg", [0, 1, 3, 4])
 def test_w8_silu(M, cfg):
+    if M > 16 and cfg >= 3:
+        pytest.skip("KC 256 is M <= 16 only")
     Fh, K = 2048, 4096
     x = torch.randn(M, K, device=DEV).bfloat16()
     g = torch.randn(Fh, K, device=DEV) * 0.02
@@ -83,6 +85,7 @@ def test_fp8_engine_decode_matches_reference():
                                  max_num_batched_tokens=2048, max_model_len=1024, graph_batch_sizes=[1, 2, 4, 8]),
                     model=m)
     prompts = [[128000] + list(range(200 + 7 * i, 260 + 11 * i)) for i in range(3)]
+    prompts += [[128000] + list(range(900 + 3 * i, 930 + 3 * i)) for i in range(17)]  # 20 rows: the MT=4 kernel
     outs = eng.generate(prompts, SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True))
     for p, gen in zip(prompts, outs):
         assert len(gen) == 8

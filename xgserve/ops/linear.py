@@ -302,7 +302,7 @@ def deinterleave_gate_up(w: torch.Tensor):
 # ---------------------------------------------------------------------------- FP8 weights
 # Weight-only FP8 (OCP E4M3 + one fp32 scale per output channel) for batch <= 16
 # decode: csrc/kernels/gemm_w8.hip streams half the bytes of the bf16 kernels.
-W8_MAX_M = 16
+W8_MAX_M = 64
 # cfg -> (columns per workgroup, k chunk)
 W8_CFGS = {0: (128, 128), 1: (64, 128), 2: (64, 128), 3: (64, 256), 4: (128, 256)}
 # (N, K, mode) -> (split_k, cfg), measured at M = 1 / 16 with cold weights
@@ -312,6 +312,14 @@ _W8_TUNED = {
     (28672, 4096, MODE_SILU): (1, 3), (4096, 14336, MODE_PARTIAL): (8, 2),
     (10240, 8192, MODE_PARTIAL): (4, 2), (8192, 8192, MODE_PARTIAL): (4, 2),
     (57344, 8192, MODE_SILU): (1, 3), (8192, 28672, MODE_PARTIAL): (4, 2),
+}
+# 16 < M <= 64 (four 16-row x tiles, KC 128 configurations 0-2 only), measured at M = 64
+# (profiles/r1_w8_sweep_m64.jsonl)
+_W8_TUNED64 = {
+    (6144, 4096, MODE_PARTIAL): (4, 1), (4096, 4096, MODE_PARTIAL): (4, 2),
+    (28672, 4096, MODE_SILU): (1, 0), (4096, 14336, MODE_PARTIAL): (8, 0),
+    (10240, 8192, MODE_PARTIAL): (8, 0), (8192, 8192, MODE_PARTIAL): (4, 0),
+    (57344, 8192, MODE_SILU): (1, 0), (8192, 28672, MODE_PARTIAL): (4, 0),
 }
 # Projections below this many weight elements keep bf16 (gemm_m64g) in the fp8
 # decode chain. 0: in isolation the 8B QKV / O are latency-bound either way (fp8
@@ -338,7 +346,7 @@ def w8_plan(M: int, N: int, K: int, mode: int):
     tiles per wave; otherwise the smallest split-K giving >= 256 workgroups."""
     if not (1 <= M <= W8_MAX_M):
         return None
-    t = _W8_TUNED.get((N, K, mode))
+    t = (_W8_TUNED if M <= 16 else _W8_TUNED64).get((N, K, mode))
     if t is not None:
         return t
     cfg = 1

@@ -83,7 +83,7 @@ class WorkerSection:
     tp: int = 1                       # tensor-parallel degree per replica
     gpus: Optional[str] = None        # e.g. "0,1,2,3"; default 0..replicas*tp-1
     device: Optional[str] = None      # "cpu" forces the CPU path
-    quantization: str = "bf16"        # bf16 | fp16 | fp32 | fp8 (fp8 = E4M3 weights for batch <= 16 decode, bf16 activations)
+    quantization: str = "bf16"        # bf16 | fp16 | fp32 | fp8 (fp8 = E4M3 weights for decode batches <= 64, bf16 activations)
     block_size: int = 16
     max_num_seqs: int = 256
     max_num_batched_tokens: int = 8192
