@@ -70,7 +70,7 @@ class ModelRunner:
         self.kv_caches = [(self.kv[i, 0], self.kv[i, 1]) for i in range(cfg.num_layers)]
         self.is_cuda = self.device.type == "cuda"
         Hq_local = cfg.num_heads // model.tp
-        self.max_splits = 16
+        self.max_splits = int(os.environ.get("XGS_DECODE_MAX_SPLITS", "16"))
         self.workspace = DecodeWorkspace(max(max_num_seqs, 1), Hq_local, cfg.head_dim, self.max_splits,
                                          self.device) if self.is_cuda else None
         # pinned staging for eager steps
