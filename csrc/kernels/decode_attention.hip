@@ -143,6 +143,55 @@ __device__ __forceinline__ void decode_qkv_prologue(const QkvFuse& fq, int b, in
 //     from a 4 KiB wave-private LDS tile via ds_read_b64_tr_b16
 //   the next tile's K and V loads are issued before the current tile's math.
 // kc / vc are not __restrict__: the fused form writes the new row through fq.
+// Write-through (sc1) 4-B store: visible chip-wide once the storing wave's vmcnt
+// drains (the in-launch combine's hand-off needs no release fence). Not counted by
+// hipcc: the explicit vmcnt(0) before the ticket covers it.
+__device__ __forceinline__ void st4_sc1(float* p, float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("global_store_dword %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+#else
+  *p = v;
+#endif
+}
+
+// softmax(lse)-weighted sum over splits of one output element: po[s * D], lse[s].
+// All lse / partial loads of a 16-split batch are issued before any arithmetic
+// (unconditional clamped loads, masked after): a batch-1 decode has few heads, so
+// the reduce is pure latency and a dependent per-split loop costs ~7 us.
+template <int D>
+__device__ __forceinline__ float combine_splits(const float* __restrict__ lse, const float* __restrict__ po,
+                                                int num_splits) {
+  constexpr int SB = 16;
+  float M = -INFINITY, den = 0.f, acc = 0.f;
+  for (int s0 = 0; s0 < num_splits; s0 += SB) {
+    float l[SB], v[SB];
+#pragma unroll
+    for (int i = 0; i < SB; ++i) {
+      const int sc = min(s0 + i, num_splits - 1);
+      l[i] = lse[sc];
+      v[i] = po[static_cast<int64_t>(sc) * D];
+    }
+#pragma unroll
+    for (int i = 0; i < SB; ++i)
+      if (s0 + i >= num_splits) l[i] = -INFINITY;
+    float m2 = M;
+#pragma unroll
+    for (int i = 0; i < SB; ++i) m2 = fmaxf(m2, l[i]);
+    if (m2 == -INFINITY) continue;
+    const float r = __expf(M - m2);  // rescale the running sums (M == -inf -> 0)
+    den *= r;
+    acc *= r;
+#pragma unroll
+    for (int i = 0; i < SB; ++i) {
+      const float wgt = __expf(l[i] - m2);
+      den += wgt;
+      acc += wgt * v[i];
+    }
+    M = m2;
+  }
+  return den > 0.f ? acc / den : 0.f;
+}
+
 template <int D, int G, bool FQ, int NWAVES = 4>
 __global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
@@ -308,27 +357,33 @@ __global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
       out[static_cast<int64_t>(b) * out_stride + static_cast<int64_t>(qhead) * D + d] = f2bf(res);
     } else {
       const int64_t pi = (static_cast<int64_t>(b) * Hq + qhead) * num_splits + split;
-      part_out[pi * D + d] = res;
-      if (d == 0) part_lse[pi] = Ls > 0.f ? M + __logf(Ls) : -INFINITY;
+      const float lse_v = Ls > 0.f ? M + __logf(Ls) : -INFINITY;
+      if (counters != nullptr) {  // in-launch combine: write-through, published by the drain + ticket below
+        st4_sc1(part_out + pi * D + d, res);
+        if (d == 0) st4_sc1(part_lse + pi, lse_v);
+      } else {
+        part_out[pi * D + d] = res;
+        if (d == 0) part_lse[pi] = lse_v;
+      }
     }
   }
   if (num_splits == 1 || counters == nullptr) return;
   // In-launch split-K combine: the last split of (b, kv head) to arrive merges all
-  // splits' (O, lse) for its G query heads (cdna_hip_programming.md §5 "In-launch
-  // split-K reduction": agent-scope release before the ticket, acquire after it).
+  // splits' (O, lse) for its G query heads. Slabs were stored sc1 (write-through), so
+  // the hand-off is drain -> relaxed agent ticket, no release fence; the winner takes
+  // an agent acquire and reads with plain, batched loads (cdna_hip_programming.md §5
+  // "In-launch split-K reduction", sc1-store form; §5 trap (c): no load per branch).
   __shared__ int am_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int* cnt = counters + b * Hkv + kvh;
     const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     am_last = prev == num_splits - 1;
     if (am_last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      *cnt = 0;  // re-armed for the next launch (graph replays included)
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed (graph replays)
     }
   }
   __syncthreads();
@@ -336,64 +391,22 @@ __global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
   for (int idx = threadIdx.x; idx < G * D; idx += blockDim.x) {
     const int qhead = kvh * G + idx / D, d = idx % D;
     const int64_t bh = static_cast<int64_t>(b) * Hq + qhead;
-    const float* lse = part_lse + bh * num_splits;
-    float M = -INFINITY;
-    for (int s2 = 0; s2 < num_splits; ++s2) M = fmaxf(M, lse[s2]);
-    float den = 0.f, acc = 0.f;
-    if (M != -INFINITY) {
-      for (int s2 = 0; s2 < num_splits; ++s2) {
-        const float wgt = __expf(lse[s2] - M);
-        den += wgt;
-        acc += wgt * part_out[(bh * num_splits + s2) * D + d];
-      }
-    }
-    out[static_cast<int64_t>(b) * out_stride + static_cast<int64_t>(qhead) * D + d] = f2bf(den > 0.f ? acc / den : 0.f);
+    out[static_cast<int64_t>(b) * out_stride + static_cast<int64_t>(qhead) * D + d] =
+        f2bf(combine_splits<D>(part_lse + bh * num_splits, part_out + bh * num_splits * D + d, num_splits));
   }
 }
 
-// Split-K reduction: out[b, h, :] = sum_s softmax(lse)_s * part_out[b, h, s, :]
-// All lse / partial loads are issued before any arithmetic (fixed 16-wide
-// register batches): a batch-1 decode has few heads, so this launch is pure
-// latency and the dependent per-split loop it replaces cost ~7 us.
+// Split-K reduction launch: out[b, h, :] = sum_s softmax(lse)_s * part_out[b, h, s, :]
 template <int D>
 __global__ void __launch_bounds__(D) decode_combine_kernel(const float* __restrict__ part_out,
                                                            const float* __restrict__ part_lse,
                                                            uint16_t* __restrict__ out, int64_t out_stride,
                                                            int Hq, int num_splits) {
-  constexpr int SB = 16;
   const int bh = blockIdx.x;
   const int b = bh / Hq, h = bh % Hq;
-  const float* lse = part_lse + static_cast<int64_t>(bh) * num_splits;
-  const float* po = part_out + static_cast<int64_t>(bh) * num_splits * D + threadIdx.x;
-  float M = -INFINITY, den = 0.f, acc = 0.f;
-  for (int s0 = 0; s0 < num_splits; s0 += SB) {
-    float l[SB], v[SB];
-#pragma unroll
-    for (int i = 0; i < SB; ++i) {  // unconditional (clamped) loads, masked after: no branch per load
-      const int sc = min(s0 + i, num_splits - 1);
-      l[i] = lse[sc];
-      v[i] = po[static_cast<int64_t>(sc) * D];
-    }
-#pragma unroll
-    for (int i = 0; i < SB; ++i)
-      if (s0 + i >= num_splits) l[i] = -INFINITY;
-    float m2 = M;
-#pragma unroll
-    for (int i = 0; i < SB; ++i) m2 = fmaxf(m2, l[i]);
-    if (m2 == -INFINITY) continue;
-    const float r = __expf(M - m2);  // rescale the running sums (M == -inf -> 0)
-    den *= r;
-    acc *= r;
-#pragma unroll
-    for (int i = 0; i < SB; ++i) {
-      const float wgt = __expf(l[i] - m2);
-      den += wgt;
-      acc += wgt * v[i];
-    }
-    M = m2;
-  }
   out[static_cast<int64_t>(b) * out_stride + static_cast<int64_t>(h) * D + threadIdx.x] =
-      f2bf(den > 0.f ? acc / den : 0.f);
+      f2bf(combine_splits<D>(part_lse + static_cast<int64_t>(bh) * num_splits,
+                             part_out + static_cast<int64_t>(bh) * num_splits * D + threadIdx.x, num_splits));
 }
 
 // XGS_DECODE_ATTN_WAVES: 4 (default) or 8 waves per workgroup for the fused form (A/B).
@@ -455,7 +468,7 @@ int decode_attention_fq(const float* part, int S_qkv, const int32_t* positions, 
                         const int32_t* slots, uint16_t* kc, uint16_t* vc, const int32_t* bt, int bt_stride,
                         const int32_t* seq_lens, float* part_out, float* part_lse, uint16_t* out,
                         int64_t out_stride, int B, int Hq, int Hkv, int D, int bs, float scale, int num_splits,
-                        int apply_rope, hipStream_t st) {
+                        int apply_rope, int* counters, hipStream_t st) {
   if (B <= 0) return 0;
   if (part == nullptr || S_qkv < 1 || bs % 16 != 0 || Hq % Hkv != 0 || D != 128 || num_splits < 1) return -1;
   if (num_splits > 1 && (part_out == nullptr || part_lse == nullptr)) return -1;
@@ -464,7 +477,7 @@ int decode_attention_fq(const float* part, int S_qkv, const int32_t* positions, 
 #define XGK_DECF(GG)                                                                                         \
   if (G == GG) {                                                                                             \
     launch_decode<128, GG, true>(nullptr, 0, kc, vc, bt, bt_stride, seq_lens, part_out, part_lse, out,       \
-                                 out_stride, B, Hq, Hkv, bs, scale, num_splits, nullptr, fq, st);            \
+                                 out_stride, B, Hq, Hkv, bs, scale, num_splits, counters, fq, st);           \
     return 0;                                                                                                \
   }
   XGK_DECF(1) XGK_DECF(2) XGK_DECF(4) XGK_DECF(8)

@@ -87,8 +87,10 @@ def _paged(lens, Hkv, D, bs, extra_pages=8):
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 8)])
 @pytest.mark.parametrize("S", [1, 4, 8])
-@pytest.mark.parametrize("splits", [1, 3])
-def test_decode_attention_fused_prologue(Hq, Hkv, S, splits):
+@pytest.mark.parametrize("splits,in_kernel", [(1, False), (3, False), (3, True), (16, True)])
+def test_decode_attention_fused_prologue(Hq, Hkv, S, splits, in_kernel, monkeypatch):
+    import xgserve.ops.attention as A
+    monkeypatch.setattr(A, "IN_KERNEL_COMBINE", in_kernel)
     D, bs = 128, 16
     lens = [1, 17, 300, 64, 0, 129]  # row 4: a graph padding row (no KV write, no attention)
     kc, vc, bt = _paged([max(1, L) for L in lens], Hkv, D, bs)
@@ -101,7 +103,12 @@ def test_decode_attention_fused_prologue(Hq, Hkv, S, splits):
     cs = ops.build_cos_sin(D, 4096, 500000.0, device=DEV)
     scale = 1.0 / math.sqrt(D)
     kc1, vc1, kc2, vc2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
-    out = ops.decode_attention_fused(PendingSum(part, S), pos, slots, cs, kc1, vc1, bt, sl, Hq, scale, splits)
+    ws = A.DecodeWorkspace(B, Hq, D, splits, DEV)
+    for _ in range(2 if in_kernel else 1):  # the second launch needs the tickets re-armed by the first
+        out = ops.decode_attention_fused(PendingSum(part, S), pos, slots, cs, kc1, vc1, bt, sl, Hq, scale, splits,
+                                         workspace=ws)
+    if in_kernel:
+        assert int(ws.counters.abs().sum().item()) == 0
     # reference: the unfused chain (rope_cache_partials -> fp32 attention reference)
     q = torch.empty(B, Hq * D, dtype=torch.bfloat16, device=DEV)
     ops.rope_cache_partials(PendingSum(part, S), q, pos, cs, kc2, vc2, slots, Hq, Hkv, D)

@@ -2,16 +2,20 @@
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
 
 from ._native import kernels, stream_ptr, use_native
 
-# split-K decode: the last-arriving split merges in-launch instead of a combine launch.
-# Measured slower on MI355X (8B batch 1: 4.14 vs 3.89 ms/step; c64 -2.5%): the serial merge
-# on the tail workgroup costs more than the ~4 us launch boundary it saves. Kept switchable.
-IN_KERNEL_COMBINE = False
+# split-K decode: the last-arriving split merges in-launch instead of a combine launch
+# (XGS_DECODE_INLAUNCH_COMBINE=1). A first form with a dependent per-split merge loop
+# measured slower on MI355X (8B batch 1: 4.14 vs 3.89 ms/step); the current one stores
+# the slabs write-through and merges with batched loads (combine_splits): correct, and
+# still 0.4-1.6 % slower than the graph-captured combine launch at batch 1 / 8 / 64
+# (profiles/r1_inlaunch_combine_ab.md), so the separate launch stays the default.
+IN_KERNEL_COMBINE = os.environ.get("XGS_DECODE_INLAUNCH_COMBINE", "0") == "1"
 
 
 def choose_num_splits(batch: int, num_kv_heads: int, max_seq_len: int, num_cus: int = 256) -> int:
@@ -137,16 +141,17 @@ def decode_attention_fused(pend, positions: torch.Tensor, slot_mapping: torch.Te
     assert positions.dtype == torch.int32 and slot_mapping.dtype == torch.int32 and cos_sin.dtype == torch.float32
     if out is None:
         out = torch.empty(B, Hq * D, dtype=torch.bfloat16, device=pend.part.device)
-    po = pl = 0
+    po = pl = cnt = 0
     if num_splits > 1:
         if workspace is None or workspace.max_splits < num_splits or workspace.part_lse.numel() < B * Hq * num_splits:
             workspace = DecodeWorkspace(B, Hq, D, num_splits, pend.part.device)
         po, pl = workspace.part_out.data_ptr(), workspace.part_lse.data_ptr()
+        cnt = workspace.counters.data_ptr() if IN_KERNEL_COMBINE else 0
     kernels().decode_attention_fq(pend.part.data_ptr(), S, positions.data_ptr(), cos_sin.data_ptr(),
                                   slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                   block_tables.data_ptr(), block_tables.stride(0), seq_lens.data_ptr(), po, pl,
                                   out.data_ptr(), out.stride(0), B, Hq, Hkv, D, bs, float(scale), int(num_splits),
-                                  1 if apply_rope else 0, stream_ptr())
+                                  1 if apply_rope else 0, cnt, stream_ptr())
     return out
 
 
