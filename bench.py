@@ -61,12 +61,20 @@ def main():
     st = init_distributed(tp_size=a.tp)
     rank = st.rank
     dp = world // a.tp
-    dev = torch.device("cuda", torch.cuda.current_device())
+    on_gpu = torch.cuda.is_available()
+    # CPU (gloo) runs exist only to test this script's multi-rank plumbing (tests/test_bench_cli.py)
+    dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
     max_len = a.prompt_len + 2 * a.output_len + 16
     ecfg = EngineConfig(model=a.model, device=str(dev), tp=a.tp, max_num_seqs=max(64, a.concurrency),
                         max_num_batched_tokens=a.max_batched_tokens, max_model_len=max_len,
-                        use_graphs=not a.no_graphs, enable_prefix_cache=not a.no_prefix_cache, moe_comm=a.moe_comm,
-                        weight_dtype=a.weight_dtype,
+                        use_graphs=on_gpu and not a.no_graphs, enable_prefix_cache=not a.no_prefix_cache,
+                        moe_comm=a.moe_comm,
+                        weight_dtype=a.weight_dtype, dtype=None if on_gpu else "float32",
                         graph_batch_sizes=[b for b in [1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128]
                                            if b <= max(64, a.concurrency)], seed=st.dp_rank)
     eng = LLMEngine(ecfg)
@@ -116,10 +124,10 @@ def main():
 
     for _ in range(a.warmup):
         run_step()
-    torch.cuda.synchronize()
+    sync()
     if lgroup is not None:
         dist.barrier(group=lgroup)
-    torch.cuda.synchronize()
+    sync()
     if os.environ.get("XGS_STEP_TIMING"):
         eng.enable_step_timing()
     t_start_wall = time.perf_counter()
@@ -127,11 +135,11 @@ def main():
     first_before = set(first_tok)
     for _ in range(a.steps):
         tokens += run_step()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t_start_wall
     if lgroup is not None:
         dist.barrier(group=lgroup)
-    torch.cuda.synchronize()
+    sync()
     ttfts = [first_tok[r] - arrival[r] for r in first_tok if r not in first_before]
     p50_local = float(np.median(ttfts)) if ttfts else float("nan")
 
@@ -158,7 +166,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if a.weight_dtype is None else "bf16 activations, fp8 (E4M3) decode weights",
+            "dtype": ("bf16" if on_gpu else "fp32") if a.weight_dtype is None else "bf16 activations, fp8 (E4M3) decode weights",
             "data": "synthetic (random-token prompts, random-init weights)",
             "ttft_p50_ms": round(1000 * p50, 2) if p50 == p50 else None,
             "config": {"model": a.model, "global_batch": a.concurrency * dp,

@@ -1,0 +1,51 @@
+"""bench.py's driver contract (one JSON line from rank 0, whole-job aggregate,
+max-over-ranks time) exercised on CPU with gloo ranks: DP=2, TP=2 (leader +
+follower) and DP=2 x TP=2 with a MoE model. The GPU path is the same script with
+RCCL; only the device and the graph capture differ."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(nproc, *args):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+           "--gpus", str(nproc), "--steps", "4", "--warmup", "2", "--concurrency", "2", "--prompt-len", "16",
+           "--output-len", "4", *args]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]  # rank 0 only
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("nproc,tp,model,par", [(2, 1, "llama-tiny", "dp2"), (2, 2, "llama-tiny", "tp2"),
+                                                (4, 2, "mixtral-tiny", "dp2xtp2")])
+def test_bench_multi_rank_json_contract(nproc, tp, model, par):
+    r = _run(nproc, "--tp", str(tp), "--model", model)
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert key in r
+    assert r["n_gpus"] == nproc and r["steps"] == 4 and r["warmup"] == 2
+    assert r["higher_is_better"] is True and r["scaling"] == "weak"
+    cfg = r["config"]
+    assert cfg["model"] == model and cfg["parallelism"] == par
+    assert cfg["global_batch"] == 2 * (nproc // tp)  # concurrency per replica x replicas
+    # whole-job tokens / slowest rank's time. A step emits at most one token per running
+    # sequence plus the immediate first token of a sequence admitted in it (outputs of
+    # step N are delivered while step N+1 runs): <= 2 x concurrency per replica.
+    assert 0 < r["value"] <= 2 * cfg["global_batch"] * 1000.0 / r["ms_per_step"] + 1e-6
