@@ -63,7 +63,35 @@ struct QkvFuse {
   uint16_t* k_cache;            // the kernel's kc / vc, writable
   uint16_t* v_cache;
   int apply_rope;
+  // Next-GEMM weight prefetch: grid slices z >= num_splits read pf_bytes of the O
+  // projection's weights while the attention slices (latency-bound at small batch,
+  // HBM mostly idle) run, so the O GEMM that follows streams them from the
+  // Infinity Cache instead of HBM. pf_slices = 0: none.
+  const uint8_t* pf;
+  int64_t pf_bytes;
+  int pf_slices;
 };
+
+// One prefetch workgroup: reads its contiguous share of [pf, pf + pf_bytes) in
+// 16-B lanes, four loads in flight per lane (tail clamped, no branch per load),
+// and folds them into a value stored only under a condition the host never sets
+// (pf_slices < 0), so the loads are kept. Plain loads: hipcc counts their waits.
+__device__ __forceinline__ void prefetch_share(const QkvFuse& fq, int wg, int nwg) {
+  const int64_t n16 = fq.pf_bytes >> 4;
+  const int64_t per = (n16 + nwg - 1) / nwg;
+  const int64_t lo = static_cast<int64_t>(wg) * per, hi = min(n16, lo + per);
+  const float4* base = reinterpret_cast<const float4*>(fq.pf);
+  const int nt = blockDim.x;
+  float acc = 0.f;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += 4 * nt) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = base[min(i + u * nt, hi - 1)];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+  }
+  if (fq.pf_slices < 0) reinterpret_cast<float*>(fq.v_cache)[threadIdx.x] = acc;
+}
 
 // f[0..4) = sum_s part[s * slab + off + 0..4): batches of 4 clamped loads issued
 // before the adds (a runtime trip count with one load per iteration would chain S
@@ -199,6 +227,11 @@ __global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
     float* __restrict__ part_out, float* __restrict__ part_lse, uint16_t* __restrict__ out, int64_t out_stride,
     int Hq, int Hkv, int bs, float scale, int num_splits, int* __restrict__ counters, QkvFuse fq, int min_tps) {
   using C = DecodeCfg<D, G, NWAVES>;
+  if (FQ && static_cast<int>(blockIdx.z) >= num_splits) {  // weight-prefetch slice (whole workgroup)
+    prefetch_share(fq, (blockIdx.z - num_splits) * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x,
+                   fq.pf_slices * gridDim.x * gridDim.y);
+    return;
+  }
   const int kvh = blockIdx.x, b = blockIdx.y, split = blockIdx.z;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -432,11 +465,12 @@ static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, con
                           const int32_t* bt, int bts, const int32_t* sl, float* po, float* pl, uint16_t* out,
                           int64_t os, int B, int Hq, int Hkv, int bs, float scale, int S, int* counters,
                           const QkvFuse& fq, hipStream_t st) {
+  const int gz = S + (FQ ? fq.pf_slices : 0);
   if (FQ && decode_attn_waves() == 8)
-    hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, 8>), dim3(Hkv, B, S), dim3(512), 0, st, q, qs, kc, vc, bt, bts,
+    hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, 8>), dim3(Hkv, B, gz), dim3(512), 0, st, q, qs, kc, vc, bt, bts,
                        sl, po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq, S > 1 ? decode_min_split_tiles() : 1);
   else
-  hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt, bts, sl,
+  hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ>), dim3(Hkv, B, gz), dim3(256), 0, st, q, qs, kc, vc, bt, bts, sl,
                      po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq, S > 1 ? decode_min_split_tiles() : 1);
   if (S > 1 && counters == nullptr)
     hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
@@ -450,7 +484,7 @@ int decode_attention(const uint16_t* q, int64_t q_stride, const uint16_t* kc, co
   if (B <= 0) return 0;
   if (bs % 16 != 0 || Hq % Hkv != 0) return -1;
   const int G = Hq / Hkv;
-  const QkvFuse nofuse{nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+  const QkvFuse nofuse{nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0, 0};
 #define XGK_DEC(DD, GG)                                                                                  \
   if (D == DD && G == GG) {                                                                              \
     launch_decode<DD, GG, false>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, part_out, part_lse, out,  \
@@ -468,11 +502,14 @@ int decode_attention_fq(const float* part, int S_qkv, const int32_t* positions, 
                         const int32_t* slots, uint16_t* kc, uint16_t* vc, const int32_t* bt, int bt_stride,
                         const int32_t* seq_lens, float* part_out, float* part_lse, uint16_t* out,
                         int64_t out_stride, int B, int Hq, int Hkv, int D, int bs, float scale, int num_splits,
-                        int apply_rope, int* counters, hipStream_t st) {
+                        int apply_rope, int* counters, const void* pf, int64_t pf_bytes, int pf_slices,
+                        hipStream_t st) {
   if (B <= 0) return 0;
   if (part == nullptr || S_qkv < 1 || bs % 16 != 0 || Hq % Hkv != 0 || D != 128 || num_splits < 1) return -1;
   if (num_splits > 1 && (part_out == nullptr || part_lse == nullptr)) return -1;
-  const QkvFuse fq{part, S_qkv, positions, cos_sin, slots, kc, vc, apply_rope};
+  if (pf_slices < 0 || (pf_slices > 0 && (pf == nullptr || pf_bytes <= 0))) return -1;
+  const QkvFuse fq{part, S_qkv, positions, cos_sin, slots, kc, vc, apply_rope,
+                   static_cast<const uint8_t*>(pf), pf_bytes, pf_slices};
   const int G = Hq / Hkv;
 #define XGK_DECF(GG)                                                                                         \
   if (G == GG) {                                                                                             \

@@ -28,7 +28,7 @@ void add_partials_resid(const float*, int, int, uint16_t*, float*, int, hipStrea
 void row_sumsq(const uint16_t*, int, int, float*, hipStream_t);
 int decode_attention_fq(const float*, int, const int32_t*, const float*, const int32_t*, uint16_t*, uint16_t*,
                         const int32_t*, int, const int32_t*, float*, float*, uint16_t*, int64_t, int, int, int, int,
-                        int, float, int, int, int*, hipStream_t);
+                        int, float, int, int, int*, const void*, int64_t, int, hipStream_t);
 int moe_gemm_m64g(const uint16_t*, const int32_t*, const int32_t*, int, int, const uint16_t*, int, int, float*,
                   uint16_t*, int, int, int, int, int, hipStream_t);
 void add_partials_rmsnorm(const float*, int, int, uint16_t*, const uint16_t*, uint16_t*, int, float, hipStream_t);
@@ -241,11 +241,13 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("decode_attention_fq", [](uintptr_t part, int S_, uintptr_t pos, uintptr_t cs, uintptr_t slots, uintptr_t kc,
                                   uintptr_t vc, uintptr_t bt, int bts, uintptr_t sl, uintptr_t po, uintptr_t pl,
                                   uintptr_t out, int64_t os, int B, int Hq, int Hkv, int D, int bs, float scale,
-                                  int splits, int apply_rope, uintptr_t cnt, uintptr_t st) {
+                                  int splits, int apply_rope, uintptr_t cnt, uintptr_t pf, int64_t pf_bytes,
+                                  int pf_slices, uintptr_t st) {
     check(xgk::decode_attention_fq(P<const float>(part), S_, P<const int32_t>(pos), P<const float>(cs),
                                    P<const int32_t>(slots), P<uint16_t>(kc), P<uint16_t>(vc), P<const int32_t>(bt),
                                    bts, P<const int32_t>(sl), P<float>(po), P<float>(pl), P<uint16_t>(out), os, B, Hq,
-                                   Hkv, D, bs, scale, splits, apply_rope, P<int>(cnt), S(st)),
+                                   Hkv, D, bs, scale, splits, apply_rope, P<int>(cnt), P<const void>(pf), pf_bytes,
+                                   pf_slices, S(st)),
           "decode_attention_fq");
   });
   m.def("moe_gemm_m64g", [](uintptr_t x, uintptr_t rows, uintptr_t offs, int E, int K, uintptr_t w, int N, int P_,

@@ -87,8 +87,10 @@ def _paged(lens, Hkv, D, bs, extra_pages=8):
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 8)])
 @pytest.mark.parametrize("S", [1, 4, 8])
-@pytest.mark.parametrize("splits,in_kernel", [(1, False), (3, False), (3, True), (16, True)])
-def test_decode_attention_fused_prologue(Hq, Hkv, S, splits, in_kernel, monkeypatch):
+@pytest.mark.parametrize("splits,in_kernel,pf", [(1, False, False), (3, False, False), (3, True, False),
+                                                 (16, True, False), (1, False, True), (3, False, True),
+                                                 (16, True, True)])
+def test_decode_attention_fused_prologue(Hq, Hkv, S, splits, in_kernel, pf, monkeypatch):
     import xgserve.ops.attention as A
     monkeypatch.setattr(A, "IN_KERNEL_COMBINE", in_kernel)
     D, bs = 128, 16
@@ -104,9 +106,12 @@ def test_decode_attention_fused_prologue(Hq, Hkv, S, splits, in_kernel, monkeypa
     scale = 1.0 / math.sqrt(D)
     kc1, vc1, kc2, vc2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
     ws = A.DecodeWorkspace(B, Hq, D, splits, DEV)
+    # prefetch slices over an odd-sized weight (the tail share is partial); must not disturb the result
+    wpf = torch.randn(4096 * 1000 + 8, dtype=torch.bfloat16, device=DEV) if pf else None
+    monkeypatch.setattr(A, "ATTN_PREFETCH", True)
     for _ in range(2 if in_kernel else 1):  # the second launch needs the tickets re-armed by the first
         out = ops.decode_attention_fused(PendingSum(part, S), pos, slots, cs, kc1, vc1, bt, sl, Hq, scale, splits,
-                                         workspace=ws)
+                                         workspace=ws, prefetch=wpf)
     if in_kernel:
         assert int(ws.counters.abs().sum().item()) == 0
     # reference: the unfused chain (rope_cache_partials -> fp32 attention reference)

@@ -300,7 +300,7 @@ class LlamaLayer(nn.Module):
         returns the statistics of the new residual for the next layer."""
         eps = self.cfg.norm_eps
         pqkv = m64_norm_linear(resid, self.qkv, MODE_PARTIAL, stats, eps)
-        a = self.attn.fused_decode(pqkv, meta, kv, cos_sin)
+        a = self.attn.fused_decode(pqkv, meta, kv, cos_sin, prefetch=self.o)
         st = m64_resid_linear(a, self.o, resid, ws, site, eps)
         act = m64_norm_linear(resid, self.gate_up, MODE_SILU, st, eps)
         return m64_resid_linear(act, self.down, resid, ws, site + 1, eps)

@@ -16,6 +16,14 @@ from ._native import kernels, stream_ptr, use_native
 # still 0.4-1.6 % slower than the graph-captured combine launch at batch 1 / 8 / 64
 # (profiles/r1_inlaunch_combine_ab.md), so the separate launch stays the default.
 IN_KERNEL_COMBINE = os.environ.get("XGS_DECODE_INLAUNCH_COMBINE", "0") == "1"
+# Small-batch decode (opt-in, XGS_ATTN_PREFETCH=1): extra workgroups of the fused
+# attention launch read the O projection's weights into the Infinity Cache while the
+# latency-bound attention runs. Measured slower (8B batch 1 +3 %, batch 8 +7 %, 70B
+# batch 1 +10 % ms/step, profiles/r1_attn_prefetch_ab.md): the launch now ends only
+# when its prefetch share has streamed, which costs more than the O GEMM saves.
+ATTN_PREFETCH = os.environ.get("XGS_ATTN_PREFETCH", "0") == "1"
+ATTN_PREFETCH_MAX_B = int(os.environ.get("XGS_ATTN_PREFETCH_MAX_B", "8"))
+ATTN_PREFETCH_WGS = int(os.environ.get("XGS_ATTN_PREFETCH_WGS", "128"))
 
 
 def choose_num_splits(batch: int, num_kv_heads: int, max_seq_len: int, num_cus: int = 256) -> int:
@@ -128,11 +136,14 @@ def decode_attention_fused(pend, positions: torch.Tensor, slot_mapping: torch.Te
                            k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                            seq_lens: torch.Tensor, num_heads: int, scale: float, num_splits: int = 1,
                            workspace: Optional[DecodeWorkspace] = None, apply_rope: bool = True,
-                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                           out: Optional[torch.Tensor] = None,
+                           prefetch: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Paged decode attention on the QKV projection's split-K partials (PendingSum
     [S, B, (Hq + 2 Hkv) D]): each workgroup's prologue reduces its (sequence, kv
     head) slice, applies RoPE and appends the new K/V row to the cache -- the work
-    of rope_cache_partials without its launch or the q round trip. -> [B, Hq * D]."""
+    of rope_cache_partials without its launch or the q round trip. -> [B, Hq * D].
+    `prefetch` (the next GEMM's weight): read into the Infinity Cache by extra
+    workgroups of the same launch when B <= ATTN_PREFETCH_MAX_B."""
     S, B, W = pend.part.shape
     Hkv, bs, D = k_cache.shape[1], k_cache.shape[2], k_cache.shape[3]
     Hq = num_heads
@@ -147,11 +158,17 @@ def decode_attention_fused(pend, positions: torch.Tensor, slot_mapping: torch.Te
             workspace = DecodeWorkspace(B, Hq, D, num_splits, pend.part.device)
         po, pl = workspace.part_out.data_ptr(), workspace.part_lse.data_ptr()
         cnt = workspace.counters.data_ptr() if IN_KERNEL_COMBINE else 0
+    pf, pf_bytes, pf_slices = 0, 0, 0
+    if prefetch is not None and ATTN_PREFETCH and B <= ATTN_PREFETCH_MAX_B and prefetch.is_contiguous():
+        pf, pf_bytes = prefetch.data_ptr(), prefetch.numel() * prefetch.element_size()
+        skip = -pf % 16  # 16-B lanes start aligned
+        pf, pf_bytes = pf + skip, pf_bytes - skip
+        pf_slices = max(1, -(-ATTN_PREFETCH_WGS // (Hkv * B)))
     kernels().decode_attention_fq(pend.part.data_ptr(), S, positions.data_ptr(), cos_sin.data_ptr(),
                                   slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                   block_tables.data_ptr(), block_tables.stride(0), seq_lens.data_ptr(), po, pl,
                                   out.data_ptr(), out.stride(0), B, Hq, Hkv, D, bs, float(scale), int(num_splits),
-                                  1 if apply_rope else 0, cnt, stream_ptr())
+                                  1 if apply_rope else 0, cnt, pf, pf_bytes, pf_slices, stream_ptr())
     return out
 
 
