@@ -49,15 +49,70 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`python bench.py --gpus N` without an external launcher: start N fresh rank
+    processes (one per GPU, RANK/LOCAL_RANK/WORLD_SIZE set, rendezvous on
+    127.0.0.1) and return the worst exit code. Runs before anything imports torch,
+    so this parent never initialises the GPU; rank 0's JSON line reaches our
+    stdout directly. If one rank dies the others are terminated (no hung
+    collective)."""
+    import signal
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        if live:
+            time.sleep(0.05)
+    return rc
+
+
 def main():
     a = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        return launch_ranks(a.gpus)
+    world = int(env_world or "1")
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}: refusing to report a mismatched run",
+              file=sys.stderr)
+        return 2
+    if a.gpus % a.tp:
+        print(f"bench.py: --gpus {a.gpus} is not a multiple of --tp {a.tp}", file=sys.stderr)
+        return 2
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     import torch
     import torch.distributed as dist
     from xgserve.parallel.state import init_distributed
     from xgserve.engine import EngineConfig, LLMEngine, SamplingParams
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if torch.cuda.is_available() and torch.cuda.device_count() < local_world:
+        # two ranks sharing one device would report a fake multi-GPU number
+        print(f"bench.py: {local_world} ranks on this node but only {torch.cuda.device_count()} visible GPUs",
+              file=sys.stderr)
+        return 2
     st = init_distributed(tp_size=a.tp)
     rank = st.rank
     dp = world // a.tp

@@ -196,6 +196,10 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("moe_topk_softmax", [](uintptr_t logits, int is_f32, int T, int E, int k, int renorm, uintptr_t w,
                                uintptr_t ids, uintptr_t st) {
+    // the kernel keeps the router row and the selection in fixed local arrays (v[64], sel[16])
+    if (E < 1 || E > 64) throw std::invalid_argument("moe_topk_softmax: 1 <= E <= 64");
+    if (k < 1 || k > 16 || k > E) throw std::invalid_argument("moe_topk_softmax: 1 <= k <= min(16, E)");
+    if (T < 0) throw std::invalid_argument("moe_topk_softmax: T < 0");
     xgk::moe_topk_softmax(P<const void>(logits), is_f32, T, E, k, renorm, P<float>(w), P<int32_t>(ids), S(st));
     check(0, "moe_topk_softmax");
   });

@@ -79,13 +79,15 @@ std::vector<int> PrefixCache::match(const int32_t* tokens, int n_tokens, int max
     out.push_back(c->block);
     cur = c;
   }
-  if (count) {
-    int hit = static_cast<int>(out.size()) * bs_;
-    stats_.hit_tokens += hit;
-    stats_.miss_tokens += std::max(0, n_tokens - hit);
-    if (out.empty()) ++stats_.miss_count; else ++stats_.hit_count;
-  }
+  if (count) record_lookup(n_tokens, static_cast<int>(out.size()));
   return out;
+}
+
+void PrefixCache::record_lookup(int n_tokens, int hit_pages) {
+  int hit = hit_pages * bs_;
+  stats_.hit_tokens += hit;
+  stats_.miss_tokens += std::max(0, n_tokens - hit);
+  if (hit_pages == 0) ++stats_.miss_count; else ++stats_.hit_count;
 }
 
 int PrefixCache::insert(const int32_t* tokens, int n_tokens, const int* blocks, int n_blocks) {

@@ -64,6 +64,9 @@ class PrefixCache {
   // Longest cached page-aligned prefix of tokens[0:max_tokens). Returns the
   // page ids (NOT incref'd) and touches the path. Counts a hit/miss.
   std::vector<int> match(const int32_t* tokens, int n_tokens, int max_tokens, bool count = true);
+  // hit/miss accounting of one lookup, for callers that count only once the
+  // lookup's result is actually used (scheduler admission can fail and retry)
+  void record_lookup(int n_tokens, int hit_pages);
   // Insert the first n_full_pages pages of (tokens, blocks). The cache takes a
   // reference on every page it newly stores. Returns #pages newly cached.
   int insert(const int32_t* tokens, int n_tokens, const int* blocks, int n_blocks);

@@ -14,13 +14,16 @@ StepScheduler::StepScheduler(const SchedulerConfig& cfg)
   max_blocks_per_seq_ = (cfg_.max_model_len + cfg_.block_size - 1) / cfg_.block_size + 1;
   free_slots_.reserve(cfg_.max_num_seqs);
   for (int i = cfg_.max_num_seqs - 1; i >= 0; --i) free_slots_.push_back(i);
+  slots_created_ = cfg_.max_num_seqs;
 }
 
 void StepScheduler::set_limits(int max_num_seqs, int max_num_batched_tokens) {
-  // Slots only grow (a running sequence keeps its slot).
-  for (int i = cfg_.max_num_seqs; i < max_num_seqs; ++i) free_slots_.insert(free_slots_.begin(), i);
-  if (max_num_seqs > cfg_.max_num_seqs) cfg_.max_num_seqs = max_num_seqs;
-  else cfg_.max_num_seqs = std::max(1, max_num_seqs);
+  // The slot pool only grows: ids below the high-water mark already exist (free or
+  // held by a running sequence); a shrink just lowers the admission limit, which
+  // the running_.size() < max_num_seqs check enforces.
+  for (int i = slots_created_; i < max_num_seqs; ++i) free_slots_.insert(free_slots_.begin(), i);
+  slots_created_ = std::max(slots_created_, max_num_seqs);
+  cfg_.max_num_seqs = std::max(1, max_num_seqs);
   cfg_.max_num_batched_tokens = std::max(1, max_num_batched_tokens);
 }
 
@@ -279,9 +282,11 @@ const StepPlan& StepScheduler::schedule() {
     Sequence* s = waiting_.front();
     if (s->tokens.back() == kPlaceholder) break;  // preempted by a lookahead plan: wait for commit()
     int matched_pages = 0;
+    bool looked_up = false;
     if (cfg_.enable_prefix_cache && s->blocks.empty() && s->num_computed == 0) {
+      looked_up = true;
       const int n = static_cast<int>(s->tokens.size());
-      std::vector<int> pages = cache_.match(s->tokens.data(), n, n - 1, /*count=*/s->num_preemptions == 0);
+      std::vector<int> pages = cache_.match(s->tokens.data(), n, n - 1, /*count=*/false);
       for (int b : pages) {
         alloc_.incref(b);
         s->blocks.push_back(b);
@@ -307,6 +312,8 @@ const StepPlan& StepScheduler::schedule() {
       break;
     }
     waiting_.pop_front();
+    if (looked_up && s->num_preemptions == 0)  // count the lookup once, when it is used
+      cache_.record_lookup(static_cast<int>(s->tokens.size()), matched_pages);
     s->status = SeqStatus::Running;
     if (free_slots_.empty()) throw std::runtime_error("scheduler: slot pool exhausted");
     s->slot = free_slots_.back();

@@ -172,6 +172,7 @@ class StepScheduler {
   std::deque<Sequence*> waiting_;
   std::vector<Sequence*> running_;
   std::vector<int> free_slots_;
+  int slots_created_ = 0;  // slot ids [0, slots_created_) exist (free or in use)
   StepPlan plan_;
   std::vector<Sequence*> plan_seqs_;
   int64_t arrival_counter_ = 0;

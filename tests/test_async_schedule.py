@@ -123,3 +123,48 @@ def test_lookahead_under_preemption():
     assert a == b and fa == fb
     assert all(len(v) == 20 for v in b.values())
     assert sb.total_preemptions() > 0 if hasattr(sb, "total_preemptions") else True
+
+
+def test_shrink_then_grow_keeps_slots_distinct():
+    """set_limits(max//2) then set_limits(max) (degradation ladder, hot reload) must
+    not duplicate slot ids: two running sequences sharing a slot would share the
+    engine's per-slot sampling state."""
+    s = _sched(num_blocks=256, max_seqs=8)
+    for _ in range(3):
+        s.set_limits(4, 64)
+        s.set_limits(8, 64)
+    for i in range(8):
+        assert s.add(i + 1, [5 + i, 6, 7], 4, 1, True, False, [], 0)
+    plan = s.schedule()
+    assert plan["num_seqs"] == 8
+    slots = [int(x) for x in plan["slots"]]
+    assert sorted(slots) == list(range(8)), slots
+    # growing beyond the original size creates exactly the new ids
+    s.set_limits(4, 64)
+    s.set_limits(10, 64)
+    for i in range(2):
+        assert s.add(100 + i, [9, 9, 9, 9], 4, 1, True, False, [], 0)
+    s.update(np.ones(int(plan["num_sample"]), np.int32), np.ones(int(plan["num_sample"]), np.int32))
+    plan2 = s.schedule()
+    new = [int(x) for x, sid in zip(plan2["slots"], plan2["seq_ids"]) if int(sid) >= 100]
+    assert sorted(new) == [8, 9]
+    assert len(set(int(x) for x in plan2["slots"])) == plan2["num_seqs"]
+
+
+def test_prefix_lookup_counted_once_per_admission():
+    """A request whose admission fails for lack of pages is retried every step: its
+    prefix-cache lookup must be counted once (when admitted), not per retry."""
+    s = _sched(num_blocks=8, max_seqs=4)
+    assert s.add(1, list(range(10, 26)), 8, 1, True, False, [], 0)   # 4 pages + decode page
+    plan = s.schedule()
+    assert s.add(2, list(range(40, 64)), 4, 1, True, False, [], 0)   # needs 6+ pages: must wait
+    before = s.cache_stats()
+    for _ in range(3):
+        s.update(np.ones(int(plan["num_sample"]), np.int32), np.ones(int(plan["num_sample"]), np.int32))
+        plan = s.schedule()
+        if 2 in [int(x) for x in plan["seq_ids"]]:
+            break
+    mid = s.cache_stats()
+    waiting_lookups = (mid["hit_count"] + mid["miss_count"]) - (before["hit_count"] + before["miss_count"])
+    admitted = 2 in [int(x) for x in plan["seq_ids"]]
+    assert waiting_lookups == (1 if admitted else 0)

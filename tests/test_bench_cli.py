@@ -20,13 +20,24 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _run(nproc, *args):
+def _env():
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
-           "--gpus", str(nproc), "--steps", "4", "--warmup", "2", "--concurrency", "2", "--prompt-len", "16",
-           "--output-len", "4", *args]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+SMALL = ["--steps", "4", "--warmup", "2", "--concurrency", "2", "--prompt-len", "16", "--output-len", "4"]
+
+
+def _run(nproc, *args, launcher=True):
+    if launcher:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py")]
+    else:  # bench.py spawns its own ranks (the driver's `python bench.py --gpus N` form)
+        cmd = [sys.executable, str(ROOT / "bench.py")]
+    cmd += ["--gpus", str(nproc), *SMALL, *args]
+    p = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]  # rank 0 only
@@ -37,6 +48,30 @@ def _run(nproc, *args):
                                                 (4, 2, "mixtral-tiny", "dp2xtp2")])
 def test_bench_multi_rank_json_contract(nproc, tp, model, par):
     r = _run(nproc, "--tp", str(tp), "--model", model)
+    _check_contract(r, nproc, model, par, tp)
+
+
+@pytest.mark.parametrize("nproc,tp,par", [(2, 1, "dp2"), (4, 2, "dp2xtp2")])
+def test_bench_self_launches_ranks(nproc, tp, par):
+    """`python bench.py --gpus N` with no external launcher starts N ranks itself."""
+    r = _run(nproc, "--tp", str(tp), "--model", "llama-tiny", launcher=False)
+    _check_contract(r, nproc, "llama-tiny", par, tp)
+
+
+def test_bench_single_gpu_default_unchanged():
+    r = _run(1, "--model", "llama-tiny", launcher=False)
+    _check_contract(r, 1, "llama-tiny", "dp1", 1)
+
+
+def test_bench_rejects_world_mismatch():
+    env = dict(_env(), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", *SMALL, "--model", "llama-tiny"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 2 and "WORLD_SIZE" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def _check_contract(r, nproc, model, par, tp):
     for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
                 "scaling", "vs_baseline", "dtype", "data", "config"):
         assert key in r
