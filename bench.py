@@ -165,9 +165,17 @@ def main():
     for i in range(a.concurrency):
         submit(max(1, int(round(1 + (2 * a.output_len - 1) * (i + 0.5) / a.concurrency))))
 
+    step_log = [] if os.environ.get("XGS_STEP_LOG") else None
+
     def run_step():
+        if step_log is not None:
+            t0, c0 = time.perf_counter(), dict(eng.stats_counters)
         outs = eng.step()
         now = time.perf_counter()
+        if step_log is not None:
+            c1 = eng.stats_counters
+            step_log.append((round(1000 * (now - t0), 3), c1["prefill_tokens_computed"] - c0["prefill_tokens_computed"],
+                             c1["decode_steps"] - c0["decode_steps"], c1["generation_tokens"] - c0["generation_tokens"]))
         n_tok = 0
         for o in outs:
             n_tok += len(o.new_token_ids)
@@ -195,6 +203,11 @@ def main():
     if lgroup is not None:
         dist.barrier(group=lgroup)
     sync()
+    if step_log is not None:
+        with open(os.environ["XGS_STEP_LOG"], "w") as f:
+            for i, e in enumerate(step_log):
+                f.write(json.dumps({"i": i, "timed": i >= a.warmup, "ms": e[0], "prefill_tokens": e[1],
+                                    "decode_step": e[2], "gen_tokens": e[3]}) + "\n")
     ttfts = [first_tok[r] - arrival[r] for r in first_tok if r not in first_before]
     p50_local = float(np.median(ttfts)) if ttfts else float("nan")
 

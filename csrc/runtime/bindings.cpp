@@ -231,6 +231,7 @@ PYBIND11_MODULE(_runtime, m) {
       .def_readwrite("cache_threshold", &SchedulerConfig::cache_threshold)
       .def_readwrite("admit_watermark", &SchedulerConfig::admit_watermark)
       .def_readwrite("max_prefill_seqs", &SchedulerConfig::max_prefill_seqs)
+      .def_readwrite("decode_prefill_cap", &SchedulerConfig::decode_prefill_cap)
       .def_readwrite("eos_ids", &SchedulerConfig::eos_ids);
 
   py::class_<StepScheduler>(m, "StepScheduler")

@@ -241,6 +241,7 @@ const StepPlan& StepScheduler::schedule() {
     --budget;
   }
   plan_.num_decodes = plan_.num_seqs;
+  if (cfg_.decode_prefill_cap > 0 && plan_.num_decodes > 0) budget = std::min(budget, cfg_.decode_prefill_cap);
 
   // Pass 2: verify steps (decode + draft) and continuing prefill chunks.
   int n_prefill = 0;

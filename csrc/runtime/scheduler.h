@@ -47,6 +47,10 @@ struct SchedulerConfig {
   float cache_threshold = 0.8f;   // max share of the pool the prefix cache may hold
   float admit_watermark = 0.01f;  // keep this share of pages free when admitting
   int max_prefill_seqs = 1 << 30; // cap on prefill sequences per step
+  // cap on prefill tokens in a step that also carries decode rows (0: no cap).
+  // Stall-free batching: prompt chunks ride on the decode step's weight reads
+  // instead of stalling every running stream behind one large prefill step.
+  int decode_prefill_cap = 0;
   std::vector<int32_t> eos_ids;
 };
 

@@ -68,6 +68,8 @@ class EngineConfig:
     seed: int = 0
     moe_comm: str = "alltoall"
     max_prefill_seqs: int = 1 << 30
+    # prefill tokens allowed in a step that also decodes (0: only the token budget)
+    decode_prefill_cap: int = 0
     # speculative decoding (Req 12)
     draft_model: Optional[str] = None
     num_speculative_tokens: int = 0
@@ -124,6 +126,7 @@ class LLMEngine:
         sc.chunked_prefill = cfg.chunked_prefill
         sc.cache_threshold = cfg.cache_threshold
         sc.max_prefill_seqs = cfg.max_prefill_seqs
+        sc.decode_prefill_cap = int(os.environ.get("XGS_DECODE_PREFILL_CAP", cfg.decode_prefill_cap))
         sc.eos_ids = list(self.mcfg.eos_token_ids)
         self.sched = R.StepScheduler(sc)
         # decode graphs capture the TP collectives: RCCL (and the IPC all-reduce) can be
