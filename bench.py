@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--weight-dtype", default=None, choices=["fp8"],
                     help="fp8: E4M3 weight copies for batch <= 16 decode (not the bf16 headline)")
     ap.add_argument("--no-prefix-cache", action="store_true")
+    ap.add_argument("--tp-shard", type=int, default=1,
+                    help="single-GPU simulation of ONE rank of a TP group of this degree: the rank's weight / "
+                         "KV shards and kernels, collectives replaced by local reductions (not a TP measurement: "
+                         "xGMI time is excluded; reported with parallelism 'tpN-shard-sim')")
     return ap.parse_args()
 
 
@@ -132,7 +136,15 @@ def main():
                         weight_dtype=a.weight_dtype, dtype=None if on_gpu else "float32",
                         graph_batch_sizes=[b for b in [1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128]
                                            if b <= max(64, a.concurrency)], seed=st.dp_rank)
-    eng = LLMEngine(ecfg)
+    shard_model = None
+    if a.tp_shard > 1:
+        if world != 1 or a.tp != 1:
+            print("bench.py: --tp-shard simulates one TP rank in a single process (--gpus 1 --tp 1)", file=sys.stderr)
+            return 2
+        from xgserve.models import build_model, get_config
+        shard_model = build_model(get_config(a.model), device=dev, tp=a.tp_shard, rank=0,
+                                  weight_dtype=a.weight_dtype)
+    eng = LLMEngine(ecfg, model=shard_model)
     leader = st.tp_rank == 0
     # timing collectives run among the TP leaders only (followers sit in follower_loop)
     leaders = [r for r in range(world) if r % a.tp == 0]
@@ -223,6 +235,8 @@ def main():
         value = tokens / elapsed
         st_ = eng.stats()
         par = f"dp{dp}" if a.tp == 1 else (f"tp{a.tp}" if dp == 1 else f"dp{dp}xtp{a.tp}")
+        if a.tp_shard > 1:
+            par = f"tp{a.tp_shard}-shard-sim"
         print(json.dumps({
             "metric": "output_tokens_per_sec",
             "value": round(value, 2),

@@ -22,6 +22,10 @@ SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "dow
           "qkv70": (10240, 8192), "o70": (8192, 8192), "gate_up70": (57344, 8192), "down70": (8192, 28672),
           "qkv70t8": (1280, 8192), "o70t8": (8192, 1024), "gate_up70t8": (7168, 8192), "down70t8": (8192, 3584),
           "qkv8t2": (3072, 4096), "o8t2": (4096, 2048), "gate_up8t2": (14336, 4096), "down8t2": (4096, 7168),
+          "qkv8t4": (1536, 4096), "o8t4": (4096, 1024), "gate_up8t4": (7168, 4096), "down8t4": (4096, 3584),
+          "qkv8t8": (768, 4096), "o8t8": (4096, 512), "gate_up8t8": (3584, 4096), "down8t8": (4096, 1792),
+          "qkv70t2": (5120, 8192), "o70t2": (8192, 4096), "gate_up70t2": (28672, 8192), "down70t2": (8192, 14336),
+          "qkv70t4": (2560, 8192), "o70t4": (8192, 2048), "gate_up70t4": (14336, 8192), "down70t4": (8192, 7168),
           # gate_up shapes as plain split-K partial GEMMs (what a split SiLU epilogue would stream)
           "gate_up_p": (28672, 4096), "gate_up70_p": (57344, 8192)}
 

@@ -15,8 +15,10 @@
 //     4. sum chunk b over ranks 0..W-1 in fixed rank order (bit-identical
 //        results on every rank) with fp32 accumulation; write the output
 //   gen is a per-block counter kept in device memory, so the kernel is HIP
-//   graph capturable (no host-side sequence number). gens[CAR_MAX_BLOCKS]
-//   counts peer-wait timeouts (a missing peer never hangs the GPU).
+//   graph capturable (no host-side sequence number). A peer wait that times out
+//   (~1 s) bumps the device error counter `err` and gives up instead of hanging
+//   the GPU; the host reads the counter after every step (CustomAllReduce.check)
+//   and fails the step, so a missing peer is an error, never a wrong sum.
 //
 // Double buffering (slot = gen & 1) makes reuse safe: before a block writes slot
 // s at generation g, every peer has passed generation g-1 of the same block,
@@ -65,7 +67,8 @@ __device__ __forceinline__ void acc8<uint16_t>(float* a, uint4 v) {  // bf16
 template <typename T>
 __global__ void __launch_bounds__(CAR_THREADS) car_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                           int64_t nbytes, int64_t slot_bytes, CarPtrs p, int rank,
-                                                          int world, uint32_t* __restrict__ gens) {
+                                                          int world, uint32_t* __restrict__ gens,
+                                                          uint32_t* __restrict__ err) {
   const int b = blockIdx.x;
   const int t = threadIdx.x;
   const uint32_t gen = gens[b] + 1;
@@ -95,7 +98,7 @@ __global__ void __launch_bounds__(CAR_THREADS) car_kernel(const uint8_t* __restr
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins > (1u << 24)) {  // ~1 s: a peer never arrived -- record it and bail out rather than hang
-        atomicAdd(gens + CAR_MAX_BLOCKS, 1u);
+        atomicAdd(err, 1u);
         break;
       }
     }
@@ -145,13 +148,17 @@ template <typename T>
 __global__ void __launch_bounds__(CAR_THREADS) car2_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                            int64_t nbytes, int64_t shard, int64_t slot_bytes,
                                                            CarPtrs p, int rank, int world,
-                                                           uint32_t* __restrict__ gens) {
+                                                           uint32_t* __restrict__ gens,
+                                                           uint32_t* __restrict__ err) {
   const int b = blockIdx.x;
   const int t = threadIdx.x;
   const uint32_t gen = gens[b] + 1;
   const int64_t slot_off = (gen & 1) * slot_bytes;
   const int64_t cbase = static_cast<int64_t>(b) * CAR_CHUNK;
+  // slot layout [block][shard][16 KiB]: block b's region is the same in every
+  // launch whatever the message size (the per-block double-buffering argument)
   uint8_t* mine = p.data[rank] + slot_off;
+  const int64_t bbase = static_cast<int64_t>(b) * world * CAR_CHUNK;
   // 1. stage chunk b of every shard (loads first, then stores: W*4 x 16 B in flight)
   for (int s = 0; s < world; ++s) {
     uint4 v[4];
@@ -163,36 +170,238 @@ __global__ void __launch_bounds__(CAR_THREADS) car2_kernel(const uint8_t* __rest
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int64_t o = cbase + (static_cast<int64_t>(i) * CAR_THREADS + t) * 16;
+      const int64_t lo = (static_cast<int64_t>(i) * CAR_THREADS + t) * 16;
+      const int64_t o = cbase + lo;
       const int64_t g = s * shard + o;
-      if (o < shard && g < nbytes) st16(mine + g, v[i]);
+      if (o < shard && g < nbytes) st16(mine + bbase + s * CAR_CHUNK + lo, v[i]);
     }
   }
-  car_signal_wait<T>(p, 0, rank, world, b, gen, gens + CAR_MAX_BLOCKS);
+  car_signal_wait<T>(p, 0, rank, world, b, gen, err);
   // 2. reduce my shard's chunk b in rank order
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int64_t o = cbase + (static_cast<int64_t>(i) * CAR_THREADS + t) * 16;
+    const int64_t lo = (static_cast<int64_t>(i) * CAR_THREADS + t) * 16;
+    const int64_t o = cbase + lo;
     const int64_t g = rank * shard + o;
     if (o >= shard || g >= nbytes) continue;
+    const int64_t so = bbase + rank * CAR_CHUNK + lo;
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int r = 0; r < world; ++r) acc8<T>(a, ld16_nt(p.data[r] + slot_off + g));
+    for (int r = 0; r < world; ++r) acc8<T>(a, ld16_nt(p.data[r] + slot_off + so));
     const uint4 y = pack8(a);
     st16(out + g, y);
-    st16(mine + g, y);
+    st16(mine + so, y);
   }
-  car_signal_wait<T>(p, 1, rank, world, b, gen, gens + CAR_MAX_BLOCKS);
+  car_signal_wait<T>(p, 1, rank, world, b, gen, err);
   // 3. gather every other shard's chunk b from its owner
   for (int s = 0; s < world; ++s) {
     if (s == rank) continue;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int64_t o = cbase + (static_cast<int64_t>(i) * CAR_THREADS + t) * 16;
+      const int64_t lo = (static_cast<int64_t>(i) * CAR_THREADS + t) * 16;
+      const int64_t o = cbase + lo;
       const int64_t g = s * shard + o;
-      if (o < shard && g < nbytes) st16(out + g, ld16_nt(p.data[s] + slot_off + g));
+      if (o < shard && g < nbytes) st16(out + g, ld16_nt(p.data[s] + slot_off + bbase + s * CAR_CHUNK + lo));
     }
   }
   if (t == 0) gens[b] = gen;
+}
+
+// Fused decode layer under TP (row-parallel O / down projections): one launch
+// replaces reduce_partials -> all-reduce -> add + RMSNorm statistics.
+//   block (t, chunk) owns row t, columns [chunk*1024, chunk*1024 + 1024) (128 lanes x 8):
+//     1. sum this rank's S split-K fp32 partial slices, round to bf16 (the value
+//        every rank contributes -- the message is bf16, as in the unfused path),
+//        store into my IPC slot
+//     2. signal / wait exactly as car_kernel (block index = t * nchunk + chunk)
+//     3. resid = bf16(resid + sum over ranks in rank order) -- bit-identical on
+//        every rank, so the replicated residual stream never diverges
+//     4. the new residual's sum of squares -> ss_part[chunk * T + t] (the
+//        RowStats layout of add_partials_resid: the next GEMM adds the H/1024
+//        chunk sums in order and applies the RMSNorm as a row scale)
+// T * H/1024 <= CAR_MAX_BLOCKS (decode: T <= 64, H <= 8192).
+template <int SP>
+__global__ void __launch_bounds__(128) car_resid_kernel(const float* __restrict__ part, int S, int T,
+                                                        uint16_t* __restrict__ resid, float* __restrict__ ss_part,
+                                                        int H, int64_t slot_bytes, CarPtrs p, int rank, int world,
+                                                        uint32_t* __restrict__ gens, uint32_t* __restrict__ err) {
+  __shared__ float red[2];
+  const int t = blockIdx.x, chunk = blockIdx.y;
+  const int b = t * gridDim.y + chunk;
+  const int lane = threadIdx.x;
+  const uint32_t gen = gens[b] + 1;
+  const int64_t slot_off = (gen & 1) * slot_bytes;
+  const int64_t e = static_cast<int64_t>(t) * H + (chunk * 128 + lane) * 8;  // element offset
+  // 1. local split-K reduction -> bf16 contribution
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int ns = SP > 0 ? SP : S;
+#pragma unroll
+  for (int s = 0; s < ns; ++s) {
+    const float* pp = part + static_cast<int64_t>(s) * T * H + e;
+    const float4 a = *reinterpret_cast<const float4*>(pp);
+    const float4 c = *reinterpret_cast<const float4*>(pp + 4);
+    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+    v[4] += c.x; v[5] += c.y; v[6] += c.z; v[7] += c.w;
+  }
+  const uint4 mine = pack8(v);
+  const uint4 r_old = ld16(resid + e);
+  st16(p.data[rank] + slot_off + e * 2, mine);
+  // 2. publish + wait
+  __threadfence_system();
+  __syncthreads();
+  if (lane < world && lane != rank)
+    __hip_atomic_store(p.sig[lane] + rank * CAR_MAX_BLOCKS + b, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane < world && lane != rank) {
+    const uint32_t* f = p.sig[rank] + lane * CAR_MAX_BLOCKS + b;
+    uint32_t spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 24)) {
+        atomicAdd(err, 1u);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __threadfence_system();
+  // 3. cross-rank sum in rank order (all peer loads issued before the adds)
+  uint4 pv[CAR_MAX_RANKS];
+#pragma unroll
+  for (int r = 0; r < CAR_MAX_RANKS; ++r)
+    if (r < world) pv[r] = (r == rank) ? mine : ld16_nt(p.data[r] + slot_off + e * 2);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < CAR_MAX_RANKS; ++r)
+    if (r < world) acc8<uint16_t>(acc, pv[r]);
+  float ro[8];
+  unpack8(r_old, ro);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ro[i] += acc[i];
+  const uint4 pk = pack8(ro);
+  st16(resid + e, pk);
+  // 4. statistics of the stored (rounded) residual
+  unpack8(pk, ro);
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ss += ro[i] * ro[i];
+  ss = block_sum(ss, red);
+  if (lane == 0) {
+    ss_part[static_cast<int64_t>(chunk) * T + t] = ss;
+    gens[b] = gen;
+  }
+}
+
+int custom_allreduce_resid(const float* part, int S, int T, uint16_t* resid, float* ss_part, int H,
+                           int64_t slot_bytes, const uintptr_t* data_ptrs, const uintptr_t* sig_ptrs, int rank,
+                           int world, uint32_t* gens, uint32_t* err, hipStream_t st) {
+  if (world < 2 || world > CAR_MAX_RANKS || rank < 0 || rank >= world) return 1;
+  if (T <= 0 || S <= 0 || H <= 0 || H % 1024) return 1;
+  if (static_cast<int64_t>(T) * (H / 1024) > CAR_MAX_BLOCKS) return 1;
+  if (static_cast<int64_t>(T) * H * 2 > slot_bytes) return 1;
+  CarPtrs p{};
+  for (int r = 0; r < world; ++r) {
+    p.data[r] = reinterpret_cast<uint8_t*>(data_ptrs[r]);
+    p.sig[r] = reinterpret_cast<uint32_t*>(sig_ptrs[r]);
+  }
+  const dim3 g(T, H / 1024);
+#define XGK_CARR(SPV)                                                                                          \
+  hipLaunchKernelGGL((car_resid_kernel<SPV>), g, dim3(128), 0, st, part, S, T, resid, ss_part, H, slot_bytes, p, \
+                     rank, world, gens, err)
+  if (S == 1) XGK_CARR(1);
+  else if (S == 2) XGK_CARR(2);
+  else if (S == 4) XGK_CARR(4);
+  else if (S == 8) XGK_CARR(8);
+  else XGK_CARR(0);
+#undef XGK_CARR
+  return 0;
+}
+
+// All-gather along the last dimension through peer memory (the vocab-parallel LM
+// head of a decode step: [T, V/W] bf16 logits per rank -> [T, V] everywhere).
+// Graph capturable like car_kernel; every rank reads each peer's shard over its
+// own xGMI link concurrently. Block b handles the 16 KiB chunks b, b + 512, ...
+// of the flat shard (a fixed stride, NOT the grid size: a block's slot region must
+// be the same in every launch for the per-block double-buffering argument) (rows x cb bytes, cb % 16 == 0): it stages them into its IPC
+// slot and straight into its own output columns, signals once, waits for every
+// peer's block b, then copies the peers' chunks into their output columns.
+__global__ void __launch_bounds__(CAR_THREADS) car_gather_kernel(const uint8_t* __restrict__ in,
+                                                                 uint8_t* __restrict__ out, uint32_t nbytes,
+                                                                 uint32_t cb, int64_t slot_bytes, CarPtrs p, int rank,
+                                                                 int world, uint32_t* __restrict__ gens,
+                                                                 uint32_t* __restrict__ err) {
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;
+  const uint32_t gen = gens[b] + 1;
+  const int64_t slot_off = (gen & 1) * slot_bytes;
+  const int64_t row_bytes = static_cast<int64_t>(world) * cb;
+  for (uint32_t base = static_cast<uint32_t>(b) * CAR_CHUNK; base < nbytes; base += CAR_MAX_BLOCKS * CAR_CHUNK) {
+    uint4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t off = base + (i * CAR_THREADS + t) * 16;
+      if (off < nbytes) v[i] = ld16(in + off);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t off = base + (i * CAR_THREADS + t) * 16;
+      if (off < nbytes) {
+        st16(p.data[rank] + slot_off + off, v[i]);
+        st16(out + (off / cb) * row_bytes + static_cast<int64_t>(rank) * cb + off % cb, v[i]);
+      }
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (t < world && t != rank)
+    __hip_atomic_store(p.sig[t] + rank * CAR_MAX_BLOCKS + b, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t < world && t != rank) {
+    const uint32_t* f = p.sig[rank] + t * CAR_MAX_BLOCKS + b;
+    uint32_t spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 24)) {
+        atomicAdd(err, 1u);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __threadfence_system();
+  for (int r = 0; r < world; ++r) {
+    if (r == rank) continue;
+    for (uint32_t base = static_cast<uint32_t>(b) * CAR_CHUNK; base < nbytes; base += CAR_MAX_BLOCKS * CAR_CHUNK) {
+      uint4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t off = base + (i * CAR_THREADS + t) * 16;
+        if (off < nbytes) v[i] = ld16_nt(p.data[r] + slot_off + off);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t off = base + (i * CAR_THREADS + t) * 16;
+        if (off < nbytes) st16(out + (off / cb) * row_bytes + static_cast<int64_t>(r) * cb + off % cb, v[i]);
+      }
+    }
+  }
+  if (t == 0) gens[b] = gen;
+}
+
+int custom_allgather_lastdim(const void* in, void* out, int64_t rows, int64_t cb, int64_t slot_bytes,
+                             const uintptr_t* data_ptrs, const uintptr_t* sig_ptrs, int rank, int world,
+                             uint32_t* gens, uint32_t* err, hipStream_t st) {
+  if (world < 2 || world > CAR_MAX_RANKS || rank < 0 || rank >= world) return 1;
+  const int64_t nbytes = rows * cb;
+  if (rows <= 0 || cb <= 0 || cb % 16 || nbytes > slot_bytes || nbytes >= (int64_t{1} << 31)) return 1;
+  CarPtrs p{};
+  for (int r = 0; r < world; ++r) {
+    p.data[r] = reinterpret_cast<uint8_t*>(data_ptrs[r]);
+    p.sig[r] = reinterpret_cast<uint32_t*>(sig_ptrs[r]);
+  }
+  const int64_t chunks = (nbytes + CAR_CHUNK - 1) / CAR_CHUNK;
+  const int blocks = static_cast<int>(chunks < CAR_MAX_BLOCKS ? chunks : CAR_MAX_BLOCKS);
+  hipLaunchKernelGGL(car_gather_kernel, dim3(blocks), dim3(CAR_THREADS), 0, st, static_cast<const uint8_t*>(in),
+                     static_cast<uint8_t*>(out), static_cast<uint32_t>(nbytes), static_cast<uint32_t>(cb), slot_bytes,
+                     p, rank, world, gens, err);
+  return 0;
 }
 
 int car_max_blocks() { return CAR_MAX_BLOCKS; }
@@ -201,7 +410,8 @@ int car_max_ranks() { return CAR_MAX_RANKS; }
 
 // bf16 only (the activation dtype of every TP model here); nbytes % 16 == 0.
 int custom_allreduce(const void* in, void* out, int64_t nbytes, int64_t slot_bytes, const uintptr_t* data_ptrs,
-                     const uintptr_t* sig_ptrs, int rank, int world, uint32_t* gens, hipStream_t st) {
+                     const uintptr_t* sig_ptrs, int rank, int world, uint32_t* gens, uint32_t* err,
+                     hipStream_t st) {
   if (world < 2 || world > CAR_MAX_RANKS || rank < 0 || rank >= world) return 1;
   if (nbytes <= 0 || nbytes % 16 || nbytes > slot_bytes) return 1;
   const int64_t blocks = (nbytes + CAR_CHUNK - 1) / CAR_CHUNK;
@@ -213,18 +423,19 @@ int custom_allreduce(const void* in, void* out, int64_t nbytes, int64_t slot_byt
   }
   hipLaunchKernelGGL(car_kernel<uint16_t>, dim3(static_cast<unsigned>(blocks)), dim3(CAR_THREADS), 0, st,
                      static_cast<const uint8_t*>(in), static_cast<uint8_t*>(out), nbytes, slot_bytes, p, rank, world,
-                     gens);
+                     gens, err);
   return 0;
 }
 
 // Two-shot: the signal arrays passed here hold 2 phases x [CAR_MAX_RANKS][CAR_MAX_BLOCKS].
 int custom_allreduce_2shot(const void* in, void* out, int64_t nbytes, int64_t slot_bytes, const uintptr_t* data_ptrs,
-                           const uintptr_t* sig_ptrs, int rank, int world, uint32_t* gens, hipStream_t st) {
+                           const uintptr_t* sig_ptrs, int rank, int world, uint32_t* gens, uint32_t* err,
+                     hipStream_t st) {
   if (world < 2 || world > CAR_MAX_RANKS || rank < 0 || rank >= world) return 1;
   if (nbytes <= 0 || nbytes % 16 || nbytes > slot_bytes) return 1;
   const int64_t shard = ((nbytes + world - 1) / world + 15) / 16 * 16;
   const int64_t blocks = (shard + CAR_CHUNK - 1) / CAR_CHUNK;
-  if (blocks > CAR_MAX_BLOCKS) return 1;
+  if (blocks > CAR_MAX_BLOCKS || blocks * world * CAR_CHUNK > slot_bytes) return 1;
   CarPtrs p{};
   for (int r = 0; r < world; ++r) {
     p.data[r] = reinterpret_cast<uint8_t*>(data_ptrs[r]);
@@ -232,7 +443,7 @@ int custom_allreduce_2shot(const void* in, void* out, int64_t nbytes, int64_t sl
   }
   hipLaunchKernelGGL(car2_kernel<uint16_t>, dim3(static_cast<unsigned>(blocks)), dim3(CAR_THREADS), 0, st,
                      static_cast<const uint8_t*>(in), static_cast<uint8_t*>(out), nbytes, shard, slot_bytes, p, rank,
-                     world, gens);
+                     world, gens, err);
   return 0;
 }
 

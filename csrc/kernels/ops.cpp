@@ -56,9 +56,13 @@ int moe_route(const uint16_t*, const uint16_t*, int, int, int, int, int, float*,
 int moe_gemm_m64(const uint16_t*, const int32_t*, const int32_t*, int, int, const uint16_t*, int, int, float*,
                  uint16_t*, int, int, int, hipStream_t);
 int custom_allreduce(const void*, void*, int64_t, int64_t, const uintptr_t*, const uintptr_t*, int, int, uint32_t*,
-                     hipStream_t);
+                     uint32_t*, hipStream_t);
 int custom_allreduce_2shot(const void*, void*, int64_t, int64_t, const uintptr_t*, const uintptr_t*, int, int,
-                           uint32_t*, hipStream_t);
+                           uint32_t*, uint32_t*, hipStream_t);
+int custom_allreduce_resid(const float*, int, int, uint16_t*, float*, int, int64_t, const uintptr_t*,
+                           const uintptr_t*, int, int, uint32_t*, uint32_t*, hipStream_t);
+int custom_allgather_lastdim(const void*, void*, int64_t, int64_t, int64_t, const uintptr_t*, const uintptr_t*, int,
+                             int, uint32_t*, uint32_t*, hipStream_t);
 int car_max_blocks();
 int car_chunk();
 int car_max_ranks();
@@ -312,19 +316,42 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("car_free", [](uintptr_t p) { return xgk::car_free(reinterpret_cast<void*>(p)) == 0; });
   m.def("custom_allreduce", [](uintptr_t in, uintptr_t out, int64_t nbytes, int64_t slot_bytes,
                                std::vector<uintptr_t> data, std::vector<uintptr_t> sig, int rank, uintptr_t gens,
-                               uintptr_t st) {
+                               uintptr_t err, uintptr_t st) {
     if (data.size() != sig.size()) throw std::invalid_argument("custom_allreduce: pointer lists differ in size");
     check(xgk::custom_allreduce(P<void>(in), P<void>(out), nbytes, slot_bytes, data.data(), sig.data(), rank,
-                                static_cast<int>(data.size()), P<uint32_t>(gens), S(st)),
+                                static_cast<int>(data.size()), P<uint32_t>(gens), P<uint32_t>(err), S(st)),
           "custom_allreduce");
   });
   m.def("custom_allreduce_2shot", [](uintptr_t in, uintptr_t out, int64_t nbytes, int64_t slot_bytes,
                                      std::vector<uintptr_t> data, std::vector<uintptr_t> sig, int rank,
-                                     uintptr_t gens, uintptr_t st) {
+                                     uintptr_t gens, uintptr_t err, uintptr_t st) {
     if (data.size() != sig.size()) throw std::invalid_argument("custom_allreduce_2shot: pointer lists differ");
     check(xgk::custom_allreduce_2shot(P<void>(in), P<void>(out), nbytes, slot_bytes, data.data(), sig.data(), rank,
-                                      static_cast<int>(data.size()), P<uint32_t>(gens), S(st)),
+                                      static_cast<int>(data.size()), P<uint32_t>(gens), P<uint32_t>(err), S(st)),
           "custom_allreduce_2shot");
+  });
+  m.def("custom_allreduce_resid", [](uintptr_t part, int S_, int T, uintptr_t resid, uintptr_t ss_part, int H,
+                                     int64_t slot_bytes, std::vector<uintptr_t> data, std::vector<uintptr_t> sig,
+                                     int rank, uintptr_t gens, uintptr_t err, uintptr_t st) {
+    if (data.size() != sig.size()) throw std::invalid_argument("custom_allreduce_resid: pointer lists differ");
+    if (T < 1 || S_ < 1 || H % 1024 || static_cast<int64_t>(T) * (H / 1024) > xgk::car_max_blocks() ||
+        static_cast<int64_t>(T) * H * 2 > slot_bytes)
+      throw std::invalid_argument("custom_allreduce_resid: T * H/1024 must fit the block table and T * H * 2 the slot");
+    check(xgk::custom_allreduce_resid(P<const float>(part), S_, T, P<uint16_t>(resid), P<float>(ss_part), H,
+                                      slot_bytes, data.data(), sig.data(), rank, static_cast<int>(data.size()),
+                                      P<uint32_t>(gens), P<uint32_t>(err), S(st)),
+          "custom_allreduce_resid");
+  });
+  m.def("custom_allgather_lastdim", [](uintptr_t in, uintptr_t out, int64_t rows, int64_t cb, int64_t slot_bytes,
+                                       std::vector<uintptr_t> data, std::vector<uintptr_t> sig, int rank,
+                                       uintptr_t gens, uintptr_t err, uintptr_t st) {
+    if (data.size() != sig.size()) throw std::invalid_argument("custom_allgather_lastdim: pointer lists differ");
+    if (rows < 1 || cb < 16 || cb % 16 || rows * cb > slot_bytes)
+      throw std::invalid_argument("custom_allgather_lastdim: row bytes must be a multiple of 16 and fit the slot");
+    check(xgk::custom_allgather_lastdim(P<const void>(in), P<void>(out), rows, cb, slot_bytes, data.data(),
+                                        sig.data(), rank, static_cast<int>(data.size()), P<uint32_t>(gens),
+                                        P<uint32_t>(err), S(st)),
+          "custom_allgather_lastdim");
   });
 
   m.def("gemm_m64", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,

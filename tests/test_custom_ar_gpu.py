@@ -16,7 +16,10 @@ def _port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q, two_shot_min=None):
+SIZES = (8, 512, 4096, 8192, 24584, 65536, 1 << 20, 2 << 20, 6 << 20)
+
+
+def _worker(rank, world, port, q, two_shot_min=None, sizes=SIZES):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
     import torch.distributed as dist
     try:
@@ -25,7 +28,7 @@ def _worker(rank, world, port, q, two_shot_min=None):
         from xgserve.parallel.custom_ar import CustomAllReduce
         ar = CustomAllReduce(rank, world, torch.device("cuda:0"), two_shot_min=two_shot_min)
         errs = []
-        for n in (8, 512, 4096, 8192, 24584, 65536, 1 << 20, 2 << 20, 6 << 20):  # elements (bf16)
+        for n in sizes:  # elements (bf16)
             for it in range(3):
                 g = torch.Generator().manual_seed(1000 * it + n)
                 xs = [torch.randn(n, generator=g).bfloat16() for _ in range(world)]
@@ -61,15 +64,31 @@ def _worker(rank, world, port, q, two_shot_min=None):
         q.put((rank, [repr(e)], -1))
 
 
-@pytest.mark.parametrize("world,two_shot_min", [(2, None), (2, 0), (4, None), (4, 0)])
-def test_custom_allreduce_one_gpu(world, two_shot_min):
-    """world ranks share the GPU; two_shot_min=0 forces the two-shot kernel for
-    every size, None is the production choice (one-shot small, two-shot large at 4 ranks)."""
+def _run(target, world, *args):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, two_shot_min)) for r in range(world)]
+    ps = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in ps]
+    for p in ps:
+        p.join(60)
+    return res
+
+
+@pytest.mark.parametrize("world,two_shot_min", [(2, None), (2, 0), (4, None), (4, 0), (8, None), (8, 0)])
+def test_custom_allreduce_one_gpu(world, two_shot_min):
+    """world ranks share the GPU; two_shot_min=0 forces the two-shot kernel for
+    every size, None is the production choice (one-shot small, two-shot large at 4 ranks).
+    world=8 is the Llama-3-70B TP8 group's protocol (8 peers, 7 remote slots per block)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    sizes = SIZES if world < 8 else SIZES[:7]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, two_shot_min, sizes)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=240) for _ in ps]
@@ -78,3 +97,91 @@ def test_custom_allreduce_one_gpu(world, two_shot_min):
     for rank, errs, tmo in res:
         assert errs == [], (rank, errs)
         assert tmo == 0
+
+
+def _resid_worker(rank, world, port, q):
+    """custom_allreduce_resid against an fp32 loop reference with the kernel's
+    summation order: local split-K slices in order, bf16 contribution per rank,
+    rank-order sum, + residual, one bf16 rounding."""
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    import torch.distributed as dist
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from xgserve.parallel.custom_ar import CustomAllReduce
+        ar = CustomAllReduce(rank, world, torch.device("cuda:0"))
+        errs = []
+        for (S, T, H) in ((4, 1, 4096), (8, 16, 8192), (2, 64, 8192), (1, 3, 1024), (3, 64, 4096)):
+            for it in range(2):
+                g = torch.Generator().manual_seed(7 * it + 131 * T + H + S)
+                parts = [torch.randn(S, T, H, generator=g) for _ in range(world)]
+                resid0 = torch.randn(T, H, generator=g).bfloat16()
+                contrib = []
+                for r in range(world):
+                    a = torch.zeros(T, H)
+                    for s_ in range(S):
+                        a = a + parts[r][s_]
+                    contrib.append(a.bfloat16().float())
+                tot = torch.zeros(T, H)
+                for r in range(world):
+                    tot = tot + contrib[r]
+                want = (resid0.float() + tot).bfloat16()
+                want_ss = want.float().view(T, H // 1024, 1024).pow(2).sum(-1).t().contiguous()  # [chunk, T]
+                resid = resid0.cuda()
+                ss = torch.full((H // 1024 * T,), -1.0, device="cuda:0")
+                ar.all_reduce_resid(parts[rank].cuda(), resid, ss)
+                torch.cuda.synchronize()
+                if not torch.equal(resid.cpu(), want):
+                    errs.append(("resid", S, T, H, it, float((resid.cpu().float() - want.float()).abs().max())))
+                if not torch.allclose(ss.cpu().view(H // 1024, T), want_ss, rtol=1e-4, atol=1e-2):
+                    errs.append(("ss", S, T, H, it))
+        ar.poll_async()
+        torch.cuda.synchronize()
+        ar.check()
+        q.put((rank, errs, ar.timeouts()))
+        ar.close()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, [repr(e)], -1))
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_custom_allreduce_resid_one_gpu(world):
+    for rank, errs, tmo in _run(_resid_worker, world):
+        assert errs == [], (rank, errs)
+        assert tmo == 0
+
+
+def _timeout_worker(rank, world, port, q):
+    """Rank 1 skips the collective: rank 0's kernel must give up, count the timeout,
+    and check() must raise -- never return the stale sum silently."""
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    import torch.distributed as dist
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from xgserve.parallel.custom_ar import CustomAllReduce, CustomAllReduceTimeout
+        ar = CustomAllReduce(rank, world, torch.device("cuda:0"))
+        raised = None
+        if rank == 0:
+            x = torch.ones(1024, dtype=torch.bfloat16, device="cuda:0")
+            ar.all_reduce(x, out=torch.empty_like(x))
+            ar.poll_async()
+            torch.cuda.synchronize()
+            try:
+                ar.check()
+                raised = False
+            except CustomAllReduceTimeout:
+                raised = True
+        dist.barrier()
+        q.put((rank, raised, ar.timeouts()))
+        ar.close()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), -1))
+
+
+def test_custom_allreduce_timeout_is_fatal():
+    res = dict((r, (raised, n)) for r, raised, n in _run(_timeout_worker, 2))
+    assert res[0][0] is True and res[0][1] >= 1, res
+    assert res[1][1] == 0, res

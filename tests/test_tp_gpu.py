@@ -36,9 +36,10 @@ def _cfg(model):
     return replace(get_config("mixtral-8x7b"), num_layers=2, intermediate_size=1792, name="tp-test")
 
 
-def _rank_main(rank, world, port, ck, moe_comm, q):
+def _rank_main(rank, world, port, ck, moe_comm, q, env=None):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
+    os.environ.update(env or {})
     try:
         from xgserve.engine import EngineConfig, LLMEngine, SamplingParams
         from xgserve.parallel.state import destroy_distributed, init_distributed
@@ -50,7 +51,9 @@ def _rank_main(rank, world, port, ck, moe_comm, q):
         if rank == 0:
             outs = eng.generate(PROMPTS, SamplingParams(max_tokens=N_GEN, temperature=0.0, ignore_eos=True))
             eng.stop_followers()
-            q.put(("ok", outs, eng.custom_ar is not None))
+            mode = {"custom_ar": eng.custom_ar is not None, "graphs": bool(eng.runner.graphs), "async": eng._async,
+                    "fused": eng.model._fused_ok}
+            q.put(("ok", outs, mode))
         else:
             eng.follower_loop()
         torch.cuda.synchronize()
@@ -61,11 +64,20 @@ def _rank_main(rank, world, port, ck, moe_comm, q):
         raise
 
 
-@pytest.mark.parametrize("model,moe_comm", [("llama", "alltoall"), ("mixtral", "alltoall"),
-                                            ("mixtral", "allreduce")])
-def test_tp2_on_one_gpu_matches_fp32_reference(tmp_path, model, moe_comm):
-    """Llama: TP=2 attention + MLP shards. Mixtral: TP=2 attention, EP=2 experts
-    (4 + 4) exchanged by fixed-capacity all-to-all or combined by all-reduce."""
+_UNFUSED = {"XGS_FUSED_DECODE": "0", "XGS_ASYNC_SCHED": "0"}
+
+
+@pytest.mark.parametrize("model,moe_comm,world,env", [
+    ("llama", "alltoall", 2, None), ("llama", "alltoall", 2, _UNFUSED), ("llama", "alltoall", 4, None),
+    ("mixtral", "alltoall", 2, None), ("mixtral", "allreduce", 2, None)])
+def test_tp2_on_one_gpu_matches_fp32_reference(tmp_path, model, moe_comm, world, env):
+    """Llama: TP attention + MLP shards; by default the fused TP decode layer (one
+    custom all-reduce launch per row-parallel projection reduces the split-K
+    partials, sums across ranks, adds the residual and emits the next norm's
+    statistics), IPC LM-head gather, HIP graphs and asynchronous scheduling with
+    the followers substituting their own sampled tokens; _UNFUSED is the eager
+    unfused chain. Mixtral: TP=2 attention, EP=2 experts (4 + 4) exchanged by
+    fixed-capacity all-to-all or combined by all-reduce."""
     from xgserve.models import build_model, save_checkpoint
     from xgserve.models.reference import reference_logits
     from xgserve.ops import _native
@@ -78,11 +90,11 @@ def test_tp2_on_one_gpu_matches_fp32_reference(tmp_path, model, moe_comm):
     ctx = torch.multiprocessing.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, ck, moe_comm, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, ck, moe_comm, q, env)) for r in range(world)]
     for p in procs:
         p.start()
     try:
-        kind, outs, used_custom_ar = q.get(timeout=100)
+        kind, outs, mode = q.get(timeout=150)
     finally:
         for p in procs:
             p.join(timeout=30)
@@ -90,7 +102,9 @@ def test_tp2_on_one_gpu_matches_fp32_reference(tmp_path, model, moe_comm):
                 p.kill()
     assert kind == "ok", outs
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    assert used_custom_ar  # decode all-reduces on the IPC one-shot kernel
+    assert mode["custom_ar"], mode  # decode all-reduces on the IPC kernels
+    if model == "llama" and env is None:
+        assert mode["graphs"] and mode["async"] and mode["fused"], mode
 
     base = None
     if model == "mixtral":

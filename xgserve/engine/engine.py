@@ -80,7 +80,9 @@ class EngineConfig:
     # asynchronous scheduling: plan + launch step N+1 (its decode ids substituted on
     # the GPU from step N's sampled tokens) before step N's tokens reach the host,
     # so the host's per-step work (commit, schedule, metadata, launch) overlaps the
-    # GPU instead of sitting between steps. TP=1, no speculation, graph decode steps.
+    # GPU instead of sitting between steps. No speculation, graph decode steps; under
+    # TP the followers get (plan, sampling rows, src) per launch and sample the same
+    # tokens from the same all-gathered logits, so their substitutions agree.
     async_schedule: bool = True
     # "fp8": weight-only E4M3 copies for batch <= 16 decode (bf16 activations)
     weight_dtype: Optional[str] = None
@@ -132,12 +134,19 @@ class LLMEngine:
         # decode graphs capture the TP collectives: RCCL (and the IPC all-reduce) can be
         # captured into a HIP graph, gloo (CPU-staged) cannot -> eager decode there
         use_graphs = cfg.use_graphs and (st.tp_size == 1 or st.backend == "nccl")
+        graph_bs = cfg.graph_batch_sizes
+        if cfg.use_graphs and not use_graphs and self.custom_ar is not None and not self.mcfg.num_experts:
+            # gloo CPU group but a dense model whose decode collectives (fused residual
+            # all-reduce, LM-head gather) all run on the IPC kernels: capturable as long
+            # as every captured batch stays on them (<= 64 tokens)
+            use_graphs = True
+            graph_bs = [b for b in (graph_bs or [1, 2, 4, 8, 16, 24, 32, 48, 64]) if b <= 64]
         if cfg.use_graphs and not use_graphs:
             log.info("TP over %s: decode graphs disabled (collectives not capturable)", st.backend)
         self.runner = ModelRunner(self.model, block_size=cfg.block_size, num_blocks=num_blocks,
                                   max_num_seqs=cfg.max_num_seqs, max_num_batched_tokens=cfg.max_num_batched_tokens,
                                   max_model_len=self.max_model_len, use_graphs=use_graphs,
-                                  graph_batch_sizes=cfg.graph_batch_sizes, is_driver=self.is_driver)
+                                  graph_batch_sizes=graph_bs, is_driver=self.is_driver)
         self.runner.capture_graphs()
         H = self.mcfg.hidden_size
         self.embed_acc = torch.zeros(cfg.max_num_seqs, H, dtype=torch.float32, device=self.device)
@@ -168,8 +177,7 @@ class LLMEngine:
                                            cfg.spec_min_acceptance_rate)
         self._inflight = None  # (plan, handle): launched by the previous step() (async scheduling)
         self._async = (cfg.async_schedule and os.environ.get("XGS_ASYNC_SCHED", "1") != "0"
-                       and self.device.type == "cuda" and get_state().tp_size == 1 and self.spec is None
-                       and bool(self.runner.graphs))
+                       and self.device.type == "cuda" and self.spec is None and bool(self.runner.graphs))
         log.info("engine ready: model=%s tp=%d blocks=%d (%.1f GiB KV) load=%.1fs", self.mcfg.name, get_state().tp_size,
                  num_blocks, self.runner.kv_bytes() / 2**30, self.load_time)
 
@@ -357,6 +365,12 @@ class LLMEngine:
             raise RuntimeError("async scheduling: placeholder without a producing row")
         return np.where(need, j, -1).astype(np.int32)
 
+    def _launch(self, plan, samp, src=None):
+        """runner.launch on every TP rank: followers receive the same launch."""
+        if get_state().tp_size > 1:
+            comm.tp_broadcast_object(("launch", (plan, samp, src)), src=0)
+        return self.runner.launch(plan, samp, src=src)
+
     def _step_async(self) -> List[RequestOutput]:
         """One step of the pipelined loop: retire the step launched by the previous
         call (or launch one now), but first plan and launch its successor when it is
@@ -377,7 +391,7 @@ class LLMEngine:
             self._bind_slots(plan)
             samp = self._sampling_rows(plan)
             t = self._tick("prepare", t)
-            handle = self.runner.launch(plan, samp)
+            handle = self._launch(plan, samp)
             t = self._tick("launch", t)
         else:
             plan, handle = cur
@@ -394,7 +408,7 @@ class LLMEngine:
                     self._bind_slots(nplan)
                     nsamp = self._sampling_rows(nplan)
                     src = self._lookahead_src(plan, nplan)
-                    self._inflight = (nplan, self.runner.launch(nplan, nsamp, src=src))
+                    self._inflight = (nplan, self._launch(nplan, nsamp, src=src))
                 t = self._tick("launch", t)
         outs += self._flush_deferred()  # previous step's outputs, while the GPU runs
         t = self._tick("emit_overlapped", t)
@@ -592,15 +606,31 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ followers (TP > 1)
     def follower_loop(self):
-        """Non-leader TP ranks: mirror the leader's steps until told to stop."""
+        """Non-leader TP ranks: mirror the leader's steps until told to stop.
+        "plan" (synchronous steps): run it to completion. "launch" (asynchronous
+        scheduling): enqueue it, then wait for the PREVIOUS launch only, so the
+        next step is already queued behind the running one, as on the leader."""
+        prev = None
         while True:
             kind, payload = comm.tp_broadcast_object(None, src=0)
             if kind == "stop":
+                if prev is not None:
+                    self.runner.wait(prev)
                 return
             if kind == "plan":
+                if prev is not None:
+                    self.runner.wait(prev)
+                    prev = None
                 plan = payload
                 if plan["num_tokens"]:
                     self.runner.execute(plan, None)
+            elif kind == "launch":
+                plan, samp, src = payload
+                if plan["num_tokens"]:
+                    h = self.runner.launch(plan, samp, src=src)
+                    if prev is not None:
+                        self.runner.wait(prev)
+                    prev = h
 
     def stop_followers(self):
         if get_state().tp_size > 1 and self.is_driver:

@@ -24,6 +24,7 @@ import torch
 from .. import ops
 from ..models.base import AttnMeta
 from ..ops.attention import DecodeWorkspace
+from ..parallel import comm
 
 log = logging.getLogger("xgserve.runner")
 
@@ -221,8 +222,23 @@ class ModelRunner:
         """True if the step wrote its sampled tokens to g_out_tok (a graph step)."""
         return len(handle) > 4 and handle[4]
 
+    @staticmethod
+    def _poll_comm():
+        """Queue the custom all-reduce's error-counter copy behind this step's work
+        (TP): wait() then fails the step if a peer wait timed out."""
+        ar = comm.custom_allreduce()
+        if ar is not None:
+            ar.poll_async()
+
+    @staticmethod
+    def _check_comm():
+        ar = comm.custom_allreduce()
+        if ar is not None:
+            ar.check()
+
     def _record_out(self, n: int, tok: torch.Tensor, lp: torch.Tensor, hidden, graph: bool):
         """Tokens / logprobs D2H into the next of the two pinned buffers + an event."""
+        self._poll_comm()
         i = self.out_idx
         self.out_idx ^= 1
         self.h_toks[i][:n].copy_(tok[:n], non_blocking=True)
@@ -236,10 +252,16 @@ class ModelRunner:
         if ready is not None:
             return ready
         if out is None:
-            torch.cuda.current_stream().synchronize()
+            ev = handle[5] if len(handle) > 5 else None
+            if ev is not None:
+                ev.synchronize()  # this step only (TP follower with a successor queued)
+            else:
+                torch.cuda.current_stream().synchronize()
+            self._check_comm()
             return None, None, hidden
         i, ev = out
         ev.synchronize()  # this step only: a step queued behind it keeps running
+        self._check_comm()
         return self.h_toks[i][:n].numpy().copy(), self.h_lps[i][:n].numpy().copy(), hidden
 
     def _execute_graph(self, plan, samp: Optional[SamplingRows], n: int, bs: int, src: Optional[np.ndarray]):
@@ -285,7 +307,10 @@ class ModelRunner:
         self.graphs[(bs, greedy)].replay()
         if not self.is_driver:
             # no D2H to wait on; wait() still drains before the pinned inputs get rewritten
-            return (n, None, None, None, True)
+            self._poll_comm()
+            ev = torch.cuda.Event()
+            ev.record()
+            return (n, None, None, None, True, ev)
         return self._record_out(n, self.g_out_tok, self.g_out_lp, None, True)
 
     def _execute_eager(self, plan, samp: Optional[SamplingRows], need_hidden: bool, src: Optional[np.ndarray]):
@@ -344,7 +369,10 @@ class ModelRunner:
         if self.capture_logits:
             self.last_logits = logits.float().cpu()
         if not self.is_driver:
-            return (S, hid, None, None) if self.is_cuda else (S, hid, (None, None, hid), None)
+            if self.is_cuda:
+                self._poll_comm()
+                return (S, hid, None, None)
+            return (S, hid, (None, None, hid), None)
         if samp is None or samp.all_greedy:
             tok, lp = ops.argmax_logprob(logits)
         else:

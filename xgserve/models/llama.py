@@ -44,8 +44,11 @@ FAST_M_SLAB = 64    # tokens per step for the O-projection slab kernel
 # RMSNorms become GEMM epilogue row scales (norm weights folded into W), the
 # residual adds + norm statistics run inside the O / down GEMM launches and the
 # QKV reduce + RoPE + KV append inside the attention prologue: 4 GEMM launches +
-# 1 attention launch per layer instead of 9. XGS_FUSED_DECODE=0 restores the
-# unfused chain (A/B measurements, tests).
+# 1 attention launch per layer instead of 9. Under TP the O / down GEMMs emit
+# split-K partials and ONE custom all-reduce launch per projection reduces them,
+# sums across ranks over xGMI, adds the residual and writes the next norm's
+# statistics (comm.tp_allreduce_resid): 6 launches + attention per layer instead
+# of 11. XGS_FUSED_DECODE=0 restores the unfused chain (A/B measurements, tests).
 FUSED_DECODE = os.environ.get("XGS_FUSED_DECODE", "1") != "0"
 # TP > 1 prefill-sized steps: the row-parallel all-reduces are pipelined over this
 # many token chunks and overlapped with the next chunk's GEMMs (RCCL stream); a
@@ -301,9 +304,24 @@ class LlamaLayer(nn.Module):
         eps = self.cfg.norm_eps
         pqkv = m64_norm_linear(resid, self.qkv, MODE_PARTIAL, stats, eps)
         a = self.attn.fused_decode(pqkv, meta, kv, cos_sin, prefetch=self.o)
+        if self.tp > 1:
+            return self._fused_tp_tail(a, resid, ws, site)
         st = m64_resid_linear(a, self.o, resid, ws, site, eps)
         act = m64_norm_linear(resid, self.gate_up, MODE_SILU, st, eps)
         return m64_resid_linear(act, self.down, resid, ws, site + 1, eps)
+
+    def _fused_tp_tail(self, a: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace, site: int) -> RowStats:
+        """Row-parallel half of the fused decode layer under TP: O GEMM partials ->
+        all-reduce + residual + statistics (one launch) -> gate_up (norm row scale,
+        SiLU-gate) -> down GEMM partials -> all-reduce + residual + statistics."""
+        T, H = resid.shape
+        po = m64_linear(a, self.o, MODE_PARTIAL)
+        comm.tp_allreduce_resid(po.part, resid, ws.ss[site])
+        st = RowStats(ws.ss[site], H // 1024, T)
+        act = m64_norm_linear(resid, self.gate_up, MODE_SILU, st, self.cfg.norm_eps)
+        pd = m64_linear(act, self.down, MODE_PARTIAL)
+        comm.tp_allreduce_resid(pd.part, resid, ws.ss[site + 1])
+        return RowStats(ws.ss[site + 1], H // 1024, T)
 
 
 class LlamaForCausalLM(nn.Module):
@@ -330,7 +348,7 @@ class LlamaForCausalLM(nn.Module):
         l0 = self.layers[0]
         self.norms_folded = False
         self.weight_dtype = "bf16"
-        self._fused_ok = (self.tp == 1 and self.device.type == "cuda" and not l0.moe and l0.m64_ok
+        self._fused_ok = (self.device.type == "cuda" and not l0.moe and l0.m64_ok
                           and l0.m64_silu_ok and cfg.head_dim == 128 and l0.Hq % l0.Hkv == 0
                           and l0.Hq // l0.Hkv in (1, 2, 4, 8) and H % 1024 == 0 and H // 1024 <= 8)
         self._fused_small_ok = self._fused_ok and l0.m64_small_ok
@@ -379,6 +397,8 @@ class LlamaForCausalLM(nn.Module):
     def fused_decode_ok(self, meta: AttnMeta) -> bool:
         T = meta.num_tokens
         if not (FUSED_DECODE and self._fused_ok and self.norms_folded) or T != meta.num_decodes or not 0 < T <= 64:
+            return False
+        if self.tp > 1 and not comm.resid_allreduce_ok(T, self.cfg.hidden_size):
             return False
         return T > FAST_M_SMALL or self._fused_small_ok
 

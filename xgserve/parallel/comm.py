@@ -42,6 +42,31 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+def resid_allreduce_ok(T: int, H: int) -> bool:
+    """Can `tp_allreduce_resid` take a [T, H] message in one launch? True with the
+    custom all-reduce registered, and for a simulated TP shard (a model built
+    with tp > 1 in a single-rank process: the collective is a local reduction)."""
+    s = get_state()
+    if s.tp_size == 1:
+        return True
+    return _CUSTOM_AR is not None and _CUSTOM_AR.can_resid(T, H)
+
+
+def tp_allreduce_resid(part: torch.Tensor, resid: torch.Tensor, ss: torch.Tensor) -> None:
+    """Row-parallel projection epilogue of the fused decode layer:
+    resid += all-reduce(sum_s part[s]) in place (bf16), ss[chunk * T + t] <- the new
+    residual's sum of squares per 1024 columns. `part` is this rank's fp32 split-K
+    partials [S, T, H]. One launch on the custom all-reduce; a simulated TP shard
+    (single-rank process) reduces locally."""
+    from ..ops._native import kernels, stream_ptr
+    S, T, H = part.shape
+    s = get_state()
+    if s.tp_size == 1:
+        kernels().add_partials_resid(part.data_ptr(), S, T, resid.data_ptr(), ss.data_ptr(), H, stream_ptr())
+        return
+    _CUSTOM_AR.all_reduce_resid(part, resid, ss)
+
+
 class _Done:
     def wait(self):
         return True
@@ -65,6 +90,9 @@ def tp_all_gather_lastdim(x: torch.Tensor) -> torch.Tensor:
     if s.tp_size == 1:
         return x
     x = x.contiguous()
+    ar = _CUSTOM_AR
+    if ar is not None and ar.can_gather(x):
+        return ar.all_gather_lastdim(x)  # IPC peer reads, graph capturable
     # flat [tp*rows, ...] output (the layout every backend accepts), viewed as [tp, ...]
     out = torch.empty((s.tp_size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     dist.all_gather_into_tensor(out, x, group=s.tp_group)

@@ -12,6 +12,18 @@ Path choice, bf16 messages of 16-byte multiples:
   * two-shot (reduce-scatter + all-gather through peer memory, ~2n/W bytes per
     xGMI link) from `two_shot_min` to `two_shot_max` bytes at TP >= 4;
   * RCCL above that (comm.tp_all_reduce falls back automatically).
+
+Fused decode layer under TP: `all_reduce_resid` takes a row-parallel GEMM's
+fp32 split-K partials and, in one launch, reduces them locally, exchanges the
+bf16 contributions over IPC, adds the sum to the replicated residual stream and
+writes the new residual's RMSNorm statistics (custom_allreduce_resid). It has
+its own slots, signals and generation counters.
+
+Failure semantics: a peer that does not arrive within ~1 s makes the kernels
+bump a device error counter and give up (the GPU never hangs). After every
+step the runner copies that counter to pinned host memory behind the step's
+work (`poll_async`) and `check()` raises CustomAllReduceTimeout, so the step
+fails (and the replica restarts) instead of returning a stale sum.
 """
 from __future__ import annotations
 
@@ -26,7 +38,16 @@ from ..ops._native import kernels, stream_ptr
 log = logging.getLogger("xgserve.comm")
 
 
+class CustomAllReduceTimeout(RuntimeError):
+    """A TP peer did not reach a custom all-reduce within the kernel's wait limit."""
+
+
 class CustomAllReduce:
+    # fused residual path: T * H bf16 per rank (decode: T <= 64, H <= 8192 -> 1 MiB)
+    RESID_SLOT = 1 << 20
+    # last-dim all-gather (vocab-parallel LM head of decode steps): T * V/W bf16 per rank
+    GATHER_SLOT = 16 << 20
+
     def __init__(self, rank: int, world: int, device: torch.device, cpu_group=None, max_bytes: int = 8 << 20,
                  two_shot_min: Optional[int] = None, two_shot_max: int = 32 << 20):
         k = kernels()
@@ -48,9 +69,11 @@ class CustomAllReduce:
         # failure anywhere disables the path everywhere instead of hanging peers
         mine = None
         try:
-            # [one-shot 2 x slot | two-shot 2 x slot2] and [one-shot | two-shot phase 0 | phase 1] signals
-            self.data = k.car_alloc_uncached(2 * self.slot + 2 * self.slot2)
-            self.sig = k.car_alloc_uncached(3 * nsig)
+            # [one-shot 2 x slot | two-shot 2 x slot2 | resid 2 x RESID_SLOT | gather 2 x GATHER_SLOT]
+            # and [one-shot | two-shot phase 0 | phase 1 | resid | gather] signals
+            self.data = k.car_alloc_uncached(2 * self.slot + 2 * self.slot2 + 2 * self.RESID_SLOT
+                                             + 2 * self.GATHER_SLOT)
+            self.sig = k.car_alloc_uncached(5 * nsig)
             mine = (k.car_ipc_handle(self.data), k.car_ipc_handle(self.sig))
         except RuntimeError as e:
             log.warning("custom all-reduce: local setup failed: %s", e)
@@ -84,13 +107,28 @@ class CustomAllReduce:
             raise RuntimeError("custom all-reduce: peer mapping failed on some rank")
         self.data_ptrs2 = [d + 2 * self.slot for d in self.data_ptrs]
         self.sig_ptrs2 = [s_ + nsig for s_ in self.sig_ptrs]
+        self.data_ptrs3 = [d + 2 * self.slot + 2 * self.slot2 for d in self.data_ptrs]
+        self.sig_ptrs3 = [s_ + 3 * nsig for s_ in self.sig_ptrs]
+        self.data_ptrs4 = [d + 2 * self.slot + 2 * self.slot2 + 2 * self.RESID_SLOT for d in self.data_ptrs]
+        self.sig_ptrs4 = [s_ + 4 * nsig for s_ in self.sig_ptrs]
+        self.chunk = chunk
         self.gens = torch.zeros(self.max_blocks + 1, dtype=torch.int32, device=device)
         self.gens2 = torch.zeros(self.max_blocks + 1, dtype=torch.int32, device=device)
+        self.gens3 = torch.zeros(self.max_blocks + 1, dtype=torch.int32, device=device)
+        self.gens4 = torch.zeros(self.max_blocks + 1, dtype=torch.int32, device=device)
+        # peer-wait timeouts of every path (device), mirrored to pinned host memory
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.h_err = torch.zeros(1, dtype=torch.int32).pin_memory()
         log.info("custom all-reduce ready: rank %d/%d, one-shot <= %d KiB, two-shot <= %d MiB", rank, world,
                  min(self.slot, self.two_shot_min) >> 10, self.slot2 >> 20)
 
     def _two_shot(self, n: int) -> bool:
-        return self.two_shot_min <= n <= self.slot2
+        if not self.two_shot_min <= n <= self.slot2:
+            return False
+        # slot layout [block][rank shard][chunk]: the padded shards must fit the slot
+        shard = (-(-n // self.world) + 15) // 16 * 16
+        blocks = -(-shard // self.chunk)
+        return blocks <= self.max_blocks and blocks * self.world * self.chunk <= self.slot2
 
     def can_run(self, x: torch.Tensor) -> bool:
         n = x.numel() * x.element_size()
@@ -102,15 +140,57 @@ class CustomAllReduce:
         n = x.numel() * x.element_size()
         if self._two_shot(n):
             self._k.custom_allreduce_2shot(x.data_ptr(), out.data_ptr(), n, self.slot2, self.data_ptrs2,
-                                           self.sig_ptrs2, self.rank, self.gens2.data_ptr(), stream_ptr())
+                                           self.sig_ptrs2, self.rank, self.gens2.data_ptr(), self.err.data_ptr(),
+                                           stream_ptr())
         else:
             self._k.custom_allreduce(x.data_ptr(), out.data_ptr(), n, self.slot, self.data_ptrs, self.sig_ptrs,
-                                     self.rank, self.gens.data_ptr(), stream_ptr())
+                                     self.rank, self.gens.data_ptr(), self.err.data_ptr(), stream_ptr())
+        return out
+
+    def can_resid(self, T: int, H: int) -> bool:
+        return 1 <= T and H % 1024 == 0 and T * (H // 1024) <= self.max_blocks and T * H * 2 <= self.RESID_SLOT
+
+    def all_reduce_resid(self, part: torch.Tensor, resid: torch.Tensor, ss: torch.Tensor) -> None:
+        """resid (bf16 [T, H], replicated) += sum over ranks of sum_s part[s] (this
+        rank's fp32 split-K partials [S, T, H]); ss[chunk * T + t] <- the new
+        residual's sum of squares per 1024-column chunk. One launch."""
+        S, T, H = part.shape
+        if not (part.is_contiguous() and part.dtype == torch.float32 and resid.is_contiguous()
+                and tuple(resid.shape) == (T, H) and resid.dtype == torch.bfloat16 and ss.numel() >= T * (H // 1024)):
+            raise ValueError(f"all_reduce_resid: bad operands part={tuple(part.shape)} resid={tuple(resid.shape)}")
+        self._k.custom_allreduce_resid(part.data_ptr(), S, T, resid.data_ptr(), ss.data_ptr(), H, self.RESID_SLOT,
+                                       self.data_ptrs3, self.sig_ptrs3, self.rank, self.gens3.data_ptr(),
+                                       self.err.data_ptr(), stream_ptr())
+
+    def can_gather(self, x: torch.Tensor) -> bool:
+        cb = x.shape[-1] * x.element_size()
+        return (x.is_cuda and x.dim() == 2 and x.is_contiguous() and cb % 16 == 0 and 0 < x.numel()
+                and x.numel() * x.element_size() <= self.GATHER_SLOT)
+
+    def all_gather_lastdim(self, x: torch.Tensor) -> torch.Tensor:
+        """[T, n] per rank -> [T, world * n] (rank-major columns), one launch."""
+        T, n = x.shape
+        out = torch.empty(T, self.world * n, dtype=x.dtype, device=x.device)
+        self._k.custom_allgather_lastdim(x.data_ptr(), out.data_ptr(), T, n * x.element_size(), self.GATHER_SLOT,
+                                         self.data_ptrs4, self.sig_ptrs4, self.rank, self.gens4.data_ptr(),
+                                         self.err.data_ptr(), stream_ptr())
         return out
 
     def timeouts(self) -> int:
-        """Peer-wait timeouts recorded by the kernels (0 when healthy)."""
-        return int(self.gens[self.max_blocks].item()) + int(self.gens2[self.max_blocks].item())
+        """Peer-wait timeouts recorded by the kernels (0 when healthy). Synchronises."""
+        return int(self.err.item())
+
+    def poll_async(self) -> None:
+        """Queue a copy of the error counter behind the current stream's work."""
+        self.h_err.copy_(self.err, non_blocking=True)
+
+    def check(self) -> None:
+        """Raise if any wait timed out up to the last poll_async whose stream work has
+        completed (call after synchronising on the step)."""
+        n = int(self.h_err[0])
+        if n:
+            raise CustomAllReduceTimeout(f"custom all-reduce: {n} peer wait(s) timed out on TP rank {self.rank} "
+                                         "(a peer is dead or stalled); failing the step")
 
     def close(self) -> None:
         for p in self._opened:
