@@ -40,6 +40,7 @@ class MockEngine:
         self.crash_after_steps = crash_after_steps
         self.eos_every = eos_every
         self.hang = False
+        self.fail_collective = False  # fault injection: the next step raises a TP collective timeout
         self.requests: Dict[str, EngineRequest] = {}
         self._order: List[str] = []
         self._lock = threading.Lock()
@@ -84,6 +85,9 @@ class MockEngine:
             time.sleep(0.02)
         if self.hang:
             return []
+        if self.fail_collective:
+            from ..parallel.custom_ar import CustomAllReduceTimeout
+            raise CustomAllReduceTimeout("mock: peer wait timed out (fault injection)")
         if self.step_latency_s:
             time.sleep(self.step_latency_s)
         self.steps += 1

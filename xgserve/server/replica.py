@@ -7,7 +7,10 @@ design.md:310-361) as an *engine loop* that owns one LLMEngine (a TP group).
   that raises is contained: HIP OOM -> flush the prefix cache and retry once
   (Req 9.3), then fail only the requests that were in flight with
   `out_of_memory`; any other exception fails the in-flight requests with
-  `inference_failed` (Property 22) and the loop keeps serving.
+  `inference_failed` (Property 22) and the loop keeps serving -- except a TP
+  collective timeout (CustomAllReduceTimeout: a peer died or stalled, the group
+  is out of step), which fails the in-flight requests and kills the replica so
+  the orchestrator restarts it.
 * `InProcessReplica` -- engine + loop on a thread of the server process
   (tp == 1; tests, CPU configs).
 * `ProcessReplica` -- one OS process per GPU (spawned, so HIP is initialised
@@ -133,6 +136,8 @@ class EngineLoop:
                 self.engine.clear_prefix_cache()
             elif op == "hang":  # fault injection (tests)
                 self.engine.hang = True
+            elif op == "fail_collective":  # fault injection (tests)
+                self.engine.fail_collective = True
             elif op == "stop":
                 self._stop = True
 
@@ -158,6 +163,13 @@ class EngineLoop:
                 except SystemExit:
                     raise
                 except Exception as e:  # contain the failure to the in-flight requests
+                    from ..parallel.custom_ar import CustomAllReduceTimeout
+                    if isinstance(e, CustomAllReduceTimeout):
+                        # the TP group is out of step (a peer died or stalled): fail what is in
+                        # flight, then let the replica die so the orchestrator restarts it
+                        log.error("TP collective timed out: %s", e)
+                        self.emit("out", outs + self._fail_inflight("inference_failed", f"Inference failed: {e}"))
+                        raise
                     if _is_oom(e):
                         log.warning("OOM in engine step; flushing prefix cache and retrying")
                         try:
@@ -242,6 +254,9 @@ class Replica:
 
     def inject_hang(self) -> None:
         self._send(("hang",))
+
+    def inject_collective_timeout(self) -> None:
+        self._send(("fail_collective",))
 
     def heartbeat_age(self) -> float:
         return time.monotonic() - self.last_hb
