@@ -324,6 +324,56 @@ def test_collective_timeout_fails_step_and_restarts_replica():
     assert run_with_client(cfg, fn)
 
 
+def test_runtime_add_remove_replicas_without_dropping_traffic():
+    """Req 7.5: POST /admin/replicas adds and removes replicas while requests flow;
+    every request succeeds and the new replica takes traffic."""
+    cfg = mock_config(worker={"replicas": 2, "mock_latency_ms": 2.0}, scheduler={"strategy": "round_robin"})
+
+    async def fn(c, srv):
+        stop = asyncio.Event()
+        statuses = []
+
+        async def traffic():
+            while not stop.is_set():
+                rs = await asyncio.gather(*[_gen(c, max_tokens=4) for _ in range(4)])
+                statuses.extend(r.status for r in rs)
+
+        task = asyncio.create_task(traffic())
+        await asyncio.sleep(0.1)
+        r = await c.post("/admin/replicas", data=json.dumps({"action": "add", "count": 1}))
+        d = await r.json()
+        assert r.status == 200, d
+        new_id = d["added"][0]
+        assert sorted(d["replicas"]) == [0, 1, new_id]
+        await asyncio.sleep(0.3)
+        assert srv.replicas[new_id].loop.steps > 0  # the new replica serves traffic
+        r = await c.post("/admin/replicas", data=json.dumps({"action": "remove", "ids": [0]}))
+        d = await r.json()
+        assert r.status == 200, d
+        assert sorted(d["replicas"]) == [1, new_id]
+        await asyncio.sleep(0.3)
+        stop.set()
+        await task
+        assert statuses and all(st == 200 for st in statuses), statuses
+        h = await (await c.get("/health")).json()
+        assert h["status"] == "ok" and h["replicas_total"] == 2
+        g = await (await c.get("/admin/replicas")).json()
+        assert sorted(g["routable"]) == [1, new_id]
+        # cannot remove every replica; bad ids are rejected
+        r = await c.post("/admin/replicas", data=json.dumps({"action": "remove", "ids": [1, new_id]}))
+        assert r.status == 400
+        r = await c.post("/admin/replicas", data=json.dumps({"action": "remove", "ids": [99]}))
+        assert r.status == 400
+        for _ in range(50):
+            if 0 not in srv.replicas:
+                break
+            await asyncio.sleep(0.05)
+        assert 0 not in srv.replicas  # drained and stopped
+        return True
+
+    assert run_with_client(cfg, fn)
+
+
 def test_degradation_rejects_low_priority():
     async def fn(c, srv):
         p = {"v": 0.92}

@@ -66,3 +66,31 @@ def test_stop_inside_accepted_run():
     """EOS / max_tokens inside an accepted draft run truncates exactly like plain decoding."""
     sp = SamplingParams(max_tokens=7, temperature=0.0, ignore_eos=True)
     assert _engine("llama-tiny", 4).generate(PROMPTS, sp) == _engine().generate(PROMPTS, sp)
+
+
+def test_speedup_factor_is_measured():
+    """Req 12.4: the engine times speculating steps (propose + verify) and plain
+    decode steps; speedup = tokens per speculated row-step x plain / spec step time."""
+    eng = _engine("llama-tiny", 3)
+    eng.add_request("g", PROMPTS[0], SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True))
+    eng.add_request("s", PROMPTS[1], SamplingParams(max_tokens=40, temperature=0.8, seed=3, ignore_eos=True))
+    for _ in range(300):
+        if not eng.has_work():
+            break
+        eng.step()
+    st = eng.stats()["speculative"]
+    sp = eng.spec
+    assert sp.ema_spec_ms and sp.ema_plain_ms  # both kinds of steps were seen
+    assert 1.0 < sp.ema_tokens_per_row <= 4.0
+    want = sp.ema_tokens_per_row * sp.ema_plain_ms / sp.ema_spec_ms
+    assert st["speedup_factor"] == pytest.approx(want, rel=1e-3)
+    assert st["speedup_factor"] > 0
+
+
+def test_speedup_factor_exported():
+    from xgserve.obs.metrics import MetricsCollector
+    m = MetricsCollector()
+    assert "xgs_spec_speedup_factor" not in m.prometheus()
+    m.set_spec_totals(100, 80, 1.75)
+    assert "xgs_spec_speedup_factor 1.75" in m.prometheus()
+    assert m.snapshot()["speculative"]["speedup_factor"] == 1.75

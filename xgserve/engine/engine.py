@@ -429,7 +429,7 @@ class LLMEngine:
         if self._async:
             return self._step_async()
         outs: List[RequestOutput] = []
-        t = time.perf_counter()
+        t = t_step0 = time.perf_counter()
         with self._lock:
             for rid in self._pending_aborts:
                 outs.append(RequestOutput(rid, [], "", True, "abort"))
@@ -460,6 +460,8 @@ class LLMEngine:
             t = self._tick("wait_gpu", t)
         if counts is None:
             counts = np.ones(int(plan["num_sample"]), np.int32)
+        if self.spec is not None and self.is_driver:
+            self.spec.record_step(time.perf_counter() - t_step0, plan, counts)
         return outs + self._finish_step(plan, toks, lps, hidden, counts, None, t)
 
     def _finish_step(self, plan, toks, lps, hidden, counts, fin_map, t) -> List[RequestOutput]:

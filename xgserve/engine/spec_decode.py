@@ -15,6 +15,13 @@ its single-token steps). Each engine step:
               plus the target's own token at the first mismatch (so every verify
               yields >= 1 token and the output equals plain greedy decoding).
 
+Speedup (Req 12.4, requirements.md:169) is measured, not assumed: the engine
+times every step it runs with the draft (propose + verify) and every pure-decode
+step without verify rows, and `stats()` reports
+  speedup_factor = (tokens per sequence-step when speculating / spec step time)
+                 / (1 token per sequence-step / plain decode step time)
+from exponential moving averages of both (None until both kinds were seen).
+
 Acceptance is tracked per request and globally; a request whose acceptance rate
 stays below `min_acceptance_rate` (0.5, requirements.md:170) after a few
 verifies stops speculating (its draft pages are freed). Sampled (temperature >
@@ -64,6 +71,9 @@ class SpeculativeDecoder:
         self.accepted = 0
         self.verifies = 0
         self.seqs: Dict[int, _DraftSeq] = {}
+        self.ema_spec_ms: Optional[float] = None   # step time with verify rows (propose + verify)
+        self.ema_plain_ms: Optional[float] = None  # pure-decode step time without verify rows
+        self.ema_tokens_per_row: Optional[float] = None  # tokens per speculated sequence-step
         if not self.enabled:
             return
         if isinstance(draft_model, str):
@@ -100,11 +110,40 @@ class SpeculativeDecoder:
             ds.blocks.append(self.free.pop())
         return True
 
+    EMA = 0.1
+
+    def _ema(self, old: Optional[float], x: float) -> float:
+        return x if old is None else (1 - self.EMA) * old + self.EMA * x
+
+    def record_step(self, seconds: float, plan: dict, counts: Optional[np.ndarray]) -> None:
+        """Engine hook: wall time of one step run with the draft attached."""
+        ns, nd = int(plan["num_seqs"]), int(plan["num_decodes"])
+        if ns == 0:
+            return
+        q, pre = plan["q_lens"], plan["is_prefill"]
+        verify = (q > 1) & (pre == 0)
+        if verify.any() and counts is not None:
+            nrows = int(verify.sum())
+            sidx = plan["sample_seq_index"]
+            vtoks = int(sum(int(c) for j, c in enumerate(counts.tolist()) if verify[int(sidx[j])]))
+            self.ema_spec_ms = self._ema(self.ema_spec_ms, 1000.0 * seconds)
+            self.ema_tokens_per_row = self._ema(self.ema_tokens_per_row, vtoks / nrows)
+        elif nd == ns:
+            self.ema_plain_ms = self._ema(self.ema_plain_ms, 1000.0 * seconds)
+
+    def speedup_factor(self) -> Optional[float]:
+        if self.ema_spec_ms is None or self.ema_plain_ms is None or not self.ema_spec_ms:
+            return None
+        return self.ema_tokens_per_row * self.ema_plain_ms / self.ema_spec_ms
+
     def stats(self) -> dict:
+        sf = self.speedup_factor()
         return {"draft_tokens_proposed": self.proposed, "draft_tokens_accepted": self.accepted,
                 "acceptance_rate": self.accepted / self.proposed if self.proposed else 0.0,
                 "verify_steps": self.verifies,
                 "mean_tokens_per_verify": (self.accepted + self.verifies) / self.verifies if self.verifies else 0.0,
+                "spec_step_ms": self.ema_spec_ms, "plain_decode_step_ms": self.ema_plain_ms,
+                "speedup_factor": None if sf is None else round(sf, 4),
                 "active": sum(1 for d in self.seqs.values() if not d.disabled)}
 
     # ------------------------------------------------------------------ draft steps

@@ -62,6 +62,7 @@ class MetricsCollector:
         self.workers: Dict[int, dict] = {}
         self.spec_proposed = 0
         self.spec_accepted = 0
+        self.spec_speedup: Optional[float] = None
         self._recent_lat: deque = deque(maxlen=4096)
         self._tok_events: deque = deque()  # (t, prompt, gen)
         self.rejected_total: Dict[str, int] = defaultdict(int)
@@ -140,10 +141,12 @@ class MetricsCollector:
             self.spec_proposed += proposed
             self.spec_accepted += accepted
 
-    def set_spec_totals(self, proposed: int, accepted: int):
-        """Absolute draft-token counters (summed over replicas' heartbeats)."""
+    def set_spec_totals(self, proposed: int, accepted: int, speedup: Optional[float] = None):
+        """Absolute draft-token counters (summed over replicas' heartbeats) and the
+        measured speculation speedup factor (mean over replicas that report one)."""
         with self._lock:
             self.spec_proposed, self.spec_accepted = proposed, accepted
+            self.spec_speedup = speedup
 
     # ---- snapshot (design.md:480-491) -------------------------------------
     def snapshot(self) -> dict:
@@ -178,7 +181,7 @@ class MetricsCollector:
                 "rejections": dict(self.rejected_total),
                 "speculative": {"proposed": self.spec_proposed, "accepted": self.spec_accepted,
                                 "acceptance_rate": self.spec_accepted / self.spec_proposed
-                                if self.spec_proposed else 0.0},
+                                if self.spec_proposed else 0.0, "speedup_factor": self.spec_speedup},
                 "uptime_s": now - self.start,
             }
 
@@ -234,4 +237,7 @@ class MetricsCollector:
                   [({"worker": str(k)}, v.get("kv_usage", 0.0)) for k, v in sorted(self.workers.items())])
             counter("xgs_spec_proposed_tokens_total", "draft tokens proposed", [({}, self.spec_proposed)])
             counter("xgs_spec_accepted_tokens_total", "draft tokens accepted", [({}, self.spec_accepted)])
+            if self.spec_speedup is not None:
+                gauge("xgs_spec_speedup_factor", "measured speculative-decoding speedup (tokens/s per sequence "
+                      "with speculation / without)", [({}, self.spec_speedup)])
         return "\n".join(out) + "\n"

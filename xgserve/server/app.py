@@ -7,6 +7,7 @@ Endpoints
   GET  /health                           200 ok|degraded, 503 unhealthy
   POST /admin/config                     hot reload (Req 10.5)
   POST /admin/model                      model hot-swap (Req 13)
+  GET|POST /admin/replicas               list / add / remove replicas at runtime (Req 7.5)
   GET  /debug/traces                     recent request spans (Req 8.5)
   POST /v1/completions, /v1/chat/completions, /v1/embeddings, GET /v1/models
                                          OpenAI-compatible aliases
@@ -266,6 +267,34 @@ async def handle_admin_model(request: web.Request) -> web.Response:
     return _json({"status": "ok", **res})
 
 
+async def handle_admin_replicas(request: web.Request) -> web.Response:
+    """GET: the replica set. POST {"action": "add", "count": n, "gpus": [..]} or
+    {"action": "remove", "ids": [..]} / {"action": "remove", "count": n}."""
+    srv: InferenceServer = request.app[SERVER_KEY]
+    if request.method == "GET":
+        return _json({"replicas": srv.stats()["replicas"], "routable": list(srv.routable)})
+    try:
+        d = json.loads(await _body(request))
+        if not isinstance(d, dict) or d.get("action") not in ("add", "remove"):
+            raise ValueError('expected {"action": "add"|"remove", ...}')
+        count = d.get("count", 1)
+        if not isinstance(count, int) or isinstance(count, bool):
+            raise ValueError("count must be an integer")
+        if d["action"] == "add":
+            gpus = d.get("gpus")
+            if gpus is not None and not (isinstance(gpus, list) and all(isinstance(g, int) for g in gpus)):
+                raise ValueError("gpus must be a list of integers")
+            res = await srv.add_replicas(count, gpus)
+        else:
+            ids = d.get("ids")
+            if ids is not None and not (isinstance(ids, list) and all(isinstance(i, int) for i in ids)):
+                raise ValueError("ids must be a list of integers")
+            res = await srv.remove_replicas(ids, count)
+    except (ValueError, ConfigError) as e:
+        raise ApiValidationError(ValidationError.invalid_parameter("replicas", str(e)))
+    return _json({"status": "ok", **res})
+
+
 # ---------------------------------------------------------------------- OpenAI aliases
 def _oa_stop(d: dict):
     s = d.get("stop")
@@ -370,6 +399,7 @@ def build_app(srv: InferenceServer) -> web.Application:
     r.add_get("/debug/traces", handle_traces)
     r.add_route("*", "/admin/config", handle_admin_config)
     r.add_route("*", "/admin/model", handle_admin_model)
+    r.add_route("*", "/admin/replicas", handle_admin_replicas)
     r.add_post("/v1/completions", handle_v1_completions)
     r.add_post("/v1/chat/completions", handle_v1_chat)
     r.add_post("/v1/embeddings", handle_v1_embeddings)

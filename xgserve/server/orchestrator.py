@@ -534,8 +534,10 @@ class InferenceServer:
         healthy = self._healthy_ids()
         specs = [r.stats.get("speculative") for r in self.replicas.values() if r.stats.get("speculative")]
         if specs:
+            sfs = [x["speedup_factor"] for x in specs if x.get("speedup_factor") is not None]
             self.metrics.set_spec_totals(sum(x["draft_tokens_proposed"] for x in specs),
-                                         sum(x["draft_tokens_accepted"] for x in specs))
+                                         sum(x["draft_tokens_accepted"] for x in specs),
+                                         sum(sfs) / len(sfs) if sfs else None)
         for rid in list(self.routable):
             r = self.replicas.get(rid)
             if r is None:
@@ -674,6 +676,78 @@ class InferenceServer:
             self._loop.create_task(self._drain_and_stop(old_ids))
             log.info("model swapped: %s -> %s", old_name, self.model_name)
             return {"previous_model": old_name, "model": self.model_name, "replicas": ids}
+
+    def _free_gpus(self, n: int) -> List[int]:
+        """The n lowest GPU indices no live process replica holds (the configured
+        `worker.gpus` list first, if any)."""
+        used = {g for r in self.replicas.values() for g in (getattr(r, "gpus", None) or [])}
+        pool = self._gpu_list(self.cfg.worker) if self.cfg.worker.gpus else []
+        cand = [g for g in pool if g not in used]
+        g = 0
+        while len(cand) < n:
+            if g not in used and g not in cand:
+                cand.append(g)
+            g += 1
+        return cand[:n]
+
+    async def add_replicas(self, count: int = 1, gpus: Optional[List[int]] = None,
+                           ready_timeout: Optional[float] = None) -> dict:
+        """Req 7.5: start `count` more replicas of the serving model at runtime and
+        route to them once ready; traffic on the existing replicas is untouched."""
+        if count < 1 or count > 64:
+            raise ConfigError("count must be in [1, 64]")
+        async with self._swap_lock:
+            w = self.cfg.worker
+            spec = self._spec
+            tp = max(1, int(w.tp))
+            if gpus is not None and len(gpus) != count * tp:
+                raise ConfigError(f"need {count * tp} GPU ids for {count} replica(s) of tp={tp}, got {len(gpus)}")
+            gl = list(gpus) if gpus is not None else (self._free_gpus(count * tp) if not w.in_process else [])
+            new: List[Replica] = []
+            for i in range(count):
+                rid = self._next_replica_id
+                self._next_replica_id += 1
+                r = self._make_replica(rid, spec, gl[i * tp:(i + 1) * tp] or list(range(tp)), w)
+                self.replicas[rid] = r
+                new.append(r)
+                r.start()
+            timeout = ready_timeout or (60.0 if w.mock else 1800.0)
+            oks = await asyncio.gather(*[asyncio.to_thread(r.wait_ready, timeout) for r in new])
+            if not all(oks):
+                errs = [f"replica {r.id}: {r.error or 'not ready in time'}" for r, ok in zip(new, oks) if not ok]
+                for r in new:
+                    await asyncio.to_thread(r.shutdown, 5.0)
+                    self.replicas.pop(r.id, None)
+                raise ApiInternal("; ".join(errs), code="replica_start_failed")
+            for r in new:
+                self.router.register(r.id, int(r.stats.get("memory_available", 1 << 40)) if r.stats else 1 << 40)
+                self.routable.append(r.id)
+            self.cfg.worker.replicas = len(self.routable)
+            self._wake.set()
+            log.info("replicas added: %s (now %d)", [r.id for r in new], len(self.routable))
+            return {"added": [r.id for r in new], "replicas": list(self.routable)}
+
+    async def remove_replicas(self, ids: Optional[List[int]] = None, count: int = 1) -> dict:
+        """Req 7.5: take replicas out of routing at runtime (default: the newest
+        `count`), let their in-flight requests finish, then stop them. Queued
+        requests are dispatched to the remaining replicas; at least one stays."""
+        async with self._swap_lock:
+            if ids is None:
+                ids = list(self.routable[-count:]) if count >= 1 else []
+            ids = [int(i) for i in ids]
+            bad = [i for i in ids if i not in self.routable]
+            if bad:
+                raise ConfigError(f"unknown or inactive replica id(s) {bad}; active: {self.routable}")
+            if not ids or len(ids) >= len(self.routable):
+                raise ConfigError("removal would leave no replica serving")
+            for rid in ids:
+                self.router.unregister(rid)
+                self.routable.remove(rid)
+            self.cfg.worker.replicas = len(self.routable)
+            self._wake.set()
+            self._loop.create_task(self._drain_and_stop(ids))
+            log.info("replicas removed: %s (now %d)", ids, len(self.routable))
+            return {"removed": ids, "replicas": list(self.routable)}
 
     async def _drain_and_stop(self, ids: List[int], timeout: float = 600.0) -> None:
         t_end = time.monotonic() + timeout
