@@ -160,6 +160,43 @@ void row_sumsq(const uint16_t* x, int T, int H, float* ss, hipStream_t st) {
   if (T > 0) hipLaunchKernelGGL(row_sumsq_kernel, dim3(T), dim3(256), 0, st, x, ss, H);
 }
 
+// K7: token-embedding gather, out[t] = table[ids[t]] (bf16 rows, 16 B per lane),
+// optionally with the row's sum of squares (ss != nullptr: the fused decode
+// layer's first RMSNorm statistic -- one launch instead of gather + row_sumsq).
+// Ids outside [0, V) produce a zero row (never an out-of-bounds read).
+__global__ void __launch_bounds__(256) embed_gather_kernel(const int32_t* __restrict__ ids,
+                                                           const uint16_t* __restrict__ table,
+                                                           uint16_t* __restrict__ out, float* __restrict__ ss, int H,
+                                                           int V) {
+  __shared__ float red[8];
+  const int t = blockIdx.x;
+  const int id = ids[t];
+  const bool ok = id >= 0 && id < V;
+  const uint16_t* src = table + static_cast<int64_t>(ok ? id : 0) * H;
+  uint16_t* dst = out + static_cast<int64_t>(t) * H;
+  float s = 0.f;
+  for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
+    uint4 v = ok ? ld16(src + c * 8) : make_uint4(0u, 0u, 0u, 0u);
+    st16(dst + c * 8, v);
+    if (ss != nullptr) {
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += f[i] * f[i];
+    }
+  }
+  if (ss != nullptr) {
+    s = block_sum(s, red);
+    if (threadIdx.x == 0) ss[t] = s;
+  }
+}
+
+void embed_gather(const int32_t* ids, int T, const uint16_t* table, int V, int H, uint16_t* out, float* ss,
+                  hipStream_t st) {
+  if (T > 0) hipLaunchKernelGGL(embed_gather_kernel, dim3(T), dim3(H >= 2048 ? 256 : 128), 0, st, ids, table, out, ss,
+                                H, V);
+}
+
 void layernorm(const uint16_t* x, const uint16_t* w, const uint16_t* b, uint16_t* out, int T, int H,
                float eps, hipStream_t st) {
   if (T <= 0) return;

@@ -26,6 +26,8 @@ int gemm_m64g_ex(const uint16_t*, int, int, const uint16_t*, int, float*, uint16
                  int, int, float, uint16_t*, float*, int*, hipStream_t);
 void add_partials_resid(const float*, int, int, uint16_t*, float*, int, hipStream_t);
 void row_sumsq(const uint16_t*, int, int, float*, hipStream_t);
+void embed_gather(const int32_t*, int, const uint16_t*, int, int, uint16_t*, float*, hipStream_t);
+void mean_l2norm_rows(float*, const int32_t*, const int32_t*, float*, int, int, hipStream_t);
 int decode_attention_fq(const float*, int, const int32_t*, const float*, const int32_t*, uint16_t*, uint16_t*,
                         const int32_t*, int, const int32_t*, float*, float*, uint16_t*, int64_t, int, int, int, int,
                         int, float, int, int, int*, const void*, int64_t, int, hipStream_t);
@@ -240,6 +242,18 @@ PYBIND11_MODULE(_kernels, m) {
     if (H % 1024) throw std::invalid_argument("add_partials_resid: H % 1024 != 0");
     xgk::add_partials_resid(P<const float>(part), S_, T, P<uint16_t>(res), P<float>(ss_part), H, S(st));
     check(0, "add_partials_resid");
+  });
+  m.def("embed_gather", [](uintptr_t ids, int T, uintptr_t table, int V, int H, uintptr_t out, uintptr_t ss,
+                           uintptr_t st) {
+    if (H % 8 || T < 0 || V < 1) throw std::invalid_argument("embed_gather: H % 8 != 0 or bad sizes");
+    xgk::embed_gather(P<const int32_t>(ids), T, P<const uint16_t>(table), V, H, P<uint16_t>(out), P<float>(ss), S(st));
+    check(0, "embed_gather");
+  });
+  m.def("mean_l2norm_rows", [](uintptr_t acc, uintptr_t rows, uintptr_t counts, uintptr_t out, int n, int H,
+                               uintptr_t st) {
+    if (n < 0 || H < 1) throw std::invalid_argument("mean_l2norm_rows: bad sizes");
+    xgk::mean_l2norm_rows(P<float>(acc), P<const int32_t>(rows), P<const int32_t>(counts), P<float>(out), n, H, S(st));
+    check(0, "mean_l2norm_rows");
   });
   m.def("row_sumsq", [](uintptr_t x, int T, int H, uintptr_t ss, uintptr_t st) {
     if (H % 8) throw std::invalid_argument("row_sumsq: H % 8 != 0");

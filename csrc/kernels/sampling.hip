@@ -279,4 +279,33 @@ void subst_tokens(int32_t* ids, const int32_t* src, const int32_t* prev, int n, 
   if (n > 0) hipLaunchKernelGGL(subst_tokens_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ids, src, prev, n);
 }
 
+// K11: embeddings output -- mean-pool + L2 normalise on the device. For each
+// finished request i: v = acc[rows[i]] / counts[i]; out[i] = v / max(||v||, 1e-12);
+// the accumulator row is re-zeroed for the slot's next owner. One workgroup per row.
+__global__ void __launch_bounds__(256) mean_l2norm_rows_kernel(float* __restrict__ acc, const int32_t* __restrict__ rows,
+                                                               const int32_t* __restrict__ counts,
+                                                               float* __restrict__ out, int H) {
+  __shared__ float red[4];
+  const int i = blockIdx.x;
+  float* a = acc + static_cast<int64_t>(rows[i]) * H;
+  const float inv_n = 1.f / static_cast<float>(counts[i] > 0 ? counts[i] : 1);
+  float s = 0.f;
+  for (int c = threadIdx.x; c < H; c += blockDim.x) {
+    const float v = a[c] * inv_n;
+    s += v * v;
+  }
+  s = block_sum(s, red);
+  const float scale = inv_n / fmaxf(sqrtf(s), 1e-12f);
+  float* o = out + static_cast<int64_t>(i) * H;
+  for (int c = threadIdx.x; c < H; c += blockDim.x) {
+    o[c] = a[c] * scale;
+    a[c] = 0.f;
+  }
+}
+
+void mean_l2norm_rows(float* acc, const int32_t* rows, const int32_t* counts, float* out, int n, int H,
+                      hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(mean_l2norm_rows_kernel, dim3(n), dim3(256), 0, st, acc, rows, counts, out, H);
+}
+
 }  // namespace xgk

@@ -345,7 +345,10 @@ def test_runtime_add_remove_replicas_without_dropping_traffic():
         assert r.status == 200, d
         new_id = d["added"][0]
         assert sorted(d["replicas"]) == [0, 1, new_id]
-        await asyncio.sleep(0.3)
+        for _ in range(200):
+            if srv.replicas[new_id].loop.steps > 0:
+                break
+            await asyncio.sleep(0.05)
         assert srv.replicas[new_id].loop.steps > 0  # the new replica serves traffic
         r = await c.post("/admin/replicas", data=json.dumps({"action": "remove", "ids": [0]}))
         d = await r.json()
@@ -364,7 +367,7 @@ def test_runtime_add_remove_replicas_without_dropping_traffic():
         assert r.status == 400
         r = await c.post("/admin/replicas", data=json.dumps({"action": "remove", "ids": [99]}))
         assert r.status == 400
-        for _ in range(50):
+        for _ in range(200):
             if 0 not in srv.replicas:
                 break
             await asyncio.sleep(0.05)

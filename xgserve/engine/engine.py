@@ -586,7 +586,9 @@ class LLMEngine:
                 out.cached_tokens = req.cached_tokens
                 self._finish(req, reason)
             outs.append(out)
-        # prefill-only (embedding) completions
+        # prefill-only (embedding) completions: mean-pool + L2 normalise every finished
+        # request's accumulator row in ONE device launch, one D2H copy
+        done = []
         for sid, f in fin_map.items():
             if f[1] != FINISH_EMBED:
                 continue
@@ -597,13 +599,16 @@ class LLMEngine:
             for i in range(ns):
                 if int(seq_ids[i]) == sid:
                     slot = int(plan["slots"][i])
-            v = self.embed_acc[slot] / max(1, len(req.prompt_ids))
-            v = v / v.norm().clamp_min(1e-12)
-            emb = v.cpu().tolist()
-            self.embed_acc[slot].zero_()
-            outs.append(RequestOutput(req.request_id, [], "", True, "stop", prompt_tokens=len(req.prompt_ids),
-                                      completion_tokens=0, embedding=emb))
-            self._finish(req, FINISH_EMBED)
+            done.append((req, slot))
+        if done:
+            from .. import ops
+            rows = torch.tensor([s_ for _, s_ in done], dtype=torch.int32, device=self.device)
+            cnt = torch.tensor([len(r.prompt_ids) for r, _ in done], dtype=torch.int32, device=self.device)
+            embs = ops.mean_l2norm_rows(self.embed_acc, rows, cnt).cpu().tolist()
+            for (req, _), emb in zip(done, embs):
+                outs.append(RequestOutput(req.request_id, [], "", True, "stop", prompt_tokens=len(req.prompt_ids),
+                                          completion_tokens=0, embedding=emb))
+                self._finish(req, FINISH_EMBED)
         return outs
 
     # ------------------------------------------------------------------ followers (TP > 1)

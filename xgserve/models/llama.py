@@ -405,8 +405,8 @@ class LlamaForCausalLM(nn.Module):
     def _forward_fused(self, input_ids: torch.Tensor, meta: AttnMeta,
                        kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         ws = self._fused_ws
-        resid = F.embedding(input_ids, self.embed)
-        st = RowStats(ops.row_sumsq(resid, ws.ss[0]), 1, meta.num_tokens)
+        resid = ops.embed_gather(input_ids, self.embed, ws.ss[0])  # gather + first norm statistic, one launch
+        st = RowStats(ws.ss[0], 1, meta.num_tokens)
         for i, layer in enumerate(self.layers):
             st = layer.forward_fused(resid, st, meta, kv_caches[i], self.cos_sin, ws, 2 * i + 1)
         return ops.rmsnorm(resid, self.norm, self.cfg.norm_eps)
@@ -438,7 +438,8 @@ class LlamaForCausalLM(nn.Module):
                 kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         if self.fused_decode_ok(meta):
             return self._forward_fused(input_ids, meta, kv_caches)
-        x = F.embedding(input_ids, self.embed)
+        x = ops.embed_gather(input_ids, self.embed) if input_ids.dtype == torch.int32 else \
+            F.embedding(input_ids, self.embed)
         residual = None
         for i, layer in enumerate(self.layers):
             x, residual = layer(x, residual, meta, kv_caches[i], self.cos_sin)

@@ -12,6 +12,7 @@ from .linear import skinny_linear, PendingSum
 from .attention import (decode_attention, decode_attention_fused, prefill_attention, decode_attention_ref,
                         prefill_attention_ref, choose_num_splits)
 from .sampling import argmax_logprob, sample_tokens, argmax_logprob_ref, segment_sum, subst_tokens
+from .embedding import embed_gather, mean_l2norm_rows
 from .moe import moe_topk_softmax, moe_route, moe_align, moe_forward_ref, fused_moe
 from ._native import available as native_available
 
@@ -21,6 +22,7 @@ __all__ = [
     "RotaryCache", "rope_cache", "rope_cache_ref", "build_cos_sin",
     "decode_attention", "decode_attention_fused", "prefill_attention", "decode_attention_ref", "prefill_attention_ref", "choose_num_splits",
     "argmax_logprob", "sample_tokens", "argmax_logprob_ref", "segment_sum", "subst_tokens",
+    "embed_gather", "mean_l2norm_rows",
     "moe_topk_softmax", "moe_route", "moe_align", "moe_forward_ref", "fused_moe",
     "native_available",
 ]
