@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Serve-path benchmark: N concurrent SSE streams against `python -m xgserve serve`
+(BASELINE.json config 1 on the CPU, and the HTTP path of config 3 on a GPU).
+
+    python bench/serve_bench.py --launch "--model gpt2 --device cpu --in-process" \
+        --concurrency 8 --prompt-len 128 --output-len 64 --duration 30
+    python bench/serve_bench.py --url http://127.0.0.1:8000 --concurrency 64 ...
+
+Each client is a closed loop: POST /generate {"stream": true, "ignore_eos": true}
+with a synthetic ASCII prompt (one token per byte with the synthetic tokenizer of
+random-init models, so --prompt-len is exact) and staggered max_tokens (uniform on
+[1, 2*output_len], mean output_len, as bench.py), reads the SSE events, and
+starts the next request when `done` arrives. After --warmup seconds it measures
+for --duration seconds:
+  * output tok/s seen by the clients (token events received in the window),
+  * TTFT (request sent -> first token event) p50 / p99,
+  * inter-token gap at the client p50 / p99,
+  * Req 5.1 token delivery delay (token on the server host -> SSE event written;
+    server-side histogram, /server/stats token_delivery_ms) p50 / p99 / max vs 10 ms,
+  * Req 8.4 prompt vs generation tokens/s from the server's own counters.
+Prints ONE JSON line. `--launch` starts the server as a child process on a free
+port (127.0.0.1) and stops it afterwards.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import random
+import shlex
+import socket
+import string
+import subprocess
+import sys
+import time
+
+import aiohttp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _pct(xs, q):
+    if not xs:
+        return None
+    v = sorted(xs)
+    return v[min(len(v) - 1, max(0, int(round(q * len(v))) - 1))]
+
+
+async def _wait_ready(url: str, timeout: float) -> None:
+    t_end = time.monotonic() + timeout
+    async with aiohttp.ClientSession() as s:
+        while time.monotonic() < t_end:
+            try:
+                async with s.get(url + "/health") as r:
+                    if r.status == 200:
+                        return
+            except aiohttp.ClientError:
+                pass
+            await asyncio.sleep(0.5)
+    raise RuntimeError(f"server at {url} not ready after {timeout:.0f} s")
+
+
+async def run(a, url: str) -> dict:
+    rng = random.Random(1234)
+    st = {"t0": None, "t1": None, "tokens": 0, "ttft": [], "itl": [], "requests": 0, "errors": 0}
+    stop = asyncio.Event()
+    lens = [max(1, int(round(1 + (2 * a.output_len - 1) * (i + 0.5) / a.concurrency))) for i in range(a.concurrency)]
+
+    def prompt() -> str:
+        return "".join(rng.choice(string.ascii_lowercase) for _ in range(max(1, a.prompt_len - 1)))
+
+    async def client(i: int, s: aiohttp.ClientSession):
+        max_tokens = lens[i]
+        while not stop.is_set():
+            body = {"prompt": prompt(), "max_tokens": max_tokens, "temperature": 0.0, "stream": True,
+                    "ignore_eos": True}
+            sent = time.monotonic()
+            last = None
+            try:
+                async with s.post(url + "/generate", json=body) as r:
+                    if r.status != 200:
+                        st["errors"] += 1
+                        await r.read()
+                        await asyncio.sleep(0.05)
+                        continue
+                    async for raw in r.content:
+                        line = raw.strip()
+                        if not line.startswith(b"data: "):
+                            continue
+                        ev = json.loads(line[6:])
+                        now = time.monotonic()
+                        in_win = st["t0"] is not None and st["t1"] is None
+                        if ev["type"] == "token":
+                            if last is None:
+                                if in_win:
+                                    st["ttft"].append(now - sent)
+                            elif in_win:
+                                st["itl"].append(now - last)
+                            last = now
+                            if in_win:
+                                st["tokens"] += 1
+                        elif ev["type"] in ("done", "error"):
+                            if ev["type"] == "error":
+                                st["errors"] += 1
+                            elif in_win:
+                                st["requests"] += 1
+                            break
+            except aiohttp.ClientError:
+                st["errors"] += 1
+            max_tokens = a.output_len  # later requests: the mean length (bench.py replaces the same way)
+
+    async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None)) as s:
+        tasks = [asyncio.create_task(client(i, s)) for i in range(a.concurrency)]
+        await asyncio.sleep(a.warmup)
+        async with s.get(url + "/server/stats") as r:
+            s0 = await r.json()
+        st["t0"] = time.monotonic()
+        await asyncio.sleep(a.duration)
+        st["t1"] = time.monotonic()
+        async with s.get(url + "/server/stats") as r:
+            s1 = await r.json()
+        stop.set()
+        await asyncio.wait(tasks, timeout=120)
+    win = st["t1"] - st["t0"]
+    m0, m1 = s0["metrics"], s1["metrics"]
+    dp = m1["prompt_tokens_total"] - m0["prompt_tokens_total"]
+    dg = m1["generation_tokens_total"] - m0["generation_tokens_total"]
+    dl = m1.get("token_delivery_ms", {})
+    ms = lambda x: None if x is None else round(1000 * x, 3)  # noqa: E731
+    return {
+        "metric": "serve_output_tokens_per_sec", "value": round(st["tokens"] / win, 2), "unit": "tokens/s",
+        "window_s": round(win, 2), "concurrency": a.concurrency, "prompt_len": a.prompt_len,
+        "output_len": a.output_len, "requests_completed": st["requests"], "errors": st["errors"],
+        "ttft_p50_ms": ms(_pct(st["ttft"], 0.5)), "ttft_p99_ms": ms(_pct(st["ttft"], 0.99)),
+        "client_itl_p50_ms": ms(_pct(st["itl"], 0.5)), "client_itl_p99_ms": ms(_pct(st["itl"], 0.99)),
+        "token_delivery_ms": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in dl.items()},
+        "req_5_1_delivery_within_10ms": (dl.get("p99") is not None and dl["p99"] <= 10.0),
+        "server_prompt_tokens_per_sec": round(dp / win, 2), "server_generation_tokens_per_sec": round(dg / win, 2),
+        "model": s1.get("model"),
+    }
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--url", help="an already running server, e.g. http://127.0.0.1:8000")
+    ap.add_argument("--launch", help="start `python -m xgserve serve <ARGS>` (quoted) on a free port")
+    ap.add_argument("--concurrency", type=int, default=8)
+    ap.add_argument("--prompt-len", type=int, default=128)
+    ap.add_argument("--output-len", type=int, default=64)
+    ap.add_argument("--warmup", type=float, default=5.0)
+    ap.add_argument("--duration", type=float, default=20.0)
+    ap.add_argument("--ready-timeout", type=float, default=900.0)
+    ap.add_argument("--out", help="also append the JSON line to this file")
+    a = ap.parse_args()
+    if bool(a.url) == bool(a.launch):
+        ap.error("give exactly one of --url / --launch")
+    proc = None
+    url = a.url
+    try:
+        if a.launch:
+            port = _free_port()
+            cmd = [sys.executable, "-m", "xgserve", "serve", "--host", "127.0.0.1", "--port", str(port)]
+            cmd += shlex.split(a.launch)
+            proc = subprocess.Popen(cmd, cwd=ROOT, start_new_session=True)
+            url = f"http://127.0.0.1:{port}"
+        asyncio.run(_wait_ready(url, a.ready_timeout))
+        res = asyncio.run(run(a, url))
+        line = json.dumps(res)
+        print(line, flush=True)
+        if a.out:
+            with open(a.out, "a") as f:
+                f.write(line + "\n")
+        return 0 if res["errors"] == 0 else 1
+    finally:
+        if proc is not None:
+            proc.terminate()
+            try:
+                proc.wait(60)
+            except subprocess.TimeoutExpired:
+                proc.kill()
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -215,6 +215,36 @@ def test_segment_sum():
     torch.testing.assert_close(out, ref, atol=1e-2, rtol=1e-3)
 
 
+@pytest.mark.parametrize("T,V,H", [(1, 1000, 4096), (37, 128256, 4096), (5, 512, 8192), (3, 300, 256)])
+def test_embed_gather(T, V, H):
+    table = rnd(V, H)
+    ids = torch.randint(0, V, (T,), dtype=torch.int32, device=DEV)
+    ids[0] = V - 1
+    if T > 2:
+        ids[2] = -1  # invalid ids give zero rows, never an out-of-bounds read
+    ss = torch.full((T,), -1.0, device=DEV)
+    out = ops.embed_gather(ids, table, ss)
+    ref = table.cpu().float()[ids.cpu().long().clamp(0, V - 1)]
+    ref[ids.cpu() < 0] = 0
+    assert torch.equal(out.cpu().float(), ref)
+    torch.testing.assert_close(ss.cpu(), ref.pow(2).sum(-1), rtol=1e-4, atol=1e-3)
+    out2 = ops.embed_gather(ids, table)  # without the statistic
+    assert torch.equal(out2, out)
+
+
+def test_mean_l2norm_rows():
+    acc = torch.randn(8, 4096, device=DEV)
+    rows = torch.tensor([5, 1, 6], dtype=torch.int32, device=DEV)
+    cnt = torch.tensor([3, 1, 100], dtype=torch.int32, device=DEV)
+    ref_in = acc.cpu().clone()
+    out = ops.mean_l2norm_rows(acc, rows, cnt).cpu()
+    for i, (r, n) in enumerate(zip(rows.tolist(), cnt.tolist())):
+        v = ref_in[r] / n
+        torch.testing.assert_close(out[i], v / v.norm(), rtol=1e-4, atol=1e-6)
+        assert bool((acc[r] == 0).all())
+    assert torch.equal(acc[0].cpu(), ref_in[0])  # other rows untouched
+
+
 def _w13(E, F, H):
     """per-expert block-16 interleaved gate|up rows (the serving layout)."""
     from xgserve.ops.linear import interleave_gate_up

@@ -395,3 +395,20 @@ def test_degradation_rejects_low_priority():
 
     cfg = mock_config()
     assert run_with_client(cfg, fn)
+
+
+def test_token_delivery_delay_is_measured():
+    """Req 5.1: the server records token-on-host -> SSE-write delay per token event."""
+    async def fn(c, srv):
+        r = await c.post("/generate", data=json.dumps({"prompt": "hello", "max_tokens": 8, "stream": True}))
+        assert r.status == 200
+        await r.read()
+        st = await (await c.get("/server/stats")).json()
+        d = st["metrics"]["token_delivery_ms"]
+        assert d["n"] >= 7 and 0 <= d["p50"] <= d["p99"] <= d["max"]
+        assert d["p99"] < 1000.0
+        text = await (await c.get("/metrics")).text()
+        assert "xgs_token_delivery_seconds_count" in text
+        return True
+
+    assert run_with_client(mock_config(), fn)

@@ -413,6 +413,7 @@ class LLMEngine:
         outs += self._flush_deferred()  # previous step's outputs, while the GPU runs
         t = self._tick("emit_overlapped", t)
         toks, lps, hidden = self.runner.wait(handle)
+        plan["_t_tokens"] = time.monotonic()
         t = self._tick("wait_gpu", t)
         n_sample = int(plan["num_sample"])
         counts = np.ones(n_sample, np.int32)
@@ -451,12 +452,14 @@ class LLMEngine:
         counts = None
         if self.spec is not None and self.is_driver and plan["num_seqs"] > plan["num_decodes"]:
             toks, lps, hidden, counts = self.spec.verify_execute(plan, samp)
+            plan["_t_tokens"] = time.monotonic()
         else:
             handle = self.runner.launch(plan, samp)
             t = self._tick("launch", t)
             outs += self._flush_deferred()  # previous step's outputs, while this one runs
             t = self._tick("emit_overlapped", t)
             toks, lps, hidden = self.runner.wait(handle)
+            plan["_t_tokens"] = time.monotonic()
             t = self._tick("wait_gpu", t)
         if counts is None:
             counts = np.ones(int(plan["num_sample"]), np.int32)
@@ -482,7 +485,11 @@ class LLMEngine:
         if not self.is_driver:
             return []
         first_tokens = bool(plan["is_prefill"][plan["sample_seq_index"]].any()) if n_sample else False
-        if self.cfg.overlap_outputs and self.spec is None and not first_tokens and not fin_map:
+        # deferral only pays where the next step runs asynchronously (a GPU): on the CPU
+        # the next launch computes the whole step, so deferring would add a step of
+        # token delivery delay (Req 5.1) for nothing
+        if (self.cfg.overlap_outputs and self.device.type == "cuda" and self.spec is None and not first_tokens
+                and not fin_map):
             self._deferred = (plan, toks, lps, counts, fin_map)
             return []
         with self._lock:
@@ -551,6 +558,7 @@ class LLMEngine:
         n_sample = int(plan["num_sample"])
         now = time.monotonic()
         sidx = plan["sample_seq_index"]
+        t_tok = plan.get("_t_tokens", now)
         k = 0
         for j in range(n_sample):
             c = int(counts[j])
@@ -581,7 +589,7 @@ class LLMEngine:
             out = RequestOutput(req.request_id, new, text, reason is not None,
                                 FINISH_NAMES.get(reason) if reason else None,
                                 prompt_tokens=len(req.prompt_ids), completion_tokens=len(req.output_ids),
-                                logprobs=new_lps)
+                                logprobs=new_lps, t_tokens=t_tok)
             if reason is not None:
                 out.cached_tokens = req.cached_tokens
                 self._finish(req, reason)

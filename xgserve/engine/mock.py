@@ -138,7 +138,8 @@ class MockEngine:
                     text += r.detok.flush()
                 self.stats_counters["generation_tokens"] += 1
                 outs.append(RequestOutput(rid, [tok], text, reason is not None, reason,
-                                          prompt_tokens=len(r.prompt_ids), completion_tokens=len(r.output_ids)))
+                                          prompt_tokens=len(r.prompt_ids), completion_tokens=len(r.output_ids),
+                                          t_tokens=time.monotonic()))
                 if reason is not None:
                     self._drop(rid)
         return outs

@@ -54,6 +54,10 @@ class RequestOutput:
     embedding: Optional[List[float]] = None
     error: Optional[str] = None
     error_code: Optional[str] = None
+    # time.monotonic() when this output's tokens reached the host (Req 5.1 delivery
+    # delay = socket write time - t_tokens; CLOCK_MONOTONIC is system-wide, so it holds
+    # across replica processes)
+    t_tokens: float = 0.0
 
 
 @dataclass

@@ -19,6 +19,7 @@ from typing import Dict, List, Optional, Tuple
 _LAT_BUCKETS = (0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10, 30, 60, 120)
 _TTFT_BUCKETS = (0.001, 0.005, 0.01, 0.02, 0.05, 0.1, 0.2, 0.5, 1, 2, 5, 10, 30)
 _ITL_BUCKETS = (0.001, 0.002, 0.005, 0.01, 0.02, 0.05, 0.1, 0.25, 0.5, 1)
+_DELIVERY_BUCKETS = (0.0005, 0.001, 0.002, 0.005, 0.01, 0.02, 0.05, 0.1, 0.5)
 _BATCH_BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256, 512)
 
 
@@ -41,6 +42,14 @@ def _labels(d: Dict[str, str]) -> str:
     return "{" + ",".join(f'{k}="{v}"' for k, v in sorted(d.items())) + "}"
 
 
+def _pcts(xs) -> dict:
+    if not xs:
+        return {"p50": None, "p99": None, "max": None, "n": 0}
+    v = sorted(xs)
+    pick = lambda q: 1000 * v[min(len(v) - 1, int(math.ceil(q * len(v))) - 1)]  # noqa: E731
+    return {"p50": pick(0.5), "p99": pick(0.99), "max": 1000 * v[-1], "n": len(v)}
+
+
 class MetricsCollector:
     def __init__(self, window_s: float = 60.0):
         self._lock = threading.Lock()
@@ -51,6 +60,8 @@ class MetricsCollector:
         self.requests_active = 0
         self.ttft = Histogram(_TTFT_BUCKETS)
         self.itl = Histogram(_ITL_BUCKETS)
+        self.delivery = Histogram(_DELIVERY_BUCKETS)
+        self._recent_delivery: deque = deque(maxlen=8192)
         self.batch = Histogram(_BATCH_BUCKETS)
         self.padding_ratio_sum = 0.0
         self.prompt_tokens_total = 0
@@ -104,6 +115,13 @@ class MetricsCollector:
     def record_ttft(self, s: float):
         with self._lock:
             self.ttft.observe(s)
+
+    def record_delivery(self, s: float):
+        """Req 5.1: token delivery delay -- from the token reaching the host (after
+        the engine step) to its SSE event being written to the client socket."""
+        with self._lock:
+            self.delivery.observe(s)
+            self._recent_delivery.append(s)
 
     def record_itl(self, s: float):
         with self._lock:
@@ -182,6 +200,7 @@ class MetricsCollector:
                 "speculative": {"proposed": self.spec_proposed, "accepted": self.spec_accepted,
                                 "acceptance_rate": self.spec_accepted / self.spec_proposed
                                 if self.spec_proposed else 0.0, "speedup_factor": self.spec_speedup},
+                "token_delivery_ms": _pcts(self._recent_delivery),
                 "uptime_s": now - self.start,
             }
 
@@ -221,6 +240,8 @@ class MetricsCollector:
             gauge("xgs_requests_active", "requests in flight", [({}, self.requests_active)])
             hist("xgs_ttft_seconds", "time to first token", [({}, self.ttft)])
             hist("xgs_itl_seconds", "inter-token latency", [({}, self.itl)])
+            hist("xgs_token_delivery_seconds", "token on host -> SSE event written (Req 5.1: <= 10 ms)",
+                 [({}, self.delivery)])
             hist("xgs_batch_size", "sequences per engine step", [({}, self.batch)])
             counter("xgs_prompt_tokens_total", "prompt tokens processed", [({}, self.prompt_tokens_total)])
             counter("xgs_generation_tokens_total", "tokens generated", [({}, self.generation_tokens_total)])

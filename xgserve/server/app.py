@@ -132,6 +132,9 @@ async def _sse(request: web.Request, srv: InferenceServer, sreq: ServerRequest, 
             data = ev.sse() if fmt is None else fmt(ev)
             if data:
                 await resp.write(data)
+                t_tok = getattr(ev, "t_tokens", 0.0)
+                if t_tok:
+                    srv.metrics.record_delivery(time.monotonic() - t_tok)
             n += 1
             if ev.type in ("done", "error"):
                 break

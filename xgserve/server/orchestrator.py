@@ -457,8 +457,10 @@ class InferenceServer:
                     sreq.logprobs.extend(o.logprobs)
                 if sreq.sender is not None:
                     if o.new_text:
-                        sreq.sender.send(TokenEvent.tok(o.new_text, sreq.completion_tokens - 1,
-                                                        o.logprobs[-1] if o.logprobs else None))
+                        ev = TokenEvent.tok(o.new_text, sreq.completion_tokens - 1,
+                                            o.logprobs[-1] if o.logprobs else None)
+                        ev.t_tokens = o.t_tokens  # not serialised: delivery-delay measurement (Req 5.1)
+                        sreq.sender.send(ev)
                 else:
                     sreq.text_parts.append(o.new_text)
             elif o.new_text:
