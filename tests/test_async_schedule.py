@@ -168,3 +168,16 @@ def test_prefix_lookup_counted_once_per_admission():
     waiting_lookups = (mid["hit_count"] + mid["miss_count"]) - (before["hit_count"] + before["miss_count"])
     admitted = 2 in [int(x) for x in plan["seq_ids"]]
     assert waiting_lookups == (1 if admitted else 0)
+
+
+def test_kv_usage_excludes_evictable_prefix_pages():
+    """A warm prefix cache is not memory pressure: after every request finished, the
+    cached pages stay allocated but kv_usage (the degradation ladder's input) is 0."""
+    from xgserve.engine import EngineConfig, LLMEngine, SamplingParams
+    eng = LLMEngine(EngineConfig(model="llama-tiny", device="cpu", dtype="float32", num_blocks=64, max_num_seqs=4,
+                                 max_num_batched_tokens=256, use_graphs=False))
+    eng.generate([[1] + list(range(10, 80)), [1] + list(range(100, 170))],
+                 SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True))
+    st = eng.stats()
+    assert st["kv_blocks_used"] > 0 and st["running"] == 0
+    assert st["kv_usage"] == 0.0

@@ -673,7 +673,11 @@ class LLMEngine:
         return [results[r] for r in rids]
 
     def kv_usage(self) -> float:
-        return self.sched.num_used_blocks() / max(1, self.sched.num_blocks())
+        """Memory pressure of the KV pool: pages pinned by live sequences. Prefix-cache
+        pages nobody references are evictable on demand, so they do not count (else a
+        warm cache would read as ~100 % and trip the degradation ladder)."""
+        pinned = self.sched.num_used_blocks() - self.sched.num_evictable_blocks()
+        return max(0, pinned) / max(1, self.sched.num_blocks())
 
     def stats(self) -> dict:
         cs = self.sched.cache_stats()
