@@ -67,10 +67,10 @@ async def _wait_ready(url: str, timeout: float) -> None:
     raise RuntimeError(f"server at {url} not ready after {timeout:.0f} s")
 
 
-async def run(a, url: str) -> dict:
-    rng = random.Random(1234)
-    st = {"t0": None, "t1": None, "tokens": 0, "ttft": [], "itl": [], "requests": 0, "errors": 0}
-    stop = asyncio.Event()
+async def run_clients(a, url: str, first: int, n: int, t0: float, t1: float) -> dict:
+    """Clients [first, first + n) of the closed loop; measures in [t0, t1) (monotonic)."""
+    rng = random.Random(1234 + first)
+    st = {"tokens": 0, "ttft": [], "itl": [], "requests": 0, "errors": 0}
     lens = [max(1, int(round(1 + (2 * a.output_len - 1) * (i + 0.5) / a.concurrency))) for i in range(a.concurrency)]
 
     def prompt() -> str:
@@ -78,7 +78,7 @@ async def run(a, url: str) -> dict:
 
     async def client(i: int, s: aiohttp.ClientSession):
         max_tokens = lens[i]
-        while not stop.is_set():
+        while time.monotonic() < t1:
             body = {"prompt": prompt(), "max_tokens": max_tokens, "temperature": 0.0, "stream": True,
                     "ignore_eos": True}
             sent = time.monotonic()
@@ -91,22 +91,21 @@ async def run(a, url: str) -> dict:
                         await asyncio.sleep(0.05)
                         continue
                     async for raw in r.content:
-                        line = raw.strip()
-                        if not line.startswith(b"data: "):
+                        if not raw.startswith(b"data: "):
                             continue
-                        ev = json.loads(line[6:])
                         now = time.monotonic()
-                        in_win = st["t0"] is not None and st["t1"] is None
-                        if ev["type"] == "token":
+                        in_win = t0 <= now < t1
+                        if raw.startswith(b'data: {"type":"token"'):
                             if last is None:
-                                if in_win:
+                                if in_win and t0 <= sent:
                                     st["ttft"].append(now - sent)
                             elif in_win:
                                 st["itl"].append(now - last)
                             last = now
                             if in_win:
                                 st["tokens"] += 1
-                        elif ev["type"] in ("done", "error"):
+                        else:
+                            ev = json.loads(raw[6:])
                             if ev["type"] == "error":
                                 st["errors"] += 1
                             elif in_win:
@@ -116,18 +115,49 @@ async def run(a, url: str) -> dict:
                 st["errors"] += 1
             max_tokens = a.output_len  # later requests: the mean length (bench.py replaces the same way)
 
-    async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None)) as s:
-        tasks = [asyncio.create_task(client(i, s)) for i in range(a.concurrency)]
-        await asyncio.sleep(a.warmup)
+    conn = aiohttp.TCPConnector(limit=0)
+    async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None), connector=conn) as s:
+        await asyncio.gather(*[client(first + i, s) for i in range(n)])
+    return st
+
+
+def _proc_main(a, url, first, n, t0, t1, q):
+    q.put(asyncio.run(run_clients(a, url, first, n, t0, t1)))
+
+
+async def _stats(url: str) -> dict:
+    async with aiohttp.ClientSession() as s:
         async with s.get(url + "/server/stats") as r:
-            s0 = await r.json()
-        st["t0"] = time.monotonic()
-        await asyncio.sleep(a.duration)
-        st["t1"] = time.monotonic()
-        async with s.get(url + "/server/stats") as r:
-            s1 = await r.json()
-        stop.set()
-        await asyncio.wait(tasks, timeout=120)
+            return await r.json()
+
+
+def run(a, url: str) -> dict:
+    """Client processes (--procs) so the load generator never is the bottleneck."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    t_start = time.monotonic() + 2.0  # processes up
+    t0, t1 = t_start + a.warmup, t_start + a.warmup + a.duration
+    P = max(1, min(a.procs, a.concurrency))
+    per = [a.concurrency // P + (1 if i < a.concurrency % P else 0) for i in range(P)]
+    firsts = [sum(per[:i]) for i in range(P)]
+    ps = [ctx.Process(target=_proc_main, args=(a, url, firsts[i], per[i], t0, t1, q)) for i in range(P)]
+    for p in ps:
+        p.start()
+    time.sleep(max(0.0, t0 - time.monotonic()))
+    s0 = asyncio.run(_stats(url))
+    time.sleep(max(0.0, t1 - time.monotonic()))
+    s1 = asyncio.run(_stats(url))
+    parts = [q.get(timeout=a.duration + 600) for _ in ps]
+    for p in ps:
+        p.join(60)
+    st = {"tokens": sum(x["tokens"] for x in parts), "ttft": sum((x["ttft"] for x in parts), []),
+          "itl": sum((x["itl"] for x in parts), []), "requests": sum(x["requests"] for x in parts),
+          "errors": sum(x["errors"] for x in parts), "t0": t0, "t1": t1}
+    return _report(a, st, s0, s1)
+
+
+def _report(a, st, s0, s1) -> dict:
     win = st["t1"] - st["t0"]
     m0, m1 = s0["metrics"], s1["metrics"]
     dp = m1["prompt_tokens_total"] - m0["prompt_tokens_total"]
@@ -143,6 +173,7 @@ async def run(a, url: str) -> dict:
         "token_delivery_ms": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in dl.items()},
         "req_5_1_delivery_within_10ms": (dl.get("p99") is not None and dl["p99"] <= 10.0),
         "server_prompt_tokens_per_sec": round(dp / win, 2), "server_generation_tokens_per_sec": round(dg / win, 2),
+        "event_loop_lag_ms": m1.get("event_loop_lag_ms"), "client_procs": a.procs,
         "model": s1.get("model"),
     }
 
@@ -157,6 +188,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=float, default=5.0)
     ap.add_argument("--duration", type=float, default=20.0)
     ap.add_argument("--ready-timeout", type=float, default=900.0)
+    ap.add_argument("--procs", type=int, default=4, help="client processes")
     ap.add_argument("--out", help="also append the JSON line to this file")
     a = ap.parse_args()
     if bool(a.url) == bool(a.launch):
@@ -171,7 +203,7 @@ def main() -> int:
             proc = subprocess.Popen(cmd, cwd=ROOT, start_new_session=True)
             url = f"http://127.0.0.1:{port}"
         asyncio.run(_wait_ready(url, a.ready_timeout))
-        res = asyncio.run(run(a, url))
+        res = run(a, url)
         line = json.dumps(res)
         print(line, flush=True)
         if a.out:

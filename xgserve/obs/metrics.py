@@ -61,7 +61,8 @@ class MetricsCollector:
         self.ttft = Histogram(_TTFT_BUCKETS)
         self.itl = Histogram(_ITL_BUCKETS)
         self.delivery = Histogram(_DELIVERY_BUCKETS)
-        self._recent_delivery: deque = deque(maxlen=8192)
+        self._recent_delivery: deque = deque(maxlen=1 << 16)
+        self._recent_loop_lag: deque = deque(maxlen=4096)
         self.batch = Histogram(_BATCH_BUCKETS)
         self.padding_ratio_sum = 0.0
         self.prompt_tokens_total = 0
@@ -122,6 +123,11 @@ class MetricsCollector:
         with self._lock:
             self.delivery.observe(s)
             self._recent_delivery.append(s)
+
+    def record_loop_lag(self, s: float):
+        """Event-loop responsiveness: how late a periodic wake-up fired."""
+        with self._lock:
+            self._recent_loop_lag.append(s)
 
     def record_itl(self, s: float):
         with self._lock:
@@ -201,6 +207,7 @@ class MetricsCollector:
                                 "acceptance_rate": self.spec_accepted / self.spec_proposed
                                 if self.spec_proposed else 0.0, "speedup_factor": self.spec_speedup},
                 "token_delivery_ms": _pcts(self._recent_delivery),
+                "event_loop_lag_ms": _pcts(self._recent_loop_lag),
                 "uptime_s": now - self.start,
             }
 

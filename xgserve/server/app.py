@@ -126,19 +126,23 @@ async def _sse(request: web.Request, srv: InferenceServer, sreq: ServerRequest, 
         resp = web.StreamResponse(status=200, headers={"Content-Type": "text/event-stream",
                                                        "Cache-Control": "no-cache", "X-Request-Id": sreq.id})
         await resp.prepare(request)
-        ev = first
+        batch = [first] + sreq.token_stream.take_ready()
         n = 0
         while True:
-            data = ev.sse() if fmt is None else fmt(ev)
+            # coalesce whatever is queued into one write (one wake-up per backlog, not per token)
+            data = b"".join(d for d in ((e.sse() if fmt is None else fmt(e)) for e in batch) if d)
             if data:
                 await resp.write(data)
-                t_tok = getattr(ev, "t_tokens", 0.0)
-                if t_tok:
-                    srv.metrics.record_delivery(time.monotonic() - t_tok)
-            n += 1
-            if ev.type in ("done", "error"):
+                now = time.monotonic()
+                for e in batch:
+                    t_tok = getattr(e, "t_tokens", 0.0)
+                    if t_tok:
+                        srv.metrics.record_delivery(now - t_tok)
+            n += len(batch)
+            if batch[-1].type in ("done", "error"):
                 break
             ev = await it.__anext__()
+            batch = [ev] + sreq.token_stream.take_ready()
         if fmt is not None:
             await resp.write(b"data: [DONE]\n\n")
         await resp.write_eof()

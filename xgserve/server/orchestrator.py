@@ -162,7 +162,8 @@ class InferenceServer:
         self._tasks = [asyncio.create_task(self._dispatch_loop(), name="dispatch"),
                        asyncio.create_task(self._sweeper_loop(), name="sweeper"),
                        asyncio.create_task(self._health_loop(), name="health"),
-                       asyncio.create_task(self._degradation_loop(), name="degradation")]
+                       asyncio.create_task(self._degradation_loop(), name="degradation"),
+                       asyncio.create_task(self._lag_loop(), name="loop-lag")]
         if self.cfg.batcher.mode == "static":
             self._tasks.append(asyncio.create_task(self._batch_loop(), name="batcher"))
         log.info("server ready: model=%s replicas=%d tp=%d", self.model_name, len(ids), self.cfg.worker.tp)
@@ -598,6 +599,14 @@ class InferenceServer:
             self._wake.set()
         else:
             log.error("replica %d failed to restart: %s", r.id, r.error)
+
+    async def _lag_loop(self, period: float = 0.02) -> None:
+        """Event-loop lag probe: everything on the serve path (outputs, SSE writes,
+        admission) runs on this loop, so a late wake-up is delay every stream sees."""
+        while True:
+            t = time.monotonic()
+            await asyncio.sleep(period)
+            self.metrics.record_loop_lag(max(0.0, time.monotonic() - t - period))
 
     async def _degradation_loop(self) -> None:
         while True:

@@ -53,6 +53,21 @@ class TokenStream:
                 return
             yield ev
 
+    def take_ready(self) -> list:
+        """Every event already queued, without waiting (stops at the end marker,
+        which it puts back): lets the SSE writer coalesce a backlog into one socket
+        write instead of one coroutine wake-up + write per token."""
+        out = []
+        while True:
+            try:
+                ev = self._q.get_nowait()
+            except asyncio.QueueEmpty:
+                return out
+            if ev is _END:
+                self._q.put_nowait(_END)
+                return out
+            out.append(ev)
+
 
 class TokenStreamer:
     def __init__(self):
