@@ -157,6 +157,27 @@ def run(a, url: str) -> dict:
     return _report(a, st, s0, s1)
 
 
+def _replica_delta(s0, s1, win) -> list:
+    """Per replica over the window: engine steps/s, mean tokens per step and, with
+    XGS_STEP_TIMING=1 in the server's env, host seconds per phase per step."""
+    out = []
+    r0 = {r["id"]: r.get("engine", {}) for r in s0.get("replicas", [])}
+    for r in s1.get("replicas", []):
+        e1, e0 = r.get("engine", {}), r0.get(r["id"], {})
+        if not e1 or not e0:
+            continue
+        steps = e1.get("steps", 0) - e0.get("steps", 0)
+        d = {"id": r["id"], "steps_per_s": round(steps / win, 2),
+             "gen_tokens_per_step": round((e1.get("generation_tokens", 0) - e0.get("generation_tokens", 0))
+                                          / max(1, steps), 2)}
+        for key in ("loop_time_s", "step_timing_s"):
+            if key in e1 and key in e0 and steps:
+                d[key.replace("_s", "_ms_per_step")] = {k: round(1000 * (v - e0[key].get(k, 0.0)) / steps, 4)
+                                                        for k, v in e1[key].items()}
+        out.append(d)
+    return out
+
+
 def _report(a, st, s0, s1) -> dict:
     win = st["t1"] - st["t0"]
     m0, m1 = s0["metrics"], s1["metrics"]
@@ -174,6 +195,7 @@ def _report(a, st, s0, s1) -> dict:
         "req_5_1_delivery_within_10ms": (dl.get("p99") is not None and dl["p99"] <= 10.0),
         "server_prompt_tokens_per_sec": round(dp / win, 2), "server_generation_tokens_per_sec": round(dg / win, 2),
         "event_loop_lag_ms": m1.get("event_loop_lag_ms"), "client_procs": a.procs,
+        "replica_window": _replica_delta(s0, s1, win),
         "model": s1.get("model"),
     }
 

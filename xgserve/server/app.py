@@ -426,6 +426,10 @@ def build_app(srv: InferenceServer) -> web.Application:
 
 def serve(srv: InferenceServer) -> None:
     """Blocking: run the HTTP server until SIGINT/SIGTERM, then shut down gracefully."""
+    import sys
+    # replica reader threads unpickle outputs; they must hand the GIL back to the
+    # event loop quickly (token delivery, Req 5.1), not after the default 5 ms
+    sys.setswitchinterval(0.0005)
     app = build_app(srv)
     web.run_app(app, host=srv.cfg.api.host, port=srv.cfg.api.port, handler_cancellation=True,
                 access_log=None, print=lambda *a: log.info(*a) if a else None)

@@ -151,9 +151,15 @@ class EngineLoop:
 
     def run(self) -> None:
         last_hb = 0.0
+        timing = bool(os.environ.get("XGS_STEP_TIMING")) and hasattr(self.engine, "enable_step_timing")
+        if timing:  # per-phase host time of the engine loop, reported with the heartbeat
+            self.engine.enable_step_timing()
+        loop_t = {"engine_step": 0.0, "emit": 0.0, "drain": 0.0, "idle": 0.0}
         while not self._stop:
             outs: list = []
+            ta = time.perf_counter()
             self._drain(outs)
+            loop_t["drain"] += time.perf_counter() - ta
             if self._stop:
                 break
             if self.engine.has_work():
@@ -181,17 +187,26 @@ class EngineLoop:
                         log.error("engine step failed: %s\n%s", e, traceback.format_exc())
                         outs += self._fail_inflight("inference_failed", f"Inference failed: {e}")
                 self.last_step_s = time.perf_counter() - t0
+                loop_t["engine_step"] += self.last_step_s
                 self.steps += 1
             else:
+                ti = time.perf_counter()
                 self._wake.wait(0.02)
                 self._wake.clear()
+                loop_t["idle"] += time.perf_counter() - ti
             if outs:
+                te = time.perf_counter()
                 self.emit("out", outs)
+                loop_t["emit"] += time.perf_counter() - te
             now = time.monotonic()
             if now - last_hb >= HEARTBEAT_S:
                 last_hb = now
                 st = self.engine.stats()
                 st["last_step_ms"] = 1000 * self.last_step_s
+                st["loop_steps"] = self.steps
+                if timing:
+                    st["loop_time_s"] = dict(loop_t)
+                    st["step_timing_s"] = self.engine.step_timing()
                 self.emit("hb", st)
         try:
             if hasattr(self.engine, "stop_followers"):
@@ -306,9 +321,18 @@ class InProcessReplica(Replica):
             self.thread.join(timeout)
 
 
-def _worker_main(spec: dict, rank: int, env: dict, cmd_q, out_q) -> None:
-    """Entry point of a replica process (one per GPU)."""
+def _worker_main(spec: dict, rank: int, env: dict, cmd_q, out_q, out_w=None) -> None:
+    """Entry point of a replica process (one per GPU).
+
+    Outputs and heartbeats go over `out_w` (a one-way pipe) written synchronously by
+    the engine-loop thread: an mp.Queue would pickle them on a feeder thread that
+    then holds the GIL when the loop thread returns from a GPU wait, stalling the
+    next launch by up to the interpreter's switch interval (measured: ~3-5 ms per
+    step at 64 streams). ready / fatal (any rank, rare) keep using `out_q`."""
+    import pickle
+    import sys
     os.environ.update(env)
+    sys.setswitchinterval(0.0005)  # the cmd reader thread must never hold the GIL for long
     logging.basicConfig(level=os.environ.get("XGS_LOG_LEVEL", "WARNING"),
                         format=f"[replica {env.get('XGS_REPLICA', '?')} rank {rank}] %(levelname)s %(message)s")
     try:
@@ -322,9 +346,12 @@ def _worker_main(spec: dict, rank: int, env: dict, cmd_q, out_q) -> None:
         if rank != 0:
             eng.follower_loop()
             return
+
         def emit(kind, payload):
             if kind == "out":  # plain tuples pickle ~3x faster than dataclass instances
-                out_q.put(("outp", [tuple(o.__dict__.values()) for o in payload]))
+                kind, payload = "outp", [tuple(o.__dict__.values()) for o in payload]
+            if out_w is not None and kind in ("outp", "hb"):
+                out_w.send_bytes(pickle.dumps((kind, payload), protocol=pickle.HIGHEST_PROTOCOL))
             else:
                 out_q.put((kind, payload))
 
@@ -365,32 +392,46 @@ class ProcessReplica(Replica):
         import multiprocessing as mp
         ctx = mp.get_context("spawn")
         self.cmd_q, self.out_q = ctx.Queue(), ctx.Queue()
+        out_r, out_w = ctx.Pipe(duplex=False)
         tp = self.spec.get("tp", 1)
         self.procs = []
         for k in range(tp):
             env = {"RANK": str(k), "WORLD_SIZE": str(tp), "LOCAL_RANK": str(self.gpus[k]),
                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(self.master_port), "XGS_REPLICA": str(self.id),
                    "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
-            p = ctx.Process(target=_worker_main, args=(self.spec, k, env, self.cmd_q if k == 0 else None, self.out_q),
+            p = ctx.Process(target=_worker_main, args=(self.spec, k, env, self.cmd_q if k == 0 else None, self.out_q,
+                                                       out_w if k == 0 else None),
                             daemon=True, name=f"xgs-r{self.id}-tp{k}")
             p.start()
             self.procs.append(p)
+        out_w.close()  # the child holds the write end; EOF on its death ends the pipe reader
 
-        def reader():
+        def reader():  # ready / fatal
             while True:
                 try:
                     kind, payload = self.out_q.get()
-                except (EOFError, OSError):
+                except (EOFError, OSError, ValueError):
                     return
-                if kind == "outp":
-                    from ..engine.request import RequestOutput
-                    kind, payload = "out", [RequestOutput(*t) for t in payload]
                 self._event(kind, payload)
                 if kind == "fatal":
                     return
 
+        def pipe_reader():  # outputs + heartbeats
+            import pickle
+            from ..engine.request import RequestOutput
+            while True:
+                try:
+                    kind, payload = pickle.loads(out_r.recv_bytes())
+                except (EOFError, OSError):
+                    return
+                if kind == "outp":
+                    kind, payload = "out", [RequestOutput(*t) for t in payload]
+                self._event(kind, payload)
+
         self._reader = threading.Thread(target=reader, daemon=True, name=f"replica-{self.id}-reader")
         self._reader.start()
+        self._pipe_reader = threading.Thread(target=pipe_reader, daemon=True, name=f"replica-{self.id}-outputs")
+        self._pipe_reader.start()
 
     def _send(self, cmd):
         if self.cmd_q is not None:
