@@ -10,7 +10,7 @@ namespace xgs {
 // ---------------------------------------------------------------------------
 // BlockAllocator
 // ---------------------------------------------------------------------------
-BlockAllocator::BlockAllocator(int num_blocks) : n_(num_blocks), ref_(num_blocks, 0) {
+BlockAllocator::BlockAllocator(int num_blocks) : n_(num_blocks), ref_(num_blocks, 0), cached_(num_blocks, 0) {
   free_.reserve(num_blocks);
   // Pop order ascending page id: keeps early pages (and their TLB entries) hot.
   for (int i = num_blocks - 1; i >= 0; --i) free_.push_back(i);
@@ -26,12 +26,21 @@ int BlockAllocator::alloc() {
 
 void BlockAllocator::incref(int b) {
   if (b < 0 || b >= n_ || ref_[b] <= 0) throw std::runtime_error("incref on a free page");
+  if (cached_[b] && ref_[b] == 1) --n_evictable_;
   ++ref_[b];
 }
 
 void BlockAllocator::decref(int b) {
   if (b < 0 || b >= n_ || ref_[b] <= 0) throw std::runtime_error("decref on a free page");
   if (--ref_[b] == 0) free_.push_back(b);
+  else if (cached_[b] && ref_[b] == 1) ++n_evictable_;
+}
+
+void BlockAllocator::set_cached(int b, bool cached) {
+  if (b < 0 || b >= n_ || ref_[b] <= 0) throw std::runtime_error("set_cached on a free page");
+  if (cached == static_cast<bool>(cached_[b])) return;
+  cached_[b] = cached ? 1 : 0;
+  if (ref_[b] == 1) n_evictable_ += cached ? 1 : -1;
 }
 
 // ---------------------------------------------------------------------------
@@ -75,7 +84,7 @@ std::vector<int> PrefixCache::match(const int32_t* tokens, int n_tokens, int max
   for (int p = 0; p < pages; ++p) {
     RadixNode* c = find_child(cur, tokens + p * bs_);
     if (!c) break;
-    c->last_access = tick_;
+    touch(c);
     out.push_back(c->block);
     cur = c;
   }
@@ -106,13 +115,16 @@ int PrefixCache::insert(const int32_t* tokens, int n_tokens, const int* blocks, 
       node->parent = cur;
       node->last_access = tick_;
       alloc_->incref(blocks[p]);
+      alloc_->set_cached(blocks[p], true);
       c = node.get();
       by_block_[blocks[p]] = c;
+      if (cur != &root_ && cur->children.empty()) leaves_.erase({cur->last_access, cur});  // no longer a leaf
       cur->children[hash_page(t, bs_)].push_back(std::move(node));
+      leaves_.insert({c->last_access, c});
       ++stats_.entries;
       ++added;
     } else {
-      c->last_access = tick_;
+      touch(c);
     }
     cur = c;
   }
@@ -120,63 +132,62 @@ int PrefixCache::insert(const int32_t* tokens, int n_tokens, const int* blocks, 
   return added;
 }
 
-void PrefixCache::collect_leaves(RadixNode* n, std::vector<RadixNode*>& out) const {
-  for (auto& kv : n->children)
-    for (auto& c : kv.second) {
-      if (c->children.empty())
-        out.push_back(c.get());
-      else
-        collect_leaves(c.get(), out);
-    }
+void PrefixCache::touch(RadixNode* n) {
+  if (n->last_access == tick_) return;
+  const bool leaf = n->children.empty();
+  if (leaf) leaves_.erase({n->last_access, n});
+  n->last_access = tick_;
+  if (leaf) leaves_.insert({n->last_access, n});
 }
 
 void PrefixCache::remove_leaf(RadixNode* leaf) {
   RadixNode* par = leaf->parent;
+  leaves_.erase({leaf->last_access, leaf});
   uint64_t h = hash_page(leaf->key.data(), bs_);
   auto it = par->children.find(h);
   auto& vec = it->second;
   int block = leaf->block;
   for (size_t i = 0; i < vec.size(); ++i) {
     if (vec[i].get() == leaf) {
-      vec.erase(vec.begin() + i);
+      vec.erase(vec.begin() + i);  // destroys the node
       break;
     }
   }
   if (vec.empty()) par->children.erase(it);
+  if (par != &root_ && par->children.empty()) leaves_.insert({par->last_access, par});  // became a leaf
   by_block_.erase(block);
+  alloc_->set_cached(block, false);
   alloc_->decref(block);
   --stats_.entries;
   ++stats_.eviction_count;
 }
 
 int PrefixCache::evict(int n) {
-  if (n <= 0) return 0;
-  using E = std::pair<uint64_t, RadixNode*>;
-  auto cmp = [](const E& a, const E& b) { return a.first > b.first; };
-  std::priority_queue<E, std::vector<E>, decltype(cmp)> heap(cmp);
-  std::vector<RadixNode*> leaves;
-  collect_leaves(&root_, leaves);
-  for (RadixNode* l : leaves)
-    if (alloc_->refcount(l->block) == 1) heap.push({l->last_access, l});
+  // oldest leaves first; a parent that becomes a leaf joins the index at its own
+  // (older or newer) access time, so sweep again while a pass made progress
   int done = 0;
-  while (done < n && !heap.empty()) {
-    RadixNode* l = heap.top().second;
-    heap.pop();
-    RadixNode* par = l->parent;
-    remove_leaf(l);
-    ++done;
-    if (par != &root_ && par->children.empty() && alloc_->refcount(par->block) == 1)
-      heap.push({par->last_access, par});
+  bool progress = true;
+  while (done < n && progress) {
+    progress = false;
+    for (auto it = leaves_.begin(); done < n && it != leaves_.end();) {
+      RadixNode* l = it->second;
+      if (alloc_->refcount(l->block) != 1) {  // still used by a live sequence
+        ++it;
+        continue;
+      }
+      ++it;  // remove_leaf erases l (and may insert its parent) -- advance first
+      const uint64_t next_key = it != leaves_.end() ? it->first : UINT64_MAX;
+      RadixNode* next_node = it != leaves_.end() ? it->second : nullptr;
+      remove_leaf(l);
+      ++done;
+      progress = true;
+      it = next_node ? leaves_.find({next_key, next_node}) : leaves_.end();
+    }
   }
   return done;
 }
 
-int PrefixCache::evictable() const {
-  int n = 0;
-  for (const auto& kv : by_block_)
-    if (alloc_->refcount(kv.first) == 1) ++n;
-  return n;
-}
+int PrefixCache::evictable() const { return alloc_->num_evictable(); }
 
 void PrefixCache::enforce_limit() {
   int excess = static_cast<int>(stats_.entries) - max_cached_;
@@ -197,8 +208,12 @@ void PrefixCache::clear() {
         stack.push_back(c.get());
       }
   }
-  for (RadixNode* n : all) alloc_->decref(n->block);
+  for (RadixNode* n : all) {
+    alloc_->set_cached(n->block, false);
+    alloc_->decref(n->block);
+  }
   stats_.eviction_count += static_cast<int64_t>(all.size());
+  leaves_.clear();
   root_.children.clear();
   by_block_.clear();
   stats_.entries = 0;

@@ -18,7 +18,9 @@
 
 #include <cstdint>
 #include <memory>
+#include <set>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 namespace xgs {
@@ -32,11 +34,17 @@ class BlockAllocator {
   int refcount(int b) const { return ref_[b]; }
   int num_free() const { return static_cast<int>(free_.size()); }
   int num_blocks() const { return n_; }
+  // Prefix-cache membership: a cached page whose only reference is the cache's is
+  // evictable; the count is kept up to date on every refcount transition (O(1)).
+  void set_cached(int b, bool cached);
+  int num_evictable() const { return n_evictable_; }
 
  private:
   int n_;
   std::vector<int> free_;
   std::vector<int> ref_;
+  std::vector<uint8_t> cached_;
+  int n_evictable_ = 0;
 };
 
 struct RadixNode {
@@ -88,9 +96,9 @@ class PrefixCache {
  private:
   static uint64_t hash_page(const int32_t* t, int n);
   RadixNode* find_child(RadixNode* n, const int32_t* t) const;
-  void collect_leaves(RadixNode* n, std::vector<RadixNode*>& out) const;
   void remove_leaf(RadixNode* leaf);
   void enforce_limit();
+  void touch(RadixNode* n);  // last_access = tick_, keeping the leaf index ordered
 
   BlockAllocator* alloc_;
   int bs_;
@@ -99,6 +107,10 @@ class PrefixCache {
   uint64_t tick_ = 0;
   PrefixCacheStats stats_;
   std::unordered_map<int, RadixNode*> by_block_;
+  // every leaf ordered by (last_access, node): LRU eviction walks it from the front,
+  // skipping leaves still referenced by a sequence (at most one tail page per live
+  // sequence), so eviction costs O(log n) per page instead of a whole-tree walk
+  std::set<std::pair<uint64_t, RadixNode*>> leaves_;
 };
 
 }  // namespace xgs

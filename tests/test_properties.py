@@ -303,6 +303,60 @@ def test_prop10_memory_limit_enforced():
     assert c.stats()["entries"] <= 8
 
 
+@S
+@given(st.lists(st.tuples(st.integers(0, 5), st.integers(1, 4), st.booleans()), min_size=1, max_size=40),
+       st.integers(1, 30))
+def test_prop10_evictable_count_and_lru_order_under_sharing(ops_, n_evict):
+    """Branching prefixes, some pages still referenced by 'sequences': the O(1)
+    evictable count equals a brute-force count, eviction never frees a page a
+    sequence holds, and it frees leaves oldest-access first."""
+    a = R.BlockAllocator(512)
+    c = R.PrefixCache(a, 4, 512)
+    held = []
+    for i, (branch, pages, keep) in enumerate(ops_):
+        toks = [branch] * 4 + [1000 + i * 10 + j for j in range(4 * (pages - 1))]
+        blocks = c.match(toks, len(toks), False)
+        for b in blocks:
+            a.incref(b)
+        while len(blocks) < pages:
+            blocks.append(a.alloc())
+        c.insert(toks, blocks)
+        for b in blocks:
+            if keep:
+                held.append(b)
+            else:
+                a.decref(b)
+    cached = [b for b in range(512) if c.last_access_of(b) > 0]
+    assert c.evictable() == sum(1 for b in cached if a.refcount(b) == 1)
+    ev = c.evict(n_evict)
+    assert all(a.refcount(b) >= 1 for b in held)  # pages a sequence holds survive
+    cached2 = [b for b in range(512) if c.last_access_of(b) > 0]
+    assert len(cached) - len(cached2) == ev
+    assert c.evictable() == sum(1 for b in cached2 if a.refcount(b) == 1)
+
+
+def test_eviction_scales_with_cache_size():
+    """A full 64K-page cache: single-page evictions (what every page allocation
+    does once the pool is full) must not walk the tree -- 2000 of them well under a
+    second (a whole-tree walk per eviction would take minutes)."""
+    import time
+    n = 1 << 16
+    a = R.BlockAllocator(n)
+    c = R.PrefixCache(a, 16, n)
+    for s_ in range(n // 32):  # 2048 sequences x 32 pages
+        toks = [s_ * 7 + 1] + list(range(2, 16 * 32 + 1))
+        blocks = [a.alloc() for _ in range(32)]
+        c.insert(toks, blocks)
+        for b in blocks:
+            a.decref(b)
+    assert c.evictable() == n and a.num_free() == 0
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        assert c.evict(1) == 1
+    assert time.perf_counter() - t0 < 1.0
+    assert c.evictable() == n - 2000 and a.num_free() == 2000
+
+
 # ----------------------------------------------------------------------------- KV serialisation (Property 12)
 @S
 @given(st.integers(1, 3), st.integers(0, 4), st.sampled_from(["bfloat16", "float16", "float32"]), st.integers(0, 9999))
