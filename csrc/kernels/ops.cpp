@@ -43,7 +43,7 @@ int rope_cache(uint16_t*, int64_t, const int32_t*, const float*, uint16_t*, uint
 int decode_attention(const uint16_t*, int64_t, const uint16_t*, const uint16_t*, const int32_t*, int, const int32_t*,
                      float*, float*, uint16_t*, int64_t, int, int, int, int, int, float, int, int*, hipStream_t);
 int prefill_attention(const uint16_t*, int64_t, const uint16_t*, const uint16_t*, const int32_t*, int, const int32_t*,
-                      const int32_t*, uint16_t*, int64_t, int, int, int, int, int, int, float, hipStream_t);
+                      const int32_t*, uint16_t*, int64_t, int, int, int, int, int, int, float, hipStream_t, int);
 void argmax_logprob(const void*, int, int64_t, int, int, int32_t*, float*, hipStream_t);
 void sample_tokens(const void*, int, int64_t, int, int, const float*, const float*, const int32_t*, const uint64_t*,
                    uint64_t, int32_t*, float*, hipStream_t);
@@ -165,12 +165,14 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("prefill_attention", [](uintptr_t q, int64_t qs, uintptr_t kc, uintptr_t vc, uintptr_t bt, int bts,
                                 uintptr_t qsl, uintptr_t sl, uintptr_t out, int64_t os, int ns, int maxq, int Hq,
-                                int Hkv, int D, int bs, float scale, uintptr_t st) {
+                                int Hkv, int D, int bs, float scale, uintptr_t st, int gh) {
     check(xgk::prefill_attention(P<const uint16_t>(q), qs, P<const uint16_t>(kc), P<const uint16_t>(vc),
                                  P<const int32_t>(bt), bts, P<const int32_t>(qsl), P<const int32_t>(sl),
-                                 P<uint16_t>(out), os, ns, maxq, Hq, Hkv, D, bs, scale, S(st)),
+                                 P<uint16_t>(out), os, ns, maxq, Hq, Hkv, D, bs, scale, S(st), gh),
           "prefill_attention");
-  });
+  }, py::arg("q"), py::arg("qs"), py::arg("kc"), py::arg("vc"), py::arg("bt"), py::arg("bts"), py::arg("qsl"),
+     py::arg("sl"), py::arg("out"), py::arg("os"), py::arg("ns"), py::arg("maxq"), py::arg("Hq"), py::arg("Hkv"),
+     py::arg("D"), py::arg("bs"), py::arg("scale"), py::arg("st"), py::arg("gh") = 0);
   m.def("argmax_logprob", [](uintptr_t logits, int is_f32, int64_t stride, int B, int V, uintptr_t tok, uintptr_t lp,
                              uintptr_t st) {
     xgk::argmax_logprob(P<const void>(logits), is_f32, stride, B, V, P<int32_t>(tok), P<float>(lp), S(st));

@@ -1,8 +1,12 @@
 // K5: varlen causal flash attention over the paged KV cache (prefill, chunked
 // prefill, prefix-cache hits, speculative verify), GQA.
 //
-// Grid (num_seqs * q_tiles, Hq); workgroup = 4 waves = 64 query rows (16 per
-// wave); KV streamed in 64-key tiles through LDS. Query chunk i of a sequence
+// Grid (num_seqs * q_tiles, Hkv * G / GH); workgroup = GH query heads of ONE kv
+// head x 64 query rows = 4*GH waves (16 rows per wave): the GH heads of a GQA group
+// share every K/V tile they stream (read from HBM once per group slice instead of
+// once per query head). KV streamed in 64-key tiles through a double-buffered LDS
+// ring: the next tile's registers land in the other buffer right after this tile's
+// MFMAs, so each tile costs one barrier. Query chunk i of a sequence
 // with ctx cached keys sits at absolute position ctx + i and sees keys
 // [0, ctx + i] -- the new chunk's K/V were already appended to the paged
 // cache by rope_cache, so prefix-cached and chunked prefill are one code path.
@@ -23,14 +27,16 @@
 
 namespace xgk {
 
-template <int D>
+template <int D, int GH = 1>
 struct PrefillCfg {
-  static constexpr int BM = 64;          // query rows per workgroup
+  static constexpr int BM = 64;          // query rows per workgroup (per head)
   static constexpr int BN = 64;          // keys per KV tile
   static constexpr int KK = D / 32;      // k-steps of S^T
   static constexpr int MT = D / 16;      // 16-dim tiles of O^T
   static constexpr int NCH = D / 8;      // 16-B chunks per row
-  static constexpr int LOADS = BN * NCH / 256;  // 16-B chunks per thread per tile (K and V each)
+  static constexpr int THREADS = 256 * GH;
+  static constexpr int LOADS = BN * NCH / THREADS;  // 16-B chunks per thread per tile (K and V each)
+  static_assert(LOADS >= 1 && BN * NCH % THREADS == 0, "tile chunks must split evenly over the workgroup");
 };
 
 template <int D>
@@ -42,28 +48,29 @@ __device__ __forceinline__ int v_swz(int row, int ch) {
   return ch ^ (((row & 7) << 1) & (PrefillCfg<D>::NCH - 1));
 }
 
-template <int D>
-__global__ void __launch_bounds__(256) prefill_attn_kernel(
+template <int D, int GH>
+__global__ void __launch_bounds__(256 * GH) prefill_attn_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
     const uint16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int bt_stride,
     const int32_t* __restrict__ qsl, const int32_t* __restrict__ seq_lens, uint16_t* __restrict__ out,
     int64_t out_stride, int Hq, int Hkv, int bs, float scale, int tiles_per_seq) {
-  using C = PrefillCfg<D>;
+  using C = PrefillCfg<D, GH>;
   const int s = blockIdx.x / tiles_per_seq;
   const int qt = tiles_per_seq - 1 - (blockIdx.x % tiles_per_seq);  // heavy (late) tiles first
-  const int h = blockIdx.y;
   const int q0 = qsl[s];
   const int qlen = qsl[s + 1] - q0;
   const int i0 = qt * C::BM;
   if (i0 >= qlen) return;
   const int L = seq_lens[s];
   const int ctx = L - qlen;
-  const int kvh = h / (Hq / Hkv);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid_all = threadIdx.x >> 6;
+  const int wid = wid_all & 3;                       // 16-row slice of the 64-row tile
+  const int h = blockIdx.y * GH + (wid_all >> 2);    // this wave's query head
+  const int kvh = (blockIdx.y * GH) / (Hq / Hkv);   // shared by the workgroup's GH heads
   const int g = lane >> 4, li = lane & 15;
 
-  __shared__ __attribute__((aligned(16))) uint16_t k_lds[C::BN * D];
-  __shared__ __attribute__((aligned(16))) uint16_t v_lds[C::BN * D];
+  // one LDS array (double-buffered K and V tiles): [buf][K | V][BN * D]
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * C::BN * D];
 
   // Q^T fragment for this wave's 16 rows: lane holds Q[row li][32kk + 8g + j]
   const int my_row = i0 + wid * 16 + li;  // query index within the chunk
@@ -85,7 +92,7 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(
   auto gload = [&](int tile) {
 #pragma unroll
     for (int it = 0; it < C::LOADS; ++it) {
-      const int ci = threadIdx.x + it * 256;
+      const int ci = threadIdx.x + it * C::THREADS;
       const int key = ci / C::NCH, ch = ci % C::NCH;
       const int kabs = tile * C::BN + key;
       if (kabs < L) {
@@ -100,10 +107,12 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(
       }
     }
   };
-  auto lstore = [&]() {
+  auto lstore = [&](int buf) {
+    uint16_t* k_lds = lds + buf * 2 * C::BN * D;
+    uint16_t* v_lds = k_lds + C::BN * D;
 #pragma unroll
     for (int it = 0; it < C::LOADS; ++it) {
-      const int ci = threadIdx.x + it * 256;
+      const int ci = threadIdx.x + it * C::THREADS;
       const int key = ci / C::NCH, ch = ci % C::NCH;
       st16(k_lds + key * D + k_swz<D>(key, ch) * 8, kr[it]);
       st16(v_lds + key * D + v_swz<D>(key, ch) * 8, vr[it]);
@@ -117,12 +126,14 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(
 
   if (ntiles > 0) {
     gload(0);
-    lstore();
+    lstore(0);
   }
   __syncthreads();
   for (int j = 0; j < ntiles; ++j) {
     if (j + 1 < ntiles) gload(j + 1);
     const int kv0 = j * C::BN;
+    const uint16_t* k_lds = lds + (j & 1) * 2 * C::BN * D;
+    const uint16_t* v_lds = k_lds + C::BN * D;
 
     // ---- S^T = K . Q^T : 4 subtiles of 16 keys
     f32x4_t sacc[4];
@@ -193,11 +204,10 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(
         o[mt] = mfma16x16x32(vfrag, pfrag, o[mt]);
       }
     }
+    // tile j+1 into the other buffer: its last readers (tile j-1) all passed the
+    // previous iteration's barrier, so one barrier per tile orders both hazards
+    if (j + 1 < ntiles) lstore((j + 1) & 1);
     __syncthreads();
-    if (j + 1 < ntiles) {
-      lstore();
-      __syncthreads();
-    }
   }
 
   // ---- epilogue: O[row li][16mt + 4g + r] = o[mt][r] / l
@@ -214,24 +224,46 @@ __global__ void __launch_bounds__(256) prefill_attn_kernel(
   }
 }
 
+// GQA grouping: GH query heads of one kv head per workgroup (4*GH waves). gh <= 0
+// picks the widest GH in {4, 2, 1} dividing the group size that still gives >= 256
+// workgroups (one per CU); measured (bench/prefill_bench.py, profiles/
+// r2_prefill_bench.jsonl): Llama-3-8B heads at L = 8192: GH 1 / 2 / 4 = 287 / 315 /
+// 443 TFLOP/s, L = 2048: 161 / 199 / 300; at L = 512 GH = 4 leaves CUs idle (66 vs
+// 88). D = 64 supports GH <= 2.
 int prefill_attention(const uint16_t* q, int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
                       const int32_t* bt, int bt_stride, const int32_t* qsl, const int32_t* seq_lens,
                       uint16_t* out, int64_t out_stride, int num_seqs, int max_q_len, int Hq, int Hkv, int D,
-                      int bs, float scale, hipStream_t st) {
+                      int bs, float scale, hipStream_t st, int gh) {
   if (num_seqs <= 0 || max_q_len <= 0) return 0;
   if (bs % 16 != 0 || Hq % Hkv != 0) return -1;
+  const int G = Hq / Hkv;
   const int tps = (max_q_len + 63) / 64;
-  dim3 grid(num_seqs * tps, Hq), block(256);
+  if (gh <= 0) {
+    gh = 1;
+    for (int c = (D == 64 ? 2 : 4); c > 1; c >>= 1)
+      if (G % c == 0 && static_cast<int64_t>(num_seqs) * tps * (Hq / c) >= 256) {
+        gh = c;
+        break;
+      }
+  }
+  if (G % gh != 0 || (gh != 1 && gh != 2 && gh != 4)) return -1;
+  dim3 grid(num_seqs * tps, Hq / gh), block(256 * gh);
+#define XGK_PF(DV, GV)                                                                                          \
+  hipLaunchKernelGGL((prefill_attn_kernel<DV, GV>), grid, block, 0, st, q, q_stride, kc, vc, bt, bt_stride, qsl, \
+                     seq_lens, out, out_stride, Hq, Hkv, bs, scale, tps)
   if (D == 128) {
-    hipLaunchKernelGGL(prefill_attn_kernel<128>, grid, block, 0, st, q, q_stride, kc, vc, bt, bt_stride, qsl,
-                       seq_lens, out, out_stride, Hq, Hkv, bs, scale, tps);
+    if (gh == 1) XGK_PF(128, 1);
+    else if (gh == 2) XGK_PF(128, 2);
+    else XGK_PF(128, 4);
     return 0;
   }
   if (D == 64) {
-    hipLaunchKernelGGL(prefill_attn_kernel<64>, grid, block, 0, st, q, q_stride, kc, vc, bt, bt_stride, qsl,
-                       seq_lens, out, out_stride, Hq, Hkv, bs, scale, tps);
+    if (gh == 1) XGK_PF(64, 1);
+    else if (gh == 2) XGK_PF(64, 2);
+    else return -1;
     return 0;
   }
+#undef XGK_PF
   return -1;
 }
 

@@ -134,9 +134,11 @@ def test_decode_attention_zero_len_rows():
     assert out[0].float().abs().max().item() == 0.0
 
 
-@pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 1, 128), (12, 12, 64)])
+@pytest.mark.parametrize("Hq,Hkv,D,gh", [(32, 8, 128, 0), (32, 8, 128, 1), (32, 8, 128, 4), (8, 1, 128, 2),
+                                         (8, 1, 128, 4), (12, 12, 64, 0), (16, 4, 64, 2)])
 @pytest.mark.parametrize("qlens,ctxs", [([100], [0]), ([64, 1, 130, 7], [0, 5, 40, 300]), ([5, 5], [1000, 17])])
-def test_prefill_attention(Hq, Hkv, D, qlens, ctxs):
+def test_prefill_attention(Hq, Hkv, D, gh, qlens, ctxs):
+    """gh = query heads of one GQA group per workgroup (0: the kernel's default)."""
     bs = 16
     lens = [q + c for q, c in zip(qlens, ctxs)]
     kc, vc, bt = _paged(lens, Hkv, D, bs)
@@ -146,7 +148,7 @@ def test_prefill_attention(Hq, Hkv, D, qlens, ctxs):
     qsl = torch.tensor([0] + list(torch.cumsum(torch.tensor(qlens), 0)), dtype=torch.int32, device=DEV)
     sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
     scale = 1.0 / math.sqrt(D)
-    out = ops.prefill_attention(q, kc, vc, bt, qsl, sl, max(qlens), scale)
+    out = ops.prefill_attention(q, kc, vc, bt, qsl, sl, max(qlens), scale, gh=gh)
     ref = ops.prefill_attention_ref(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), qsl.cpu(), sl.cpu(), scale)
     torch.testing.assert_close(out.cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
 

@@ -172,9 +172,13 @@ def decode_attention_fused(pend, positions: torch.Tensor, slot_mapping: torch.Te
     return out
 
 
+# query heads of one GQA group per prefill workgroup (0: kernel default, 2 for even groups)
+PREFILL_GH = int(os.environ.get("XGS_PREFILL_GH", "0"))
+
+
 def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                       query_start_loc: torch.Tensor, seq_lens: torch.Tensor, max_q_len: int, scale: float,
-                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      out: Optional[torch.Tensor] = None, gh: Optional[int] = None) -> torch.Tensor:
     """q: [T, Hq, D] packed varlen (rows may be strided); causal w.r.t. absolute
     positions ctx+i where ctx = seq_len - q_len; keys read from the paged cache."""
     if not use_native(q):
@@ -192,5 +196,5 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
     kernels().prefill_attention(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                 block_tables.data_ptr(), block_tables.stride(0), query_start_loc.data_ptr(),
                                 seq_lens.data_ptr(), out.data_ptr(), out.stride(0), S, int(max_q_len), Hq, Hkv, D,
-                                bs, float(scale), stream_ptr())
+                                bs, float(scale), stream_ptr(), PREFILL_GH if gh is None else int(gh))
     return out
