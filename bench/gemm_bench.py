@@ -222,10 +222,12 @@ def moe_sweep(a):
             wv = 2 if cfg >= 4 else 4
             if (2 * F) % (32 * wv):
                 continue
-            fn = lambda w, cfg=cfg: k.moe_gemm_m64g_rows(  # noqa: E731
-                x.data_ptr(), rows.data_ptr(), offs.data_ptr(), E, H, w.data_ptr(), 2 * F, P, 0, act.data_ptr(), 1, 2, 2,
-                cfg, 2 * T, st)
-            res.append(("w13", timeit([lambda w=w, fn=fn: fn(w) for w in w13s]), 2, 1, cfg))
+            for vd in (0, 1):
+                fn = lambda w, cfg=cfg, vd=vd: k.moe_gemm_m64g_rows(  # noqa: E731
+                    x.data_ptr(), rows.data_ptr(), offs.data_ptr(), E, H, w.data_ptr(), 2 * F, P, 0, act.data_ptr(), 1,
+                    2, 2, cfg, 2 * T, st, rows.data_ptr() if vd else 0)
+                res.append(("w13" + ("+rowdispatch" if vd else ""), timeit([lambda w=w, fn=fn: fn(w) for w in w13s]),
+                            2, 1, cfg))
         for cfg in range(7):
             wv = 2 if cfg >= 4 else 4
             kc = 64 if cfg in (2, 3, 4, 5) else 128
@@ -234,11 +236,13 @@ def moe_sweep(a):
                     if H % (16 * nw * wv) or F % (S * kc):
                         continue
                     part = torch.empty(S, P, H, dtype=torch.float32, device="cuda")
-                    fn = lambda w, cfg=cfg, nw=nw, S=S, part=part: k.moe_gemm_m64g_rows(  # noqa: E731
-                        act.data_ptr(), 0, offs.data_ptr(), E, F, w.data_ptr(), H, P, part.data_ptr(), 0, S, 1, nw, cfg,
-                        2 * T, st)
-                    res.append(("w2", timeit([lambda w=w, fn=fn: fn(w) for w in w2s]), nw, S, cfg))
-        for name in ("w13", "w2"):
+                    for vd in (0, 1):
+                        fn = lambda w, cfg=cfg, nw=nw, S=S, part=part, vd=vd: k.moe_gemm_m64g_rows(  # noqa: E731
+                            act.data_ptr(), 0, offs.data_ptr(), E, F, w.data_ptr(), H, P, part.data_ptr(), 0, S, 1, nw,
+                            cfg, 2 * T, st, rows.data_ptr() if vd else 0)
+                        res.append(("w2" + ("+rowdispatch" if vd else ""),
+                                    timeit([lambda w=w, fn=fn: fn(w) for w in w2s]), nw, S, cfg))
+        for name in ("w13", "w13+rowdispatch", "w2", "w2+rowdispatch"):
             for us, nw, S, cfg in sorted((r[1], r[2], r[3], r[4]) for r in res if r[0] == name)[:8]:
                 print(json.dumps({"moe": name, "T": T, "P": P, "nw": nw, "S": S, "cfg": cfg, "us": round(us, 2)}),
                       flush=True)

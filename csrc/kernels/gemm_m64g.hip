@@ -353,46 +353,22 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   }
 }
 
-// Grouped (MoE) form of the same pipeline: W [E, N, K]; x rows gathered through
-// the block-64 padded expert-sorted layout (rows[p] = source row, -1 = pad;
-// rows == nullptr: x already in padded layout); offs[E+1] padded segment starts.
-// Grid (column tiles, k-splits, P / 64 row tiles): one workgroup per row tile, so
-// an expert's row tiles run concurrently -- the column tiles of one row tile
-// (N / cols <= a few hundred) are fewer than the resident workgroups, so the
-// next row tiles of the same weight tile are in flight together and re-read it
-// from L2/MALL (a per-expert loop over row tiles serialised them). The column
-// tile stays the fastest dimension: consecutive workgroups spread over the 8 XCDs
-// (row-tile-fastest put a batch-1 step's two active experts on 2 XCDs). Row tiles
-// past the last expert's segment (capacity padding) exit at once.
 template <int NW, int WV, int KC, bool NT, int MT>
-__global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uint16_t* __restrict__ x,
-                                                                       const int32_t* __restrict__ rows,
-                                                                       const int32_t* __restrict__ offs, int E,
-                                                                       int K, const uint16_t* __restrict__ w, int N,
-                                                                       int P, float* __restrict__ part,
-                                                                       uint16_t* __restrict__ out, int mode) {
+__device__ __forceinline__ void grouped_body(const uint16_t* __restrict__ x, const int32_t* __restrict__ rows, int e,
+                                             int p0, int p1, int rt0, int K, const uint16_t* __restrict__ w, int N,
+                                             int P, float* __restrict__ part, uint16_t* __restrict__ out, int mode,
+                                             uint8_t* lds0, uint8_t* lds1, uint8_t* lds2) {
   constexpr int RB = KC * 2;
   constexpr int GPR = KC / 8;
   constexpr int RPI = 1024 / RB;
-  constexpr int XROWS = 16 * MT;  // MT = 1: <= 16 real rows per expert (batch <= 8 at top-2)
+  constexpr int XROWS = 16 * MT;
   constexpr int XBYTES = XROWS * RB;
   constexpr int XI = XROWS / RPI / WV;
   constexpr int WROWS = 16 * NW;
   constexpr int WI = WROWS / RPI;
   constexpr int WBYTES = WROWS * RB;
-  constexpr int SLOT = XBYTES + WV * WBYTES;
   constexpr int G = XI + WI;
   static_assert(XI >= 1 && WI >= 1 && XROWS % (RPI * WV) == 0, "bad m64g geometry");
-  __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
-  __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
-  __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
-
-  const int rt0 = blockIdx.z * 64;
-  int e = -1;
-  for (int i = 0; i < E; ++i)
-    if (rt0 >= offs[i] && rt0 < offs[i + 1]) e = i;
-  if (e < 0) return;  // capacity padding past the last segment
-  const int p0 = offs[e], p1 = offs[e + 1];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int S = gridDim.y, s = blockIdx.y;
@@ -519,6 +495,66 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
   }
 }
 
+// Grouped (MoE) form of the same pipeline: W [E, N, K]; x rows gathered through
+// the block-64 padded expert-sorted layout (rows[p] = source row, -1 = pad;
+// rows == nullptr: x already in padded layout); offs[E+1] padded segment starts.
+// Grid (column tiles, k-splits, P / 64 row tiles): one workgroup per row tile, so
+// an expert's row tiles run concurrently -- the column tiles of one row tile
+// (N / cols <= a few hundred) are fewer than the resident workgroups, so the
+// next row tiles of the same weight tile are in flight together and re-read it
+// from L2/MALL (a per-expert loop over row tiles serialised them). The column
+// tile stays the fastest dimension: consecutive workgroups spread over the 8 XCDs
+// (row-tile-fastest put a batch-1 step's two active experts on 2 XCDs). Row tiles
+// past the last expert's segment (capacity padding) exit at once.
+// Row-occupancy dispatch: `valid` (the sorted rows, -1 = pad) tells each workgroup
+// how many of its 64 rows are real; it runs the 16-, 32- or 64-row body (MT_MAX
+// caps it), so a decode step's ~16-30 rows per expert stage and multiply 1-2 x
+// sub-tiles instead of 4 -- the x tile is re-read from L2 by every one of an
+// expert's column tiles (448 for Mixtral w13), as many bytes as the weights.
+// Rows past the body's 16*MT are never written (pads only: w2 runs the same body
+// on the same rows, so it never reads them either).
+template <int NW, int WV, int KC, bool NT, int MT_MAX>
+__global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uint16_t* __restrict__ x,
+                                                                       const int32_t* __restrict__ rows,
+                                                                       const int32_t* __restrict__ offs,
+                                                                       const int32_t* __restrict__ valid, int E,
+                                                                       int K, const uint16_t* __restrict__ w, int N,
+                                                                       int P, float* __restrict__ part,
+                                                                       uint16_t* __restrict__ out, int mode) {
+  constexpr int SLOT = 16 * MT_MAX * KC * 2 + WV * 16 * NW * KC * 2;
+  __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
+  __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
+  __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
+  const int rt0 = blockIdx.z * 64;
+  int e = -1;
+  for (int i = 0; i < E; ++i)
+    if (rt0 >= offs[i] && rt0 < offs[i + 1]) e = i;
+  if (e < 0) return;  // capacity padding past the last segment
+  const int p0 = offs[e], p1 = offs[e + 1];
+  int amt = MT_MAX;
+  if (valid != nullptr && MT_MAX > 1) {
+    const int t = threadIdx.x;
+    const int real = __syncthreads_count(t < 64 && rt0 + t < p1 && valid[rt0 + t] >= 0);
+    amt = (real + 15) / 16;
+  }
+  constexpr int RPI = 1024 / (KC * 2);
+  constexpr bool MT1_OK = (16 / RPI / WV) >= 1;  // one 16-row x sub-tile is >= one DMA per wave
+  if constexpr (MT_MAX >= 4) {
+    if (amt > 2) {
+      grouped_body<NW, WV, KC, NT, 4>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2);
+      return;
+    }
+  }
+  if constexpr (MT_MAX >= 2) {
+    if (amt == 2 || !MT1_OK) {
+      grouped_body<NW, WV, KC, NT, 2>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2);
+      return;
+    }
+  }
+  if constexpr (MT1_OK)
+    grouped_body<NW, WV, KC, NT, 1>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2);
+}
+
 // M <= 16 takes the one-x-tile kernel (MT = 1) except for the 4-wave KC-64 configs,
 // whose 16 x rows would be less than one DMA instruction per wave.
 // XGS_M64G_MT1=0 keeps MT = 4 everywhere (A/B).
@@ -532,17 +568,17 @@ static bool m64g_mt1_enabled() {
 
 template <int NW>
 static void launch_m64g_grouped(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, const int32_t* rows,
-                                const int32_t* offs, int E, int K, const uint16_t* w, int N, int P, float* part,
-                                uint16_t* out, int mode, bool mt1) {
+                                const int32_t* offs, const int32_t* valid, int E, int K, const uint16_t* w, int N,
+                                int P, float* part, uint16_t* out, int mode, bool mt1) {
 #define XGK_GRP_MT(WV, KC, NT, MT)                                                                              \
-  hipLaunchKernelGGL((gemm_m64g_grouped_kernel<NW, WV, KC, NT, MT>), grid, dim3(64 * WV), 0, st, x, rows, offs, E, \
-                     K, w, N, P, part, out, mode)
+  hipLaunchKernelGGL((gemm_m64g_grouped_kernel<NW, WV, KC, NT, MT>), grid, dim3(64 * WV), 0, st, x, rows, offs, \
+                     valid, E, K, w, N, P, part, out, mode)
 #define XGK_GRP(WV, KC, NT)              \
   do {                                   \
     if (mt1) XGK_GRP_MT(WV, KC, NT, 1);  \
     else XGK_GRP_MT(WV, KC, NT, 4);      \
   } while (0)
-  // the 4-wave KC-64 configs have < 1 x DMA instruction per wave at 16 rows: MT = 4
+  // the 4-wave KC-64 configs have < 1 x DMA instruction per wave at 16 rows: MT >= 2
   switch (cfg) {
     case 1: XGK_GRP(4, 128, true); break;
     case 2: XGK_GRP_MT(4, 64, false, 4); break;
@@ -561,8 +597,10 @@ int m64g_cfg_kc(int cfg);
 
 // max_rows: a bound on the real rows of any expert (<= 16 selects the one-x-tile
 // kernel; rows 16..63 of each padded tile are then left unwritten -- pads only).
+// valid: the sorted rows (-1 = pad) for the row-occupancy dispatch, or nullptr (all 64 rows).
 int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, int E, int K, const uint16_t* w, int N,
-                  int P, float* part, uint16_t* out, int S, int mode, int nw, int cfg, int max_rows, hipStream_t st) {
+                  int P, float* part, uint16_t* out, int S, int mode, int nw, int cfg, int max_rows, hipStream_t st,
+                  const int32_t* valid) {
   if (E < 1 || P < 0 || P % 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 6) return 1;
   if (mode != GG_BF16 && mode != GG_PARTIAL && mode != GG_SILU) return 1;
   const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
@@ -573,8 +611,8 @@ int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, i
   if (P == 0) return 0;
   const dim3 grid(N / cols, S, P / 64);
   const bool mt1 = max_rows <= 16 && cfg != 2 && cfg != 3 && m64g_mt1_enabled();
-  if (nw == 1) launch_m64g_grouped<1>(cfg, grid, st, x, rows, offs, E, K, w, N, P, part, out, mode, mt1);
-  else launch_m64g_grouped<2>(cfg, grid, st, x, rows, offs, E, K, w, N, P, part, out, mode, mt1);
+  if (nw == 1) launch_m64g_grouped<1>(cfg, grid, st, x, rows, offs, valid, E, K, w, N, P, part, out, mode, mt1);
+  else launch_m64g_grouped<2>(cfg, grid, st, x, rows, offs, valid, E, K, w, N, P, part, out, mode, mt1);
   return 0;
 }
 

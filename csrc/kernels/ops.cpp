@@ -32,7 +32,7 @@ int decode_attention_fq(const float*, int, const int32_t*, const float*, const i
                         const int32_t*, int, const int32_t*, float*, float*, uint16_t*, int64_t, int, int, int, int,
                         int, float, int, int, int*, const void*, int64_t, int, hipStream_t);
 int moe_gemm_m64g(const uint16_t*, const int32_t*, const int32_t*, int, int, const uint16_t*, int, int, float*,
-                  uint16_t*, int, int, int, int, int, hipStream_t);
+                  uint16_t*, int, int, int, int, int, hipStream_t, const int32_t*);
 void add_partials_rmsnorm(const float*, int, int, uint16_t*, const uint16_t*, uint16_t*, int, float, hipStream_t);
 void reduce_partials(const float*, int, int64_t, uint16_t*, hipStream_t);
 int rope_cache_partials(const float*, int, uint16_t*, int64_t, const int32_t*, const float*, uint16_t*, uint16_t*,
@@ -278,18 +278,21 @@ PYBIND11_MODULE(_kernels, m) {
                             uintptr_t part, uintptr_t out, int splits, int mode, int nw, int cfg, uintptr_t st) {
     check(xgk::moe_gemm_m64g(P<const uint16_t>(x), P<const int32_t>(rows), P<const int32_t>(offs), E, K,
                              P<const uint16_t>(w), N, P_, P<float>(part), P<uint16_t>(out), splits, mode, nw, cfg,
-                             64, S(st)),
+                             64, S(st), nullptr),
           "moe_gemm_m64g");
   });
   // same, with a host-known bound on the real rows of any expert (<= 16: one-x-tile kernel)
+  // valid: the sorted rows (-1 = pad) -> per-workgroup 16/32/64-row body; 0: all rows
   m.def("moe_gemm_m64g_rows", [](uintptr_t x, uintptr_t rows, uintptr_t offs, int E, int K, uintptr_t w, int N, int P_,
                                  uintptr_t part, uintptr_t out, int splits, int mode, int nw, int cfg, int max_rows,
-                                 uintptr_t st) {
+                                 uintptr_t st, uintptr_t valid) {
     check(xgk::moe_gemm_m64g(P<const uint16_t>(x), P<const int32_t>(rows), P<const int32_t>(offs), E, K,
                              P<const uint16_t>(w), N, P_, P<float>(part), P<uint16_t>(out), splits, mode, nw, cfg,
-                             max_rows, S(st)),
+                             max_rows, S(st), P<const int32_t>(valid)),
           "moe_gemm_m64g_rows");
-  });
+  }, py::arg("x"), py::arg("rows"), py::arg("offs"), py::arg("E"), py::arg("K"), py::arg("w"), py::arg("N"),
+     py::arg("P"), py::arg("part"), py::arg("out"), py::arg("splits"), py::arg("mode"), py::arg("nw"), py::arg("cfg"),
+     py::arg("max_rows"), py::arg("st"), py::arg("valid") = 0);
   m.def("moe_route", [](uintptr_t h, uintptr_t wr, int T, int H, int E, int k, int renorm, uintptr_t w, uintptr_t ids,
                         uintptr_t st) {
     check(xgk::moe_route(P<const uint16_t>(h), P<const uint16_t>(wr), T, H, E, k, renorm, P<float>(w),

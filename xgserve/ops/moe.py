@@ -23,6 +23,7 @@ MOE_CFG_W2 = 1
 # an expert's tiles sharing its weight stream through L2/MALL) is faster
 # (2,680 vs 2,638 tok/s); XGS_MOE_DENSE_MIN_PAIRS=256 turns it on.
 import os as _os
+MOE_ROW_DISPATCH = _os.environ.get("XGS_MOE_ROW_DISPATCH", "1") != "0"
 MOE_DENSE_MIN_PAIRS = int(_os.environ.get("XGS_MOE_DENSE_MIN_PAIRS", str(1 << 30)))
 
 
@@ -119,9 +120,11 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     kn = kernels()
     if MOE_GLDS:
         max_rows = T * k  # no expert holds more rows than (token, choice) pairs
+        # per-workgroup real-row count -> 16 / 32 / 64-row body (MOE_ROW_DISPATCH=0: always 64)
+        valid = sorted_rows.data_ptr() if MOE_ROW_DISPATCH else 0
 
         def gemm(*a, cfg=0):
-            kn.moe_gemm_m64g_rows(*a[:-1], cfg, max_rows, a[-1])
+            kn.moe_gemm_m64g_rows(*a[:-1], cfg, max_rows, a[-1], valid)
     else:
         def gemm(*a, cfg=0):
             kn.moe_gemm_m64(*a)
