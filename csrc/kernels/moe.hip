@@ -12,7 +12,11 @@
 //   (the grouped expert GEMMs are gemm_m64_grouped in gemm_m64.hip: W [E, N, K]
 //    streamed once per step per column tile, fused SiLU-gate on w13)
 //   moe_combine      : out[t] = sum_j w[t, j] * y[dest[t*k + j]], y bf16 or
-//                      fp32 split-K partials of the w2 GEMM.
+//                      fp32 split-K partials of the w2 GEMM (also the EP source-side
+//                      unpermute: y = rows returned by the expert owners).
+//   ep_plan / ep_scatter : expert-parallel dispatch -- deterministic per-destination
+//                      slots (fixed-capacity or count-exact packed layout), local
+//                      expert ids for the owners, the row copy into the send buffer.
 #include "common.h"
 
 namespace xgk {
@@ -242,6 +246,121 @@ int moe_combine(const void* y, int S, int P, const int32_t* dest, const float* w
     case 4: hipLaunchKernelGGL(combine_kernel<4>, g, b, 0, st, y, S, P, dest, w, out, k, H); return 0;
     default: return 1;
   }
+}
+
+// ---------------------------------------------------------------- expert-parallel dispatch
+// (llama.py LlamaLayer._moe_alltoall: a rank routes its token slice and ships each
+// (token, choice) row to the rank owning that expert, rank r owning global experts
+// [r * E_local, (r + 1) * E_local).)
+//
+// ep_plan: ONE workgroup plans the whole dispatch. Pair i goes to d = ids[i] / E_local
+// at a stable, deterministic slot: slot[i] = base[d] + #{i' < i : d(i') = d}, where
+// base[d] = d * cap (fixed-capacity layout: a graph-capturable all_to_all with equal
+// splits) or the exclusive prefix of the per-destination counts (packed layout: the
+// count-exact all_to_all of eager steps). send_eid[slot] = the owner's LOCAL expert id;
+// unused capacity slots get -1, which the owner's moe_align skips (no padding rows
+// routed to any expert). counts[d] = pairs for rank d. Pairs with an out-of-range id
+// get slot -1 (never sent, never combined).
+// Each thread owns a contiguous chunk of pairs: per-destination counts in registers
+// -> block exclusive scan (wave shuffles + per-wave totals in LDS) -> second pass
+// assigns slots in pair order.
+constexpr int EP_MAX_RANKS = 8;
+constexpr int EP_PLAN_THREADS = 1024;
+
+__global__ void __launch_bounds__(EP_PLAN_THREADS) ep_plan_kernel(const int32_t* __restrict__ ids, int n_pairs,
+                                                                   int E_local, int tp, int cap, int packed,
+                                                                   int32_t* __restrict__ slot,
+                                                                   int32_t* __restrict__ send_eid,
+                                                                   int32_t* __restrict__ counts) {
+  constexpr int NWAVE = EP_PLAN_THREADS / 64;
+  __shared__ int wave_tot[EP_MAX_RANKS][NWAVE];
+  __shared__ int base_s[EP_MAX_RANKS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int chunk = (n_pairs + EP_PLAN_THREADS - 1) / EP_PLAN_THREADS;
+  const int i0 = min(n_pairs, tid * chunk), i1 = min(n_pairs, i0 + chunk);
+  const int n_eid = packed ? n_pairs : tp * cap;
+  if (!packed)
+    for (int s = tid; s < n_eid; s += EP_PLAN_THREADS) send_eid[s] = -1;
+  int cnt[EP_MAX_RANKS];
+#pragma unroll
+  for (int d = 0; d < EP_MAX_RANKS; ++d) cnt[d] = 0;
+  const int n_exp = E_local * tp;
+  for (int i = i0; i < i1; ++i) {
+    const int e = ids[i];
+    const int d = (e >= 0 && e < n_exp) ? e / E_local : -1;
+#pragma unroll
+    for (int q = 0; q < EP_MAX_RANKS; ++q) cnt[q] += (d == q);
+  }
+  // exclusive prefix over threads, per destination
+  int excl[EP_MAX_RANKS];
+#pragma unroll
+  for (int d = 0; d < EP_MAX_RANKS; ++d) {
+    int v = cnt[d];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(v, o, 64);
+      if (lane >= o) v += u;
+    }
+    excl[d] = v - cnt[d];
+    if (lane == 63) wave_tot[d][wid] = v;
+  }
+  __syncthreads();  // also orders the -1 fill before the slot writes below
+  if (tid == 0) {
+    int acc = 0;
+    for (int d = 0; d < EP_MAX_RANKS; ++d) {
+      int tot = 0;
+      for (int w = 0; w < NWAVE; ++w) tot += wave_tot[d][w];
+      base_s[d] = packed ? acc : d * cap;
+      if (d < tp) {
+        counts[d] = tot;
+        acc += tot;
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < EP_MAX_RANKS; ++d)
+    for (int w = 0; w < wid; ++w) excl[d] += wave_tot[d][w];
+  __syncthreads();
+  for (int i = i0; i < i1; ++i) {
+    const int e = ids[i];
+    const int d = (e >= 0 && e < n_exp) ? e / E_local : -1;
+    int s = -1;
+#pragma unroll
+    for (int q = 0; q < EP_MAX_RANKS; ++q)
+      if (d == q) s = base_s[q] + excl[q]++;
+    slot[i] = s;
+    if (s >= 0) send_eid[s] = e - d * E_local;
+  }
+}
+
+int ep_plan(const int32_t* ids, int n_pairs, int E_local, int tp, int cap, int packed, int32_t* slot, int32_t* send_eid,
+            int32_t* counts, hipStream_t st) {
+  if (tp < 1 || tp > EP_MAX_RANKS || E_local < 1 || n_pairs < 0 || (!packed && cap < 0)) return 1;
+  hipLaunchKernelGGL(ep_plan_kernel, dim3(1), dim3(EP_PLAN_THREADS), 0, st, ids, n_pairs, E_local, tp, cap, packed,
+                     slot, send_eid, counts);
+  return 0;
+}
+
+// ep_scatter: send[slot[i]] = x[i / k] (one wave per pair, 16-B vector copies).
+__global__ void __launch_bounds__(256) ep_scatter_kernel(const uint16_t* __restrict__ x, int64_t x_stride, int k,
+                                                         const int32_t* __restrict__ slot, int n_pairs, int H,
+                                                         uint16_t* __restrict__ send) {
+  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (pair >= n_pairs) return;
+  const int s = slot[pair];
+  if (s < 0) return;
+  const uint16_t* src = x + static_cast<int64_t>(pair / k) * x_stride;
+  uint16_t* dst = send + static_cast<int64_t>(s) * H;
+  for (int c = lane; c < H / 8; c += 64) st16(dst + 8 * c, ld16(src + 8 * c));
+}
+
+int ep_scatter(const uint16_t* x, int64_t x_stride, int k, const int32_t* slot, int n_pairs, int H, uint16_t* send,
+               hipStream_t st) {
+  if (n_pairs <= 0) return 0;
+  if (H % 8 || x_stride % 8 || k < 1) return 1;
+  hipLaunchKernelGGL(ep_scatter_kernel, dim3((n_pairs + 3) / 4), dim3(256), 0, st, x, x_stride, k, slot, n_pairs, H,
+                     send);
+  return 0;
 }
 
 

@@ -359,3 +359,59 @@ def test_fused_moe_prefill_per_expert_path(T, offset, monkeypatch):
     tol = 3e-2 * ref.std().item()
     torch.testing.assert_close(dense.cpu().float(), ref, atol=tol, rtol=3e-2)
     torch.testing.assert_close(dense.float(), grouped.float(), atol=tol, rtol=3e-2)
+
+
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("Ts,k,E_local,tp", [(1, 2, 4, 2), (37, 2, 4, 2), (64, 2, 2, 4), (700, 2, 1, 8), (5, 4, 2, 8)])
+def test_ep_dispatch_kernels_match_torch(Ts, k, E_local, tp, packed):
+    """ep_plan / ep_scatter / ep_combine (HIP) against their torch fallbacks: identical
+    slots, local expert ids and counts (the plan is deterministic), identical rows,
+    and the weighted combine against an fp32 loop."""
+    H = 512
+    ids = torch.randint(0, E_local * tp, (Ts, k), dtype=torch.int32)
+    cap = Ts * k
+    s_ref, e_ref, c_ref = ops.ep_plan(ids, E_local, tp, cap, packed)
+    s, e, c = ops.ep_plan(ids.to(DEV), E_local, tp, cap, packed)
+    assert torch.equal(s.cpu(), s_ref) and torch.equal(c.cpu(), c_ref) and torch.equal(e.cpu(), e_ref)
+    x = rnd(Ts, H)
+    rows = Ts * k if packed else tp * cap
+    send = ops.ep_scatter(x, k, s, rows)
+    src = torch.arange(Ts * k) // k
+    assert torch.equal(send[s.long()].cpu(), x.cpu()[src])
+    w = torch.rand(Ts, k, device=DEV)
+    back = rnd(rows, H)
+    out = torch.zeros(Ts + 3, H, dtype=torch.bfloat16, device=DEV)
+    ops.ep_combine(back, s, w, out)
+    want = (back.cpu().float()[s.long().cpu()] * w.cpu().reshape(-1, 1)).view(Ts, k, H).sum(1)
+    torch.testing.assert_close(out[:Ts].cpu().float(), want, atol=2e-2, rtol=1e-2)
+    assert bool((out[Ts:] == 0).all())
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (65, 256, 4096), (127, 384, 192), (575, 6144, 4096),
+                                   (300, 4096, 14336), (1030, 1280, 8192)])
+def test_gemm_mfma_matches_fp32(M, N, K):
+    from xgserve.ops.gemm_mfma import gemm_mfma
+    x = rnd(M, K)
+    w = rnd(N, K, scale=0.02)
+    ref = x.cpu().float() @ w.cpu().float().t()
+    y = gemm_mfma(x, w).cpu().float()
+    torch.testing.assert_close(y, ref, atol=2e-2 * float(ref.abs().max()) / 4 + 1e-3, rtol=1e-2)
+
+
+@pytest.mark.parametrize("M", [70, 575])
+def test_gemm_mfma_silu_and_strided_rows(M):
+    """Fused SiLU-gate epilogue on an interleaved gate|up weight, x a row slice of a
+    wider buffer (row stride != K), output rows with their own stride."""
+    from xgserve.ops.gemm_mfma import MODE_SILU, gemm_mfma
+    from xgserve.ops.linear import interleave_gate_up
+    K, F = 1024, 512
+    buf = rnd(M, K + 64)
+    x = buf[:, 32:32 + K]
+    gate, up = rnd(F, K, scale=0.03), rnd(F, K, scale=0.03)
+    w = interleave_gate_up(gate, up).contiguous()
+    out_buf = torch.zeros(M, F + 16, dtype=torch.bfloat16, device=DEV)
+    gemm_mfma(x, w, MODE_SILU, out=out_buf[:, :F])
+    xf = x.cpu().float()
+    want = torch.nn.functional.silu(xf @ gate.cpu().float().t()) * (xf @ up.cpu().float().t())
+    torch.testing.assert_close(out_buf[:, :F].cpu().float(), want, atol=2e-2, rtol=2e-2)
+    assert bool((out_buf[:, F:] == 0).all())

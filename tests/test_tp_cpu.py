@@ -2,7 +2,8 @@
 rank): TP=4 and TP=8 of a GQA model with 8 kv heads (TP=8 -> ONE kv head per
 rank, the Llama-3-70B TP8 layout) and a vocabulary that does not divide by the
 TP degree (the vocab-parallel LM head pads to V_pad and the gather trims it);
-Mixtral-style EP=4 (8 experts, 2 per rank) with both exchange modes.
+Mixtral-style EP=4 (8 experts, 2 per rank) with both exchange modes, the
+all_to_all one both with fixed-capacity and with count-exact splits.
 
 Every rank loads its shard of the same safetensors checkpoint; the leader
 drives the engine and the followers mirror its plans. Each greedily decoded
@@ -38,6 +39,9 @@ def _cfg(kind):
 def _rank_main(rank, world, port, ck, moe_comm, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
+    if moe_comm == "alltoall-exact":  # every step on the count-exact (packed) EP dispatch
+        os.environ["XGS_EP_EXACT_MIN_PAIRS"] = "0"
+        moe_comm = "alltoall"
     torch.set_num_threads(1)
     try:
         from xgserve.engine import EngineConfig, LLMEngine, SamplingParams
@@ -61,7 +65,8 @@ def _rank_main(rank, world, port, ck, moe_comm, q):
 
 
 @pytest.mark.parametrize("kind,world,moe_comm", [("gqa8", 4, "alltoall"), ("gqa8", 8, "alltoall"),
-                                                 ("mixtral", 4, "alltoall"), ("mixtral", 4, "allreduce")])
+                                                 ("mixtral", 4, "alltoall"), ("mixtral", 4, "alltoall-exact"),
+                                                 ("mixtral", 2, "alltoall-exact"), ("mixtral", 4, "allreduce")])
 def test_tp_full_degree_matches_fp32_reference(tmp_path, kind, world, moe_comm):
     from xgserve.models import build_model, save_checkpoint
     from xgserve.models.reference import reference_logits

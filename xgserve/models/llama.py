@@ -8,10 +8,11 @@ Tensor parallelism (Megatron layout, one process per GPU, RCCL/xGMI):
 Expert parallelism (Mixtral): EP == TP group, rank r owns experts
 [r*E/tp, (r+1)*E/tp). Two exchange modes:
   * "alltoall" (default for tp > 1, BASELINE config 5): each rank routes its
-    token slice, dispatches (token, choice) rows to the expert owners with a
-    fixed-capacity all_to_all (graph-capturable: no host sync on counts),
-    runs its local experts as one grouped GEMM, returns rows with a second
-    all_to_all, combines, and all-gathers the slices;
+    token slice, packs (token, choice) rows for the expert owners with the HIP
+    ep_plan / ep_scatter kernels (count-exact splits on eager prefill steps,
+    fixed capacity under graph capture), runs its local experts as one grouped
+    GEMM, returns rows with a second all_to_all, combines them with ep_combine
+    and all-gathers the slices;
   * "allreduce": every rank runs its local experts on all tokens and one
     all-reduce sums the partial outputs.
 Per layer the hot path is: fused_add_rmsnorm (K1) -> QKV GEMM -> rope+KV append
@@ -56,6 +57,9 @@ FUSED_DECODE = os.environ.get("XGS_FUSED_DECODE", "1") != "0"
 # GEMM-sized share of the layer. XGS_TP_OVERLAP_CHUNKS=1 disables it.
 TP_OVERLAP_CHUNKS = int(os.environ.get("XGS_TP_OVERLAP_CHUNKS", "2"))
 TP_OVERLAP_MIN_TOKENS = int(os.environ.get("XGS_TP_OVERLAP_MIN_TOKENS", "256"))
+# EP all_to_all: steps with at least this many (token, choice) pairs (and not under
+# graph capture) exchange exact per-destination counts first and send only real rows
+EP_EXACT_MIN_PAIRS = int(os.environ.get("XGS_EP_EXACT_MIN_PAIRS", "256"))
 
 
 @torch.no_grad()
@@ -146,39 +150,46 @@ class LlamaLayer(nn.Module):
         return self._ar(out)
 
     def _moe_alltoall(self, h: torch.Tensor) -> torch.Tensor:
+        """Expert-parallel MoE with an all_to_all dispatch: this rank routes its token
+        slice, ep_plan/ep_scatter (HIP) pack each (token, choice) row for the rank that
+        owns the expert, the owners run their experts as one grouped GEMM (send_eid =
+        -1 rows are skipped by the align), the rows travel back and ep_combine
+        (HIP) applies the routing weights; an all_gather rebuilds the replicated
+        [T, H] the next layer's head-parallel attention reads.
+        Split policy: count-exact (packed layout, splits exchanged first: one host
+        sync per layer) for eager steps of >= EP_EXACT_MIN_PAIRS pairs; fixed
+        capacity (per * k rows per destination, no host sync) otherwise, which is
+        what a captured decode graph needs."""
         tp, r = self.tp, self.rank
         T, H = h.shape
         k = self.cfg.experts_per_token
         per = (T + tp - 1) // tp
         lo, hi = min(T, r * per), min(T, (r + 1) * per)
-        hs = h[lo:hi]
         Ts = hi - lo
-        cap = per * k  # fixed per-destination capacity: no host sync on counts
-        send = torch.zeros(tp, cap, H, dtype=h.dtype, device=h.device)
-        send_eid = torch.full((tp, cap), -1, dtype=torch.int32, device=h.device)
-        slot_of_pair = None
+        cap = per * k
         if Ts > 0:
-            w, ids = ops.moe_route(hs, self.router, k)
-            flat_ids = ids.reshape(-1).long()
-            dest = flat_ids // self.E_local                                     # [Ts*k]
-            onehot = F.one_hot(dest, tp).to(torch.int32)                        # [Ts*k, tp]
-            pos = (torch.cumsum(onehot, 0) - onehot).gather(1, dest[:, None])[:, 0]  # rank-local slot
-            slot_of_pair = dest * cap + pos
-            rows = torch.arange(Ts * k, device=h.device) // k
-            send.view(tp * cap, H).index_copy_(0, slot_of_pair, hs[rows])
-            send_eid.view(-1).index_copy_(0, slot_of_pair, (flat_ids - dest * self.E_local).to(torch.int32))
-        recv = comm.tp_all_to_all(send.view(tp * cap, H), [cap] * tp, [cap] * tp)
-        recv_eid = comm.tp_all_to_all(send_eid.view(tp * cap, 1), [cap] * tp, [cap] * tp).view(-1)
-        valid = recv_eid >= 0
-        ones = valid.to(torch.float32)[:, None]
-        eids = torch.where(valid, recv_eid, torch.zeros_like(recv_eid)).to(torch.int32)[:, None]
-        y = ops.fused_moe(recv, self.w13, self.w2, ones, eids, 0)
-        back = comm.tp_all_to_all(y, [cap] * tp, [cap] * tp)                     # [tp*cap, H] in send order
+            w, ids = ops.moe_route(h[lo:hi], self.router, k)
+        else:
+            w = torch.empty(0, k, dtype=torch.float32, device=h.device)
+            ids = torch.empty(0, k, dtype=torch.int32, device=h.device)
+        capturing = h.is_cuda and torch.cuda.is_current_stream_capturing()
+        packed = not capturing and T * k >= EP_EXACT_MIN_PAIRS
+        slot, send_eid, counts = ops.ep_plan(ids, self.E_local, tp, cap, packed)
+        rows = Ts * k if packed else tp * cap
+        send = ops.ep_scatter(h[lo:hi], k, slot, rows)
+        if packed:
+            recv_counts = comm.tp_exchange_counts(counts)
+            send_splits, recv_splits = counts.tolist(), recv_counts.tolist()
+        else:
+            send_splits = recv_splits = [cap] * tp
+        recv = comm.tp_all_to_all(send, send_splits, recv_splits)
+        recv_eid = comm.tp_all_to_all(send_eid.view(-1, 1), send_splits, recv_splits).view(-1, 1)
+        ones = torch.ones(recv.shape[0], 1, dtype=torch.float32, device=h.device)
+        y = ops.fused_moe(recv, self.w13, self.w2, ones, recv_eid, 0)    # unused slots (eid -1) -> 0 rows
+        back = comm.tp_all_to_all(y, recv_splits, send_splits)            # rows in this rank's send order
         out_slice = torch.zeros(per, H, dtype=h.dtype, device=h.device)
-        if Ts > 0:
-            contrib = back[slot_of_pair].float() * w.reshape(-1, 1)
-            out_slice[:Ts] = contrib.view(Ts, k, H).sum(1).to(h.dtype)
-        full = comm.tp_all_gather_rows(out_slice)                               # [tp*per, H]
+        ops.ep_combine(back, slot, w, out_slice)
+        full = comm.tp_all_gather_rows(out_slice)                         # [tp*per, H]
         return full[:T].contiguous()
 
     def mlp(self, h: torch.Tensor) -> torch.Tensor:

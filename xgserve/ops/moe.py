@@ -168,3 +168,63 @@ def _moe_per_expert(x, w13, w2, topk_w, sorted_rows, offs, dest, T, k):
     kernels().moe_combine(part.data_ptr(), 1, P, dest.data_ptr(), topk_w.float().contiguous().data_ptr(),
                           out.data_ptr(), T, k, H, stream_ptr())
     return out
+
+
+# ---------------------------------------------------------------------------- expert parallel
+def ep_plan(ids: torch.Tensor, E_local: int, tp: int, cap: int, packed: bool):
+    """Dispatch plan for expert parallelism (csrc/kernels/moe.hip ep_plan): pair
+    i = (t, j) of ids [Ts, k] goes to rank d = ids[i] // E_local at a stable slot
+    base[d] + (earlier pairs bound for d), base[d] = d * cap (fixed capacity: equal
+    all_to_all splits, graph-capturable) or the exclusive prefix of the counts
+    (packed: the count-exact all_to_all). -> (slot [Ts*k] int32, send_eid [rows]
+    int32 = the owner's local expert id (-1 = unused capacity slot), counts [tp])."""
+    n = ids.numel()
+    rows = n if packed else tp * cap
+    if not use_native(ids):
+        flat = ids.reshape(-1).long()
+        dest = flat // E_local
+        onehot = torch.nn.functional.one_hot(dest, tp)
+        pos = (torch.cumsum(onehot, 0) - onehot).gather(1, dest[:, None])[:, 0]
+        counts = onehot.sum(0)
+        base = (torch.cumsum(counts, 0) - counts) if packed else torch.arange(tp) * cap
+        slot = base[dest] + pos
+        send_eid = torch.full((rows,), -1, dtype=torch.int32)
+        send_eid[slot] = (flat - dest * E_local).to(torch.int32)
+        return slot.to(torch.int32), send_eid, counts.to(torch.int32)
+    dev = ids.device
+    slot = torch.empty(n, dtype=torch.int32, device=dev)
+    send_eid = torch.empty(rows, dtype=torch.int32, device=dev)
+    counts = torch.empty(tp, dtype=torch.int32, device=dev)
+    kernels().ep_plan(ids.contiguous().data_ptr(), n, E_local, tp, cap, 1 if packed else 0, slot.data_ptr(),
+                      send_eid.data_ptr(), counts.data_ptr(), stream_ptr())
+    return slot, send_eid, counts
+
+
+def ep_scatter(x: torch.Tensor, k: int, slot: torch.Tensor, rows: int) -> torch.Tensor:
+    """send [rows, H]: send[slot[i]] = x[i // k] (unused capacity rows are left
+    uninitialised: their expert id is -1, so no kernel reads them)."""
+    T, H = x.shape
+    send = torch.empty(rows, H, dtype=x.dtype, device=x.device)
+    if not use_native(x):
+        src = torch.arange(slot.numel()) // k
+        send[slot.long()] = x[src]
+        return send
+    kernels().ep_scatter(x.data_ptr(), x.stride(0), k, slot.data_ptr(), slot.numel(), H, send.data_ptr(),
+                         stream_ptr())
+    return send
+
+
+def ep_combine(back: torch.Tensor, slot: torch.Tensor, topk_w: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """Source-side unpermute + weighted sum: out[t] = sum_j w[t, j] * back[slot[t*k+j]]
+    (fp32 accumulation, one bf16 rounding), written into out[:T]."""
+    T, k = topk_w.shape
+    if T == 0:
+        return out
+    H = back.shape[1]
+    if not use_native(back):
+        contrib = back[slot.long()].float() * topk_w.reshape(-1, 1).float()
+        out[:T] = contrib.view(T, k, H).sum(1).to(out.dtype)
+        return out
+    kernels().moe_combine(back.data_ptr(), 0, back.shape[0], slot.data_ptr(), topk_w.float().contiguous().data_ptr(),
+                          out.data_ptr(), T, k, H, stream_ptr())
+    return out
