@@ -55,7 +55,6 @@ void moe_topk_softmax(const void*, int, int, int, int, int, float*, int32_t*, hi
 void moe_align(const int32_t*, int, int, int, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
 int moe_combine(const void*, int, int, const int32_t*, const float*, uint16_t*, int, int, int, hipStream_t);
 int moe_route(const uint16_t*, const uint16_t*, int, int, int, int, int, float*, int32_t*, hipStream_t);
-int gemm_mfma(const uint16_t*, int, int, int64_t, const uint16_t*, int, uint16_t*, int64_t, int, hipStream_t);
 int ep_plan(const int32_t*, int, int, int, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
 int ep_scatter(const uint16_t*, int64_t, int, const int32_t*, int, int, uint16_t*, hipStream_t);
 int moe_gemm_m64(const uint16_t*, const int32_t*, const int32_t*, int, int, const uint16_t*, int, int, float*,
@@ -301,12 +300,6 @@ PYBIND11_MODULE(_kernels, m) {
     check(xgk::moe_route(P<const uint16_t>(h), P<const uint16_t>(wr), T, H, E, k, renorm, P<float>(w),
                          P<int32_t>(ids), S(st)),
           "moe_route");
-  });
-  m.def("gemm_mfma", [](uintptr_t x, int M, int K, int64_t lda, uintptr_t w, int N, uintptr_t out, int64_t ldc,
-                        int mode, uintptr_t st) {
-    if (M < 0 || N % 128 || K % 64 || K < 64) throw std::invalid_argument("gemm_mfma: N % 128 == 0, K % 64 == 0");
-    check(xgk::gemm_mfma(P<const uint16_t>(x), M, K, lda, P<const uint16_t>(w), N, P<uint16_t>(out), ldc, mode, S(st)),
-          "gemm_mfma");
   });
   m.def("ep_plan", [](uintptr_t ids, int n_pairs, int E_local, int tp, int cap, int packed, uintptr_t slot,
                       uintptr_t send_eid, uintptr_t counts, uintptr_t st) {

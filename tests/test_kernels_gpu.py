@@ -385,33 +385,3 @@ def test_ep_dispatch_kernels_match_torch(Ts, k, E_local, tp, packed):
     want = (back.cpu().float()[s.long().cpu()] * w.cpu().reshape(-1, 1)).view(Ts, k, H).sum(1)
     torch.testing.assert_close(out[:Ts].cpu().float(), want, atol=2e-2, rtol=1e-2)
     assert bool((out[Ts:] == 0).all())
-
-
-@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (65, 256, 4096), (127, 384, 192), (575, 6144, 4096),
-                                   (300, 4096, 14336), (1030, 1280, 8192)])
-def test_gemm_mfma_matches_fp32(M, N, K):
-    from xgserve.ops.gemm_mfma import gemm_mfma
-    x = rnd(M, K)
-    w = rnd(N, K, scale=0.02)
-    ref = x.cpu().float() @ w.cpu().float().t()
-    y = gemm_mfma(x, w).cpu().float()
-    torch.testing.assert_close(y, ref, atol=2e-2 * float(ref.abs().max()) / 4 + 1e-3, rtol=1e-2)
-
-
-@pytest.mark.parametrize("M", [70, 575])
-def test_gemm_mfma_silu_and_strided_rows(M):
-    """Fused SiLU-gate epilogue on an interleaved gate|up weight, x a row slice of a
-    wider buffer (row stride != K), output rows with their own stride."""
-    from xgserve.ops.gemm_mfma import MODE_SILU, gemm_mfma
-    from xgserve.ops.linear import interleave_gate_up
-    K, F = 1024, 512
-    buf = rnd(M, K + 64)
-    x = buf[:, 32:32 + K]
-    gate, up = rnd(F, K, scale=0.03), rnd(F, K, scale=0.03)
-    w = interleave_gate_up(gate, up).contiguous()
-    out_buf = torch.zeros(M, F + 16, dtype=torch.bfloat16, device=DEV)
-    gemm_mfma(x, w, MODE_SILU, out=out_buf[:, :F])
-    xf = x.cpu().float()
-    want = torch.nn.functional.silu(xf @ gate.cpu().float().t()) * (xf @ up.cpu().float().t())
-    torch.testing.assert_close(out_buf[:, :F].cpu().float(), want, atol=2e-2, rtol=2e-2)
-    assert bool((out_buf[:, F:] == 0).all())
