@@ -472,7 +472,7 @@ static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, con
   else
   hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ>), dim3(Hkv, B, gz), dim3(256), 0, st, q, qs, kc, vc, bt, bts, sl,
                      po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq, S > 1 ? decode_min_split_tiles() : 1);
-  if (S > 1 && counters == nullptr)
+  if (S > 1 && counters == nullptr && out != nullptr)  // out == nullptr: merged by the consumer (gemm_m64g XA)
     hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
 }
 
@@ -507,6 +507,7 @@ int decode_attention_fq(const float* part, int S_qkv, const int32_t* positions, 
   if (B <= 0) return 0;
   if (part == nullptr || S_qkv < 1 || bs % 16 != 0 || Hq % Hkv != 0 || D != 128 || num_splits < 1) return -1;
   if (num_splits > 1 && (part_out == nullptr || part_lse == nullptr)) return -1;
+  if (out == nullptr && (num_splits == 1 || counters != nullptr)) return -1;  // deferred combine needs split slabs
   if (pf_slices < 0 || (pf_slices > 0 && (pf == nullptr || pf_bytes <= 0))) return -1;
   const QkvFuse fq{part, S_qkv, positions, cos_sin, slots, kc, vc, apply_rope,
                    static_cast<const uint8_t*>(pf), pf_bytes, pf_slices};

@@ -56,7 +56,75 @@ struct M64Epi {
   uint16_t* resid;
   float* ss_out;
   int* counters;
+  // XA form: x is the decode attention output still in split-K form (the combine
+  // launch is skipped): att_po [M, att_hq, att_splits, 128] fp32 normalised partial
+  // outputs, att_lse [M, att_hq, att_splits] their log-sum-exps.
+  const float* att_po;
+  const float* att_lse;
+  int att_splits;
+  int att_hq;
 };
+
+// XA prologue: the workgroup's x slice -- rows 0..15 x its kws = K / S columns, i.e.
+// kws / 128 attention heads -- merged from the split partials (online log-sum-exp
+// merge, batches of 8 splits with every load issued before the arithmetic) and
+// written as bf16 into xbuf in the DMA ring's x image: chunk c of KC columns at
+// c * 16 * RB, row m, 16-B granule j at (j ^ (m & (GPR - 1))) * 16. Rows >= M are
+// zero. Replaces the decode_combine launch of small-batch decode.
+template <int KC, int NTHR>
+__device__ __forceinline__ void m64g_xa_prologue(const M64Epi& epi, int M, int k0, int kws, uint8_t* xbuf) {
+  constexpr int RB = KC * 2, GPR = KC / 8, SB = 8;
+  const int nh = kws / 128;
+  const int NS = epi.att_splits;
+  for (int it = threadIdx.x; it < 16 * nh * 16; it += NTHR) {
+    const int m = it / (nh * 16), rem = it - m * (nh * 16);
+    const int hj = rem >> 4, c8 = rem & 15;
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (m < M) {
+      const int64_t bh = static_cast<int64_t>(m) * epi.att_hq + k0 / 128 + hj;
+      const float* lse = epi.att_lse + bh * NS;
+      const float* po = epi.att_po + bh * NS * 128 + 8 * c8;
+      float mx = -INFINITY, den = 0.f;
+      for (int s0 = 0; s0 < NS; s0 += SB) {
+        float l[SB];
+        float4 va[SB], vb[SB];
+#pragma unroll
+        for (int i = 0; i < SB; ++i) {
+          const int sc = min(s0 + i, NS - 1);
+          l[i] = lse[sc];
+          va[i] = *reinterpret_cast<const float4*>(po + static_cast<int64_t>(sc) * 128);
+          vb[i] = *reinterpret_cast<const float4*>(po + static_cast<int64_t>(sc) * 128 + 4);
+        }
+#pragma unroll
+        for (int i = 0; i < SB; ++i)
+          if (s0 + i >= NS) l[i] = -INFINITY;
+        float m2 = mx;
+#pragma unroll
+        for (int i = 0; i < SB; ++i) m2 = fmaxf(m2, l[i]);
+        if (m2 == -INFINITY) continue;
+        const float r = __expf(mx - m2);
+        den *= r;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] *= r;
+#pragma unroll
+        for (int i = 0; i < SB; ++i) {
+          const float wgt = __expf(l[i] - m2);
+          den += wgt;
+          o[0] += wgt * va[i].x; o[1] += wgt * va[i].y; o[2] += wgt * va[i].z; o[3] += wgt * va[i].w;
+          o[4] += wgt * vb[i].x; o[5] += wgt * vb[i].y; o[6] += wgt * vb[i].z; o[7] += wgt * vb[i].w;
+        }
+        mx = m2;
+      }
+      const float inv = den > 0.f ? 1.f / den : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] *= inv;
+    }
+    const int k = hj * 128 + 8 * c8;
+    const int ch = k / KC, gr = (k % KC) / 8;
+    *reinterpret_cast<uint4*>(xbuf + ch * 16 * RB + m * RB + (gr ^ (m & (GPR - 1))) * 16) = pack8(o);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ordered for the readers by the ring's first barrier
+}
 
 // Every wave drains its stores (write-through), then one relaxed agent-scope
 // ticket; returns in every thread whether this workgroup drew `last_value`. The
@@ -153,7 +221,7 @@ __device__ __forceinline__ void m64g_resid_tail(const float* __restrict__ part, 
 //   NT  non-temporal weight DMA (streamed once; keeps x resident in L2)
 //   MT  16-row x tiles (4: 16 < M <= 64; 1: M <= 16 -- a quarter of the x DMA and
 //       LDS per chunk, so the weight stream owns the load path at batch 1)
-template <int NW, int WV, int KC, bool NT, int MT>
+template <int NW, int WV, int KC, bool NT, int MT, bool XA = false>
 __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* __restrict__ x, int M, int K,
                                                                const uint16_t* __restrict__ w, int N,
                                                                float* __restrict__ part, uint16_t* __restrict__ out,
@@ -163,16 +231,18 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   constexpr int RPI = 1024 / RB;                 // rows per DMA instruction (64 lanes x 16 B)
   constexpr int XROWS = 16 * MT;
   constexpr int XBYTES = XROWS * RB;
-  constexpr int XI = XROWS / RPI / WV;           // x DMA instructions per wave per chunk
+  constexpr int XI = XA ? 0 : XROWS / RPI / WV;  // x DMA instructions per wave per chunk (XA: x pre-staged)
   constexpr int WROWS = 16 * NW;                 // weight rows per wave
   constexpr int WI = WROWS / RPI;                // weight DMA instructions per wave per chunk
   constexpr int WBYTES = WROWS * RB;             // per wave per slot
   constexpr int SLOT = XBYTES + WV * WBYTES;
   constexpr int G = XI + WI;
-  static_assert(XI >= 1 && WI >= 1 && XROWS % (RPI * WV) == 0, "bad m64g geometry");
+  static_assert((XA ? MT == 1 : XI >= 1) && WI >= 1 && XROWS % (RPI * WV) == 0, "bad m64g geometry");
+  constexpr int XA_KMAX = 1024;                  // XA: the x slice [16][kws <= 1024] bf16
   __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
+  __shared__ __attribute__((aligned(1024))) uint8_t xbuf[XA ? 16 * XA_KMAX * 2 : 16];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -189,7 +259,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
     const int r = RPI * i + dr;
     wsrc[i] = w + static_cast<int64_t>(nbase + r) * K + k0 + 8 * (dj ^ (r & (GPR - 1)));
   }
-  const uint16_t* xsrc[XI];
+  const uint16_t* xsrc[XI > 0 ? XI : 1];
 #pragma unroll
   for (int i = 0; i < XI; ++i) {
     const int r = RPI * (wid * XI + i) + dr;     // x row 0..XROWS-1
@@ -213,8 +283,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](const uint8_t* slot) {
-    const uint8_t* xs = slot;
+  auto compute = [&](const uint8_t* slot, int c) {
+    const uint8_t* xs = XA ? xbuf + c * XBYTES : slot;
     const uint8_t* ws = slot + XBYTES + wid * WBYTES;
 #pragma unroll
     for (int t = 0; t < KC / 32; ++t) {
@@ -238,7 +308,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
     else wait_vmcnt<0>();
     raw_barrier();
     if (c + 2 < nchunks) issue(nxt2, c + 2);
-    compute(cur);
+    compute(cur, c);
   };
 
   // RMSNorm statistics of the input rows, loaded before the weight stream starts
@@ -258,6 +328,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
 
   issue(lds0, 0);
   if (nchunks > 1) issue(lds1, 1);
+  // XA: merge the attention splits into xbuf while the first weight chunks stream
+  if constexpr (XA) m64g_xa_prologue<KC, 64 * WV>(epi, M, k0, kws, xbuf);
   int c = 0;
   for (; c + 3 <= nchunks; c += 3) {
     step(lds0, lds2, c);
@@ -622,9 +694,13 @@ template <int NW>
 static void launch_m64g(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N,
                         float* part, uint16_t* out, int mode, const M64Epi& epi) {
   const bool mt1 = M <= 16 && cfg != 2 && cfg != 3 && m64g_mt1_enabled();
+  const bool xa = epi.att_po != nullptr;  // m64g_check: only with mt1
 #define XGK_M64G(WV, KC, NT)                                                                                         \
   do {                                                                                                               \
-    if (mt1)                                                                                                         \
+    if (xa)                                                                                                          \
+      hipLaunchKernelGGL((gemm_m64g_kernel<NW, WV, KC, NT, 1, true>), grid, dim3(64 * WV), 0, st, x, M, K, w, N,     \
+                         part, out, mode, epi);                                                                      \
+    else if (mt1)                                                                                                    \
       hipLaunchKernelGGL((gemm_m64g_kernel<NW, WV, KC, NT, 1>), grid, dim3(64 * WV), 0, st, x, M, K, w, N, part, out, \
                          mode, epi);                                                                                 \
     else                                                                                                             \
@@ -664,6 +740,12 @@ static int m64g_check(int M, int K, int N, const float* part, const uint16_t* ou
   if (mode == GG_RESID && (epi.resid == nullptr || epi.ss_out == nullptr || epi.counters == nullptr)) return 1;
   if (epi.ss_in != nullptr && (epi.ss_n < 1 || epi.ss_n > 64 || epi.ss_stride < M || (epi.ss_n > 8 && M > 16)))
     return 1;
+  if (epi.att_po != nullptr) {  // XA: one-x-tile kernel, whole heads of 128 per K slice, slice fits xbuf
+    const int kws = K / S;
+    if (M > 16 || cfg == 2 || cfg == 3 || !m64g_mt1_enabled() || epi.att_lse == nullptr || epi.att_splits < 1 ||
+        kws % 128 || kws > 1024 || K != epi.att_hq * 128)
+      return 1;
+  }
   return 0;
 }
 
@@ -676,7 +758,7 @@ static void m64g_launch(const uint16_t* x, int M, int K, const uint16_t* w, int 
 
 int gemm_m64g(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
               int nw, int cfg, hipStream_t st) {
-  const M64Epi epi{nullptr, 0, 0, 0.f, nullptr, nullptr, nullptr};
+  const M64Epi epi{nullptr, 0, 0, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
   if (mode == GG_RESID || m64g_check(M, K, N, part, out, S, mode, nw, cfg, epi)) return 1;
   m64g_launch(x, M, K, w, N, part, out, S, mode, nw, cfg, epi, st);
   return 0;
@@ -686,8 +768,9 @@ int gemm_m64g(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* 
 // epilogue; ss_out holds (N / cols) * M floats, counters N / cols ints.
 int gemm_m64g_ex(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S,
                  int mode, int nw, int cfg, const float* ss_in, int ss_n, int ss_stride, float eps, uint16_t* resid,
-                 float* ss_out, int* counters, hipStream_t st) {
-  const M64Epi epi{ss_in, ss_n, ss_stride, eps, resid, ss_out, counters};
+                 float* ss_out, int* counters, hipStream_t st, const float* att_po, const float* att_lse,
+                 int att_splits, int att_hq) {
+  const M64Epi epi{ss_in, ss_n, ss_stride, eps, resid, ss_out, counters, att_po, att_lse, att_splits, att_hq};
   if (m64g_check(M, K, N, part, out, S, mode, nw, cfg, epi)) return 1;
   m64g_launch(x, M, K, w, N, part, out, S, mode, nw, cfg, epi, st);
   return 0;

@@ -23,7 +23,7 @@ int skinny_slab_kmax(int);
 int gemm_m64(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 int gemm_m64g(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 int gemm_m64g_ex(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, const float*,
-                 int, int, float, uint16_t*, float*, int*, hipStream_t);
+                 int, int, float, uint16_t*, float*, int*, hipStream_t, const float*, const float*, int, int);
 void add_partials_resid(const float*, int, int, uint16_t*, float*, int, hipStream_t);
 void row_sumsq(const uint16_t*, int, int, float*, hipStream_t);
 void embed_gather(const int32_t*, int, const uint16_t*, int, int, uint16_t*, float*, hipStream_t);
@@ -235,10 +235,13 @@ PYBIND11_MODULE(_kernels, m) {
   // ---- fused decode layer (gemm_m64g.hip epilogues, decode_attention.hip FQ prologue)
   m.def("gemm_m64g_ex", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
                            int mode, int nw, int cfg, uintptr_t ss_in, int ss_n, int ss_stride, float eps,
-                           uintptr_t resid, uintptr_t ss_out, uintptr_t counters, uintptr_t st) {
+                           uintptr_t resid, uintptr_t ss_out, uintptr_t counters, uintptr_t st, uintptr_t att_po,
+                           uintptr_t att_lse, int att_splits, int att_hq) {
+    // att_po != 0: x is the decode attention output in split form (merged in the GEMM prologue)
     check(xgk::gemm_m64g_ex(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode,
                             nw, cfg, P<const float>(ss_in), ss_n, ss_stride, eps, P<uint16_t>(resid),
-                            P<float>(ss_out), P<int>(counters), S(st)),
+                            P<float>(ss_out), P<int>(counters), S(st), P<const float>(att_po),
+                            P<const float>(att_lse), att_splits, att_hq),
           "gemm_m64g_ex");
   });
   m.def("add_partials_resid", [](uintptr_t part, int S_, int T, uintptr_t res, uintptr_t ss_part, int H,

@@ -173,3 +173,45 @@ def test_fused_batch_decode_matches_unfused(llama_small, monkeypatch):
         outs[fused] = eng.generate(prompts, sp)
     agree = sum(a[1] == b[1] for a, b in zip(outs[True], outs[False]))
     assert agree >= 4, outs
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (16, 4)])
+@pytest.mark.parametrize("lens", [[600], [1, 17, 300, 64, 0, 129]])
+@pytest.mark.parametrize("splits", [3, 16])
+def test_o_projection_merges_split_attention(Hq, Hkv, lens, splits, monkeypatch):
+    """XA form: the attention launch skips its split combine (PendingAttn) and the O
+    projection's gemm_m64g prologue merges the splits -- against the combine launch
+    followed by the plain GEMM (resid epilogue and PendingSum forms)."""
+    import xgserve.ops.attention as A
+    monkeypatch.setattr(lin, "XA_MAX_M", 16)  # opt-in path (measured slower end to end)
+    D, bs, S = 128, 16, 4
+    kc, vc, bt = _paged([max(1, L) for L in lens], Hkv, D, bs)
+    B = len(lens)
+    part = torch.randn(S, B, (Hq + 2 * Hkv) * D, device=DEV) * 0.3
+    pos = torch.tensor([max(0, L - 1) for L in lens], dtype=torch.int32, device=DEV)
+    slots = torch.tensor([int(bt[b, (L - 1) // bs]) * bs + (L - 1) % bs if L > 0 else -1
+                          for b, L in enumerate(lens)], dtype=torch.int32, device=DEV)
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    cs = ops.build_cos_sin(D, 4096, 500000.0, device=DEV)
+    scale = 1.0 / math.sqrt(D)
+    ws_a, ws_b = A.DecodeWorkspace(B, Hq, D, splits, DEV), A.DecodeWorkspace(B, Hq, D, splits, DEV)
+    a = ops.decode_attention_fused(PendingSum(part, S), pos, slots, cs, kc.clone(), vc.clone(), bt, sl, Hq, scale,
+                                   splits, workspace=ws_a)
+    pa = ops.decode_attention_fused(PendingSum(part, S), pos, slots, cs, kc.clone(), vc.clone(), bt, sl, Hq, scale,
+                                    splits, workspace=ws_b, defer_combine=True)
+    assert isinstance(pa, A.PendingAttn)
+    N, K = 4096, Hq * D
+    assert lin.m64_xa_ok(B, N, K)
+    w = rnd(N, K, scale=0.02)
+    want = a.float() @ w.float().t()
+    got = lin.m64_xa_linear(pa, w).part.sum(0)
+    assert rel_err(got, want) < 1e-2
+    r0 = rnd(B, N)
+    rw = ResidWorkspace(4, 64, N, DEV)
+    r1, r2 = r0.clone(), r0.clone()
+    st1 = m64_resid_linear(a, w, r1, rw, 1, 1e-5)
+    st2 = m64_resid_linear(pa, w, r2, rw, 2, 1e-5)
+    assert rel_err(r2, r1) < 1e-2
+    ss1 = st1.ss[:st1.n * B].view(st1.n, B).sum(0)
+    ss2 = st2.ss[:st2.n * B].view(st2.n, B).sum(0)
+    torch.testing.assert_close(ss2, ss1, rtol=2e-2, atol=1e-2)

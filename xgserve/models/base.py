@@ -84,13 +84,15 @@ class PagedAttention:
         return self.attend(q.view(T, self.Hq, self.D), meta, kv)
 
     def fused_decode(self, pend, meta: AttnMeta, kv: Tuple[torch.Tensor, torch.Tensor],
-                     cos_sin: torch.Tensor, prefetch: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     cos_sin: torch.Tensor, prefetch: Optional[torch.Tensor] = None, defer_combine: bool = False):
         """Pure-decode step on QKV split-K partials: the attention kernel's prologue
         reduces them, applies RoPE and appends K/V (ops.decode_attention_fused);
-        `prefetch` = the O projection weight, warmed into the Infinity Cache."""
+        `prefetch` = the O projection weight, warmed into the Infinity Cache;
+        defer_combine: return the split partials (PendingAttn) for the O GEMM to merge."""
         return ops.decode_attention_fused(pend, meta.positions, meta.slot_mapping, cos_sin, kv[0], kv[1],
                                           meta.dec_block_tables, meta.dec_seq_lens, self.Hq, self.scale,
-                                          meta.num_splits, meta.workspace, self.use_rope, prefetch=prefetch)
+                                          meta.num_splits, meta.workspace, self.use_rope, prefetch=prefetch,
+                                          defer_combine=defer_combine)
 
     def attend(self, q: torch.Tensor, meta: AttnMeta, kv: Tuple[torch.Tensor, torch.Tensor],
                out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -33,7 +33,8 @@ from ..parallel import comm
 from ..parallel.state import get_state
 from ..ops.linear import (MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace, RowStats,
                           m64_linear,
-                          m64_norm_linear, m64_plan, m64_resid_linear, pick_split, quantize_fp8, skinny_linear,
+                          m64_norm_linear, m64_plan, m64_resid_linear, m64_xa_linear, m64_xa_ok, pick_split,
+                          quantize_fp8, skinny_linear,
                           w8_linear, w8_plan)
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
 from .config import ModelConfig
@@ -314,7 +315,10 @@ class LlamaLayer(nn.Module):
         returns the statistics of the new residual for the next layer."""
         eps = self.cfg.norm_eps
         pqkv = m64_norm_linear(resid, self.qkv, MODE_PARTIAL, stats, eps)
-        a = self.attn.fused_decode(pqkv, meta, kv, cos_sin, prefetch=self.o)
+        # small batches: the attention's split combine runs in the O GEMM's prologue
+        T = resid.shape[0]
+        xa = meta.num_splits > 1 and self.attn.D == 128 and m64_xa_ok(T, self.o.shape[0], self.o.shape[1])
+        a = self.attn.fused_decode(pqkv, meta, kv, cos_sin, prefetch=self.o, defer_combine=xa)
         if self.tp > 1:
             return self._fused_tp_tail(a, resid, ws, site)
         st = m64_resid_linear(a, self.o, resid, ws, site, eps)
@@ -326,7 +330,7 @@ class LlamaLayer(nn.Module):
         all-reduce + residual + statistics (one launch) -> gate_up (norm row scale,
         SiLU-gate) -> down GEMM partials -> all-reduce + residual + statistics."""
         T, H = resid.shape
-        po = m64_linear(a, self.o, MODE_PARTIAL)
+        po = m64_linear(a, self.o, MODE_PARTIAL) if isinstance(a, torch.Tensor) else m64_xa_linear(a, self.o)
         comm.tp_allreduce_resid(po.part, resid, ws.ss[site])
         st = RowStats(ws.ss[site], H // 1024, T)
         act = m64_norm_linear(resid, self.gate_up, MODE_SILU, st, self.cfg.norm_eps)

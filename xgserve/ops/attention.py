@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import math
 import os
+from dataclasses import dataclass
 from typing import Optional
 
 import torch
@@ -87,6 +88,23 @@ def prefill_attention_ref(q, k_cache, v_cache, block_tables, query_start_loc, se
     return out
 
 
+@dataclass
+class PendingAttn:
+    """Decode attention output still in split-K form (the combine launch skipped):
+    part_out [B, Hq, S, D] normalised partial outputs, part_lse [B, Hq, S]. The O
+    projection merges it in its prologue (ops.linear m64 XA form)."""
+    part_out: torch.Tensor
+    part_lse: torch.Tensor
+    S: int
+    B: int
+    Hq: int
+    D: int
+
+    @property
+    def shape(self):
+        return (self.B, self.Hq * self.D)
+
+
 class DecodeWorkspace:
     """Split-K partial buffers, sized once (graph-capture safe)."""
 
@@ -137,20 +155,22 @@ def decode_attention_fused(pend, positions: torch.Tensor, slot_mapping: torch.Te
                            seq_lens: torch.Tensor, num_heads: int, scale: float, num_splits: int = 1,
                            workspace: Optional[DecodeWorkspace] = None, apply_rope: bool = True,
                            out: Optional[torch.Tensor] = None,
-                           prefetch: Optional[torch.Tensor] = None) -> torch.Tensor:
+                           prefetch: Optional[torch.Tensor] = None, defer_combine: bool = False):
     """Paged decode attention on the QKV projection's split-K partials (PendingSum
     [S, B, (Hq + 2 Hkv) D]): each workgroup's prologue reduces its (sequence, kv
     head) slice, applies RoPE and appends the new K/V row to the cache -- the work
     of rope_cache_partials without its launch or the q round trip. -> [B, Hq * D].
     `prefetch` (the next GEMM's weight): read into the Infinity Cache by extra
-    workgroups of the same launch when B <= ATTN_PREFETCH_MAX_B."""
+    workgroups of the same launch when B <= ATTN_PREFETCH_MAX_B. defer_combine with
+    num_splits > 1: no combine launch, returns a PendingAttn for the O GEMM."""
     S, B, W = pend.part.shape
     Hkv, bs, D = k_cache.shape[1], k_cache.shape[2], k_cache.shape[3]
     Hq = num_heads
     assert W == (Hq + 2 * Hkv) * D and pend.part.is_contiguous()
     assert block_tables.dtype == torch.int32 and seq_lens.dtype == torch.int32 and block_tables.stride(1) == 1
     assert positions.dtype == torch.int32 and slot_mapping.dtype == torch.int32 and cos_sin.dtype == torch.float32
-    if out is None:
+    defer = defer_combine and num_splits > 1 and not IN_KERNEL_COMBINE
+    if out is None and not defer:
         out = torch.empty(B, Hq * D, dtype=torch.bfloat16, device=pend.part.device)
     po = pl = cnt = 0
     if num_splits > 1:
@@ -167,8 +187,11 @@ def decode_attention_fused(pend, positions: torch.Tensor, slot_mapping: torch.Te
     kernels().decode_attention_fq(pend.part.data_ptr(), S, positions.data_ptr(), cos_sin.data_ptr(),
                                   slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                   block_tables.data_ptr(), block_tables.stride(0), seq_lens.data_ptr(), po, pl,
-                                  out.data_ptr(), out.stride(0), B, Hq, Hkv, D, bs, float(scale), int(num_splits),
-                                  1 if apply_rope else 0, cnt, pf, pf_bytes, pf_slices, stream_ptr())
+                                  0 if defer else out.data_ptr(), 0 if defer else out.stride(0), B, Hq, Hkv, D, bs,
+                                  float(scale), int(num_splits), 1 if apply_rope else 0, cnt, pf, pf_bytes, pf_slices,
+                                  stream_ptr())
+    if defer:
+        return PendingAttn(workspace.part_out, workspace.part_lse, int(num_splits), B, Hq, D)
     return out
 
 

@@ -252,6 +252,39 @@ class ResidWorkspace:
         self.counters = torch.zeros(n_sites, self.MAX_TILES, dtype=torch.int32, device=device)
 
 
+# Attention split-combine folded into the O projection (gemm_m64g XA prologue) for
+# pure-decode steps of at most this many rows (XGS_XA_MAX_M; 0 = off, the default).
+# Measured slower (8B batch 1: 3.297 vs 3.265 ms/step, batch 8: 3.76 vs 3.56;
+# profiles/r2_xa_ab.md): every one of the O GEMM's column-tile workgroups re-reads
+# the split slabs of its heads (64 KB at 16 splits, 16 MB per launch) before its
+# weight stream can retire, which costs more than the combine launch it removes.
+import os as _os
+XA_MAX_M = int(_os.environ.get("XGS_XA_MAX_M", "0"))
+
+
+def m64_xa_ok(M: int, N: int, K: int) -> bool:
+    """Can gemm_m64g take x as attention split partials at this shape? One-x-tile
+    kernel (M <= 16, not the 4-wave KC-64 configs), whole 128-dim heads per K slice,
+    slice <= 1024 columns (the LDS x image)."""
+    if not (1 <= M <= min(16, XA_MAX_M)):
+        return False
+    p = m64_plan(M, N, K, MODE_PARTIAL)
+    if p is None:
+        return False
+    nw, S, cfg = p
+    kws = K // S
+    return cfg not in (2, 3) and kws % 128 == 0 and kws <= 1024
+
+
+def _xa(x):
+    """(x pointer, M, K, att_po, att_lse, att_splits, att_hq) for a tensor or a PendingAttn."""
+    from .attention import PendingAttn
+    if isinstance(x, PendingAttn):
+        return 0, x.B, x.Hq * x.D, x.part_out.data_ptr(), x.part_lse.data_ptr(), x.S, x.Hq
+    M, K = x.shape
+    return x.data_ptr(), M, K, 0, 0, 0, 0
+
+
 def m64_norm_linear(x: torch.Tensor, w: torch.Tensor, mode: int, stats: RowStats, eps: float,
                     out: Optional[torch.Tensor] = None):
     """gemm_m64g on the raw residual stream x with its RMSNorm applied as a per-row
@@ -268,39 +301,53 @@ def m64_norm_linear(x: torch.Tensor, w: torch.Tensor, mode: int, stats: RowStats
     if mode == MODE_PARTIAL:
         part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
         k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg, *st,
-                       0, 0, 0, stream_ptr())
+                       0, 0, 0, stream_ptr(), 0, 0, 0, 0)
         return PendingSum(part, S)
     if out is None:
         out = torch.empty(M, N // 2 if mode == MODE_SILU else N, dtype=torch.bfloat16, device=x.device)
     k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, cfg, *st, 0, 0, 0,
-                   stream_ptr())
+                   stream_ptr(), 0, 0, 0, 0)
     return out
 
 
-def m64_resid_linear(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace, site: int,
+def m64_resid_linear(x, w: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace, site: int,
                      eps: float) -> RowStats:
     """resid += x . w^T (bf16 residual stream, in place) on gemm_m64g; returns the
     new residual's RMSNorm statistics. Small split-K slabs are reduced inside the
-    GEMM launch (GG_RESID), large ones by the wide add_partials_resid kernel."""
-    M, K = x.shape
+    GEMM launch (GG_RESID), large ones by the wide add_partials_resid kernel.
+    x: bf16 [M, K] or a PendingAttn (split attention merged in the GEMM prologue)."""
+    xp, M, K, apo, alse, asp, ahq = _xa(x)
     N = w.shape[0]
     plan = m64_plan(M, N, K, MODE_PARTIAL)
     if plan is None or N % 1024 or tuple(resid.shape) != (M, N):
         raise ValueError(f"gemm_m64g resid: unsupported shape M={M} N={N} K={K}")
     nw, S, cfg = plan
     k = kernels()
-    part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+    part = torch.empty(S, M, N, dtype=torch.float32, device=resid.device)
     ss = ws.ss[site]
     cols = 16 * nw * M64G_CFGS[cfg][0]
     ntiles = N // cols
     if (S * M * cols * 4 <= RESID_INLAUNCH_MAX_BYTES and ntiles <= ws.MAX_TILES
             and M <= ws.IN_LAUNCH_MAX_M):
-        k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_RESID, nw, cfg, 0, 0, 0,
-                       float(eps), resid.data_ptr(), ss.data_ptr(), ws.counters[site].data_ptr(), stream_ptr())
+        k.gemm_m64g_ex(xp, M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_RESID, nw, cfg, 0, 0, 0,
+                       float(eps), resid.data_ptr(), ss.data_ptr(), ws.counters[site].data_ptr(), stream_ptr(),
+                       apo, alse, asp, ahq)
         return RowStats(ss, ntiles, M)  # one partial sum per column tile
-    k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg, stream_ptr())
+    k.gemm_m64g_ex(xp, M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg, 0, 0, 0, 0.0, 0, 0, 0,
+                   stream_ptr(), apo, alse, asp, ahq)
     k.add_partials_resid(part.data_ptr(), S, M, resid.data_ptr(), ss.data_ptr(), N, stream_ptr())
     return RowStats(ss, N // 1024, M)  # one partial sum per 1024-column chunk
+
+
+def m64_xa_linear(x, w: torch.Tensor) -> PendingSum:
+    """PendingSum of x . w^T where x is a PendingAttn (row-parallel O projection under TP)."""
+    xp, M, K, apo, alse, asp, ahq = _xa(x)
+    N = w.shape[0]
+    nw, S, cfg = m64_plan(M, N, K, MODE_PARTIAL)
+    part = torch.empty(S, M, N, dtype=torch.float32, device=w.device)
+    kernels().gemm_m64g_ex(xp, M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg, 0, 0, 0, 0.0, 0,
+                           0, 0, stream_ptr(), apo, alse, asp, ahq)
+    return PendingSum(part, S)
 
 
 def interleave_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
