@@ -42,7 +42,9 @@ enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2, GG_RESID = 3 };
 //           partial sums of squares per row, ss_in[j * ss_stride + m], added in a
 //           fixed order; output row m is scaled by rsqrt(sum / K + eps).
 //           ss_n <= 8: any M (lane group g of row m sums j = g, g + 4);
-//           8 < ss_n <= 64: M <= 16 only (wave w, group g sums j = 4w + g + 4 WV q, q < 8).
+//           8 < ss_n <= 64: M <= 16: wave w, group g sums j = 4w + g + 4 WV q, q < 8;
+//           M > 16 (MT = 4): lane m of wave w sums j = w + WV q (64 / WV loads), the
+//           waves' sums added through LDS in wave order (deterministic).
 //   GG_RESID: resid[m, n] += sum_s part[s, m, n] (bf16 residual stream, in place);
 //           ss_out[tile * M + m] = sum over the tile's columns of resid[m, n]^2
 //           (the next GEMM's ss_in with ss_n = gridDim.x). counters: gridDim.x tile
@@ -314,9 +316,18 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   // RMSNorm statistics of the input rows, loaded before the weight stream starts
   // (clamped unconditional loads, masked when combined; held in 8 registers)
   const bool has_ss = epi.ss_in != nullptr;
-  const bool wide_ss = has_ss && epi.ss_n > 8;  // per-tile sums (M <= 16): spread over waves too
+  // per-tile sums (ss_n > 8): M <= 16 spreads them over the waves too (wide); M > 16
+  // (MT = 4, "tall"): lane = row, wave w sums j = w + WV q, combined through LDS
+  const bool tall_ss = MT > 1 && has_ss && epi.ss_n > 8 && M > 16;
+  const bool wide_ss = has_ss && epi.ss_n > 8 && !tall_ss;
+  constexpr int TQ = MT > 1 ? 64 / WV : 1;
   float ssv[8];
-  if (has_ss) {
+  float ssb[TQ];
+  if (tall_ss) {
+#pragma unroll
+    for (int q = 0; q < TQ; ++q)
+      ssb[q] = epi.ss_in[min(wid + WV * q, epi.ss_n - 1) * epi.ss_stride + min(lane, M - 1)];
+  } else if (has_ss) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       if (!wide_ss && (i >> 1) >= MT) break;
@@ -341,7 +352,23 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
 
   if (has_ss) {  // input RMSNorm as a row scale of the (linear) output
     float tot[MT];
-    if (!wide_ss) {
+    if (tall_ss) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < TQ; ++q) v += wid + WV * q < epi.ss_n ? ssb[q] : 0.f;
+      float* red = reinterpret_cast<float*>(lds0);
+      __syncthreads();  // all waves are past their last slot read (no DMA in flight)
+      red[wid * 64 + lane] = v;
+      __syncthreads();
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        float t = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < WV; ++w2) t += red[w2 * 64 + 16 * mt + li];
+        tot[mt] = t;
+      }
+      __syncthreads();  // red is re-used as the GG_RESID ticket flag below
+    } else if (!wide_ss) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         float v = (g < epi.ss_n ? ssv[2 * mt] : 0.f) + (g + 4 < epi.ss_n ? ssv[2 * mt + 1] : 0.f);
@@ -738,8 +765,7 @@ static int m64g_check(int M, int K, int N, const float* part, const uint16_t* ou
   if ((mode == GG_PARTIAL || mode == GG_RESID) && part == nullptr) return 1;
   if ((mode == GG_BF16 || mode == GG_SILU) && out == nullptr) return 1;
   if (mode == GG_RESID && (epi.resid == nullptr || epi.ss_out == nullptr || epi.counters == nullptr)) return 1;
-  if (epi.ss_in != nullptr && (epi.ss_n < 1 || epi.ss_n > 64 || epi.ss_stride < M || (epi.ss_n > 8 && M > 16)))
-    return 1;
+  if (epi.ss_in != nullptr && (epi.ss_n < 1 || epi.ss_n > 64 || epi.ss_stride < M)) return 1;
   if (epi.att_po != nullptr) {  // XA: one-x-tile kernel, whole heads of 128 per K slice, slice fits xbuf
     const int kws = K / S;
     if (M > 16 || cfg == 2 || cfg == 3 || !m64g_mt1_enabled() || epi.att_lse == nullptr || epi.att_splits < 1 ||

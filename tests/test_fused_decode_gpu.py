@@ -34,7 +34,7 @@ def rel_err(a, b):
 
 
 @pytest.mark.parametrize("M,n_parts", [(1, 1), (5, 4), (16, 8), (24, 1), (64, 4), (64, 8), (1, 64), (9, 64),
-                                        (16, 32)])
+                                        (16, 32), (33, 64), (64, 64), (64, 32), (40, 16)])
 def test_norm_linear_row_scale(M, n_parts):
     K = 4096
     x = rnd(M, K)
@@ -64,7 +64,11 @@ def test_resid_linear(M, N, K, inlaunch, monkeypatch):
         st = m64_resid_linear(x, w, r, ws, 1, 1e-5)
         torch.testing.assert_close(r.float(), ref, atol=3e-2, rtol=2e-2)
         ss = st.ss.reshape(-1)[: st.n * st.stride].view(st.n, st.stride)[:, :M].sum(0)
-        assert st.n == (64 if inlaunch and M <= 16 else N // 1024)
+        if inlaunch:  # one partial sum per column tile
+            nw, _, cfg = lin.m64_plan(M, N, K, MODE_PARTIAL)
+            assert st.n == N // (16 * nw * lin.M64G_CFGS[cfg][0])
+        else:
+            assert st.n == N // 1024
         assert rel_err(ss, (r.float() ** 2).sum(-1)) < 1e-5
         runs.append((r.clone(), ss.clone()))
     assert all(torch.equal(runs[0][0], a) and torch.equal(runs[0][1], b) for a, b in runs)  # deterministic

@@ -224,7 +224,7 @@ MODE_RESID = 3
 # this many bytes -- the tile's last arriver reads it serially (~1 us per 16 KB,
 # cdna_hip_programming.md §5); larger slabs (M ~ 64) go through the wide
 # add_partials_resid kernel instead.
-RESID_INLAUNCH_MAX_BYTES = 32 << 10
+RESID_INLAUNCH_MAX_BYTES = int(__import__("os").environ.get("XGS_RESID_INLAUNCH_MAX_BYTES", str(32 << 10)))
 
 
 @dataclass
@@ -241,8 +241,8 @@ class ResidWorkspace:
     Statistics site 0 is the embedding; sites 2i+1 / 2i+2 follow layer i's
     attention / MLP residual adds."""
 
-    MAX_TILES = 64  # per-tile statistics a consumer can combine (ss_n <= 64, M <= 16)
-    IN_LAUNCH_MAX_M = 16
+    MAX_TILES = 64  # per-tile statistics a consumer can combine (ss_n <= 64)
+    IN_LAUNCH_MAX_M = 64
 
     def __init__(self, n_sites: int, max_m: int, H: int, device):
         self.max_m = max_m
