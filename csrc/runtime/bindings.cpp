@@ -232,6 +232,8 @@ PYBIND11_MODULE(_runtime, m) {
       .def_readwrite("admit_watermark", &SchedulerConfig::admit_watermark)
       .def_readwrite("max_prefill_seqs", &SchedulerConfig::max_prefill_seqs)
       .def_readwrite("decode_prefill_cap", &SchedulerConfig::decode_prefill_cap)
+      .def_readwrite("align_tokens", &SchedulerConfig::align_tokens)
+      .def_readwrite("align_slack", &SchedulerConfig::align_slack)
       .def_readwrite("eos_ids", &SchedulerConfig::eos_ids);
 
   py::class_<StepScheduler>(m, "StepScheduler")

@@ -51,6 +51,14 @@ struct SchedulerConfig {
   // Stall-free batching: prompt chunks ride on the decode step's weight reads
   // instead of stalling every running stream behind one large prefill step.
   int decode_prefill_cap = 0;
+  // GEMM-tile alignment of mixed steps: when a step's token count exceeds a
+  // multiple of align_tokens by at most align_slack, its last prefill chunk is
+  // trimmed back to that multiple (the trimmed tokens run next step). The prefill
+  // projections (hipBLASLt) cost a step function of M with steps at multiples of
+  // 256 rows: Llama-3-8B M 575 costs 286 us/layer, M 512 221 us
+  // (profiles/r2_prefill_m_sweep.jsonl). 0: off.
+  int align_tokens = 0;
+  int align_slack = 0;
   std::vector<int32_t> eos_ids;
 };
 
@@ -160,6 +168,7 @@ class StepScheduler {
   void preempt(Sequence& s);
   void insert_waiting(Sequence* s);
   void emit(Sequence& s, int q_len, bool prefill, bool sample);
+  void align_step();
   int check_stop(Sequence& s);
   void forget(Sequence* s);  // drop s from the plan / lookahead records
 

@@ -70,6 +70,13 @@ class EngineConfig:
     max_prefill_seqs: int = 1 << 30
     # prefill tokens allowed in a step that also decodes (0: only the token budget)
     decode_prefill_cap: int = 0
+    # mixed steps that overshoot a multiple of align_tokens by <= align_slack tokens
+    # trim their last prompt chunk back to it (GEMM tile quantization; 0: off).
+    # Off by default: measured slower at 64 concurrent (6.03-6.04 vs 5.93-5.97
+    # ms/step, p50 TTFT 20 vs 14 ms; profiles/r2_align_ab.md) -- the trimmed prompt's
+    # eager follow-up step costs more than the 575 -> 512-row GEMM step saves.
+    align_tokens: int = 0
+    align_slack: int = 64
     # speculative decoding (Req 12)
     draft_model: Optional[str] = None
     num_speculative_tokens: int = 0
@@ -129,6 +136,8 @@ class LLMEngine:
         sc.cache_threshold = cfg.cache_threshold
         sc.max_prefill_seqs = cfg.max_prefill_seqs
         sc.decode_prefill_cap = int(os.environ.get("XGS_DECODE_PREFILL_CAP", cfg.decode_prefill_cap))
+        sc.align_tokens = int(os.environ.get("XGS_ALIGN_TOKENS", cfg.align_tokens))
+        sc.align_slack = int(os.environ.get("XGS_ALIGN_SLACK", cfg.align_slack))
         sc.eos_ids = list(self.mcfg.eos_token_ids)
         self.sched = R.StepScheduler(sc)
         # decode graphs capture the TP collectives: RCCL (and the IPC all-reduce) can be
