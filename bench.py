@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--prompt-len", type=int, default=512)
     ap.add_argument("--output-len", type=int, default=256)
     ap.add_argument("--max-batched-tokens", type=int, default=8192)
-    ap.add_argument("--moe-comm", default="alltoall", choices=["alltoall", "allreduce"])
+    ap.add_argument("--moe-comm", default="auto", choices=["auto", "alltoall", "allreduce"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--weight-dtype", default=None, choices=["fp8"],
                     help="fp8: E4M3 weight copies for batch <= 16 decode (not the bf16 headline)")

@@ -66,7 +66,8 @@ def _rank_main(rank, world, port, ck, moe_comm, q):
 
 @pytest.mark.parametrize("kind,world,moe_comm", [("gqa8", 4, "alltoall"), ("gqa8", 8, "alltoall"),
                                                  ("mixtral", 4, "alltoall"), ("mixtral", 4, "alltoall-exact"),
-                                                 ("mixtral", 2, "alltoall-exact"), ("mixtral", 4, "allreduce")])
+                                                 ("mixtral", 2, "alltoall-exact"), ("mixtral", 4, "allreduce"),
+                                                 ("mixtral", 2, "auto")])
 def test_tp_full_degree_matches_fp32_reference(tmp_path, kind, world, moe_comm):
     from xgserve.models import build_model, save_checkpoint
     from xgserve.models.reference import reference_logits

@@ -69,7 +69,8 @@ _UNFUSED = {"XGS_FUSED_DECODE": "0", "XGS_ASYNC_SCHED": "0"}
 
 @pytest.mark.parametrize("model,moe_comm,world,env", [
     ("llama", "alltoall", 2, None), ("llama", "alltoall", 2, _UNFUSED), ("llama", "alltoall", 4, None),
-    ("mixtral", "alltoall", 2, None), ("mixtral", "allreduce", 2, None)])
+    ("mixtral", "alltoall", 2, None), ("mixtral", "allreduce", 2, None), ("mixtral", "auto", 2, None),
+    ("mixtral", "alltoall", 2, {"XGS_EP_EXACT_MIN_PAIRS": "0"})])
 def test_tp2_on_one_gpu_matches_fp32_reference(tmp_path, model, moe_comm, world, env):
     """Llama: TP attention + MLP shards; by default the fused TP decode layer (one
     custom all-reduce launch per row-parallel projection reduces the split-K
@@ -77,7 +78,9 @@ def test_tp2_on_one_gpu_matches_fp32_reference(tmp_path, model, moe_comm, world,
     statistics), IPC LM-head gather, HIP graphs and asynchronous scheduling with
     the followers substituting their own sampled tokens; _UNFUSED is the eager
     unfused chain. Mixtral: TP=2 attention, EP=2 experts (4 + 4) exchanged by
-    fixed-capacity all-to-all or combined by all-reduce."""
+    all-to-all (HIP dispatch kernels, fixed-capacity or count-exact splits) or
+    combined by all-reduce, or "auto" (all-reduce on the custom IPC kernel for the
+    decode steps, all-to-all for the prompt step)."""
     from xgserve.models import build_model, save_checkpoint
     from xgserve.models.reference import reference_logits
     from xgserve.ops import _native

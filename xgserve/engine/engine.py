@@ -66,7 +66,7 @@ class EngineConfig:
     use_graphs: bool = True
     graph_batch_sizes: Optional[List[int]] = None
     seed: int = 0
-    moe_comm: str = "alltoall"
+    moe_comm: str = "auto"
     max_prefill_seqs: int = 1 << 30
     # prefill tokens allowed in a step that also decodes (0: only the token budget)
     decode_prefill_cap: int = 0

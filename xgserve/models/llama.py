@@ -6,8 +6,10 @@ Tensor parallelism (Megatron layout, one process per GPU, RCCL/xGMI):
   * the LM head is vocab-parallel (logits all-gathered), the embedding is
     replicated (2 GB for 70B -- negligible in 288 GB of HBM).
 Expert parallelism (Mixtral): EP == TP group, rank r owns experts
-[r*E/tp, (r+1)*E/tp). Two exchange modes:
-  * "alltoall" (default for tp > 1, BASELINE config 5): each rank routes its
+[r*E/tp, (r+1)*E/tp). Two exchange forms, chosen per step by moe_comm "auto" (the
+default: allreduce for decode-sized steps on the custom IPC all-reduce, all_to_all
+for prefill-sized ones) or forced with "alltoall" / "allreduce":
+  * "alltoall" (prefill steps under "auto"; BASELINE config 5): each rank routes its
     token slice, packs (token, choice) rows for the expert owners with the HIP
     ep_plan / ep_scatter kernels (count-exact splits on eager prefill steps,
     fixed capacity under graph capture), runs its local experts as one grouped
@@ -61,6 +63,9 @@ TP_OVERLAP_MIN_TOKENS = int(os.environ.get("XGS_TP_OVERLAP_MIN_TOKENS", "256"))
 # EP all_to_all: steps with at least this many (token, choice) pairs (and not under
 # graph capture) exchange exact per-destination counts first and send only real rows
 EP_EXACT_MIN_PAIRS = int(os.environ.get("XGS_EP_EXACT_MIN_PAIRS", "256"))
+# moe_comm "auto": steps of at most this many tokens use the allreduce form when the
+# custom IPC all-reduce can take the [T, H] message
+EP_AR_MAX_TOKENS = int(os.environ.get("XGS_EP_AR_MAX_TOKENS", "64"))
 
 
 @torch.no_grad()
@@ -105,7 +110,7 @@ class LlamaLayer(nn.Module):
             self.gate_up = _p(z(2 * Fl, H))
             self.down = _p(z(H, Fl))
         self.attn = PagedAttention(Hq, Hkv, D)
-        self.moe_comm = "allreduce"
+        self.moe_comm = "auto"
         # decode fast path: skinny split-K GEMMs whose partial sums are reduced by
         # the consuming kernel (rope_cache / add+rmsnorm); SiLU fused in gate_up.
         Nqkv = (Hq + 2 * Hkv) * D
@@ -193,9 +198,28 @@ class LlamaLayer(nn.Module):
         full = comm.tp_all_gather_rows(out_slice)                         # [tp*per, H]
         return full[:T].contiguous()
 
+    def _moe_use_alltoall(self, h: torch.Tensor) -> bool:
+        """Exchange choice for a TP > 1 MoE layer. "auto" (default): the activations
+        are replicated after the head-parallel attention, so the allreduce form needs
+        no dispatch at all -- each rank runs its experts on the tokens routed to them
+        and one all-reduce sums the partial outputs. For decode-sized steps that
+        all-reduce is ONE launch of the custom IPC kernel (~latency of one xGMI hop),
+        where the all_to_all form costs three RCCL all_to_alls + an all_gather of tiny
+        messages per layer; prefill-sized steps take the all_to_all, which moves only
+        the routed rows (count-exact) instead of the whole [T, H] partial."""
+        if self.moe_comm == "alltoall":
+            return True
+        if self.moe_comm == "allreduce":
+            return False
+        if get_state().tp_size == 1:  # a simulated TP shard (bench --tp-shard): collectives are local
+            return False
+        ar = comm.custom_allreduce()
+        # the partial output is a fresh contiguous [T, H] bf16 tensor like h
+        return not (h.shape[0] <= EP_AR_MAX_TOKENS and ar is not None and ar.can_run(h.contiguous()))
+
     def mlp(self, h: torch.Tensor) -> torch.Tensor:
         if self.moe:
-            if self.tp > 1 and self.moe_comm == "alltoall":
+            if self.tp > 1 and self._moe_use_alltoall(h):
                 return self._moe_alltoall(h)
             return self._moe_allreduce(h)
         gu = F.linear(h, self.gate_up)

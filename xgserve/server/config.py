@@ -94,7 +94,7 @@ class WorkerSection:
     in_process: bool = False          # run the engine in a thread of the server process
     mock: bool = False                # deterministic MockEngine (tests / plumbing)
     mock_latency_ms: float = 1.0
-    moe_comm: str = "alltoall"
+    moe_comm: str = "auto"
     seed: int = 0
 
 
