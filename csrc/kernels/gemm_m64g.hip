@@ -630,6 +630,26 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
     if (rt0 >= offs[i] && rt0 < offs[i + 1]) e = i;
   if (e < 0) return;  // capacity padding past the last segment
   const int p0 = offs[e], p1 = offs[e + 1];
+  // MT_MAX 8 (prefill-sized steps): the two 64-row tiles of an aligned pair within
+  // the expert's segment run as ONE 128-row workgroup when the second tile holds
+  // real rows -- the expert's weight tile is streamed once per 128 rows instead of
+  // once per 64 (at ~144 rows per expert the re-reads are what bound the GEMM).
+  // Both workgroups of the pair count the pair's real rows the same way; the odd
+  // one exits when the even one takes the pair. Real rows lead each segment.
+  if constexpr (MT_MAX >= 8) {
+    const int lt = (rt0 - p0) >> 6, ntl = (p1 - p0) >> 6;
+    const int pe = lt & ~1;
+    if (pe + 1 < ntl) {
+      const int r0 = p0 + 64 * pe;
+      const int t = threadIdx.x;
+      const int real = valid != nullptr ? __syncthreads_count(t < 128 && valid[r0 + t] >= 0) : 128;
+      if (real > 64) {
+        if (lt & 1) return;
+        grouped_body<NW, WV, KC, NT, 8>(x, rows, e, p0, p1, r0, K, w, N, P, part, out, mode, lds0, lds1, lds2);
+        return;
+      }
+    }
+  }
   int amt = MT_MAX;
   if (valid != nullptr && MT_MAX > 1) {
     const int t = threadIdx.x;
@@ -665,10 +685,21 @@ static bool m64g_mt1_enabled() {
   return on;
 }
 
+// XGS_M64G_MT8=0: no 128-row pairs in the grouped GEMM (A/B).
+static bool m64g_mt8_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("XGS_M64G_MT8");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
+int m64g_cfg_kc(int cfg);
+
 template <int NW>
 static void launch_m64g_grouped(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, const int32_t* rows,
                                 const int32_t* offs, const int32_t* valid, int E, int K, const uint16_t* w, int N,
-                                int P, float* part, uint16_t* out, int mode, bool mt1) {
+                                int P, float* part, uint16_t* out, int mode, bool mt1, bool mt8) {
 #define XGK_GRP_MT(WV, KC, NT, MT)                                                                              \
   hipLaunchKernelGGL((gemm_m64g_grouped_kernel<NW, WV, KC, NT, MT>), grid, dim3(64 * WV), 0, st, x, rows, offs, \
                      valid, E, K, w, N, P, part, out, mode)
@@ -677,17 +708,25 @@ static void launch_m64g_grouped(int cfg, dim3 grid, hipStream_t st, const uint16
     if (mt1) XGK_GRP_MT(WV, KC, NT, 1);  \
     else XGK_GRP_MT(WV, KC, NT, 4);      \
   } while (0)
+  // 128-row pairs (KC 64 configs only: the x slot doubles)
+#define XGK_GRP8(WV, KC, NT)                         \
+  do {                                               \
+    if (mt8) XGK_GRP_MT(WV, KC, NT, 8);              \
+    else if (mt1) XGK_GRP_MT(WV, KC, NT, 1);         \
+    else XGK_GRP_MT(WV, KC, NT, 4);                  \
+  } while (0)
   // the 4-wave KC-64 configs have < 1 x DMA instruction per wave at 16 rows: MT >= 2
   switch (cfg) {
     case 1: XGK_GRP(4, 128, true); break;
-    case 2: XGK_GRP_MT(4, 64, false, 4); break;
-    case 3: XGK_GRP_MT(4, 64, true, 4); break;
-    case 4: XGK_GRP(2, 64, false); break;
-    case 5: XGK_GRP(2, 64, true); break;
+    case 2: if (mt8) XGK_GRP_MT(4, 64, false, 8); else XGK_GRP_MT(4, 64, false, 4); break;
+    case 3: if (mt8) XGK_GRP_MT(4, 64, true, 8); else XGK_GRP_MT(4, 64, true, 4); break;
+    case 4: XGK_GRP8(2, 64, false); break;
+    case 5: XGK_GRP8(2, 64, true); break;
     case 6: XGK_GRP(2, 128, true); break;
     default: XGK_GRP(4, 128, false); break;
   }
 #undef XGK_GRP
+#undef XGK_GRP8
 #undef XGK_GRP_MT
 }
 
@@ -710,8 +749,11 @@ int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, i
   if (P == 0) return 0;
   const dim3 grid(N / cols, S, P / 64);
   const bool mt1 = max_rows <= 16 && cfg != 2 && cfg != 3 && m64g_mt1_enabled();
-  if (nw == 1) launch_m64g_grouped<1>(cfg, grid, st, x, rows, offs, valid, E, K, w, N, P, part, out, mode, mt1);
-  else launch_m64g_grouped<2>(cfg, grid, st, x, rows, offs, valid, E, K, w, N, P, part, out, mode, mt1);
+  // 128-row pairs for prefill-sized steps (> 256 pairs; decode keeps the 48 KB-slot
+  // kernel and its occupancy), KC 64 configs only
+  const bool mt8 = max_rows > 256 && m64g_cfg_kc(cfg) == 64 && m64g_mt8_enabled();
+  if (nw == 1) launch_m64g_grouped<1>(cfg, grid, st, x, rows, offs, valid, E, K, w, N, P, part, out, mode, mt1, mt8);
+  else launch_m64g_grouped<2>(cfg, grid, st, x, rows, offs, valid, E, K, w, N, P, part, out, mode, mt1, mt8);
   return 0;
 }
 

@@ -254,7 +254,10 @@ def _w13(E, F, H):
 
 
 @pytest.mark.parametrize("T,E,k,H,F", [(1, 8, 2, 512, 256), (2, 8, 2, 1024, 512), (37, 8, 2, 1024, 512),
-                                       (64, 8, 2, 4096, 1792), (200, 8, 2, 4096, 1792)])
+                                       (64, 8, 2, 4096, 1792), (200, 8, 2, 4096, 1792),
+                                       # prefill-sized: experts with > 64 rows -> 128-row tile pairs
+                                       # (odd tile counts, a partial second tile, one-tile experts)
+                                       (300, 4, 2, 1024, 512), (575, 8, 2, 4096, 1792), (97, 2, 2, 512, 256)])
 def test_fused_moe(T, E, k, H, F):
     x = rnd(T, H)
     w13 = _w13(E, F, H)

@@ -25,6 +25,11 @@ MOE_CFG_W2 = 1
 import os as _os
 MOE_ROW_DISPATCH = _os.environ.get("XGS_MOE_ROW_DISPATCH", "1") != "0"
 MOE_DENSE_MIN_PAIRS = int(_os.environ.get("XGS_MOE_DENSE_MIN_PAIRS", str(1 << 30)))
+# prefill-sized steps (> 256 token-expert pairs): w2 on a KC-64 config so the grouped
+# kernel can run 128-row tile pairs (each expert's weights streamed once per 128 rows
+# instead of per 64; XGS_M64G_MT8=0 turns the pairs off, and w13's cfg 5 is KC 64)
+MOE_PREFILL_PAIRS = 256
+MOE_CFG_W2_PREFILL = int(_os.environ.get("XGS_MOE_CFG_W2_PREFILL", "3"))
 
 
 def moe_topk_softmax(router_logits: torch.Tensor, k: int, renorm: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -133,7 +138,7 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
          act.data_ptr(), 1, 2, 2, stream_ptr(), cfg=cfg13)
     # w2 has only H/128 column tiles per expert: split K while few experts are active
     nw2 = 2 if H % 128 == 0 else 1
-    cfg2 = MOE_CFG_W2 if MOE_GLDS and nw2 == 2 else 0
+    cfg2 = (MOE_CFG_W2_PREFILL if T * k > MOE_PREFILL_PAIRS else MOE_CFG_W2) if MOE_GLDS and nw2 == 2 else 0
     kc2 = 128
     S = 1
     for sk in ((4, 2) if T * k <= 4 else (2,) if T * k <= 16 else ()):
