@@ -630,21 +630,35 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
     if (rt0 >= offs[i] && rt0 < offs[i + 1]) e = i;
   if (e < 0) return;  // capacity padding past the last segment
   const int p0 = offs[e], p1 = offs[e + 1];
-  // MT_MAX 8 (prefill-sized steps): the two 64-row tiles of an aligned pair within
-  // the expert's segment run as ONE 128-row workgroup when the second tile holds
-  // real rows -- the expert's weight tile is streamed once per 128 rows instead of
-  // once per 64 (at ~144 rows per expert the re-reads are what bound the GEMM).
-  // Both workgroups of the pair count the pair's real rows the same way; the odd
-  // one exits when the even one takes the pair. Real rows lead each segment.
+  // MT_MAX 8 / 12 (prefill-sized steps): the 64-row tiles of an aligned group of 2 / 3
+  // within the expert's segment run as ONE 128- or 192-row workgroup when more than
+  // one of them holds real rows -- the expert's weight tile is streamed once per
+  // group instead of once per 64 rows (at ~144 rows per expert the re-reads are
+  // what bound the GEMM). Every workgroup of a group counts the group's real rows
+  // the same way; all but the leader exit when it takes them. Real rows lead each
+  // segment, so the tiles past them are pads (never read by the combine).
   if constexpr (MT_MAX >= 8) {
+    constexpr int GT = MT_MAX / 4;                // tiles per group (2: pairs, 3: triples)
     const int lt = (rt0 - p0) >> 6, ntl = (p1 - p0) >> 6;
-    const int pe = lt & ~1;
-    if (pe + 1 < ntl) {
-      const int r0 = p0 + 64 * pe;
+    const int gs = lt / GT * GT, gn = min(GT, ntl - gs);
+    if (gn >= 2) {
+      const int r0 = p0 + 64 * gs, nrow = 64 * gn;
       const int t = threadIdx.x;
-      const int real = valid != nullptr ? __syncthreads_count(t < 128 && valid[r0 + t] >= 0) : 128;
-      if (real > 64) {
-        if (lt & 1) return;
+      int real = nrow;
+      if (valid != nullptr) {
+        real = __syncthreads_count(t < nrow && valid[r0 + t] >= 0);
+        if constexpr (64 * WV < 64 * GT)
+          real += __syncthreads_count(t + 64 * WV < nrow && valid[r0 + t + 64 * WV] >= 0);
+      }
+      const int need = (real + 63) >> 6;           // tiles holding real rows (they lead the segment)
+      if (need >= 2) {
+        if (lt != gs) return;                      // the group leader takes the group's real tiles
+        if constexpr (GT >= 3) {
+          if (need == 3) {
+            grouped_body<NW, WV, KC, NT, 12>(x, rows, e, p0, p1, r0, K, w, N, P, part, out, mode, lds0, lds1, lds2);
+            return;
+          }
+        }
         grouped_body<NW, WV, KC, NT, 8>(x, rows, e, p0, p1, r0, K, w, N, P, part, out, mode, lds0, lds1, lds2);
         return;
       }
@@ -694,6 +708,18 @@ static bool m64g_mt8_enabled() {
   return on;
 }
 
+// XGS_M64G_GROUP=3: groups of up to three tiles (an expert of up to 192 rows in one
+// workgroup). Default 2 (pairs): measured faster on Mixtral's mixed steps (35.7 vs
+// 38.5 ms, profiles/r2_moe_pairs_ab.md) -- the 192-row body's registers halve the
+// occupancy of every workgroup in the launch.
+static bool m64g_group3() {
+  static const bool on = [] {
+    const char* e = std::getenv("XGS_M64G_GROUP");
+    return e != nullptr && e[0] == '3';
+  }();
+  return on;
+}
+
 int m64g_cfg_kc(int cfg);
 
 template <int NW>
@@ -711,15 +737,24 @@ static void launch_m64g_grouped(int cfg, dim3 grid, hipStream_t st, const uint16
   // 128-row pairs (KC 64 configs only: the x slot doubles)
 #define XGK_GRP8(WV, KC, NT)                         \
   do {                                               \
-    if (mt8) XGK_GRP_MT(WV, KC, NT, 8);              \
+    if (mt8 && m64g_group3()) XGK_GRP_MT(WV, KC, NT, 12); \
+    else if (mt8) XGK_GRP_MT(WV, KC, NT, 8);         \
     else if (mt1) XGK_GRP_MT(WV, KC, NT, 1);         \
     else XGK_GRP_MT(WV, KC, NT, 4);                  \
   } while (0)
   // the 4-wave KC-64 configs have < 1 x DMA instruction per wave at 16 rows: MT >= 2
   switch (cfg) {
     case 1: XGK_GRP(4, 128, true); break;
-    case 2: if (mt8) XGK_GRP_MT(4, 64, false, 8); else XGK_GRP_MT(4, 64, false, 4); break;
-    case 3: if (mt8) XGK_GRP_MT(4, 64, true, 8); else XGK_GRP_MT(4, 64, true, 4); break;
+    case 2:
+      if (mt8 && m64g_group3()) XGK_GRP_MT(4, 64, false, 12);
+      else if (mt8) XGK_GRP_MT(4, 64, false, 8);
+      else XGK_GRP_MT(4, 64, false, 4);
+      break;
+    case 3:
+      if (mt8 && m64g_group3()) XGK_GRP_MT(4, 64, true, 12);
+      else if (mt8) XGK_GRP_MT(4, 64, true, 8);
+      else XGK_GRP_MT(4, 64, true, 4);
+      break;
     case 4: XGK_GRP8(2, 64, false); break;
     case 5: XGK_GRP8(2, 64, true); break;
     case 6: XGK_GRP(2, 128, true); break;
