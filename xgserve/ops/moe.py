@@ -30,6 +30,7 @@ MOE_DENSE_MIN_PAIRS = int(_os.environ.get("XGS_MOE_DENSE_MIN_PAIRS", str(1 << 30
 # instead of per 64; XGS_M64G_MT8=0 turns the pairs off, and w13's cfg 5 is KC 64)
 MOE_PREFILL_PAIRS = 256
 MOE_CFG_W2_PREFILL = int(_os.environ.get("XGS_MOE_CFG_W2_PREFILL", "3"))
+MOE_CFG_W13_PREFILL = int(_os.environ.get("XGS_MOE_CFG_W13_PREFILL", "3"))
 
 
 def moe_topk_softmax(router_logits: torch.Tensor, k: int, renorm: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -133,7 +134,8 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     else:
         def gemm(*a, cfg=0):
             kn.moe_gemm_m64(*a)
-    cfg13 = MOE_CFG_W13 if (MOE_GLDS and H % (64 * 1) == 0 and F2 % 128 == 0) else 0
+    cfg13 = ((MOE_CFG_W13_PREFILL if T * k > MOE_PREFILL_PAIRS else MOE_CFG_W13)
+             if (MOE_GLDS and H % (64 * 1) == 0 and F2 % 128 == 0) else 0)
     gemm(x.contiguous().data_ptr(), sorted_rows.data_ptr(), offs.data_ptr(), E, H, w13.data_ptr(), F2, P, 0,
          act.data_ptr(), 1, 2, 2, stream_ptr(), cfg=cfg13)
     # w2 has only H/128 column tiles per expert: split K while few experts are active
