@@ -110,6 +110,9 @@ class LlamaLayer(nn.Module):
             self.gate_up = _p(z(2 * Fl, H))
             self.down = _p(z(H, Fl))
         self.attn = PagedAttention(Hq, Hkv, D)
+        # the decode attention kernel's fused-QKV form (D = 128, GQA groups of 1/2/4/8)
+        self.attn_fq_ok = (torch.device(device).type == "cuda" and D == 128 and Hq % Hkv == 0
+                           and Hq // Hkv in (1, 2, 4, 8))
         self.moe_comm = "auto"
         # decode fast path: skinny split-K GEMMs whose partial sums are reduced by
         # the consuming kernel (rope_cache / add+rmsnorm); SiLU fused in gate_up.
@@ -266,9 +269,14 @@ class LlamaLayer(nn.Module):
             return self._row_parallel_fast(act, self.down, self.split_down), residual
         if self.m64_ok and T <= FAST_M_SLAB:
             # gemm_m64g (LDS-DMA weight streaming) for every projection: split-K partials
-            # go to the consumers (rope_cache / add+rmsnorm), SiLU-gate fused in gate_up
+            # go to the consumers (rope_cache / add+rmsnorm), SiLU-gate fused in gate_up;
+            # pure-decode steps reduce the QKV partials + RoPE + KV append in the
+            # attention prologue (one launch instead of two; MoE layers, TP fallback)
             pqkv = m64_linear(h, self.qkv, MODE_PARTIAL)
-            a = self.attn.from_partials(pqkv, meta, kv, cos_sin)
+            if T == meta.num_decodes and self.attn_fq_ok:
+                a = self.attn.fused_decode(pqkv, meta, kv, cos_sin)
+            else:
+                a = self.attn.from_partials(pqkv, meta, kv, cos_sin)
             o = m64_linear(a, self.o, MODE_PARTIAL)
             if self.tp > 1:
                 o = self._ar(o.materialize())
