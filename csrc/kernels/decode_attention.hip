@@ -70,6 +70,7 @@ struct QkvFuse {
   const uint8_t* pf;
   int64_t pf_bytes;
   int pf_slices;
+  int preload;  // request the first K/V tiles before the prologue (XGS_DECODE_PRELOAD, default 1)
 };
 
 // One prefetch workgroup: reads its contiguous share of [pf, pf + pf_bytes) in
@@ -248,6 +249,34 @@ __global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
   __shared__ float o_lds[C::WAVES][G][D];
   __shared__ __attribute__((aligned(16))) uint16_t q_lds[FQ ? G * D : 8];
 
+  const int32_t* bt = block_tables + static_cast<int64_t>(b) * bt_stride;
+  const int64_t head_stride = static_cast<int64_t>(bs) * D;
+  // two register tiles per wave (K fragments + V rows): tile t+W and t+2W are in
+  // flight while tile t is processed (one tile of lookahead left HBM idle between
+  // a wave's tiles at 64 concurrent sequences)
+  uint4 kfA[C::KK], vrA[C::VLD], kfB[C::KK], vrB[C::VLD];
+  auto load_tile = [&](int t, uint4 (&kf)[C::KK], uint4 (&vr)[C::VLD]) {
+    const int key0 = t * 16;
+    const int page = bt[key0 / bs];
+    const int64_t base = (static_cast<int64_t>(page) * Hkv + kvh) * head_stride + static_cast<int64_t>(key0 % bs) * D;
+    const uint16_t* kp = kc + base + li * D + 8 * g;
+#pragma unroll
+    for (int kk = 0; kk < C::KK; ++kk) kf[kk] = ld16(kp + kk * 32);
+#pragma unroll
+    for (int i = 0; i < C::VLD; ++i) {
+      const int c = lane + 64 * i;  // chunk id in the 16 x NCH tile
+      vr[i] = ld16(vc + base + (c / C::NCH) * D + (c % C::NCH) * 8);
+    }
+  };
+  const int t0 = t_begin + wid;
+  // FQ: the first two tiles of each wave are requested BEFORE the prologue (their
+  // bytes do not depend on q), so the K/V latency overlaps the QKV-partial reads --
+  // except the tile holding the key the prologue appends (the last one), which is
+  // loaded after the prologue's barrier as before
+  const bool preA = FQ && fq.preload && t0 < t_end && t0 != ntiles - 1;
+  const bool preB = FQ && fq.preload && t0 + C::WAVES < t_end && t0 + C::WAVES != ntiles - 1;
+  if (preA) load_tile(t0, kfA, vrA);
+  if (preB) load_tile(t0 + C::WAVES, kfB, vrB);
   if constexpr (FQ) {
     if (L > 0) decode_qkv_prologue<D, G>(fq, b, kvh, Hq, Hkv, bs, split == (ntiles - 1) / tps, q_lds);
     __syncthreads();
@@ -271,27 +300,7 @@ __global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
 #pragma unroll
   for (int mt = 0; mt < C::MT; ++mt) o[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int32_t* bt = block_tables + static_cast<int64_t>(b) * bt_stride;
-  const int64_t head_stride = static_cast<int64_t>(bs) * D;
   uint16_t* my_v = v_lds[wid];
-
-  // two register tiles per wave (K fragments + V rows): tile t+W and t+2W are in
-  // flight while tile t is processed (one tile of lookahead left HBM idle between
-  // a wave's tiles at 64 concurrent sequences)
-  uint4 kfA[C::KK], vrA[C::VLD], kfB[C::KK], vrB[C::VLD];
-  auto load_tile = [&](int t, uint4 (&kf)[C::KK], uint4 (&vr)[C::VLD]) {
-    const int key0 = t * 16;
-    const int page = bt[key0 / bs];
-    const int64_t base = (static_cast<int64_t>(page) * Hkv + kvh) * head_stride + static_cast<int64_t>(key0 % bs) * D;
-    const uint16_t* kp = kc + base + li * D + 8 * g;
-#pragma unroll
-    for (int kk = 0; kk < C::KK; ++kk) kf[kk] = ld16(kp + kk * 32);
-#pragma unroll
-    for (int i = 0; i < C::VLD; ++i) {
-      const int c = lane + 64 * i;  // chunk id in the 16 x NCH tile
-      vr[i] = ld16(vc + base + (c / C::NCH) * D + (c % C::NCH) * 8);
-    }
-  };
 
   auto process = [&](int t, uint4 (&kf)[C::KK], uint4 (&vr)[C::VLD]) {
     uint4 kcur[C::KK];
@@ -349,9 +358,9 @@ __global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
     }
   };
 
-  int t = t_begin + wid;
-  if (t < t_end) load_tile(t, kfA, vrA);
-  if (t + C::WAVES < t_end) load_tile(t + C::WAVES, kfB, vrB);
+  int t = t0;
+  if (t < t_end && !preA) load_tile(t, kfA, vrA);
+  if (t + C::WAVES < t_end && !preB) load_tile(t + C::WAVES, kfB, vrB);
   for (; t < t_end; t += 2 * C::WAVES) {
     process(t, kfA, vrA);
     if (t + C::WAVES >= t_end) break;
@@ -484,7 +493,7 @@ int decode_attention(const uint16_t* q, int64_t q_stride, const uint16_t* kc, co
   if (B <= 0) return 0;
   if (bs % 16 != 0 || Hq % Hkv != 0) return -1;
   const int G = Hq / Hkv;
-  const QkvFuse nofuse{nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0, 0};
+  const QkvFuse nofuse{nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0, 0, 0};
 #define XGK_DEC(DD, GG)                                                                                  \
   if (D == DD && G == GG) {                                                                              \
     launch_decode<DD, GG, false>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, part_out, part_lse, out,  \
@@ -509,8 +518,12 @@ int decode_attention_fq(const float* part, int S_qkv, const int32_t* positions, 
   if (num_splits > 1 && (part_out == nullptr || part_lse == nullptr)) return -1;
   if (out == nullptr && (num_splits == 1 || counters != nullptr)) return -1;  // deferred combine needs split slabs
   if (pf_slices < 0 || (pf_slices > 0 && (pf == nullptr || pf_bytes <= 0))) return -1;
+  static const int preload = [] {
+    const char* e = std::getenv("XGS_DECODE_PRELOAD");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
   const QkvFuse fq{part, S_qkv, positions, cos_sin, slots, kc, vc, apply_rope,
-                   static_cast<const uint8_t*>(pf), pf_bytes, pf_slices};
+                   static_cast<const uint8_t*>(pf), pf_bytes, pf_slices, preload};
   const int G = Hq / Hkv;
 #define XGK_DECF(GG)                                                                                         \
   if (G == GG) {                                                                                             \
