@@ -76,10 +76,15 @@ void moe_topk_softmax(const void* logits, int is_f32, int T, int E, int k, int r
 // 8-element chunks of the hidden row with all EM (>= E) router rows in fp32,
 // block reduction, then lane 0 selects the top k (softmax over all E, optionally
 // renormalised over the chosen k: Mixtral semantics).
-template <int EM>
+// Fused-decode form (NORM): h is the raw residual stream; the workgroup first takes
+// the row's RMSNorm (sum of squares, block reduction), writes the normalised row
+// hn = bf16(x * rsqrt(mean(x^2) + eps) * norm_w) for the expert GEMMs and routes on
+// those bf16 values -- the post-attention RMSNorm launch disappears.
+template <int EM, bool NORM = false>
 __global__ void __launch_bounds__(256) route_kernel(const uint16_t* __restrict__ h, const uint16_t* __restrict__ wr,
                                                     int H, int E, int k, int renorm, float* __restrict__ w,
-                                                    int32_t* __restrict__ ids) {
+                                                    int32_t* __restrict__ ids, const uint16_t* __restrict__ norm_w = nullptr,
+                                                    float eps = 0.f, uint16_t* __restrict__ hn = nullptr) {
   __shared__ float red[4][EM];
   const int t = blockIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -87,9 +92,34 @@ __global__ void __launch_bounds__(256) route_kernel(const uint16_t* __restrict__
 #pragma unroll
   for (int e = 0; e < EM; ++e) acc[e] = 0.f;
   const uint16_t* hr = h + static_cast<int64_t>(t) * H;
+  float scale = 1.f;
+  if constexpr (NORM) {
+    float ss = 0.f;
+    for (int c = threadIdx.x; c < H / 8; c += 256) {
+      float x[8];
+      unpack8(ld16(hr + c * 8), x);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += x[i] * x[i];
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) red[wid][0] = ss;
+    __syncthreads();
+    ss = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    __syncthreads();  // red is reused for the router sums below
+    scale = rsqrtf(ss / static_cast<float>(H) + eps);
+  }
   for (int c = threadIdx.x; c < H / 8; c += 256) {
     float x[8];
     unpack8(ld16(hr + c * 8), x);
+    if constexpr (NORM) {
+      float g[8];
+      unpack8(ld16(norm_w + c * 8), g);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] = x[i] * scale * g[i];
+      const uint4 q = pack8(x);
+      st16(hn + static_cast<int64_t>(t) * H + c * 8, q);
+      unpack8(q, x);  // route on the bf16 values the experts will see
+    }
 #pragma unroll
     for (int e = 0; e < EM; ++e) {
       if (e >= E) break;
@@ -135,16 +165,23 @@ __global__ void __launch_bounds__(256) route_kernel(const uint16_t* __restrict__
 }
 
 int moe_route(const uint16_t* h, const uint16_t* wr, int T, int H, int E, int k, int renorm, float* w, int32_t* ids,
-              hipStream_t st) {
+              hipStream_t st, const uint16_t* norm_w, float eps, uint16_t* hn) {
   if (T <= 0) return 0;
   if (H % 8 || E < 1 || E > 64 || k < 1 || k > 16 || k > E) return 1;
+  if ((norm_w == nullptr) != (hn == nullptr)) return 1;
   const dim3 g(T), b(256);
+  if (norm_w != nullptr) {
+    if (E <= 8) hipLaunchKernelGGL((route_kernel<8, true>), g, b, 0, st, h, wr, H, E, k, renorm, w, ids, norm_w, eps, hn);
+    else if (E <= 16) hipLaunchKernelGGL((route_kernel<16, true>), g, b, 0, st, h, wr, H, E, k, renorm, w, ids, norm_w, eps, hn);
+    else hipLaunchKernelGGL((route_kernel<64, true>), g, b, 0, st, h, wr, H, E, k, renorm, w, ids, norm_w, eps, hn);
+    return 0;
+  }
   if (E <= 8)
-    hipLaunchKernelGGL(route_kernel<8>, g, b, 0, st, h, wr, H, E, k, renorm, w, ids);
+    hipLaunchKernelGGL((route_kernel<8, false>), g, b, 0, st, h, wr, H, E, k, renorm, w, ids, nullptr, 0.f, nullptr);
   else if (E <= 16)
-    hipLaunchKernelGGL(route_kernel<16>, g, b, 0, st, h, wr, H, E, k, renorm, w, ids);
+    hipLaunchKernelGGL((route_kernel<16, false>), g, b, 0, st, h, wr, H, E, k, renorm, w, ids, nullptr, 0.f, nullptr);
   else
-    hipLaunchKernelGGL(route_kernel<64>, g, b, 0, st, h, wr, H, E, k, renorm, w, ids);
+    hipLaunchKernelGGL((route_kernel<64, false>), g, b, 0, st, h, wr, H, E, k, renorm, w, ids, nullptr, 0.f, nullptr);
   return 0;
 }
 
@@ -231,6 +268,77 @@ __global__ void __launch_bounds__(256) combine_kernel(const void* __restrict__ y
       for (int i = 0; i < 8; ++i) acc[i] += wt * f[i];
     }
     st16(out + static_cast<int64_t>(t) * H + c * 8, pack8(acc));
+  }
+}
+
+// Fused-decode form: resid[t] += sum_j w[t, j] * sum_s part[s][dest[t*k + j]] in place
+// (bf16 residual stream) and ss[c * T + t] = sum over 1024-column chunk c of the new
+// residual row squared (the next layer's RMSNorm statistics, read by gemm_m64g).
+// One workgroup per token; H <= 8192.
+template <int SP>
+__global__ void __launch_bounds__(256) combine_resid_kernel(const float* __restrict__ part, int P,
+                                                            const int32_t* __restrict__ dest,
+                                                            const float* __restrict__ w, uint16_t* __restrict__ resid,
+                                                            float* __restrict__ ss, int T, int k, int H) {
+  __shared__ float red[4][8];
+  const int t = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float sq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // per 1024-column chunk
+  for (int c = threadIdx.x; c < H / 8; c += 256) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < k; ++j) {
+      const int p = dest[t * k + j];
+      if (p < 0) continue;
+      const float wt = w[t * k + j];
+      float f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int s = 0; s < SP; ++s) {
+        const float* q = part + (static_cast<int64_t>(s) * P + p) * H + c * 8;
+        const float4 a = *reinterpret_cast<const float4*>(q);
+        const float4 b = *reinterpret_cast<const float4*>(q + 4);
+        f[0] += a.x; f[1] += a.y; f[2] += a.z; f[3] += a.w;
+        f[4] += b.x; f[5] += b.y; f[6] += b.z; f[7] += b.w;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += wt * f[i];
+    }
+    uint16_t* rp = resid + static_cast<int64_t>(t) * H + c * 8;
+    float r[8];
+    unpack8(ld16(rp), r);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] += acc[i];
+    const uint4 o = pack8(r);
+    st16(rp, o);
+    unpack8(o, r);  // statistics of the rounded bf16 residual
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v += r[i] * r[i];
+    const int chunk = (c * 8) >> 10;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sq[q] += chunk == q ? v : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float v = wave_sum(sq[q]);
+    if (lane == 0) red[wid][q] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < H / 1024) {
+    const int q = threadIdx.x;
+    ss[static_cast<int64_t>(q) * T + t] = red[0][q] + red[1][q] + red[2][q] + red[3][q];
+  }
+}
+
+int moe_combine_resid(const float* part, int S, int P, const int32_t* dest, const float* w, uint16_t* resid, float* ss,
+                      int T, int k, int H, hipStream_t st) {
+  if (T <= 0) return 0;
+  if (H % 1024 || H > 8192) return 1;
+  const dim3 g(T), b(256);
+  switch (S) {
+    case 1: hipLaunchKernelGGL(combine_resid_kernel<1>, g, b, 0, st, part, P, dest, w, resid, ss, T, k, H); return 0;
+    case 2: hipLaunchKernelGGL(combine_resid_kernel<2>, g, b, 0, st, part, P, dest, w, resid, ss, T, k, H); return 0;
+    case 4: hipLaunchKernelGGL(combine_resid_kernel<4>, g, b, 0, st, part, P, dest, w, resid, ss, T, k, H); return 0;
+    default: return 1;
   }
 }
 

@@ -54,7 +54,10 @@ int gemm_w8(const uint16_t*, int, int, const uint8_t*, const float*, int, float*
 void moe_topk_softmax(const void*, int, int, int, int, int, float*, int32_t*, hipStream_t);
 void moe_align(const int32_t*, int, int, int, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
 int moe_combine(const void*, int, int, const int32_t*, const float*, uint16_t*, int, int, int, hipStream_t);
-int moe_route(const uint16_t*, const uint16_t*, int, int, int, int, int, float*, int32_t*, hipStream_t);
+int moe_route(const uint16_t*, const uint16_t*, int, int, int, int, int, float*, int32_t*, hipStream_t,
+              const uint16_t*, float, uint16_t*);
+int moe_combine_resid(const float*, int, int, const int32_t*, const float*, uint16_t*, float*, int, int, int,
+                      hipStream_t);
 int ep_plan(const int32_t*, int, int, int, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
 int ep_scatter(const uint16_t*, int64_t, int, const int32_t*, int, int, uint16_t*, hipStream_t);
 int moe_gemm_m64(const uint16_t*, const int32_t*, const int32_t*, int, int, const uint16_t*, int, int, float*,
@@ -299,10 +302,19 @@ PYBIND11_MODULE(_kernels, m) {
      py::arg("P"), py::arg("part"), py::arg("out"), py::arg("splits"), py::arg("mode"), py::arg("nw"), py::arg("cfg"),
      py::arg("max_rows"), py::arg("st"), py::arg("valid") = 0);
   m.def("moe_route", [](uintptr_t h, uintptr_t wr, int T, int H, int E, int k, int renorm, uintptr_t w, uintptr_t ids,
-                        uintptr_t st) {
+                        uintptr_t st, uintptr_t norm_w, float eps, uintptr_t hn) {
+    // norm_w / hn != 0: h is the raw residual stream, normalised in-kernel (fused decode layer)
     check(xgk::moe_route(P<const uint16_t>(h), P<const uint16_t>(wr), T, H, E, k, renorm, P<float>(w),
-                         P<int32_t>(ids), S(st)),
+                         P<int32_t>(ids), S(st), P<const uint16_t>(norm_w), eps, P<uint16_t>(hn)),
           "moe_route");
+  }, py::arg("h"), py::arg("wr"), py::arg("T"), py::arg("H"), py::arg("E"), py::arg("k"), py::arg("renorm"),
+     py::arg("w"), py::arg("ids"), py::arg("st"), py::arg("norm_w") = 0, py::arg("eps") = 0.f, py::arg("hn") = 0);
+  m.def("moe_combine_resid", [](uintptr_t part, int splits, int P_, uintptr_t dest, uintptr_t w, uintptr_t resid,
+                                uintptr_t ss, int T, int k, int H, uintptr_t st) {
+    if (H % 1024 || H > 8192) throw std::invalid_argument("moe_combine_resid: H % 1024 == 0, H <= 8192");
+    check(xgk::moe_combine_resid(P<const float>(part), splits, P_, P<const int32_t>(dest), P<const float>(w),
+                                 P<uint16_t>(resid), P<float>(ss), T, k, H, S(st)),
+          "moe_combine_resid");
   });
   m.def("ep_plan", [](uintptr_t ids, int n_pairs, int E_local, int tp, int cap, int packed, uintptr_t slot,
                       uintptr_t send_eid, uintptr_t counts, uintptr_t st) {

@@ -54,6 +54,8 @@ FAST_M_SLAB = 64    # tokens per step for the O-projection slab kernel
 # statistics (comm.tp_allreduce_resid): 6 launches + attention per layer instead
 # of 11. XGS_FUSED_DECODE=0 restores the unfused chain (A/B measurements, tests).
 FUSED_DECODE = os.environ.get("XGS_FUSED_DECODE", "1") != "0"
+# MoE (Mixtral) layers on the fused decode layer (_fused_moe_tail); 0: the m64 chain
+FUSED_MOE_DECODE = os.environ.get("XGS_FUSED_MOE_DECODE", "1") != "0"
 # TP > 1 prefill-sized steps: the row-parallel all-reduces are pipelined over this
 # many token chunks and overlapped with the next chunk's GEMMs (RCCL stream); a
 # 2k-token 8B step moves 16 MiB per all-reduce -- ~100 us on 7 xGMI links, a
@@ -351,11 +353,36 @@ class LlamaLayer(nn.Module):
         T = resid.shape[0]
         xa = meta.num_splits > 1 and self.attn.D == 128 and m64_xa_ok(T, self.o.shape[0], self.o.shape[1])
         a = self.attn.fused_decode(pqkv, meta, kv, cos_sin, prefetch=self.o, defer_combine=xa)
+        if self.moe:
+            return self._fused_moe_tail(a, resid, ws, site)
         if self.tp > 1:
             return self._fused_tp_tail(a, resid, ws, site)
         st = m64_resid_linear(a, self.o, resid, ws, site, eps)
         act = m64_norm_linear(resid, self.gate_up, MODE_SILU, st, eps)
         return m64_resid_linear(act, self.down, resid, ws, site + 1, eps)
+
+    def _fused_moe_tail(self, a, resid: torch.Tensor, ws: ResidWorkspace, site: int) -> RowStats:
+        """MoE half of the fused decode layer: O GEMM (+ residual; under TP the custom
+        all-reduce with the residual) -> router with the post-attention RMSNorm in its
+        prologue (writes the normalised rows for the experts) -> align -> grouped w13
+        (SiLU-gate) -> grouped w2 -> combine + residual + next-norm statistics (under
+        TP: this rank's experts' partial through the residual all-reduce -- the
+        activations are replicated, so no dispatch). 7 launches instead of 9."""
+        T, H = resid.shape
+        eps = self.cfg.norm_eps
+        if self.tp > 1:
+            po = m64_linear(a, self.o, MODE_PARTIAL) if isinstance(a, torch.Tensor) else m64_xa_linear(a, self.o)
+            comm.tp_allreduce_resid(po.part, resid, ws.ss[site])
+        else:
+            m64_resid_linear(a, self.o, resid, ws, site, eps)  # its statistics go unused: the router renorms
+        hn, w, ids = ops.moe_route_norm(resid, self.post_norm, eps, self.router, self.cfg.experts_per_token)
+        ss = ws.ss[site + 1]
+        if self.tp > 1:
+            part = ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset)
+            comm.tp_allreduce_resid(part.float().unsqueeze(0), resid, ss)
+        else:
+            ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, resid=resid, ss=ss)
+        return RowStats(ss, H // 1024, T)
 
     def _fused_tp_tail(self, a: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace, site: int) -> RowStats:
         """Row-parallel half of the fused decode layer under TP: O GEMM partials ->
@@ -395,8 +422,8 @@ class LlamaForCausalLM(nn.Module):
         l0 = self.layers[0]
         self.norms_folded = False
         self.weight_dtype = "bf16"
-        self._fused_ok = (self.device.type == "cuda" and not l0.moe and l0.m64_ok
-                          and l0.m64_silu_ok and cfg.head_dim == 128 and l0.Hq % l0.Hkv == 0
+        self._fused_ok = (self.device.type == "cuda" and l0.m64_ok and (l0.moe or l0.m64_silu_ok)
+                          and (FUSED_MOE_DECODE or not l0.moe) and cfg.head_dim == 128 and l0.Hq % l0.Hkv == 0
                           and l0.Hq // l0.Hkv in (1, 2, 4, 8) and H % 1024 == 0 and H // 1024 <= 8)
         self._fused_small_ok = self._fused_ok and l0.m64_small_ok
         self._fused_ws = ResidWorkspace(2 * cfg.num_layers + 1, FAST_M_SLAB, H, device) if self._fused_ok else None
@@ -444,6 +471,9 @@ class LlamaForCausalLM(nn.Module):
     def fused_decode_ok(self, meta: AttnMeta) -> bool:
         T = meta.num_tokens
         if not (FUSED_DECODE and self._fused_ok and self.norms_folded) or T != meta.num_decodes or not 0 < T <= 64:
+            return False
+        l0 = self.layers[0]
+        if l0.moe and self.tp > 1 and l0.moe_comm == "alltoall":  # the fused MoE tail is the allreduce form
             return False
         if self.tp > 1 and not comm.resid_allreduce_ok(T, self.cfg.hidden_size):
             return False

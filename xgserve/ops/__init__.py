@@ -13,7 +13,8 @@ from .attention import (decode_attention, decode_attention_fused, prefill_attent
                         prefill_attention_ref, choose_num_splits)
 from .sampling import argmax_logprob, sample_tokens, argmax_logprob_ref, segment_sum, subst_tokens
 from .embedding import embed_gather, mean_l2norm_rows
-from .moe import moe_topk_softmax, moe_route, moe_align, moe_forward_ref, fused_moe, ep_plan, ep_scatter, ep_combine
+from .moe import (moe_topk_softmax, moe_route, moe_route_norm, moe_align, moe_forward_ref, fused_moe, ep_plan,
+                  ep_scatter, ep_combine)
 from ._native import available as native_available
 
 __all__ = [
@@ -23,6 +24,6 @@ __all__ = [
     "decode_attention", "decode_attention_fused", "prefill_attention", "decode_attention_ref", "prefill_attention_ref", "choose_num_splits",
     "argmax_logprob", "sample_tokens", "argmax_logprob_ref", "segment_sum", "subst_tokens",
     "embed_gather", "mean_l2norm_rows",
-    "moe_topk_softmax", "moe_route", "moe_align", "moe_forward_ref", "fused_moe", "ep_plan", "ep_scatter", "ep_combine",
+    "moe_topk_softmax", "moe_route", "moe_route_norm", "moe_align", "moe_forward_ref", "fused_moe", "ep_plan", "ep_scatter", "ep_combine",
     "native_available",
 ]

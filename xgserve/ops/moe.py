@@ -64,6 +64,25 @@ def moe_route(h: torch.Tensor, router: torch.Tensor, k: int, renorm: bool = True
     return w, ids
 
 
+def moe_route_norm(resid: torch.Tensor, norm_w: torch.Tensor, eps: float, router: torch.Tensor, k: int,
+                   renorm: bool = True):
+    """Fused decode layer: RMSNorm of the raw residual stream + router + top-k in one
+    launch -> (hn = bf16 normalised rows for the experts, weights, expert ids)."""
+    T, H = resid.shape
+    if not use_native(resid):
+        rf = resid.float()
+        hn = (rf * torch.rsqrt(rf.pow(2).mean(-1, keepdim=True) + eps) * norm_w.float()).to(resid.dtype)
+        w, ids = moe_route(hn, router, k, renorm)
+        return hn, w, ids
+    E = router.shape[0]
+    hn = torch.empty_like(resid)
+    w = torch.empty(T, k, dtype=torch.float32, device=resid.device)
+    ids = torch.empty(T, k, dtype=torch.int32, device=resid.device)
+    kernels().moe_route(resid.data_ptr(), router.data_ptr(), T, H, E, k, 1 if renorm else 0, w.data_ptr(),
+                        ids.data_ptr(), stream_ptr(), norm_w.data_ptr(), float(eps), hn.data_ptr())
+    return hn, w, ids
+
+
 def moe_align(ids: torch.Tensor, num_experts: int, expert_offset: int = 0, block_m: int = BLOCK_M):
     """Expert-sorted, block_m-padded layout of this rank's experts
     [expert_offset, expert_offset + num_experts). -> (sorted_rows [cap] (-1 = pad),
@@ -106,21 +125,32 @@ def moe_forward_ref(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w
 
 
 def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
-              topk_ids: torch.Tensor, expert_offset: int = 0) -> torch.Tensor:
+              topk_ids: torch.Tensor, expert_offset: int = 0, resid: Optional[torch.Tensor] = None,
+              ss: Optional[torch.Tensor] = None):
     """Local-expert MoE FFN: sum_j w_j * FFN_{e_j}(x) over choices owned locally
     (ids in [expert_offset, expert_offset + E_local)); others contribute nothing.
 
     align (one tiny kernel) -> grouped gemm_m64 on w13 with the SiLU-gate fused
     (x gathered through the sorted rows) -> grouped gemm_m64 on w2 (split-K
-    partials when few experts are active) -> combine (weights, partial sums)."""
+    partials when few experts are active) -> combine (weights, partial sums).
+    resid / ss given (fused decode layer): the combine adds into the bf16 residual
+    stream in place and writes the next RMSNorm's per-1024-column statistics
+    ss[c * T + t]; returns None."""
     if not use_native(x):
-        return moe_forward_ref(x, w13, w2, topk_w, topk_ids, expert_offset)
+        out = moe_forward_ref(x, w13, w2, topk_w, topk_ids, expert_offset)
+        if resid is None:
+            return out
+        r = (resid.float() + out.float()).to(resid.dtype)
+        resid.copy_(r)
+        T, H = r.shape
+        ss[: (H // 1024) * T].copy_(r.float().view(T, H // 1024, 1024).pow(2).sum(-1).t().reshape(-1))
+        return None
     T, k = topk_ids.shape
     E, F2, H = w13.shape
     F = F2 // 2
     sorted_rows, offs, dest = moe_align(topk_ids, E, expert_offset)
     P = sorted_rows.shape[0]
-    if T * k >= MOE_DENSE_MIN_PAIRS and not torch.cuda.is_current_stream_capturing():
+    if T * k >= MOE_DENSE_MIN_PAIRS and not torch.cuda.is_current_stream_capturing() and resid is None:
         return _moe_per_expert(x, w13, w2, topk_w, sorted_rows, offs, dest, T, k)
     act = torch.empty(P, F, dtype=x.dtype, device=x.device)
     kn = kernels()
@@ -150,6 +180,10 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     part = torch.empty(S, P, H, dtype=torch.float32, device=x.device)
     gemm(act.data_ptr(), 0, offs.data_ptr(), E, F, w2.data_ptr(), H, P, part.data_ptr(), 0, S, 1, nw2, stream_ptr(),
          cfg=cfg2)
+    if resid is not None:
+        kn.moe_combine_resid(part.data_ptr(), S, P, dest.data_ptr(), topk_w.float().contiguous().data_ptr(),
+                             resid.data_ptr(), ss.data_ptr(), T, k, H, stream_ptr())
+        return None
     out = torch.empty(T, H, dtype=x.dtype, device=x.device)
     kn.moe_combine(part.data_ptr(), S, P, dest.data_ptr(), topk_w.float().contiguous().data_ptr(), out.data_ptr(), T,
                    k, H, stream_ptr())
