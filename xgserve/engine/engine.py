@@ -110,6 +110,8 @@ class LLMEngine:
         self.tp_rank = st.tp_rank
         self.is_driver = st.tp_rank == 0
         device = cfg.resolved_device()
+        from ..tuning import enable_gemm_table
+        self.gemm_table = enable_gemm_table(device)  # replay the shipped hipBLASLt / rocBLAS choices
         dtype = {"bfloat16": torch.bfloat16, "float32": torch.float32, "float16": torch.float16,
                  None: None}[cfg.dtype]
         t0 = time.time()
