@@ -440,32 +440,59 @@ std::vector<FinishedSeq> StepScheduler::update(const int32_t* tokens, const int3
 
 bool StepScheduler::lookahead(bool across_length_finish) {
   const StepPlan& p = plan_;
-  if (p.num_seqs == 0 || p.num_decodes != p.num_seqs || p.num_sample != p.num_seqs) return false;
+  if (p.num_seqs == 0 || p.num_sample == 0) return false;
+  if (!cfg_.lookahead_mixed && (p.num_decodes != p.num_seqs || p.num_sample != p.num_seqs)) return false;
   for (int i = 0; i < p.num_seqs; ++i) {
     const Sequence* s = plan_seqs_[i];
     if (s == nullptr) continue;
-    if (!s->draft.empty()) return false;
-    // a row that reaches its length limit with this token frees its slot at commit;
-    // planning the next step synchronously lets a waiting request take it at once
-    // (admission latency = TTFT) instead of one step later
-    if (!across_length_finish && s->status == SeqStatus::Running &&
-        (s->num_generated() + 1 >= s->max_tokens ||
-         static_cast<int>(s->tokens.size()) + 1 >= cfg_.max_model_len))
+    if (!s->draft.empty() || p.is_embed[i]) return false;  // verify / embedding steps stay synchronous
+    // a sampled row that reaches its length limit with this token: either released
+    // early below, or (the default) this plan stays synchronous
+    const int i_sampled = p.do_sample[i];
+    if (i_sampled && !cfg_.early_release && !across_length_finish && s->status == SeqStatus::Running &&
+        (s->num_generated() + 1 >= s->max_tokens || static_cast<int>(s->tokens.size()) + 1 >= cfg_.max_model_len))
       return false;
   }
+  // Every sampled row (decodes and prompts completing this step) gets a placeholder
+  // token in sample order; prompt chunks that do not complete advance as update()
+  // would advance them. A sampled row that reaches its length limit with this token
+  // finishes at commit whatever the token is: unless across_length_finish, its slot
+  // and pages are released NOW (published to the prefix cache without the
+  // placeholder), so the plan made next can admit a waiting request into them
+  // (admission latency = TTFT) while this step is still on the GPU -- the GPU
+  // stream orders this step's reads of those pages before the next step's writes.
   Inflight r;
-  r.seqs.reserve(p.num_seqs);
-  r.pos.reserve(p.num_seqs);
-  for (int i = 0; i < p.num_seqs; ++i) {
+  r.seqs.reserve(p.num_sample);
+  r.pos.reserve(p.num_sample);
+  std::vector<uint8_t> sampled(p.num_seqs, 0);
+  for (int j = 0; j < p.num_sample; ++j) {
+    const int i = p.sample_seq_index[j];
+    sampled[i] = 1;
     Sequence* s = plan_seqs_[i];
     r.seqs.push_back(s);
     if (s == nullptr || s->status != SeqStatus::Running) {
       r.pos.push_back(-1);
       continue;
     }
+    const bool first_sample = s->num_generated() == 0;
     r.pos.push_back(static_cast<int>(s->tokens.size()));
     s->tokens.push_back(kPlaceholder);
     s->num_computed = static_cast<int>(s->tokens.size()) - 1;
+    if (first_sample && cfg_.enable_prefix_cache)  // publish the prompt pages early (as update())
+      cache_.insert(s->tokens.data(), s->num_computed, s->blocks.data(), static_cast<int>(s->blocks.size()));
+    const bool length_end = s->num_generated() >= s->max_tokens ||
+                            static_cast<int>(s->tokens.size()) >= cfg_.max_model_len;
+    if (length_end && !across_length_finish && cfg_.early_release) {
+      release(*s, /*publish=*/true);
+      running_.erase(std::remove(running_.begin(), running_.end(), s), running_.end());
+      s->status = SeqStatus::Finished;
+      s->released_early = true;
+    }
+  }
+  for (int i = 0; i < p.num_seqs; ++i) {
+    Sequence* s = plan_seqs_[i];
+    if (s == nullptr || sampled[i] || s->status != SeqStatus::Running) continue;
+    s->num_computed += p.q_lens[i];
   }
   inflight_.push_back(std::move(r));
   for (auto& q : plan_seqs_) q = nullptr;  // the plan is now owned by the record
@@ -481,11 +508,12 @@ std::vector<FinishedSeq> StepScheduler::commit(const int32_t* tokens, int num_sa
   for (int i = 0; i < num_sample; ++i) {
     Sequence* s = r.seqs[i];
     const int pos = r.pos[i];
-    if (s == nullptr || pos < 0 || s->status == SeqStatus::Finished) continue;
+    if (s == nullptr || pos < 0 || (s->status == SeqStatus::Finished && !s->released_early)) continue;
     if (pos != static_cast<int>(s->tokens.size()) - 1 || s->tokens[pos] != kPlaceholder)
       throw std::logic_error("commit: placeholder bookkeeping out of order");
     s->tokens[pos] = tokens[i];
     int reason = check_stop(*s);
+    if (s->released_early && !reason) reason = static_cast<int>(SeqFinish::Length);
     if (reason) {
       s->finish = static_cast<SeqFinish>(reason);
       finished.push_back(s);

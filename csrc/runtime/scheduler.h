@@ -59,6 +59,12 @@ struct SchedulerConfig {
   // (profiles/r2_prefill_m_sweep.jsonl). 0: off.
   int align_tokens = 0;
   int align_slack = 0;
+  // lookahead() over prompt steps (1) or pure-decode plans only (0)
+  int lookahead_mixed = 1;
+  // a length-finishing row: released at lookahead() so the next plan can admit into
+  // its slot (1), or the plan stays synchronous so a request that arrives when it
+  // finishes is admitted in the very next step (0: the TTFT-preserving default)
+  int early_release = 0;
   std::vector<int32_t> eos_ids;
 };
 
@@ -75,6 +81,7 @@ struct Sequence {
   int min_tokens = 0;
   bool ignore_eos = false;
   bool embed = false;  // prefill-only (embeddings endpoint)
+  bool released_early = false;  // length-finishing row released at lookahead(); reported at commit()
   std::vector<std::vector<int32_t>> stop_seqs;
   std::vector<int> blocks;
   std::vector<int32_t> draft;  // speculative tokens for the next step
@@ -125,16 +132,18 @@ class StepScheduler {
   // many belong to sampled sequence i (1 for plain decode). Returns finished.
   std::vector<FinishedSeq> update(const int32_t* tokens, const int32_t* counts, int num_sample);
 
-  // Asynchronous scheduling (one step of lookahead): for a plan of plain decode
-  // rows whose tokens are still being sampled on the GPU, append a placeholder
-  // token (kPlaceholder) to every sequence so schedule() can plan the NEXT step
+  // Asynchronous scheduling (one step of lookahead): for a plan whose tokens are
+  // still being sampled on the GPU, append a placeholder token (kPlaceholder) to
+  // every sampled sequence (decode rows and prompts completing this step; prompt
+  // chunks that do not complete just advance) so schedule() can plan the NEXT step
   // before this one finishes -- the runner substitutes the placeholders on the
   // device from this step's sampled-token buffer. commit() later resolves the
-  // oldest lookahead plan with its real tokens (one per row, plan order) and runs
-  // the stop checks; a sequence that stopped there may already be in the next
-  // plan, whose row for it is then ignored. Returns false (and does nothing) if
-  // the current plan is not a pure-decode plan, or (unless across_length_finish)
-  // if a row of it reaches its length limit (so its freed slot is refilled at once).
+  // oldest lookahead plan with its real tokens (one per sampled row, sample order)
+  // and runs the stop checks; a sequence that stopped there may already be in the
+  // next plan, whose row for it is then ignored. A row that reaches its length
+  // limit with this token is released at once (unless across_length_finish), so
+  // the next plan can admit into its slot; commit() reports it. Returns false (and
+  // does nothing) for verify / embedding plans.
   static constexpr int32_t kPlaceholder = -1;
   bool lookahead(bool across_length_finish = false);
   std::vector<FinishedSeq> commit(const int32_t* tokens, int num_sample);
@@ -173,7 +182,7 @@ class StepScheduler {
   void forget(Sequence* s);  // drop s from the plan / lookahead records
 
   struct Inflight {
-    std::vector<Sequence*> seqs;  // plan order (every row samples)
+    std::vector<Sequence*> seqs;  // the plan's sampled rows, in sample order
     std::vector<int> pos;         // index of the placeholder in seqs[i]->tokens, -1 = none
   };
   std::deque<Inflight> inflight_;

@@ -10,8 +10,9 @@ from xgserve import _runtime as R
 PH = -1
 
 
-def _sched(num_blocks=64, eos=(), max_seqs=8):
+def _sched(num_blocks=64, eos=(), max_seqs=8, early=False):
     c = R.SchedulerConfig()
+    c.early_release = 1 if early else 0
     c.block_size = 4
     c.num_blocks = num_blocks
     c.max_num_seqs = max_seqs
@@ -26,8 +27,8 @@ def _oracle(seq_id, step):  # the "model": a deterministic token per (sequence, 
     return 1000 + 7 * seq_id + step
 
 
-def _run(sync: bool, prompts, max_tokens, eos=(), abort_at=None, num_blocks=64, across=True):
-    s = _sched(eos=eos, num_blocks=num_blocks)
+def _run(sync: bool, prompts, max_tokens, eos=(), abort_at=None, num_blocks=64, across=True, early=False):
+    s = _sched(eos=eos, num_blocks=num_blocks, early=early)
     for i, (p, m) in enumerate(zip(prompts, max_tokens)):
         assert s.add(i + 1, p, m, 1, not eos, False, [], 0)
     out = {i + 1: [] for i in range(len(prompts))}
@@ -78,13 +79,14 @@ def _run(sync: bool, prompts, max_tokens, eos=(), abort_at=None, num_blocks=64, 
     return out, finished, s
 
 
+@pytest.mark.parametrize("early", [False, True])
 @pytest.mark.parametrize("across", [True, False])
 @pytest.mark.parametrize("eos", [(), (1000 + 7 * 2 + 9,)])
-def test_lookahead_matches_sync(eos, across):
+def test_lookahead_matches_sync(eos, across, early):
     prompts = [[1, 2, 3], [4, 5, 6, 7, 8], [9] * 11]
     mt = [5, 12, 3]
     a, fa, sa = _run(True, prompts, mt, eos)
-    b, fb, sb = _run(False, prompts, mt, eos, across=across)
+    b, fb, sb = _run(False, prompts, mt, eos, across=across, early=early)
     assert a == b
     assert fa == fb
     assert sa.num_used_blocks() == sb.num_used_blocks()
@@ -98,19 +100,61 @@ def test_lookahead_with_abort():
     assert sb.num_running() == 0 and sb.num_free_blocks() + sb.num_evictable_blocks() == 64 - 0
 
 
-def test_lookahead_refuses_mixed_plans_and_update_guard():
+def test_lookahead_over_prefill_plans_and_update_guard():
+    """A prompt step can be looked ahead too (its completing rows get placeholders,
+    partial chunks advance); update() is refused while a lookahead is in flight and
+    commit() resolves exactly one record."""
     s = _sched()
     assert s.add(1, [1, 2, 3], 4, 1, True, False, [], 0)
-    plan = s.schedule()  # prefill
-    assert not s.lookahead()
-    s.update(np.array([5], np.int32), np.ones(1, np.int32))
-    s.schedule()
+    s.schedule()  # prefill of the whole prompt: samples the first token
     assert s.lookahead()
+    nxt = s.schedule()
+    assert nxt["num_decodes"] == 1 and nxt["input_ids"][0] == PH  # substituted on the device
     with pytest.raises(Exception):
         s.update(np.array([6], np.int32), np.ones(1, np.int32))
     s.commit(np.array([6], np.int32))
     with pytest.raises(Exception):
         s.commit(np.array([7], np.int32))
+    assert s.lookahead()
+    s.commit(np.array([7], np.int32))
+
+
+def test_lookahead_over_partial_prompt_chunk():
+    """A chunked prompt (budget smaller than the prompt): the non-completing chunk
+    advances at lookahead, the next plan carries the following chunk."""
+    c = R.SchedulerConfig()
+    c.block_size = 4
+    c.num_blocks = 64
+    c.max_num_seqs = 4
+    c.max_num_batched_tokens = 8
+    c.max_model_len = 256
+    s = R.StepScheduler(c)
+    assert s.add(1, list(range(1, 21)), 3, 1, True, False, [], 0)  # 20-token prompt, 8-token budget
+    p0 = s.schedule()
+    assert p0["num_tokens"] == 8 and p0["num_sample"] == 0
+    assert not s.lookahead()  # nothing sampled: nothing to look ahead over
+    s.update(np.zeros(0, np.int32), np.zeros(0, np.int32))
+    p1 = s.schedule()
+    assert int(p1["ctx_lens"][0]) == 8 and p1["num_sample"] == 0
+
+
+def test_length_finish_released_at_lookahead_and_slot_reused():
+    """A row that reaches max_tokens with the token in flight is released at
+    lookahead(): the next plan admits the waiting request into its slot at once,
+    and commit() still reports the finished sequence (reason length)."""
+    s = _sched(max_seqs=1, early=True)
+    assert s.add(1, [1, 2, 3], 2, 1, True, False, [], 0)
+    assert s.add(2, [4, 5, 6, 7], 3, 1, True, False, [], 0)
+    s.schedule()  # prompt 1 (only one slot)
+    s.update(np.array([10], np.int32), np.ones(1, np.int32))  # token 1 of 2
+    p = s.schedule()
+    assert p["num_decodes"] == 1 and int(p["seq_ids"][0]) == 1
+    assert s.lookahead()  # row 1 ends with this token: released now
+    nxt = s.schedule()
+    assert [int(x) for x in nxt["seq_ids"]] == [2] and nxt["num_decodes"] == 0  # admitted at once
+    fins = s.commit(np.array([11], np.int32))
+    assert [(f[0], f[1], f[3]) for f in fins] == [(1, 2, 2)]  # id 1, reason Length, 2 tokens generated
+    assert s.num_running() == 1
 
 
 def test_lookahead_under_preemption():

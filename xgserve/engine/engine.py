@@ -140,6 +140,12 @@ class LLMEngine:
         sc.decode_prefill_cap = int(os.environ.get("XGS_DECODE_PREFILL_CAP", cfg.decode_prefill_cap))
         sc.align_tokens = int(os.environ.get("XGS_ALIGN_TOKENS", cfg.align_tokens))
         sc.align_slack = int(os.environ.get("XGS_ALIGN_SLACK", cfg.align_slack))
+        # asynchronous scheduling over prompt steps + early release of length-finishing
+        # rows (XGS_ASYNC_MIXED=0: only pure-decode graph steps are looked ahead)
+        sc.lookahead_mixed = int(os.environ.get("XGS_ASYNC_MIXED", "1"))
+        # release length-finishing rows at lookahead (throughput) instead of a synchronous
+        # step (TTFT of a request that arrives when they finish); XGS_EARLY_RELEASE=1
+        sc.early_release = int(os.environ.get("XGS_EARLY_RELEASE", "0"))
         sc.eos_ids = list(self.mcfg.eos_token_ids)
         self.sched = R.StepScheduler(sc)
         # decode graphs capture the TP collectives: RCCL (and the IPC all-reduce) can be
@@ -359,15 +365,16 @@ class LLMEngine:
 
     @staticmethod
     def _lookahead_src(prev: dict, nxt: dict) -> Optional[np.ndarray]:
-        """Per decode row of `nxt`: the row of `prev` (a pure-decode graph step, one
-        sampled token per row) whose token is this row's placeholder input, -1 if the
-        row has a real id. None if no row needs one."""
+        """Per decode row of `nxt`: the index, in `prev`'s sampled-token buffer (sample
+        order: a decode graph step's rows, or an eager step's sampled rows), of the
+        token that is this row's placeholder input; -1 if the row has a real id. None
+        if no row needs one."""
         nd = int(nxt["num_decodes"])
         ids = nxt["input_ids"][:nd]
         need = ids == -1  # StepScheduler::kPlaceholder
         if not need.any():
             return None
-        pids, cids = prev["seq_ids"], nxt["seq_ids"][:nd]
+        pids, cids = prev["seq_ids"][prev["sample_seq_index"]], nxt["seq_ids"][:nd]
         sorter = np.argsort(pids, kind="stable")
         k = np.clip(np.searchsorted(pids, cids, sorter=sorter), 0, len(pids) - 1)
         j = sorter[k]

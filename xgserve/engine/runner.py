@@ -26,6 +26,10 @@ from ..models.base import AttnMeta
 from ..ops.attention import DecodeWorkspace
 from ..parallel import comm
 
+# eager (prompt) steps leave their sampled tokens on the device for a looked-ahead
+# successor (XGS_ASYNC_MIXED=0: only decode graph steps do)
+ASYNC_MIXED = os.environ.get("XGS_ASYNC_MIXED", "1") != "0"
+
 log = logging.getLogger("xgserve.runner")
 
 
@@ -219,7 +223,9 @@ class ModelRunner:
         return self._execute_eager(plan, samp, need_hidden, src)
 
     def launched_as_graph(self, handle) -> bool:
-        """True if the step wrote its sampled tokens to g_out_tok (a graph step)."""
+        """True if the step left its sampled tokens in g_out_tok (every graph step,
+        and eager steps that qualify for tokens_to_device): the next step may be
+        planned and launched before this one completes."""
         return len(handle) > 4 and handle[4]
 
     @staticmethod
@@ -324,6 +330,8 @@ class ModelRunner:
         qsl = plan["query_start_loc"]
         parts = [plan["input_ids"], plan["positions"], plan["slot_mapping"],
                  plan["block_tables"], plan["seq_lens"], (qsl[Nd:] - Nd).astype(np.int32), li]
+        if src is not None:  # staged with the other inputs: no blocking copy ahead of the queued step
+            parts.append(np.ascontiguousarray(src, dtype=np.int32))
         sizes = [p.size for p in parts]
         total = sum(sizes)
         si = self.stage_idx
@@ -353,9 +361,8 @@ class ModelRunner:
         sl = dev[o[4]:o[5]]
         pre_qsl = dev[o[5]:o[6]]
         lidx = dev[o[6]:o[7]]
-        if src is not None:  # decode rows first: their ids from the previous graph step
-            d_src = torch.from_numpy(np.ascontiguousarray(src, dtype=np.int32)).to(self.device, non_blocking=False)
-            ops.subst_tokens(ids[:src.shape[0]], d_src, self.g_out_tok)
+        if src is not None:  # decode rows first: their ids from the previous step's sampled tokens
+            ops.subst_tokens(ids[:src.shape[0]], dev[o[7]:o[8]], self.g_out_tok)
         meta = AttnMeta(num_tokens=T, num_decodes=Nd, positions=pos, slot_mapping=slots,
                         dec_block_tables=bt[:Nd], dec_seq_lens=sl[:Nd],
                         num_splits=self.decode_splits(Nd) if self.is_cuda else 1, workspace=self.workspace,
@@ -384,5 +391,17 @@ class ModelRunner:
                 gen = torch.Generator().manual_seed(int(samp.seeds[0]) & 0x7FFFFFFF)
             tok, lp = ops.sample_tokens(logits, dev_f[0], dev_f[1], topk, seeds, step=0, generator=gen)
         if self.is_cuda:
-            return self._record_out(S, tok, lp, hid, False)
+            on_dev = self.tokens_to_device(S, tok, plan)
+            return self._record_out(S, tok, lp, hid, on_dev)
         return (S, hid, (tok.numpy().astype(np.int32), lp.numpy().astype(np.float32), hid), None)
+
+    def tokens_to_device(self, S: int, tok: torch.Tensor, plan: dict) -> bool:
+        """Eager step (TP = 1): also leave the sampled tokens in g_out_tok, in sample
+        order, so the engine can plan and launch the next step before this one ends
+        (its decode rows substitute their ids from there). Verify / embedding steps
+        and batches wider than the graph buffers stay synchronous."""
+        if (not ASYNC_MIXED or not self.graphs or S > self.g_B or comm.get_state().tp_size > 1
+                or bool(plan["is_embed"].any()) or int(plan["num_sample"]) != S):
+            return False
+        self.g_out_tok[:S].copy_(tok[:S])
+        return True
