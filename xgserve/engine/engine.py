@@ -37,6 +37,9 @@ from .runner import ModelRunner, SamplingRows
 from .tokenizer import IncrementalDetokenizer, load_tokenizer
 
 log = logging.getLogger("xgserve.engine")
+# split a step's emission: rows that cannot wait (finished, first tokens) before the
+# next step is planned, the rest in its overlap window (XGS_EMIT_SPLIT=0: all at once)
+EMIT_SPLIT = os.environ.get("XGS_EMIT_SPLIT", "1") != "0"
 
 _MASK63 = (1 << 63) - 1
 
@@ -506,10 +509,24 @@ class LLMEngine:
         # deferral only pays where the next step runs asynchronously (a GPU): on the CPU
         # the next launch computes the whole step, so deferring would add a step of
         # token delivery delay (Req 5.1) for nothing
-        if (self.cfg.overlap_outputs and self.device.type == "cuda" and self.spec is None and not first_tokens
-                and not fin_map):
+        overlap = self.cfg.overlap_outputs and self.device.type == "cuda" and self.spec is None
+        if overlap and not first_tokens and not fin_map:
             self._deferred = (plan, toks, lps, counts, fin_map)
             return []
+        if overlap and EMIT_SPLIT:
+            # only the rows whose output cannot wait -- finished requests (their slots are
+            # being refilled) and first tokens (TTFT) -- are emitted before the next
+            # step is planned; the other rows' outputs ride the next step's overlap window
+            now_ids = set(fin_map) if fin_map else set()
+            if first_tokens:
+                sidx = plan["sample_seq_index"]
+                pre = plan["is_prefill"][sidx].astype(bool)
+                now_ids.update(int(x) for x in plan["seq_ids"][sidx][pre])
+            with self._lock:
+                outs = self._emit(plan, toks, lps, counts, fin_map, only=now_ids)
+            self._deferred = (plan, toks, lps, counts, fin_map, now_ids)
+            self._tick("emit_blocking", t)
+            return outs
         with self._lock:
             outs = self._emit(plan, toks, lps, counts, fin_map)
         self._tick("emit_blocking", t)
@@ -528,6 +545,8 @@ class LLMEngine:
         if d is None:
             return []
         with self._lock:
+            if len(d) == 6:  # the rest of a split emission
+                return self._emit(*d[:5], skip=d[5])
             return self._emit(*d)
 
     def _accumulate_embeddings(self, plan, hidden):
@@ -568,8 +587,10 @@ class LLMEngine:
         self.stats_counters["generation_tokens"] += int(counts.sum())
         return {f[0]: f for f in finished}
 
-    def _emit(self, plan, toks, lps, counts, fin_map) -> List[RequestOutput]:
-        """Per-request host work of a step: detokenise, stop strings, RequestOutputs."""
+    def _emit(self, plan, toks, lps, counts, fin_map, only=None, skip=None) -> List[RequestOutput]:
+        """Per-request host work of a step: detokenise, stop strings, RequestOutputs.
+        only / skip: sets of sequence ids to restrict the sampled rows to / to leave out
+        (a step's outputs emitted in two parts)."""
         outs: List[RequestOutput] = []
         ns = int(plan["num_seqs"])
         seq_ids = plan["seq_ids"]
@@ -582,7 +603,7 @@ class LLMEngine:
             c = int(counts[j])
             sid = int(seq_ids[sidx[j]])
             req = self.by_seq.get(sid)
-            if req is None:
+            if req is None or (only is not None and sid not in only) or (skip is not None and sid in skip):
                 k += c
                 continue
             f = fin_map.get(sid)
@@ -616,7 +637,7 @@ class LLMEngine:
         # request's accumulator row in ONE device launch, one D2H copy
         done = []
         for sid, f in fin_map.items():
-            if f[1] != FINISH_EMBED:
+            if f[1] != FINISH_EMBED or (only is not None and sid not in only) or (skip is not None and sid in skip):
                 continue
             req = self.by_seq.get(sid)
             if req is None:
