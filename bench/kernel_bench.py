@@ -51,6 +51,34 @@ def bench_decode(res, B, L, splits_list, Hq=32, Hkv=8, D=128, bs=16):
                     "TB/s": round(nbytes / us / 1e6, 3)})
 
 
+def bench_decode_fq(res, B, L, S_qkv, stagger=0, Hq=32, Hkv=8, D=128, bs=16):
+    """Fused-QKV decode attention (the dense decode layer's form): QKV split-K
+    partials -> RoPE + KV append + attention, next to the plain kernel at the same
+    lengths. stagger > 0: sequence b has L - U[0, stagger) keys (a batch in flight)."""
+    from xgserve.ops.linear import PendingSum
+    dev = "cuda"
+    kc, vc, bt = paged(B, L, Hkv, D, bs, dev)
+    g = torch.Generator().manual_seed(0)
+    lens = (L - torch.randint(0, max(stagger, 1), (B,), generator=g)).int().to(dev)
+    pos = (lens - 1).int()
+    slots = (bt.gather(1, (pos // bs).long().view(B, 1)).view(B) * bs + pos % bs).int()
+    cs = torch.randn(L + 16, D, device=dev)
+    part = torch.randn(S_qkv, B, (Hq + 2 * Hkv) * D, device=dev)
+    pend = PendingSum(part, S_qkv)
+    q = torch.randn(B, Hq, D, device=dev).bfloat16()
+    out = torch.empty(B, Hq * D, device=dev, dtype=torch.bfloat16)
+    nbytes = int(lens.sum().item()) * Hkv * D * 2 * 2
+    sc = 1 / math.sqrt(D)
+    us = timeit(lambda: ops.decode_attention_fused(pend, pos, slots, cs, kc, vc, bt, lens, Hq, sc, 1, None,
+                                                   out=out))
+    res.append({"op": "decode_attention_fq", "B": B, "L": L, "stagger": stagger, "S_qkv": S_qkv, "us": round(us, 2),
+                "TB/s": round(nbytes / us / 1e6, 3)})
+    o3 = out.view(B, Hq, D)
+    us = timeit(lambda: ops.decode_attention(q, kc, vc, bt, lens, sc, 1, None, o3))
+    res.append({"op": "decode_attention", "B": B, "L": L, "stagger": stagger, "splits": 1, "us": round(us, 2),
+                "TB/s": round(nbytes / us / 1e6, 3)})
+
+
 def bench_prefill(res, T, Hq=32, Hkv=8, D=128, bs=16):
     dev = "cuda"
     kc, vc, bt = paged(1, T, Hkv, D, bs, dev)
@@ -97,6 +125,10 @@ def main():
         bench_decode(res, 64, 800, [1, 2, 4])
         bench_decode(res, 1, 1024, [1, 8, 16, 32])
         bench_decode(res, 256, 2048, [1, 2])
+        bench_decode_fq(res, 64, 768, 4, stagger=256)
+        bench_decode_fq(res, 64, 640, 4, stagger=128)
+        bench_decode_fq(res, 64, 800, 4)
+        bench_decode_fq(res, 64, 2048, 4)
     if a.what in ("all", "prefill"):
         for T in (512, 2048, 8192):
             bench_prefill(res, T)
