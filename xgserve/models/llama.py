@@ -33,8 +33,8 @@ import torch.nn.functional as F
 from .. import ops
 from ..parallel import comm
 from ..parallel.state import get_state
-from ..ops.linear import (MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace, RowStats,
-                          m64_linear,
+from ..ops.linear import (MODE_BF16, MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace,
+                          RowStats, m64_linear,
                           m64_norm_linear, m64_plan, m64_resid_linear, m64_xa_linear, m64_xa_ok, pick_split,
                           quantize_fp8, skinny_linear,
                           w8_linear, w8_plan)
@@ -68,6 +68,9 @@ EP_EXACT_MIN_PAIRS = int(os.environ.get("XGS_EP_EXACT_MIN_PAIRS", "256"))
 # moe_comm "auto": steps of at most this many tokens use the allreduce form when the
 # custom IPC all-reduce can take the [T, H] message
 EP_AR_MAX_TOKENS = int(os.environ.get("XGS_EP_AR_MAX_TOKENS", "64"))
+# LM head of decode-sized steps (<= 64 rows, TP=1) on gemm_m64g (bf16 epilogue)
+# instead of hipBLASLt (XGS_LMHEAD_M64=1; A/B in profiles/r2_lmhead_argmax.md)
+LMHEAD_M64 = os.environ.get("XGS_LMHEAD_M64", "0") == "1"
 
 
 @torch.no_grad()
@@ -527,6 +530,9 @@ class LlamaForCausalLM(nn.Module):
 
     def compute_logits(self, h: torch.Tensor) -> torch.Tensor:
         w = self.embed if self.lm_head is None else self.lm_head
+        if (LMHEAD_M64 and self.tp == 1 and h.is_cuda and h.dtype == torch.bfloat16 and h.shape[0] <= 64
+                and h.is_contiguous() and m64_plan(h.shape[0], w.shape[0], w.shape[1], MODE_BF16)):
+            return m64_linear(h, w, MODE_BF16)[:, :self.cfg.vocab_size]
         logits = F.linear(h, w)
         if self.tp > 1:
             logits = comm.tp_all_gather_lastdim(logits)

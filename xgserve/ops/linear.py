@@ -137,6 +137,8 @@ _M64_TUNED = {
     (3072, 4096, MODE_PARTIAL): {64: (2, 8, 4), 32: (1, 4, 2), 16: (2, 4, 6)},  # qkv8t2
     (1536, 4096, MODE_PARTIAL): {64: (1, 8, 2), 32: (1, 4, 1), 16: (1, 8, 4)},  # qkv8t4
     (768, 4096, MODE_PARTIAL): {64: (1, 8, 5), 32: (1, 8, 2), 16: (2, 8, 0)},  # qkv8t8
+    # Llama-3 LM head, bf16 logits (profiles/r2_lmhead_sweep.jsonl)
+    (128256, 4096, MODE_BF16): {64: (2, 1, 3), 16: (1, 1, 3)},
 }
 
 
