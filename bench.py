@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--weight-dtype", default=None, choices=["fp8"],
                     help="fp8: E4M3 weight copies for batch <= 16 decode (not the bf16 headline)")
     ap.add_argument("--no-prefix-cache", action="store_true")
+    ap.add_argument("--temperature", type=float, default=0.0,
+                    help="sampling temperature of every request (0 = greedy, the headline)")
+    ap.add_argument("--top-p", type=float, default=1.0)
+    ap.add_argument("--top-k", type=int, default=0)
     ap.add_argument("--tp-shard", type=int, default=1,
                     help="single-GPU simulation of ONE rank of a TP group of this degree: the rank's weight / "
                          "KV shards and kernels, collectives replaced by local reductions (not a TP measurement: "
@@ -169,7 +173,9 @@ def main():
         counter[0] += 1
         # random token prompts: no accidental prefix sharing across requests
         prompt = rng.integers(10, V - 10, size=a.prompt_len).tolist()
-        eng.add_request(rid, prompt, SamplingParams(max_tokens=max_tokens, temperature=0.0, ignore_eos=True))
+        eng.add_request(rid, prompt, SamplingParams(max_tokens=max_tokens, temperature=a.temperature,
+                                                   top_p=a.top_p, top_k=a.top_k, seed=counter[0],
+                                                   ignore_eos=True))
         arrival[rid] = time.perf_counter()
 
     # staggered output lengths (uniform on [1, 2*output_len], mean output_len) ->
@@ -254,7 +260,9 @@ def main():
             "config": {"model": a.model, "global_batch": a.concurrency * dp,
                        "seq_len": a.prompt_len + a.output_len, "prompt_len": a.prompt_len,
                        "output_len": a.output_len, "parallelism": par,
-                       "concurrency_per_replica": a.concurrency},
+                       "concurrency_per_replica": a.concurrency,
+                       "sampling": ("greedy" if a.temperature <= 0 else
+                                    f"temperature {a.temperature}, top_p {a.top_p}, top_k {a.top_k}")},
             "detail": {"preemptions": st_["preemptions"], "kv_blocks": st_["kv_blocks_total"],
                        "decode_steps_total": st_["decode_steps"], "steps_total": st_["steps"],
                        "gemm_table": bool(getattr(eng, "gemm_table", False)),

@@ -79,6 +79,23 @@ def bench_decode_fq(res, B, L, S_qkv, stagger=0, Hq=32, Hkv=8, D=128, bs=16):
                 "TB/s": round(nbytes / us / 1e6, 3)})
 
 
+def bench_sampling(res, B, V=128256):
+    """Greedy argmax and temperature / top-p / top-k sampling over bf16 logits."""
+    dev = "cuda"
+    logits = (torch.randn(B, V, device=dev) * 3).bfloat16()
+    nbytes = B * V * 2
+    us = timeit(lambda: ops.argmax_logprob(logits))
+    res.append({"op": "argmax", "B": B, "V": V, "us": round(us, 2), "TB/s": round(nbytes / us / 1e6, 3)})
+    temps = torch.full((B,), 0.8, device=dev)
+    seeds = torch.arange(B, dtype=torch.int64, device=dev)
+    for name, tp, tk in (("temp", None, None), ("top_p0.9", torch.full((B,), 0.9, device=dev), None),
+                         ("top_k50", None, torch.full((B,), 50, dtype=torch.int32, device=dev)),
+                         ("top_p0.9+k50", torch.full((B,), 0.9, device=dev),
+                          torch.full((B,), 50, dtype=torch.int32, device=dev))):
+        us = timeit(lambda: ops.sample_tokens(logits, temps, tp, tk, seeds, 7), iters=20, warm=3)
+        res.append({"op": "sample_" + name, "B": B, "V": V, "us": round(us, 2)})
+
+
 def bench_prefill(res, T, Hq=32, Hkv=8, D=128, bs=16):
     dev = "cuda"
     kc, vc, bt = paged(1, T, Hkv, D, bs, dev)
@@ -136,6 +153,9 @@ def main():
         for (N, K) in ((6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)):
             for M in (1, 64):
                 bench_gemm(res, M, N, K)
+    if a.what in ("all", "sampling"):
+        for B in (1, 64):
+            bench_sampling(res, B)
     if a.what in ("all", "small"):
         bench_small(res)
     for r in res:

@@ -46,7 +46,8 @@ int prefill_attention(const uint16_t*, int64_t, const uint16_t*, const uint16_t*
                       const int32_t*, uint16_t*, int64_t, int, int, int, int, int, int, float, hipStream_t, int);
 void argmax_logprob(const void*, int, int64_t, int, int, int32_t*, float*, hipStream_t);
 void sample_tokens(const void*, int, int64_t, int, int, const float*, const float*, const int32_t*, const uint64_t*,
-                   uint64_t, int32_t*, float*, hipStream_t);
+                   uint64_t, int32_t*, float*, void*, hipStream_t);
+size_t sample_ws_row_bytes();
 void segment_sum(const uint16_t*, int, const int32_t*, const int32_t*, float*, int, hipStream_t);
 void subst_tokens(int32_t*, const int32_t*, const int32_t*, int, hipStream_t);
 int gemm_w8(const uint16_t*, int, int, const uint8_t*, const float*, int, float*, uint16_t*, int, int, int,
@@ -185,11 +186,16 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("sample_tokens", [](uintptr_t logits, int is_f32, int64_t stride, int B, int V, uintptr_t temps,
                             uintptr_t top_ps, uintptr_t top_ks, uintptr_t seeds, uint64_t step, uintptr_t tok,
-                            uintptr_t lp, uintptr_t st) {
+                            uintptr_t lp, uintptr_t st, uintptr_t ws, int ws_rows) {
+    if (ws != 0 && ws_rows < B) throw std::invalid_argument("sample_tokens: workspace holds fewer rows than B");
     xgk::sample_tokens(P<const void>(logits), is_f32, stride, B, V, P<const float>(temps), P<const float>(top_ps),
-                       P<const int32_t>(top_ks), P<const uint64_t>(seeds), step, P<int32_t>(tok), P<float>(lp), S(st));
+                       P<const int32_t>(top_ks), P<const uint64_t>(seeds), step, P<int32_t>(tok), P<float>(lp),
+                       P<void>(ws), S(st));
     check(0, "sample_tokens");
-  });
+  }, py::arg("logits"), py::arg("is_f32"), py::arg("stride"), py::arg("B"), py::arg("V"), py::arg("temps"),
+     py::arg("top_ps"), py::arg("top_ks"), py::arg("seeds"), py::arg("step"), py::arg("tok"), py::arg("lp"),
+     py::arg("st"), py::arg("ws") = 0, py::arg("ws_rows") = 0);
+  m.def("sample_ws_row_bytes", []() { return static_cast<int64_t>(xgk::sample_ws_row_bytes()); });
   m.def("gemm_w8", [](uintptr_t x, int M, int K, uintptr_t w, uintptr_t scale, int N, uintptr_t part, uintptr_t out,
                       int splits, int mode, int cfg, uintptr_t st) {
     check(xgk::gemm_w8(P<const uint16_t>(x), M, K, P<const uint8_t>(w), P<const float>(scale), N, P<float>(part),

@@ -208,6 +208,80 @@ def test_sample_tokens_greedy_and_distribution():
     assert set(s3.cpu().tolist()) <= allowed
 
 
+def _sample_v1(logits, temps, top_ps, top_ks, seeds, step):
+    """The one-workgroup-per-row kernel (bisection thresholds), for cross-checks."""
+    from xgserve.ops._native import kernels, stream_ptr, ptr
+    B, V = logits.shape
+    tok = torch.empty(B, dtype=torch.int32, device=DEV)
+    lp = torch.empty(B, dtype=torch.float32, device=DEV)
+    kernels().sample_tokens(logits.data_ptr(), 1 if logits.dtype == torch.float32 else 0, logits.stride(0), B, V,
+                            temps.data_ptr(), ptr(top_ps), ptr(top_ks), ptr(seeds), step, tok.data_ptr(),
+                            lp.data_ptr(), stream_ptr(), 0, 0)
+    return tok, lp
+
+
+def _nucleus(prow, top_p):
+    sp, si = prow.sort(descending=True)
+    n = int((sp.cumsum(0) < top_p).sum()) + 1
+    return set(si[:n].tolist())
+
+
+@pytest.mark.parametrize("dtype,V", [(torch.bfloat16, 128256), (torch.float32, 50257), (torch.bfloat16, 1000)])
+def test_sample_split_matches_single_row_kernel(dtype, V):
+    """The split-row sampler draws exactly what the single-workgroup kernel draws
+    whenever the kept sets agree (same counter hash): always for temperature-only and
+    greedy rows; top-p / top-k rows agree up to threshold-resolution ties."""
+    assert ops.sampling.SAMPLE_SPLIT
+    B = 48
+    logits = rnd(B, V, scale=3.0, dtype=dtype)
+    temps = torch.tensor([0.0, 1.0, 0.7, 1.3] * (B // 4), device=DEV)
+    top_ps = torch.tensor([1.0, 1.0, 0.9, 0.5, 1.0, 0.95] * (B // 6), device=DEV)
+    top_ks = torch.tensor([0, 0, 0, 50, 1, 7, 0, 200] * (B // 8), dtype=torch.int32, device=DEV)
+    seeds = torch.arange(B, device=DEV, dtype=torch.int64) * 7919
+    t2, l2 = ops.sample_tokens(logits, temps, top_ps, top_ks, seeds, step=11)
+    t1, l1 = _sample_v1(logits, temps, top_ps, top_ks, seeds, 11)
+    assert (t2 == t1).float().mean().item() >= 0.95
+    plain = (top_ps >= 1.0) & (top_ks == 0)
+    assert torch.equal(t2[plain], t1[plain])
+    torch.testing.assert_close(l2, l1, atol=2e-3, rtol=1e-3)
+    greedy = temps <= 0
+    assert torch.equal(t2[greedy].long(), logits[greedy].float().argmax(-1))
+    # reproducible: same seed / step -> same draw (the histogram workspace is re-zeroed)
+    t3, _ = ops.sample_tokens(logits, temps, top_ps, top_ks, seeds, step=11)
+    assert torch.equal(t3, t2)
+    t4, _ = ops.sample_tokens(logits, temps, top_ps, top_ks, seeds, step=12)
+    assert not torch.equal(t4[~greedy], t2[~greedy])
+
+
+def test_sample_split_top_p_top_k_sets():
+    V, N = 4000, 4096
+    base = rnd(1, V, scale=2.0, dtype=torch.float32)
+    rows = base.repeat(N, 1)
+    seeds = torch.arange(N, device=DEV, dtype=torch.int64)
+    ones = torch.ones(N, device=DEV)
+    p = torch.softmax(base[0].cpu(), -1)
+    # top-p 0.6: every draw inside the nucleus; the nucleus' head tokens all drawn
+    s, _ = ops.sample_tokens(rows, ones, torch.full((N,), 0.6, device=DEV), None, seeds, step=5)
+    nuc = _nucleus(p, 0.6)
+    got = set(s.cpu().tolist())
+    assert got <= nuc
+    # frequencies follow the renormalised nucleus
+    keep = torch.tensor(sorted(nuc))
+    q = torch.zeros(V)
+    q[keep] = p[keep] / p[keep].sum()
+    freq = torch.bincount(s.long().cpu(), minlength=V).float() / N
+    top = q.argsort(descending=True)[:5]
+    assert (freq[top] - q[top]).abs().max() < 0.03
+    # top-k 20: exactly the 20 most likely tokens are reachable
+    s, _ = ops.sample_tokens(rows, ones, None, torch.full((N,), 20, dtype=torch.int32, device=DEV), seeds, step=5)
+    top20 = set(p.argsort(descending=True)[:20].tolist())
+    got = set(s.cpu().tolist())
+    assert got <= top20 and len(got) >= 15
+    # top-k 1 is greedy
+    s, _ = ops.sample_tokens(rows[:64], ones[:64], None, torch.ones(64, dtype=torch.int32, device=DEV), seeds[:64])
+    assert (s.long().cpu() == int(p.argmax())).all()
+
+
 def test_segment_sum():
     h = rnd(20, 4096)
     cu = torch.tensor([0, 3, 3, 20], dtype=torch.int32, device=DEV)

@@ -1,6 +1,7 @@
 """K9 sampling + K11 pooling helpers."""
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -74,10 +75,33 @@ def sample_tokens(logits: torch.Tensor, temps: torch.Tensor, top_ps: Optional[to
     B, V = logits.shape
     tok = torch.empty(B, dtype=torch.int32, device=logits.device)
     lp = torch.empty(B, dtype=torch.float32, device=logits.device)
+    ws = _sample_workspace(logits.device, B) if SAMPLE_SPLIT else None
     kernels().sample_tokens(logits.data_ptr(), 1 if logits.dtype == torch.float32 else 0, logits.stride(0), B, V,
                             temps.data_ptr(), ptr(top_ps), ptr(top_ks), ptr(seeds), int(step) & ((1 << 64) - 1),
-                            tok.data_ptr(), lp.data_ptr(), stream_ptr())
+                            tok.data_ptr(), lp.data_ptr(), stream_ptr(), ptr(ws),
+                            0 if ws is None else ws.shape[0])
     return tok, lp
+
+
+# Split-row sampler (csrc/kernels/sampling.hip "sample v2": several workgroups per row,
+# histogram thresholds instead of a 24-pass bisection); XGS_SAMPLE_SPLIT=0 selects the
+# one-workgroup-per-row kernel (A/B in profiles/r2_sampling.md).
+SAMPLE_SPLIT = os.environ.get("XGS_SAMPLE_SPLIT", "1") != "0"
+_SAMPLE_WS = {}
+
+
+def _sample_workspace(device, B: int) -> torch.Tensor:
+    """Per-device zeroed scratch of the split-row sampler, one row per batch row; the
+    kernels leave it zero after every call (ticket winners re-zero what they used), so
+    one allocation serves eager calls and captured graphs. Grown (never shrunk, never
+    freed) to the largest batch seen."""
+    key = (device.type, device.index)
+    wss = _SAMPLE_WS.setdefault(key, [])
+    if not wss or wss[-1].shape[0] < B:
+        row = kernels().sample_ws_row_bytes()
+        # earlier (smaller) workspaces stay alive: captured graphs may still use them
+        wss.append(torch.zeros(max(B, 256), row // 8, dtype=torch.int64, device=device))
+    return wss[-1]
 
 
 def segment_sum(hidden: torch.Tensor, cu: torch.Tensor, out: torch.Tensor,
