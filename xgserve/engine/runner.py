@@ -15,6 +15,7 @@ from __future__ import annotations
 import logging
 import math
 import os
+import time
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -29,6 +30,10 @@ from ..parallel import comm
 # eager (prompt) steps leave their sampled tokens on the device for a looked-ahead
 # successor (XGS_ASYNC_MIXED=0: only decode graph steps do)
 ASYNC_MIXED = os.environ.get("XGS_ASYNC_MIXED", "1") != "0"
+# host wait for a step's results: poll the event (default; XGS_SPIN_WAIT=0: a
+# blocking synchronize) for at most XGS_SPIN_MAX_MS before blocking (profiles/r2_spin_wait.md)
+SPIN_WAIT = os.environ.get("XGS_SPIN_WAIT", "1") != "0"
+SPIN_MAX_S = float(os.environ.get("XGS_SPIN_MAX_MS", "50")) / 1000.0
 
 log = logging.getLogger("xgserve.runner")
 
@@ -253,6 +258,20 @@ class ModelRunner:
         ev.record()
         return (n, hidden, None, (i, ev), graph)
 
+    @staticmethod
+    def _wait_event(ev):
+        """Block until `ev` completed. SPIN_WAIT: poll hipEventQuery instead of a
+        blocking synchronize (whose sleeping wake-up costs ~0.1 ms per step on the host
+        critical path), falling back to the blocking wait after SPIN_MAX_S."""
+        if not SPIN_WAIT:
+            ev.synchronize()
+            return
+        t_end = time.perf_counter() + SPIN_MAX_S
+        while not ev.query():
+            if time.perf_counter() > t_end:
+                ev.synchronize()
+                return
+
     def wait(self, handle):
         n, hidden, ready, out = handle[:4]
         if ready is not None:
@@ -260,13 +279,13 @@ class ModelRunner:
         if out is None:
             ev = handle[5] if len(handle) > 5 else None
             if ev is not None:
-                ev.synchronize()  # this step only (TP follower with a successor queued)
+                self._wait_event(ev)  # this step only (TP follower with a successor queued)
             else:
                 torch.cuda.current_stream().synchronize()
             self._check_comm()
             return None, None, hidden
         i, ev = out
-        ev.synchronize()  # this step only: a step queued behind it keeps running
+        self._wait_event(ev)  # this step only: a step queued behind it keeps running
         self._check_comm()
         return self.h_toks[i][:n].numpy().copy(), self.h_lps[i][:n].numpy().copy(), hidden
 
