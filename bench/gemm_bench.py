@@ -156,14 +156,15 @@ def m64g_sweep(a):
     """Every valid gemm_m64g configuration per shape (cold weights); prints the
     checked-correct ones, fastest first."""
     k = kernels()
-    waves = {c: (2 if c >= 4 else 4) for c in range(7)}
-    kcs = {c: (64 if c in (2, 3, 4, 5) else 128) for c in range(7)}
+    waves = {c: v[0] for c, v in L.M64G_CFGS.items()}
+    kcs = {c: v[1] for c, v in L.M64G_CFGS.items()}
     for name in a.shapes:
         N, K = SHAPES[name]
         nbytes = N * K * 2
         copies = max(2, min(8, (1 << 30) // nbytes + 1))
         ws = [(torch.randn(N, K, device="cuda") * 0.02).bfloat16() for _ in range(copies)]
         mode = L.MODE_SILU if name.startswith("gate_up") and not name.endswith("_p") else (L.MODE_BF16 if name == "lm_head" else L.MODE_PARTIAL)
+        cnt = L.tile_counters(torch.device("cuda"), N)
         for M in a.M:
             x = torch.randn(M, K, device="cuda").bfloat16()
             if mode == L.MODE_SILU:
@@ -172,9 +173,9 @@ def m64g_sweep(a):
             else:
                 want = x.float() @ ws[0].float().t()
             rows = []
-            for cfg in range(7):
+            for cfg in L.M64G_CFGS:
                 for nw in ((2,) if mode == L.MODE_SILU else (1, 2)):
-                    for S in ((1,) if mode != L.MODE_PARTIAL else (1, 2, 4, 8)):
+                    for S in ((1, 2, 4) if mode == L.MODE_SILU else (1,) if mode != L.MODE_PARTIAL else (1, 2, 4, 8)):
                         cols = 16 * nw * waves[cfg]
                         if N % cols or K % (S * kcs[cfg]):
                             continue
@@ -183,6 +184,11 @@ def m64g_sweep(a):
                                           device="cuda")
 
                         def fn(w, nw=nw, S=S, cfg=cfg, part=part, out=out):
+                            if mode == L.MODE_SILU and S > 1:
+                                k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), out.data_ptr(),
+                                               S, mode, nw, cfg, 0, 0, 0, 0.0, 0, 0, cnt.data_ptr(),
+                                               torch.cuda.current_stream().cuda_stream, 0, 0, 0, 0)
+                                return
                             k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N,
                                         part.data_ptr() if mode == L.MODE_PARTIAL else 0,
                                         out.data_ptr() if mode != L.MODE_PARTIAL else 0, S, mode, nw, cfg,

@@ -215,6 +215,38 @@ __device__ __forceinline__ void m64g_resid_tail(const float* __restrict__ part, 
   m64g_resid_reduce<COLS, NTHR>(part, S, M, N, blockIdx.x, epi);
 }
 
+// Split-K GG_SILU tail: every workgroup has stored its fp32 partial of the tile
+// (write-through); the tile's last arriver sums the S slabs and applies the SiLU
+// gate (gate / up rows interleaved in blocks of 16) into out [M, N / 2]. Lets the
+// wide (8-wave, 256-column) tile run at M = 64: half the x bytes per weight byte
+// of the 128-column tile, which is what bounds the per-CU LDS-DMA ingest there.
+template <int COLS, int NTHR>
+__device__ __forceinline__ void m64g_silu_tail(const float* __restrict__ part, int S, int M, int N,
+                                               uint16_t* __restrict__ out, int* counters, int* flag) {
+  if (!agent_ticket(counters + blockIdx.x, S - 1, flag)) return;
+  constexpr int O4 = COLS / 8;  // 4-wide output groups per row (COLS / 2 outputs)
+  const int F = N / 2, n0 = blockIdx.x * COLS;
+  const int64_t slab = static_cast<int64_t>(M) * N;
+  for (int idx = threadIdx.x; idx < M * O4; idx += NTHR) {
+    const int m = idx / O4, oc = 4 * (idx % O4);
+    const int64_t go = static_cast<int64_t>(m) * N + n0 + (oc >> 4) * 32 + (oc & 15);
+    float gs[4] = {0.f, 0.f, 0.f, 0.f}, us[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < S; ++s) {
+      const float4 gv = *reinterpret_cast<const float4*>(part + s * slab + go);
+      const float4 uv = *reinterpret_cast<const float4*>(part + s * slab + go + 16);
+      gs[0] += gv.x; gs[1] += gv.y; gs[2] += gv.z; gs[3] += gv.w;
+      us[0] += uv.x; us[1] += uv.y; us[2] += uv.z; us[3] += uv.w;
+    }
+    float o[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = gs[r] / (1.f + __expf(-gs[r])) * us[r];
+    uint2 v;
+    v.x = pack2(o[0], o[1]);
+    v.y = pack2(o[2], o[3]);
+    *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * F + n0 / 2 + oc) = v;
+  }
+}
+
 // Dense kernel, parametrised for the decode shapes (bench/gemm_bench.py picks):
 //   NW  16-column MFMA tiles per wave (2 = 32 columns; required by the SiLU epilogue)
 //   WV  waves per workgroup (4 or 2): fewer waves = more, smaller workgroups, so a
@@ -404,7 +436,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   }
 
   // acc[nt][mt][r] = out[m = 16 mt + li][n = nbase + 16 nt + 4 g + r]
-  if (mode == GG_PARTIAL || mode == GG_RESID) {
+  const bool silu_split = NW == 2 && mode == GG_SILU && S > 1;
+  if (mode == GG_PARTIAL || mode == GG_RESID || silu_split) {
     float* pp = part + static_cast<int64_t>(s) * M * N;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -413,12 +446,14 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
 #pragma unroll
       for (int nt = 0; nt < NW; ++nt) {
         float* dst = pp + static_cast<int64_t>(m) * N + nbase + 16 * nt + 4 * g;
-        if (mode == GG_RESID) st16_sc1(dst, acc[nt][mt]);
+        if (mode != GG_PARTIAL) st16_sc1(dst, acc[nt][mt]);
         else *reinterpret_cast<float4*>(dst) = make_float4(acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]);
       }
     }
     if (mode == GG_RESID)
       m64g_resid_tail<16 * NW * WV, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0));
+    else if (silu_split)
+      m64g_silu_tail<16 * NW * WV, 64 * WV>(part, S, M, N, out, epi.counters, reinterpret_cast<int*>(lds0));
   } else if (mode == GG_BF16) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -793,7 +828,8 @@ int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, i
 }
 
 // cfg: 0 = (4 waves, KC 128), 1 = (4, 128, nt), 2 = (4, 64), 3 = (4, 64, nt),
-//      4 = (2, 64), 5 = (2, 64, nt), 6 = (2, 128, nt)
+//      4 = (2, 64), 5 = (2, 64, nt), 6 = (2, 128, nt), 7 = (8, 64, nt; four x tiles only:
+//      a 16-row x tile is less than one DMA instruction per wave at 8 waves)
 template <int NW>
 static void launch_m64g(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N,
                         float* part, uint16_t* out, int mode, const M64Epi& epi) {
@@ -821,23 +857,25 @@ static void launch_m64g(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, i
     case 4: XGK_M64G(2, 64, false); break;
     case 5: XGK_M64G(2, 64, true); break;
     case 6: XGK_M64G(2, 128, true); break;
+    case 7: XGK_M64G4(8, 64, true); break;
     default: XGK_M64G(4, 128, false); break;
   }
 #undef XGK_M64G
 #undef XGK_M64G4
 }
 
-int m64g_cfg_waves(int cfg) { return cfg >= 4 ? 2 : 4; }
-int m64g_cfg_kc(int cfg) { return (cfg == 2 || cfg == 3 || cfg == 4 || cfg == 5) ? 64 : 128; }
+int m64g_cfg_waves(int cfg) { return cfg == 7 ? 8 : (cfg >= 4 ? 2 : 4); }
+int m64g_cfg_kc(int cfg) { return (cfg == 2 || cfg == 3 || cfg == 4 || cfg == 5 || cfg == 7) ? 64 : 128; }
 
 // Host-side shape / operand checks shared by both entry points (0 = valid).
 static int m64g_check(int M, int K, int N, const float* part, const uint16_t* out, int S, int mode, int nw, int cfg,
                       const M64Epi& epi) {
-  if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 6) return 1;
+  if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 7) return 1;
   if (mode < GG_BF16 || mode > GG_RESID) return 1;
   const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
   if (K % (S * kc) || N % cols) return 1;
-  if (mode == GG_SILU && (nw != 2 || S != 1)) return 1;
+  // split-K SiLU: fp32 slabs + one zeroed arrival ticket per column tile (m64g_silu_tail)
+  if (mode == GG_SILU && (nw != 2 || (S > 1 && (part == nullptr || epi.counters == nullptr)))) return 1;
   if (mode == GG_BF16 && S != 1) return 1;
   if ((mode == GG_PARTIAL || mode == GG_RESID) && part == nullptr) return 1;
   if ((mode == GG_BF16 || mode == GG_SILU) && out == nullptr) return 1;
@@ -845,7 +883,7 @@ static int m64g_check(int M, int K, int N, const float* part, const uint16_t* ou
   if (epi.ss_in != nullptr && (epi.ss_n < 1 || epi.ss_n > 64 || epi.ss_stride < M)) return 1;
   if (epi.att_po != nullptr) {  // XA: one-x-tile kernel, whole heads of 128 per K slice, slice fits xbuf
     const int kws = K / S;
-    if (M > 16 || cfg == 2 || cfg == 3 || !m64g_mt1_enabled() || epi.att_lse == nullptr || epi.att_splits < 1 ||
+    if (M > 16 || cfg == 2 || cfg == 3 || cfg == 7 || !m64g_mt1_enabled() || epi.att_lse == nullptr || epi.att_splits < 1 ||
         kws % 128 || kws > 1024 || K != epi.att_hq * 128)
       return 1;
   }

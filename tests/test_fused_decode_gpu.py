@@ -50,6 +50,46 @@ def test_norm_linear_row_scale(M, n_parts):
     assert rel_err(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("M", [1, 17, 64])
+@pytest.mark.parametrize("S,cfg", [(1, 7), (2, 7), (4, 7), (2, 1), (2, 5)])
+@pytest.mark.parametrize("normed", [False, True])
+def test_split_silu_and_wide_tile(M, S, cfg, normed):
+    """Split-K SiLU-gate (fp32 slabs, per-tile tickets, last arriver reduces + gates)
+    and the 8-wave 256-column tile, against fp32; the tickets must be re-armed (zero)
+    after every launch, so a second launch on the same counters gives the same result."""
+    K, F2 = 4096, 2 * 4096
+    x = rnd(M, K)
+    g, u = rnd(F2 // 2, K, scale=0.02), rnd(F2 // 2, K, scale=0.02)
+    w = interleave_gate_up(g, u)
+    h = x.float()
+    st = None
+    if normed:
+        sq = h ** 2
+        st = RowStats(sq.view(M, 4, -1).sum(-1).t().contiguous(), 4, M)
+        h = h * torch.rsqrt(sq.sum(-1, keepdim=True) / K + 1e-5)
+    ref = F.silu(h @ g.float().t()) * (h @ u.float().t())
+    lin._M64_TUNED[(F2, K, MODE_SILU)] = {64: (2, S, cfg), 32: (2, S, cfg), 16: (2, S, cfg)}
+    try:
+        for _ in range(2):
+            if normed:
+                y = m64_norm_linear(x, w, MODE_SILU, st, 1e-5)
+            else:
+                y = lin.m64_linear(x, w, MODE_SILU)
+            assert rel_err(y, ref) < 1e-2
+    finally:
+        del lin._M64_TUNED[(F2, K, MODE_SILU)]
+    torch.cuda.synchronize()
+    assert int(lin.tile_counters(x.device, F2).abs().sum()) == 0
+
+
+@pytest.mark.parametrize("M", [1, 40, 64])
+@pytest.mark.parametrize("N,K,S", [(6144, 4096, 4), (4096, 14336, 8), (4096, 4096, 2)])
+def test_wide_tile_partials(M, N, K, S):
+    x, w = rnd(M, K), rnd(N, K, scale=0.02)
+    pend = lin.m64_linear(x, w, MODE_PARTIAL, split_k=S, nw=2, cfg=7)
+    assert rel_err(pend.part.sum(0), x.float() @ w.float().t()) < 2e-3
+
+
 @pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 14336)])
 @pytest.mark.parametrize("inlaunch", [True, False])

@@ -92,7 +92,7 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, split_k: Optional[int] = Non
 # gemm_m64g launch configurations (csrc/kernels/gemm_m64g.hip launch_m64g):
 # cfg -> (waves per workgroup, k chunk, non-temporal weight DMA)
 M64G_CFGS = {0: (4, 128, False), 1: (4, 128, True), 2: (4, 64, False), 3: (4, 64, True),
-             4: (2, 64, False), 5: (2, 64, True), 6: (2, 128, True)}
+             4: (2, 64, False), 5: (2, 64, True), 6: (2, 128, True), 7: (8, 64, True)}
 
 # Measured on MI355X with cold weights (bench/gemm_bench.py --m64g-sweep,
 # profiles/r1_m64g_sweep.jsonl; bucket 16 re-swept with the MT=1 kernel: r1_m64g_mt1_sweep.jsonl): (N, K, mode) -> {M bucket: (nw, split_k, cfg)}.
@@ -142,11 +142,24 @@ _M64_TUNED = {
 }
 
 
+def _apply_plan_overrides(spec: str) -> None:
+    """XGS_M64_PLANS="NxKxMODE@BUCKET=nw,S,cfg;..." replaces tuned plans (A/B sweeps)."""
+    for item in filter(None, (t.strip() for t in spec.split(";"))):
+        key, plan = item.split("=")
+        shape, bucket = key.split("@")
+        n, k, mode = (int(v) for v in shape.split("x"))
+        _M64_TUNED.setdefault((n, k, mode), {})[int(bucket)] = tuple(int(v) for v in plan.split(","))
+
+
+_apply_plan_overrides(__import__("os").environ.get("XGS_M64_PLANS", ""))
+
+
 def _m64_valid(N: int, K: int, mode: int, nw: int, S: int, cfg: int) -> bool:
     wv, kc, _ = M64G_CFGS[cfg]
     if N % (16 * nw * wv) or K % (S * kc):
         return False
-    return not (mode == MODE_SILU and (nw != 2 or S != 1)) and not (mode == MODE_BF16 and S != 1)
+    # split-K SiLU reduces its slabs in the GEMM's tail (m64g_silu_tail): NW = 2 pairs only
+    return not (mode == MODE_SILU and nw != 2) and not (mode == MODE_BF16 and S != 1)
 
 
 def m64_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL):
@@ -212,7 +225,11 @@ def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split
     ncol = N // 2 if mode == MODE_SILU else N
     if out is None:
         out = torch.empty(M, ncol, dtype=torch.bfloat16, device=x.device)
-    if var == 4:
+    if mode == MODE_SILU and S > 1:  # split-K SiLU: slabs + tile tickets, reduced in the GEMM tail
+        part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+        k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), out.data_ptr(), S, mode, nw, cfg,
+                       0, 0, 0, 0.0, 0, 0, tile_counters(x.device, N).data_ptr(), stream_ptr(), 0, 0, 0, 0)
+    elif var == 4:
         k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, cfg, stream_ptr())
     else:
         k.gemm_m64(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, var, stream_ptr())
@@ -287,6 +304,21 @@ def _xa(x):
     return x.data_ptr(), M, K, 0, 0, 0, 0
 
 
+_TILE_COUNTERS = {}
+
+
+def tile_counters(device, n: int) -> torch.Tensor:
+    """Zeroed int32 arrival tickets (one per column tile, >= n / 16 words) shared by the
+    split-K SiLU launches of a device: every ticket winner re-arms its word, so each
+    launch leaves them zero for the next one on the stream."""
+    key = str(device)
+    t = _TILE_COUNTERS.get(key)
+    need = max(1024, n // 16)
+    if t is None or t.numel() < need:
+        t = _TILE_COUNTERS[key] = torch.zeros(need, dtype=torch.int32, device=device)
+    return t
+
+
 def m64_norm_linear(x: torch.Tensor, w: torch.Tensor, mode: int, stats: RowStats, eps: float,
                     out: Optional[torch.Tensor] = None):
     """gemm_m64g on the raw residual stream x with its RMSNorm applied as a per-row
@@ -307,6 +339,11 @@ def m64_norm_linear(x: torch.Tensor, w: torch.Tensor, mode: int, stats: RowStats
         return PendingSum(part, S)
     if out is None:
         out = torch.empty(M, N // 2 if mode == MODE_SILU else N, dtype=torch.bfloat16, device=x.device)
+    if mode == MODE_SILU and S > 1:  # split-K SiLU: slabs + tile tickets, reduced in the GEMM tail
+        part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+        k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), out.data_ptr(), S, mode, nw, cfg, *st,
+                       0, 0, tile_counters(x.device, N).data_ptr(), stream_ptr(), 0, 0, 0, 0)
+        return out
     k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, cfg, *st, 0, 0, 0,
                    stream_ptr(), 0, 0, 0, 0)
     return out
