@@ -35,7 +35,7 @@
 
 namespace xgk {
 
-enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2, GG_RESID = 3 };
+enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2, GG_RESID = 3, GG_RESID_COOP = 4 };
 
 // Fused-decode epilogue operands (all null / 0 for a plain GEMM).
 //   ss_in / ss_n / ss_stride: RMSNorm statistics of the input rows as ss_n
@@ -50,6 +50,13 @@ enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2, GG_RESID = 3 };
 //           (the next GEMM's ss_in with ss_n = gridDim.x). counters: gridDim.x tile
 //           tickets, zero before the first launch; every ticket winner re-zeroes
 //           its word, so each launch leaves them zero.
+//   GG_RESID_COOP: the same result, reduced cooperatively: the S split workgroups of a
+//           column tile wait for each other (arrive / depart words counters[2 tile],
+//           counters[2 tile + 1]; the host enables it only when the whole grid is
+//           co-resident, one workgroup per CU) and each reduces M / S of the tile's rows
+//           -- no serial last-arriver pass over S x M x COLS fp32 and no separate
+//           add_partials_resid launch at M ~ 64. Bounded spin: a peer that never
+//           arrives costs ~1 s and a wrong tile, never a hang.
 struct M64Epi {
   const float* ss_in;
   int ss_n;
@@ -159,16 +166,18 @@ __device__ __forceinline__ bool agent_ticket(int* cnt, int last_value, int* flag
 // over them); every lane runs every butterfly.
 template <int COLS, int NTHR>
 __device__ __forceinline__ void m64g_resid_reduce(const float* __restrict__ part, int S, int M, int N, int tile,
-                                                  const M64Epi& epi) {
+                                                  const M64Epi& epi, int r0 = 0, int r1 = -1) {
   constexpr int C4 = COLS / 4;
   static_assert(64 % C4 == 0 && NTHR % C4 == 0, "row groups must not straddle waves");
   const int tid = threadIdx.x;
   const int n0 = tile * COLS;
   const int64_t slab = static_cast<int64_t>(M) * N;
-  for (int base = 0; base < M * C4; base += NTHR) {
+  if (r1 < 0) r1 = M;
+  const int nr = r1 - r0;
+  for (int base = 0; base < nr * C4; base += NTHR) {
     const int idx = base + tid;
-    const bool ok = idx < M * C4;
-    const int m = ok ? idx / C4 : 0, c = idx % C4;
+    const bool ok = idx < nr * C4;
+    const int m = r0 + (ok ? idx / C4 : 0), c = idx % C4;
     const int64_t off = static_cast<int64_t>(m) * N + n0 + 4 * c;
     float y[4] = {0.f, 0.f, 0.f, 0.f};
     for (int s0 = 0; s0 < S; s0 += 4) {
@@ -213,6 +222,37 @@ __device__ __forceinline__ void m64g_resid_tail(const float* __restrict__ part, 
                                                 const M64Epi& epi, int* flag) {
   if (S > 1 && !agent_ticket(epi.counters + blockIdx.x, S - 1, flag)) return;
   m64g_resid_reduce<COLS, NTHR>(part, S, M, N, blockIdx.x, epi);
+}
+
+// GG_RESID_COOP tail: the tile's S workgroups meet (arrive word), each reduces its
+// row share, and the last to depart re-arms both words for the next launch.
+template <int COLS, int NTHR>
+__device__ __forceinline__ void m64g_resid_coop_tail(const float* __restrict__ part, int S, int M, int N,
+                                                     const M64Epi& epi, int* flag) {
+  int* arrive = epi.counters + 2 * blockIdx.x;
+  int* depart = arrive + 1;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's write-through slab stores are done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t spins = 0;
+    while (__hip_atomic_load(arrive, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < S) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 24)) break;  // ~1 s: a peer was not co-resident -- give up rather than hang
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    *flag = 0;
+  }
+  __syncthreads();
+  const int rows = (M + S - 1) / S;
+  const int r0 = min(M, blockIdx.y * rows), r1 = min(M, r0 + rows);
+  if (r0 < r1) m64g_resid_reduce<COLS, NTHR>(part, S, M, N, blockIdx.x, epi, r0, r1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0 && __hip_atomic_fetch_add(depart, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1) {
+    __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(depart, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Split-K GG_SILU tail: every workgroup has stored its fp32 partial of the tile
@@ -437,7 +477,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
 
   // acc[nt][mt][r] = out[m = 16 mt + li][n = nbase + 16 nt + 4 g + r]
   const bool silu_split = NW == 2 && mode == GG_SILU && S > 1;
-  if (mode == GG_PARTIAL || mode == GG_RESID || silu_split) {
+  if (mode == GG_PARTIAL || mode == GG_RESID || mode == GG_RESID_COOP || silu_split) {
     float* pp = part + static_cast<int64_t>(s) * M * N;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -452,6 +492,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
     }
     if (mode == GG_RESID)
       m64g_resid_tail<16 * NW * WV, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0));
+    else if (mode == GG_RESID_COOP)
+      m64g_resid_coop_tail<16 * NW * WV, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0));
     else if (silu_split)
       m64g_silu_tail<16 * NW * WV, 64 * WV>(part, S, M, N, out, epi.counters, reinterpret_cast<int*>(lds0));
   } else if (mode == GG_BF16) {
@@ -871,15 +913,19 @@ int m64g_cfg_kc(int cfg) { return (cfg == 2 || cfg == 3 || cfg == 4 || cfg == 5 
 static int m64g_check(int M, int K, int N, const float* part, const uint16_t* out, int S, int mode, int nw, int cfg,
                       const M64Epi& epi) {
   if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 7) return 1;
-  if (mode < GG_BF16 || mode > GG_RESID) return 1;
+  if (mode < GG_BF16 || mode > GG_RESID_COOP) return 1;
+  // co-residency of every split of a tile: one workgroup per CU for the whole grid
+  if (mode == GG_RESID_COOP && (N / (16 * nw * m64g_cfg_waves(cfg))) * S > 256) return 1;
   const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
   if (K % (S * kc) || N % cols) return 1;
   // split-K SiLU: fp32 slabs + one zeroed arrival ticket per column tile (m64g_silu_tail)
   if (mode == GG_SILU && (nw != 2 || (S > 1 && (part == nullptr || epi.counters == nullptr)))) return 1;
   if (mode == GG_BF16 && S != 1) return 1;
-  if ((mode == GG_PARTIAL || mode == GG_RESID) && part == nullptr) return 1;
+  if ((mode == GG_PARTIAL || mode == GG_RESID || mode == GG_RESID_COOP) && part == nullptr) return 1;
   if ((mode == GG_BF16 || mode == GG_SILU) && out == nullptr) return 1;
-  if (mode == GG_RESID && (epi.resid == nullptr || epi.ss_out == nullptr || epi.counters == nullptr)) return 1;
+  if ((mode == GG_RESID || mode == GG_RESID_COOP) &&
+      (epi.resid == nullptr || epi.ss_out == nullptr || epi.counters == nullptr))
+    return 1;
   if (epi.ss_in != nullptr && (epi.ss_n < 1 || epi.ss_n > 64 || epi.ss_stride < M)) return 1;
   if (epi.att_po != nullptr) {  // XA: one-x-tile kernel, whole heads of 128 per K slice, slice fits xbuf
     const int kws = K / S;
@@ -900,7 +946,7 @@ static void m64g_launch(const uint16_t* x, int M, int K, const uint16_t* w, int 
 int gemm_m64g(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
               int nw, int cfg, hipStream_t st) {
   const M64Epi epi{nullptr, 0, 0, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
-  if (mode == GG_RESID || m64g_check(M, K, N, part, out, S, mode, nw, cfg, epi)) return 1;
+  if (mode == GG_RESID || mode == GG_RESID_COOP || m64g_check(M, K, N, part, out, S, mode, nw, cfg, epi)) return 1;
   m64g_launch(x, M, K, w, N, part, out, S, mode, nw, cfg, epi, st);
   return 0;
 }

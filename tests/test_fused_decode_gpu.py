@@ -92,9 +92,12 @@ def test_wide_tile_partials(M, N, K, S):
 
 @pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 14336)])
-@pytest.mark.parametrize("inlaunch", [True, False])
+@pytest.mark.parametrize("inlaunch", [True, False, "coop"])
 def test_resid_linear(M, N, K, inlaunch, monkeypatch):
-    monkeypatch.setattr(lin, "RESID_INLAUNCH_MAX_BYTES", (1 << 30) if inlaunch else 0)
+    """inlaunch True: last-arriver ticket reduce; "coop": the tile's split workgroups
+    meet and reduce M / S rows each (GG_RESID_COOP); False: separate add_partials_resid."""
+    monkeypatch.setattr(lin, "RESID_INLAUNCH_MAX_BYTES", (1 << 30) if inlaunch is True else 0)
+    monkeypatch.setattr(lin, "RESID_COOP", inlaunch == "coop")
     x, w, r0 = rnd(M, K), rnd(N, K, scale=0.02), rnd(M, N)
     ws = ResidWorkspace(4, 64, N, DEV)
     ref = (r0.float() + x.float() @ w.float().t()).bfloat16().float()
@@ -104,8 +107,8 @@ def test_resid_linear(M, N, K, inlaunch, monkeypatch):
         st = m64_resid_linear(x, w, r, ws, 1, 1e-5)
         torch.testing.assert_close(r.float(), ref, atol=3e-2, rtol=2e-2)
         ss = st.ss.reshape(-1)[: st.n * st.stride].view(st.n, st.stride)[:, :M].sum(0)
-        if inlaunch:  # one partial sum per column tile
-            nw, _, cfg = lin.m64_plan(M, N, K, MODE_PARTIAL)
+        nw, S, cfg = lin.m64_plan(M, N, K, MODE_PARTIAL)
+        if inlaunch is True or (inlaunch == "coop" and S > 1):  # one partial sum per column tile
             assert st.n == N // (16 * nw * lin.M64G_CFGS[cfg][0])
         else:
             assert st.n == N // 1024

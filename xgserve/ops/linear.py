@@ -239,6 +239,14 @@ def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split
 
 # ---------------------------------------------------------------------------- fused decode layer
 MODE_RESID = 3
+MODE_RESID_COOP = 4
+# XGS_RESID_COOP=1: slabs above RESID_INLAUNCH_MAX_BYTES are reduced inside the GEMM
+# launch cooperatively (every split workgroup of a column tile reduces M / S rows
+# after the tile's splits meet; needs the whole grid co-resident, <= 256 workgroups)
+# instead of by the separate add_partials_resid launch. Measured slower (8B 64
+# concurrent 6.34-6.40 vs 5.88-5.92 ms/step: each tile waits for its slowest split
+# with its CUs held; profiles/r2_resid_coop.md), so off by default.
+RESID_COOP = __import__("os").environ.get("XGS_RESID_COOP", "0") == "1"
 # GG_RESID (residual add + next-norm statistics inside the GEMM launch) reduces a
 # column tile in-launch while its split-K slab (S x M x columns fp32) is at most
 # this many bytes -- the tile's last arriver reads it serially (~1 us per 16 KB,
@@ -268,8 +276,9 @@ class ResidWorkspace:
         self.max_m = max_m
         rows = max(self.MAX_TILES * self.IN_LAUNCH_MAX_M, max(1, H // 1024) * max_m)
         self.ss = torch.zeros(n_sites, rows, dtype=torch.float32, device=device)
-        # arrival tickets: zero here, and every ticket winner re-arms its word
-        self.counters = torch.zeros(n_sites, self.MAX_TILES, dtype=torch.int32, device=device)
+        # arrival tickets (GG_RESID: one word per tile; GG_RESID_COOP: arrive / depart
+        # pairs): zero here, and every launch re-arms the words it used
+        self.counters = torch.zeros(n_sites, 2 * self.MAX_TILES, dtype=torch.int32, device=device)
 
 
 # Attention split-combine folded into the O projection (gemm_m64g XA prologue) for
@@ -373,6 +382,11 @@ def m64_resid_linear(x, w: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace
                        float(eps), resid.data_ptr(), ss.data_ptr(), ws.counters[site].data_ptr(), stream_ptr(),
                        apo, alse, asp, ahq)
         return RowStats(ss, ntiles, M)  # one partial sum per column tile
+    if RESID_COOP and S > 1 and ntiles * S <= 256 and ntiles <= ws.MAX_TILES and M <= ws.IN_LAUNCH_MAX_M:
+        k.gemm_m64g_ex(xp, M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_RESID_COOP, nw, cfg, 0, 0, 0,
+                       float(eps), resid.data_ptr(), ss.data_ptr(), ws.counters[site].data_ptr(), stream_ptr(),
+                       apo, alse, asp, ahq)
+        return RowStats(ss, ntiles, M)
     k.gemm_m64g_ex(xp, M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg, 0, 0, 0, 0.0, 0, 0, 0,
                    stream_ptr(), apo, alse, asp, ahq)
     k.add_partials_resid(part.data_ptr(), S, M, resid.data_ptr(), ss.data_ptr(), N, stream_ptr())
