@@ -221,7 +221,12 @@ __device__ __forceinline__ float combine_splits(const float* __restrict__ lse, c
   return den > 0.f ? acc / den : 0.f;
 }
 
-template <int D, int G, bool FQ, int NWAVES = 4>
+// KL (K through LDS): the K tile is fetched like V -- each wave instruction moves 4
+// full 256-B key rows (coalesced) instead of 16 rows x 64 B in the MFMA A-fragment
+// shape -- and staged into a wave-private, XOR-swizzled LDS tile whose ds_read_b128
+// fragment reads are conflict-free; the fragment-shaped global loads occupy the
+// texture-address path per byte moved, which caps the KV stream at 64 concurrent.
+template <int D, int G, bool FQ, int NWAVES = 4, bool KL = false>
 __global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ seq_lens,
@@ -245,6 +250,7 @@ __global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
   const int t_end = min(ntiles, t_begin + tps);
 
   __shared__ __attribute__((aligned(16))) uint16_t v_lds[C::WAVES][16 * D];
+  __shared__ __attribute__((aligned(16))) uint16_t k_lds[KL ? C::WAVES : 1][KL ? 16 * D : 8];
   __shared__ float m_lds[C::WAVES][16], l_lds[C::WAVES][16];
   __shared__ float o_lds[C::WAVES][G][D];
   __shared__ __attribute__((aligned(16))) uint16_t q_lds[FQ ? G * D : 8];
@@ -259,9 +265,18 @@ __global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
     const int key0 = t * 16;
     const int page = bt[key0 / bs];
     const int64_t base = (static_cast<int64_t>(page) * Hkv + kvh) * head_stride + static_cast<int64_t>(key0 % bs) * D;
-    const uint16_t* kp = kc + base + li * D + 8 * g;
+    if constexpr (KL) {
+      static_assert(C::KK == C::VLD, "K and V tiles split into the same chunks per lane");
 #pragma unroll
-    for (int kk = 0; kk < C::KK; ++kk) kf[kk] = ld16(kp + kk * 32);
+      for (int i = 0; i < C::KK; ++i) {
+        const int c = lane + 64 * i;  // chunk id in the 16 x NCH tile (4 full rows per instruction)
+        kf[i] = ld16(kc + base + (c / C::NCH) * D + (c % C::NCH) * 8);
+      }
+    } else {
+      const uint16_t* kp = kc + base + li * D + 8 * g;
+#pragma unroll
+      for (int kk = 0; kk < C::KK; ++kk) kf[kk] = ld16(kp + kk * 32);
+    }
 #pragma unroll
     for (int i = 0; i < C::VLD; ++i) {
       const int c = lane + 64 * i;  // chunk id in the 16 x NCH tile
@@ -301,11 +316,21 @@ __global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
   for (int mt = 0; mt < C::MT; ++mt) o[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   uint16_t* my_v = v_lds[wid];
+  uint16_t* my_k = k_lds[KL ? wid : 0];
 
   auto process = [&](int t, uint4 (&kf)[C::KK], uint4 (&vr)[C::VLD]) {
     uint4 kcur[C::KK];
+    if constexpr (KL) {  // stage K rows, chunk ch of row r at granule ch ^ r (r < 16)
 #pragma unroll
-    for (int kk = 0; kk < C::KK; ++kk) kcur[kk] = kf[kk];
+      for (int i = 0; i < C::KK; ++i) {
+        const int c = lane + 64 * i;
+        const int row = c / C::NCH, ch = c % C::NCH;
+        st16(my_k + row * D + (ch ^ row) * 8, kf[i]);
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < C::KK; ++kk) kcur[kk] = kf[kk];
+    }
     // stage this tile's V rows into the wave-private LDS image (swizzled)
 #pragma unroll
     for (int i = 0; i < C::VLD; ++i) {
@@ -314,6 +339,11 @@ __global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
       st16(my_v + row * D + dswz<D>(row, ch) * 8, vr[i]);
     }
     if (t + 2 * C::WAVES < t_end) load_tile(t + 2 * C::WAVES, kf, vr);  // refill this register tile
+    if constexpr (KL) {  // A fragment: key li, dims 32 kk + 8 g .. +8 (same wave wrote it: LDS order)
+#pragma unroll
+      for (int kk = 0; kk < C::KK; ++kk)
+        kcur[kk] = *reinterpret_cast<const uint4*>(my_k + li * D + ((4 * kk + g) ^ li) * 8);
+    }
 
     f32x4_t s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -469,18 +499,36 @@ static int decode_min_split_tiles() {
   return v;
 }
 
+// XGS_DECODE_K_LDS=0: K fragments loaded straight from HBM in the MFMA shape (A/B).
+static bool decode_k_lds() {
+  static const bool on = [] {
+    const char* e = std::getenv("XGS_DECODE_K_LDS");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 template <int D, int G, bool FQ>
 static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, const uint16_t* vc,
                           const int32_t* bt, int bts, const int32_t* sl, float* po, float* pl, uint16_t* out,
                           int64_t os, int B, int Hq, int Hkv, int bs, float scale, int S, int* counters,
                           const QkvFuse& fq, hipStream_t st) {
   const int gz = S + (FQ ? fq.pf_slices : 0);
-  if (FQ && decode_attn_waves() == 8)
+  const bool klds = D == 128 && decode_k_lds() && !(FQ && decode_attn_waves() == 8);
+  if constexpr (D == 128) {
+    if (klds)
+      hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, 4, true>), dim3(Hkv, B, gz), dim3(256), 0, st, q, qs, kc, vc,
+                         bt, bts, sl, po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq,
+                         S > 1 ? decode_min_split_tiles() : 1);
+  }
+  if (klds) {
+  } else if (FQ && decode_attn_waves() == 8) {
     hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, 8>), dim3(Hkv, B, gz), dim3(512), 0, st, q, qs, kc, vc, bt, bts,
                        sl, po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq, S > 1 ? decode_min_split_tiles() : 1);
-  else
-  hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ>), dim3(Hkv, B, gz), dim3(256), 0, st, q, qs, kc, vc, bt, bts, sl,
-                     po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq, S > 1 ? decode_min_split_tiles() : 1);
+  } else {
+    hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ>), dim3(Hkv, B, gz), dim3(256), 0, st, q, qs, kc, vc, bt, bts, sl,
+                       po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq, S > 1 ? decode_min_split_tiles() : 1);
+  }
   if (S > 1 && counters == nullptr && out != nullptr)  // out == nullptr: merged by the consumer (gemm_m64g XA)
     hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
 }
