@@ -82,6 +82,24 @@ def test_split_silu_and_wide_tile(M, S, cfg, normed):
     assert int(lin.tile_counters(x.device, F2).abs().sum()) == 0
 
 
+@pytest.mark.parametrize("M", [65, 575, 1536])
+def test_splitk_prefill_down_into_add_rmsnorm(M):
+    """Prefill-sized down projection as one K-split batched GEMM with fp32 partials,
+    reduced by the consumer (add + RMSNorm prologue), against fp32."""
+    N, K = 4096, 14336
+    x, w, r0 = rnd(M, K, scale=0.5), rnd(N, K, scale=0.02), rnd(M, N)
+    nw = (torch.rand(N, device=DEV) + 0.5).bfloat16()
+    assert lin.splitk_prefill_ok(x, w)
+    pend = lin.splitk_linear(x, w, 2)
+    d = x.float() @ w.float().t()
+    assert rel_err(pend.part.sum(0), d) < 1e-5
+    h, r = ops.fused_add_rmsnorm(pend, r0.clone(), nw, 1e-5)
+    rr = r0.float() + d
+    assert rel_err(r, rr) < 1e-2
+    ref = rr.bfloat16().float() * torch.rsqrt((rr.bfloat16().float() ** 2).mean(-1, keepdim=True) + 1e-5) * nw.float()
+    assert rel_err(h, ref) < 1e-2
+
+
 @pytest.mark.parametrize("M", [1, 40, 64])
 @pytest.mark.parametrize("N,K,S", [(6144, 4096, 4), (4096, 14336, 8), (4096, 4096, 2)])
 def test_wide_tile_partials(M, N, K, S):

@@ -36,7 +36,7 @@ from ..parallel.state import get_state
 from ..ops.linear import (MODE_BF16, MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace,
                           RowStats, m64_linear,
                           m64_norm_linear, m64_plan, m64_resid_linear, m64_xa_linear, m64_xa_ok, pick_split,
-                          quantize_fp8, skinny_linear,
+                          quantize_fp8, skinny_linear, splitk_linear, splitk_prefill_ok,
                           w8_linear, w8_plan)
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
 from .config import ModelConfig
@@ -232,6 +232,8 @@ class LlamaLayer(nn.Module):
             return self._moe_allreduce(h)
         gu = F.linear(h, self.gate_up)
         a = ops.silu_and_mul(gu, interleave16=True)
+        if self.tp == 1 and splitk_prefill_ok(a, self.down):
+            return splitk_linear(a, self.down, 2)  # partials reduced by the next add + norm
         return self._ar(F.linear(a, self.down))
 
     def _row_parallel_fast(self, a: torch.Tensor, w: torch.Tensor, split: int):

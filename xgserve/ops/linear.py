@@ -314,6 +314,30 @@ def _xa(x):
     return x.data_ptr(), M, K, 0, 0, 0, 0
 
 
+# Prefill-sized down projections (K = 3.5 N) have too few output tiles for the chip at
+# M ~ 512-1536 (N = 4096: 66-160 library tiles); a K-split strided-batched GEMM with
+# fp32 outputs doubles them and its partials are reduced for free by the consumer
+# (add_partials_rmsnorm). bench/splitk_prefill_bench.py, profiles/r2_splitk_prefill.md:
+# 8B down at M 575 87.8 -> 70.3 us (+3.3 us of fp32 slab traffic in the consumer).
+SPLITK_PREFILL_MAX_M = int(_os.environ.get("XGS_SPLITK_PREFILL_MAX_M", "1536"))
+
+
+def splitk_linear(x: torch.Tensor, w: torch.Tensor, S: int) -> PendingSum:
+    """x [M, K] . w[N, K]^T as S fp32 K-slice partials [S, M, N] from ONE strided
+    batched library GEMM (no copies: both operands are strided views)."""
+    M, K = x.shape
+    N = w.shape[0]
+    a = x.view(M, S, K // S).permute(1, 0, 2)
+    b = w.view(N, S, K // S).permute(1, 2, 0)
+    return PendingSum(torch.bmm(a, b, out_dtype=torch.float32), S)
+
+
+def splitk_prefill_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    M, K = x.shape
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()
+            and 64 < M <= SPLITK_PREFILL_MAX_M and K >= 3 * w.shape[0] and K % 512 == 0)
+
+
 _TILE_COUNTERS = {}
 
 
