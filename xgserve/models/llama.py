@@ -33,6 +33,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..parallel import comm
 from ..parallel.state import get_state
+from ..ops import linear as linear_mod
 from ..ops.linear import (MODE_BF16, MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace,
                           RowStats, m64_linear,
                           m64_norm_linear, m64_plan, m64_resid_linear, m64_xa_linear, m64_xa_ok, pick_split,
@@ -309,7 +310,10 @@ class LlamaLayer(nn.Module):
         a = self.attn(qkv, meta, kv, cos_sin)
         if self.tp > 1 and not self.moe and T >= TP_OVERLAP_MIN_TOKENS and TP_OVERLAP_CHUNKS > 1:
             return self._forward_tp_overlap(a, residual)
-        o = self._ar(F.linear(a, self.o))
+        if self.tp == 1 and linear_mod.SPLITK_O and splitk_prefill_ok(a, self.o, min_ratio=1):
+            o = splitk_linear(a, self.o, 2)  # partials reduced by the add + norm below
+        else:
+            o = self._ar(F.linear(a, self.o))
         h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
         return self.mlp(h), residual
 

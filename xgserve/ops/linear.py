@@ -332,10 +332,15 @@ def splitk_linear(x: torch.Tensor, w: torch.Tensor, S: int) -> PendingSum:
     return PendingSum(torch.bmm(a, b, out_dtype=torch.float32), S)
 
 
-def splitk_prefill_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+# XGS_SPLITK_O=1: the O projection of prefill-sized steps too (K = N). Measured within noise
+# at 64 concurrent (3 pairs: 11,304-11,472 vs 11,381-11,412 tok/s, profiles/r2_splitk_prefill.md)
+SPLITK_O = _os.environ.get("XGS_SPLITK_O", "0") == "1"
+
+
+def splitk_prefill_ok(x: torch.Tensor, w: torch.Tensor, min_ratio: int = 3) -> bool:
     M, K = x.shape
     return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous()
-            and 64 < M <= SPLITK_PREFILL_MAX_M and K >= 3 * w.shape[0] and K % 512 == 0)
+            and 64 < M <= SPLITK_PREFILL_MAX_M and K >= min_ratio * w.shape[0] and K % 512 == 0)
 
 
 _TILE_COUNTERS = {}
