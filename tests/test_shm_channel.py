@@ -37,7 +37,7 @@ def test_single_process_roundtrip():
     # nothing new: receive times out and returns None
     t = time.time()
     assert rd.receive(0, 0.05) is None
-    assert time.time() - t < 1.0
+    assert time.time() - t < 5.0  # a 50 ms timeout must not block (slack for a loaded host)
     # the producer cannot publish twice without the reader acknowledging
     assert ch.publish(b"one", 1.0)
     assert not ch.publish(b"two", 0.05)
