@@ -514,8 +514,9 @@ static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, con
                           int64_t os, int B, int Hq, int Hkv, int bs, float scale, int S, int* counters,
                           const QkvFuse& fq, hipStream_t st) {
   const int gz = S + (FQ ? fq.pf_slices : 0);
-  const bool klds = D == 128 && decode_k_lds() && !(FQ && decode_attn_waves() == 8);
-  if constexpr (D == 128) {
+  // G <= 4 only: at G = 8 (one kv head per TP-8 rank of the 70B) measured 0.5-6 % slower
+  const bool klds = D == 128 && G <= 4 && decode_k_lds() && !(FQ && decode_attn_waves() == 8);
+  if constexpr (D == 128 && G <= 4) {
     if (klds)
       hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, 4, true>), dim3(Hkv, B, gz), dim3(256), 0, st, q, qs, kc, vc,
                          bt, bts, sl, po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq,
