@@ -344,6 +344,7 @@ def splitk_prefill_ok(x: torch.Tensor, w: torch.Tensor, min_ratio: int = 3) -> b
 
 
 _TILE_COUNTERS = {}
+_TILE_COUNTERS_RETIRED = []
 
 
 def tile_counters(device, n: int) -> torch.Tensor:
@@ -352,8 +353,10 @@ def tile_counters(device, n: int) -> torch.Tensor:
     launch leaves them zero for the next one on the stream."""
     key = str(device)
     t = _TILE_COUNTERS.get(key)
-    need = max(1024, n // 16)
+    need = max(4096, n // 16)
     if t is None or t.numel() < need:
+        if t is not None:  # captured HIP graphs may hold the old words: keep them alive
+            _TILE_COUNTERS_RETIRED.append(t)
         t = _TILE_COUNTERS[key] = torch.zeros(need, dtype=torch.int32, device=device)
     return t
 
