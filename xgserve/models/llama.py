@@ -234,7 +234,7 @@ class LlamaLayer(nn.Module):
         gu = F.linear(h, self.gate_up)
         a = ops.silu_and_mul(gu, interleave16=True)
         if self.tp == 1 and splitk_prefill_ok(a, self.down):
-            return splitk_linear(a, self.down, 2)  # partials reduced by the next add + norm
+            return splitk_linear(a, self.down, linear_mod.SPLITK_PREFILL_S)  # reduced by the next add + norm
         return self._ar(F.linear(a, self.down))
 
     def _row_parallel_fast(self, a: torch.Tensor, w: torch.Tensor, split: int):

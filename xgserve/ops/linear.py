@@ -320,6 +320,7 @@ def _xa(x):
 # (add_partials_rmsnorm). bench/splitk_prefill_bench.py, profiles/r2_splitk_prefill.md:
 # 8B down at M 575 87.8 -> 70.3 us (+3.3 us of fp32 slab traffic in the consumer).
 SPLITK_PREFILL_MAX_M = int(_os.environ.get("XGS_SPLITK_PREFILL_MAX_M", "1536"))
+SPLITK_PREFILL_S = int(_os.environ.get("XGS_SPLITK_PREFILL_S", "4"))
 
 
 def splitk_linear(x: torch.Tensor, w: torch.Tensor, S: int) -> PendingSum:
