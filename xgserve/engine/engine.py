@@ -40,6 +40,11 @@ log = logging.getLogger("xgserve.engine")
 # split a step's emission: rows that cannot wait (finished, first tokens) before the
 # next step is planned, the rest in its overlap window (XGS_EMIT_SPLIT=0: all at once)
 EMIT_SPLIT = os.environ.get("XGS_EMIT_SPLIT", "1") != "0"
+# Outputs emitted in a step's overlap window go to `output_sink` (the serving
+# replica's writer) right away instead of riding the step's return value, which
+# comes only after the GPU step in flight finishes (a whole step of delivery delay,
+# Req 5.1). XGS_EARLY_OUTPUTS=0: return them with the step.
+EARLY_OUTPUTS = os.environ.get("XGS_EARLY_OUTPUTS", "1") != "0"
 
 _MASK63 = (1 << 63) - 1
 
@@ -181,6 +186,9 @@ class LLMEngine:
         self.slot_seed = np.zeros(ns, np.uint64)
         self.slot_ngen = np.zeros(ns, np.int64)  # tokens generated by the slot's owner (sampling counter)
         self._deferred = None  # (plan, toks, lps, counts, fin_map) awaiting detokenisation
+        # callable(List[RequestOutput]) taking overlap-window outputs immediately (a server
+        # replica sets it); None: every output is returned by step()
+        self.output_sink = None
         self._timing = None
         self._tprof = None  # torch.profiler state (XGS_TORCH_PROFILE)
         self._tprof_left = 0
@@ -431,7 +439,7 @@ class LLMEngine:
                     src = self._lookahead_src(plan, nplan)
                     self._inflight = (nplan, self._launch(nplan, nsamp, src=src))
                 t = self._tick("launch", t)
-        outs += self._flush_deferred()  # previous step's outputs, while the GPU runs
+        outs += self._emit_early(self._flush_deferred())  # previous step's outputs, while the GPU runs
         t = self._tick("emit_overlapped", t)
         toks, lps, hidden = self.runner.wait(handle)
         plan["_t_tokens"] = time.monotonic()
@@ -477,7 +485,7 @@ class LLMEngine:
         else:
             handle = self.runner.launch(plan, samp)
             t = self._tick("launch", t)
-            outs += self._flush_deferred()  # previous step's outputs, while this one runs
+            outs += self._emit_early(self._flush_deferred())  # previous step's outputs, while this one runs
             t = self._tick("emit_overlapped", t)
             toks, lps, hidden = self.runner.wait(handle)
             plan["_t_tokens"] = time.monotonic()
@@ -539,6 +547,13 @@ class LLMEngine:
 
     def step_timing(self) -> dict:
         return dict(self._timing or {})
+
+    def _emit_early(self, outs: List[RequestOutput]) -> List[RequestOutput]:
+        """Hand overlap-window outputs to the sink now (returns what is left for step())."""
+        if outs and EARLY_OUTPUTS and self.output_sink is not None:
+            self.output_sink(outs)
+            return []
+        return outs
 
     def _flush_deferred(self) -> List[RequestOutput]:
         d, self._deferred = self._deferred, None

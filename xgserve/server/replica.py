@@ -155,6 +155,9 @@ class EngineLoop:
         if timing:  # per-phase host time of the engine loop, reported with the heartbeat
             self.engine.enable_step_timing()
         loop_t = {"engine_step": 0.0, "emit": 0.0, "drain": 0.0, "idle": 0.0}
+        if hasattr(self.engine, "output_sink"):
+            # tokens emitted while a GPU step runs leave for the server at once (Req 5.1)
+            self.engine.output_sink = lambda o: self.emit("out", o)
         while not self._stop:
             outs: list = []
             ta = time.perf_counter()
