@@ -279,3 +279,26 @@ def test_mixed_step_tile_alignment():
                 d.setdefault(sid, []).append(t)
         return d
     assert streams(o_al) == streams(o_no)
+
+
+def test_overlap_outputs_go_to_the_sink_immediately(monkeypatch):
+    """A serving replica sets LLMEngine.output_sink: outputs detokenised in a step's
+    overlap window are handed over before the GPU wait instead of being returned
+    with step() (Req 5.1 delivery); without a sink (bench.py) they stay in step()'s
+    return value, and XGS_EARLY_OUTPUTS=0 restores that for a replica too."""
+    from types import SimpleNamespace
+
+    from xgserve.engine import engine as E
+    from xgserve.engine.request import RequestOutput
+
+    outs = [RequestOutput("a", [1], "x", False), RequestOutput("b", [2], "y", False)]
+    got = []
+    eng = SimpleNamespace(output_sink=got.extend)
+    monkeypatch.setattr(E, "EARLY_OUTPUTS", True)
+    assert E.LLMEngine._emit_early(eng, list(outs)) == [] and got == outs
+    assert E.LLMEngine._emit_early(eng, []) == []
+    eng.output_sink = None
+    assert E.LLMEngine._emit_early(eng, list(outs)) == outs
+    monkeypatch.setattr(E, "EARLY_OUTPUTS", False)
+    eng.output_sink = got.append
+    assert E.LLMEngine._emit_early(eng, list(outs)) == outs and len(got) == 2
