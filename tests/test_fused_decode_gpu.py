@@ -51,7 +51,7 @@ def test_norm_linear_row_scale(M, n_parts):
 
 
 @pytest.mark.parametrize("M", [1, 17, 64])
-@pytest.mark.parametrize("S,cfg", [(1, 7), (2, 7), (4, 7), (2, 1), (2, 5)])
+@pytest.mark.parametrize("S,cfg", [(1, 7), (2, 7), (4, 7), (2, 1), (2, 5), (2, 6), (4, 6), (4, 0), (4, 1), (4, 3)])
 @pytest.mark.parametrize("normed", [False, True])
 def test_split_silu_and_wide_tile(M, S, cfg, normed):
     """Split-K SiLU-gate (fp32 slabs, per-tile tickets, last arriver reduces + gates)
