@@ -168,20 +168,28 @@ def main():
     arrival = {}
     first_tok = {}
 
-    def submit(max_tokens):
+    def submit(max_tokens, extra=0):
         rid = f"r{rank}-{counter[0]}"
         counter[0] += 1
         # random token prompts: no accidental prefix sharing across requests
-        prompt = rng.integers(10, V - 10, size=a.prompt_len).tolist()
+        prompt = rng.integers(10, V - 10, size=a.prompt_len + extra).tolist()
         eng.add_request(rid, prompt, SamplingParams(max_tokens=max_tokens, temperature=a.temperature,
                                                    top_p=a.top_p, top_k=a.top_k, seed=counter[0],
                                                    ignore_eos=True))
         arrival[rid] = time.perf_counter()
 
-    # staggered output lengths (uniform on [1, 2*output_len], mean output_len) ->
-    # requests finish and get replaced continuously from the first steps on
+    # The initial population is drawn from the closed loop's STEADY STATE: every
+    # replacement request runs exactly output_len tokens, so at any instant the live
+    # requests' ages are uniform on [0, output_len). Request i starts with
+    # remaining = (i + 0.5) * output_len / C tokens to generate and a context already
+    # extended by its age (prompt_len + age prompt tokens), so from the first timed
+    # step one request finishes every output_len / C steps and is replaced by a fresh
+    # prompt_len prompt -- the same prefill share and KV-context mix as a 3,000-step run.
+    initial = []
     for i in range(a.concurrency):
-        submit(max(1, int(round(1 + (2 * a.output_len - 1) * (i + 0.5) / a.concurrency))))
+        remaining = max(1, int(round((i + 0.5) * a.output_len / a.concurrency)))
+        submit(remaining, extra=a.output_len - remaining)
+        initial.append(f"r{rank}-{counter[0] - 1}")
 
     step_log = [] if os.environ.get("XGS_STEP_LOG") else None
 
@@ -203,6 +211,12 @@ def main():
                 submit(a.output_len)
         return n_tok
 
+    # population fill (untimed setup, before the W warmup steps): prefill the initial
+    # population until every initial request has produced its first token
+    fill_steps = 0
+    while any(r not in first_tok for r in initial) and fill_steps < 10_000:
+        run_step()
+        fill_steps += 1
     for _ in range(a.warmup):
         run_step()
     sync()
@@ -214,10 +228,14 @@ def main():
     t_start_wall = time.perf_counter()
     tokens = 0
     first_before = set(first_tok)
+    c_before = dict(eng.stats_counters)
     for _ in range(a.steps):
         tokens += run_step()
     sync()
     elapsed = time.perf_counter() - t_start_wall
+    c_after = dict(eng.stats_counters)
+    window_steps = c_after["steps"] - c_before["steps"]
+    window_mixed = window_steps - (c_after["decode_steps"] - c_before["decode_steps"])
     if lgroup is not None:
         dist.barrier(group=lgroup)
     sync()
@@ -263,7 +281,10 @@ def main():
                        "concurrency_per_replica": a.concurrency,
                        "sampling": ("greedy" if a.temperature <= 0 else
                                     f"temperature {a.temperature}, top_p {a.top_p}, top_k {a.top_k}")},
-            "detail": {"preemptions": st_["preemptions"], "kv_blocks": st_["kv_blocks_total"],
+            "detail": {"initial_population": "steady-state (ages uniform on [0, output_len))",
+                       "fill_steps": fill_steps, "window_engine_steps": window_steps,
+                       "window_prompt_steps": window_mixed, "ttft_samples": len(ttfts),
+                       "preemptions": st_["preemptions"], "kv_blocks": st_["kv_blocks_total"],
                        "decode_steps_total": st_["decode_steps"], "steps_total": st_["steps"],
                        "gemm_table": bool(getattr(eng, "gemm_table", False)),
                        **({"host_ms_per_step": {k: round(1000 * v / a.steps, 4)

@@ -16,7 +16,7 @@
 //        results on every rank) with fp32 accumulation; write the output
 //   gen is a per-block counter kept in device memory, so the kernel is HIP
 //   graph capturable (no host-side sequence number). A peer wait that times out
-//   (~1 s) bumps the device error counter `err` and gives up instead of hanging
+//   (the limit in ctl[1], see car_wait) bumps the device error counter ctl[0] and gives up instead of hanging
 //   the GPU; the host reads the counter after every step (CustomAllReduce.check)
 //   and fails the step, so a missing peer is an error, never a wrong sum.
 //
@@ -64,6 +64,32 @@ __device__ __forceinline__ void acc8<uint16_t>(float* a, uint4 v) {  // bf16
   for (int i = 0; i < 8; ++i) a[i] += f[i];
 }
 
+// Peer waits: ctl[0] counts timeouts (the host polls it after every step),
+// ctl[1] is the wait limit in wall-clock ticks (wall_clock64, the device's constant
+// real-time counter; the host writes it -- generous during warmup / graph capture,
+// the configured collective timeout afterwards -- and captured graphs read the
+// current value on every replay). A wait gives up at once when ctl[0] is already
+// non-zero: after the first timeout of a step every later collective of that step
+// returns immediately instead of spinning its own full limit, so a dead peer is
+// reported within one limit, not one limit per collective.
+__device__ __forceinline__ bool car_wait(const uint32_t* f, uint32_t gen, uint32_t* ctl) {
+  if (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+  const uint64_t limit = __hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t t0 = wall_clock64();
+  uint32_t spins = 0;
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
+    __builtin_amdgcn_s_sleep(2);
+    if ((++spins & 63) == 0) {
+      if (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+      if (wall_clock64() - t0 > limit) {
+        atomicAdd(ctl, 1u);
+        return false;
+      }
+    }
+  }
+  return true;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(CAR_THREADS) car_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                           int64_t nbytes, int64_t slot_bytes, CarPtrs p, int rank,
@@ -94,14 +120,7 @@ __global__ void __launch_bounds__(CAR_THREADS) car_kernel(const uint8_t* __restr
   // 3. wait for every peer's flag for this block
   if (t < world && t != rank) {
     const uint32_t* f = p.sig[rank] + t * CAR_MAX_BLOCKS + b;
-    uint32_t spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 24)) {  // ~1 s: a peer never arrived -- record it and bail out rather than hang
-        atomicAdd(err, 1u);
-        break;
-      }
-    }
+    car_wait(f, gen, err);
   }
   __syncthreads();
   __threadfence_system();  // acquire side for every thread before reading peer data
@@ -131,14 +150,7 @@ __device__ __forceinline__ void car_signal_wait(const CarPtrs& p, int phase, int
     __hip_atomic_store(p.sig[t] + ph + rank * CAR_MAX_BLOCKS + b, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   if (t < world && t != rank) {
     const uint32_t* f = p.sig[rank] + ph + t * CAR_MAX_BLOCKS + b;
-    uint32_t spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 24)) {
-        atomicAdd(timeouts, 1u);
-        break;
-      }
-    }
+    car_wait(f, gen, timeouts);
   }
   __syncthreads();
   __threadfence_system();
@@ -252,14 +264,7 @@ __global__ void __launch_bounds__(128) car_resid_kernel(const float* __restrict_
     __hip_atomic_store(p.sig[lane] + rank * CAR_MAX_BLOCKS + b, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   if (lane < world && lane != rank) {
     const uint32_t* f = p.sig[rank] + lane * CAR_MAX_BLOCKS + b;
-    uint32_t spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 24)) {
-        atomicAdd(err, 1u);
-        break;
-      }
-    }
+    car_wait(f, gen, err);
   }
   __syncthreads();
   __threadfence_system();
@@ -355,14 +360,7 @@ __global__ void __launch_bounds__(CAR_THREADS) car_gather_kernel(const uint8_t* 
     __hip_atomic_store(p.sig[t] + rank * CAR_MAX_BLOCKS + b, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   if (t < world && t != rank) {
     const uint32_t* f = p.sig[rank] + t * CAR_MAX_BLOCKS + b;
-    uint32_t spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 24)) {
-        atomicAdd(err, 1u);
-        break;
-      }
-    }
+    car_wait(f, gen, err);
   }
   __syncthreads();
   __threadfence_system();
@@ -405,6 +403,13 @@ int custom_allgather_lastdim(const void* in, void* out, int64_t rows, int64_t cb
 }
 
 int car_max_blocks() { return CAR_MAX_BLOCKS; }
+// wall_clock64() ticks per millisecond on the current device (the peer-wait limit unit)
+int car_wallclock_khz() {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) return 0;
+  return khz;
+}
 int car_chunk() { return CAR_CHUNK; }
 int car_max_ranks() { return CAR_MAX_RANKS; }
 

@@ -63,36 +63,7 @@ struct QkvFuse {
   uint16_t* k_cache;            // the kernel's kc / vc, writable
   uint16_t* v_cache;
   int apply_rope;
-  // Next-GEMM weight prefetch: grid slices z >= num_splits read pf_bytes of the O
-  // projection's weights while the attention slices (latency-bound at small batch,
-  // HBM mostly idle) run, so the O GEMM that follows streams them from the
-  // Infinity Cache instead of HBM. pf_slices = 0: none.
-  const uint8_t* pf;
-  int64_t pf_bytes;
-  int pf_slices;
-  int preload;  // request the first K/V tiles before the prologue (XGS_DECODE_PRELOAD, default 1)
 };
-
-// One prefetch workgroup: reads its contiguous share of [pf, pf + pf_bytes) in
-// 16-B lanes, four loads in flight per lane (tail clamped, no branch per load),
-// and folds them into a value stored only under a condition the host never sets
-// (pf_slices < 0), so the loads are kept. Plain loads: hipcc counts their waits.
-__device__ __forceinline__ void prefetch_share(const QkvFuse& fq, int wg, int nwg) {
-  const int64_t n16 = fq.pf_bytes >> 4;
-  const int64_t per = (n16 + nwg - 1) / nwg;
-  const int64_t lo = static_cast<int64_t>(wg) * per, hi = min(n16, lo + per);
-  const float4* base = reinterpret_cast<const float4*>(fq.pf);
-  const int nt = blockDim.x;
-  float acc = 0.f;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += 4 * nt) {
-    float4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = base[min(i + u * nt, hi - 1)];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc += (v[u].x + v[u].y) + (v[u].z + v[u].w);
-  }
-  if (fq.pf_slices < 0) reinterpret_cast<float*>(fq.v_cache)[threadIdx.x] = acc;
-}
 
 // f[0..4) = sum_s part[s * slab + off + 0..4): batches of 4 clamped loads issued
 // before the adds (a runtime trip count with one load per iteration would chain S
@@ -172,17 +143,6 @@ __device__ __forceinline__ void decode_qkv_prologue(const QkvFuse& fq, int b, in
 //     from a 4 KiB wave-private LDS tile via ds_read_b64_tr_b16
 //   the next tile's K and V loads are issued before the current tile's math.
 // kc / vc are not __restrict__: the fused form writes the new row through fq.
-// Write-through (sc1) 4-B store: visible chip-wide once the storing wave's vmcnt
-// drains (the in-launch combine's hand-off needs no release fence). Not counted by
-// hipcc: the explicit vmcnt(0) before the ticket covers it.
-__device__ __forceinline__ void st4_sc1(float* p, float v) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm volatile("global_store_dword %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-#else
-  *p = v;
-#endif
-}
-
 // softmax(lse)-weighted sum over splits of one output element: po[s * D], lse[s].
 // All lse / partial loads of a 16-split batch are issued before any arithmetic
 // (unconditional clamped loads, masked after): a batch-1 decode has few heads, so
@@ -226,26 +186,23 @@ __device__ __forceinline__ float combine_splits(const float* __restrict__ lse, c
 // shape -- and staged into a wave-private, XOR-swizzled LDS tile whose ds_read_b128
 // fragment reads are conflict-free; the fragment-shaped global loads occupy the
 // texture-address path per byte moved, which caps the KV stream at 64 concurrent.
-template <int D, int G, bool FQ, int NWAVES = 4, bool KL = false>
-__global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
+// (Measured and removed, A/B records in profiles/: an in-launch split combine by the
+// last-arriving split, r1_inlaunch_combine_ab.md; O-weight prefetch workgroups inside
+// this launch, r1_attn_prefetch_ab.md; 8 waves per workgroup, r1_decode_waves_c1.md.)
+template <int D, int G, bool FQ, bool KL = false>
+__global__ void __launch_bounds__(256) decode_attn_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ seq_lens,
     float* __restrict__ part_out, float* __restrict__ part_lse, uint16_t* __restrict__ out, int64_t out_stride,
-    int Hq, int Hkv, int bs, float scale, int num_splits, int* __restrict__ counters, QkvFuse fq, int min_tps) {
-  using C = DecodeCfg<D, G, NWAVES>;
-  if (FQ && static_cast<int>(blockIdx.z) >= num_splits) {  // weight-prefetch slice (whole workgroup)
-    prefetch_share(fq, (blockIdx.z - num_splits) * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x,
-                   fq.pf_slices * gridDim.x * gridDim.y);
-    return;
-  }
+    int Hq, int Hkv, int bs, float scale, int num_splits, QkvFuse fq) {
+  using C = DecodeCfg<D, G>;
   const int kvh = blockIdx.x, b = blockIdx.y, split = blockIdx.z;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int L = seq_lens[b];
   const int ntiles = (L + 15) >> 4;
-  // tiles per split: an even share, but at least min_tps, so short sequences leave
-  // their trailing splits empty (they publish lse = -inf) and long ones spread out
-  const int tps = max(min_tps, (ntiles + num_splits - 1) / num_splits);
+  // tiles per split: an even share (a split past the sequence publishes lse = -inf)
+  const int tps = (ntiles + num_splits - 1) / num_splits;
   const int t_begin = split * tps;
   const int t_end = min(ntiles, t_begin + tps);
 
@@ -288,8 +245,8 @@ __global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
   // bytes do not depend on q), so the K/V latency overlaps the QKV-partial reads --
   // except the tile holding the key the prologue appends (the last one), which is
   // loaded after the prologue's barrier as before
-  const bool preA = FQ && fq.preload && t0 < t_end && t0 != ntiles - 1;
-  const bool preB = FQ && fq.preload && t0 + C::WAVES < t_end && t0 + C::WAVES != ntiles - 1;
+  const bool preA = FQ && t0 < t_end && t0 != ntiles - 1;
+  const bool preB = FQ && t0 + C::WAVES < t_end && t0 + C::WAVES != ntiles - 1;
   if (preA) load_tile(t0, kfA, vrA);
   if (preB) load_tile(t0 + C::WAVES, kfB, vrB);
   if constexpr (FQ) {
@@ -430,44 +387,11 @@ __global__ void __launch_bounds__(64 * NWAVES) decode_attn_kernel(
     } else {
       const int64_t pi = (static_cast<int64_t>(b) * Hq + qhead) * num_splits + split;
       const float lse_v = Ls > 0.f ? M + __logf(Ls) : -INFINITY;
-      if (counters != nullptr) {  // in-launch combine: write-through, published by the drain + ticket below
-        st4_sc1(part_out + pi * D + d, res);
-        if (d == 0) st4_sc1(part_lse + pi, lse_v);
-      } else {
-        part_out[pi * D + d] = res;
-        if (d == 0) part_lse[pi] = lse_v;
-      }
+      part_out[pi * D + d] = res;
+      if (d == 0) part_lse[pi] = lse_v;
     }
-  }
-  if (num_splits == 1 || counters == nullptr) return;
-  // In-launch split-K combine: the last split of (b, kv head) to arrive merges all
-  // splits' (O, lse) for its G query heads. Slabs were stored sc1 (write-through), so
-  // the hand-off is drain -> relaxed agent ticket, no release fence; the winner takes
-  // an agent acquire and reads with plain, batched loads (cdna_hip_programming.md §5
-  // "In-launch split-K reduction", sc1-store form; §5 trap (c): no load per branch).
-  __shared__ int am_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int* cnt = counters + b * Hkv + kvh;
-    const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    am_last = prev == num_splits - 1;
-    if (am_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed (graph replays)
-    }
-  }
-  __syncthreads();
-  if (!am_last) return;
-  for (int idx = threadIdx.x; idx < G * D; idx += blockDim.x) {
-    const int qhead = kvh * G + idx / D, d = idx % D;
-    const int64_t bh = static_cast<int64_t>(b) * Hq + qhead;
-    out[static_cast<int64_t>(b) * out_stride + static_cast<int64_t>(qhead) * D + d] =
-        f2bf(combine_splits<D>(part_lse + bh * num_splits, part_out + bh * num_splits * D + d, num_splits));
   }
 }
-
 // Split-K reduction launch: out[b, h, :] = sum_s softmax(lse)_s * part_out[b, h, s, :]
 template <int D>
 __global__ void __launch_bounds__(D) decode_combine_kernel(const float* __restrict__ part_out,
@@ -481,72 +405,35 @@ __global__ void __launch_bounds__(D) decode_combine_kernel(const float* __restri
                              part_out + static_cast<int64_t>(bh) * num_splits * D + threadIdx.x, num_splits));
 }
 
-// XGS_DECODE_ATTN_WAVES: 4 (default) or 8 waves per workgroup for the fused form (A/B).
-static int decode_attn_waves() {
-  static const int v = [] {
-    const char* e = std::getenv("XGS_DECODE_ATTN_WAVES");
-    return (e && std::atoi(e) == 8) ? 8 : 4;
-  }();
-  return v;
-}
-
-// XGS_DECODE_MIN_SPLIT_TILES: minimum 16-key tiles per split (default 1 = even split).
-static int decode_min_split_tiles() {
-  static const int v = [] {
-    const char* e = std::getenv("XGS_DECODE_MIN_SPLIT_TILES");
-    return e ? std::max(1, std::atoi(e)) : 1;
-  }();
-  return v;
-}
-
-// XGS_DECODE_K_LDS=0: K fragments loaded straight from HBM in the MFMA shape (A/B).
-static bool decode_k_lds() {
-  static const bool on = [] {
-    const char* e = std::getenv("XGS_DECODE_K_LDS");
-    return e == nullptr || e[0] != '0';
-  }();
-  return on;
-}
-
 template <int D, int G, bool FQ>
 static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, const uint16_t* vc,
                           const int32_t* bt, int bts, const int32_t* sl, float* po, float* pl, uint16_t* out,
-                          int64_t os, int B, int Hq, int Hkv, int bs, float scale, int S, int* counters,
-                          const QkvFuse& fq, hipStream_t st) {
-  const int gz = S + (FQ ? fq.pf_slices : 0);
-  // G <= 4 only: at G = 8 (one kv head per TP-8 rank of the 70B) measured 0.5-6 % slower
-  const bool klds = D == 128 && G <= 4 && decode_k_lds() && !(FQ && decode_attn_waves() == 8);
-  if constexpr (D == 128 && G <= 4) {
-    if (klds)
-      hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, 4, true>), dim3(Hkv, B, gz), dim3(256), 0, st, q, qs, kc, vc,
-                         bt, bts, sl, po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq,
-                         S > 1 ? decode_min_split_tiles() : 1);
-  }
-  if (klds) {
-  } else if (FQ && decode_attn_waves() == 8) {
-    hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, 8>), dim3(Hkv, B, gz), dim3(512), 0, st, q, qs, kc, vc, bt, bts,
-                       sl, po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq, S > 1 ? decode_min_split_tiles() : 1);
-  } else {
-    hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ>), dim3(Hkv, B, gz), dim3(256), 0, st, q, qs, kc, vc, bt, bts, sl,
-                       po, pl, out, os, Hq, Hkv, bs, scale, S, counters, fq, S > 1 ? decode_min_split_tiles() : 1);
-  }
-  if (S > 1 && counters == nullptr && out != nullptr)  // out == nullptr: merged by the consumer (gemm_m64g XA)
-    hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
+                          int64_t os, int B, int Hq, int Hkv, int bs, float scale, int S, const QkvFuse& fq,
+                          hipStream_t st) {
+  // K through LDS for G <= 4; at G = 8 (one kv head per TP-8 rank of the 70B) the
+  // fragment-shaped K loads measured 0.5-6 % faster
+  if constexpr (D == 128 && G <= 4)
+    hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, true>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt,
+                       bts, sl, po, pl, out, os, Hq, Hkv, bs, scale, S, fq);
+  else
+    hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt, bts, sl,
+                       po, pl, out, os, Hq, Hkv, bs, scale, S, fq);
+  if (S > 1) hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
 }
 
 // returns 0 on success, -1 for an unsupported (D, G) combination
 int decode_attention(const uint16_t* q, int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
                      const int32_t* bt, int bt_stride, const int32_t* seq_lens, float* part_out, float* part_lse,
                      uint16_t* out, int64_t out_stride, int B, int Hq, int Hkv, int D, int bs, float scale,
-                     int num_splits, int* counters, hipStream_t st) {
+                     int num_splits, hipStream_t st) {
   if (B <= 0) return 0;
   if (bs % 16 != 0 || Hq % Hkv != 0) return -1;
   const int G = Hq / Hkv;
-  const QkvFuse nofuse{nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0, 0, 0};
+  const QkvFuse nofuse{nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
 #define XGK_DEC(DD, GG)                                                                                  \
   if (D == DD && G == GG) {                                                                              \
     launch_decode<DD, GG, false>(q, q_stride, kc, vc, bt, bt_stride, seq_lens, part_out, part_lse, out,  \
-                                 out_stride, B, Hq, Hkv, bs, scale, num_splits, counters, nofuse, st);   \
+                                 out_stride, B, Hq, Hkv, bs, scale, num_splits, nofuse, st);             \
     return 0;                                                                                            \
   }
   XGK_DEC(128, 1) XGK_DEC(128, 2) XGK_DEC(128, 4) XGK_DEC(128, 8) XGK_DEC(128, 16)
@@ -560,24 +447,17 @@ int decode_attention_fq(const float* part, int S_qkv, const int32_t* positions, 
                         const int32_t* slots, uint16_t* kc, uint16_t* vc, const int32_t* bt, int bt_stride,
                         const int32_t* seq_lens, float* part_out, float* part_lse, uint16_t* out,
                         int64_t out_stride, int B, int Hq, int Hkv, int D, int bs, float scale, int num_splits,
-                        int apply_rope, int* counters, const void* pf, int64_t pf_bytes, int pf_slices,
-                        hipStream_t st) {
+                        int apply_rope, hipStream_t st) {
   if (B <= 0) return 0;
   if (part == nullptr || S_qkv < 1 || bs % 16 != 0 || Hq % Hkv != 0 || D != 128 || num_splits < 1) return -1;
   if (num_splits > 1 && (part_out == nullptr || part_lse == nullptr)) return -1;
-  if (out == nullptr && (num_splits == 1 || counters != nullptr)) return -1;  // deferred combine needs split slabs
-  if (pf_slices < 0 || (pf_slices > 0 && (pf == nullptr || pf_bytes <= 0))) return -1;
-  static const int preload = [] {
-    const char* e = std::getenv("XGS_DECODE_PRELOAD");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  const QkvFuse fq{part, S_qkv, positions, cos_sin, slots, kc, vc, apply_rope,
-                   static_cast<const uint8_t*>(pf), pf_bytes, pf_slices, preload};
+  if (out == nullptr) return -1;
+  const QkvFuse fq{part, S_qkv, positions, cos_sin, slots, kc, vc, apply_rope};
   const int G = Hq / Hkv;
 #define XGK_DECF(GG)                                                                                         \
   if (G == GG) {                                                                                             \
     launch_decode<128, GG, true>(nullptr, 0, kc, vc, bt, bt_stride, seq_lens, part_out, part_lse, out,       \
-                                 out_stride, B, Hq, Hkv, bs, scale, num_splits, counters, fq, st);           \
+                                 out_stride, B, Hq, Hkv, bs, scale, num_splits, fq, st);                     \
     return 0;                                                                                                \
   }
   XGK_DECF(1) XGK_DECF(2) XGK_DECF(4) XGK_DECF(8)

@@ -35,7 +35,7 @@
 
 namespace xgk {
 
-enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2, GG_RESID = 3, GG_RESID_COOP = 4 };
+enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2, GG_RESID = 3 };
 
 // Fused-decode epilogue operands (all null / 0 for a plain GEMM).
 //   ss_in / ss_n / ss_stride: RMSNorm statistics of the input rows as ss_n
@@ -50,13 +50,6 @@ enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2, GG_RESID = 3, GG_RESID_CO
 //           (the next GEMM's ss_in with ss_n = gridDim.x). counters: gridDim.x tile
 //           tickets, zero before the first launch; every ticket winner re-zeroes
 //           its word, so each launch leaves them zero.
-//   GG_RESID_COOP: the same result, reduced cooperatively: the S split workgroups of a
-//           column tile wait for each other (arrive / depart words counters[2 tile],
-//           counters[2 tile + 1]; the host enables it only when the whole grid is
-//           co-resident, one workgroup per CU) and each reduces M / S of the tile's rows
-//           -- no serial last-arriver pass over S x M x COLS fp32 and no separate
-//           add_partials_resid launch at M ~ 64. Bounded spin: a peer that never
-//           arrives costs ~1 s and a wrong tile, never a hang.
 struct M64Epi {
   const float* ss_in;
   int ss_n;
@@ -65,75 +58,7 @@ struct M64Epi {
   uint16_t* resid;
   float* ss_out;
   int* counters;
-  // XA form: x is the decode attention output still in split-K form (the combine
-  // launch is skipped): att_po [M, att_hq, att_splits, 128] fp32 normalised partial
-  // outputs, att_lse [M, att_hq, att_splits] their log-sum-exps.
-  const float* att_po;
-  const float* att_lse;
-  int att_splits;
-  int att_hq;
 };
-
-// XA prologue: the workgroup's x slice -- rows 0..15 x its kws = K / S columns, i.e.
-// kws / 128 attention heads -- merged from the split partials (online log-sum-exp
-// merge, batches of 8 splits with every load issued before the arithmetic) and
-// written as bf16 into xbuf in the DMA ring's x image: chunk c of KC columns at
-// c * 16 * RB, row m, 16-B granule j at (j ^ (m & (GPR - 1))) * 16. Rows >= M are
-// zero. Replaces the decode_combine launch of small-batch decode.
-template <int KC, int NTHR>
-__device__ __forceinline__ void m64g_xa_prologue(const M64Epi& epi, int M, int k0, int kws, uint8_t* xbuf) {
-  constexpr int RB = KC * 2, GPR = KC / 8, SB = 8;
-  const int nh = kws / 128;
-  const int NS = epi.att_splits;
-  for (int it = threadIdx.x; it < 16 * nh * 16; it += NTHR) {
-    const int m = it / (nh * 16), rem = it - m * (nh * 16);
-    const int hj = rem >> 4, c8 = rem & 15;
-    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (m < M) {
-      const int64_t bh = static_cast<int64_t>(m) * epi.att_hq + k0 / 128 + hj;
-      const float* lse = epi.att_lse + bh * NS;
-      const float* po = epi.att_po + bh * NS * 128 + 8 * c8;
-      float mx = -INFINITY, den = 0.f;
-      for (int s0 = 0; s0 < NS; s0 += SB) {
-        float l[SB];
-        float4 va[SB], vb[SB];
-#pragma unroll
-        for (int i = 0; i < SB; ++i) {
-          const int sc = min(s0 + i, NS - 1);
-          l[i] = lse[sc];
-          va[i] = *reinterpret_cast<const float4*>(po + static_cast<int64_t>(sc) * 128);
-          vb[i] = *reinterpret_cast<const float4*>(po + static_cast<int64_t>(sc) * 128 + 4);
-        }
-#pragma unroll
-        for (int i = 0; i < SB; ++i)
-          if (s0 + i >= NS) l[i] = -INFINITY;
-        float m2 = mx;
-#pragma unroll
-        for (int i = 0; i < SB; ++i) m2 = fmaxf(m2, l[i]);
-        if (m2 == -INFINITY) continue;
-        const float r = __expf(mx - m2);
-        den *= r;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] *= r;
-#pragma unroll
-        for (int i = 0; i < SB; ++i) {
-          const float wgt = __expf(l[i] - m2);
-          den += wgt;
-          o[0] += wgt * va[i].x; o[1] += wgt * va[i].y; o[2] += wgt * va[i].z; o[3] += wgt * va[i].w;
-          o[4] += wgt * vb[i].x; o[5] += wgt * vb[i].y; o[6] += wgt * vb[i].z; o[7] += wgt * vb[i].w;
-        }
-        mx = m2;
-      }
-      const float inv = den > 0.f ? 1.f / den : 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] *= inv;
-    }
-    const int k = hj * 128 + 8 * c8;
-    const int ch = k / KC, gr = (k % KC) / 8;
-    *reinterpret_cast<uint4*>(xbuf + ch * 16 * RB + m * RB + (gr ^ (m & (GPR - 1))) * 16) = pack8(o);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ordered for the readers by the ring's first barrier
-}
 
 // Every wave drains its stores (write-through), then one relaxed agent-scope
 // ticket; returns in every thread whether this workgroup drew `last_value`. The
@@ -224,37 +149,6 @@ __device__ __forceinline__ void m64g_resid_tail(const float* __restrict__ part, 
   m64g_resid_reduce<COLS, NTHR>(part, S, M, N, blockIdx.x, epi);
 }
 
-// GG_RESID_COOP tail: the tile's S workgroups meet (arrive word), each reduces its
-// row share, and the last to depart re-arms both words for the next launch.
-template <int COLS, int NTHR>
-__device__ __forceinline__ void m64g_resid_coop_tail(const float* __restrict__ part, int S, int M, int N,
-                                                     const M64Epi& epi, int* flag) {
-  int* arrive = epi.counters + 2 * blockIdx.x;
-  int* depart = arrive + 1;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's write-through slab stores are done
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t spins = 0;
-    while (__hip_atomic_load(arrive, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < S) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 24)) break;  // ~1 s: a peer was not co-resident -- give up rather than hang
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    *flag = 0;
-  }
-  __syncthreads();
-  const int rows = (M + S - 1) / S;
-  const int r0 = min(M, blockIdx.y * rows), r1 = min(M, r0 + rows);
-  if (r0 < r1) m64g_resid_reduce<COLS, NTHR>(part, S, M, N, blockIdx.x, epi, r0, r1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0 && __hip_atomic_fetch_add(depart, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1) {
-    __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(depart, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // Split-K GG_SILU tail: every workgroup has stored its fp32 partial of the tile
 // (write-through); the tile's last arriver sums the S slabs and applies the SiLU
 // gate (gate / up rows interleaved in blocks of 16) into out [M, N / 2]. Lets the
@@ -295,7 +189,7 @@ __device__ __forceinline__ void m64g_silu_tail(const float* __restrict__ part, i
 //   NT  non-temporal weight DMA (streamed once; keeps x resident in L2)
 //   MT  16-row x tiles (4: 16 < M <= 64; 1: M <= 16 -- a quarter of the x DMA and
 //       LDS per chunk, so the weight stream owns the load path at batch 1)
-template <int NW, int WV, int KC, bool NT, int MT, bool XA = false>
+template <int NW, int WV, int KC, bool NT, int MT>
 __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* __restrict__ x, int M, int K,
                                                                const uint16_t* __restrict__ w, int N,
                                                                float* __restrict__ part, uint16_t* __restrict__ out,
@@ -305,18 +199,16 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   constexpr int RPI = 1024 / RB;                 // rows per DMA instruction (64 lanes x 16 B)
   constexpr int XROWS = 16 * MT;
   constexpr int XBYTES = XROWS * RB;
-  constexpr int XI = XA ? 0 : XROWS / RPI / WV;  // x DMA instructions per wave per chunk (XA: x pre-staged)
+  constexpr int XI = XROWS / RPI / WV;           // x DMA instructions per wave per chunk
   constexpr int WROWS = 16 * NW;                 // weight rows per wave
   constexpr int WI = WROWS / RPI;                // weight DMA instructions per wave per chunk
   constexpr int WBYTES = WROWS * RB;             // per wave per slot
   constexpr int SLOT = XBYTES + WV * WBYTES;
   constexpr int G = XI + WI;
-  static_assert((XA ? MT == 1 : XI >= 1) && WI >= 1 && XROWS % (RPI * WV) == 0, "bad m64g geometry");
-  constexpr int XA_KMAX = 1024;                  // XA: the x slice [16][kws <= 1024] bf16
+  static_assert(XI >= 1 && WI >= 1 && XROWS % (RPI * WV) == 0, "bad m64g geometry");
   __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
-  __shared__ __attribute__((aligned(1024))) uint8_t xbuf[XA ? 16 * XA_KMAX * 2 : 16];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -333,7 +225,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
     const int r = RPI * i + dr;
     wsrc[i] = w + static_cast<int64_t>(nbase + r) * K + k0 + 8 * (dj ^ (r & (GPR - 1)));
   }
-  const uint16_t* xsrc[XI > 0 ? XI : 1];
+  const uint16_t* xsrc[XI];
 #pragma unroll
   for (int i = 0; i < XI; ++i) {
     const int r = RPI * (wid * XI + i) + dr;     // x row 0..XROWS-1
@@ -357,8 +249,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](const uint8_t* slot, int c) {
-    const uint8_t* xs = XA ? xbuf + c * XBYTES : slot;
+  auto compute = [&](const uint8_t* slot) {
+    const uint8_t* xs = slot;
     const uint8_t* ws = slot + XBYTES + wid * WBYTES;
 #pragma unroll
     for (int t = 0; t < KC / 32; ++t) {
@@ -382,7 +274,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
     else wait_vmcnt<0>();
     raw_barrier();
     if (c + 2 < nchunks) issue(nxt2, c + 2);
-    compute(cur, c);
+    compute(cur);
   };
 
   // RMSNorm statistics of the input rows, loaded before the weight stream starts
@@ -411,8 +303,6 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
 
   issue(lds0, 0);
   if (nchunks > 1) issue(lds1, 1);
-  // XA: merge the attention splits into xbuf while the first weight chunks stream
-  if constexpr (XA) m64g_xa_prologue<KC, 64 * WV>(epi, M, k0, kws, xbuf);
   int c = 0;
   for (; c + 3 <= nchunks; c += 3) {
     step(lds0, lds2, c);
@@ -477,7 +367,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
 
   // acc[nt][mt][r] = out[m = 16 mt + li][n = nbase + 16 nt + 4 g + r]
   const bool silu_split = NW == 2 && mode == GG_SILU && S > 1;
-  if (mode == GG_PARTIAL || mode == GG_RESID || mode == GG_RESID_COOP || silu_split) {
+  if (mode == GG_PARTIAL || mode == GG_RESID || silu_split) {
     float* pp = part + static_cast<int64_t>(s) * M * N;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -492,8 +382,6 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
     }
     if (mode == GG_RESID)
       m64g_resid_tail<16 * NW * WV, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0));
-    else if (mode == GG_RESID_COOP)
-      m64g_resid_coop_tail<16 * NW * WV, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0));
     else if (silu_split)
       m64g_silu_tail<16 * NW * WV, 64 * WV>(part, S, M, N, out, epi.counters, reinterpret_cast<int*>(lds0));
   } else if (mode == GG_BF16) {
@@ -707,15 +595,15 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
     if (rt0 >= offs[i] && rt0 < offs[i + 1]) e = i;
   if (e < 0) return;  // capacity padding past the last segment
   const int p0 = offs[e], p1 = offs[e + 1];
-  // MT_MAX 8 / 12 (prefill-sized steps): the 64-row tiles of an aligned group of 2 / 3
-  // within the expert's segment run as ONE 128- or 192-row workgroup when more than
-  // one of them holds real rows -- the expert's weight tile is streamed once per
+  // MT_MAX 8 (prefill-sized steps): the 64-row tiles of an aligned pair within the
+  // expert's segment run as ONE 128-row workgroup when both of them hold real rows -- the expert's weight tile is streamed once per
   // group instead of once per 64 rows (at ~144 rows per expert the re-reads are
   // what bound the GEMM). Every workgroup of a group counts the group's real rows
   // the same way; all but the leader exit when it takes them. Real rows lead each
   // segment, so the tiles past them are pads (never read by the combine).
   if constexpr (MT_MAX >= 8) {
-    constexpr int GT = MT_MAX / 4;                // tiles per group (2: pairs, 3: triples)
+    constexpr int GT = MT_MAX / 4;                // tiles per group (pairs); groups of three
+                                                  // measured slower (profiles/r2_moe_pairs_ab.md)
     const int lt = (rt0 - p0) >> 6, ntl = (p1 - p0) >> 6;
     const int gs = lt / GT * GT, gn = min(GT, ntl - gs);
     if (gn >= 2) {
@@ -730,12 +618,6 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
       const int need = (real + 63) >> 6;           // tiles holding real rows (they lead the segment)
       if (need >= 2) {
         if (lt != gs) return;                      // the group leader takes the group's real tiles
-        if constexpr (GT >= 3) {
-          if (need == 3) {
-            grouped_body<NW, WV, KC, NT, 12>(x, rows, e, p0, p1, r0, K, w, N, P, part, out, mode, lds0, lds1, lds2);
-            return;
-          }
-        }
         grouped_body<NW, WV, KC, NT, 8>(x, rows, e, p0, p1, r0, K, w, N, P, part, out, mode, lds0, lds1, lds2);
         return;
       }
@@ -765,38 +647,6 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
     grouped_body<NW, WV, KC, NT, 1>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2);
 }
 
-// M <= 16 takes the one-x-tile kernel (MT = 1) except for the 4-wave KC-64 configs,
-// whose 16 x rows would be less than one DMA instruction per wave.
-// XGS_M64G_MT1=0 keeps MT = 4 everywhere (A/B).
-static bool m64g_mt1_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("XGS_M64G_MT1");
-    return e == nullptr || e[0] != '0';
-  }();
-  return on;
-}
-
-// XGS_M64G_MT8=0: no 128-row pairs in the grouped GEMM (A/B).
-static bool m64g_mt8_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("XGS_M64G_MT8");
-    return e == nullptr || e[0] != '0';
-  }();
-  return on;
-}
-
-// XGS_M64G_GROUP=3: groups of up to three tiles (an expert of up to 192 rows in one
-// workgroup). Default 2 (pairs): measured faster on Mixtral's mixed steps (35.7 vs
-// 38.5 ms, profiles/r2_moe_pairs_ab.md) -- the 192-row body's registers halve the
-// occupancy of every workgroup in the launch.
-static bool m64g_group3() {
-  static const bool on = [] {
-    const char* e = std::getenv("XGS_M64G_GROUP");
-    return e != nullptr && e[0] == '3';
-  }();
-  return on;
-}
-
 int m64g_cfg_kc(int cfg);
 
 template <int NW>
@@ -812,24 +662,21 @@ static void launch_m64g_grouped(int cfg, dim3 grid, hipStream_t st, const uint16
     else XGK_GRP_MT(WV, KC, NT, 4);      \
   } while (0)
   // 128-row pairs (KC 64 configs only: the x slot doubles)
-#define XGK_GRP8(WV, KC, NT)                         \
-  do {                                               \
-    if (mt8 && m64g_group3()) XGK_GRP_MT(WV, KC, NT, 12); \
-    else if (mt8) XGK_GRP_MT(WV, KC, NT, 8);         \
-    else if (mt1) XGK_GRP_MT(WV, KC, NT, 1);         \
-    else XGK_GRP_MT(WV, KC, NT, 4);                  \
+#define XGK_GRP8(WV, KC, NT)                 \
+  do {                                       \
+    if (mt8) XGK_GRP_MT(WV, KC, NT, 8);      \
+    else if (mt1) XGK_GRP_MT(WV, KC, NT, 1); \
+    else XGK_GRP_MT(WV, KC, NT, 4);          \
   } while (0)
   // the 4-wave KC-64 configs have < 1 x DMA instruction per wave at 16 rows: MT >= 2
   switch (cfg) {
     case 1: XGK_GRP(4, 128, true); break;
     case 2:
-      if (mt8 && m64g_group3()) XGK_GRP_MT(4, 64, false, 12);
-      else if (mt8) XGK_GRP_MT(4, 64, false, 8);
+      if (mt8) XGK_GRP_MT(4, 64, false, 8);
       else XGK_GRP_MT(4, 64, false, 4);
       break;
     case 3:
-      if (mt8 && m64g_group3()) XGK_GRP_MT(4, 64, true, 12);
-      else if (mt8) XGK_GRP_MT(4, 64, true, 8);
+      if (mt8) XGK_GRP_MT(4, 64, true, 8);
       else XGK_GRP_MT(4, 64, true, 4);
       break;
     case 4: XGK_GRP8(2, 64, false); break;
@@ -860,10 +707,10 @@ int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, i
   if (mode != GG_PARTIAL && out == nullptr) return 1;
   if (P == 0) return 0;
   const dim3 grid(N / cols, S, P / 64);
-  const bool mt1 = max_rows <= 16 && cfg != 2 && cfg != 3 && m64g_mt1_enabled();
+  const bool mt1 = max_rows <= 16 && cfg != 2 && cfg != 3;  // 16 x rows >= one DMA per wave
   // 128-row pairs for prefill-sized steps (> 256 pairs; decode keeps the 48 KB-slot
   // kernel and its occupancy), KC 64 configs only
-  const bool mt8 = max_rows > 256 && m64g_cfg_kc(cfg) == 64 && m64g_mt8_enabled();
+  const bool mt8 = max_rows > 256 && m64g_cfg_kc(cfg) == 64;
   if (nw == 1) launch_m64g_grouped<1>(cfg, grid, st, x, rows, offs, valid, E, K, w, N, P, part, out, mode, mt1, mt8);
   else launch_m64g_grouped<2>(cfg, grid, st, x, rows, offs, valid, E, K, w, N, P, part, out, mode, mt1, mt8);
   return 0;
@@ -875,14 +722,12 @@ int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, i
 template <int NW>
 static void launch_m64g(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N,
                         float* part, uint16_t* out, int mode, const M64Epi& epi) {
-  const bool mt1 = M <= 16 && cfg != 2 && cfg != 3 && m64g_mt1_enabled();
-  const bool xa = epi.att_po != nullptr;  // m64g_check: only with mt1
+  // M <= 16: the one-x-tile kernel, except the 4-wave KC-64 configs (16 x rows would
+  // be less than one DMA instruction per wave)
+  const bool mt1 = M <= 16 && cfg != 2 && cfg != 3;
 #define XGK_M64G(WV, KC, NT)                                                                                         \
   do {                                                                                                               \
-    if (xa)                                                                                                          \
-      hipLaunchKernelGGL((gemm_m64g_kernel<NW, WV, KC, NT, 1, true>), grid, dim3(64 * WV), 0, st, x, M, K, w, N,     \
-                         part, out, mode, epi);                                                                      \
-    else if (mt1)                                                                                                    \
+    if (mt1)                                                                                                         \
       hipLaunchKernelGGL((gemm_m64g_kernel<NW, WV, KC, NT, 1>), grid, dim3(64 * WV), 0, st, x, M, K, w, N, part, out, \
                          mode, epi);                                                                                 \
     else                                                                                                             \
@@ -913,26 +758,16 @@ int m64g_cfg_kc(int cfg) { return (cfg == 2 || cfg == 3 || cfg == 4 || cfg == 5 
 static int m64g_check(int M, int K, int N, const float* part, const uint16_t* out, int S, int mode, int nw, int cfg,
                       const M64Epi& epi) {
   if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 7) return 1;
-  if (mode < GG_BF16 || mode > GG_RESID_COOP) return 1;
-  // co-residency of every split of a tile: one workgroup per CU for the whole grid
-  if (mode == GG_RESID_COOP && (N / (16 * nw * m64g_cfg_waves(cfg))) * S > 256) return 1;
+  if (mode < GG_BF16 || mode > GG_RESID) return 1;
   const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
   if (K % (S * kc) || N % cols) return 1;
   // split-K SiLU: fp32 slabs + one zeroed arrival ticket per column tile (m64g_silu_tail)
   if (mode == GG_SILU && (nw != 2 || (S > 1 && (part == nullptr || epi.counters == nullptr)))) return 1;
   if (mode == GG_BF16 && S != 1) return 1;
-  if ((mode == GG_PARTIAL || mode == GG_RESID || mode == GG_RESID_COOP) && part == nullptr) return 1;
+  if ((mode == GG_PARTIAL || mode == GG_RESID) && part == nullptr) return 1;
   if ((mode == GG_BF16 || mode == GG_SILU) && out == nullptr) return 1;
-  if ((mode == GG_RESID || mode == GG_RESID_COOP) &&
-      (epi.resid == nullptr || epi.ss_out == nullptr || epi.counters == nullptr))
-    return 1;
+  if (mode == GG_RESID && (epi.resid == nullptr || epi.ss_out == nullptr || epi.counters == nullptr)) return 1;
   if (epi.ss_in != nullptr && (epi.ss_n < 1 || epi.ss_n > 64 || epi.ss_stride < M)) return 1;
-  if (epi.att_po != nullptr) {  // XA: one-x-tile kernel, whole heads of 128 per K slice, slice fits xbuf
-    const int kws = K / S;
-    if (M > 16 || cfg == 2 || cfg == 3 || cfg == 7 || !m64g_mt1_enabled() || epi.att_lse == nullptr || epi.att_splits < 1 ||
-        kws % 128 || kws > 1024 || K != epi.att_hq * 128)
-      return 1;
-  }
   return 0;
 }
 
@@ -945,8 +780,8 @@ static void m64g_launch(const uint16_t* x, int M, int K, const uint16_t* w, int 
 
 int gemm_m64g(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
               int nw, int cfg, hipStream_t st) {
-  const M64Epi epi{nullptr, 0, 0, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
-  if (mode == GG_RESID || mode == GG_RESID_COOP || m64g_check(M, K, N, part, out, S, mode, nw, cfg, epi)) return 1;
+  const M64Epi epi{nullptr, 0, 0, 0.f, nullptr, nullptr, nullptr};
+  if (mode == GG_RESID || m64g_check(M, K, N, part, out, S, mode, nw, cfg, epi)) return 1;
   m64g_launch(x, M, K, w, N, part, out, S, mode, nw, cfg, epi, st);
   return 0;
 }
@@ -955,9 +790,8 @@ int gemm_m64g(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* 
 // epilogue; ss_out holds (N / cols) * M floats, counters N / cols ints.
 int gemm_m64g_ex(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S,
                  int mode, int nw, int cfg, const float* ss_in, int ss_n, int ss_stride, float eps, uint16_t* resid,
-                 float* ss_out, int* counters, hipStream_t st, const float* att_po, const float* att_lse,
-                 int att_splits, int att_hq) {
-  const M64Epi epi{ss_in, ss_n, ss_stride, eps, resid, ss_out, counters, att_po, att_lse, att_splits, att_hq};
+                 float* ss_out, int* counters, hipStream_t st) {
+  const M64Epi epi{ss_in, ss_n, ss_stride, eps, resid, ss_out, counters};
   if (m64g_check(M, K, N, part, out, S, mode, nw, cfg, epi)) return 1;
   m64g_launch(x, M, K, w, N, part, out, S, mode, nw, cfg, epi, st);
   return 0;

@@ -20,17 +20,16 @@ void layernorm(const uint16_t*, const uint16_t*, const uint16_t*, uint16_t*, int
 void silu_and_mul(const uint16_t*, uint16_t*, int, int, int, hipStream_t);
 int skinny_gemm(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, hipStream_t);
 int skinny_slab_kmax(int);
-int gemm_m64(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 int gemm_m64g(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 int gemm_m64g_ex(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, const float*,
-                 int, int, float, uint16_t*, float*, int*, hipStream_t, const float*, const float*, int, int);
+                 int, int, float, uint16_t*, float*, int*, hipStream_t);
 void add_partials_resid(const float*, int, int, uint16_t*, float*, int, hipStream_t);
 void row_sumsq(const uint16_t*, int, int, float*, hipStream_t);
 void embed_gather(const int32_t*, int, const uint16_t*, int, int, uint16_t*, float*, hipStream_t);
 void mean_l2norm_rows(float*, const int32_t*, const int32_t*, float*, int, int, hipStream_t);
 int decode_attention_fq(const float*, int, const int32_t*, const float*, const int32_t*, uint16_t*, uint16_t*,
                         const int32_t*, int, const int32_t*, float*, float*, uint16_t*, int64_t, int, int, int, int,
-                        int, float, int, int, int*, const void*, int64_t, int, hipStream_t);
+                        int, float, int, int, hipStream_t);
 int moe_gemm_m64g(const uint16_t*, const int32_t*, const int32_t*, int, int, const uint16_t*, int, int, float*,
                   uint16_t*, int, int, int, int, int, hipStream_t, const int32_t*);
 void add_partials_rmsnorm(const float*, int, int, uint16_t*, const uint16_t*, uint16_t*, int, float, hipStream_t);
@@ -41,7 +40,7 @@ void gelu_tanh(const uint16_t*, uint16_t*, int64_t, hipStream_t);
 int rope_cache(uint16_t*, int64_t, const int32_t*, const float*, uint16_t*, uint16_t*, const int32_t*, int, int, int,
                int, int, int, hipStream_t);
 int decode_attention(const uint16_t*, int64_t, const uint16_t*, const uint16_t*, const int32_t*, int, const int32_t*,
-                     float*, float*, uint16_t*, int64_t, int, int, int, int, int, float, int, int*, hipStream_t);
+                     float*, float*, uint16_t*, int64_t, int, int, int, int, int, float, int, hipStream_t);
 int prefill_attention(const uint16_t*, int64_t, const uint16_t*, const uint16_t*, const int32_t*, int, const int32_t*,
                       const int32_t*, uint16_t*, int64_t, int, int, int, int, int, int, float, hipStream_t, int);
 void argmax_logprob(const void*, int, int64_t, int, int, int32_t*, float*, hipStream_t);
@@ -61,8 +60,6 @@ int moe_combine_resid(const float*, int, int, const int32_t*, const float*, uint
                       hipStream_t);
 int ep_plan(const int32_t*, int, int, int, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
 int ep_scatter(const uint16_t*, int64_t, int, const int32_t*, int, int, uint16_t*, hipStream_t);
-int moe_gemm_m64(const uint16_t*, const int32_t*, const int32_t*, int, int, const uint16_t*, int, int, float*,
-                 uint16_t*, int, int, int, hipStream_t);
 int custom_allreduce(const void*, void*, int64_t, int64_t, const uintptr_t*, const uintptr_t*, int, int, uint32_t*,
                      uint32_t*, hipStream_t);
 int custom_allreduce_2shot(const void*, void*, int64_t, int64_t, const uintptr_t*, const uintptr_t*, int, int,
@@ -72,6 +69,7 @@ int custom_allreduce_resid(const float*, int, int, uint16_t*, float*, int, int64
 int custom_allgather_lastdim(const void*, void*, int64_t, int64_t, int64_t, const uintptr_t*, const uintptr_t*, int,
                              int, uint32_t*, uint32_t*, hipStream_t);
 int car_max_blocks();
+int car_wallclock_khz();
 int car_chunk();
 int car_max_ranks();
 int car_alloc_uncached(int64_t, void**);
@@ -163,10 +161,10 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("decode_attention", [](uintptr_t q, int64_t qs, uintptr_t kc, uintptr_t vc, uintptr_t bt, int bts,
                                uintptr_t sl, uintptr_t po, uintptr_t pl, uintptr_t out, int64_t os, int B, int Hq,
-                               int Hkv, int D, int bs, float scale, int splits, uintptr_t counters, uintptr_t st) {
+                               int Hkv, int D, int bs, float scale, int splits, uintptr_t st) {
     check(xgk::decode_attention(P<const uint16_t>(q), qs, P<const uint16_t>(kc), P<const uint16_t>(vc),
                                 P<const int32_t>(bt), bts, P<const int32_t>(sl), P<float>(po), P<float>(pl),
-                                P<uint16_t>(out), os, B, Hq, Hkv, D, bs, scale, splits, P<int>(counters), S(st)),
+                                P<uint16_t>(out), os, B, Hq, Hkv, D, bs, scale, splits, S(st)),
           "decode_attention");
   });
   m.def("prefill_attention", [](uintptr_t q, int64_t qs, uintptr_t kc, uintptr_t vc, uintptr_t bt, int bts,
@@ -229,12 +227,6 @@ PYBIND11_MODULE(_kernels, m) {
                    P<int32_t>(expert_offsets), P<int32_t>(dest), S(st));
     check(0, "moe_align");
   });
-  m.def("moe_gemm_m64", [](uintptr_t x, uintptr_t rows, uintptr_t offs, int E, int K, uintptr_t w, int N, int P_,
-                           uintptr_t part, uintptr_t out, int splits, int mode, int nw, uintptr_t st) {
-    check(xgk::moe_gemm_m64(P<const uint16_t>(x), P<const int32_t>(rows), P<const int32_t>(offs), E, K,
-                            P<const uint16_t>(w), N, P_, P<float>(part), P<uint16_t>(out), splits, mode, nw, S(st)),
-          "moe_gemm_m64");
-  });
   m.def("gemm_m64g", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
                         int mode, int nw, int cfg, uintptr_t st) {
     check(xgk::gemm_m64g(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode, nw,
@@ -244,13 +236,10 @@ PYBIND11_MODULE(_kernels, m) {
   // ---- fused decode layer (gemm_m64g.hip epilogues, decode_attention.hip FQ prologue)
   m.def("gemm_m64g_ex", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
                            int mode, int nw, int cfg, uintptr_t ss_in, int ss_n, int ss_stride, float eps,
-                           uintptr_t resid, uintptr_t ss_out, uintptr_t counters, uintptr_t st, uintptr_t att_po,
-                           uintptr_t att_lse, int att_splits, int att_hq) {
-    // att_po != 0: x is the decode attention output in split form (merged in the GEMM prologue)
+                           uintptr_t resid, uintptr_t ss_out, uintptr_t counters, uintptr_t st) {
     check(xgk::gemm_m64g_ex(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode,
                             nw, cfg, P<const float>(ss_in), ss_n, ss_stride, eps, P<uint16_t>(resid),
-                            P<float>(ss_out), P<int>(counters), S(st), P<const float>(att_po),
-                            P<const float>(att_lse), att_splits, att_hq),
+                            P<float>(ss_out), P<int>(counters), S(st)),
           "gemm_m64g_ex");
   });
   m.def("add_partials_resid", [](uintptr_t part, int S_, int T, uintptr_t res, uintptr_t ss_part, int H,
@@ -279,13 +268,11 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("decode_attention_fq", [](uintptr_t part, int S_, uintptr_t pos, uintptr_t cs, uintptr_t slots, uintptr_t kc,
                                   uintptr_t vc, uintptr_t bt, int bts, uintptr_t sl, uintptr_t po, uintptr_t pl,
                                   uintptr_t out, int64_t os, int B, int Hq, int Hkv, int D, int bs, float scale,
-                                  int splits, int apply_rope, uintptr_t cnt, uintptr_t pf, int64_t pf_bytes,
-                                  int pf_slices, uintptr_t st) {
+                                  int splits, int apply_rope, uintptr_t st) {
     check(xgk::decode_attention_fq(P<const float>(part), S_, P<const int32_t>(pos), P<const float>(cs),
                                    P<const int32_t>(slots), P<uint16_t>(kc), P<uint16_t>(vc), P<const int32_t>(bt),
                                    bts, P<const int32_t>(sl), P<float>(po), P<float>(pl), P<uint16_t>(out), os, B, Hq,
-                                   Hkv, D, bs, scale, splits, apply_rope, P<int>(cnt), P<const void>(pf), pf_bytes,
-                                   pf_slices, S(st)),
+                                   Hkv, D, bs, scale, splits, apply_rope, S(st)),
           "decode_attention_fq");
   });
   m.def("moe_gemm_m64g", [](uintptr_t x, uintptr_t rows, uintptr_t offs, int E, int K, uintptr_t w, int N, int P_,
@@ -350,6 +337,7 @@ PYBIND11_MODULE(_kernels, m) {
   });
 
   // ---- custom one-shot xGMI all-reduce (csrc/comm/custom_allreduce.hip)
+  m.def("car_wallclock_khz", []() { return xgk::car_wallclock_khz(); });
   m.def("car_limits", []() { return py::make_tuple(xgk::car_max_ranks(), xgk::car_max_blocks(), xgk::car_chunk()); });
   m.def("car_alloc_uncached", [](int64_t bytes) {
     void* p = nullptr;
@@ -412,10 +400,4 @@ PYBIND11_MODULE(_kernels, m) {
           "custom_allgather_lastdim");
   });
 
-  m.def("gemm_m64", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
-                       int mode, int nw, int variant, uintptr_t st) {
-    check(xgk::gemm_m64(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode, nw,
-                        variant, S(st)),
-          "gemm_m64");
-  });
 }

@@ -110,12 +110,10 @@ def test_wide_tile_partials(M, N, K, S):
 
 @pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 14336)])
-@pytest.mark.parametrize("inlaunch", [True, False, "coop"])
+@pytest.mark.parametrize("inlaunch", [True, False])
 def test_resid_linear(M, N, K, inlaunch, monkeypatch):
-    """inlaunch True: last-arriver ticket reduce; "coop": the tile's split workgroups
-    meet and reduce M / S rows each (GG_RESID_COOP); False: separate add_partials_resid."""
+    """inlaunch True: last-arriver ticket reduce; False: separate add_partials_resid."""
     monkeypatch.setattr(lin, "RESID_INLAUNCH_MAX_BYTES", (1 << 30) if inlaunch is True else 0)
-    monkeypatch.setattr(lin, "RESID_COOP", inlaunch == "coop")
     x, w, r0 = rnd(M, K), rnd(N, K, scale=0.02), rnd(M, N)
     ws = ResidWorkspace(4, 64, N, DEV)
     ref = (r0.float() + x.float() @ w.float().t()).bfloat16().float()
@@ -126,7 +124,7 @@ def test_resid_linear(M, N, K, inlaunch, monkeypatch):
         torch.testing.assert_close(r.float(), ref, atol=3e-2, rtol=2e-2)
         ss = st.ss.reshape(-1)[: st.n * st.stride].view(st.n, st.stride)[:, :M].sum(0)
         nw, S, cfg = lin.m64_plan(M, N, K, MODE_PARTIAL)
-        if inlaunch is True or (inlaunch == "coop" and S > 1):  # one partial sum per column tile
+        if inlaunch is True:  # one partial sum per column tile
             assert st.n == N // (16 * nw * lin.M64G_CFGS[cfg][0])
         else:
             assert st.n == N // 1024
@@ -152,12 +150,9 @@ def _paged(lens, Hkv, D, bs, extra_pages=8):
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 8)])
 @pytest.mark.parametrize("S", [1, 4, 8])
-@pytest.mark.parametrize("splits,in_kernel,pf", [(1, False, False), (3, False, False), (3, True, False),
-                                                 (16, True, False), (1, False, True), (3, False, True),
-                                                 (16, True, True)])
-def test_decode_attention_fused_prologue(Hq, Hkv, S, splits, in_kernel, pf, monkeypatch):
+@pytest.mark.parametrize("splits", [1, 3, 16])
+def test_decode_attention_fused_prologue(Hq, Hkv, S, splits):
     import xgserve.ops.attention as A
-    monkeypatch.setattr(A, "IN_KERNEL_COMBINE", in_kernel)
     D, bs = 128, 16
     lens = [1, 17, 300, 64, 0, 129]  # row 4: a graph padding row (no KV write, no attention)
     kc, vc, bt = _paged([max(1, L) for L in lens], Hkv, D, bs)
@@ -171,14 +166,8 @@ def test_decode_attention_fused_prologue(Hq, Hkv, S, splits, in_kernel, pf, monk
     scale = 1.0 / math.sqrt(D)
     kc1, vc1, kc2, vc2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
     ws = A.DecodeWorkspace(B, Hq, D, splits, DEV)
-    # prefetch slices over an odd-sized weight (the tail share is partial); must not disturb the result
-    wpf = torch.randn(4096 * 1000 + 8, dtype=torch.bfloat16, device=DEV) if pf else None
-    monkeypatch.setattr(A, "ATTN_PREFETCH", True)
-    for _ in range(2 if in_kernel else 1):  # the second launch needs the tickets re-armed by the first
-        out = ops.decode_attention_fused(PendingSum(part, S), pos, slots, cs, kc1, vc1, bt, sl, Hq, scale, splits,
-                                         workspace=ws, prefetch=wpf)
-    if in_kernel:
-        assert int(ws.counters.abs().sum().item()) == 0
+    out = ops.decode_attention_fused(PendingSum(part, S), pos, slots, cs, kc1, vc1, bt, sl, Hq, scale, splits,
+                                     workspace=ws)
     # reference: the unfused chain (rope_cache_partials -> fp32 attention reference)
     q = torch.empty(B, Hq * D, dtype=torch.bfloat16, device=DEV)
     ops.rope_cache_partials(PendingSum(part, S), q, pos, cs, kc2, vc2, slots, Hq, Hkv, D)
@@ -238,48 +227,6 @@ def test_fused_batch_decode_matches_unfused(llama_small, monkeypatch):
         outs[fused] = eng.generate(prompts, sp)
     agree = sum(a[1] == b[1] for a, b in zip(outs[True], outs[False]))
     assert agree >= 4, outs
-
-
-@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (16, 4)])
-@pytest.mark.parametrize("lens", [[600], [1, 17, 300, 64, 0, 129]])
-@pytest.mark.parametrize("splits", [3, 16])
-def test_o_projection_merges_split_attention(Hq, Hkv, lens, splits, monkeypatch):
-    """XA form: the attention launch skips its split combine (PendingAttn) and the O
-    projection's gemm_m64g prologue merges the splits -- against the combine launch
-    followed by the plain GEMM (resid epilogue and PendingSum forms)."""
-    import xgserve.ops.attention as A
-    monkeypatch.setattr(lin, "XA_MAX_M", 16)  # opt-in path (measured slower end to end)
-    D, bs, S = 128, 16, 4
-    kc, vc, bt = _paged([max(1, L) for L in lens], Hkv, D, bs)
-    B = len(lens)
-    part = torch.randn(S, B, (Hq + 2 * Hkv) * D, device=DEV) * 0.3
-    pos = torch.tensor([max(0, L - 1) for L in lens], dtype=torch.int32, device=DEV)
-    slots = torch.tensor([int(bt[b, (L - 1) // bs]) * bs + (L - 1) % bs if L > 0 else -1
-                          for b, L in enumerate(lens)], dtype=torch.int32, device=DEV)
-    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
-    cs = ops.build_cos_sin(D, 4096, 500000.0, device=DEV)
-    scale = 1.0 / math.sqrt(D)
-    ws_a, ws_b = A.DecodeWorkspace(B, Hq, D, splits, DEV), A.DecodeWorkspace(B, Hq, D, splits, DEV)
-    a = ops.decode_attention_fused(PendingSum(part, S), pos, slots, cs, kc.clone(), vc.clone(), bt, sl, Hq, scale,
-                                   splits, workspace=ws_a)
-    pa = ops.decode_attention_fused(PendingSum(part, S), pos, slots, cs, kc.clone(), vc.clone(), bt, sl, Hq, scale,
-                                    splits, workspace=ws_b, defer_combine=True)
-    assert isinstance(pa, A.PendingAttn)
-    N, K = 4096, Hq * D
-    assert lin.m64_xa_ok(B, N, K)
-    w = rnd(N, K, scale=0.02)
-    want = a.float() @ w.float().t()
-    got = lin.m64_xa_linear(pa, w).part.sum(0)
-    assert rel_err(got, want) < 1e-2
-    r0 = rnd(B, N)
-    rw = ResidWorkspace(4, 64, N, DEV)
-    r1, r2 = r0.clone(), r0.clone()
-    st1 = m64_resid_linear(a, w, r1, rw, 1, 1e-5)
-    st2 = m64_resid_linear(pa, w, r2, rw, 2, 1e-5)
-    assert rel_err(r2, r1) < 1e-2
-    ss1 = st1.ss[:st1.n * B].view(st1.n, B).sum(0)
-    ss2 = st2.ss[:st2.n * B].view(st2.n, B).sum(0)
-    torch.testing.assert_close(ss2, ss1, rtol=2e-2, atol=1e-2)
 
 
 @pytest.fixture(scope="module")

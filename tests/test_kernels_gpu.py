@@ -370,30 +370,21 @@ def test_moe_route_matches_fp32(T, E, k, H):
     torch.testing.assert_close(w.cpu().sort(-1).values, rw.sort(-1).values, atol=1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize("glds", [True, False])
-@pytest.mark.parametrize("T", [1, 3, 64, 150])
-def test_fused_moe_both_pipelines(T, glds, monkeypatch):
-    from xgserve.ops import moe as M
-    monkeypatch.setattr(M, "MOE_DENSE_MIN_PAIRS", 1 << 30)  # the grouped pipelines at every T
+@pytest.mark.parametrize("T", [1, 3, 64, 150, 300])
+def test_fused_moe_grouped(T):
     E, k, H, F = 8, 2, 1024, 512
     x = rnd(T, H)
     w13 = _w13(E, F, H)
     w2 = rnd(E, H, F, scale=0.05)
     w, ids = ops.moe_topk_softmax(rnd(T, E, dtype=torch.float32), k)
-    old = M.MOE_GLDS
-    M.MOE_GLDS = glds
-    try:
-        out = ops.fused_moe(x, w13, w2, w, ids)
-    finally:
-        M.MOE_GLDS = old
+    out = ops.fused_moe(x, w13, w2, w, ids)
     ref = ops.moe_forward_ref(x.cpu(), w13.cpu(), w2.cpu(), w.cpu(), ids.cpu()).float()
     torch.testing.assert_close(out.cpu().float(), ref, atol=2e-2 * ref.std().item(), rtol=2e-2)
 
 
-@pytest.mark.parametrize("in_kernel", [True, False])
-def test_decode_attention_split_combine_rearms(in_kernel):
-    """The in-launch combine's arrival tickets re-arm: repeated launches on one
-    workspace (as graph replays do) stay correct; also the two-launch fallback."""
+def test_decode_attention_split_combine_repeats():
+    """Repeated split-K launches on one workspace (as graph replays do) with varying
+    split counts stay correct."""
     from xgserve.ops import attention as A
     Hq, Hkv, D, bs = 32, 8, 128, 16
     lens = [700, 33, 1, 256]
@@ -401,41 +392,11 @@ def test_decode_attention_split_combine_rearms(in_kernel):
     B = len(lens)
     sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
     ws = A.DecodeWorkspace(B, Hq, D, 16, DEV)
-    old = A.IN_KERNEL_COMBINE
-    A.IN_KERNEL_COMBINE = in_kernel
-    try:
-        for it, splits in enumerate((16, 16, 5, 16)):
-            q = rnd(B, Hq, D)
-            out = ops.decode_attention(q, kc, vc, bt, sl, 0.088, num_splits=splits, workspace=ws)
-            ref = ops.decode_attention_ref(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), sl.cpu(), 0.088)
-            torch.testing.assert_close(out.cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
-    finally:
-        A.IN_KERNEL_COMBINE = old
-    assert int(ws.counters.abs().sum()) == 0
-
-
-@pytest.mark.parametrize("T,offset", [(300, 0), (300, 4), (1100, 0)])
-def test_fused_moe_prefill_per_expert_path(T, offset, monkeypatch):
-    """Prefill-sized MoE (per-expert hipBLASLt path) vs the fp32 reference and vs the
-    grouped m64g path on the same routing, incl. an expert-parallel shard."""
-    from xgserve.ops import moe as MO
-    E, k, H, F = 8, 2, 1024, 512
-    El = 4 if offset else E
-    x = rnd(T, H)
-    w13 = _w13(El, F, H)
-    w2 = rnd(El, H, F, scale=0.05)
-    logits = rnd(T, E, dtype=torch.float32)
-    w, ids = ops.moe_topk_softmax(logits, k)
-    monkeypatch.setattr(MO, "MOE_DENSE_MIN_PAIRS", 1)
-    dense = ops.fused_moe(x, w13, w2, w, ids, offset)
-    monkeypatch.setattr(MO, "MOE_DENSE_MIN_PAIRS", 1 << 30)
-    grouped = ops.fused_moe(x, w13, w2, w, ids, offset)
-    ref = ops.moe_forward_ref(x.cpu(), w13.cpu(), w2.cpu(), w.cpu(), ids.cpu(), offset).float()
-    # the hipBLASLt path rounds gate and up to bf16 before the SiLU-gate (the grouped
-    # kernel applies it to fp32 accumulators): one extra bf16 rounding
-    tol = 3e-2 * ref.std().item()
-    torch.testing.assert_close(dense.cpu().float(), ref, atol=tol, rtol=3e-2)
-    torch.testing.assert_close(dense.float(), grouped.float(), atol=tol, rtol=3e-2)
+    for it, splits in enumerate((16, 16, 5, 16)):
+        q = rnd(B, Hq, D)
+        out = ops.decode_attention(q, kc, vc, bt, sl, 0.088, num_splits=splits, workspace=ws)
+        ref = ops.decode_attention_ref(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), sl.cpu(), 0.088)
+        torch.testing.assert_close(out.cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("packed", [False, True])

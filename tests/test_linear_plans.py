@@ -43,8 +43,7 @@ def test_splitk_prefill_gate_cpu():
 
 def _check(mode, M=64, N=28672, K=4096, S=2, nw=2, cfg=1, part=1, counters=0, resid=0, ss=0):
     k = kernels()
-    return k.gemm_m64g_ex(1, M, K, 1, N, part, 1, S, mode, nw, cfg, 0, 0, 0, 1e-5, resid, ss, counters,
-                          0, 0, 0, 0, 0)
+    return k.gemm_m64g_ex(1, M, K, 1, N, part, 1, S, mode, nw, cfg, 0, 0, 0, 1e-5, resid, ss, counters, 0)
 
 
 def test_split_silu_needs_slabs_and_tickets():
@@ -54,9 +53,3 @@ def test_split_silu_needs_slabs_and_tickets():
         _check(L.MODE_SILU, part=0, counters=1)  # S > 1 without fp32 slabs
     with pytest.raises(Exception):
         _check(L.MODE_SILU, nw=1, counters=1)
-
-
-def test_coop_resid_rejects_grids_that_cannot_be_co_resident():
-    # 4096 columns / 64 per tile = 64 tiles x split 8 = 512 workgroups > 256 CUs
-    with pytest.raises(Exception):
-        _check(L.MODE_RESID_COOP, N=4096, K=14336, S=8, nw=1, cfg=0, counters=1, resid=1, ss=1)

@@ -38,13 +38,13 @@ from .tokenizer import IncrementalDetokenizer, load_tokenizer
 
 log = logging.getLogger("xgserve.engine")
 # split a step's emission: rows that cannot wait (finished, first tokens) before the
-# next step is planned, the rest in its overlap window (XGS_EMIT_SPLIT=0: all at once)
-EMIT_SPLIT = os.environ.get("XGS_EMIT_SPLIT", "1") != "0"
+# next step is planned, the rest in its overlap window (A/B in profiles/r2_async_mixed_ab.md)
+EMIT_SPLIT = True
 # Outputs emitted in a step's overlap window go to `output_sink` (the serving
 # replica's writer) right away instead of riding the step's return value, which
 # comes only after the GPU step in flight finishes (a whole step of delivery delay,
-# Req 5.1). XGS_EARLY_OUTPUTS=0: return them with the step.
-EARLY_OUTPUTS = os.environ.get("XGS_EARLY_OUTPUTS", "1") != "0"
+# Req 5.1). False: return them with the step (tests).
+EARLY_OUTPUTS = True
 
 _MASK63 = (1 << 63) - 1
 
@@ -78,13 +78,6 @@ class EngineConfig:
     max_prefill_seqs: int = 1 << 30
     # prefill tokens allowed in a step that also decodes (0: only the token budget)
     decode_prefill_cap: int = 0
-    # mixed steps that overshoot a multiple of align_tokens by <= align_slack tokens
-    # trim their last prompt chunk back to it (GEMM tile quantization; 0: off).
-    # Off by default: measured slower at 64 concurrent (6.03-6.04 vs 5.93-5.97
-    # ms/step, p50 TTFT 20 vs 14 ms; profiles/r2_align_ab.md) -- the trimmed prompt's
-    # eager follow-up step costs more than the 575 -> 512-row GEMM step saves.
-    align_tokens: int = 0
-    align_slack: int = 64
     # speculative decoding (Req 12)
     draft_model: Optional[str] = None
     num_speculative_tokens: int = 0
@@ -101,6 +94,9 @@ class EngineConfig:
     async_schedule: bool = True
     # "fp8": weight-only E4M3 copies for batch <= 16 decode (bf16 activations)
     weight_dtype: Optional[str] = None
+    # custom xGMI all-reduce peer-wait limit while serving: a TP peer this late fails
+    # the step (CustomAllReduceTimeout -> replica restart); warmup runs under 20 s
+    collective_timeout_s: float = 2.0
 
     def resolved_device(self) -> torch.device:
         if self.device:
@@ -145,12 +141,9 @@ class LLMEngine:
         sc.chunked_prefill = cfg.chunked_prefill
         sc.cache_threshold = cfg.cache_threshold
         sc.max_prefill_seqs = cfg.max_prefill_seqs
-        sc.decode_prefill_cap = int(os.environ.get("XGS_DECODE_PREFILL_CAP", cfg.decode_prefill_cap))
-        sc.align_tokens = int(os.environ.get("XGS_ALIGN_TOKENS", cfg.align_tokens))
-        sc.align_slack = int(os.environ.get("XGS_ALIGN_SLACK", cfg.align_slack))
-        # asynchronous scheduling over prompt steps + early release of length-finishing
-        # rows (XGS_ASYNC_MIXED=0: only pure-decode graph steps are looked ahead)
-        sc.lookahead_mixed = int(os.environ.get("XGS_ASYNC_MIXED", "1"))
+        sc.decode_prefill_cap = cfg.decode_prefill_cap
+        # asynchronous scheduling over prompt steps too (r2_async_mixed_ab.md)
+        sc.lookahead_mixed = 1
         # release length-finishing rows at lookahead (throughput) instead of a synchronous
         # step (TTFT of a request that arrives when they finish); XGS_EARLY_RELEASE=1
         sc.early_release = int(os.environ.get("XGS_EARLY_RELEASE", "0"))
@@ -172,6 +165,7 @@ class LLMEngine:
                                   max_num_seqs=cfg.max_num_seqs, max_num_batched_tokens=cfg.max_num_batched_tokens,
                                   max_model_len=self.max_model_len, use_graphs=use_graphs,
                                   graph_batch_sizes=graph_bs, is_driver=self.is_driver)
+        self.runner.collective_timeout_s = cfg.collective_timeout_s
         self.runner.capture_graphs()
         H = self.mcfg.hidden_size
         self.embed_acc = torch.zeros(cfg.max_num_seqs, H, dtype=torch.float32, device=self.device)

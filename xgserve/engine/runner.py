@@ -27,13 +27,12 @@ from ..models.base import AttnMeta
 from ..ops.attention import DecodeWorkspace
 from ..parallel import comm
 
-# eager (prompt) steps leave their sampled tokens on the device for a looked-ahead
-# successor (XGS_ASYNC_MIXED=0: only decode graph steps do)
-ASYNC_MIXED = os.environ.get("XGS_ASYNC_MIXED", "1") != "0"
+# eager (prompt) steps leave their sampled tokens on the device for a looked-ahead successor
+ASYNC_MIXED = True
 # host wait for a step's results: poll the event (default; XGS_SPIN_WAIT=0: a
-# blocking synchronize) for at most XGS_SPIN_MAX_MS before blocking (profiles/r2_spin_wait.md)
+# blocking synchronize) for at most 50 ms before blocking (profiles/r2_spin_wait.md)
 SPIN_WAIT = os.environ.get("XGS_SPIN_WAIT", "1") != "0"
-SPIN_MAX_S = float(os.environ.get("XGS_SPIN_MAX_MS", "50")) / 1000.0
+SPIN_MAX_S = 0.050
 
 log = logging.getLogger("xgserve.runner")
 
@@ -106,12 +105,18 @@ class ModelRunner:
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self._graph_pool = None
         self._init_graph_buffers()
+        # custom all-reduce peer-wait limit while serving (EngineConfig.collective_timeout_s);
+        # warmup, graph capture and the first WARM_LAUNCHES steps run under the warmup limit
+        self.collective_timeout_s = 2.0
+        self._warm_launches = self.WARM_LAUNCHES
+        from ..parallel.custom_ar import CustomAllReduce
+        self._set_comm_timeout(CustomAllReduce.WARMUP_TIMEOUT_S)
 
     # ------------------------------------------------------------------ utils
     def kv_bytes(self) -> int:
         return self.kv.numel() * self.kv.element_size()
 
-    DECODE_SPLIT_WGS = int(os.environ.get("XGS_DECODE_SPLIT_WGS", "512"))
+    DECODE_SPLIT_WGS = 512
 
     def decode_splits(self, bs: int) -> int:
         wgs = max(1, bs * self.Hkv)
@@ -164,6 +169,15 @@ class ModelRunner:
                                         self.g_seed[:bs], step=0)
             self.g_out_tok[:bs].copy_(tok)
             self.g_out_lp[:bs].copy_(lp)
+
+    # the first launches run under the generous peer-wait limit too (first-call RCCL
+    # communicator setup of a subgroup, first-seen library GEMM shapes)
+    WARM_LAUNCHES = 32
+
+    def _set_comm_timeout(self, seconds: float) -> None:
+        ar = comm.custom_allreduce()
+        if ar is not None:
+            ar.set_timeout(seconds)
 
     @torch.no_grad()
     def capture_graphs(self):
@@ -221,6 +235,10 @@ class ModelRunner:
         ns = int(plan["num_seqs"])
         if T == 0:
             return (0, None, (None, None, None), None)
+        if self._warm_launches:
+            self._warm_launches -= 1
+            if self._warm_launches == 0:
+                self._set_comm_timeout(self.collective_timeout_s)
         need_hidden = bool(plan["is_embed"].any()) if ns else False
         bucket = self._graph_bucket(Nd) if (Nd == ns and T == Nd and not need_hidden) else None
         if bucket is not None and self.graphs:
@@ -396,8 +414,12 @@ class ModelRunner:
             self.last_logits = logits.float().cpu()
         if not self.is_driver:
             if self.is_cuda:
+                # an event of THIS step: a follower that queued its successor waits
+                # for this launch only (engine.follower_loop), not the whole stream
                 self._poll_comm()
-                return (S, hid, None, None)
+                ev = torch.cuda.Event()
+                ev.record()
+                return (S, hid, None, None, False, ev)
             return (S, hid, (None, None, hid), None)
         if samp is None or samp.all_greedy:
             tok, lp = ops.argmax_logprob(logits)

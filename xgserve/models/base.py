@@ -2,9 +2,7 @@
 attention layer, and TP-sharded parameter helpers."""
 from __future__ import annotations
 
-import contextlib
 import math
-import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -13,23 +11,6 @@ import torch
 from .. import ops
 from ..ops.attention import DecodeWorkspace
 from ..parallel.state import get_state
-
-# Mixed prefill + decode steps: XGS_MIXED_ATTN_OVERLAP=1 runs the decode attention on
-# a side stream, concurrent with the prefill attention. Measured at 64 concurrent
-# (profiles/r2_mixed_attn_overlap.md): within noise (mixed steps 22.44 vs 22.09 ms
-# host wall, tok/s +-1 %), so off by default.
-MIXED_ATTN_OVERLAP = os.environ.get("XGS_MIXED_ATTN_OVERLAP", "0") == "1"
-_SIDE_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
-_nullctx = contextlib.nullcontext
-
-
-def _side_stream(device: torch.device) -> "torch.cuda.Stream":
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    s = _SIDE_STREAMS.get(idx)
-    if s is None:
-        s = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=idx)
-    return s
-
 
 @dataclass
 class AttnMeta:
@@ -102,15 +83,12 @@ class PagedAttention:
         return self.attend(q.view(T, self.Hq, self.D), meta, kv)
 
     def fused_decode(self, pend, meta: AttnMeta, kv: Tuple[torch.Tensor, torch.Tensor],
-                     cos_sin: torch.Tensor, prefetch: Optional[torch.Tensor] = None, defer_combine: bool = False):
+                     cos_sin: torch.Tensor) -> torch.Tensor:
         """Pure-decode step on QKV split-K partials: the attention kernel's prologue
-        reduces them, applies RoPE and appends K/V (ops.decode_attention_fused);
-        `prefetch` = the O projection weight, warmed into the Infinity Cache;
-        defer_combine: return the split partials (PendingAttn) for the O GEMM to merge."""
+        reduces them, applies RoPE and appends K/V (ops.decode_attention_fused)."""
         return ops.decode_attention_fused(pend, meta.positions, meta.slot_mapping, cos_sin, kv[0], kv[1],
                                           meta.dec_block_tables, meta.dec_seq_lens, self.Hq, self.scale,
-                                          meta.num_splits, meta.workspace, self.use_rope, prefetch=prefetch,
-                                          defer_combine=defer_combine)
+                                          meta.num_splits, meta.workspace, self.use_rope)
 
     def attend(self, q: torch.Tensor, meta: AttnMeta, kv: Tuple[torch.Tensor, torch.Tensor],
                out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -119,22 +97,14 @@ class PagedAttention:
         if out is None:
             out = torch.empty(T, self.Hq, self.D, dtype=q.dtype, device=q.device)
         nd = meta.num_decodes
-        side = None
-        if 0 < nd < T and MIXED_ATTN_OVERLAP and q.is_cuda and not torch.cuda.is_current_stream_capturing():
-            # mixed step: the decode rows' attention (memory-bound, split-K) runs on a
-            # side stream under the prefill chunk's attention (one workgroup per q tile,
-            # causal-imbalanced: the CUs of the light tiles idle otherwise)
-            side = _side_stream(q.device)
-            side.wait_stream(torch.cuda.current_stream(q.device))
+        # (decode rows' attention on a side stream under the prefill chunk's attention
+        # measured within noise, profiles/r2_mixed_attn_overlap.md)
         if nd > 0:
-            with torch.cuda.stream(side) if side is not None else _nullctx():
-                ops.decode_attention(q[:nd], kc, vc, meta.dec_block_tables, meta.dec_seq_lens, self.scale,
-                                     meta.num_splits, meta.workspace, out=out[:nd])
+            ops.decode_attention(q[:nd], kc, vc, meta.dec_block_tables, meta.dec_seq_lens, self.scale,
+                                 meta.num_splits, meta.workspace, out=out[:nd])
         if T > nd:
             ops.prefill_attention(q[nd:], kc, vc, meta.pre_block_tables, meta.pre_qsl, meta.pre_seq_lens,
                                   meta.pre_max_q, self.scale, out=out[nd:])
-        if side is not None:
-            torch.cuda.current_stream(q.device).wait_stream(side)
         return out.view(T, self.Hq * self.D)
 
 

@@ -34,11 +34,9 @@ from .. import ops
 from ..parallel import comm
 from ..parallel.state import get_state
 from ..ops import linear as linear_mod
-from ..ops.linear import (MODE_BF16, MODE_PARTIAL, MODE_SILU, SKINNY_MAX_M, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace,
-                          RowStats, m64_linear,
-                          m64_norm_linear, m64_plan, m64_resid_linear, m64_xa_linear, m64_xa_ok, pick_split,
-                          quantize_fp8, skinny_linear, splitk_linear, splitk_prefill_ok,
-                          w8_linear, w8_plan)
+from ..ops.linear import (MODE_PARTIAL, MODE_SILU, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace, RowStats, m64_linear,
+                          m64_norm_linear, m64_plan, m64_resid_linear, pick_split, quantize_fp8, skinny_linear,
+                          splitk_linear, splitk_prefill_ok, w8_linear, w8_plan)
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
 from .config import ModelConfig
 
@@ -55,8 +53,6 @@ FAST_M_SLAB = 64    # tokens per step for the O-projection slab kernel
 # statistics (comm.tp_allreduce_resid): 6 launches + attention per layer instead
 # of 11. XGS_FUSED_DECODE=0 restores the unfused chain (A/B measurements, tests).
 FUSED_DECODE = os.environ.get("XGS_FUSED_DECODE", "1") != "0"
-# MoE (Mixtral) layers on the fused decode layer (_fused_moe_tail); 0: the m64 chain
-FUSED_MOE_DECODE = os.environ.get("XGS_FUSED_MOE_DECODE", "1") != "0"
 # TP > 1 prefill-sized steps: the row-parallel all-reduces are pipelined over this
 # many token chunks and overlapped with the next chunk's GEMMs (RCCL stream); a
 # 2k-token 8B step moves 16 MiB per all-reduce -- ~100 us on 7 xGMI links, a
@@ -68,10 +64,7 @@ TP_OVERLAP_MIN_TOKENS = int(os.environ.get("XGS_TP_OVERLAP_MIN_TOKENS", "256"))
 EP_EXACT_MIN_PAIRS = int(os.environ.get("XGS_EP_EXACT_MIN_PAIRS", "256"))
 # moe_comm "auto": steps of at most this many tokens use the allreduce form when the
 # custom IPC all-reduce can take the [T, H] message
-EP_AR_MAX_TOKENS = int(os.environ.get("XGS_EP_AR_MAX_TOKENS", "64"))
-# LM head of decode-sized steps (<= 64 rows, TP=1) on gemm_m64g (bf16 epilogue)
-# instead of hipBLASLt (XGS_LMHEAD_M64=1; A/B in profiles/r2_lmhead_argmax.md)
-LMHEAD_M64 = os.environ.get("XGS_LMHEAD_M64", "0") == "1"
+EP_AR_MAX_TOKENS = 64
 
 
 @torch.no_grad()
@@ -310,10 +303,7 @@ class LlamaLayer(nn.Module):
         a = self.attn(qkv, meta, kv, cos_sin)
         if self.tp > 1 and not self.moe and T >= TP_OVERLAP_MIN_TOKENS and TP_OVERLAP_CHUNKS > 1:
             return self._forward_tp_overlap(a, residual)
-        if self.tp == 1 and linear_mod.SPLITK_O and splitk_prefill_ok(a, self.o, min_ratio=1):
-            o = splitk_linear(a, self.o, 2)  # partials reduced by the add + norm below
-        else:
-            o = self._ar(F.linear(a, self.o))
+        o = self._ar(F.linear(a, self.o))
         h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
         return self.mlp(h), residual
 
@@ -358,10 +348,7 @@ class LlamaLayer(nn.Module):
         returns the statistics of the new residual for the next layer."""
         eps = self.cfg.norm_eps
         pqkv = m64_norm_linear(resid, self.qkv, MODE_PARTIAL, stats, eps)
-        # small batches: the attention's split combine runs in the O GEMM's prologue
-        T = resid.shape[0]
-        xa = meta.num_splits > 1 and self.attn.D == 128 and m64_xa_ok(T, self.o.shape[0], self.o.shape[1])
-        a = self.attn.fused_decode(pqkv, meta, kv, cos_sin, prefetch=self.o, defer_combine=xa)
+        a = self.attn.fused_decode(pqkv, meta, kv, cos_sin)
         if self.moe:
             return self._fused_moe_tail(a, resid, ws, site)
         if self.tp > 1:
@@ -380,7 +367,7 @@ class LlamaLayer(nn.Module):
         T, H = resid.shape
         eps = self.cfg.norm_eps
         if self.tp > 1:
-            po = m64_linear(a, self.o, MODE_PARTIAL) if isinstance(a, torch.Tensor) else m64_xa_linear(a, self.o)
+            po = m64_linear(a, self.o, MODE_PARTIAL)
             comm.tp_allreduce_resid(po.part, resid, ws.ss[site])
         else:
             m64_resid_linear(a, self.o, resid, ws, site, eps)  # its statistics go unused: the router renorms
@@ -398,7 +385,7 @@ class LlamaLayer(nn.Module):
         all-reduce + residual + statistics (one launch) -> gate_up (norm row scale,
         SiLU-gate) -> down GEMM partials -> all-reduce + residual + statistics."""
         T, H = resid.shape
-        po = m64_linear(a, self.o, MODE_PARTIAL) if isinstance(a, torch.Tensor) else m64_xa_linear(a, self.o)
+        po = m64_linear(a, self.o, MODE_PARTIAL)
         comm.tp_allreduce_resid(po.part, resid, ws.ss[site])
         st = RowStats(ws.ss[site], H // 1024, T)
         act = m64_norm_linear(resid, self.gate_up, MODE_SILU, st, self.cfg.norm_eps)
@@ -432,7 +419,7 @@ class LlamaForCausalLM(nn.Module):
         self.norms_folded = False
         self.weight_dtype = "bf16"
         self._fused_ok = (self.device.type == "cuda" and l0.m64_ok and (l0.moe or l0.m64_silu_ok)
-                          and (FUSED_MOE_DECODE or not l0.moe) and cfg.head_dim == 128 and l0.Hq % l0.Hkv == 0
+                          and cfg.head_dim == 128 and l0.Hq % l0.Hkv == 0
                           and l0.Hq // l0.Hkv in (1, 2, 4, 8) and H % 1024 == 0 and H // 1024 <= 8)
         self._fused_small_ok = self._fused_ok and l0.m64_small_ok
         self._fused_ws = ResidWorkspace(2 * cfg.num_layers + 1, FAST_M_SLAB, H, device) if self._fused_ok else None
@@ -536,9 +523,6 @@ class LlamaForCausalLM(nn.Module):
 
     def compute_logits(self, h: torch.Tensor) -> torch.Tensor:
         w = self.embed if self.lm_head is None else self.lm_head
-        if (LMHEAD_M64 and self.tp == 1 and h.is_cuda and h.dtype == torch.bfloat16 and h.shape[0] <= 64
-                and h.is_contiguous() and m64_plan(h.shape[0], w.shape[0], w.shape[1], MODE_BF16)):
-            return m64_linear(h, w, MODE_BF16)[:, :self.cfg.vocab_size]
         logits = F.linear(h, w)
         if self.tp > 1:
             logits = comm.tp_all_gather_lastdim(logits)

@@ -2,30 +2,12 @@
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import Optional
 
 import torch
 
 from ._native import kernels, stream_ptr, use_native
-
-# split-K decode: the last-arriving split merges in-launch instead of a combine launch
-# (XGS_DECODE_INLAUNCH_COMBINE=1). A first form with a dependent per-split merge loop
-# measured slower on MI355X (8B batch 1: 4.14 vs 3.89 ms/step); the current one stores
-# the slabs write-through and merges with batched loads (combine_splits): correct, and
-# still 0.4-1.6 % slower than the graph-captured combine launch at batch 1 / 8 / 64
-# (profiles/r1_inlaunch_combine_ab.md), so the separate launch stays the default.
-IN_KERNEL_COMBINE = os.environ.get("XGS_DECODE_INLAUNCH_COMBINE", "0") == "1"
-# Small-batch decode (opt-in, XGS_ATTN_PREFETCH=1): extra workgroups of the fused
-# attention launch read the O projection's weights into the Infinity Cache while the
-# latency-bound attention runs. Measured slower (8B batch 1 +3 %, batch 8 +7 %, 70B
-# batch 1 +10 % ms/step, profiles/r1_attn_prefetch_ab.md): the launch now ends only
-# when its prefetch share has streamed, which costs more than the O GEMM saves.
-ATTN_PREFETCH = os.environ.get("XGS_ATTN_PREFETCH", "0") == "1"
-ATTN_PREFETCH_MAX_B = int(os.environ.get("XGS_ATTN_PREFETCH_MAX_B", "8"))
-ATTN_PREFETCH_WGS = int(os.environ.get("XGS_ATTN_PREFETCH_WGS", "128"))
-
 
 def choose_num_splits(batch: int, num_kv_heads: int, max_seq_len: int, num_cus: int = 256) -> int:
     """Split-K factor so the decode grid has >= ~2 workgroups per CU, but every
@@ -88,23 +70,6 @@ def prefill_attention_ref(q, k_cache, v_cache, block_tables, query_start_loc, se
     return out
 
 
-@dataclass
-class PendingAttn:
-    """Decode attention output still in split-K form (the combine launch skipped):
-    part_out [B, Hq, S, D] normalised partial outputs, part_lse [B, Hq, S]. The O
-    projection merges it in its prologue (ops.linear m64 XA form)."""
-    part_out: torch.Tensor
-    part_lse: torch.Tensor
-    S: int
-    B: int
-    Hq: int
-    D: int
-
-    @property
-    def shape(self):
-        return (self.B, self.Hq * self.D)
-
-
 class DecodeWorkspace:
     """Split-K partial buffers, sized once (graph-capture safe)."""
 
@@ -112,9 +77,6 @@ class DecodeWorkspace:
         self.part_out = torch.empty(max_batch * num_q_heads * max_splits * head_dim, dtype=torch.float32,
                                     device=device)
         self.part_lse = torch.empty(max_batch * num_q_heads * max_splits, dtype=torch.float32, device=device)
-        # arrival tickets of the in-launch split combine ([B, Hkv] <= [B, Hq]); the last
-        # split of each (sequence, kv head) re-zeroes its ticket
-        self.counters = torch.zeros(max_batch * num_q_heads, dtype=torch.int32, device=device)
         self.max_splits = max_splits
 
 
@@ -140,13 +102,12 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         if workspace is None or workspace.max_splits < num_splits or workspace.part_lse.numel() < B * Hq * num_splits:
             workspace = DecodeWorkspace(B, Hq, D, num_splits, q.device)
         po, pl = workspace.part_out.data_ptr(), workspace.part_lse.data_ptr()
-        cnt = workspace.counters.data_ptr() if IN_KERNEL_COMBINE else 0
     else:
-        po = pl = cnt = 0
+        po = pl = 0
     kernels().decode_attention(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                block_tables.data_ptr(), block_tables.stride(0), seq_lens.data_ptr(), po, pl,
                                out.data_ptr(), out.stride(0), B, Hq, Hkv, D, bs, float(scale), int(num_splits),
-                               cnt, stream_ptr())
+                               stream_ptr())
     return out
 
 
@@ -154,49 +115,30 @@ def decode_attention_fused(pend, positions: torch.Tensor, slot_mapping: torch.Te
                            k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                            seq_lens: torch.Tensor, num_heads: int, scale: float, num_splits: int = 1,
                            workspace: Optional[DecodeWorkspace] = None, apply_rope: bool = True,
-                           out: Optional[torch.Tensor] = None,
-                           prefetch: Optional[torch.Tensor] = None, defer_combine: bool = False):
+                           out: Optional[torch.Tensor] = None):
     """Paged decode attention on the QKV projection's split-K partials (PendingSum
     [S, B, (Hq + 2 Hkv) D]): each workgroup's prologue reduces its (sequence, kv
     head) slice, applies RoPE and appends the new K/V row to the cache -- the work
-    of rope_cache_partials without its launch or the q round trip. -> [B, Hq * D].
-    `prefetch` (the next GEMM's weight): read into the Infinity Cache by extra
-    workgroups of the same launch when B <= ATTN_PREFETCH_MAX_B. defer_combine with
-    num_splits > 1: no combine launch, returns a PendingAttn for the O GEMM."""
+    of rope_cache_partials without its launch or the q round trip. -> [B, Hq * D]."""
     S, B, W = pend.part.shape
     Hkv, bs, D = k_cache.shape[1], k_cache.shape[2], k_cache.shape[3]
     Hq = num_heads
     assert W == (Hq + 2 * Hkv) * D and pend.part.is_contiguous()
     assert block_tables.dtype == torch.int32 and seq_lens.dtype == torch.int32 and block_tables.stride(1) == 1
     assert positions.dtype == torch.int32 and slot_mapping.dtype == torch.int32 and cos_sin.dtype == torch.float32
-    defer = defer_combine and num_splits > 1 and not IN_KERNEL_COMBINE
-    if out is None and not defer:
+    if out is None:
         out = torch.empty(B, Hq * D, dtype=torch.bfloat16, device=pend.part.device)
-    po = pl = cnt = 0
+    po = pl = 0
     if num_splits > 1:
         if workspace is None or workspace.max_splits < num_splits or workspace.part_lse.numel() < B * Hq * num_splits:
             workspace = DecodeWorkspace(B, Hq, D, num_splits, pend.part.device)
         po, pl = workspace.part_out.data_ptr(), workspace.part_lse.data_ptr()
-        cnt = workspace.counters.data_ptr() if IN_KERNEL_COMBINE else 0
-    pf, pf_bytes, pf_slices = 0, 0, 0
-    if prefetch is not None and ATTN_PREFETCH and B <= ATTN_PREFETCH_MAX_B and prefetch.is_contiguous():
-        pf, pf_bytes = prefetch.data_ptr(), prefetch.numel() * prefetch.element_size()
-        skip = -pf % 16  # 16-B lanes start aligned
-        pf, pf_bytes = pf + skip, pf_bytes - skip
-        pf_slices = max(1, -(-ATTN_PREFETCH_WGS // (Hkv * B)))
     kernels().decode_attention_fq(pend.part.data_ptr(), S, positions.data_ptr(), cos_sin.data_ptr(),
                                   slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                   block_tables.data_ptr(), block_tables.stride(0), seq_lens.data_ptr(), po, pl,
-                                  0 if defer else out.data_ptr(), 0 if defer else out.stride(0), B, Hq, Hkv, D, bs,
-                                  float(scale), int(num_splits), 1 if apply_rope else 0, cnt, pf, pf_bytes, pf_slices,
-                                  stream_ptr())
-    if defer:
-        return PendingAttn(workspace.part_out, workspace.part_lse, int(num_splits), B, Hq, D)
+                                  out.data_ptr(), out.stride(0), B, Hq, Hkv, D, bs, float(scale), int(num_splits),
+                                  1 if apply_rope else 0, stream_ptr())
     return out
-
-
-# query heads of one GQA group per prefill workgroup (0: kernel default, 2 for even groups)
-PREFILL_GH = int(os.environ.get("XGS_PREFILL_GH", "0"))
 
 
 def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
@@ -219,5 +161,5 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
     kernels().prefill_attention(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                                 block_tables.data_ptr(), block_tables.stride(0), query_start_loc.data_ptr(),
                                 seq_lens.data_ptr(), out.data_ptr(), out.stride(0), S, int(max_q_len), Hq, Hkv, D,
-                                bs, float(scale), stream_ptr(), PREFILL_GH if gh is None else int(gh))
+                                bs, float(scale), stream_ptr(), 0 if gh is None else int(gh))
     return out

@@ -190,16 +190,11 @@ def m64_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL):
     return nw, S, 0
 
 
-# 4: LDS-DMA staging (gemm_m64g.hip, fastest on every measured shape); 0-3: register-ring gemm_m64
-# (bit0: two W chunks in flight; bit1: default cache policy for W, else non-temporal)
-M64_VARIANT = 4
-
-
 def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split_k: Optional[int] = None,
-               nw: Optional[int] = None, out: Optional[torch.Tensor] = None, variant: Optional[int] = None,
-               cfg: Optional[int] = None):
-    """gemm_m64 (csrc/kernels/gemm_m64.hip) for 16 < M <= 64: bf16 [M, N], PendingSum
-    (MODE_PARTIAL) or silu(gate)*up [M, N/2] (MODE_SILU, interleaved gate|up weight)."""
+               nw: Optional[int] = None, out: Optional[torch.Tensor] = None, cfg: Optional[int] = None):
+    """gemm_m64g (csrc/kernels/gemm_m64g.hip, LDS-DMA weight streaming) for M <= 64:
+    bf16 [M, N], PendingSum (MODE_PARTIAL) or silu(gate)*up [M, N/2] (MODE_SILU,
+    interleaved gate|up weight)."""
     M, K = x.shape
     N = w.shape[0]
     plan = m64_plan(M, N, K, mode)
@@ -213,15 +208,10 @@ def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split
         cfg = plan[2] if cfg is None else cfg
         if not _m64_valid(N, K, mode, nw, S, cfg):
             cfg = 0
-    var = M64_VARIANT if variant is None else variant
     k = kernels()
     if mode == MODE_PARTIAL:
         part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
-        if var == 4:  # LDS-DMA staging (gemm_m64g.hip)
-            k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg,
-                        stream_ptr())
-        else:
-            k.gemm_m64(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, var, stream_ptr())
+        k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg, stream_ptr())
         return PendingSum(part, S)
     ncol = N // 2 if mode == MODE_SILU else N
     if out is None:
@@ -229,30 +219,23 @@ def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split
     if mode == MODE_SILU and S > 1:  # split-K SiLU: slabs + tile tickets, reduced in the GEMM tail
         part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
         k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), out.data_ptr(), S, mode, nw, cfg,
-                       0, 0, 0, 0.0, 0, 0, tile_counters(x.device, N).data_ptr(), stream_ptr(), 0, 0, 0, 0)
-    elif var == 4:
-        k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, cfg, stream_ptr())
+                       0, 0, 0, 0.0, 0, 0, tile_counters(x.device, N).data_ptr(), stream_ptr())
     else:
-        k.gemm_m64(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, var, stream_ptr())
+        k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, cfg, stream_ptr())
     return out
 
 
 # ---------------------------------------------------------------------------- fused decode layer
 MODE_RESID = 3
-MODE_RESID_COOP = 4
-# XGS_RESID_COOP=1: slabs above RESID_INLAUNCH_MAX_BYTES are reduced inside the GEMM
-# launch cooperatively (every split workgroup of a column tile reduces M / S rows
-# after the tile's splits meet; needs the whole grid co-resident, <= 256 workgroups)
-# instead of by the separate add_partials_resid launch. Measured slower (8B 64
-# concurrent 6.34-6.40 vs 5.88-5.92 ms/step: each tile waits for its slowest split
-# with its CUs held; profiles/r2_resid_coop.md), so off by default.
-RESID_COOP = __import__("os").environ.get("XGS_RESID_COOP", "0") == "1"
+# (A cooperative in-launch reduce of the larger slabs -- every split workgroup of a
+# tile reducing M / S rows after the splits meet -- measured 2-8 % slower end to end,
+# profiles/r2_resid_coop.md, and was removed.)
 # GG_RESID (residual add + next-norm statistics inside the GEMM launch) reduces a
 # column tile in-launch while its split-K slab (S x M x columns fp32) is at most
 # this many bytes -- the tile's last arriver reads it serially (~1 us per 16 KB,
 # cdna_hip_programming.md §5); larger slabs (M ~ 64) go through the wide
 # add_partials_resid kernel instead.
-RESID_INLAUNCH_MAX_BYTES = int(__import__("os").environ.get("XGS_RESID_INLAUNCH_MAX_BYTES", str(32 << 10)))
+RESID_INLAUNCH_MAX_BYTES = 32 << 10
 
 
 @dataclass
@@ -276,42 +259,9 @@ class ResidWorkspace:
         self.max_m = max_m
         rows = max(self.MAX_TILES * self.IN_LAUNCH_MAX_M, max(1, H // 1024) * max_m)
         self.ss = torch.zeros(n_sites, rows, dtype=torch.float32, device=device)
-        # arrival tickets (GG_RESID: one word per tile; GG_RESID_COOP: arrive / depart
-        # pairs): zero here, and every launch re-arms the words it used
+        # arrival tickets (GG_RESID: one word per tile): zero here, and every launch
+        # re-arms the words it used
         self.counters = torch.zeros(n_sites, 2 * self.MAX_TILES, dtype=torch.int32, device=device)
-
-
-# Attention split-combine folded into the O projection (gemm_m64g XA prologue) for
-# pure-decode steps of at most this many rows (XGS_XA_MAX_M; 0 = off, the default).
-# Measured slower (8B batch 1: 3.297 vs 3.265 ms/step, batch 8: 3.76 vs 3.56;
-# profiles/r2_xa_ab.md): every one of the O GEMM's column-tile workgroups re-reads
-# the split slabs of its heads (64 KB at 16 splits, 16 MB per launch) before its
-# weight stream can retire, which costs more than the combine launch it removes.
-import os as _os
-XA_MAX_M = int(_os.environ.get("XGS_XA_MAX_M", "0"))
-
-
-def m64_xa_ok(M: int, N: int, K: int) -> bool:
-    """Can gemm_m64g take x as attention split partials at this shape? One-x-tile
-    kernel (M <= 16, not the 4-wave KC-64 configs), whole 128-dim heads per K slice,
-    slice <= 1024 columns (the LDS x image)."""
-    if not (1 <= M <= min(16, XA_MAX_M)):
-        return False
-    p = m64_plan(M, N, K, MODE_PARTIAL)
-    if p is None:
-        return False
-    nw, S, cfg = p
-    kws = K // S
-    return cfg not in (2, 3) and kws % 128 == 0 and kws <= 1024
-
-
-def _xa(x):
-    """(x pointer, M, K, att_po, att_lse, att_splits, att_hq) for a tensor or a PendingAttn."""
-    from .attention import PendingAttn
-    if isinstance(x, PendingAttn):
-        return 0, x.B, x.Hq * x.D, x.part_out.data_ptr(), x.part_lse.data_ptr(), x.S, x.Hq
-    M, K = x.shape
-    return x.data_ptr(), M, K, 0, 0, 0, 0
 
 
 # Prefill-sized down projections (K = 3.5 N) have too few output tiles for the chip at
@@ -319,8 +269,8 @@ def _xa(x):
 # fp32 outputs doubles them and its partials are reduced for free by the consumer
 # (add_partials_rmsnorm). bench/splitk_prefill_bench.py, profiles/r2_splitk_prefill.md:
 # 8B down at M 575 87.8 -> 70.3 us (+3.3 us of fp32 slab traffic in the consumer).
-SPLITK_PREFILL_MAX_M = int(_os.environ.get("XGS_SPLITK_PREFILL_MAX_M", "1536"))
-SPLITK_PREFILL_S = int(_os.environ.get("XGS_SPLITK_PREFILL_S", "4"))
+SPLITK_PREFILL_MAX_M = 1536
+SPLITK_PREFILL_S = 4
 
 
 def splitk_linear(x: torch.Tensor, w: torch.Tensor, S: int) -> PendingSum:
@@ -331,11 +281,6 @@ def splitk_linear(x: torch.Tensor, w: torch.Tensor, S: int) -> PendingSum:
     a = x.view(M, S, K // S).permute(1, 0, 2)
     b = w.view(N, S, K // S).permute(1, 2, 0)
     return PendingSum(torch.bmm(a, b, out_dtype=torch.float32), S)
-
-
-# XGS_SPLITK_O=1: the O projection of prefill-sized steps too (K = N). Measured within noise
-# at 64 concurrent (3 pairs: 11,304-11,472 vs 11,381-11,412 tok/s, profiles/r2_splitk_prefill.md)
-SPLITK_O = _os.environ.get("XGS_SPLITK_O", "0") == "1"
 
 
 def splitk_prefill_ok(x: torch.Tensor, w: torch.Tensor, min_ratio: int = 3) -> bool:
@@ -378,17 +323,17 @@ def m64_norm_linear(x: torch.Tensor, w: torch.Tensor, mode: int, stats: RowStats
     if mode == MODE_PARTIAL:
         part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
         k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg, *st,
-                       0, 0, 0, stream_ptr(), 0, 0, 0, 0)
+                       0, 0, 0, stream_ptr())
         return PendingSum(part, S)
     if out is None:
         out = torch.empty(M, N // 2 if mode == MODE_SILU else N, dtype=torch.bfloat16, device=x.device)
     if mode == MODE_SILU and S > 1:  # split-K SiLU: slabs + tile tickets, reduced in the GEMM tail
         part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
         k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), out.data_ptr(), S, mode, nw, cfg, *st,
-                       0, 0, tile_counters(x.device, N).data_ptr(), stream_ptr(), 0, 0, 0, 0)
+                       0, 0, tile_counters(x.device, N).data_ptr(), stream_ptr())
         return out
     k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, cfg, *st, 0, 0, 0,
-                   stream_ptr(), 0, 0, 0, 0)
+                   stream_ptr())
     return out
 
 
@@ -397,8 +342,9 @@ def m64_resid_linear(x, w: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace
     """resid += x . w^T (bf16 residual stream, in place) on gemm_m64g; returns the
     new residual's RMSNorm statistics. Small split-K slabs are reduced inside the
     GEMM launch (GG_RESID), large ones by the wide add_partials_resid kernel.
-    x: bf16 [M, K] or a PendingAttn (split attention merged in the GEMM prologue)."""
-    xp, M, K, apo, alse, asp, ahq = _xa(x)
+    x: bf16 [M, K]."""
+    M, K = x.shape
+    xp = x.data_ptr()
     N = w.shape[0]
     plan = m64_plan(M, N, K, MODE_PARTIAL)
     if plan is None or N % 1024 or tuple(resid.shape) != (M, N):
@@ -412,29 +358,11 @@ def m64_resid_linear(x, w: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace
     if (S * M * cols * 4 <= RESID_INLAUNCH_MAX_BYTES and ntiles <= ws.MAX_TILES
             and M <= ws.IN_LAUNCH_MAX_M):
         k.gemm_m64g_ex(xp, M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_RESID, nw, cfg, 0, 0, 0,
-                       float(eps), resid.data_ptr(), ss.data_ptr(), ws.counters[site].data_ptr(), stream_ptr(),
-                       apo, alse, asp, ahq)
+                       float(eps), resid.data_ptr(), ss.data_ptr(), ws.counters[site].data_ptr(), stream_ptr())
         return RowStats(ss, ntiles, M)  # one partial sum per column tile
-    if RESID_COOP and S > 1 and ntiles * S <= 256 and ntiles <= ws.MAX_TILES and M <= ws.IN_LAUNCH_MAX_M:
-        k.gemm_m64g_ex(xp, M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_RESID_COOP, nw, cfg, 0, 0, 0,
-                       float(eps), resid.data_ptr(), ss.data_ptr(), ws.counters[site].data_ptr(), stream_ptr(),
-                       apo, alse, asp, ahq)
-        return RowStats(ss, ntiles, M)
-    k.gemm_m64g_ex(xp, M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg, 0, 0, 0, 0.0, 0, 0, 0,
-                   stream_ptr(), apo, alse, asp, ahq)
+    k.gemm_m64g(xp, M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg, stream_ptr())
     k.add_partials_resid(part.data_ptr(), S, M, resid.data_ptr(), ss.data_ptr(), N, stream_ptr())
     return RowStats(ss, N // 1024, M)  # one partial sum per 1024-column chunk
-
-
-def m64_xa_linear(x, w: torch.Tensor) -> PendingSum:
-    """PendingSum of x . w^T where x is a PendingAttn (row-parallel O projection under TP)."""
-    xp, M, K, apo, alse, asp, ahq = _xa(x)
-    N = w.shape[0]
-    nw, S, cfg = m64_plan(M, N, K, MODE_PARTIAL)
-    part = torch.empty(S, M, N, dtype=torch.float32, device=w.device)
-    kernels().gemm_m64g_ex(xp, M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg, 0, 0, 0, 0.0, 0,
-                           0, 0, stream_ptr(), apo, alse, asp, ahq)
-    return PendingSum(part, S)
 
 
 def interleave_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:

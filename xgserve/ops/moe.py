@@ -9,28 +9,20 @@ from ._native import kernels, stream_ptr, use_native
 from .activation import silu_and_mul
 
 BLOCK_M = 64
-MOE_GLDS = True  # expert GEMMs on the LDS-DMA pipeline (gemm_m64g.hip); False: register-ring gemm_m64
 # gemm_m64g launch configurations for the expert GEMMs (see ops/linear.py M64G_CFGS);
 # measured with bench/gemm_bench.py --moe-sweep
 # (Mixtral 8x7B; profiles/r1_moe_sweep_v2.jsonl, per-row-tile grid + MT=1: w13 cfg 5 = 324 us at
 # T=64 (cfg 3: 338), 81 us at T=1; w2 nw 2 + cfg 1 = 153 us at T=64)
 MOE_CFG_W13 = 5  # (2 waves, KC 64, nt): best at T = 1..64 with the per-row-tile grid (bench --moe-sweep)
 MOE_CFG_W2 = 1
-# Optional prefill MoE path (>= this many (token, expert) pairs, eager steps only):
-# read the expert offsets to the host (one small sync) and run each expert's rows
-# as two hipBLASLt GEMMs around the SiLU-gate kernel. Off by default: measured on
-# Mixtral 64-concurrent the grouped m64g kernel (one workgroup per 64-row tile,
-# an expert's tiles sharing its weight stream through L2/MALL) is faster
-# (2,680 vs 2,638 tok/s); XGS_MOE_DENSE_MIN_PAIRS=256 turns it on.
-import os as _os
-MOE_ROW_DISPATCH = _os.environ.get("XGS_MOE_ROW_DISPATCH", "1") != "0"
-MOE_DENSE_MIN_PAIRS = int(_os.environ.get("XGS_MOE_DENSE_MIN_PAIRS", str(1 << 30)))
 # prefill-sized steps (> 256 token-expert pairs): w2 on a KC-64 config so the grouped
 # kernel can run 128-row tile pairs (each expert's weights streamed once per 128 rows
-# instead of per 64; XGS_M64G_MT8=0 turns the pairs off, and w13's cfg 5 is KC 64)
+# instead of per 64; profiles/r2_moe_pairs_ab.md). A per-expert hipBLASLt path for
+# these steps measured slower than the grouped kernel (2,638 vs 2,680 tok/s) and was
+# removed.
 MOE_PREFILL_PAIRS = 256
-MOE_CFG_W2_PREFILL = int(_os.environ.get("XGS_MOE_CFG_W2_PREFILL", "3"))
-MOE_CFG_W13_PREFILL = int(_os.environ.get("XGS_MOE_CFG_W13_PREFILL", "3"))
+MOE_CFG_W2_PREFILL = 3
+MOE_CFG_W13_PREFILL = 3
 
 
 def moe_topk_softmax(router_logits: torch.Tensor, k: int, renorm: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -150,27 +142,20 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     F = F2 // 2
     sorted_rows, offs, dest = moe_align(topk_ids, E, expert_offset)
     P = sorted_rows.shape[0]
-    if T * k >= MOE_DENSE_MIN_PAIRS and not torch.cuda.is_current_stream_capturing() and resid is None:
-        return _moe_per_expert(x, w13, w2, topk_w, sorted_rows, offs, dest, T, k)
     act = torch.empty(P, F, dtype=x.dtype, device=x.device)
     kn = kernels()
-    if MOE_GLDS:
-        max_rows = T * k  # no expert holds more rows than (token, choice) pairs
-        # per-workgroup real-row count -> 16 / 32 / 64-row body (MOE_ROW_DISPATCH=0: always 64)
-        valid = sorted_rows.data_ptr() if MOE_ROW_DISPATCH else 0
+    max_rows = T * k  # no expert holds more rows than (token, choice) pairs
+    valid = sorted_rows.data_ptr()  # per-workgroup real-row count -> 16 / 32 / 64-row body
 
-        def gemm(*a, cfg=0):
-            kn.moe_gemm_m64g_rows(*a[:-1], cfg, max_rows, a[-1], valid)
-    else:
-        def gemm(*a, cfg=0):
-            kn.moe_gemm_m64(*a)
+    def gemm(*a, cfg=0):
+        kn.moe_gemm_m64g_rows(*a[:-1], cfg, max_rows, a[-1], valid)
     cfg13 = ((MOE_CFG_W13_PREFILL if T * k > MOE_PREFILL_PAIRS else MOE_CFG_W13)
-             if (MOE_GLDS and H % (64 * 1) == 0 and F2 % 128 == 0) else 0)
+             if (H % 64 == 0 and F2 % 128 == 0) else 0)
     gemm(x.contiguous().data_ptr(), sorted_rows.data_ptr(), offs.data_ptr(), E, H, w13.data_ptr(), F2, P, 0,
          act.data_ptr(), 1, 2, 2, stream_ptr(), cfg=cfg13)
     # w2 has only H/128 column tiles per expert: split K while few experts are active
     nw2 = 2 if H % 128 == 0 else 1
-    cfg2 = (MOE_CFG_W2_PREFILL if T * k > MOE_PREFILL_PAIRS else MOE_CFG_W2) if MOE_GLDS and nw2 == 2 else 0
+    cfg2 = (MOE_CFG_W2_PREFILL if T * k > MOE_PREFILL_PAIRS else MOE_CFG_W2) if nw2 == 2 else 0
     kc2 = 128
     S = 1
     for sk in ((4, 2) if T * k <= 4 else (2,) if T * k <= 16 else ()):
@@ -190,28 +175,6 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     return out
 
 
-def _moe_per_expert(x, w13, w2, topk_w, sorted_rows, offs, dest, T, k):
-    """Prefill-sized MoE: per active expert, its padded row segment (rows gathered
-    from x; pad rows read row 0 and are never combined) -> hipBLASLt gate_up ->
-    SiLU-gate -> hipBLASLt down -> fp32 slab row segment -> the same combine."""
-    E, F2, H = w13.shape
-    P = sorted_rows.shape[0]
-    o = offs.tolist()  # host sync: E + 1 ints
-    xs = x.index_select(0, sorted_rows.clamp(min=0).long())
-    part = torch.empty(1, P, H, dtype=torch.float32, device=x.device)
-    for e in range(E):
-        a, b = o[e], o[e + 1]
-        if b <= a:
-            continue
-        act = silu_and_mul(torch.mm(xs[a:b], w13[e].t()), interleave16=True)
-        part[0, a:b].copy_(torch.mm(act, w2[e].t()))
-    out = torch.empty(T, H, dtype=x.dtype, device=x.device)
-    kernels().moe_combine(part.data_ptr(), 1, P, dest.data_ptr(), topk_w.float().contiguous().data_ptr(),
-                          out.data_ptr(), T, k, H, stream_ptr())
-    return out
-
-
-# ---------------------------------------------------------------------------- expert parallel
 def ep_plan(ids: torch.Tensor, E_local: int, tp: int, cap: int, packed: bool):
     """Dispatch plan for expert parallelism (csrc/kernels/moe.hip ep_plan): pair
     i = (t, j) of ids [Ts, k] goes to rank d = ids[i] // E_local at a stable slot

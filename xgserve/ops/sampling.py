@@ -1,7 +1,6 @@
 """K9 sampling + K11 pooling helpers."""
 from __future__ import annotations
 
-import os
 from typing import Optional, Tuple
 
 import torch
@@ -84,9 +83,9 @@ def sample_tokens(logits: torch.Tensor, temps: torch.Tensor, top_ps: Optional[to
 
 
 # Split-row sampler (csrc/kernels/sampling.hip "sample v2": several workgroups per row,
-# histogram thresholds instead of a 24-pass bisection); XGS_SAMPLE_SPLIT=0 selects the
-# one-workgroup-per-row kernel (A/B in profiles/r2_sampling.md).
-SAMPLE_SPLIT = os.environ.get("XGS_SAMPLE_SPLIT", "1") != "0"
+# histogram thresholds instead of a 24-pass bisection); False selects the
+# one-workgroup-per-row kernel (the tests' cross-check; A/B in profiles/r2_sampling.md).
+SAMPLE_SPLIT = True
 _SAMPLE_WS = {}
 
 

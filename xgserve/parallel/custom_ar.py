@@ -19,11 +19,16 @@ bf16 contributions over IPC, adds the sum to the replicated residual stream and
 writes the new residual's RMSNorm statistics (custom_allreduce_resid). It has
 its own slots, signals and generation counters.
 
-Failure semantics: a peer that does not arrive within ~1 s makes the kernels
-bump a device error counter and give up (the GPU never hangs). After every
-step the runner copies that counter to pinned host memory behind the step's
-work (`poll_async`) and `check()` raises CustomAllReduceTimeout, so the step
-fails (and the replica restarts) instead of returning a stale sum.
+Failure semantics: a peer that does not arrive within the wait limit makes the
+kernels bump a device error counter and give up (the GPU never hangs); once the
+counter is non-zero every later wait returns at once, so a dead peer costs one
+limit per step, not one per collective. The limit is a device word read by every
+launch (graph replays included): `set_timeout` makes it generous around warmup
+and graph capture (first-call RCCL setup, first-seen GEMM shapes) and sets the
+configured collective timeout for serving. After every step the runner copies
+the counter to pinned host memory behind the step's work (`poll_async`) and
+`check()` raises CustomAllReduceTimeout, so the step fails (and the replica
+restarts) instead of returning a stale sum.
 """
 from __future__ import annotations
 
@@ -47,6 +52,9 @@ class CustomAllReduce:
     RESID_SLOT = 1 << 20
     # last-dim all-gather (vocab-parallel LM head of decode steps): T * V/W bf16 per rank
     GATHER_SLOT = 16 << 20
+    # peer-wait limits: while serving, and around warmup / graph capture
+    SERVE_TIMEOUT_S = 2.0
+    WARMUP_TIMEOUT_S = 20.0  # (the 32-bit tick word caps the limit at ~21 s at 100 MHz)
 
     def __init__(self, rank: int, world: int, device: torch.device, cpu_group=None, max_bytes: int = 8 << 20,
                  two_shot_min: Optional[int] = None, two_shot_max: int = 32 << 20):
@@ -116,9 +124,14 @@ class CustomAllReduce:
         self.gens2 = torch.zeros(self.max_blocks + 1, dtype=torch.int32, device=device)
         self.gens3 = torch.zeros(self.max_blocks + 1, dtype=torch.int32, device=device)
         self.gens4 = torch.zeros(self.max_blocks + 1, dtype=torch.int32, device=device)
-        # peer-wait timeouts of every path (device), mirrored to pinned host memory
-        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        # ctl[0]: peer-wait timeouts of every path (device), mirrored to pinned host
+        # memory; ctl[1]: the wait limit in wall-clock ticks (set_timeout)
+        self.ctl = torch.zeros(2, dtype=torch.int32, device=device)
+        self.err = self.ctl[:1]
         self.h_err = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self._khz = max(1, int(k.car_wallclock_khz()) or 100_000)
+        self.timeout_s = 0.0
+        self.set_timeout(self.SERVE_TIMEOUT_S)
         log.info("custom all-reduce ready: rank %d/%d, one-shot <= %d KiB, two-shot <= %d MiB", rank, world,
                  min(self.slot, self.two_shot_min) >> 10, self.slot2 >> 20)
 
@@ -175,6 +188,16 @@ class CustomAllReduce:
                                          self.data_ptrs4, self.sig_ptrs4, self.rank, self.gens4.data_ptr(),
                                          self.err.data_ptr(), stream_ptr())
         return out
+
+    def set_timeout(self, seconds: float) -> None:
+        """Peer-wait limit of every later launch (stream-ordered; captured graphs read
+        the word at replay). Clamped to the 32-bit tick range."""
+        ticks = int(min(max(seconds, 1e-3) * self._khz * 1000, 0x7FFFFFFF))
+        self.ctl[1].fill_(ticks)
+        self.timeout_s = float(seconds)
+
+    def reset_errors(self) -> None:
+        self.err.zero_()
 
     def timeouts(self) -> int:
         """Peer-wait timeouts recorded by the kernels (0 when healthy). Synchronises."""

@@ -689,43 +689,59 @@ class InferenceServer:
             return {"previous_model": old_name, "model": self.model_name, "replicas": ids}
 
     def _free_gpus(self, n: int) -> List[int]:
-        """The n lowest GPU indices no live process replica holds (the configured
-        `worker.gpus` list first, if any)."""
+        """The n lowest GPU indices no live process replica holds, taken from the
+        configured `worker.gpus` list, else from the GPUs this node has (mock
+        replicas touch no GPU: any index). ConfigError when fewer are free."""
         used = {g for r in self.replicas.values() for g in (getattr(r, "gpus", None) or [])}
-        pool = self._gpu_list(self.cfg.worker) if self.cfg.worker.gpus else []
+        w = self.cfg.worker
+        if w.gpus:
+            pool = self._gpu_list(w)
+        elif w.mock:
+            pool = list(range(len(used) + n))
+        else:
+            import torch  # device_count() does not initialise the GPU in this process
+            pool = list(range(torch.cuda.device_count()))
         cand = [g for g in pool if g not in used]
-        g = 0
-        while len(cand) < n:
-            if g not in used and g not in cand:
-                cand.append(g)
-            g += 1
+        if len(cand) < n:
+            raise ConfigError(f"need {n} free GPU(s), only {len(cand)} of {len(pool)} are free")
         return cand[:n]
 
     async def add_replicas(self, count: int = 1, gpus: Optional[List[int]] = None,
                            ready_timeout: Optional[float] = None) -> dict:
         """Req 7.5: start `count` more replicas of the serving model at runtime and
-        route to them once ready; traffic on the existing replicas is untouched."""
-        if count < 1 or count > 64:
-            raise ConfigError("count must be in [1, 64]")
+        route to them once ready; traffic on the existing replicas is untouched.
+        The swap lock is held only while GPUs are reserved and processes started,
+        and again while the ready replicas are registered -- not across the load."""
+        w = self.cfg.worker
+        max_count = 64 if w.mock else 8
+        if count < 1 or count > max_count:
+            raise ConfigError(f"count must be in [1, {max_count}]")
         async with self._swap_lock:
-            w = self.cfg.worker
             spec = self._spec
             tp = max(1, int(w.tp))
             if gpus is not None and len(gpus) != count * tp:
                 raise ConfigError(f"need {count * tp} GPU ids for {count} replica(s) of tp={tp}, got {len(gpus)}")
+            if gpus is not None:
+                held = {g for r in self.replicas.values() for g in (getattr(r, "gpus", None) or [])}
+                if held & set(gpus):
+                    raise ConfigError(f"GPU(s) {sorted(held & set(gpus))} already hold a replica")
             gl = list(gpus) if gpus is not None else (self._free_gpus(count * tp) if not w.in_process else [])
             new: List[Replica] = []
             for i in range(count):
                 rid = self._next_replica_id
                 self._next_replica_id += 1
                 r = self._make_replica(rid, spec, gl[i * tp:(i + 1) * tp] or list(range(tp)), w)
-                self.replicas[rid] = r
+                self.replicas[rid] = r  # reserves its GPUs for concurrent calls
                 new.append(r)
                 r.start()
-            timeout = ready_timeout or (60.0 if w.mock else 1800.0)
-            oks = await asyncio.gather(*[asyncio.to_thread(r.wait_ready, timeout) for r in new])
-            if not all(oks):
-                errs = [f"replica {r.id}: {r.error or 'not ready in time'}" for r, ok in zip(new, oks) if not ok]
+            model_at_start = self.model_name
+        timeout = ready_timeout or (60.0 if w.mock else 1800.0)
+        oks = await asyncio.gather(*[asyncio.to_thread(r.wait_ready, timeout) for r in new])
+        async with self._swap_lock:
+            swapped = self.model_name != model_at_start
+            if not all(oks) or swapped:
+                errs = ([f"replica {r.id}: {r.error or 'not ready in time'}" for r, ok in zip(new, oks) if not ok]
+                        or ["the serving model was swapped while the replicas loaded"])
                 for r in new:
                     await asyncio.to_thread(r.shutdown, 5.0)
                     self.replicas.pop(r.id, None)

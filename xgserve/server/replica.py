@@ -331,10 +331,24 @@ def _worker_main(spec: dict, rank: int, env: dict, cmd_q, out_q, out_w=None) -> 
     the engine-loop thread: an mp.Queue would pickle them on a feeder thread that
     then holds the GIL when the loop thread returns from a GPU wait, stalling the
     next launch by up to the interpreter's switch interval (measured: ~3-5 ms per
-    step at 64 streams). ready / fatal (any rank, rare) keep using `out_q`."""
+    step at 64 streams). The leader's fatal report rides the same pipe (ordered after
+    its last outputs); ready and followers' fatal reports use `out_q`."""
     import pickle
     import sys
     os.environ.update(env)
+
+    def send_fatal(msg: str) -> None:
+        # the leader reports over the outputs pipe, behind the outputs it already
+        # wrote (e.g. the inference_failed outputs of a collective timeout), so the
+        # orchestrator sees them in order; followers have only the queue
+        if out_w is not None:
+            try:
+                out_w.send_bytes(pickle.dumps(("fatal", msg), protocol=pickle.HIGHEST_PROTOCOL))
+                return
+            except (OSError, ValueError):
+                pass
+        out_q.put(("fatal", msg))
+
     sys.setswitchinterval(0.0005)  # the cmd reader thread must never hold the GIL for long
     logging.basicConfig(level=os.environ.get("XGS_LOG_LEVEL", "WARNING"),
                         format=f"[replica {env.get('XGS_REPLICA', '?')} rank {rank}] %(levelname)s %(message)s")
@@ -371,10 +385,10 @@ def _worker_main(spec: dict, rank: int, env: dict, cmd_q, out_q, out_w=None) -> 
         out_q.put(("ready", engine_info(eng)))
         loop.run()
     except SystemExit as e:
-        out_q.put(("fatal", f"worker exited: {e}"))
+        send_fatal(f"worker exited: {e}")
         raise
     except BaseException as e:  # noqa: BLE001
-        out_q.put(("fatal", f"{type(e).__name__}: {e}\n{traceback.format_exc()}"))
+        send_fatal(f"{type(e).__name__}: {e}\n{traceback.format_exc()}")
         raise
 
 
@@ -430,6 +444,8 @@ class ProcessReplica(Replica):
                 if kind == "outp":
                     kind, payload = "out", [RequestOutput(*t) for t in payload]
                 self._event(kind, payload)
+                if kind == "fatal":
+                    return
 
         self._reader = threading.Thread(target=reader, daemon=True, name=f"replica-{self.id}-reader")
         self._reader.start()
