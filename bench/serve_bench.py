@@ -83,6 +83,7 @@ async def run_clients(a, url: str, first: int, n: int, t0: float, t1: float) -> 
                     "ignore_eos": True}
             sent = time.monotonic()
             last = None
+            last_idx = -1
             try:
                 async with s.post(url + "/generate", json=body) as r:
                     if r.status != 200:
@@ -102,8 +103,14 @@ async def run_clients(a, url: str, first: int, n: int, t0: float, t1: float) -> 
                             elif in_win:
                                 st["itl"].append(now - last)
                             last = now
+                            # an event carries the tokens since the previous one (a token whose
+                            # text is an incomplete UTF-8 sequence rides the next event): count
+                            # by the event's index, the generated-token position
+                            i = raw.rfind(b'"index":')
+                            idx = int(raw[i + 8:raw.index(b"}", i)].split(b",")[0]) if i >= 0 else last_idx + 1
                             if in_win:
-                                st["tokens"] += 1
+                                st["tokens"] += idx - last_idx
+                            last_idx = idx
                         else:
                             ev = json.loads(raw[6:])
                             if ev["type"] == "error":

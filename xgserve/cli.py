@@ -43,11 +43,12 @@ def _common(p: argparse.ArgumentParser) -> None:
     p.add_argument("--draft-model", help="speculative decoding draft model")
     p.add_argument("--num-speculative-tokens", type=int)
     p.add_argument("--log-level")
+    p.add_argument("--frontends", type=int, help="HTTP front-end processes over one orchestrator")
 
 
 def _overrides(a) -> dict:
     return {
-        "api": {"host": a.host, "port": a.port},
+        "api": {"host": a.host, "port": a.port, "frontends": getattr(a, "frontends", None)},
         "worker": {"model": a.model, "checkpoint": a.checkpoint, "tp": a.tp, "replicas": a.replicas, "gpus": a.gpus,
                    "device": a.device, "quantization": a.quantization, "max_num_seqs": a.max_num_seqs,
                    "max_model_len": a.max_model_len, "mock": a.mock, "in_process": a.in_process,
@@ -72,7 +73,12 @@ def cmd_serve(a) -> int:
     from .server.app import serve
     from .server.orchestrator import InferenceServer
     try:
-        serve(InferenceServer(cfg))
+        if cfg.api.frontends > 1:
+            import asyncio
+            from .server.frontend import run_hub
+            asyncio.run(run_hub(InferenceServer(cfg), cfg.api.frontends))
+        else:
+            serve(InferenceServer(cfg))
     except ApiError as e:
         print(f"startup failed: {e.message}", file=sys.stderr)
         return 3

@@ -92,6 +92,7 @@ class EngineConfig:
     # TP the followers get (plan, sampling rows, src) per launch and sample the same
     # tokens from the same all-gathered logits, so their substitutions agree.
     async_schedule: bool = True
+    early_release: bool = True
     # "fp8": weight-only E4M3 copies for batch <= 16 decode (bf16 activations)
     weight_dtype: Optional[str] = None
     # custom xGMI all-reduce peer-wait limit while serving: a TP peer this late fails
@@ -144,9 +145,12 @@ class LLMEngine:
         sc.decode_prefill_cap = cfg.decode_prefill_cap
         # asynchronous scheduling over prompt steps too (r2_async_mixed_ab.md)
         sc.lookahead_mixed = 1
-        # release length-finishing rows at lookahead (throughput) instead of a synchronous
-        # step (TTFT of a request that arrives when they finish); XGS_EARLY_RELEASE=1
-        sc.early_release = int(os.environ.get("XGS_EARLY_RELEASE", "0"))
+        # release length-finishing rows at lookahead: the next step is planned before a
+        # finishing row's last token reaches the host, so the GPU never waits for the
+        # host at a finish (a request arriving just then is admitted one step later).
+        # Steady state 64 concurrent: +1.3 % tok/s, p50 TTFT 12.4 -> 16.6 ms
+        # (profiles/r3_steady_state.md). XGS_EARLY_RELEASE=0: synchronous finishing steps.
+        sc.early_release = int(os.environ.get("XGS_EARLY_RELEASE", "1" if cfg.early_release else "0"))
         sc.eos_ids = list(self.mcfg.eos_token_ids)
         self.sched = R.StepScheduler(sc)
         # decode graphs capture the TP collectives: RCCL (and the IPC all-reduce) can be

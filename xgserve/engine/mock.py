@@ -31,11 +31,12 @@ class _MockModelCfg:
 class MockEngine:
     def __init__(self, model_name: str = "mock", vocab_size: int = 1000, hidden_size: int = 16,
                  step_latency_s: float = 0.0, max_num_seqs: int = 256, fail_marker: str = "__FAIL__",
-                 crash_after_steps: Optional[int] = None, eos_every: Optional[int] = None):
+                 crash_after_steps: Optional[int] = None, eos_every: Optional[int] = None, kv_seqs: int = 0):
         self.mcfg = _MockModelCfg(model_name, vocab_size, hidden_size)
         self.tokenizer = SyntheticTokenizer(vocab_size, 1, [2])
         self.step_latency_s = step_latency_s
         self.max_num_seqs = max_num_seqs
+        self.kv_seqs = kv_seqs  # memory-pressure model: live sequences / capacity (0: max_num_seqs)
         self.fail_marker_ids = self.tokenizer.encode(fail_marker, add_bos=False)
         self.crash_after_steps = crash_after_steps
         self.eos_every = eos_every
@@ -151,7 +152,7 @@ class MockEngine:
         self.stats_counters["requests_finished"] += 1
 
     def kv_usage(self) -> float:
-        return min(1.0, len(self.requests) / max(1, self.max_num_seqs))
+        return min(1.0, len(self.requests) / max(1, self.kv_seqs or self.max_num_seqs))
 
     def stats(self) -> dict:
         used = len(self.requests)

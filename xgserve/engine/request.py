@@ -58,6 +58,10 @@ class RequestOutput:
     # delay = socket write time - t_tokens; CLOCK_MONOTONIC is system-wide, so it holds
     # across replica processes)
     t_tokens: float = 0.0
+    # the native SSE token event of this output, already framed as one HTTP/1.1 chunk
+    # (encoded by the replica process that produced it, so the HTTP process only
+    # writes bytes: server/replica.py encode_sse_chunk); None: encode on the server
+    sse: Optional[bytes] = None
 
 
 @dataclass

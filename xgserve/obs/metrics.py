@@ -10,6 +10,7 @@ format 0.0.4 (hand-rolled: no dependency), `/server/stats` the JSON snapshot.
 from __future__ import annotations
 
 import bisect
+import itertools
 import math
 import threading
 import time
@@ -30,10 +31,10 @@ class Histogram:
         self.sum = 0.0
         self.n = 0
 
-    def observe(self, v: float):
-        self.counts[bisect.bisect_left(self.buckets, v)] += 1
-        self.sum += v
-        self.n += 1
+    def observe(self, v: float, n: int = 1):
+        self.counts[bisect.bisect_left(self.buckets, v)] += n
+        self.sum += v * n
+        self.n += n
 
 
 def _labels(d: Dict[str, str]) -> str:
@@ -117,12 +118,13 @@ class MetricsCollector:
         with self._lock:
             self.ttft.observe(s)
 
-    def record_delivery(self, s: float):
+    def record_delivery(self, s: float, n: int = 1):
         """Req 5.1: token delivery delay -- from the token reaching the host (after
-        the engine step) to its SSE event being written to the client socket."""
+        the engine step) to its SSE event being written to the client socket; n
+        events written together (one engine step's tokens) share the delay."""
         with self._lock:
-            self.delivery.observe(s)
-            self._recent_delivery.append(s)
+            self.delivery.observe(s, n)
+            self._recent_delivery.extend(itertools.repeat(s, n))
 
     def record_loop_lag(self, s: float):
         """Event-loop responsiveness: how late a periodic wake-up fired."""
@@ -132,6 +134,17 @@ class MetricsCollector:
     def record_itl(self, s: float):
         with self._lock:
             self.itl.observe(s)
+
+    def record_itl_many(self, xs) -> None:
+        """One engine step's inter-token latencies (one lock, one pass)."""
+        h = self.itl
+        b, counts = h.buckets, h.counts
+        bl = bisect.bisect_left
+        with self._lock:
+            for v in xs:
+                counts[bl(b, v)] += 1
+            h.sum += sum(xs)
+            h.n += len(xs)
 
     def record_cache_access(self, hit: bool, n: int = 1):
         with self._lock:

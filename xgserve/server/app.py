@@ -35,7 +35,7 @@ from ..core.wire import (ChatChoice, ChatMessage, ChatRequest, ChatResponse, Emb
                          TokenEvent, Usage)
 from ..engine.request import RequestType, SamplingParams
 from ..obs import trace
-from .orchestrator import InferenceServer, ServerRequest
+from .orchestrator import InferenceServer, ServerRequest, sse_chunk
 
 log = logging.getLogger("xgserve.http")
 
@@ -141,6 +141,21 @@ async def _sse(request: web.Request, srv: InferenceServer, sreq: ServerRequest, 
             n += len(batch)
             if batch[-1].type in ("done", "error"):
                 break
+            if sreq.sse_native and sreq.wire is None and request.transport is not None:
+                # the response has started (headers flushed): from here on the server's
+                # output handler writes this stream's token chunks straight to the
+                # socket; only the final done / error event comes through the queue.
+                # Events queued meanwhile go out first, in order, in this same step.
+                tail = sreq.token_stream.take_ready()
+                toks = [e for e in tail if e.type == "token"]
+                if toks:
+                    request.transport.write(b"".join(sse_chunk(e) for e in toks))
+                    n += len(toks)
+                sreq.wire = request.transport
+                rest = [e for e in tail if e.type != "token"]
+                if rest:
+                    batch = rest
+                    continue
             ev = await it.__anext__()
             batch = [ev] + sreq.token_stream.take_ready()
         if fmt is not None:
@@ -178,8 +193,8 @@ async def handle_generate(request: web.Request) -> web.StreamResponse:
         srv.validate_generate(req.prompt, req.max_tokens, req.temperature, req.top_p)
     ids = srv.encode(req.prompt)
     sp = _params(req.max_tokens, req.temperature, req.top_p, req.stop_sequences, req.seed, req.ignore_eos, req.logprobs)
-    sreq = srv.admit(RequestType.Generate, ids, sp, req.priority if req.priority is not None else Priority.Normal,
-                     stream=req.stream)
+    sreq = await srv.aadmit(RequestType.Generate, ids, sp, req.priority if req.priority is not None else Priority.Normal,
+                     stream=req.stream, sse_native=req.stream)
     if req.stream:
         return await _sse(request, srv, sreq)
     r = await _await_result(request, srv, sreq)
@@ -194,7 +209,7 @@ async def handle_chat(request: web.Request) -> web.StreamResponse:
         srv.validate_chat([m.content for m in req.messages], req.max_tokens, req.temperature, req.top_p)
     ids = srv.encode(srv.tokenizer.apply_chat_template(req.messages))
     sp = _params(req.max_tokens, req.temperature, req.top_p, req.stop_sequences, req.seed, req.ignore_eos)
-    sreq = srv.admit(RequestType.Chat, ids, sp, Priority.Normal, stream=req.stream)
+    sreq = await srv.aadmit(RequestType.Chat, ids, sp, Priority.Normal, stream=req.stream, sse_native=req.stream)
     if req.stream:
         return await _sse(request, srv, sreq)
     r = await _await_result(request, srv, sreq)
@@ -205,9 +220,11 @@ async def handle_chat(request: web.Request) -> web.StreamResponse:
 
 async def _embed(srv: InferenceServer, inputs, request) -> tuple:
     srv.validate_embeddings(inputs)
-    sreqs = [srv.admit(RequestType.Embeddings, srv.encode(t), SamplingParams(max_tokens=0), Priority.Normal)
-             for t in inputs]
+    sreqs = []
     try:
+        for t in inputs:
+            sreqs.append(await srv.aadmit(RequestType.Embeddings, srv.encode(t), SamplingParams(max_tokens=0),
+                                          Priority.Normal))
         done = await asyncio.gather(*[_await_result(request, srv, s) for s in sreqs])
     except BaseException:
         for s in sreqs:
@@ -225,18 +242,17 @@ async def handle_embeddings(request: web.Request) -> web.Response:
 
 
 async def handle_stats(request: web.Request) -> web.Response:
-    return _json(request.app[SERVER_KEY].stats())
+    return _json(await request.app[SERVER_KEY].astats())
 
 
 async def handle_metrics(request: web.Request) -> web.Response:
     srv: InferenceServer = request.app[SERVER_KEY]
-    srv.check_health()
-    return web.Response(text=srv.metrics.prometheus(), content_type="text/plain",
+    return web.Response(text=await srv.ametrics_text(), content_type="text/plain",
                         headers={"X-Prometheus-Format": "0.0.4"})
 
 
 async def handle_health(request: web.Request) -> web.Response:
-    h = request.app[SERVER_KEY].health()
+    h = await request.app[SERVER_KEY].ahealth()
     return _json(h, status=200 if h["status"] != "unhealthy" else 503)
 
 
@@ -249,12 +265,12 @@ async def handle_traces(request: web.Request) -> web.Response:
 async def handle_admin_config(request: web.Request) -> web.Response:
     srv: InferenceServer = request.app[SERVER_KEY]
     if request.method == "GET":
-        return _json(srv.cfg.to_dict())
+        return _json(await srv.acfg())
     try:
         patch = json.loads(await _body(request))
         if not isinstance(patch, dict) or not all(isinstance(v, dict) for v in patch.values()):
             raise ValueError("expected {section: {key: value}}")
-        applied = srv.reload_config(patch)
+        applied = await srv.areload_config(patch)
     except (ValueError, ConfigError) as e:
         raise ApiValidationError(ValidationError.invalid_parameter("config", str(e)))
     return _json({"status": "ok", "applied": applied})
@@ -263,7 +279,7 @@ async def handle_admin_config(request: web.Request) -> web.Response:
 async def handle_admin_model(request: web.Request) -> web.Response:
     srv: InferenceServer = request.app[SERVER_KEY]
     if request.method == "GET":
-        return _json({"model": srv.model_name, "info": srv.model_info, "swaps": srv.swaps})
+        return _json(await srv.amodel_state())
     try:
         patch = json.loads(await _body(request))
         if not isinstance(patch, dict):
@@ -279,7 +295,7 @@ async def handle_admin_replicas(request: web.Request) -> web.Response:
     {"action": "remove", "ids": [..]} / {"action": "remove", "count": n}."""
     srv: InferenceServer = request.app[SERVER_KEY]
     if request.method == "GET":
-        return _json({"replicas": srv.stats()["replicas"], "routable": list(srv.routable)})
+        return _json(await srv.areplica_state())
     try:
         d = json.loads(await _body(request))
         if not isinstance(d, dict) or d.get("action") not in ("add", "remove"):
@@ -330,7 +346,7 @@ async def handle_v1_completions(request: web.Request) -> web.StreamResponse:
     req = GenerateRequest.parse(body)
     srv.validate_generate(req.prompt, req.max_tokens, req.temperature, req.top_p)
     sp = _params(req.max_tokens, req.temperature, req.top_p, req.stop_sequences, req.seed)
-    sreq = srv.admit(RequestType.Generate, srv.encode(req.prompt), sp,
+    sreq = await srv.aadmit(RequestType.Generate, srv.encode(req.prompt), sp,
                      req.priority if req.priority is not None else Priority.Normal, stream=req.stream)
     created = int(time.time())
     if req.stream:
@@ -362,7 +378,7 @@ async def handle_v1_chat(request: web.Request) -> web.StreamResponse:
     req = ChatRequest.parse(body)
     srv.validate_chat([m.content for m in req.messages], req.max_tokens, req.temperature, req.top_p)
     sp = _params(req.max_tokens, req.temperature, req.top_p, req.stop_sequences, req.seed)
-    sreq = srv.admit(RequestType.Chat, srv.encode(srv.tokenizer.apply_chat_template(req.messages)), sp,
+    sreq = await srv.aadmit(RequestType.Chat, srv.encode(srv.tokenizer.apply_chat_template(req.messages)), sp,
                      Priority.Normal, stream=req.stream)
     created = int(time.time())
     if req.stream:

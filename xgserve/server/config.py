@@ -33,6 +33,9 @@ class ApiConfig:
     grpc_addr: Optional[str] = None
     max_request_size: int = 4 * 1024 * 1024
     request_timeout_s: float = 300.0
+    # HTTP front-end processes (SO_REUSEPORT) over the one orchestrator process;
+    # 1 = HTTP on the orchestrator's own event loop (server/frontend.py)
+    frontends: int = 1
 
 
 @dataclass
@@ -94,6 +97,7 @@ class WorkerSection:
     in_process: bool = False          # run the engine in a thread of the server process
     mock: bool = False                # deterministic MockEngine (tests / plumbing)
     mock_latency_ms: float = 1.0
+    mock_kv_seqs: int = 0             # mock KV capacity in sequences (memory pressure model; 0 = max_num_seqs)
     moe_comm: str = "auto"
     seed: int = 0
 

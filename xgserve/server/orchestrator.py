@@ -22,6 +22,7 @@ from __future__ import annotations
 import asyncio
 import copy
 import logging
+import threading
 import time
 from typing import Any, Dict, List, Optional
 
@@ -54,6 +55,63 @@ class ServiceUnavailable(ApiError):
         super().__init__(message, code=code, retry_after=retry_after)
 
 
+def sse_chunk(ev: TokenEvent) -> bytes:
+    """A TokenEvent's SSE bytes framed as one HTTP/1.1 chunk (direct socket writes)."""
+    body = ev.sse()
+    return b"%x\r\n%s\r\n" % (len(body), body)
+
+
+class RemoteSender:
+    """Stream sender of a request admitted by an HTTP front-end process
+    (server/frontend.py): its final done / error event goes to that process."""
+
+    def __init__(self, hub, wid: int, rid: str):
+        self.hub, self.wid, self.rid = hub, wid, rid
+        self.closed = False
+
+    def send(self, ev: TokenEvent) -> None:
+        if not self.closed:
+            self.hub.send(self.wid, ("ev", self.rid, ev_to_tuple(ev)))
+
+    def close(self) -> None:
+        if not self.closed:
+            self.closed = True
+            self.hub.send(self.wid, ("close", self.rid))
+
+
+class RemoteWire:
+    """`ServerRequest.wire` of a native SSE stream held by a front-end process: token
+    chunks are batched to that process, which writes them to the client socket."""
+
+    def __init__(self, hub, wid: int, rid: str):
+        self.hub, self.wid, self.rid = hub, wid, rid
+        self.conn = hub.conns.get(wid)  # the front end's batching pipe end (frontend._Conn)
+
+    def is_closing(self) -> bool:
+        return False
+
+    def send(self, chunk: bytes, t_tokens: float) -> None:
+        c = self.conn
+        if c is not None:  # appended in order with the request's other events
+            c.pending.append(("tok", self.rid, chunk, t_tokens))
+            if not c._flush_armed:
+                c._flush_armed = True
+                c.loop.call_soon(c.flush)
+
+
+def ev_to_tuple(ev: TokenEvent) -> tuple:
+    u = ev.usage
+    return (ev.type, ev.token, ev.index, ev.logprob, ev.finish_reason.value if ev.finish_reason else None,
+            (u.prompt_tokens, u.completion_tokens) if u is not None else None, ev.message, ev.code)
+
+
+def ev_from_tuple(t: tuple) -> TokenEvent:
+    typ, token, index, logprob, fr, u, message, code = t
+    return TokenEvent(typ, token=token, index=index, logprob=logprob,
+                      finish_reason=FinishReason(fr) if fr is not None else None,
+                      usage=Usage.new(*u) if u is not None else None, message=message, code=code)
+
+
 class ServerRequest:
     """One admitted request (the spec's InferenceRequest, design.md:645-678)."""
 
@@ -65,6 +123,11 @@ class ServerRequest:
         self.params = params
         self.priority = int(priority)
         self.stream = stream
+        # native SSE stream (/generate, /chat): replicas pre-encode its token events and,
+        # once the response has started, _handle_outputs writes them straight to `wire`
+        # (the client transport) -- no per-token queue hop or coroutine wake-up
+        self.sse_native = False
+        self.wire = None
         self.future: Optional[asyncio.Future] = None if stream else loop.create_future()
         self.sender: Optional[StreamSender] = None
         self.token_stream = None
@@ -124,11 +187,13 @@ class InferenceServer:
         self.fault: Optional[dict] = None  # MockEngine fault-injection knobs for new replicas (tests)
         self._next_replica_id = 0
         self._loop: Optional[asyncio.AbstractEventLoop] = None
+        self._loop_thread: Optional[int] = None
         self._wake: Optional[asyncio.Event] = None
         self._tasks: List[asyncio.Task] = []
         self._swap_lock: Optional[asyncio.Lock] = None
         self._reduced = False
         self.swaps = 0
+        self.hub = None  # FrontendHub when HTTP runs in front-end processes (api.frontends > 1)
         trace.configure(cfg.observability.tracing, cfg.observability.trace_sample_rate)
 
     # ------------------------------------------------------------------ config helpers
@@ -154,6 +219,7 @@ class InferenceServer:
     # ------------------------------------------------------------------ lifecycle
     async def start(self, ready_timeout: Optional[float] = None) -> None:
         self._loop = asyncio.get_running_loop()
+        self._loop_thread = threading.get_ident()
         self._wake = asyncio.Event()
         self._swap_lock = asyncio.Lock()
         ids = await self._spawn_set(self.cfg, ready_timeout)
@@ -182,7 +248,7 @@ class InferenceServer:
             if not w.mock and w.device is None:
                 spec = dict(spec, device=None)
             return InProcessReplica(rid, spec, self._on_replica_event)
-        return ProcessReplica(rid, spec, self._on_replica_event, gpus=gpus)
+        return ProcessReplica(rid, spec, self._on_replica_event, gpus=gpus, loop=self._loop)
 
     async def _spawn_set(self, cfg: ServerConfig, ready_timeout: Optional[float]) -> List[int]:
         w = cfg.worker
@@ -209,6 +275,8 @@ class InferenceServer:
         self.model_info = info
         self.model_name = info.get("model", w.model)
         self.tokenizer = self._build_tokenizer(cfg, info)
+        if self.hub is not None:
+            self.hub.broadcast_state()
         self._spec = spec
         self._engine = None  # a pre-built engine is used once
         return [r.id for r in new]
@@ -270,8 +338,12 @@ class InferenceServer:
         return self.tokenizer.encode(text)
 
     def admit(self, kind: RequestType, prompt_ids: List[int], params: SamplingParams,
-              priority: int = Priority.Normal, stream: bool = False, rid: Optional[str] = None) -> ServerRequest:
-        """Gate + enqueue. Raises ApiError (400 / 503)."""
+              priority: int = Priority.Normal, stream: bool = False, rid: Optional[str] = None,
+              sse_native: bool = False, remote: Optional[tuple] = None) -> ServerRequest:
+        """Gate + enqueue. Raises ApiError (400 / 503). sse_native: the response is the
+        native SSE format (token events pre-encoded by the replica). remote = (hub,
+        front-end id): the request belongs to an HTTP front-end process; its events
+        and result are routed there (server/frontend.py)."""
         if not self.accepting:
             self.metrics.record_rejection("shutting_down")
             raise ServiceUnavailable("Server is not accepting requests", code="shutting_down")
@@ -287,8 +359,19 @@ class InferenceServer:
         if len(prompt_ids) > limit:
             raise ApiValidationError(ValidationError.token_limit_exceeded(len(prompt_ids), limit))
         sreq = ServerRequest(rid or new_request_id(), kind, prompt_ids, params, int(priority), stream, self._loop)
-        if stream:
+        if remote is not None:
+            hub, wid = remote
+            if stream:
+                sreq.sender = RemoteSender(hub, wid, sreq.id)
+                self.streamer.register(sreq.id, sreq.sender)
+                sreq.sse_native = sse_native
+                if sse_native:
+                    sreq.wire = RemoteWire(hub, wid, sreq.id)
+            else:
+                sreq.future.add_done_callback(lambda f, s_=sreq: hub.send_result(wid, s_, f))
+        elif stream:
             sreq.sender, sreq.token_stream = self.streamer.create_stream(sreq.id)
+            sreq.sse_native = sse_native
         if not self.queue.enqueue(sreq.id, sreq, int(priority)):
             if stream:
                 self.streamer.discard(sreq.id)
@@ -299,6 +382,33 @@ class InferenceServer:
         self._record_queue_depth()
         self._wake.set()
         return sreq
+
+    # ---- async facade: the HTTP handlers' interface, also served to front-end
+    # processes over IPC (server/frontend.py FrontendClient implements the same)
+    async def aadmit(self, *a, **kw) -> ServerRequest:
+        return self.admit(*a, **kw)
+
+    async def astats(self) -> dict:
+        return self.stats()
+
+    async def ahealth(self) -> dict:
+        return self.health()
+
+    async def ametrics_text(self) -> str:
+        self.check_health()
+        return self.metrics.prometheus()
+
+    async def areload_config(self, patch) -> dict:
+        return self.reload_config(patch)
+
+    async def acfg(self) -> dict:
+        return self.cfg.to_dict()
+
+    async def amodel_state(self) -> dict:
+        return {"model": self.model_name, "info": self.model_info, "swaps": self.swaps}
+
+    async def areplica_state(self) -> dict:
+        return {"replicas": self.stats()["replicas"], "routable": list(self.routable)}
 
     def cancel(self, rid: str) -> None:
         """Client disconnect or caller timeout: remove from the queue or abort in the engine."""
@@ -355,7 +465,7 @@ class InferenceServer:
         self.router.add_active(rid, 1)
         trace.end_span(sreq.qspan, replica=rid)
         sreq.espan = trace.start_span("engine", parent=sreq.qspan, request_id=sreq.id, replica=rid)
-        r.submit(sreq.id, sreq.prompt_ids, copy.copy(sreq.params), sreq.priority, sreq.kind.value)
+        r.submit(sreq.id, sreq.prompt_ids, copy.copy(sreq.params), sreq.priority, sreq.kind.value, sreq.sse_native)
 
     async def _dispatch_loop(self) -> None:
         while True:
@@ -411,6 +521,9 @@ class InferenceServer:
         loop = self._loop
         if loop is None or loop.is_closed():
             return
+        if threading.get_ident() == self._loop_thread:  # a reader on the loop itself (ProcessReplica)
+            self._handle_event(rid, kind, payload)
+            return
         try:
             loop.call_soon_threadsafe(self._handle_event, rid, kind, payload)
         except RuntimeError:
@@ -433,9 +546,28 @@ class InferenceServer:
     def _handle_outputs(self, rid: int, outs: List[RequestOutput]) -> None:
         now = time.monotonic()
         n_tok = 0
+        n_wire, t_wire = 0, 0.0
+        inflight = self.inflight
+        itl: List[float] = []
         for o in outs:
-            sreq = self.inflight.get(o.request_id)
+            sreq = inflight.get(o.request_id)
             if sreq is None or sreq.replica != rid:
+                continue
+            w = sreq.wire
+            if (w is not None and o.sse is not None and not o.finished and sreq.last_token_at is not None
+                    and not o.logprobs and o.embedding is None):
+                # steady-state token of a native SSE stream (the per-token hot path at node
+                # scale): the replica encoded the chunk; account it and pass it on
+                n_tok += 1
+                itl.append(now - sreq.last_token_at)
+                sreq.last_token_at = now
+                sreq.completion_tokens = o.completion_tokens
+                if w.__class__ is RemoteWire:
+                    w.send(o.sse, o.t_tokens)
+                elif not w.is_closing():
+                    w.write(o.sse)
+                    n_wire += 1
+                    t_wire = o.t_tokens
                 continue
             if o.error:
                 self._finalize(sreq)
@@ -450,7 +582,7 @@ class InferenceServer:
                     sreq.first_token_at = now
                     self.metrics.record_ttft(now - sreq.created)
                 elif sreq.last_token_at is not None:
-                    self.metrics.record_itl(now - sreq.last_token_at)
+                    itl.append(now - sreq.last_token_at)
                 sreq.last_token_at = now
                 sreq.started = True
                 sreq.completion_tokens = o.completion_tokens or (sreq.completion_tokens + len(o.new_token_ids))
@@ -458,15 +590,33 @@ class InferenceServer:
                     sreq.logprobs.extend(o.logprobs)
                 if sreq.sender is not None:
                     if o.new_text:
-                        ev = TokenEvent.tok(o.new_text, sreq.completion_tokens - 1,
-                                            o.logprobs[-1] if o.logprobs else None)
-                        ev.t_tokens = o.t_tokens  # not serialised: delivery-delay measurement (Req 5.1)
-                        sreq.sender.send(ev)
+                        w = sreq.wire
+                        if w is not None:  # direct: write the (pre-encoded) chunk to the socket now
+                            chunk = o.sse if o.sse is not None else sse_chunk(TokenEvent.tok(
+                                o.new_text, sreq.completion_tokens - 1, o.logprobs[-1] if o.logprobs else None))
+                            if w.__class__ is RemoteWire:
+                                w.send(chunk, o.t_tokens)  # the front end writes it and times the delivery
+                            elif not w.is_closing():
+                                w.write(chunk)
+                                n_wire += 1
+                                t_wire = o.t_tokens
+                        else:
+                            ev = TokenEvent.tok(o.new_text, sreq.completion_tokens - 1,
+                                                o.logprobs[-1] if o.logprobs else None)
+                            ev.t_tokens = o.t_tokens  # not serialised: delivery-delay measurement (Req 5.1)
+                            sreq.sender.send(ev)
                 else:
                     sreq.text_parts.append(o.new_text)
             elif o.new_text:
                 if sreq.sender is not None:
-                    sreq.sender.send(TokenEvent.tok(o.new_text, max(0, sreq.completion_tokens - 1)))
+                    ev = TokenEvent.tok(o.new_text, max(0, sreq.completion_tokens - 1))
+                    if sreq.wire is not None:
+                        if sreq.wire.__class__ is RemoteWire:
+                            sreq.wire.send(sse_chunk(ev), o.t_tokens)
+                        elif not sreq.wire.is_closing():
+                            sreq.wire.write(sse_chunk(ev))
+                    else:
+                        sreq.sender.send(ev)
                 else:
                     sreq.text_parts.append(o.new_text)
             if o.embedding is not None:
@@ -480,6 +630,10 @@ class InferenceServer:
                 self._complete(sreq)
         if n_tok:
             self.metrics.record_inference(0, n_tok)
+        if itl:
+            self.metrics.record_itl_many(itl)
+        if n_wire and t_wire:
+            self.metrics.record_delivery(time.monotonic() - t_wire, n_wire)
 
     def _finalize(self, sreq: ServerRequest) -> None:
         if sreq.finished:
@@ -586,7 +740,7 @@ class InferenceServer:
         w = self.cfg.worker
         spec = old.spec
         if isinstance(old, ProcessReplica):
-            r: Replica = ProcessReplica(old.id, spec, self._on_replica_event, gpus=old.gpus)
+            r: Replica = ProcessReplica(old.id, spec, self._on_replica_event, gpus=old.gpus, loop=self._loop)
         else:
             r = InProcessReplica(old.id, spec, self._on_replica_event)
         r.restarts = old.restarts + 1
@@ -654,6 +808,8 @@ class InferenceServer:
             for i in self.routable:
                 self.replicas[i].set_limits(new.worker.max_num_seqs, new.worker.max_num_batched_tokens)
         self.cfg = new
+        if self.hub is not None:
+            self.hub.broadcast_state()
         log.info("config reloaded: %s", patch)
         return {k: v for k, v in new.to_dict().items() if k in patch}
 
@@ -683,6 +839,8 @@ class InferenceServer:
             self.cfg = new_cfg
             self.metrics = MetricsCollector()  # stats reset after a swap (Req 13.5)
             self.swaps += 1
+            if self.hub is not None:
+                self.hub.broadcast_state()
             self._wake.set()
             self._loop.create_task(self._drain_and_stop(old_ids))
             log.info("model swapped: %s -> %s", old_name, self.model_name)

@@ -22,6 +22,7 @@ design.md:310-361) as an *engine loop* that owns one LLMEngine (a TP group).
 from __future__ import annotations
 
 import logging
+import json
 import os
 import queue as pyqueue
 import threading
@@ -42,7 +43,7 @@ def engine_spec(worker, cache=None, spec=None, fault: Optional[dict] = None) -> 
     MockEngine fault-injection knobs (crash_after_steps, eos_every)."""
     dt = {"bf16": "bfloat16", "fp16": "float16", "fp32": "float32", "fp8": "bfloat16"}[worker.quantization]
     wdt = "fp8" if worker.quantization == "fp8" else None
-    return dict(mock=worker.mock, mock_latency_ms=worker.mock_latency_ms, model=worker.model,
+    return dict(mock=worker.mock, mock_latency_ms=worker.mock_latency_ms, mock_kv_seqs=worker.mock_kv_seqs, model=worker.model,
                 checkpoint=worker.checkpoint, tp=worker.tp, device=worker.device, dtype=dt, weight_dtype=wdt,
                 block_size=worker.block_size, max_num_seqs=worker.max_num_seqs,
                 max_num_batched_tokens=worker.max_num_batched_tokens, max_model_len=worker.max_model_len,
@@ -62,7 +63,7 @@ def make_engine(spec: dict):
         f = spec.get("fault") or {}
         return MockEngine(model_name=spec.get("model") or "mock", step_latency_s=spec.get("mock_latency_ms", 0) / 1000.0,
                           max_num_seqs=spec.get("max_num_seqs", 256), crash_after_steps=f.get("crash_after_steps"),
-                          eos_every=f.get("eos_every"))
+                          eos_every=f.get("eos_every"), kv_seqs=spec.get("mock_kv_seqs", 0))
     from ..engine import EngineConfig, LLMEngine
     keys = set(EngineConfig.__dataclass_fields__)
     ec = EngineConfig(**{k: v for k, v in spec.items() if k in keys})
@@ -96,9 +97,23 @@ def _is_oom(e: BaseException) -> bool:
 # ---------------------------------------------------------------------------
 # the worker main loop
 # ---------------------------------------------------------------------------
+def encode_sse_chunk(text: str, index: int, logprob: Optional[float] = None) -> bytes:
+    """One native SSE token event (byte-identical to core.wire.TokenEvent.tok(...).sse())
+    framed as an HTTP/1.1 chunk, ready for the client socket."""
+    body = b'data: {"type":"token","token":' + json.dumps(text).encode()
+    body += b',"index":' + str(index).encode()
+    if logprob is not None:
+        body += b',"logprob":' + json.dumps(logprob).encode()
+    body += b"}\n\n"
+    return b"%x\r\n%s\r\n" % (len(body), body)
+
+
 class EngineLoop:
     """Drives one engine. `emit(kind, payload)` is called from the loop thread
-    with kind in {"out", "hb", "fatal"}."""
+    with kind in {"out", "hb", "fatal"}. Outputs of requests submitted with
+    sse=True carry their token event pre-encoded (RequestOutput.sse): the SSE
+    bytes of a node's streams are produced by the replica processes in parallel,
+    not by the one HTTP event loop (profiles/r3_frontend.md)."""
 
     def __init__(self, engine, emit: Callable[[str, Any], None]):
         self.engine = engine
@@ -108,6 +123,20 @@ class EngineLoop:
         self._stop = False
         self.steps = 0
         self.last_step_s = 0.0
+        self._sse: set = set()  # request ids whose outputs carry pre-encoded SSE chunks
+
+    def _encode(self, outs: list) -> None:
+        sse = self._sse
+        if not sse:
+            return
+        for o in outs:
+            rid = o.request_id
+            if rid not in sse:
+                continue
+            if o.finished:
+                sse.discard(rid)
+            if o.new_token_ids and o.new_text and o.completion_tokens and not o.error:
+                o.sse = encode_sse_chunk(o.new_text, o.completion_tokens - 1, o.logprobs[-1] if o.logprobs else None)
 
     def submit(self, cmd: tuple) -> None:
         self._inbox.put(cmd)
@@ -122,7 +151,9 @@ class EngineLoop:
                 return
             op = cmd[0]
             if op == "add":
-                _, rid, prompt_ids, params, prio, kind = cmd
+                _, rid, prompt_ids, params, prio, kind = cmd[:6]
+                if len(cmd) > 6 and cmd[6]:
+                    self._sse.add(rid)
                 try:
                     self.engine.add_request(rid, prompt_ids, params, prio, RequestType(kind))
                 except Exception as e:  # per-request rejection, never fatal
@@ -130,6 +161,7 @@ class EngineLoop:
                                               error=f"Inference failed: {e}", error_code="inference_failed"))
             elif op == "abort":
                 self.engine.abort(cmd[1])
+                self._sse.discard(cmd[1])
             elif op == "limits":
                 self.engine.set_limits(cmd[1], cmd[2])
             elif op == "clear_cache":
@@ -157,7 +189,10 @@ class EngineLoop:
         loop_t = {"engine_step": 0.0, "emit": 0.0, "drain": 0.0, "idle": 0.0}
         if hasattr(self.engine, "output_sink"):
             # tokens emitted while a GPU step runs leave for the server at once (Req 5.1)
-            self.engine.output_sink = lambda o: self.emit("out", o)
+            def sink(o):
+                self._encode(o)
+                self.emit("out", o)
+            self.engine.output_sink = sink
         while not self._stop:
             outs: list = []
             ta = time.perf_counter()
@@ -199,6 +234,7 @@ class EngineLoop:
                 loop_t["idle"] += time.perf_counter() - ti
             if outs:
                 te = time.perf_counter()
+                self._encode(outs)
                 self.emit("out", outs)
                 loop_t["emit"] += time.perf_counter() - te
             now = time.monotonic()
@@ -258,8 +294,8 @@ class Replica:
         ok = self.ready.wait(timeout)
         return ok and self.error is None
 
-    def submit(self, rid: str, prompt_ids: List[int], params, priority: int, kind: str) -> None:
-        self._send(("add", rid, list(prompt_ids), params, int(priority), kind))
+    def submit(self, rid: str, prompt_ids: List[int], params, priority: int, kind: str, sse: bool = False) -> None:
+        self._send(("add", rid, list(prompt_ids), params, int(priority), kind, bool(sse)))
 
     def abort(self, rid: str) -> None:
         self._send(("abort", rid))
@@ -395,8 +431,11 @@ def _worker_main(spec: dict, rank: int, env: dict, cmd_q, out_q, out_w=None) -> 
 class ProcessReplica(Replica):
     kind = "process"
 
-    def __init__(self, rid, spec, on_event, gpus: Optional[List[int]] = None, master_port: int = 0):
+    def __init__(self, rid, spec, on_event, gpus: Optional[List[int]] = None, master_port: int = 0, loop=None):
         super().__init__(rid, spec, on_event)
+        # the serving event loop: outputs are read by a reader callback ON it (no reader
+        # thread taking the GIL per step and re-hopping onto the loop); None: a thread
+        self.loop = loop
         tp = spec.get("tp", 1)
         self.gpus = gpus if gpus is not None else list(range(rid * tp, rid * tp + tp))
         self.master_port = master_port or _free_port()
@@ -434,23 +473,44 @@ class ProcessReplica(Replica):
                     return
 
         def pipe_reader():  # outputs + heartbeats
-            import pickle
-            from ..engine.request import RequestOutput
             while True:
                 try:
-                    kind, payload = pickle.loads(out_r.recv_bytes())
+                    data = out_r.recv_bytes()
                 except (EOFError, OSError):
                     return
-                if kind == "outp":
-                    kind, payload = "out", [RequestOutput(*t) for t in payload]
-                self._event(kind, payload)
-                if kind == "fatal":
+                if self._on_pipe_msg(data):
                     return
 
         self._reader = threading.Thread(target=reader, daemon=True, name=f"replica-{self.id}-reader")
         self._reader.start()
-        self._pipe_reader = threading.Thread(target=pipe_reader, daemon=True, name=f"replica-{self.id}-outputs")
-        self._pipe_reader.start()
+        self._out_r = out_r
+        loop = self.loop
+        if loop is not None and not loop.is_closed():
+            fd = out_r.fileno()
+
+            def readable():
+                try:
+                    while out_r.poll():
+                        if self._on_pipe_msg(out_r.recv_bytes()):
+                            loop.remove_reader(fd)
+                            return
+                except (EOFError, OSError):
+                    loop.remove_reader(fd)
+
+            loop.call_soon_threadsafe(loop.add_reader, fd, readable)
+        else:
+            self._pipe_reader = threading.Thread(target=pipe_reader, daemon=True, name=f"replica-{self.id}-outputs")
+            self._pipe_reader.start()
+
+    def _on_pipe_msg(self, data: bytes) -> bool:
+        """One outputs / heartbeat / fatal message from the leader's pipe; True at the end."""
+        import pickle
+        from ..engine.request import RequestOutput
+        kind, payload = pickle.loads(data)
+        if kind == "outp":
+            kind, payload = "out", [RequestOutput(*t) for t in payload]
+        self._event(kind, payload)
+        return kind == "fatal"
 
     def _send(self, cmd):
         if self.cmd_q is not None:

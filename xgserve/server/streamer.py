@@ -80,6 +80,10 @@ class TokenStreamer:
         self._senders[rid] = s
         return s, TokenStream(rid, q)
 
+    def register(self, rid: str, sender) -> None:
+        """A sender owned elsewhere (a front-end process's RemoteSender)."""
+        self._senders[rid] = sender
+
     def send_token(self, rid: str, token: str, index: int, logprob: Optional[float] = None) -> None:
         s = self._senders.get(rid)
         if s is None:
