@@ -110,6 +110,9 @@ def main():
         print(f"bench.py: --gpus {a.gpus} is not a multiple of --tp {a.tp}", file=sys.stderr)
         return 2
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    # host threads of this rank on its GPU's NUMA node, before anything touches the GPU
+    from xgserve.parallel.affinity import bind_to_gpu_numa
+    bind_to_gpu_numa(int(os.environ.get("LOCAL_RANK", "0")))
     import torch
     import torch.distributed as dist
     from xgserve.parallel.state import init_distributed

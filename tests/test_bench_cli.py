@@ -84,3 +84,14 @@ def _check_contract(r, nproc, model, par, tp):
     # sequence plus the immediate first token of a sequence admitted in it (outputs of
     # step N are delivered while step N+1 runs): <= 2 x concurrency per replica.
     assert 0 < r["value"] <= 2 * cfg["global_batch"] * 1000.0 / r["ms_per_step"] + 1e-6
+
+
+def test_numa_cpulist_parsing_and_noop_without_gpu():
+    from xgserve.parallel import affinity as A
+    assert A._parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert A._parse_cpulist("") == set()
+    # no KFD GPU nodes in this container: nothing to bind, affinity untouched
+    import os
+    before = os.sched_getaffinity(0)
+    assert A.bind_to_gpu_numa(0) is None
+    assert os.sched_getaffinity(0) == before

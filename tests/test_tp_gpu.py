@@ -69,6 +69,9 @@ _UNFUSED = {"XGS_FUSED_DECODE": "0", "XGS_ASYNC_SCHED": "0"}
 
 @pytest.mark.parametrize("model,moe_comm,world,env", [
     ("llama", "alltoall", 2, None), ("llama", "alltoall", 2, _UNFUSED), ("llama", "alltoall", 4, None),
+    # the Llama-3-70B TP8 decode collective (8 peers, one kv head per rank): 8 processes
+    # share the GPU with one hardware queue each, so every rank's kernels are co-resident
+    ("llama", "alltoall", 8, {"GPU_MAX_HW_QUEUES": "1"}),
     ("mixtral", "alltoall", 2, None), ("mixtral", "allreduce", 2, None), ("mixtral", "auto", 2, None),
     ("mixtral", "alltoall", 2, {"XGS_EP_EXACT_MIN_PAIRS": "0"})])
 def test_tp2_on_one_gpu_matches_fp32_reference(tmp_path, model, moe_comm, world, env):
@@ -97,7 +100,7 @@ def test_tp2_on_one_gpu_matches_fp32_reference(tmp_path, model, moe_comm, world,
     for p in procs:
         p.start()
     try:
-        kind, outs, mode = q.get(timeout=150)
+        kind, outs, mode = q.get(timeout=240)
     finally:
         for p in procs:
             p.join(timeout=30)

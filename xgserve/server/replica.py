@@ -391,6 +391,8 @@ def _worker_main(spec: dict, rank: int, env: dict, cmd_q, out_q, out_w=None) -> 
     try:
         eng_spec = dict(spec)
         if not spec.get("mock"):
+            from ..parallel.affinity import bind_to_gpu_numa
+            bind_to_gpu_numa(int(env.get("LOCAL_RANK", "0")))  # before any GPU call in this process
             from ..parallel.state import init_distributed
             import torch
             dev = None if not spec.get("device") else torch.device(spec["device"])
