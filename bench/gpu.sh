@@ -1,0 +1,92 @@
+#!/usr/bin/env bash
+# Every GPU measurement this repo takes, as named suites (run through gpurun, from the
+# repo or from the .snap/ copy made by bench/snap.sh):
+#   bash bench/gpu.sh <suite> [tag] [extra bench.py args...]
+# Suites:
+#   gate     full GPU test suite, smoke(), driver-form bench, 3000-step bench, batch 1
+#   steady   headline at steady state: driver form twice, long window, step log, profile
+#   ab       same bench under each XGS_AB setting (XGS_AB="A=1;A=0"), driver form + 400 steps
+#   tp       custom all-reduce + TP tests, Llama-3-70B TP8 shard (one rank) c1 / c64
+#   moe      Mixtral: MoE tests, c64 / c1, TP2 shard c64
+#   prefill  prefill kernels: tests, 512 / 2K / 8K kernel bench + TTFT, c64 bench
+#   serve    HTTP/SSE serve bench (64 streams) next to the in-process long bench
+#   tune     rebuild the shipped TunableOp GEMM tables (xgserve/tuning/)
+#   sweep    gemm_m64g configuration sweep at the TP shard shapes
+#   profile  rocprofv3 kernel + gap profile of the headline (bench/profile.sh)
+# Each GPU step has its own time limit; the first failure ends the suite.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+suite=${1:?suite}; tag=${2:-$1}; shift; shift || true
+o=${GRAFT_REPO_ROOT:-.}/gpurun_out/$tag; mkdir -p "$o"
+
+run() {  # name seconds cmd...   -> $o/name.log, prints its last line
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "$o/$name.log" 2>&1
+  local rc=$?
+  echo "[$name rc=$rc] $(tail -n 1 "$o/$name.log" | cut -c1-400)"
+  [ $rc -eq 0 ] || { tail -n 30 "$o/$name.log"; exit $rc; }
+}
+pyt() {  # name seconds pytest-args...
+  local name=$1 secs=$2; shift 2
+  run "$name" "$secs" python -u -m pytest -x -q --timeout 240 --timeout-method thread -p no:cacheprovider "$@"
+}
+B="python -u bench.py"
+
+case $suite in
+gate)
+  pyt gputests 900 tests -m gpu
+  run smoke 150 python -u -c "import __graft_entry__ as g; g.smoke()"
+  run bench_driver 200 $B --steps 20 --warmup 5 "$@"
+  run bench_long 300 $B --steps 3000 --warmup 100 "$@"
+  run bench_c1 200 $B --concurrency 1 --steps 200 --warmup 20 "$@" ;;
+steady)
+  run smoke 150 python -u -c "import __graft_entry__ as g; g.smoke()"
+  run driver_a 200 $B --steps 20 --warmup 5 "$@"
+  run driver_b 200 $B --steps 20 --warmup 5 "$@"
+  run long 300 $B --steps 3000 --warmup 100 "$@"
+  run steplog 200 env XGS_STEP_LOG="$o/steps.jsonl" $B --steps 400 --warmup 20 "$@"
+  bash bench/profile.sh "$o/prof" "$@" ;;
+ab)
+  IFS=';' read -ra settings <<< "${XGS_AB:?set XGS_AB='VAR=a;VAR=b'}"
+  for s in "${settings[@]}"; do
+    n=$(echo "$s" | tr -c 'A-Za-z0-9_=\n' '_')
+    run "driver_$n" 200 env $s $B --steps 20 --warmup 5 "$@"
+    run "w400_$n" 250 env $s $B --steps 400 --warmup 40 "$@"
+  done ;;
+tp)
+  pyt tp_tests 600 tests/test_custom_ar_gpu.py tests/test_rccl_gpu.py tests/test_tp_gpu.py
+  run tp8_c1 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20 "$@"
+  run tp8_c64 300 $B --model llama3-70b --tp-shard 8 --steps 60 --warmup 20 "$@" ;;
+moe)
+  pyt moe_tests 400 tests/test_kernels_gpu.py tests/test_engine_gpu.py -k "moe or mixtral or expert"
+  run mixtral_c64 300 $B --model mixtral-8x7b --steps 60 --warmup 20 "$@"
+  run mixtral_c1 300 $B --model mixtral-8x7b --concurrency 1 --steps 60 --warmup 10 "$@"
+  run mixtral_tp2_c64 300 $B --model mixtral-8x7b --tp-shard 2 --steps 60 --warmup 20 "$@" ;;
+prefill)
+  pyt prefill_tests 300 tests/test_kernels_gpu.py -k prefill
+  run prefill 300 python -u bench/prefill_bench.py
+  run c64 200 $B --steps 200 --warmup 40 "$@" ;;
+serve)
+  run bench_long 300 $B --steps 3000 --warmup 100
+  run serve 400 python -u bench/serve_bench.py --launch "--model llama3-8b --max-num-seqs 64" --concurrency 64 \
+      --prompt-len 512 --output-len 256 --warmup 40 --duration 40 --out "$o/serve_8b_c64.jsonl" "$@" ;;
+tune)
+  export PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_MAX_TUNING_DURATION_MS=100
+  export XGS_GEMM_TUNING=0   # tune from scratch (do not replay the shipped table)
+  for spec in "c64:--steps 120 --warmup 40" "c1:--concurrency 1 --steps 40 --warmup 10" \
+              "c8:--concurrency 8 --steps 60 --warmup 20" "mixtral_c64:--model mixtral-8x7b --steps 40 --warmup 20" \
+              "mixtral_c1:--model mixtral-8x7b --concurrency 1 --steps 30 --warmup 10"; do
+    n=${spec%%:*}
+    run "t_$n" 600 env PYTORCH_TUNABLEOP_FILENAME="$o/t_$n.csv" $B ${spec#*:}
+  done
+  run t_prefill 600 env PYTORCH_TUNABLEOP_FILENAME="$o/t_prefill.csv" python -u bench/prefill_bench.py ;;
+sweep)
+  run sweep 500 python -u bench/gemm_bench.py --m64g-sweep --M 1 16 32 64 --shapes \
+      qkv70t8 o70t8 gate_up70t8 down70t8 qkv8t2 o8t2 gate_up8t2 down8t2 qkv8t4 o8t4 gate_up8t4 down8t4 \
+      qkv8t8 o8t8 gate_up8t8 down8t8 qkv70t2 o70t2 gate_up70t2 down70t2 qkv70t4 o70t4 gate_up70t4 down70t4 ;;
+profile)
+  bash bench/profile.sh "$o" "$@" ;;
+*)
+  echo "unknown suite $suite"; exit 2 ;;
+esac

@@ -5,7 +5,7 @@ hipBLASLt, whose default heuristic picks one solution per shape. PyTorch's
 TunableOp times every hipBLASLt and rocBLAS solution for a shape (rotating
 buffers, i.e. cold operands as in a real step) and keeps the fastest; the table
 `mi355x_gemm.csv` holds those choices for the shapes our benchmark configs issue
-(`bench/gpu_tune_tables.sh` builds it on an MI355X; its validator rows pin the
+(`bash bench/gpu.sh tune` builds it on an MI355X; its validator rows pin the
 PyTorch / HIP / hipBLASLt / rocBLAS versions and gfx950, and TunableOp ignores the
 file on any mismatch). The engine only REPLAYS it (no tuning at serve time);
 shapes not in the table keep the default heuristic. XGS_GEMM_TUNING=0 disables it
