@@ -13,6 +13,7 @@
 #   tune     rebuild the shipped TunableOp GEMM tables (xgserve/tuning/)
 #   sweep    gemm_m64g configuration sweep at the TP shard shapes
 #   profile  rocprofv3 kernel + gap profile of the headline (bench/profile.sh)
+#   b1       persistent batch-1 decode: tests, batch-1 bench vs the multi-launch path, profile
 # Each GPU step has its own time limit; the first failure ends the suite.
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -87,6 +88,14 @@ sweep)
       qkv8t8 o8t8 gate_up8t8 down8t8 qkv70t2 o70t2 gate_up70t2 down70t2 qkv70t4 o70t4 gate_up70t4 down70t4 ;;
 profile)
   bash bench/profile.sh "$o" "$@" ;;
+b1stamps)
+  run stamps 300 python -u bench/b1_stamps.py "$@" ;;
+b1)
+  pyt b1_tests 600 -v tests/test_persistent_gpu.py
+  run stamps 300 python -u bench/b1_stamps.py
+  run c1 200 env XGS_PERSISTENT_DECODE=1 $B --concurrency 1 --steps 200 --warmup 20 "$@"
+  run c1_multilaunch 200 env XGS_PERSISTENT_DECODE=0 $B --concurrency 1 --steps 200 --warmup 20 "$@"
+  XGS_PERSISTENT_DECODE=1 bash bench/profile.sh "$o/prof_c1" --concurrency 1 ;;
 *)
   echo "unknown suite $suite"; exit 2 ;;
 esac

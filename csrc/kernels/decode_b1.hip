@@ -1,0 +1,753 @@
+// Persistent batch-1 decode: every layer of a dense Llama-family model (and the final
+// RMSNorm) in ONE launch of 256 workgroups, one per CU.
+//
+// Why: at batch 1 a decode step is a 14 GB once-read weight stream (Llama-3-8B); as
+// five launches per layer every kernel boundary drains and refills the chip's memory
+// pipeline (~1.2-1.9 us each, MI355X_MICROARCH.md price list "boundary") and the
+// attention / combine kernels are pure latency with the weight stream stopped. Here
+// the weight stream never stops: each CU's loader wave walks a STATIC sequence of
+// weight lines (all layers, all projections) into an LDS ring, running ahead across
+// the data dependencies ("prefetch-credit"), while three consumer waves compute.
+//
+// Roles per workgroup (4 waves):
+//   wave 0      loader: 1-KiB lines (one global_load_lds_dwordx4 nt each) into a ring
+//               of NSLOT 16-KiB slots; counted vmcnt waits, "landed" published in LDS;
+//               a slot is refilled once every consumer has moved past it (cur[]).
+//   waves 1..3  consumers: GEMV rows (v_dot2c_f32_bf16 on 16-B lane chunks, one wave
+//               reduction per row), the hand-offs, attention, residual and norms.
+// Row ownership (W = 256 workgroups, w = blockIdx.x):
+//   QKV   : kv-head group h = w / (W / Hkv) owns its q rows (G heads), k and v rows;
+//           its W / Hkv workgroups take equal contiguous slices (norm as a row scale).
+//   attn  : workgroup i < S_att of group h = key split i (RoPE, KV append by the split
+//           that owns the new key, online softmax) -> partials; then the same
+//           workgroups combine one OPW-wide slice of the group's outputs each.
+//   O     : rows [w * H/W, +H/W) (+ residual) ; GU: features [w * F/W, +F/W) (SiLU
+//           gate, gate|up rows interleaved in blocks of 16) ; down: rows as O.
+// Hand-offs between workgroups: 8-byte granules {tag, 32-bit value} written by ONE
+// relaxed agent-scope atomic store each and swept with relaxed agent-scope loads
+// until every tag matches (cdna_hip_programming.md §6 Guideline 16, R2: the data is
+// the flag; no fence). tag = layer * 8 + edge + 1, never 0; the granule area is
+// zeroed by a memset node before every launch. Every wait is bounded (ctl[1] ticks
+// of the 100 MHz wall clock); a timeout bumps ctl[0], raises the workgroup's abort
+// flag and every later wait returns at once, so the grid always drains.
+//
+// Numerics follow the fused multi-launch path (gemm_m64g + decode attention): norm
+// statistics from the bf16 residual, projections in fp32, q/k/v rounded to bf16
+// after RoPE, attention output and residual stream in bf16, SiLU-gate in fp32.
+#include <algorithm>
+
+#include "common.h"
+#include "glds.h"
+
+namespace xgk {
+namespace b1 {
+
+constexpr int NWG = 256;
+constexpr int NTHR = 256;
+constexpr int NCW = 3;          // consumer waves
+constexpr int CT = NCW * 64;    // consumer threads
+constexpr int LINE = 1024;      // ring line: 64 lanes x 16 B
+constexpr int SLOT = 16;        // lines per slot
+constexpr int HD = 128;         // head dim
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+
+enum { E_RESID = 0, E_QKV = 1, E_PART = 2, E_ATTN = 3, E_POST = 4, E_ACT = 5 };
+enum { P_QKV = 0, P_O = 1, P_GU = 2, P_DN = 3 };
+
+struct Args {
+  const uint64_t* wptr;       // [L][4] qkv, o, gate_up (16-row interleaved), down
+  const uint64_t* kvptr;      // [L][2] k_cache, v_cache  [blocks, Hkv, bs, 128] bf16
+  const uint16_t* resid_in;   // [H] embedding row
+  const uint16_t* final_norm; // [H]
+  uint16_t* out;              // [H] normalised final hidden state
+  const int32_t* positions;   // [1]
+  const int32_t* slot_mapping;
+  const int32_t* block_table; // [max_blocks] (row of the one sequence)
+  const int32_t* seq_lens;    // [1] (includes the new token)
+  const float* cos_sin;       // [max_pos, 128] = [cos | sin]
+  uint64_t* gran;             // granule area (zeroed before each launch)
+  int* ctl;                   // [0] timeouts, [1] wait limit in wall-clock ticks, [2] test: drop WG 0's QKV
+  int L, H, F, Hq, Hkv, bs, apply_rope;
+  float eps, scale;
+  // derived on the host (decode_b1_plan)
+  int S_att, ring_lines;
+  int off_xres, off_xbig, off_ctl;  // LDS byte offsets
+  int g_resid, g_post, g_qkv, g_part, g_attn, g_act;  // granule offsets
+  uint64_t* stamps;  // diagnostics (null in production): per-(workgroup, layer) phase clocks
+};
+constexpr int NSTAMP = 10;
+
+// LDS control block
+struct Ctl {
+  int landed;       // lines landed in the ring (loader -> consumers)
+  int cur[NCW];     // first line each consumer may still read (consumers -> loader)
+  int cbar;         // consumer barrier arrivals
+  int abort_;       // set on any timeout in this workgroup
+  int pad[2];
+  float red[16];    // cross-wave reduction scratch
+};
+
+__device__ __forceinline__ uint32_t tag_of(int layer, int edge) { return static_cast<uint32_t>(layer * 8 + edge + 1); }
+
+__device__ __forceinline__ int lds_ld(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void lds_st(int* p, int v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Bounded wait bookkeeping (one per wave).
+struct Spin {
+  uint64_t t0 = 0;
+  uint32_t n = 0;
+  // true when the wait must give up (timeout here, or an abort raised elsewhere)
+  __device__ __forceinline__ bool tick(Ctl* c, int* ctl, uint64_t limit, bool global_check) {
+    __builtin_amdgcn_s_sleep(1);
+    if ((++n & 31) != 0) return false;
+    if (lds_ld(&c->abort_)) return true;
+    if (global_check && __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+      __hip_atomic_store(&c->abort_, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return true;
+    }
+    const uint64_t t = wall_clock64();
+    if (t0 == 0) t0 = t;
+    if (t - t0 > limit) {
+      if ((threadIdx.x & 63) == 0) atomicAdd(ctl, 1);
+      __hip_atomic_store(&c->abort_, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return true;
+    }
+    return false;
+  }
+};
+
+__device__ __forceinline__ void gstore(uint64_t* gran, int idx, uint32_t tag, uint32_t val) {
+  __hip_atomic_store((gu64*)(gran + idx), (static_cast<unsigned long long>(tag) << 32) | val,
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t gload(const uint64_t* gran, int idx) {
+  return __hip_atomic_load((gu64*)(const_cast<uint64_t*>(gran) + idx), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+__device__ __forceinline__ float bitsf(uint32_t u) { return __uint_as_float(u); }
+
+// ---------------------------------------------------------------- work geometry
+struct Geo {
+  int H, F, Hq, Hkv, G, WPG, RPW, RO, FW, LH, LA, LF;
+  int off_o, off_gu, off_dn, LL;
+  __device__ __forceinline__ Geo(const Args& a) {
+    H = a.H; F = a.F; Hq = a.Hq; Hkv = a.Hkv; G = Hq / Hkv;
+    WPG = NWG / Hkv;
+    RPW = (G + 2) * HD / WPG;
+    RO = H / NWG;
+    FW = F / NWG;
+    LH = H / 512; LA = Hq * HD / 512; LF = F / 512;
+    off_o = RPW * LH;
+    off_gu = off_o + RO * LA;
+    off_dn = off_gu + 2 * FW * LH;
+    LL = off_dn + RO * LF;
+  }
+  // row (of the projection's weight) of row r of this workgroup in phase p
+  __device__ __forceinline__ int row(int p, int w, int r) const {
+    if (p == P_QKV) {
+      const int h = w / WPG, idx = (w % WPG) * RPW + r;
+      if (idx < G * HD) return h * G * HD + idx;
+      if (idx < (G + 1) * HD) return Hq * HD + h * HD + (idx - G * HD);
+      return (Hq + Hkv) * HD + h * HD + (idx - (G + 1) * HD);
+    }
+    if (p == P_GU) {  // unit u = rows 4u..4u+3: gate(f0) up(f0) gate(f0+1) up(f0+1)
+      const int f = w * FW + 2 * (r >> 2) + ((r >> 1) & 1);
+      return 32 * (f >> 4) + (f & 15) + ((r & 1) ? 16 : 0);
+    }
+    return w * RO + r;  // O, down
+  }
+  __device__ __forceinline__ int nrows(int p) const { return p == P_QKV ? RPW : p == P_GU ? 2 * FW : RO; }
+  __device__ __forceinline__ int lpr(int p) const { return p == P_O ? LA : p == P_DN ? LF : LH; }
+  __device__ __forceinline__ int K(int p) const { return lpr(p) * 512; }
+  __device__ __forceinline__ int poff(int p) const {
+    return p == P_QKV ? 0 : p == P_O ? off_o : p == P_GU ? off_gu : off_dn;
+  }
+};
+
+// ---------------------------------------------------------------- loader (wave 0)
+__device__ void loader(const Args& a, const Geo& g, Ctl* c, uint8_t* ring) {
+  const int lane = threadIdx.x & 63;
+  const int RL = a.ring_lines, nslot = RL / SLOT;
+  const uint64_t limit = static_cast<uint64_t>(__hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const int w = blockIdx.x;
+  int j = 0, rpos = 0, pub = 0;
+  bool dead = false;
+  uint64_t free_wait = 0;
+  for (int layer = 0; layer < a.L && !dead; ++layer) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (dead) break;
+      const uint8_t* W = reinterpret_cast<const uint8_t*>(a.wptr[layer * 4 + p]);
+      const int lp = g.lpr(p), nr = g.nrows(p);
+      const int64_t rowbytes = static_cast<int64_t>(lp) * LINE;
+      for (int r = 0; r < nr && !dead; ++r) {
+        const uint8_t* src = W + static_cast<int64_t>(g.row(p, w, r)) * rowbytes + lane * 16;
+        for (int cc = 0; cc < lp; ++cc, ++j) {
+          if ((j & (SLOT - 1)) == 0) {
+            const int slot = j / SLOT;
+            const int need = (slot - nslot + 1) * SLOT;  // every consumer past the slot being refilled
+            if (need > 0) {
+              int mn = min(lds_ld(&c->cur[0]), min(lds_ld(&c->cur[1]), lds_ld(&c->cur[2])));
+              if (mn < need) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                pub = j;
+                lds_st(&c->landed, pub);  // everything issued has landed
+                Spin sp;
+                const uint64_t tw = a.stamps ? wall_clock64() : 0;
+                while (mn < need) {
+                  if (sp.tick(c, a.ctl, limit, false)) { dead = true; break; }
+                  mn = min(lds_ld(&c->cur[0]), min(lds_ld(&c->cur[1]), lds_ld(&c->cur[2])));
+                }
+                if (a.stamps) free_wait += wall_clock64() - tw;
+                if (dead) break;
+              }
+            }
+          }
+          glds16_nt(src + cc * LINE, ring + rpos * LINE);
+          if (++rpos == RL) rpos = 0;
+          if ((j & (SLOT - 1)) == SLOT - 1) {
+            asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // the slot issued two slots ago has landed
+            const int done = (j / SLOT - 1) * SLOT;
+            if (done > pub) {
+              pub = done;
+              lds_st(&c->landed, pub);
+            }
+          }
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_st(&c->landed, dead ? 0x7fffffff : j);
+  if (a.stamps && lane == 0) {
+    uint64_t* st = a.stamps + static_cast<int64_t>(NWG) * a.L * NSTAMP + blockIdx.x * 4;
+    st[0] = free_wait;
+    st[1] = wall_clock64();
+  }
+}
+
+// ---------------------------------------------------------------- consumer helpers
+struct Cons {
+  const Args& a;
+  const Geo& g;
+  Ctl* c;
+  const uint8_t* ring;
+  int cw, lane, ctid;
+  int landed_cache;
+  int cbar_seq;
+  uint64_t limit;
+  uint64_t line_wait = 0;  // diagnostics: wall-clock ticks spent waiting for ring lines
+  __device__ Cons(const Args& a_, const Geo& g_, Ctl* c_, const uint8_t* r_)
+      : a(a_), g(g_), c(c_), ring(r_) {
+    ctid = threadIdx.x - 64;
+    cw = ctid >> 6;
+    lane = threadIdx.x & 63;
+    landed_cache = 0;
+    cbar_seq = 0;
+    limit = static_cast<uint64_t>(__hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  }
+  __device__ __forceinline__ bool aborted() const { return lds_ld(&c->abort_) != 0; }
+
+  // barrier of the three consumer waves (the loader never joins)
+  __device__ void cbar() {
+    cbar_seq += NCW;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(&c->cbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    Spin sp;
+    while (lds_ld(&c->cbar) < cbar_seq)
+      if (sp.tick(c, a.ctl, limit, false)) break;
+    asm volatile("" ::: "memory");  // no LDS access moves above the poll (LDS is in order per wave)
+  }
+  __device__ __forceinline__ void set_cur(int line) {
+    if (lane == 0) lds_st(&c->cur[cw], line);
+  }
+  __device__ __forceinline__ void wait_line(int j) {
+    if (j < landed_cache) return;
+    Spin sp;
+    int l = lds_ld(&c->landed);
+    const uint64_t tw = (a.stamps && l <= j) ? wall_clock64() : 0;
+    while (l <= j) {
+      if (sp.tick(c, a.ctl, limit, false)) { l = 0x7fffffff; break; }
+      l = lds_ld(&c->landed);
+    }
+    asm volatile("" ::: "memory");
+    if (tw) line_wait += wall_clock64() - tw;
+    landed_cache = l;
+  }
+  // dot(x[0:K], W[row]) for the row whose first ring line is global line j0; x bf16 in LDS
+  __device__ float dot_row(int j0, int lp, const uint16_t* x) {
+    float acc0 = 0.f, acc1 = 0.f;
+    const int RL = a.ring_lines;
+    int rp = j0 % RL;
+    for (int cc = 0; cc < lp; ++cc) {
+      wait_line(j0 + cc);
+      const uint4 wv = *reinterpret_cast<const uint4*>(ring + rp * LINE + lane * 16);
+      const uint4 xv = *reinterpret_cast<const uint4*>(x + cc * 512 + lane * 8);
+      acc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv.x), __builtin_bit_cast(bf2_t, xv.x), acc0, false);
+      acc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv.y), __builtin_bit_cast(bf2_t, xv.y), acc1, false);
+      acc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv.z), __builtin_bit_cast(bf2_t, xv.z), acc0, false);
+      acc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv.w), __builtin_bit_cast(bf2_t, xv.w), acc1, false);
+      if (++rp == RL) rp = 0;
+    }
+    return wave_sum(acc0 + acc1);
+  }
+
+  // Sweep n granules (src index = map(i)) until every tag matches; data -> dst[i].
+  // The three consumer waves split the work; callers cbar() after.
+  template <typename Map>
+  __device__ void gather(int n, uint32_t tag, uint32_t* dst, Map map) {
+    constexpr int B = 8;
+    for (int base = cw * 64 * B; base < n; base += CT * B) {
+      uint64_t v[B];
+      Spin sp;
+      for (;;) {
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+          const int i = base + k * 64 + lane;
+          v[k] = i < n ? gload(a.gran, map(i)) : (static_cast<uint64_t>(tag) << 32);
+          ok &= static_cast<uint32_t>(v[k] >> 32) == tag;
+        }
+        if (__all(ok)) break;
+        if (sp.tick(c, a.ctl, limit, true)) break;
+      }
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        const int i = base + k * 64 + lane;
+        if (i < n) dst[i] = static_cast<uint32_t>(v[k]);
+      }
+    }
+  }
+
+  // sum of squares of the bf16 vector x[0:n] over the consumer threads -> rsqrt(ms + eps)
+  __device__ float norm_scale(const uint16_t* x, int n) {
+    float s = 0.f;
+    for (int i = ctid * 8; i < n; i += CT * 8) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + i), f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += f[k] * f[k];
+    }
+    s = wave_sum(s);
+    if (lane == 0) c->red[cw] = s;
+    cbar();
+    const float tot = c->red[0] + c->red[1] + c->red[2];
+    const float rs = rsqrtf(tot / static_cast<float>(n) + a.eps);
+    cbar();  // red[] is reused by the next reduction
+    return rs;
+  }
+};
+
+__device__ __forceinline__ float bf16r(float f) { return bf2f(f2bf(f)); }
+
+// ---------------------------------------------------------------- attention (split i of group h)
+__device__ void attention(Cons& k, int layer, int h, int i, uint8_t* scratch) {
+  const Args& a = k.a;
+  const Geo& g = k.g;
+  const int G = g.G, S = a.S_att;
+  const int ctx = a.seq_lens[0], pos = a.positions[0], slot = a.slot_mapping[0];
+  const int cs = (ctx + S - 1) / S;
+  const int kb = min(i * cs, ctx), ke = min(kb + cs, ctx);
+  // scratch layout (floats): gq[(G+2)*128] | qb (bf16 G*128) | knew, vnew (bf16 128 each)
+  //                          | pw[NCW][G][64] | wm[NCW][G] wl[NCW][G] | wo[NCW][G][128]
+  float* gq = reinterpret_cast<float*>(scratch);
+  uint16_t* qb = reinterpret_cast<uint16_t*>(gq + (G + 2) * HD);
+  uint16_t* knew = qb + G * HD;
+  uint16_t* vnew = knew + HD;
+  float* pw = reinterpret_cast<float*>(vnew + HD);
+  float* wm = pw + NCW * G * 64;
+  float* wl = wm + NCW * G;
+  float* wo = wl + NCW * G;
+
+  // A: this group's q/k/v rows (fp32, normed projections)
+  const int q0 = h * G * HD, k0 = g.Hq * HD + h * HD, v0 = (g.Hq + g.Hkv) * HD + h * HD;
+  const int nq = (G + 2) * HD;
+  k.gather(nq, tag_of(layer, E_QKV), reinterpret_cast<uint32_t*>(gq), [&](int x) {
+    return a.g_qkv + (x < G * HD ? q0 + x : x < (G + 1) * HD ? k0 + (x - G * HD) : v0 + (x - (G + 1) * HD));
+  });
+  k.cbar();
+  // B: RoPE (rotate-half pairs d, d + 64) and bf16 rounding
+  const float* csr = a.cos_sin + static_cast<int64_t>(pos) * HD;
+  for (int it = k.ctid; it < (G + 1) * 64 + 64; it += CT) {
+    if (it < (G + 1) * 64) {
+      const int hh = it >> 6, d = it & 63;
+      float x1 = gq[hh * HD + d], x2 = gq[hh * HD + d + 64];
+      if (a.apply_rope) {
+        const float cv = csr[d], sv = csr[64 + d];
+        const float y1 = x1 * cv - x2 * sv, y2 = x2 * cv + x1 * sv;
+        x1 = y1;
+        x2 = y2;
+      }
+      uint16_t* o = hh < G ? qb + hh * HD : knew;
+      o[d] = f2bf(x1);
+      o[d + 64] = f2bf(x2);
+    } else {
+      const int d = 2 * (it - (G + 1) * 64);
+      vnew[d] = f2bf(gq[(G + 1) * HD + d]);
+      vnew[d + 1] = f2bf(gq[(G + 1) * HD + d + 1]);
+    }
+  }
+  k.cbar();
+  uint16_t* kc = reinterpret_cast<uint16_t*>(a.kvptr[layer * 2 + 0]);
+  uint16_t* vc = reinterpret_cast<uint16_t*>(a.kvptr[layer * 2 + 1]);
+  const int bs = a.bs;
+  // the split owning the new key appends it to the paged cache (read from LDS here;
+  // the next step's launch reads it from the cache)
+  if (slot >= 0 && kb <= ctx - 1 && ctx - 1 < ke && k.cw == 0) {
+    const int64_t dst = ((static_cast<int64_t>(slot / bs) * g.Hkv + h) * bs + slot % bs) * HD;
+    const int lane = k.lane;
+    reinterpret_cast<uint32_t*>(kc + dst)[lane] = reinterpret_cast<const uint32_t*>(knew)[lane];
+    reinterpret_cast<uint32_t*>(vc + dst)[lane] = reinterpret_cast<const uint32_t*>(vnew)[lane];
+  }
+  // C: each consumer wave takes a contiguous third of the split's keys
+  const int nk = ke - kb, per = (nk + NCW - 1) / NCW;
+  const int wb = min(kb + k.cw * per, ke), we = min(wb + per, ke);
+  const int lane = k.lane;
+  float m[8], l[8], o0[8], o1[8];
+#pragma unroll
+  for (int gg = 0; gg < 8; ++gg) { m[gg] = -INFINITY; l[gg] = 0.f; o0[gg] = 0.f; o1[gg] = 0.f; }
+  const int32_t* bt = a.block_table;
+  float* mypw = pw + k.cw * G * 64;
+  for (int t0 = wb; t0 < we; t0 += 64) {
+    const int t = t0 + lane;
+    const bool valid = t < we;
+    float s[8];
+#pragma unroll
+    for (int gg = 0; gg < 8; ++gg) s[gg] = 0.f;
+    if (valid) {
+      const uint16_t* kr;
+      if (t == ctx - 1) {
+        kr = knew;
+      } else {
+        const int page = bt[t / bs];
+        kr = kc + ((static_cast<int64_t>(page) * g.Hkv + h) * bs + t % bs) * HD;
+      }
+      for (int d = 0; d < HD; d += 8) {
+        float kf[8];
+        unpack8(*reinterpret_cast<const uint4*>(kr + d), kf);
+#pragma unroll
+        for (int gg = 0; gg < 8; ++gg) {
+          if (gg < G) {
+            float qf[8];
+            unpack8(*reinterpret_cast<const uint4*>(qb + gg * HD + d), qf);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s[gg] += qf[e] * kf[e];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int gg = 0; gg < 8; ++gg) {
+      if (gg < G) {
+        const float sv = valid ? s[gg] * a.scale : -INFINITY;
+        const float cm = wave_max(sv);
+        const float nm = fmaxf(m[gg], cm);
+        const float alpha = m[gg] == -INFINITY ? 0.f : __expf(m[gg] - nm);
+        const float p = valid ? __expf(sv - nm) : 0.f;
+        l[gg] = l[gg] * alpha + wave_sum(p);
+        o0[gg] *= alpha;
+        o1[gg] *= alpha;
+        m[gg] = nm;
+        mypw[gg * 64 + lane] = p;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int nt = min(64, we - t0);
+    for (int tt = 0; tt < nt; ++tt) {
+      const int tk = t0 + tt;
+      const uint16_t* vr;
+      if (tk == ctx - 1) {
+        vr = vnew;
+      } else {
+        const int page = bt[tk / bs];
+        vr = vc + ((static_cast<int64_t>(page) * g.Hkv + h) * bs + tk % bs) * HD;
+      }
+      const uint32_t vv = reinterpret_cast<const uint32_t*>(vr)[lane];
+      const float va = __uint_as_float(vv << 16), vb = __uint_as_float(vv & 0xFFFF0000u);
+#pragma unroll
+      for (int gg = 0; gg < 8; ++gg) {
+        if (gg < G) {
+          const float p = mypw[gg * 64 + tt];
+          o0[gg] += p * va;
+          o1[gg] += p * vb;
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  for (int gg = 0; gg < G; ++gg) {
+    if (lane == 0) {
+      wm[k.cw * G + gg] = m[gg];
+      wl[k.cw * G + gg] = l[gg];
+    }
+    wo[(k.cw * G + gg) * HD + 2 * lane] = o0[gg];
+    wo[(k.cw * G + gg) * HD + 2 * lane + 1] = o1[gg];
+  }
+  k.cbar();
+  // D: merge the three waves and publish the split's partials: per head {m, l, o[128]}
+  const uint32_t tp = tag_of(layer, E_PART);
+  for (int e = k.ctid; e < G * (HD + 2); e += CT) {
+    const int gg = e / (HD + 2), kk = e % (HD + 2);
+    float M = -INFINITY;
+    for (int w = 0; w < NCW; ++w) M = fmaxf(M, wm[w * G + gg]);
+    float val;
+    if (kk == 0) {
+      val = M;
+    } else {
+      val = 0.f;
+      for (int w = 0; w < NCW; ++w) {
+        const float mw = wm[w * G + gg];
+        const float f = (mw == -INFINITY) ? 0.f : __expf(mw - M);
+        val += f * (kk == 1 ? wl[w * G + gg] : wo[(w * G + gg) * HD + kk - 2]);
+      }
+    }
+    gstore(a.gran, a.g_part + ((h * S + i) * G + gg) * (HD + 2) + kk, tp, fbits(val));
+  }
+  k.cbar();
+  // E: combine one OPW-wide slice of the group's G*128 outputs over the S splits
+  const int OPW = G * HD / S;
+  const int gs = (i * OPW) / HD, d0 = (i * OPW) % HD;
+  const int per_s = OPW + 2;
+  uint32_t* cb = reinterpret_cast<uint32_t*>(scratch);
+  k.gather(S * per_s, tp, cb, [&](int x) {
+    const int s_ = x / per_s, e_ = x % per_s;
+    return a.g_part + ((h * S + s_) * G + gs) * (HD + 2) + (e_ < 2 ? e_ : 2 + d0 + e_ - 2);
+  });
+  k.cbar();
+  const uint32_t ta = tag_of(layer, E_ATTN);
+  for (int t = k.ctid; t < OPW / 2; t += CT) {
+    float M = -INFINITY;
+    for (int s_ = 0; s_ < S; ++s_) M = fmaxf(M, bitsf(cb[s_ * per_s]));
+    float den = 0.f, n0 = 0.f, n1 = 0.f;
+    for (int s_ = 0; s_ < S; ++s_) {
+      const float ms = bitsf(cb[s_ * per_s]);
+      const float f = ms == -INFINITY ? 0.f : __expf(ms - M);
+      den += f * bitsf(cb[s_ * per_s + 1]);
+      n0 += f * bitsf(cb[s_ * per_s + 2 + 2 * t]);
+      n1 += f * bitsf(cb[s_ * per_s + 3 + 2 * t]);
+    }
+    const float inv = den > 0.f ? 1.f / den : 0.f;
+    gstore(a.gran, a.g_attn + ((h * G + gs) * HD + d0) / 2 + t, ta, pack2(n0 * inv, n1 * inv));
+  }
+}
+
+// ---------------------------------------------------------------- consumer main
+__device__ void consumer(const Args& a, const Geo& g, Ctl* c, const uint8_t* ring, uint8_t* smem) {
+  Cons k(a, g, c, ring);
+  uint16_t* xres = reinterpret_cast<uint16_t*>(smem + a.off_xres);
+  uint16_t* xbig = reinterpret_cast<uint16_t*>(smem + a.off_xbig);
+  const int w = blockIdx.x;
+  const int h = w / g.WPG, gi = w % g.WPG;
+  const int lane = k.lane;
+  uint64_t* stp = (a.stamps && k.ctid == 0) ? a.stamps + static_cast<int64_t>(w) * a.L * NSTAMP : nullptr;
+#define B1_STAMP(i) \
+  if (stp) stp[layer * NSTAMP + (i)] = wall_clock64()
+  for (int layer = 0; layer < a.L; ++layer) {
+    const int lbase = layer * g.LL;
+    B1_STAMP(0);
+    // ---- residual stream in: the embedding row, or the previous layer's down outputs
+    if (layer == 0) {
+      for (int x = k.ctid * 8; x < g.H; x += CT * 8)
+        *reinterpret_cast<uint4*>(xres + x) = *reinterpret_cast<const uint4*>(a.resid_in + x);
+    } else {
+      k.gather(g.H / 2, tag_of(layer, E_RESID), reinterpret_cast<uint32_t*>(xres),
+               [&](int x) { return a.g_resid + x; });
+    }
+    k.cbar();
+    float rs = k.norm_scale(xres, g.H);
+    B1_STAMP(1);
+    // ---- QKV rows (fp32 granules)
+    {
+      const uint32_t tq = tag_of(layer, E_QKV);
+      const int lp = g.LH;
+      for (int u = k.cw; u < g.RPW; u += NCW) {
+        const int j0 = lbase + u * lp;
+        k.set_cur(j0);
+        const float v = k.dot_row(j0, lp, xres) * rs;
+        if (lane == 0 && !(w == 0 && a.ctl[2] != 0))  // ctl[2]: fault injection (tests: a dead producer)
+          gstore(a.gran, a.g_qkv + g.row(P_QKV, w, u), tq, fbits(v));
+      }
+      k.set_cur(lbase + g.off_o);
+    }
+    B1_STAMP(2);
+    // ---- attention + combine (the first S_att workgroups of every kv-head group)
+    if (gi < a.S_att) attention(k, layer, h, gi, reinterpret_cast<uint8_t*>(xbig));
+    k.cbar();
+    B1_STAMP(3);
+    k.gather(g.Hq * HD / 2, tag_of(layer, E_ATTN), reinterpret_cast<uint32_t*>(xbig),
+             [&](int x) { return a.g_attn + x; });
+    k.cbar();
+    B1_STAMP(4);
+    // ---- O rows + residual (pairs of rows -> one bf16x2 granule)
+    {
+      const uint32_t tpo = tag_of(layer, E_POST);
+      const int lp = g.LA;
+      for (int u = k.cw; u < g.RO / 2; u += NCW) {
+        const int j0 = lbase + g.off_o + 2 * u * lp;
+        k.set_cur(j0);
+        const float v0 = k.dot_row(j0, lp, xbig);
+        const float v1 = k.dot_row(j0 + lp, lp, xbig);
+        const int r0 = w * g.RO + 2 * u;
+        if (lane == 0) gstore(a.gran, a.g_post + r0 / 2, tpo, pack2(bf2f(xres[r0]) + v0, bf2f(xres[r0 + 1]) + v1));
+      }
+      k.set_cur(lbase + g.off_gu);
+    }
+    B1_STAMP(5);
+    k.cbar();  // every wave is done with the old residual in xres
+    k.gather(g.H / 2, tag_of(layer, E_POST), reinterpret_cast<uint32_t*>(xres), [&](int x) { return a.g_post + x; });
+    k.cbar();
+    rs = k.norm_scale(xres, g.H);
+    B1_STAMP(6);
+    // ---- gate_up: units of two features (4 rows), SiLU gate -> bf16x2 granule
+    {
+      const uint32_t tg = tag_of(layer, E_ACT);
+      const int lp = g.LH;
+      for (int u = k.cw; u < g.FW / 2; u += NCW) {
+        const int j0 = lbase + g.off_gu + 4 * u * lp;
+        k.set_cur(j0);
+        const float g0 = k.dot_row(j0, lp, xres) * rs;
+        const float u0 = k.dot_row(j0 + lp, lp, xres) * rs;
+        const float g1 = k.dot_row(j0 + 2 * lp, lp, xres) * rs;
+        const float u1 = k.dot_row(j0 + 3 * lp, lp, xres) * rs;
+        const float h0 = g0 / (1.f + __expf(-g0)) * u0, h1 = g1 / (1.f + __expf(-g1)) * u1;
+        if (lane == 0) gstore(a.gran, a.g_act + (w * g.FW) / 2 + u, tg, pack2(h0, h1));
+      }
+      k.set_cur(lbase + g.off_dn);
+    }
+    B1_STAMP(7);
+    k.gather(g.F / 2, tag_of(layer, E_ACT), reinterpret_cast<uint32_t*>(xbig), [&](int x) { return a.g_act + x; });
+    k.cbar();
+    B1_STAMP(8);
+    // ---- down rows + residual -> next layer's residual granules
+    {
+      const uint32_t tr = tag_of(layer + 1, E_RESID);
+      const int lp = g.LF;
+      for (int u = k.cw; u < g.RO / 2; u += NCW) {
+        const int j0 = lbase + g.off_dn + 2 * u * lp;
+        k.set_cur(j0);
+        const float v0 = k.dot_row(j0, lp, xbig);
+        const float v1 = k.dot_row(j0 + lp, lp, xbig);
+        const int r0 = w * g.RO + 2 * u;
+        if (lane == 0) gstore(a.gran, a.g_resid + r0 / 2, tr, pack2(bf2f(xres[r0]) + v0, bf2f(xres[r0 + 1]) + v1));
+      }
+      k.set_cur(layer + 1 < a.L ? lbase + g.LL : 0x7fffffff);
+    }
+    B1_STAMP(9);
+    k.cbar();  // xres is overwritten by the next gather
+  }
+#undef B1_STAMP
+  if (stp) a.stamps[static_cast<int64_t>(NWG) * a.L * NSTAMP + w * 4 + 2] = k.line_wait;
+  // ---- final RMSNorm (workgroup 0)
+  if (w == 0) {
+    k.gather(g.H / 2, tag_of(a.L, E_RESID), reinterpret_cast<uint32_t*>(xres), [&](int x) { return a.g_resid + x; });
+    k.cbar();
+    const float rs = k.norm_scale(xres, g.H);
+    for (int x = k.ctid * 8; x < g.H; x += CT * 8) {
+      float v[8], wf[8], o[8];
+      unpack8(*reinterpret_cast<const uint4*>(xres + x), v);
+      unpack8(*reinterpret_cast<const uint4*>(a.final_norm + x), wf);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = v[e] * rs * wf[e];
+      *reinterpret_cast<uint4*>(a.out + x) = pack8(o);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(NTHR, 1) decode_b1_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  Ctl* c = reinterpret_cast<Ctl*>(smem + a.off_ctl);
+  if (threadIdx.x == 0) {
+    c->landed = 0;
+    c->cbar = 0;
+    c->abort_ = 0;
+    for (int i = 0; i < NCW; ++i) c->cur[i] = 0;
+  }
+  __syncthreads();
+  const Geo g(a);
+  if (threadIdx.x < 64)
+    loader(a, g, c, smem);
+  else
+    consumer(a, g, c, smem, smem);
+}
+
+}  // namespace b1
+
+// ---------------------------------------------------------------- host side
+// Plan: LDS carve-up, granule offsets, ring size. Returns the granule count, or -1
+// when the shape is not supported (the caller keeps the multi-launch path).
+int decode_b1_plan(int L, int H, int F, int Hq, int Hkv, int* out /*[12]*/) {
+  using namespace b1;
+  if (Hkv < 1 || Hq % Hkv || NWG % Hkv || H % (512 * 1) || F % 512 || (Hq * HD) % 512) return -1;
+  const int G = Hq / Hkv, WPG = NWG / Hkv;
+  if (G > 8 || ((G + 2) * HD) % WPG) return -1;
+  const int RPW = (G + 2) * HD / WPG, RO = H / NWG, FW = F / NWG;
+  if (H % (2 * NWG) || F % (2 * NWG) || RPW < NCW || RO / 2 < NCW || FW / 2 < NCW || (FW % 2)) return -1;
+  const int S_att = WPG < 32 ? WPG : 32;
+  if ((G * HD) % S_att || ((G * HD / S_att) % 2)) return -1;
+  // LDS: ring | xres (H bf16) | xbig (max(Hq*128, F) bf16, also the attention scratch) | ctl
+  const int xres = H * 2;
+  const int scratch_attn = ((G + 2) * HD * 4 + G * HD * 2 + 2 * HD * 2 + NCW * G * 64 * 4 + 2 * NCW * G * 4 +
+                            NCW * G * HD * 4);
+  const int scratch_comb = S_att * (G * HD / S_att + 2) * 4;
+  int xbig = std::max(std::max(Hq * HD, F) * 2, std::max(scratch_attn, scratch_comb));
+  xbig = (xbig + 15) & ~15;
+  const int ctl = static_cast<int>(sizeof(Ctl));
+  const int lds_max = 160 * 1024;
+  const int nslot = (lds_max - xres - xbig - ((ctl + 15) & ~15)) / (SLOT * LINE);
+  if (nslot < 4) return -1;
+  const int ring = nslot * SLOT * LINE;
+  int o = 0;
+  out[0] = S_att;
+  out[1] = nslot * SLOT;
+  out[2] = ring;                 // off_xres
+  out[3] = ring + xres;          // off_xbig
+  out[4] = ring + xres + xbig;   // off_ctl
+  out[5] = ring + xres + xbig + ((ctl + 15) & ~15);  // LDS bytes
+  out[6] = o; o += H / 2;                            // g_resid
+  out[7] = o; o += H / 2;                            // g_post
+  out[8] = o; o += (Hq + 2 * Hkv) * HD;              // g_qkv
+  out[9] = o; o += Hkv * S_att * G * (HD + 2);       // g_part
+  out[10] = o; o += Hq * HD / 2;                     // g_attn
+  out[11] = o; o += F / 2;                           // g_act
+  (void)L;
+  return o;
+}
+
+int decode_b1(const uint64_t* wptr, const uint64_t* kvptr, const uint16_t* resid_in, const uint16_t* final_norm,
+              uint16_t* out, const int32_t* positions, const int32_t* slot_mapping, const int32_t* block_table,
+              const int32_t* seq_lens, const float* cos_sin, uint64_t* gran, int* ctl, int L, int H, int F, int Hq,
+              int Hkv, int bs, int apply_rope, float eps, float scale, uint64_t* stamps, hipStream_t st) {
+  using namespace b1;
+  int pl[12];
+  const int ng = decode_b1_plan(L, H, F, Hq, Hkv, pl);
+  if (ng < 0 || bs % 16) return -1;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(decode_b1_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return -2;
+    attr_set = true;
+  }
+  Args a{};
+  a.wptr = wptr; a.kvptr = kvptr; a.resid_in = resid_in; a.final_norm = final_norm; a.out = out;
+  a.positions = positions; a.slot_mapping = slot_mapping; a.block_table = block_table; a.seq_lens = seq_lens;
+  a.cos_sin = cos_sin; a.gran = gran; a.ctl = ctl;
+  a.L = L; a.H = H; a.F = F; a.Hq = Hq; a.Hkv = Hkv; a.bs = bs; a.apply_rope = apply_rope;
+  a.eps = eps; a.scale = scale;
+  a.S_att = pl[0]; a.ring_lines = pl[1];
+  a.off_xres = pl[2]; a.off_xbig = pl[3]; a.off_ctl = pl[4];
+  a.stamps = stamps;
+  a.g_resid = pl[6]; a.g_post = pl[7]; a.g_qkv = pl[8]; a.g_part = pl[9]; a.g_attn = pl[10]; a.g_act = pl[11];
+  if (hipMemsetAsync(gran, 0, static_cast<size_t>(ng) * 8, st) != hipSuccess) return -3;
+  hipLaunchKernelGGL(decode_b1_kernel, dim3(NWG), dim3(NTHR), pl[5], st, a);
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+}  // namespace xgk

@@ -24,6 +24,7 @@ import torch
 
 from .. import ops
 from ..models.base import AttnMeta
+from ..ops import persistent
 from ..ops.attention import DecodeWorkspace
 from ..parallel import comm
 
@@ -178,6 +179,7 @@ class ModelRunner:
         ar = comm.custom_allreduce()
         if ar is not None:
             ar.set_timeout(seconds)
+        persistent.set_timeout_all(seconds)
 
     @torch.no_grad()
     def capture_graphs(self):
@@ -258,12 +260,14 @@ class ModelRunner:
         ar = comm.custom_allreduce()
         if ar is not None:
             ar.poll_async()
+        persistent.poll_all()
 
     @staticmethod
     def _check_comm():
         ar = comm.custom_allreduce()
         if ar is not None:
             ar.check()
+        persistent.check_all()
 
     def _record_out(self, n: int, tok: torch.Tensor, lp: torch.Tensor, hidden, graph: bool):
         """Tokens / logprobs D2H into the next of the two pinned buffers + an event."""
