@@ -30,21 +30,27 @@ def main():
                                  max_num_batched_tokens=8192, max_model_len=a.prompt_len + 64, use_graphs=False),
                     model=model)
     prompt = [128000] + [(31 * i + 7) % 120000 for i in range(a.prompt_len - 1)]
-    eng.add_request("r", prompt, SamplingParams(max_tokens=a.steps + 4, temperature=0.0, ignore_eos=True))
-    n = 0
-    reports = []
-    while eng.has_work():
+    eng.add_request("r", prompt, SamplingParams(max_tokens=32, temperature=0.0, ignore_eos=True))
+    reports = {}
+    modes = {0: "full", 1: "loader alone (consumers ignore the ring)", 2: "consumers alone (no weight loads)",
+             5: "loader alone, no projection work"}
+    for _ in range(3):
         eng.step()
-        n += 1
-        if n == 3:
-            model._b1.enable_stamps()
-        elif n > 3 and model._b1 is not None and model._b1.stamps is not None:
-            torch.cuda.synchronize()
-            reports.append(model._b1.stamp_report())
     dec = model._b1
-    print(json.dumps({"model": a.model, "prompt_len": a.prompt_len, "L": dec.L, "ring_lines": dec.plan[2],
-                      "phases_us": {k: [round(v[0], 1), round(v[1], 1)] for k, v in reports[-1].items()},
-                      "timeouts": dec.timeouts()}))
+    dec.enable_stamps()
+    for m in (0, 1, 2, 5):
+        torch.cuda.synchronize()
+        dec.ctl[3].fill_(m)
+        for _ in range(3):  # async scheduling: the mode is live from the second step on
+            eng.step()
+        torch.cuda.synchronize()
+        reports[modes[m]] = dec.stamp_report()
+    dec = model._b1
+    dec.ctl[3].zero_()
+    for name, rep in reports.items():
+        print(json.dumps({"model": a.model, "prompt_len": a.prompt_len, "L": dec.L, "ring_lines": dec.plan[2],
+                          "mode": name, "phases_us": {k: [round(v[0], 1), round(v[1], 1)] for k, v in rep.items()},
+                          "timeouts": dec.timeouts()}))
 
 
 if __name__ == "__main__":

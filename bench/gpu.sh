@@ -88,6 +88,8 @@ sweep)
       qkv8t8 o8t8 gate_up8t8 down8t8 qkv70t2 o70t2 gate_up70t2 down70t2 qkv70t4 o70t4 gate_up70t4 down70t4 ;;
 profile)
   bash bench/profile.sh "$o" "$@" ;;
+dmaprobe)
+  run dma_probe 120 ./bench/dma_probe.bin ;;
 b1stamps)
   run stamps 300 python -u bench/b1_stamps.py "$@" ;;
 b1)

@@ -68,7 +68,8 @@ struct Args {
   const int32_t* seq_lens;    // [1] (includes the new token)
   const float* cos_sin;       // [max_pos, 128] = [cos | sin]
   uint64_t* gran;             // granule area (zeroed before each launch)
-  int* ctl;                   // [0] timeouts, [1] wait limit in wall-clock ticks, [2] test: drop WG 0's QKV
+  int* ctl;                   // [0] timeouts, [1] wait limit in wall-clock ticks, [2] test: drop WG 0's QKV,
+                              // [3] diagnostics: 1 = consumers ignore the ring, 2 = no weight loads
   int L, H, F, Hq, Hkv, bs, apply_rope;
   float eps, scale;
   // derived on the host (decode_b1_plan)
@@ -77,7 +78,7 @@ struct Args {
   int g_resid, g_post, g_qkv, g_part, g_attn, g_act;  // granule offsets
   uint64_t* stamps;  // diagnostics (null in production): per-(workgroup, layer) phase clocks
 };
-constexpr int NSTAMP = 10;
+constexpr int NSTAMP = 16;
 
 // LDS control block
 struct Ctl {
@@ -86,8 +87,11 @@ struct Ctl {
   int cbar;         // consumer barrier arrivals
   int abort_;       // set on any timeout in this workgroup
   int pad[2];
+  int pages[512];   // KV pages of this workgroup's key split (block_table[kb / bs ...])
   float red[16];    // cross-wave reduction scratch
+  float res[256];   // per-item partial dot products of the current phase
 };
+constexpr int SEG = 8;  // ring lines per work item (one wave reduction each)
 
 __device__ __forceinline__ uint32_t tag_of(int layer, int edge) { return static_cast<uint32_t>(layer * 8 + edge + 1); }
 
@@ -101,10 +105,15 @@ __device__ __forceinline__ void lds_st(int* p, int v) {
 struct Spin {
   uint64_t t0 = 0;
   uint32_t n = 0;
-  // true when the wait must give up (timeout here, or an abort raised elsewhere)
+  // true when the wait must give up (timeout here, or an abort raised elsewhere).
+  // LDS polls sleep ~30 ns per pass; global (granule) polls ~0.25 us: every pass of a
+  // sweep is L2 / fabric traffic that delays the weight stream of the whole chip.
   __device__ __forceinline__ bool tick(Ctl* c, int* ctl, uint64_t limit, bool global_check) {
-    __builtin_amdgcn_s_sleep(1);
-    if ((++n & 31) != 0) return false;
+    if (global_check)
+      __builtin_amdgcn_s_sleep(2);
+    else
+      __builtin_amdgcn_s_sleep(1);
+    if ((++n & (global_check ? 7 : 31)) != 0) return false;
     if (lds_ld(&c->abort_)) return true;
     if (global_check && __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
       __hip_atomic_store(&c->abort_, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -131,6 +140,23 @@ __device__ __forceinline__ uint64_t gload(const uint64_t* gran, int idx) {
 }
 
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+
+// Sum over the 64 lanes with DPP moves only (no LDS crossbar): xor 1, xor 2, half-row
+// mirror, row mirror, then row_bcast15 / row_bcast31 fold the four rows into lane 63;
+// the result is read back as a wave-uniform value.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp<0xB1>(v);         // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);         // quad_perm [2,3,0,1]
+  v += dpp<0x141>(v);        // row_half_mirror
+  v += dpp<0x140>(v);        // row_mirror
+  v += dpp<0x142, 0xA>(v);   // row_bcast15 -> rows 1, 3
+  v += dpp<0x143, 0xC>(v);   // row_bcast31 -> rows 2, 3
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 __device__ __forceinline__ float bitsf(uint32_t u) { return __uint_as_float(u); }
 
 // ---------------------------------------------------------------- work geometry
@@ -172,14 +198,28 @@ struct Geo {
 };
 
 // ---------------------------------------------------------------- loader (wave 0)
-__device__ void loader(const Args& a, const Geo& g, Ctl* c, uint8_t* ring) {
+__device__ __forceinline__ int min_cur(Ctl* c) {
+  return __builtin_amdgcn_readfirstlane(min(lds_ld(&c->cur[0]), min(lds_ld(&c->cur[1]), lds_ld(&c->cur[2]))));
+}
+__device__ __forceinline__ void publish(Ctl* c, int& pub, int lines) {
+  if (lines > pub) {
+    pub = lines;
+    lds_st(&c->landed, pub);
+  }
+}
+
+__device__ __forceinline__ void loader(const Args& a, const Geo& g, Ctl* c, uint8_t* ring) {
   const int lane = threadIdx.x & 63;
-  const int RL = a.ring_lines, nslot = RL / SLOT;
+  const int RL = a.ring_lines;
   const uint64_t limit = static_cast<uint64_t>(__hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const int w = blockIdx.x;
   int j = 0, rpos = 0, pub = 0;
   bool dead = false;
   uint64_t free_wait = 0;
+  if (a.ctl[3] & 2) {  // diagnostics: consumers alone
+    lds_st(&c->landed, 0x7fffffff);
+    return;
+  }
   for (int layer = 0; layer < a.L && !dead; ++layer) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
@@ -190,35 +230,37 @@ __device__ void loader(const Args& a, const Geo& g, Ctl* c, uint8_t* ring) {
       for (int r = 0; r < nr && !dead; ++r) {
         const uint8_t* src = W + static_cast<int64_t>(g.row(p, w, r)) * rowbytes + lane * 16;
         for (int cc = 0; cc < lp; ++cc, ++j) {
-          if ((j & (SLOT - 1)) == 0) {
-            const int slot = j / SLOT;
-            const int need = (slot - nslot + 1) * SLOT;  // every consumer past the slot being refilled
-            if (need > 0) {
-              int mn = min(lds_ld(&c->cur[0]), min(lds_ld(&c->cur[1]), lds_ld(&c->cur[2])));
-              if (mn < need) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                pub = j;
-                lds_st(&c->landed, pub);  // everything issued has landed
-                Spin sp;
-                const uint64_t tw = a.stamps ? wall_clock64() : 0;
-                while (mn < need) {
-                  if (sp.tick(c, a.ctl, limit, false)) { dead = true; break; }
-                  mn = min(lds_ld(&c->cur[0]), min(lds_ld(&c->cur[1]), lds_ld(&c->cur[2])));
+          if ((j & 7) == 0) {
+            // group of 8 lines: it overwrites lines [j - RL, j - RL + 8), free once every
+            // consumer's current item starts at or past j - RL + 8
+            const int need = j + 8 - RL;
+            if (need > 0 && min_cur(c) < need) {
+              // ring full: publish what has landed in steps, keeping the rest of the DMA
+              // pipeline in flight (a full drain restarted it from empty every time)
+              const uint64_t tw = a.stamps ? wall_clock64() : 0;
+              asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+              publish(c, pub, j - 32);
+              if (min_cur(c) < need) {
+                asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                publish(c, pub, j - 16);
+                if (min_cur(c) < need) {
+                  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                  publish(c, pub, j);
+                  Spin sp;
+                  while (min_cur(c) < need)
+                    if (sp.tick(c, a.ctl, limit, false)) { dead = true; break; }
                 }
-                if (a.stamps) free_wait += wall_clock64() - tw;
-                if (dead) break;
               }
+              if (a.stamps) free_wait += wall_clock64() - tw;
+              if (dead) break;
             }
           }
           glds16_nt(src + cc * LINE, ring + rpos * LINE);
           if (++rpos == RL) rpos = 0;
-          if ((j & (SLOT - 1)) == SLOT - 1) {
-            asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // the slot issued two slots ago has landed
-            const int done = (j / SLOT - 1) * SLOT;
-            if (done > pub) {
-              pub = done;
-              lds_st(&c->landed, pub);
-            }
+          if ((j & 7) == 7) {
+            // vmcnt counts this wave's DMAs in issue order: all but the last 48 have landed
+            asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+            publish(c, pub, j + 1 - 48);
           }
         }
       }
@@ -242,23 +284,29 @@ struct Cons {
   int cw, lane, ctid;
   int landed_cache;
   int cbar_seq;
+  int mode;
   uint64_t limit;
   uint64_t line_wait = 0;  // diagnostics: wall-clock ticks spent waiting for ring lines
-  __device__ Cons(const Args& a_, const Geo& g_, Ctl* c_, const uint8_t* r_)
+  uint64_t* stp = nullptr;  // diagnostics: this workgroup's phase clocks (consumer thread 0)
+  __device__ __forceinline__ void stamp(int layer, int i) {
+    if (stp) stp[layer * NSTAMP + i] = wall_clock64();
+  }
+  __device__ __forceinline__ Cons(const Args& a_, const Geo& g_, Ctl* c_, const uint8_t* r_)
       : a(a_), g(g_), c(c_), ring(r_) {
     ctid = threadIdx.x - 64;
-    cw = ctid >> 6;
+    cw = __builtin_amdgcn_readfirstlane(ctid >> 6);  // wave-uniform: item loops and branches stay scalar
     lane = threadIdx.x & 63;
     landed_cache = 0;
     cbar_seq = 0;
+    mode = a.ctl[3];
     limit = static_cast<uint64_t>(__hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   }
   __device__ __forceinline__ bool aborted() const { return lds_ld(&c->abort_) != 0; }
 
   // barrier of the three consumer waves (the loader never joins)
-  __device__ void cbar() {
+  __device__ __forceinline__ void cbar() {
     cbar_seq += NCW;
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS only: global traffic needs no barrier here
     if (lane == 0) __hip_atomic_fetch_add(&c->cbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     Spin sp;
     while (lds_ld(&c->cbar) < cbar_seq)
@@ -266,10 +314,11 @@ struct Cons {
     asm volatile("" ::: "memory");  // no LDS access moves above the poll (LDS is in order per wave)
   }
   __device__ __forceinline__ void set_cur(int line) {
+    if (mode & 1) line = 0x7fffffff;  // diagnostics: the loader alone
     if (lane == 0) lds_st(&c->cur[cw], line);
   }
   __device__ __forceinline__ void wait_line(int j) {
-    if (j < landed_cache) return;
+    if (j < landed_cache || (mode & 1)) return;
     Spin sp;
     int l = lds_ld(&c->landed);
     const uint64_t tw = (a.stamps && l <= j) ? wall_clock64() : 0;
@@ -279,43 +328,67 @@ struct Cons {
     }
     asm volatile("" ::: "memory");
     if (tw) line_wait += wall_clock64() - tw;
-    landed_cache = l;
+    landed_cache = __builtin_amdgcn_readfirstlane(l);
   }
-  // dot(x[0:K], W[row]) for the row whose first ring line is global line j0; x bf16 in LDS
-  __device__ float dot_row(int j0, int lp, const uint16_t* x) {
-    float acc0 = 0.f, acc1 = 0.f;
+  // dot(x[0 : 512 * nl], W lines j0 .. j0 + nl) for one row segment (nl <= SEG); x bf16
+  // in LDS. One wait for the whole segment, then every weight and x chunk read is in
+  // flight before the first v_dot2c (a per-line read-then-use loop exposed the LDS
+  // latency on every line); one DPP reduction.
+  __device__ __forceinline__ float dot_row(int j0, int nl, const uint16_t* x) {
+    wait_line(j0 + nl - 1);
     const int RL = a.ring_lines;
-    int rp = j0 % RL;
-    for (int cc = 0; cc < lp; ++cc) {
-      wait_line(j0 + cc);
-      const uint4 wv = *reinterpret_cast<const uint4*>(ring + rp * LINE + lane * 16);
-      const uint4 xv = *reinterpret_cast<const uint4*>(x + cc * 512 + lane * 8);
-      acc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv.x), __builtin_bit_cast(bf2_t, xv.x), acc0, false);
-      acc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv.y), __builtin_bit_cast(bf2_t, xv.y), acc1, false);
-      acc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv.z), __builtin_bit_cast(bf2_t, xv.z), acc0, false);
-      acc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv.w), __builtin_bit_cast(bf2_t, xv.w), acc1, false);
-      if (++rp == RL) rp = 0;
+    const int rp0 = j0 % RL;
+    float acc0 = 0.f, acc1 = 0.f;
+    if (nl == SEG) {  // full segment: branch-free, all 16 LDS reads in flight
+      uint4 wv[SEG], xv[SEG];
+#pragma unroll
+      for (int i = 0; i < SEG; ++i) {
+        const int rp = rp0 + i >= RL ? rp0 + i - RL : rp0 + i;
+        wv[i] = *reinterpret_cast<const uint4*>(ring + rp * LINE + lane * 16);
+        xv[i] = *reinterpret_cast<const uint4*>(x + i * 512 + lane * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < SEG; ++i) {
+        acc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv[i].x), __builtin_bit_cast(bf2_t, xv[i].x), acc0, false);
+        acc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv[i].y), __builtin_bit_cast(bf2_t, xv[i].y), acc1, false);
+        acc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv[i].z), __builtin_bit_cast(bf2_t, xv[i].z), acc0, false);
+        acc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv[i].w), __builtin_bit_cast(bf2_t, xv[i].w), acc1, false);
+      }
+    } else {  // a row's tail segment (K not a multiple of 4096)
+      int rp = rp0;
+      for (int i = 0; i < nl; ++i) {
+        const uint4 wv = *reinterpret_cast<const uint4*>(ring + rp * LINE + lane * 16);
+        const uint4 xv = *reinterpret_cast<const uint4*>(x + i * 512 + lane * 8);
+        acc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv.x), __builtin_bit_cast(bf2_t, xv.x), acc0, false);
+        acc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv.y), __builtin_bit_cast(bf2_t, xv.y), acc1, false);
+        acc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv.z), __builtin_bit_cast(bf2_t, xv.z), acc0, false);
+        acc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv.w), __builtin_bit_cast(bf2_t, xv.w), acc1, false);
+        rp = rp + 1 == RL ? 0 : rp + 1;
+      }
     }
-    return wave_sum(acc0 + acc1);
+    return wave_sum_dpp(acc0 + acc1);
   }
 
   // Sweep n granules (src index = map(i)) until every tag matches; data -> dst[i].
   // The three consumer waves split the work; callers cbar() after.
-  template <typename Map>
-  __device__ void gather(int n, uint32_t tag, uint32_t* dst, Map map) {
-    constexpr int B = 8;
+  template <int B = 16, typename Map>  // B <= 64 granules per lane per pass
+  __device__ __forceinline__ void gather(int n, uint32_t tag, uint32_t* dst, Map map) {
     for (int base = cw * 64 * B; base < n; base += CT * B) {
       uint64_t v[B];
+      uint64_t pend = 0;  // granules of this lane not matched yet: only those are re-read
+#pragma unroll
+      for (int k = 0; k < B; ++k)
+        if (base + k * 64 + lane < n) pend |= 1ull << k;
       Spin sp;
       for (;;) {
-        bool ok = true;
 #pragma unroll
         for (int k = 0; k < B; ++k) {
-          const int i = base + k * 64 + lane;
-          v[k] = i < n ? gload(a.gran, map(i)) : (static_cast<uint64_t>(tag) << 32);
-          ok &= static_cast<uint32_t>(v[k] >> 32) == tag;
+          if (pend & (1ull << k)) {
+            v[k] = gload(a.gran, map(base + k * 64 + lane));
+            if (static_cast<uint32_t>(v[k] >> 32) == tag) pend &= ~(1ull << k);
+          }
         }
-        if (__all(ok)) break;
+        if (__all(pend == 0)) break;
         if (sp.tick(c, a.ctl, limit, true)) break;
       }
 #pragma unroll
@@ -327,7 +400,7 @@ struct Cons {
   }
 
   // sum of squares of the bf16 vector x[0:n] over the consumer threads -> rsqrt(ms + eps)
-  __device__ float norm_scale(const uint16_t* x, int n) {
+  __device__ __forceinline__ float norm_scale(const uint16_t* x, int n) {
     float s = 0.f;
     for (int i = ctid * 8; i < n; i += CT * 8) {
       float f[8];
@@ -348,7 +421,7 @@ struct Cons {
 __device__ __forceinline__ float bf16r(float f) { return bf2f(f2bf(f)); }
 
 // ---------------------------------------------------------------- attention (split i of group h)
-__device__ void attention(Cons& k, int layer, int h, int i, uint8_t* scratch) {
+__device__ __forceinline__ void attention(Cons& k, int layer, int h, int i, uint8_t* scratch) {
   const Args& a = k.a;
   const Geo& g = k.g;
   const int G = g.G, S = a.S_att;
@@ -366,6 +439,46 @@ __device__ void attention(Cons& k, int layer, int h, int i, uint8_t* scratch) {
   float* wl = wm + NCW * G;
   float* wo = wl + NCW * G;
 
+  uint16_t* kc = reinterpret_cast<uint16_t*>(a.kvptr[layer * 2 + 0]);
+  uint16_t* vc = reinterpret_cast<uint16_t*>(a.kvptr[layer * 2 + 1]);
+  const int bs = a.bs;
+  const int lane = k.lane;
+  const int* pg = k.c->pages - kb / 16;  // pg[t / 16] = page of key t (t in [kb, ke))
+  // each consumer wave takes a contiguous third of the split's keys, in chunks of 64
+  const int nk = ke - kb, per = (nk + NCW - 1) / NCW;
+  const int wb = min(kb + k.cw * per, ke), we = min(wb + per, ke);
+  // K rows (lane = key) and V (lane = dim pair, one register per key) of a chunk. The
+  // cached keys do not depend on this step, so the first chunk is requested BEFORE the
+  // QKV hand-off: its HBM latency hides under the wait (a dependent load per key was
+  // ~1.5 us each).
+  uint4 kreg[HD / 8];
+  uint32_t vreg[64];
+// A chunk's (<= 64 keys) pages are at most five 16-key blocks: read them once (LDS),
+// then every K / V address is arithmetic (a page lookup per key serialised ~64 LDS
+// round trips in front of the loads).
+#define B1_LOAD_CHUNK(T0)                                                                               \
+  {                                                                                                     \
+    const int b0_ = (T0) >> 4, o_ = (T0) & 15;                                                          \
+    int pp_[5];                                                                                         \
+    _Pragma("unroll") for (int q_ = 0; q_ < 5; ++q_) pp_[q_] = pg[min(b0_ + q_, (we - 1) >> 4)];       \
+    auto page_ = [&](int q) { return q == 0 ? pp_[0] : q == 1 ? pp_[1] : q == 2 ? pp_[2] : q == 3 ? pp_[3] : pp_[4]; }; \
+    const int t_ = (T0) + lane;                                                                         \
+    if (t_ < we && t_ != ctx - 1) {                                                                     \
+      const uint16_t* kr_ =                                                                             \
+          kc + ((static_cast<int64_t>(page_((o_ + lane) >> 4)) * g.Hkv + h) * 16 + (t_ & 15)) * HD;     \
+      _Pragma("unroll") for (int d_ = 0; d_ < HD / 8; ++d_) kreg[d_] =                                  \
+          *reinterpret_cast<const uint4*>(kr_ + d_ * 8);                                                \
+    }                                                                                                   \
+    _Pragma("unroll") for (int tt_ = 0; tt_ < 64; ++tt_) {                                              \
+      const int tk_ = (T0) + tt_;                                                                       \
+      if (tk_ < we && tk_ != ctx - 1)                                                                   \
+        vreg[tt_] = reinterpret_cast<const uint32_t*>(                                                  \
+            vc + ((static_cast<int64_t>(page_((o_ + tt_) >> 4)) * g.Hkv + h) * 16 + (tk_ & 15)) * HD)[lane]; \
+    }                                                                                                   \
+  }
+  if (wb < we) B1_LOAD_CHUNK(wb);
+  k.stamp(layer, 10);
+
   // A: this group's q/k/v rows (fp32, normed projections)
   const int q0 = h * G * HD, k0 = g.Hq * HD + h * HD, v0 = (g.Hq + g.Hkv) * HD + h * HD;
   const int nq = (G + 2) * HD;
@@ -373,6 +486,7 @@ __device__ void attention(Cons& k, int layer, int h, int i, uint8_t* scratch) {
     return a.g_qkv + (x < G * HD ? q0 + x : x < (G + 1) * HD ? k0 + (x - G * HD) : v0 + (x - (G + 1) * HD));
   });
   k.cbar();
+  k.stamp(layer, 11);
   // B: RoPE (rotate-half pairs d, d + 64) and bf16 rounding
   const float* csr = a.cos_sin + static_cast<int64_t>(pos) * HD;
   for (int it = k.ctid; it < (G + 1) * 64 + 64; it += CT) {
@@ -395,51 +509,42 @@ __device__ void attention(Cons& k, int layer, int h, int i, uint8_t* scratch) {
     }
   }
   k.cbar();
-  uint16_t* kc = reinterpret_cast<uint16_t*>(a.kvptr[layer * 2 + 0]);
-  uint16_t* vc = reinterpret_cast<uint16_t*>(a.kvptr[layer * 2 + 1]);
-  const int bs = a.bs;
+  k.stamp(layer, 12);
   // the split owning the new key appends it to the paged cache (read from LDS here;
   // the next step's launch reads it from the cache)
   if (slot >= 0 && kb <= ctx - 1 && ctx - 1 < ke && k.cw == 0) {
     const int64_t dst = ((static_cast<int64_t>(slot / bs) * g.Hkv + h) * bs + slot % bs) * HD;
-    const int lane = k.lane;
     reinterpret_cast<uint32_t*>(kc + dst)[lane] = reinterpret_cast<const uint32_t*>(knew)[lane];
     reinterpret_cast<uint32_t*>(vc + dst)[lane] = reinterpret_cast<const uint32_t*>(vnew)[lane];
   }
-  // C: each consumer wave takes a contiguous third of the split's keys
-  const int nk = ke - kb, per = (nk + NCW - 1) / NCW;
-  const int wb = min(kb + k.cw * per, ke), we = min(wb + per, ke);
-  const int lane = k.lane;
+  // C: online softmax over the wave's keys
   float m[8], l[8], o0[8], o1[8];
 #pragma unroll
   for (int gg = 0; gg < 8; ++gg) { m[gg] = -INFINITY; l[gg] = 0.f; o0[gg] = 0.f; o1[gg] = 0.f; }
-  const int32_t* bt = a.block_table;
   float* mypw = pw + k.cw * G * 64;
+  const uint32_t vnew_l = reinterpret_cast<const uint32_t*>(vnew)[lane];
   for (int t0 = wb; t0 < we; t0 += 64) {
+    if (t0 != wb) B1_LOAD_CHUNK(t0);
     const int t = t0 + lane;
     const bool valid = t < we;
+    if (t == ctx - 1) {
+#pragma unroll
+      for (int d = 0; d < HD / 8; ++d) kreg[d] = *reinterpret_cast<const uint4*>(knew + d * 8);
+    }
     float s[8];
 #pragma unroll
     for (int gg = 0; gg < 8; ++gg) s[gg] = 0.f;
-    if (valid) {
-      const uint16_t* kr;
-      if (t == ctx - 1) {
-        kr = knew;
-      } else {
-        const int page = bt[t / bs];
-        kr = kc + ((static_cast<int64_t>(page) * g.Hkv + h) * bs + t % bs) * HD;
-      }
-      for (int d = 0; d < HD; d += 8) {
-        float kf[8];
-        unpack8(*reinterpret_cast<const uint4*>(kr + d), kf);
 #pragma unroll
-        for (int gg = 0; gg < 8; ++gg) {
-          if (gg < G) {
-            float qf[8];
-            unpack8(*reinterpret_cast<const uint4*>(qb + gg * HD + d), qf);
+    for (int d = 0; d < HD / 8; ++d) {
+      float kf[8];
+      unpack8(kreg[d], kf);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) s[gg] += qf[e] * kf[e];
-          }
+      for (int gg = 0; gg < 8; ++gg) {
+        if (gg < G) {
+          float qf[8];
+          unpack8(*reinterpret_cast<const uint4*>(qb + gg * HD + d * 8), qf);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s[gg] += qf[e] * kf[e];
         }
       }
     }
@@ -451,7 +556,7 @@ __device__ void attention(Cons& k, int layer, int h, int i, uint8_t* scratch) {
         const float nm = fmaxf(m[gg], cm);
         const float alpha = m[gg] == -INFINITY ? 0.f : __expf(m[gg] - nm);
         const float p = valid ? __expf(sv - nm) : 0.f;
-        l[gg] = l[gg] * alpha + wave_sum(p);
+        l[gg] = l[gg] * alpha + wave_sum_dpp(p);
         o0[gg] *= alpha;
         o1[gg] *= alpha;
         m[gg] = nm;
@@ -460,37 +565,37 @@ __device__ void attention(Cons& k, int layer, int h, int i, uint8_t* scratch) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int nt = min(64, we - t0);
-    for (int tt = 0; tt < nt; ++tt) {
-      const int tk = t0 + tt;
-      const uint16_t* vr;
-      if (tk == ctx - 1) {
-        vr = vnew;
-      } else {
-        const int page = bt[tk / bs];
-        vr = vc + ((static_cast<int64_t>(page) * g.Hkv + h) * bs + tk % bs) * HD;
-      }
-      const uint32_t vv = reinterpret_cast<const uint32_t*>(vr)[lane];
-      const float va = __uint_as_float(vv << 16), vb = __uint_as_float(vv & 0xFFFF0000u);
 #pragma unroll
-      for (int gg = 0; gg < 8; ++gg) {
-        if (gg < G) {
-          const float p = mypw[gg * 64 + tt];
-          o0[gg] += p * va;
-          o1[gg] += p * vb;
+    for (int tt = 0; tt < 64; ++tt) {
+      if (tt < nt) {
+        const uint32_t vv = (t0 + tt == ctx - 1) ? vnew_l : vreg[tt];
+        const float va = __uint_as_float(vv << 16), vb = __uint_as_float(vv & 0xFFFF0000u);
+#pragma unroll
+        for (int gg = 0; gg < 8; ++gg) {
+          if (gg < G) {
+            const float p = mypw[gg * 64 + tt];
+            o0[gg] += p * va;
+            o1[gg] += p * vb;
+          }
         }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
-  for (int gg = 0; gg < G; ++gg) {
-    if (lane == 0) {
-      wm[k.cw * G + gg] = m[gg];
-      wl[k.cw * G + gg] = l[gg];
+#undef B1_LOAD_CHUNK
+#pragma unroll
+  for (int gg = 0; gg < 8; ++gg) {
+    if (gg < G) {
+      if (lane == 0) {
+        wm[k.cw * G + gg] = m[gg];
+        wl[k.cw * G + gg] = l[gg];
+      }
+      wo[(k.cw * G + gg) * HD + 2 * lane] = o0[gg];
+      wo[(k.cw * G + gg) * HD + 2 * lane + 1] = o1[gg];
     }
-    wo[(k.cw * G + gg) * HD + 2 * lane] = o0[gg];
-    wo[(k.cw * G + gg) * HD + 2 * lane + 1] = o1[gg];
   }
   k.cbar();
+  k.stamp(layer, 13);
   // D: merge the three waves and publish the split's partials: per head {m, l, o[128]}
   const uint32_t tp = tag_of(layer, E_PART);
   for (int e = k.ctid; e < G * (HD + 2); e += CT) {
@@ -511,6 +616,7 @@ __device__ void attention(Cons& k, int layer, int h, int i, uint8_t* scratch) {
     gstore(a.gran, a.g_part + ((h * S + i) * G + gg) * (HD + 2) + kk, tp, fbits(val));
   }
   k.cbar();
+  k.stamp(layer, 14);
   // E: combine one OPW-wide slice of the group's G*128 outputs over the S splits
   const int OPW = G * HD / S;
   const int gs = (i * OPW) / HD, d0 = (i * OPW) % HD;
@@ -521,32 +627,67 @@ __device__ void attention(Cons& k, int layer, int h, int i, uint8_t* scratch) {
     return a.g_part + ((h * S + s_) * G + gs) * (HD + 2) + (e_ < 2 ? e_ : 2 + d0 + e_ - 2);
   });
   k.cbar();
+  k.stamp(layer, 15);
+  // lane = split (S <= 32): max, weights and the denominator are wave reductions; each
+  // wave reduces every third output pair (a serial loop over the splits per output was
+  // ~5 us of dependent LDS reads)
   const uint32_t ta = tag_of(layer, E_ATTN);
-  for (int t = k.ctid; t < OPW / 2; t += CT) {
-    float M = -INFINITY;
-    for (int s_ = 0; s_ < S; ++s_) M = fmaxf(M, bitsf(cb[s_ * per_s]));
-    float den = 0.f, n0 = 0.f, n1 = 0.f;
-    for (int s_ = 0; s_ < S; ++s_) {
-      const float ms = bitsf(cb[s_ * per_s]);
-      const float f = ms == -INFINITY ? 0.f : __expf(ms - M);
-      den += f * bitsf(cb[s_ * per_s + 1]);
-      n0 += f * bitsf(cb[s_ * per_s + 2 + 2 * t]);
-      n1 += f * bitsf(cb[s_ * per_s + 3 + 2 * t]);
-    }
+  {
+    const int sl = lane < S ? lane : 0;
+    const float ms = lane < S ? bitsf(cb[sl * per_s]) : -INFINITY;
+    const float M = wave_max(ms);
+    const float f = ms == -INFINITY ? 0.f : __expf(ms - M);
+    const float den = wave_sum_dpp(f * (lane < S ? bitsf(cb[sl * per_s + 1]) : 0.f));
     const float inv = den > 0.f ? 1.f / den : 0.f;
-    gstore(a.gran, a.g_attn + ((h * G + gs) * HD + d0) / 2 + t, ta, pack2(n0 * inv, n1 * inv));
+    for (int t = k.cw; t < OPW / 2; t += NCW) {
+      const float n0 = wave_sum_dpp(f * bitsf(cb[sl * per_s + 2 + 2 * t]));
+      const float n1 = wave_sum_dpp(f * bitsf(cb[sl * per_s + 3 + 2 * t]));
+      if (lane == 0) gstore(a.gran, a.g_attn + ((h * G + gs) * HD + d0) / 2 + t, ta, pack2(n0 * inv, n1 * inv));
+    }
   }
 }
 
 // ---------------------------------------------------------------- consumer main
-__device__ void consumer(const Args& a, const Geo& g, Ctl* c, const uint8_t* ring, uint8_t* smem) {
+// One projection phase: its rows split into work items of <= SEG lines, dealt round-
+// robin to the consumer waves, so the three waves read adjacent lines and the ring
+// space they hold back from the loader stays ~3 items (a whole-row unit per wave held
+// the loader to a few lines of run-ahead on the 32-line gate_up units). Item partials
+// go to c->res; the caller reduces them per row after a cbar.
+__device__ __forceinline__ void phase_items(Cons& k, int jphase, int nrows, int lp, const uint16_t* x, int jnext) {
+  const int ipr = (lp + SEG - 1) / SEG;
+  const int nit = (k.mode & 4) ? 0 : nrows * ipr;  // diagnostics: 4 = no projection work
+  for (int it = k.cw; it < nit; it += NCW) {
+    const int r = it / ipr, l0 = (it % ipr) * SEG;
+    const int j0 = jphase + r * lp + l0;
+    k.set_cur(j0);
+    const float v = k.dot_row(j0, min(SEG, lp - l0), x + l0 * 512);
+    if (k.lane == 0) k.c->res[it] = v;
+  }
+  k.set_cur(jnext);
+  k.cbar();
+}
+__device__ __forceinline__ float row_sum(const Ctl* c, int r, int ipr) {
+  float v = 0.f;
+  for (int i = 0; i < ipr; ++i) v += c->res[r * ipr + i];
+  return v;
+}
+
+__device__ __forceinline__ void consumer(const Args& a, const Geo& g, Ctl* c, const uint8_t* ring, uint8_t* smem) {
   Cons k(a, g, c, ring);
   uint16_t* xres = reinterpret_cast<uint16_t*>(smem + a.off_xres);
   uint16_t* xbig = reinterpret_cast<uint16_t*>(smem + a.off_xbig);
   const int w = blockIdx.x;
   const int h = w / g.WPG, gi = w % g.WPG;
-  const int lane = k.lane;
-  uint64_t* stp = (a.stamps && k.ctid == 0) ? a.stamps + static_cast<int64_t>(w) * a.L * NSTAMP : nullptr;
+  const int ct = k.ctid;
+  const int iH = (g.LH + SEG - 1) / SEG, iA = (g.LA + SEG - 1) / SEG, iF = (g.LF + SEG - 1) / SEG;
+  uint64_t* stp = (a.stamps && ct == 0) ? a.stamps + static_cast<int64_t>(w) * a.L * NSTAMP : nullptr;
+  k.stp = stp;
+  if (gi < a.S_att) {  // the key split's pages, read once for all layers
+    const int ctx = a.seq_lens[0], cs = (ctx + a.S_att - 1) / a.S_att;
+    const int kb = min(gi * cs, ctx), ke = min(kb + cs, ctx);
+    if (ke > kb)
+      for (int p = kb / a.bs + ct; p <= (ke - 1) / a.bs; p += CT) c->pages[p - kb / a.bs] = a.block_table[p];
+  }
 #define B1_STAMP(i) \
   if (stp) stp[layer * NSTAMP + (i)] = wall_clock64()
   for (int layer = 0; layer < a.L; ++layer) {
@@ -554,7 +695,7 @@ __device__ void consumer(const Args& a, const Geo& g, Ctl* c, const uint8_t* rin
     B1_STAMP(0);
     // ---- residual stream in: the embedding row, or the previous layer's down outputs
     if (layer == 0) {
-      for (int x = k.ctid * 8; x < g.H; x += CT * 8)
+      for (int x = ct * 8; x < g.H; x += CT * 8)
         *reinterpret_cast<uint4*>(xres + x) = *reinterpret_cast<const uint4*>(a.resid_in + x);
     } else {
       k.gather(g.H / 2, tag_of(layer, E_RESID), reinterpret_cast<uint32_t*>(xres),
@@ -563,18 +704,13 @@ __device__ void consumer(const Args& a, const Geo& g, Ctl* c, const uint8_t* rin
     k.cbar();
     float rs = k.norm_scale(xres, g.H);
     B1_STAMP(1);
-    // ---- QKV rows (fp32 granules)
+    // ---- QKV rows (norm as a row scale) -> fp32 granules
+    phase_items(k, lbase, g.RPW, g.LH, xres, lbase + g.off_o);
     {
       const uint32_t tq = tag_of(layer, E_QKV);
-      const int lp = g.LH;
-      for (int u = k.cw; u < g.RPW; u += NCW) {
-        const int j0 = lbase + u * lp;
-        k.set_cur(j0);
-        const float v = k.dot_row(j0, lp, xres) * rs;
-        if (lane == 0 && !(w == 0 && a.ctl[2] != 0))  // ctl[2]: fault injection (tests: a dead producer)
-          gstore(a.gran, a.g_qkv + g.row(P_QKV, w, u), tq, fbits(v));
-      }
-      k.set_cur(lbase + g.off_o);
+      const bool drop = w == 0 && a.ctl[2] != 0;  // fault injection (tests: a dead producer)
+      for (int r = ct; r < g.RPW; r += CT)
+        if (!drop) gstore(a.gran, a.g_qkv + g.row(P_QKV, w, r), tq, fbits(row_sum(c, r, iH) * rs));
     }
     B1_STAMP(2);
     // ---- attention + combine (the first S_att workgroups of every kv-head group)
@@ -585,19 +721,15 @@ __device__ void consumer(const Args& a, const Geo& g, Ctl* c, const uint8_t* rin
              [&](int x) { return a.g_attn + x; });
     k.cbar();
     B1_STAMP(4);
-    // ---- O rows + residual (pairs of rows -> one bf16x2 granule)
+    // ---- O rows + residual -> bf16x2 granules
+    phase_items(k, lbase + g.off_o, g.RO, g.LA, xbig, lbase + g.off_gu);
     {
       const uint32_t tpo = tag_of(layer, E_POST);
-      const int lp = g.LA;
-      for (int u = k.cw; u < g.RO / 2; u += NCW) {
-        const int j0 = lbase + g.off_o + 2 * u * lp;
-        k.set_cur(j0);
-        const float v0 = k.dot_row(j0, lp, xbig);
-        const float v1 = k.dot_row(j0 + lp, lp, xbig);
+      for (int u = ct; u < g.RO / 2; u += CT) {
         const int r0 = w * g.RO + 2 * u;
-        if (lane == 0) gstore(a.gran, a.g_post + r0 / 2, tpo, pack2(bf2f(xres[r0]) + v0, bf2f(xres[r0 + 1]) + v1));
+        gstore(a.gran, a.g_post + r0 / 2, tpo,
+               pack2(bf2f(xres[r0]) + row_sum(c, 2 * u, iA), bf2f(xres[r0 + 1]) + row_sum(c, 2 * u + 1, iA)));
       }
-      k.set_cur(lbase + g.off_gu);
     }
     B1_STAMP(5);
     k.cbar();  // every wave is done with the old residual in xres
@@ -605,39 +737,30 @@ __device__ void consumer(const Args& a, const Geo& g, Ctl* c, const uint8_t* rin
     k.cbar();
     rs = k.norm_scale(xres, g.H);
     B1_STAMP(6);
-    // ---- gate_up: units of two features (4 rows), SiLU gate -> bf16x2 granule
+    // ---- gate_up: rows gate(f0) up(f0) gate(f0+1) up(f0+1) per feature pair -> SiLU gate
+    phase_items(k, lbase + g.off_gu, 2 * g.FW, g.LH, xres, lbase + g.off_dn);
     {
       const uint32_t tg = tag_of(layer, E_ACT);
-      const int lp = g.LH;
-      for (int u = k.cw; u < g.FW / 2; u += NCW) {
-        const int j0 = lbase + g.off_gu + 4 * u * lp;
-        k.set_cur(j0);
-        const float g0 = k.dot_row(j0, lp, xres) * rs;
-        const float u0 = k.dot_row(j0 + lp, lp, xres) * rs;
-        const float g1 = k.dot_row(j0 + 2 * lp, lp, xres) * rs;
-        const float u1 = k.dot_row(j0 + 3 * lp, lp, xres) * rs;
-        const float h0 = g0 / (1.f + __expf(-g0)) * u0, h1 = g1 / (1.f + __expf(-g1)) * u1;
-        if (lane == 0) gstore(a.gran, a.g_act + (w * g.FW) / 2 + u, tg, pack2(h0, h1));
+      for (int u = ct; u < g.FW / 2; u += CT) {
+        const float g0 = row_sum(c, 4 * u, iH) * rs, u0 = row_sum(c, 4 * u + 1, iH) * rs;
+        const float g1 = row_sum(c, 4 * u + 2, iH) * rs, u1 = row_sum(c, 4 * u + 3, iH) * rs;
+        gstore(a.gran, a.g_act + (w * g.FW) / 2 + u, tg,
+               pack2(g0 / (1.f + __expf(-g0)) * u0, g1 / (1.f + __expf(-g1)) * u1));
       }
-      k.set_cur(lbase + g.off_dn);
     }
     B1_STAMP(7);
-    k.gather(g.F / 2, tag_of(layer, E_ACT), reinterpret_cast<uint32_t*>(xbig), [&](int x) { return a.g_act + x; });
+    k.gather<40>(g.F / 2, tag_of(layer, E_ACT), reinterpret_cast<uint32_t*>(xbig), [&](int x) { return a.g_act + x; });
     k.cbar();
     B1_STAMP(8);
-    // ---- down rows + residual -> next layer's residual granules
+    // ---- down rows + residual -> the next layer's residual granules
+    phase_items(k, lbase + g.off_dn, g.RO, g.LF, xbig, layer + 1 < a.L ? lbase + g.LL : 0x7fffffff);
     {
       const uint32_t tr = tag_of(layer + 1, E_RESID);
-      const int lp = g.LF;
-      for (int u = k.cw; u < g.RO / 2; u += NCW) {
-        const int j0 = lbase + g.off_dn + 2 * u * lp;
-        k.set_cur(j0);
-        const float v0 = k.dot_row(j0, lp, xbig);
-        const float v1 = k.dot_row(j0 + lp, lp, xbig);
+      for (int u = ct; u < g.RO / 2; u += CT) {
         const int r0 = w * g.RO + 2 * u;
-        if (lane == 0) gstore(a.gran, a.g_resid + r0 / 2, tr, pack2(bf2f(xres[r0]) + v0, bf2f(xres[r0 + 1]) + v1));
+        gstore(a.gran, a.g_resid + r0 / 2, tr,
+               pack2(bf2f(xres[r0]) + row_sum(c, 2 * u, iF), bf2f(xres[r0 + 1]) + row_sum(c, 2 * u + 1, iF)));
       }
-      k.set_cur(layer + 1 < a.L ? lbase + g.LL : 0x7fffffff);
     }
     B1_STAMP(9);
     k.cbar();  // xres is overwritten by the next gather
@@ -649,7 +772,7 @@ __device__ void consumer(const Args& a, const Geo& g, Ctl* c, const uint8_t* rin
     k.gather(g.H / 2, tag_of(a.L, E_RESID), reinterpret_cast<uint32_t*>(xres), [&](int x) { return a.g_resid + x; });
     k.cbar();
     const float rs = k.norm_scale(xres, g.H);
-    for (int x = k.ctid * 8; x < g.H; x += CT * 8) {
+    for (int x = ct * 8; x < g.H; x += CT * 8) {
       float v[8], wf[8], o[8];
       unpack8(*reinterpret_cast<const uint4*>(xres + x), v);
       unpack8(*reinterpret_cast<const uint4*>(a.final_norm + x), wf);
@@ -689,6 +812,8 @@ int decode_b1_plan(int L, int H, int F, int Hq, int Hkv, int* out /*[12]*/) {
   if (G > 8 || ((G + 2) * HD) % WPG) return -1;
   const int RPW = (G + 2) * HD / WPG, RO = H / NWG, FW = F / NWG;
   if (H % (2 * NWG) || F % (2 * NWG) || RPW < NCW || RO / 2 < NCW || FW / 2 < NCW || (FW % 2)) return -1;
+  auto items = [](int rows, int K) { return rows * ((K / 512 + SEG - 1) / SEG); };
+  if (items(RPW, H) > 256 || items(RO, Hq * HD) > 256 || items(2 * FW, H) > 256 || items(RO, F) > 256) return -1;
   const int S_att = WPG < 32 ? WPG : 32;
   if ((G * HD) % S_att || ((G * HD / S_att) % 2)) return -1;
   // LDS: ring | xres (H bf16) | xbig (max(Hq*128, F) bf16, also the attention scratch) | ctl
@@ -727,7 +852,7 @@ int decode_b1(const uint64_t* wptr, const uint64_t* kvptr, const uint16_t* resid
   using namespace b1;
   int pl[12];
   const int ng = decode_b1_plan(L, H, F, Hq, Hkv, pl);
-  if (ng < 0 || bs % 16) return -1;
+  if (ng < 0 || bs != 16) return -1;  // 16-key pages (attention address arithmetic)
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(decode_b1_kernel),

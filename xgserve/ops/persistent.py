@@ -79,7 +79,7 @@ class B1Decoder:
         return int(self.ctl[0].item())
 
     # ------------------------------------------------------------------ diagnostics
-    NSTAMP = 10
+    NSTAMP = 16
     PHASES = ("resid gather + norm", "QKV rows", "attention + combine", "attn gather", "O rows",
               "post gather + norm", "gate_up rows", "act gather", "down rows")
 
@@ -95,6 +95,9 @@ class B1Decoder:
         st = self.stamps.cpu()
         ph = st[:256 * self.L * self.NSTAMP].view(256, self.L, self.NSTAMP).double()
         tick_us = 1000.0 / self._khz
+        att = ph[:32, :, [2, 10, 11, 12, 13, 14, 15, 3]]        # attention sub-phases (splits 0..31)
+        ad = ((att[:, :, 1:] - att[:, :, :-1]) * tick_us).sum(1)
+        ph = ph[:, :, :10]
         d = (ph[:, :, 1:] - ph[:, :, :-1]) * tick_us           # [wg, layer, 9]
         nxt = torch.cat([ph[:, 1:, 0], ph[:, -1:, 9]], 1)      # next layer's start
         tail = (nxt - ph[:, :, 9]) * tick_us
@@ -107,6 +110,11 @@ class B1Decoder:
         rep["total"] = (float(tot.mean()), float(tot.max()))
         rep["loader ring-full stall"] = (float(extra[:, 0].mean()), float(extra[:, 0].max()))
         rep["consumer line wait"] = (float(extra[:, 2].mean()), float(extra[:, 2].max()))
+        lspan = (st[256 * self.L * self.NSTAMP:].view(256, 4)[:, 1].double() - ph[:, 0, 0]) * tick_us
+        rep["loader span (start -> last line landed)"] = (float(lspan.mean()), float(lspan.max()))
+        for i, name in enumerate(("kv prefetch issue", "qkv gather", "rope", "softmax.V", "partials publish",
+                                  "combine gather", "combine + publish")):
+            rep["  attn: " + name] = (float(ad[:, i].mean()), float(ad[:, i].max()))
         return rep
 
     # ------------------------------------------------------------------ launch
@@ -124,6 +132,8 @@ class B1Decoder:
         The new token's K/V rows are appended to the paged caches."""
         kc = kv_caches[0][0]
         bs = kc.shape[2]
+        if block_tables.shape[-1] > 32 * 500:  # the kernel keeps a split's pages (<= 512) in LDS
+            raise ValueError("decode_b1: context too long for the persistent kernel")
         kvp = self._kv_table(kv_caches)
         self.k.decode_b1(self.wptr.data_ptr(), kvp.data_ptr(), resid.data_ptr(), self.final_norm.data_ptr(),
                          self.out.data_ptr(), positions.data_ptr(), slot_mapping.data_ptr(), block_tables.data_ptr(),
