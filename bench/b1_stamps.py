@@ -33,12 +33,12 @@ def main():
     eng.add_request("r", prompt, SamplingParams(max_tokens=32, temperature=0.0, ignore_eos=True))
     reports = {}
     modes = {0: "full", 1: "loader alone (consumers ignore the ring)", 2: "consumers alone (no weight loads)",
-             5: "loader alone, no projection work"}
+             5: "loader alone, no projection work", 9: "loader alone, consumers exit"}
     for _ in range(3):
         eng.step()
     dec = model._b1
     dec.enable_stamps()
-    for m in (0, 1, 2, 5):
+    for m in (0, 1, 2, 5, 9):
         torch.cuda.synchronize()
         dec.ctl[3].fill_(m)
         for _ in range(3):  # async scheduling: the mode is live from the second step on

@@ -6,7 +6,7 @@ t=$1; cmd=$2; log=${3:-/tmp/gpurun_last.log}
 for i in $(seq 1 20); do
   /usr/local/graft/bin/gpurun --timeout "$t" -- "$cmd" > "$log" 2>&1
   rc=$?
-  if [ $rc -ne 3 ] && ! grep -q "backing off" "$log"; then break; fi
+  if [ $rc -ne 3 ] && ! grep -q "backing off\|status=transient" "$log"; then break; fi
   sleep 45
 done
 echo "exit $rc"; tail -n 15 "$log"

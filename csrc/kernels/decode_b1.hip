@@ -43,8 +43,10 @@ namespace xgk {
 namespace b1 {
 
 constexpr int NWG = 256;
-constexpr int NTHR = 256;
-constexpr int NCW = 3;          // consumer waves
+constexpr int NLW = 2;          // loader waves (one wave's LDS-DMA issue tops out at ~19 GB/s per CU,
+                                // two reach ~27: bench/dma_probe.hip)
+constexpr int NCW = 2;          // consumer waves (4 waves per CU: 512 VGPRs each)
+constexpr int NTHR = (NLW + NCW) * 64;
 constexpr int CT = NCW * 64;    // consumer threads
 constexpr int LINE = 1024;      // ring line: 64 lanes x 16 B
 constexpr int SLOT = 16;        // lines per slot
@@ -77,16 +79,17 @@ struct Args {
   int off_xres, off_xbig, off_ctl;  // LDS byte offsets
   int g_resid, g_post, g_qkv, g_part, g_attn, g_act;  // granule offsets
   uint64_t* stamps;  // diagnostics (null in production): per-(workgroup, layer) phase clocks
+  const uint64_t* runs;  // [NWG][runs_stride] {address, lines}: each workgroup's weight stream as
+  int runs_stride;       // contiguous runs in line order (decode_b1_build_runs), {0, 0}-terminated
 };
-constexpr int NSTAMP = 16;
+constexpr int NSTAMP = 18;
 
 // LDS control block
 struct Ctl {
-  int landed;       // lines landed in the ring (loader -> consumers)
-  int cur[NCW];     // first line each consumer may still read (consumers -> loader)
+  int landed[NLW];  // loader L: every line of ITS 8-line groups (g % NLW == L) below this landed
+  int cur[NCW];     // first line each consumer may still read (consumers -> loaders)
   int cbar;         // consumer barrier arrivals
   int abort_;       // set on any timeout in this workgroup
-  int pad[2];
   int pages[512];   // KV pages of this workgroup's key split (block_table[kb / bs ...])
   float red[16];    // cross-wave reduction scratch
   float res[256];   // per-item partial dot products of the current phase
@@ -148,6 +151,19 @@ template <int CTRL, int ROW_MASK = 0xF>
 __device__ __forceinline__ float dpp(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
 }
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_keep(float v) {  // masked-off rows keep v
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROW_MASK, 0xF, false));
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_keep<0xB1>(v));
+  v = fmaxf(v, dpp_keep<0x4E>(v));
+  v = fmaxf(v, dpp_keep<0x141>(v));
+  v = fmaxf(v, dpp_keep<0x140>(v));
+  v = fmaxf(v, dpp_keep<0x142, 0xA>(v));
+  v = fmaxf(v, dpp_keep<0x143, 0xC>(v));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 __device__ __forceinline__ float wave_sum_dpp(float v) {
   v += dpp<0xB1>(v);         // quad_perm [1,0,3,2]
   v += dpp<0x4E>(v);         // quad_perm [2,3,0,1]
@@ -183,14 +199,36 @@ struct Geo {
       if (idx < (G + 1) * HD) return Hq * HD + h * HD + (idx - G * HD);
       return (Hq + Hkv) * HD + h * HD + (idx - (G + 1) * HD);
     }
-    if (p == P_GU) {  // unit u = rows 4u..4u+3: gate(f0) up(f0) gate(f0+1) up(f0+1)
-      const int f = w * FW + 2 * (r >> 2) + ((r >> 1) & 1);
-      return 32 * (f >> 4) + (f & 15) + ((r & 1) ? 16 : 0);
+    if (p == P_GU) {  // the workgroup's gate / up rows in memory order (long contiguous runs)
+      const int f0 = w * FW, f1 = f0 + FW;
+      int base = 0;
+      for (int b = f0 >> 4;; ++b) {
+        const int lo = max(f0, 16 * b), cnt = min(f1, 16 * b + 16) - lo;
+        if (r < base + 2 * cnt) {
+          const int rr = r - base, up = rr >= cnt;
+          return 32 * b + (lo & 15) + (up ? rr - cnt + 16 : rr);
+        }
+        base += 2 * cnt;
+      }
     }
     return w * RO + r;  // O, down
   }
-  __device__ __forceinline__ int nrows(int p) const { return p == P_QKV ? RPW : p == P_GU ? 2 * FW : RO; }
-  __device__ __forceinline__ int lpr(int p) const { return p == P_O ? LA : p == P_DN ? LF : LH; }
+  // arithmetic selects (a switch here became a lookup table in scratch memory, whose
+  // loads the loader's counted vmcnt waits then had to drain)
+  // position of feature f's gate (up = 0) or up row in the workgroup's gate_up row order
+  __device__ __forceinline__ int gu_pos(int w, int f, int up) const {
+    const int f0 = w * FW, f1 = f0 + FW;
+    int base = 0;
+    for (int b = f0 >> 4; b < (f >> 4); ++b) base += 2 * (min(f1, 16 * b + 16) - max(f0, 16 * b));
+    const int b = f >> 4, lo = max(f0, 16 * b), cnt = min(f1, 16 * b + 16) - lo;
+    return base + up * cnt + (f - lo);
+  }
+  __device__ __forceinline__ int nrows(int p) const {
+    return RO + (p == P_QKV) * (RPW - RO) + (p == P_GU) * (2 * FW - RO);
+  }
+  __device__ __forceinline__ int lpr(int p) const {
+    return LH + (p == P_O) * (LA - LH) + (p == P_DN) * (LF - LH);
+  }
   __device__ __forceinline__ int K(int p) const { return lpr(p) * 512; }
   __device__ __forceinline__ int poff(int p) const {
     return p == P_QKV ? 0 : p == P_O ? off_o : p == P_GU ? off_gu : off_dn;
@@ -199,76 +237,107 @@ struct Geo {
 
 // ---------------------------------------------------------------- loader (wave 0)
 __device__ __forceinline__ int min_cur(Ctl* c) {
-  return __builtin_amdgcn_readfirstlane(min(lds_ld(&c->cur[0]), min(lds_ld(&c->cur[1]), lds_ld(&c->cur[2]))));
+  int m = lds_ld(&c->cur[0]);
+#pragma unroll
+  for (int i = 1; i < NCW; ++i) m = min(m, lds_ld(&c->cur[i]));
+  return __builtin_amdgcn_readfirstlane(m);
 }
-__device__ __forceinline__ void publish(Ctl* c, int& pub, int lines) {
+__device__ __forceinline__ void publish(Ctl* c, int L, int& pub, int lines) {
   if (lines > pub) {
     pub = lines;
-    lds_st(&c->landed, pub);
+    lds_st(&c->landed[L], pub);
   }
 }
 
-__device__ __forceinline__ void loader(const Args& a, const Geo& g, Ctl* c, uint8_t* ring) {
-  const int lane = threadIdx.x & 63;
+// Loader wave L issues the 8-line groups g with g % NLW == L of the one static line
+// sequence; its own DMAs are counted by its own vmcnt, so its published count covers
+// its groups only (consumers check the loader of each line's group).
+__device__ __forceinline__ void loader(const Args& a, Ctl* c, uint8_t* ring, int L) {
+  const Geo g(a);  // a private copy: kept in registers (a shared reference put it in scratch)
   const int RL = a.ring_lines;
   const uint64_t limit = static_cast<uint64_t>(__hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const int w = blockIdx.x;
-  int j = 0, rpos = 0, pub = 0;
+  const int total = a.L * g.LL;
+  int j = 0, pub = 0;
   bool dead = false;
   uint64_t free_wait = 0;
   if (a.ctl[3] & 2) {  // diagnostics: consumers alone
-    lds_st(&c->landed, 0x7fffffff);
+    lds_st(&c->landed[L], 0x7fffffff);
     return;
   }
-  for (int layer = 0; layer < a.L && !dead; ++layer) {
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      if (dead) break;
-      const uint8_t* W = reinterpret_cast<const uint8_t*>(a.wptr[layer * 4 + p]);
-      const int lp = g.lpr(p), nr = g.nrows(p);
-      const int64_t rowbytes = static_cast<int64_t>(lp) * LINE;
-      for (int r = 0; r < nr && !dead; ++r) {
-        const uint8_t* src = W + static_cast<int64_t>(g.row(p, w, r)) * rowbytes + lane * 16;
-        for (int cc = 0; cc < lp; ++cc, ++j) {
-          if ((j & 7) == 0) {
-            // group of 8 lines: it overwrites lines [j - RL, j - RL + 8), free once every
-            // consumer's current item starts at or past j - RL + 8
-            const int need = j + 8 - RL;
-            if (need > 0 && min_cur(c) < need) {
-              // ring full: publish what has landed in steps, keeping the rest of the DMA
-              // pipeline in flight (a full drain restarted it from empty every time)
-              const uint64_t tw = a.stamps ? wall_clock64() : 0;
-              asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-              publish(c, pub, j - 32);
-              if (min_cur(c) < need) {
-                asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-                publish(c, pub, j - 16);
-                if (min_cur(c) < need) {
-                  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                  publish(c, pub, j);
-                  Spin sp;
-                  while (min_cur(c) < need)
-                    if (sp.tick(c, a.ctl, limit, false)) { dead = true; break; }
-                }
-              }
-              if (a.stamps) free_wait += wall_clock64() - tw;
-              if (dead) break;
-            }
-          }
-          glds16_nt(src + cc * LINE, ring + rpos * LINE);
-          if (++rpos == RL) rpos = 0;
-          if ((j & 7) == 7) {
-            // vmcnt counts this wave's DMAs in issue order: all but the last 48 have landed
-            asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
-            publish(c, pub, j + 1 - 48);
-          }
+  // the weight stream as contiguous runs (read through the scalar cache, a batch of 4
+  // runs = one 64-B line at a time); rptr / rleft: the current run
+  const int lane16 = (threadIdx.x & 63) * 16;
+  // constant address space: uniform reads become scalar loads (lgkmcnt), never vector
+  // loads, whose vmcnt would mix with the counted DMA waits
+  typedef __attribute__((address_space(4))) const uint64_t cu64;
+  cu64* rt = (cu64*)(a.runs) + static_cast<int64_t>(blockIdx.x) * a.runs_stride * 2;
+  int k = 0;
+  uint64_t rptr = rt[0];
+  int rleft = static_cast<int>(rt[1]);
+#define B1_NEXT_RUN()                                    \
+  {                                                      \
+    ++k;                                                 \
+    rptr = rt[2 * k];                                    \
+    rleft = static_cast<int>(rt[2 * k + 1]);             \
+  }
+#define B1_SKIP(N)                                       \
+  {                                                      \
+    int n_ = (N);                                        \
+    while (n_ > 0 && rleft > 0) {                        \
+      const int st_ = min(n_, rleft);                    \
+      rptr += static_cast<uint64_t>(st_) * LINE;         \
+      rleft -= st_;                                      \
+      n_ -= st_;                                         \
+      if (rleft == 0) B1_NEXT_RUN();                     \
+    }                                                    \
+  }
+  B1_SKIP(8 * L);  // this loader's first group
+  j = 8 * L;
+  int rp = j % RL;
+  for (; j < total; j += 8 * NLW) {
+    // group of 8 lines [j, j + 8): it overwrites lines [j - RL, j - RL + 8), free once
+    // every consumer holds nothing below j - RL + 8
+    const int need = j + 8 - RL;
+    if (need > 0 && min_cur(c) < need) {
+      // ring full: publish what has landed in steps, keeping the rest of this loader's
+      // DMA pipeline in flight (its groups j/8 - 2, - 4, - 6 may be outstanding here)
+      const uint64_t tw = a.stamps ? wall_clock64() : 0;
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      publish(c, L, pub, j - 40);
+      if (min_cur(c) < need) {
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        publish(c, L, pub, j - 24);
+        if (min_cur(c) < need) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          publish(c, L, pub, j - 8);
+          Spin sp;
+          while (min_cur(c) < need)
+            if (sp.tick(c, a.ctl, limit, false)) { dead = true; break; }
         }
       }
+      if (a.stamps) free_wait += wall_clock64() - tw;
+      if (dead) break;
     }
+    const int n = min(8, total - j);
+    for (int i = 0; i < n; ++i) {
+      if (rleft <= 0) break;  // defensive: the table ended early (never issue past it)
+      glds16_nt(reinterpret_cast<const uint8_t*>(rptr) + lane16, ring + (rp + i) * LINE);
+      rptr += LINE;
+      if (--rleft == 0) B1_NEXT_RUN();
+    }
+    B1_SKIP(8 * (NLW - 1));  // the other loaders' groups
+    rp += 8 * NLW;
+    if (rp >= RL) rp -= RL;
+    // this loader's last 3 groups (24 DMAs) may still be in flight: its group j/8 - 6
+    // (and every earlier one) has landed
+    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    publish(c, L, pub, j + 8 - 48);
   }
+#undef B1_NEXT_RUN
+#undef B1_SKIP
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_st(&c->landed, dead ? 0x7fffffff : j);
-  if (a.stamps && lane == 0) {
+  lds_st(&c->landed[L], dead ? 0x7fffffff : j);
+  if (a.stamps && (threadIdx.x & 63) == 0 && L == 0) {
     uint64_t* st = a.stamps + static_cast<int64_t>(NWG) * a.L * NSTAMP + blockIdx.x * 4;
     st[0] = free_wait;
     st[1] = wall_clock64();
@@ -282,7 +351,7 @@ struct Cons {
   Ctl* c;
   const uint8_t* ring;
   int cw, lane, ctid;
-  int landed_cache;
+  int landed_c0, landed_c1;  // per-loader landed counts last seen
   int cbar_seq;
   int mode;
   uint64_t limit;
@@ -293,10 +362,10 @@ struct Cons {
   }
   __device__ __forceinline__ Cons(const Args& a_, const Geo& g_, Ctl* c_, const uint8_t* r_)
       : a(a_), g(g_), c(c_), ring(r_) {
-    ctid = threadIdx.x - 64;
+    ctid = threadIdx.x - 64 * NLW;
     cw = __builtin_amdgcn_readfirstlane(ctid >> 6);  // wave-uniform: item loops and branches stay scalar
     lane = threadIdx.x & 63;
-    landed_cache = 0;
+    landed_c0 = landed_c1 = 0;
     cbar_seq = 0;
     mode = a.ctl[3];
     limit = static_cast<uint64_t>(__hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -318,23 +387,46 @@ struct Cons {
     if (lane == 0) lds_st(&c->cur[cw], line);
   }
   __device__ __forceinline__ void wait_line(int j) {
-    if (j < landed_cache || (mode & 1)) return;
+    const int L = (j >> 3) & (NLW - 1);
+    if (j < (L ? landed_c1 : landed_c0) || (mode & 1)) return;
     Spin sp;
-    int l = lds_ld(&c->landed);
+    int l = lds_ld(&c->landed[L]);
     const uint64_t tw = (a.stamps && l <= j) ? wall_clock64() : 0;
     while (l <= j) {
       if (sp.tick(c, a.ctl, limit, false)) { l = 0x7fffffff; break; }
-      l = lds_ld(&c->landed);
+      l = lds_ld(&c->landed[L]);
     }
     asm volatile("" ::: "memory");
     if (tw) line_wait += wall_clock64() - tw;
-    landed_cache = __builtin_amdgcn_readfirstlane(l);
+    const int lu = __builtin_amdgcn_readfirstlane(l);
+    if (L == 0) landed_c0 = lu; else landed_c1 = lu;
   }
-  // dot(x[0 : 512 * nl], W lines j0 .. j0 + nl) for one row segment (nl <= SEG); x bf16
-  // in LDS. One wait for the whole segment, then every weight and x chunk read is in
-  // flight before the first v_dot2c (a per-line read-then-use loop exposed the LDS
-  // latency on every line); one DPP reduction.
-  __device__ __forceinline__ float dot_row(int j0, int nl, const uint16_t* x) {
+  // one full row segment with x already in registers (phases whose rows are exactly one
+  // segment: the same x for every item, read from LDS once per phase)
+  __device__ __forceinline__ float dot_row_x(int j0, int rp0, const uint4* xr, int jrelease) {
+    wait_line(j0);
+    wait_line(j0 + SEG - 1);
+    const int RL = a.ring_lines;
+    uint4 wv[SEG];
+#pragma unroll
+    for (int i = 0; i < SEG; ++i) {
+      const int rp = rp0 + i >= RL ? rp0 + i - RL : rp0 + i;
+      wv[i] = *reinterpret_cast<const uint4*>(ring + rp * LINE + lane * 16);
+    }
+    set_cur(jrelease);
+    float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < SEG; ++i) {
+      acc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv[i].x), __builtin_bit_cast(bf2_t, xr[i].x), acc0, false);
+      acc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv[i].y), __builtin_bit_cast(bf2_t, xr[i].y), acc1, false);
+      acc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv[i].z), __builtin_bit_cast(bf2_t, xr[i].z), acc0, false);
+      acc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv[i].w), __builtin_bit_cast(bf2_t, xr[i].w), acc1, false);
+    }
+    return wave_sum_dpp(acc0 + acc1);
+  }
+
+  __device__ __forceinline__ float dot_row(int j0, int nl, const uint16_t* x, int jrelease) {
+    wait_line(j0);
     wait_line(j0 + nl - 1);
     const int RL = a.ring_lines;
     const int rp0 = j0 % RL;
@@ -347,6 +439,7 @@ struct Cons {
         wv[i] = *reinterpret_cast<const uint4*>(ring + rp * LINE + lane * 16);
         xv[i] = *reinterpret_cast<const uint4*>(x + i * 512 + lane * 8);
       }
+      set_cur(jrelease);  // the item's lines are in registers once these reads return
 #pragma unroll
       for (int i = 0; i < SEG; ++i) {
         acc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv[i].x), __builtin_bit_cast(bf2_t, xv[i].x), acc0, false);
@@ -365,6 +458,7 @@ struct Cons {
         acc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, wv.w), __builtin_bit_cast(bf2_t, xv.w), acc1, false);
         rp = rp + 1 == RL ? 0 : rp + 1;
       }
+      set_cur(jrelease);
     }
     return wave_sum_dpp(acc0 + acc1);
   }
@@ -381,13 +475,14 @@ struct Cons {
         if (base + k * 64 + lane < n) pend |= 1ull << k;
       Spin sp;
       for (;;) {
+        // every pending load issued before the first tag check (a check right after each
+        // load made the sweep one round trip per granule)
 #pragma unroll
-        for (int k = 0; k < B; ++k) {
-          if (pend & (1ull << k)) {
-            v[k] = gload(a.gran, map(base + k * 64 + lane));
-            if (static_cast<uint32_t>(v[k] >> 32) == tag) pend &= ~(1ull << k);
-          }
-        }
+        for (int k = 0; k < B; ++k)
+          if (pend & (1ull << k)) v[k] = gload(a.gran, map(base + k * 64 + lane));
+#pragma unroll
+        for (int k = 0; k < B; ++k)
+          if ((pend & (1ull << k)) && static_cast<uint32_t>(v[k] >> 32) == tag) pend &= ~(1ull << k);
         if (__all(pend == 0)) break;
         if (sp.tick(c, a.ctl, limit, true)) break;
       }
@@ -411,7 +506,9 @@ struct Cons {
     s = wave_sum(s);
     if (lane == 0) c->red[cw] = s;
     cbar();
-    const float tot = c->red[0] + c->red[1] + c->red[2];
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < NCW; ++i) tot += c->red[i];
     const float rs = rsqrtf(tot / static_cast<float>(n) + a.eps);
     cbar();  // red[] is reused by the next reduction
     return rs;
@@ -421,21 +518,23 @@ struct Cons {
 __device__ __forceinline__ float bf16r(float f) { return bf2f(f2bf(f)); }
 
 // ---------------------------------------------------------------- attention (split i of group h)
+template <int GQ>  // query heads per kv head (compile time: loops over heads unroll without guards)
 __device__ __forceinline__ void attention(Cons& k, int layer, int h, int i, uint8_t* scratch) {
   const Args& a = k.a;
   const Geo& g = k.g;
-  const int G = g.G, S = a.S_att;
+  constexpr int G = GQ;
+  const int S = a.S_att;
   const int ctx = a.seq_lens[0], pos = a.positions[0], slot = a.slot_mapping[0];
   const int cs = (ctx + S - 1) / S;
   const int kb = min(i * cs, ctx), ke = min(kb + cs, ctx);
   // scratch layout (floats): gq[(G+2)*128] | qb (bf16 G*128) | knew, vnew (bf16 128 each)
-  //                          | pw[NCW][G][64] | wm[NCW][G] wl[NCW][G] | wo[NCW][G][128]
+  //                          | pw[NCW][64][8] | wm[NCW][G] wl[NCW][G] | wo[NCW][G][128]
   float* gq = reinterpret_cast<float*>(scratch);
   uint16_t* qb = reinterpret_cast<uint16_t*>(gq + (G + 2) * HD);
   uint16_t* knew = qb + G * HD;
   uint16_t* vnew = knew + HD;
   float* pw = reinterpret_cast<float*>(vnew + HD);
-  float* wm = pw + NCW * G * 64;
+  float* wm = pw + NCW * 64 * 8;
   float* wl = wm + NCW * G;
   float* wo = wl + NCW * G;
 
@@ -452,7 +551,7 @@ __device__ __forceinline__ void attention(Cons& k, int layer, int h, int i, uint
   // QKV hand-off: its HBM latency hides under the wait (a dependent load per key was
   // ~1.5 us each).
   uint4 kreg[HD / 8];
-  uint32_t vreg[64];
+  uint32_t vreg[32];  // V of the chunk's first 32 keys (VGPR budget: 2 waves per SIMD)
 // A chunk's (<= 64 keys) pages are at most five 16-key blocks: read them once (LDS),
 // then every K / V address is arithmetic (a page lookup per key serialised ~64 LDS
 // round trips in front of the loads).
@@ -469,7 +568,7 @@ __device__ __forceinline__ void attention(Cons& k, int layer, int h, int i, uint
       _Pragma("unroll") for (int d_ = 0; d_ < HD / 8; ++d_) kreg[d_] =                                  \
           *reinterpret_cast<const uint4*>(kr_ + d_ * 8);                                                \
     }                                                                                                   \
-    _Pragma("unroll") for (int tt_ = 0; tt_ < 64; ++tt_) {                                              \
+    _Pragma("unroll") for (int tt_ = 0; tt_ < 32; ++tt_) {                                              \
       const int tk_ = (T0) + tt_;                                                                       \
       if (tk_ < we && tk_ != ctx - 1)                                                                   \
         vreg[tt_] = reinterpret_cast<const uint32_t*>(                                                  \
@@ -518,10 +617,10 @@ __device__ __forceinline__ void attention(Cons& k, int layer, int h, int i, uint
     reinterpret_cast<uint32_t*>(vc + dst)[lane] = reinterpret_cast<const uint32_t*>(vnew)[lane];
   }
   // C: online softmax over the wave's keys
-  float m[8], l[8], o0[8], o1[8];
+  float m[G], l[G], o0[G], o1[G];
 #pragma unroll
-  for (int gg = 0; gg < 8; ++gg) { m[gg] = -INFINITY; l[gg] = 0.f; o0[gg] = 0.f; o1[gg] = 0.f; }
-  float* mypw = pw + k.cw * G * 64;
+  for (int gg = 0; gg < G; ++gg) { m[gg] = -INFINITY; l[gg] = 0.f; o0[gg] = 0.f; o1[gg] = 0.f; }
+  float* mypw = pw + k.cw * 64 * 8;  // [key][8 heads]: one b128 read gives 4 heads' p
   const uint32_t vnew_l = reinterpret_cast<const uint32_t*>(vnew)[lane];
   for (int t0 = wb; t0 < we; t0 += 64) {
     if (t0 != wb) B1_LOAD_CHUNK(t0);
@@ -531,16 +630,16 @@ __device__ __forceinline__ void attention(Cons& k, int layer, int h, int i, uint
 #pragma unroll
       for (int d = 0; d < HD / 8; ++d) kreg[d] = *reinterpret_cast<const uint4*>(knew + d * 8);
     }
-    float s[8];
+    float s[G];
 #pragma unroll
-    for (int gg = 0; gg < 8; ++gg) s[gg] = 0.f;
+    for (int gg = 0; gg < G; ++gg) s[gg] = 0.f;
 #pragma unroll
     for (int d = 0; d < HD / 8; ++d) {
       float kf[8];
       unpack8(kreg[d], kf);
 #pragma unroll
-      for (int gg = 0; gg < 8; ++gg) {
-        if (gg < G) {
+      for (int gg = 0; gg < G; ++gg) {
+        {
           float qf[8];
           unpack8(*reinterpret_cast<const uint4*>(qb + gg * HD + d * 8), qf);
 #pragma unroll
@@ -549,10 +648,10 @@ __device__ __forceinline__ void attention(Cons& k, int layer, int h, int i, uint
       }
     }
 #pragma unroll
-    for (int gg = 0; gg < 8; ++gg) {
-      if (gg < G) {
+    for (int gg = 0; gg < G; ++gg) {
+      {
         const float sv = valid ? s[gg] * a.scale : -INFINITY;
-        const float cm = wave_max(sv);
+        const float cm = wave_max_dpp(sv);
         const float nm = fmaxf(m[gg], cm);
         const float alpha = m[gg] == -INFINITY ? 0.f : __expf(m[gg] - nm);
         const float p = valid ? __expf(sv - nm) : 0.f;
@@ -560,22 +659,37 @@ __device__ __forceinline__ void attention(Cons& k, int layer, int h, int i, uint
         o0[gg] *= alpha;
         o1[gg] *= alpha;
         m[gg] = nm;
-        mypw[gg * 64 + lane] = p;
+        mypw[lane * 8 + gg] = p;
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int nt = min(64, we - t0);
+    for (int half = 0; half < 2; ++half) {
+      const int tb = half * 32;
+      if (tb >= nt) break;
+      if (half == 1) {  // keys 32..63 of the chunk: V loaded now
 #pragma unroll
-    for (int tt = 0; tt < 64; ++tt) {
-      if (tt < nt) {
-        const uint32_t vv = (t0 + tt == ctx - 1) ? vnew_l : vreg[tt];
-        const float va = __uint_as_float(vv << 16), vb = __uint_as_float(vv & 0xFFFF0000u);
+        for (int tt = 0; tt < 32; ++tt) {
+          const int tk = t0 + 32 + tt;
+          if (tk < we && tk != ctx - 1)
+            vreg[tt] = reinterpret_cast<const uint32_t*>(
+                vc + ((static_cast<int64_t>(pg[tk >> 4]) * g.Hkv + h) * 16 + (tk & 15)) * HD)[lane];
+        }
+      }
 #pragma unroll
-        for (int gg = 0; gg < 8; ++gg) {
-          if (gg < G) {
-            const float p = mypw[gg * 64 + tt];
-            o0[gg] += p * va;
-            o1[gg] += p * vb;
+      for (int tt = 0; tt < 32; ++tt) {
+        if (tb + tt < nt) {
+          const uint32_t vv = (t0 + tb + tt == ctx - 1) ? vnew_l : vreg[tt];
+          const float va = __uint_as_float(vv << 16), vb = __uint_as_float(vv & 0xFFFF0000u);
+          const float4 pa = *reinterpret_cast<const float4*>(mypw + (tb + tt) * 8);
+          const float4 pb = G > 4 ? *reinterpret_cast<const float4*>(mypw + (tb + tt) * 8 + 4) : pa;
+          const float pv[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};  // heads >= G unused
+#pragma unroll
+          for (int gg = 0; gg < G; ++gg) {
+            {
+              o0[gg] += pv[gg] * va;
+              o1[gg] += pv[gg] * vb;
+            }
           }
         }
       }
@@ -584,8 +698,8 @@ __device__ __forceinline__ void attention(Cons& k, int layer, int h, int i, uint
   }
 #undef B1_LOAD_CHUNK
 #pragma unroll
-  for (int gg = 0; gg < 8; ++gg) {
-    if (gg < G) {
+  for (int gg = 0; gg < G; ++gg) {
+    {
       if (lane == 0) {
         wm[k.cw * G + gg] = m[gg];
         wl[k.cw * G + gg] = l[gg];
@@ -653,14 +767,37 @@ __device__ __forceinline__ void attention(Cons& k, int layer, int h, int i, uint
 // space they hold back from the loader stays ~3 items (a whole-row unit per wave held
 // the loader to a few lines of run-ahead on the 32-line gate_up units). Item partials
 // go to c->res; the caller reduces them per row after a cbar.
-__device__ __forceinline__ void phase_items(Cons& k, int jphase, int nrows, int lp, const uint16_t* x, int jnext) {
+__device__ __forceinline__ void phase_items(Cons& k, int jphase, int nrows, int lp, const uint16_t* x, int jnext,
+                                            int stamp_layer = -1) {
   const int ipr = (lp + SEG - 1) / SEG;
   const int nit = (k.mode & 4) ? 0 : nrows * ipr;  // diagnostics: 4 = no projection work
+  if (lp == SEG) {  // one item per row: x in registers, ring position stepped (no divisions)
+    const int RL = k.a.ring_lines, step = NCW * SEG;
+    uint4 xr[SEG];
+#pragma unroll
+    for (int i = 0; i < SEG; ++i) xr[i] = *reinterpret_cast<const uint4*>(x + i * 512 + k.lane * 8);
+    int rp = (jphase + k.cw * SEG) % RL;
+    if (k.cw < nit) k.set_cur(jphase + k.cw * SEG);
+    if (stamp_layer >= 0) k.stamp(stamp_layer, 16);
+    for (int it = k.cw; it < nit; it += NCW) {
+      const int j0 = jphase + it * SEG;
+      const float v = k.dot_row_x(j0, rp, xr, it + NCW < nit ? j0 + step : jnext);
+      if (k.lane == 0) k.c->res[it] = v;
+      rp += step;
+      if (rp >= RL) rp -= RL;
+    }
+    if (stamp_layer >= 0) k.stamp(stamp_layer, 17);
+    k.set_cur(jnext);
+    k.cbar();
+    return;
+  }
   for (int it = k.cw; it < nit; it += NCW) {
     const int r = it / ipr, l0 = (it % ipr) * SEG;
     const int j0 = jphase + r * lp + l0;
+    const int in = it + NCW;  // this wave's next item: its start is the new hold point
+    const int jn = in < nit ? jphase + (in / ipr) * lp + (in % ipr) * SEG : jnext;
     k.set_cur(j0);
-    const float v = k.dot_row(j0, min(SEG, lp - l0), x + l0 * 512);
+    const float v = k.dot_row(j0, min(SEG, lp - l0), x + l0 * 512, jn);
     if (k.lane == 0) k.c->res[it] = v;
   }
   k.set_cur(jnext);
@@ -672,8 +809,15 @@ __device__ __forceinline__ float row_sum(const Ctl* c, int r, int ipr) {
   return v;
 }
 
-__device__ __forceinline__ void consumer(const Args& a, const Geo& g, Ctl* c, const uint8_t* ring, uint8_t* smem) {
+template <int GQ>
+__device__ __forceinline__ void consumer(const Args& a, Ctl* c, const uint8_t* ring, uint8_t* smem) {
+  const Geo g(a);
   Cons k(a, g, c, ring);
+  if (k.mode & 8) {  // diagnostics: the loader streams alone, the consumers leave
+    k.set_cur(0x7fffffff);
+    if (a.stamps && k.ctid == 0) a.stamps[static_cast<int64_t>(blockIdx.x) * a.L * NSTAMP] = wall_clock64();
+    return;
+  }
   uint16_t* xres = reinterpret_cast<uint16_t*>(smem + a.off_xres);
   uint16_t* xbig = reinterpret_cast<uint16_t*>(smem + a.off_xbig);
   const int w = blockIdx.x;
@@ -714,7 +858,7 @@ __device__ __forceinline__ void consumer(const Args& a, const Geo& g, Ctl* c, co
     }
     B1_STAMP(2);
     // ---- attention + combine (the first S_att workgroups of every kv-head group)
-    if (gi < a.S_att) attention(k, layer, h, gi, reinterpret_cast<uint8_t*>(xbig));
+    if (gi < a.S_att) attention<GQ>(k, layer, h, gi, reinterpret_cast<uint8_t*>(xbig));
     k.cbar();
     B1_STAMP(3);
     k.gather(g.Hq * HD / 2, tag_of(layer, E_ATTN), reinterpret_cast<uint32_t*>(xbig),
@@ -737,13 +881,14 @@ __device__ __forceinline__ void consumer(const Args& a, const Geo& g, Ctl* c, co
     k.cbar();
     rs = k.norm_scale(xres, g.H);
     B1_STAMP(6);
-    // ---- gate_up: rows gate(f0) up(f0) gate(f0+1) up(f0+1) per feature pair -> SiLU gate
-    phase_items(k, lbase + g.off_gu, 2 * g.FW, g.LH, xres, lbase + g.off_dn);
+    // ---- gate_up (rows in memory order, Geo::row) -> SiLU gate per feature pair
+    phase_items(k, lbase + g.off_gu, 2 * g.FW, g.LH, xres, lbase + g.off_dn, layer);
     {
       const uint32_t tg = tag_of(layer, E_ACT);
       for (int u = ct; u < g.FW / 2; u += CT) {
-        const float g0 = row_sum(c, 4 * u, iH) * rs, u0 = row_sum(c, 4 * u + 1, iH) * rs;
-        const float g1 = row_sum(c, 4 * u + 2, iH) * rs, u1 = row_sum(c, 4 * u + 3, iH) * rs;
+        const int f = w * g.FW + 2 * u;
+        const float g0 = row_sum(c, g.gu_pos(w, f, 0), iH) * rs, u0 = row_sum(c, g.gu_pos(w, f, 1), iH) * rs;
+        const float g1 = row_sum(c, g.gu_pos(w, f + 1, 0), iH) * rs, u1 = row_sum(c, g.gu_pos(w, f + 1, 1), iH) * rs;
         gstore(a.gran, a.g_act + (w * g.FW) / 2 + u, tg,
                pack2(g0 / (1.f + __expf(-g0)) * u0, g1 / (1.f + __expf(-g1)) * u1));
       }
@@ -783,42 +928,75 @@ __device__ __forceinline__ void consumer(const Args& a, const Geo& g, Ctl* c, co
   }
 }
 
+template <int GQ>
 __global__ void __launch_bounds__(NTHR, 1) decode_b1_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   Ctl* c = reinterpret_cast<Ctl*>(smem + a.off_ctl);
   if (threadIdx.x == 0) {
-    c->landed = 0;
+    for (int i = 0; i < NLW; ++i) c->landed[i] = 0;
     c->cbar = 0;
     c->abort_ = 0;
     for (int i = 0; i < NCW; ++i) c->cur[i] = 0;
   }
   __syncthreads();
-  const Geo g(a);
-  if (threadIdx.x < 64)
-    loader(a, g, c, smem);
+  if (threadIdx.x < 64 * NLW)
+    loader(a, c, smem, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   else
-    consumer(a, g, c, smem, smem);
+    consumer<GQ>(a, c, smem, smem);
 }
 
+}  // namespace b1
+
+// The loader's schedule: every (layer, phase, row) of workgroup w in line order,
+// consecutive rows that are adjacent in memory merged into one run. Built once per
+// model (the weights never move); the same Geo::row as the consumers, so the two
+// sides cannot disagree on the order.
+namespace b1 {
+__global__ void decode_b1_runs_kernel(Args a, uint64_t* runs, int stride, int* overflow) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= NWG) return;
+  const Geo g(a);
+  uint64_t* rt = runs + static_cast<int64_t>(w) * stride * 2;
+  int k = -1;
+  uint64_t end = 0;
+  for (int layer = 0; layer < a.L; ++layer)
+    for (int p = 0; p < 4; ++p) {
+      const int lp = g.lpr(p);
+      const uint64_t W = a.wptr[layer * 4 + p];
+      for (int r = 0; r < g.nrows(p); ++r) {
+        const uint64_t ptr = W + static_cast<uint64_t>(g.row(p, w, r)) * lp * LINE;
+        if (k >= 0 && ptr == end) {
+          rt[2 * k + 1] += lp;
+        } else {
+          if (++k >= stride - 1) { atomicAdd(overflow, 1); return; }
+          rt[2 * k] = ptr;
+          rt[2 * k + 1] = lp;
+        }
+        end = ptr + static_cast<uint64_t>(lp) * LINE;
+      }
+    }
+  rt[2 * (k + 1)] = 0;
+  rt[2 * (k + 1) + 1] = 0;
+}
 }  // namespace b1
 
 // ---------------------------------------------------------------- host side
 // Plan: LDS carve-up, granule offsets, ring size. Returns the granule count, or -1
 // when the shape is not supported (the caller keeps the multi-launch path).
-int decode_b1_plan(int L, int H, int F, int Hq, int Hkv, int* out /*[12]*/) {
+int decode_b1_plan(int L, int H, int F, int Hq, int Hkv, int* out /*[13]*/) {
   using namespace b1;
   if (Hkv < 1 || Hq % Hkv || NWG % Hkv || H % (512 * 1) || F % 512 || (Hq * HD) % 512) return -1;
   const int G = Hq / Hkv, WPG = NWG / Hkv;
-  if (G > 8 || ((G + 2) * HD) % WPG) return -1;
+  if ((G != 1 && G != 2 && G != 4 && G != 8) || ((G + 2) * HD) % WPG) return -1;
   const int RPW = (G + 2) * HD / WPG, RO = H / NWG, FW = F / NWG;
-  if (H % (2 * NWG) || F % (2 * NWG) || RPW < NCW || RO / 2 < NCW || FW / 2 < NCW || (FW % 2)) return -1;
+  if (H % (2 * NWG) || F % (2 * NWG) || RPW < 1 || (FW % 2)) return -1;
   auto items = [](int rows, int K) { return rows * ((K / 512 + SEG - 1) / SEG); };
   if (items(RPW, H) > 256 || items(RO, Hq * HD) > 256 || items(2 * FW, H) > 256 || items(RO, F) > 256) return -1;
   const int S_att = WPG < 32 ? WPG : 32;
   if ((G * HD) % S_att || ((G * HD / S_att) % 2)) return -1;
   // LDS: ring | xres (H bf16) | xbig (max(Hq*128, F) bf16, also the attention scratch) | ctl
   const int xres = H * 2;
-  const int scratch_attn = ((G + 2) * HD * 4 + G * HD * 2 + 2 * HD * 2 + NCW * G * 64 * 4 + 2 * NCW * G * 4 +
+  const int scratch_attn = ((G + 2) * HD * 4 + G * HD * 2 + 2 * HD * 2 + NCW * 64 * 8 * 4 + 2 * NCW * G * 4 +
                             NCW * G * HD * 4);
   const int scratch_comb = S_att * (G * HD / S_att + 2) * 4;
   int xbig = std::max(std::max(Hq * HD, F) * 2, std::max(scratch_attn, scratch_comb));
@@ -841,37 +1019,64 @@ int decode_b1_plan(int L, int H, int F, int Hq, int Hkv, int* out /*[12]*/) {
   out[9] = o; o += Hkv * S_att * G * (HD + 2);       // g_part
   out[10] = o; o += Hq * HD / 2;                     // g_attn
   out[11] = o; o += F / 2;                           // g_act
+  out[12] = L * (RPW + 2 * RO + 2 * FW) + 2;          // run-table entries per workgroup (bound)
   (void)L;
   return o;
 }
 
+static void b1_geometry(b1::Args& a, const int* pl, int L, int H, int F, int Hq, int Hkv) {
+  a.L = L; a.H = H; a.F = F; a.Hq = Hq; a.Hkv = Hkv;
+  a.S_att = pl[0]; a.ring_lines = pl[1];
+  a.off_xres = pl[2]; a.off_xbig = pl[3]; a.off_ctl = pl[4];
+  a.g_resid = pl[6]; a.g_post = pl[7]; a.g_qkv = pl[8]; a.g_part = pl[9]; a.g_attn = pl[10]; a.g_act = pl[11];
+  a.runs_stride = pl[12];
+}
+
+// Once per model: the loaders' run tables (runs: NWG * plan[12] * 2 uint64).
+int decode_b1_build_runs(const uint64_t* wptr, int L, int H, int F, int Hq, int Hkv, uint64_t* runs, int* overflow,
+                         hipStream_t st) {
+  using namespace b1;
+  int pl[13];
+  if (decode_b1_plan(L, H, F, Hq, Hkv, pl) < 0) return -1;
+  Args a{};
+  a.wptr = wptr;
+  b1_geometry(a, pl, L, H, F, Hq, Hkv);
+  hipLaunchKernelGGL(decode_b1_runs_kernel, dim3(NWG / 64), dim3(64), 0, st, a, runs, pl[12], overflow);
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
 int decode_b1(const uint64_t* wptr, const uint64_t* kvptr, const uint16_t* resid_in, const uint16_t* final_norm,
               uint16_t* out, const int32_t* positions, const int32_t* slot_mapping, const int32_t* block_table,
-              const int32_t* seq_lens, const float* cos_sin, uint64_t* gran, int* ctl, int L, int H, int F, int Hq,
-              int Hkv, int bs, int apply_rope, float eps, float scale, uint64_t* stamps, hipStream_t st) {
+              const int32_t* seq_lens, const float* cos_sin, uint64_t* gran, int* ctl, const uint64_t* runs, int L,
+              int H, int F, int Hq, int Hkv, int bs, int apply_rope, float eps, float scale, uint64_t* stamps,
+              hipStream_t st) {
   using namespace b1;
-  int pl[12];
+  int pl[13];
   const int ng = decode_b1_plan(L, H, F, Hq, Hkv, pl);
   if (ng < 0 || bs != 16) return -1;  // 16-key pages (attention address arithmetic)
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(decode_b1_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-      return -2;
-    attr_set = true;
+  const int G = Hq / Hkv;
+  const void* kern = G == 1   ? reinterpret_cast<const void*>(decode_b1_kernel<1>)
+                     : G == 2 ? reinterpret_cast<const void*>(decode_b1_kernel<2>)
+                     : G == 4 ? reinterpret_cast<const void*>(decode_b1_kernel<4>)
+                     : G == 8 ? reinterpret_cast<const void*>(decode_b1_kernel<8>)
+                              : nullptr;
+  if (kern == nullptr) return -1;
+  static bool attr_set[9] = {};
+  if (!attr_set[G]) {
+    if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) return -2;
+    attr_set[G] = true;
   }
   Args a{};
   a.wptr = wptr; a.kvptr = kvptr; a.resid_in = resid_in; a.final_norm = final_norm; a.out = out;
   a.positions = positions; a.slot_mapping = slot_mapping; a.block_table = block_table; a.seq_lens = seq_lens;
-  a.cos_sin = cos_sin; a.gran = gran; a.ctl = ctl;
-  a.L = L; a.H = H; a.F = F; a.Hq = Hq; a.Hkv = Hkv; a.bs = bs; a.apply_rope = apply_rope;
+  a.cos_sin = cos_sin; a.gran = gran; a.ctl = ctl; a.runs = runs;
+  b1_geometry(a, pl, L, H, F, Hq, Hkv);
+  a.bs = bs; a.apply_rope = apply_rope;
   a.eps = eps; a.scale = scale;
-  a.S_att = pl[0]; a.ring_lines = pl[1];
-  a.off_xres = pl[2]; a.off_xbig = pl[3]; a.off_ctl = pl[4];
   a.stamps = stamps;
-  a.g_resid = pl[6]; a.g_post = pl[7]; a.g_qkv = pl[8]; a.g_part = pl[9]; a.g_attn = pl[10]; a.g_act = pl[11];
   if (hipMemsetAsync(gran, 0, static_cast<size_t>(ng) * 8, st) != hipSuccess) return -3;
-  hipLaunchKernelGGL(decode_b1_kernel, dim3(NWG), dim3(NTHR), pl[5], st, a);
+  void* args[] = {&a};
+  if (hipLaunchKernel(kern, dim3(NWG), dim3(NTHR), args, pl[5], st) != hipSuccess) return -4;
   return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 

@@ -50,6 +50,13 @@ class B1Decoder:
         self.wptr = torch.tensor([[l.qkv.data_ptr(), l.o.data_ptr(), l.gate_up.data_ptr(), l.down.data_ptr()]
                                   for l in layers], dtype=torch.int64, device=dev)
         self._layers = list(layers)  # keeps the weights (and so the pointers) alive
+        # the loaders' schedule: each workgroup's weight lines as contiguous runs (built once)
+        self.runs = torch.zeros(256 * self.plan[13] * 2, dtype=torch.int64, device=dev)
+        overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.k.decode_b1_build_runs(self.wptr.data_ptr(), self.L, H, F, Hq, Hkv, self.runs.data_ptr(),
+                                    overflow.data_ptr(), stream_ptr())
+        if int(overflow.item()):
+            raise RuntimeError("decode_b1: run table overflow")
         self.gran = torch.empty(self.plan[0], dtype=torch.int64, device=dev)
         self.ctl = torch.zeros(4, dtype=torch.int32, device=dev)  # timeouts, limit, fault injection
         self.h_err = torch.zeros(1, dtype=torch.int32, pin_memory=True)
@@ -79,7 +86,7 @@ class B1Decoder:
         return int(self.ctl[0].item())
 
     # ------------------------------------------------------------------ diagnostics
-    NSTAMP = 16
+    NSTAMP = 18
     PHASES = ("resid gather + norm", "QKV rows", "attention + combine", "attn gather", "O rows",
               "post gather + norm", "gate_up rows", "act gather", "down rows")
 
@@ -97,6 +104,7 @@ class B1Decoder:
         tick_us = 1000.0 / self._khz
         att = ph[:32, :, [2, 10, 11, 12, 13, 14, 15, 3]]        # attention sub-phases (splits 0..31)
         ad = ((att[:, :, 1:] - att[:, :, :-1]) * tick_us).sum(1)
+        gu_loop = ((ph[:, :, 17] - ph[:, :, 16]) * tick_us).sum(1)
         ph = ph[:, :, :10]
         d = (ph[:, :, 1:] - ph[:, :, :-1]) * tick_us           # [wg, layer, 9]
         nxt = torch.cat([ph[:, 1:, 0], ph[:, -1:, 9]], 1)      # next layer's start
@@ -108,6 +116,7 @@ class B1Decoder:
         rep = {name: (float(per[:, i].mean()), float(per[:, i].max())) for i, name in enumerate(self.PHASES)}
         rep["layer tail (down -> next layer)"] = (float(tail.sum(1).mean()), float(tail.sum(1).max()))
         rep["total"] = (float(tot.mean()), float(tot.max()))
+        rep["  gate_up item loop (consumer 0)"] = (float(gu_loop.mean()), float(gu_loop.max()))
         rep["loader ring-full stall"] = (float(extra[:, 0].mean()), float(extra[:, 0].max()))
         rep["consumer line wait"] = (float(extra[:, 2].mean()), float(extra[:, 2].max()))
         lspan = (st[256 * self.L * self.NSTAMP:].view(256, 4)[:, 1].double() - ph[:, 0, 0]) * tick_us
@@ -115,6 +124,18 @@ class B1Decoder:
         for i, name in enumerate(("kv prefetch issue", "qkv gather", "rope", "softmax.V", "partials publish",
                                   "combine gather", "combine + publish")):
             rep["  attn: " + name] = (float(ad[:, i].mean()), float(ad[:, i].max()))
+        # hand-off edges: producer skew (last - first workgroup to publish) and the time
+        # from the last publish to the consumers' completion (mean), summed over layers
+        for name, pi, ci in (("post (O -> gate_up)", 5, 6), ("act (gate_up -> down)", 7, 8),
+                             ("attn (combine -> O)", 3, 4)):
+            prod, cons = ph[:, :, pi], ph[:, :, ci]
+            skew = ((prod.max(0).values - prod.min(0).values) * tick_us).sum()
+            lat = ((cons.mean(0) - prod.max(0).values) * tick_us).sum()
+            rep["  edge " + name + ": skew / after-last"] = (float(skew), float(lat))
+        prod, cons = ph[:, :-1, 9], ph[:, 1:, 1]
+        rep["  edge resid (down -> next QKV): skew / after-last"] = (
+            float(((prod.max(0).values - prod.min(0).values) * tick_us).sum()),
+            float(((cons.mean(0) - prod.max(0).values) * tick_us).sum()))
         return rep
 
     # ------------------------------------------------------------------ launch
@@ -138,7 +159,7 @@ class B1Decoder:
         self.k.decode_b1(self.wptr.data_ptr(), kvp.data_ptr(), resid.data_ptr(), self.final_norm.data_ptr(),
                          self.out.data_ptr(), positions.data_ptr(), slot_mapping.data_ptr(), block_tables.data_ptr(),
                          seq_lens.data_ptr(), cos_sin.data_ptr(), self.gran.data_ptr(), self.ctl.data_ptr(),
-                         self.L, self.H, self.F, self.Hq, self.Hkv, bs, int(self.use_rope), self.eps, self.scale,
+                         self.runs.data_ptr(), self.L, self.H, self.F, self.Hq, self.Hkv, bs, int(self.use_rope), self.eps, self.scale,
                          0 if self.stamps is None else self.stamps.data_ptr(), stream_ptr())
         return self.out
 
