@@ -24,6 +24,7 @@
 //   * the next KV tile's global loads are issued before the current tile's
 //     MFMAs and written to LDS after the barrier (T14).
 #include "common.h"
+#include "glds.h"
 
 namespace xgk {
 
@@ -224,6 +225,343 @@ __global__ void __launch_bounds__(256 * GH) prefill_attn_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// prefill_attn2_kernel: the D = 128 path (Llama-3 / Mixtral heads).
+//
+// The kernel above gives each wave 16 query rows, so every 1 KiB K or V fragment
+// read from LDS feeds one 16x16x32 MFMA: at 256 B/clk of LDS per CU that caps the
+// MFMA pipe near half rate, and its one-tile register prefetch behind a dependent
+// block-table load leaves the HBM latency exposed on short prompts (the 512-token
+// prompt of a continuous-batching step ran 29 us per layer). This kernel:
+//   * 32 query rows per wave on v_mfma_f32_32x32x16_bf16: swapped S^T = K . Q^T
+//     (Q^T fragments in registers, K rows by ds_read_b128), so a lane owns one
+//     query row (lane & 31) and its 32 scores of a 64-key tile; row max / sum are
+//     one xor-32 shuffle each. The S^T accumulator IS the B operand of
+//     O^T += V^T . P^T (guide §3, permuted k order); V^T fragments come from
+//     ds_read_b64_tr_b16. Half the LDS bytes per MFMA of the 16-row form;
+//   * K and V tiles by LDS-DMA (global_load_lds_dwordx4, no staging registers,
+//     no LDS stores) into an NSLOT-deep ring, NSLOT - 1 tiles ahead; the source
+//     chunk is XOR-permuted so the DMA's lane-linear destination lands in the
+//     image (b) layout of cdna_hip_programming.md T10 (row & 3, row >> 2 XOR),
+//     conflict-free for both the K row reads and the V transposed reads;
+//   * each wave's DMA rows of a tile lie in one KV page (bs % 16 == 0), so the
+//     page index is a wave-uniform scalar load -- no dependent vector load, and
+//     counted vmcnt waits see only the DMAs; keys past the sequence end are
+//     clamped to its last row (finite data, probability 0);
+//   * one raw s_barrier per tile; a wave skips the MFMAs of tiles wholly above
+//     its rows' causal diagonal;
+//   * grid = (row tile, head group) flattened with the head group fastest: at
+//     8 kv-head groups each XCD streams one kv head's K/V; heavy (late) row
+//     tiles of every sequence are dispatched first;
+//   * KS = 2 key phases for short prompts: the waves of phase p take the odd / even
+//     64-key tiles of a 128-key ring slot and merge (m, l, O) through LDS at the end,
+//     halving the serial tile chain of the heaviest (last) row tile;
+//   * softmax in base 2 with the scale folded into one FMA, row max / sum across the
+//     two lane halves by v_permlane32_swap, and the O rescale skipped exactly when no
+//     row of the wave raised its max (ballot).
+// NW waves = GH query heads (one GQA group slice) x NW/GH/KS 32-row blocks x KS.
+// ---------------------------------------------------------------------------
+template <int NW, int GH, int KS, int NSLOT>
+struct Pf2Cfg {
+  static constexpr int D = 128;
+  static constexpr int RB = NW / GH / KS;       // 32-row blocks per head
+  static constexpr int BM = 32 * RB;            // query rows per workgroup (per head)
+  static constexpr int BN = 64;                 // keys per compute tile
+  static constexpr int SK = BN * KS;            // keys per ring slot (one tile per key phase)
+  static constexpr int WROWS = SK / NW;         // DMA rows per wave per slot
+  static constexpr int NDMA = WROWS / 4;        // 1-KiB DMAs per wave per slot, each of K and V
+  static constexpr int TILE = BN * D * 2;       // bytes of one K (or V) 64-key tile
+  static constexpr int SLOT = 2 * KS * TILE;    // [K phase 0 .. KS-1][V phase 0 .. KS-1]
+  static_assert(NW % (GH * KS) == 0 && WROWS % 4 == 0 && WROWS <= 16 && NSLOT >= 2 && NSLOT <= 4, "wave layout");
+  static_assert(NSLOT * SLOT <= 160 * 1024, "LDS");
+};
+
+// image (b): 256-B rows, 16-B chunk ch of row r at chunk slot ch ^ xsw(r)
+__device__ __forceinline__ int pf2_xsw(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ int pf2_off(int r, int ch) { return r * 256 + ((ch ^ pf2_xsw(r)) << 4); }
+
+__device__ __forceinline__ f32x16_t mfma32x32x16(bf16x8_t a, bf16x8_t b, f32x16_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+#else
+  return c;
+#endif
+}
+
+__device__ __forceinline__ void sched_fence() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
+// value combined with lane ^ 32's: v_permlane32_swap of x with itself leaves the
+// low half's values in element 0 and the high half's in element 1, in every lane
+__device__ __forceinline__ float xor32_max(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+#else
+  return x;
+#endif
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+#else
+  return x;
+#endif
+}
+
+__device__ __forceinline__ float fast_exp2(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_exp2f(x);
+#else
+  return x;
+#endif
+}
+
+template <int NW, int GH, int KS, int NSLOT>
+__global__ void __launch_bounds__(64 * NW, (NW == 4 && NSLOT <= 2 ? 2 : 1)) prefill_attn2_kernel(
+    const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* __restrict__ kc,
+    const uint16_t* __restrict__ vc, const int32_t* __restrict__ block_tables, int bt_stride,
+    const int32_t* __restrict__ qsl, const int32_t* __restrict__ seq_lens, uint16_t* __restrict__ out,
+    int64_t out_stride, int num_seqs, int Hq, int Hkv, int bs, float scale_log2, int tiles_per_seq, int n_hg) {
+  using C = Pf2Cfg<NW, GH, KS, NSLOT>;
+  constexpr int D = C::D;
+  const int bid = blockIdx.x;
+  const int hg = bid % n_hg;
+  const int rest = bid / n_hg;
+  const int s = rest % num_seqs;
+  const int qt = tiles_per_seq - 1 - rest / num_seqs;  // heavy (late) row tiles first
+  const int q0 = qsl[s];
+  const int qlen = qsl[s + 1] - q0;
+  const int i0 = qt * C::BM;
+  if (i0 >= qlen) return;
+  const int L = seq_lens[s];
+  const int ctx = L - qlen;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int hh = w % GH, rb = (w / GH) % C::RB, kp = w / (GH * C::RB);  // head, row block, key phase
+  const int h = hg * GH + hh;
+  const int kvh = (hg * GH) / (Hq / Hkv);
+  const int r = lane & 31, hf = lane >> 5;
+
+  __shared__ __attribute__((aligned(16))) char lds[NSLOT * C::SLOT];
+
+  // Q^T (B operand of S^T): lane holds Q[row r][16 ks + 8 hf + 0..7]
+  const int my_row = i0 + rb * 32 + r;
+  bf16x8_t qf[D / 16];
+  {
+    const int row = my_row < qlen ? my_row : 0;
+    const uint16_t* qp = q + static_cast<int64_t>(q0 + row) * q_stride + static_cast<int64_t>(h) * D + 8 * hf;
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) qf[ks] = as_frag(ld16(qp + 16 * ks));
+    // pin the loads' completion here, before the loop: hipcc's waitcnt pass does not
+    // see the asm DMAs, and a wait it placed at the first use inside the loop would
+    // count them
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) asm volatile("" : "+v"(qf[ks]));
+  }
+  // causal limit of this lane's row (rows past qlen: any finite limit, never stored)
+  const int lim = min(ctx + my_row, L - 1);
+  const int wave_hi = min(ctx + i0 + rb * 32 + 31, L - 1);  // largest limit in the wave
+  const int wave_lo = ctx + i0 + rb * 32;                   // smallest
+  const int kend = min(L, ctx + min(qlen, i0 + C::BM));
+  const int ntiles = (kend + C::BN - 1) / C::BN;
+  const int nslots = (ntiles + KS - 1) / KS;               // ring fills (super-tiles)
+  const int32_t* btr = block_tables + static_cast<int64_t>(s) * bt_stride;
+
+  auto issue = [&](int t) {  // super-tile t: keys [t * SK, + SK)
+    char* kb = lds + (t % NSLOT) * C::SLOT;
+    const int key0 = min(t * C::SK + w * C::WROWS, L - 1);
+    const int pidx = key0 / bs;
+    const int pg = btr[pidx];  // wave-uniform: scalar load
+    const int64_t pbase = (static_cast<int64_t>(pg) * Hkv + kvh) * bs - static_cast<int64_t>(pidx) * bs;
+#pragma unroll
+    for (int i = 0; i < C::NDMA; ++i) {
+      const int srow = w * C::WROWS + 4 * i + (lane >> 4);  // row in the super-tile
+      const int kabs = min(t * C::SK + srow, L - 1);
+      const int ch = (lane & 15) ^ pf2_xsw(srow & 63);
+      const int64_t off = (pbase + kabs) * D + ch * 8;  // kabs lies in page pidx
+      // phase srow / 64, row srow % 64 of its tile
+      char* dst = kb + (srow >> 6) * C::TILE + ((w * C::WROWS + 4 * i) & 63) * 256;
+      glds16(kc + off, dst);
+      glds16(vc + off, dst + KS * C::TILE);
+    }
+  };
+
+  f32x16_t o[D / 32];
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[db][e] = 0.f;
+  float m = -INFINITY, l = 0.f;  // m in raw score units (scale applied inside exp2)
+
+  wait_vmcnt<0>();  // Q fragments landed; from here on only the DMAs are counted
+#pragma unroll
+  for (int p = 0; p < NSLOT - 1; ++p)
+    if (p < nslots) issue(p);
+
+  const int g = lane >> 4, gi = lane & 15;
+  const int tq = gi >> 2, tp = gi & 3;
+  for (int j = 0; j < nslots; ++j) {
+    // own DMAs of super-tile j done (later ones may stay in flight), then everyone's
+    {
+      const int ahead = min(NSLOT - 2, nslots - 1 - j);  // later super-tiles issued so far
+      if constexpr (NSLOT >= 4) {
+        if (ahead >= 2) wait_vmcnt<4 * C::NDMA>();
+        else if (ahead == 1) wait_vmcnt<2 * C::NDMA>();
+        else wait_vmcnt<0>();
+      } else if constexpr (NSLOT == 3) {
+        if (ahead >= 1) wait_vmcnt<2 * C::NDMA>();
+        else wait_vmcnt<0>();
+      } else {
+        wait_vmcnt<0>();
+      }
+    }
+    raw_barrier();
+    if (j + NSLOT - 1 < nslots) issue(j + NSLOT - 1);
+    const int tile = j * KS + kp;
+    const int kv0 = tile * C::BN;
+    if (tile >= ntiles || kv0 > wave_hi) continue;  // wave-uniform: nothing of this tile is visible
+    // lane byte offsets into the tile (image (b)); per-read parts are one XOR with a
+    // constant: K chunk 2 ks + hf -> ^ (ks << 5); V chunk 4 db + .. -> ^ (db << 6)
+    const uint32_t kt_off = (j % NSLOT) * C::SLOT + kp * C::TILE;
+    const uint32_t k_lane = (kt_off + r * 256) ^ (static_cast<uint32_t>(hf ^ pf2_xsw(r)) << 4);
+    const uint32_t v_row = kt_off + KS * C::TILE + (4 * hf + tq) * 256 + 8 * (tp & 1);
+    const uint32_t v_lane0 = (v_row + ((((2 * (g & 1) + (tp >> 1)) ^ (hf & 3)) << 4))) | (tq << 6);
+    const uint32_t v_lane1 = (v_row + 8 * 256 + ((((2 * (g & 1) + (tp >> 1)) ^ ((hf + 2) & 3)) << 4))) | (tq << 6);
+
+    // ---- S^T = K . Q^T: two 32-key blocks
+    f32x16_t sacc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) sacc[kb][e] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        const uint4 kf = *reinterpret_cast<const uint4*>(lds + ((k_lane ^ (ks << 5)) + kb * 8192));
+        sacc[kb] = mfma32x32x16(as_frag(kf), qf[ks], sacc[kb]);
+      }
+      sched_fence();  // bound the hoisted fragment reads (registers)
+    }
+    // ---- online softmax (base 2, scale folded into one FMA) on this lane's query row
+    const bool need_mask = kv0 + C::BN - 1 > wave_lo || kv0 + C::BN > L;
+    float mx = -INFINITY;
+    if (need_mask) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int key = kv0 + kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * hf;
+          if (key > lim) sacc[kb][e] = -INFINITY;
+          mx = fmaxf(mx, sacc[kb][e]);
+        }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sacc[kb][e]);
+    }
+    mx = xor32_max(mx);
+    const float m_new = fmaxf(m, mx);
+    const float nms = m_new == -INFINITY ? 0.f : -m_new * scale_log2;
+    // exact rescale skip: no row of the wave raised its max -> alpha = 1 everywhere
+    if (__builtin_amdgcn_ballot_w64(m_new > m) != 0) {
+      const float alpha = fast_exp2(fmaf(m, scale_log2, nms));  // m = -inf -> 0
+      l *= alpha;
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[db][e] *= alpha;
+      m = m_new;
+    }
+    float rs = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const float pv = fast_exp2(fmaf(sacc[kb][e], scale_log2, nms));
+        sacc[kb][e] = pv;
+        rs += pv;
+      }
+    l += xor32_sum(rs);
+
+    // ---- O^T += V^T . P^T: k-step (kb, ss) takes accumulator registers 8 ss .. 8 ss + 7
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        uint4 pb;
+        pb.x = pack2(sacc[kb][8 * ss + 0], sacc[kb][8 * ss + 1]);
+        pb.y = pack2(sacc[kb][8 * ss + 2], sacc[kb][8 * ss + 3]);
+        pb.z = pack2(sacc[kb][8 * ss + 4], sacc[kb][8 * ss + 5]);
+        pb.w = pack2(sacc[kb][8 * ss + 6], sacc[kb][8 * ss + 7]);
+        const bf16x8_t pf = as_frag(pb);
+        // rows kb*32 + 16 ss + 4 hf + tq (elements 0..3) and + 8 (elements 4..7)
+#pragma unroll
+        for (int db = 0; db < D / 32; ++db) {
+          const uint32_t ro = (kb * 32 + 16 * ss) * 256;
+          const bf16x4_t a0 = lds_read_tr16(reinterpret_cast<const uint16_t*>(lds + ((v_lane0 ^ (db << 6)) + ro)));
+          const bf16x4_t a1 = lds_read_tr16(reinterpret_cast<const uint16_t*>(lds + ((v_lane1 ^ (db << 6)) + ro)));
+          const bf16x8_t vf = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+          o[db] = mfma32x32x16(vf, pf, o[db]);
+        }
+        sched_fence();
+      }
+  }
+
+  if constexpr (KS > 1) {
+    // merge the key phases of each (head, row block) through the (drained) ring:
+    // float slot [((pw * (KS - 1) + kp - 1) * 66 + idx) * 64 + lane], idx 0..63 = O, 64 = m, 65 = l
+    static_assert(GH * C::RB * (KS - 1) * 66 * 64 * 4 <= NSLOT * C::SLOT, "merge area");
+    float* mg = reinterpret_cast<float*>(lds);
+    const int pw = w % (GH * C::RB);
+    raw_barrier();  // every wave is past its last ring read (all DMAs were waited)
+    if (kp > 0) {
+      float* d = mg + (pw * (KS - 1) + kp - 1) * 66 * 64 + lane;
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) d[(db * 16 + e) * 64] = o[db][e];
+      d[64 * 64] = m;
+      d[65 * 64] = l;
+    }
+    __syncthreads();
+    if (kp > 0) return;
+#pragma unroll
+    for (int k = 1; k < KS; ++k) {
+      const float* d = mg + (pw * (KS - 1) + k - 1) * 66 * 64 + lane;
+      const float m2 = d[64 * 64], l2 = d[65 * 64];
+      const float M = fmaxf(m, m2);
+      const float Ms = M == -INFINITY ? 0.f : M * scale_log2;
+      const float a1 = fast_exp2(m * scale_log2 - Ms), a2 = fast_exp2(m2 * scale_log2 - Ms);
+      l = l * a1 + l2 * a2;
+      m = M;
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[db][e] = o[db][e] * a1 + d[(db * 16 + e) * 64] * a2;
+    }
+  }
+
+  // ---- epilogue: lane holds O[row r][32 db + 8 t + 4 hf + 0..3] in registers 4t .. 4t+3
+  if (my_row < qlen) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    uint16_t* op = out + static_cast<int64_t>(q0 + my_row) * out_stride + static_cast<int64_t>(h) * D + 4 * hf;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        uint2 v;
+        v.x = pack2(o[db][4 * t + 0] * inv, o[db][4 * t + 1] * inv);
+        v.y = pack2(o[db][4 * t + 2] * inv, o[db][4 * t + 3] * inv);
+        *reinterpret_cast<uint2*>(op + db * 32 + 8 * t) = v;
+      }
+  }
+}
+
 // GQA grouping: GH query heads of one kv head per workgroup (4*GH waves). gh <= 0
 // picks the widest GH in {4, 2, 1} dividing the group size that still gives >= 256
 // workgroups (one per CU); measured (bench/prefill_bench.py, profiles/
@@ -237,6 +575,52 @@ int prefill_attention(const uint16_t* q, int64_t q_stride, const uint16_t* kc, c
   if (num_seqs <= 0 || max_q_len <= 0) return 0;
   if (bs % 16 != 0 || Hq % Hkv != 0) return -1;
   const int G = Hq / Hkv;
+  // D = 128: prefill_attn2_kernel. gh == 0 picks the configuration; gh < 0 forces
+  // -gh = 10 * NW + GH (A/B and tests); gh > 0 selects the 16-row kernel above.
+  if (D == 128 && gh <= 0) {
+    int nw = 0, ghh = 0, ns = 0, ks = 1;
+    if (gh < 0) {  // -gh = 1000 * (KS - 1) + 100 * NSLOT + 10 * NW + GH (NSLOT 0: default)
+      ks = 1 + (-gh) / 1000;
+      ns = ((-gh) / 100) % 10;
+      nw = ((-gh) / 10) % 10;
+      ghh = (-gh) % 10;
+    } else {
+      ghh = G % 2 == 0 ? 2 : 1;
+      // 8 waves: 128 rows x 2 heads once that still gives two workgroups per CU; else
+      // 64 rows x 2 heads x 2 key phases (short prompts: half the serial tile chain).
+      // profiles/r3_prefill_attn2.md: 8K 882 / 2K 598 / 512 17 us (8B heads)
+      const int64_t wg8 = static_cast<int64_t>(num_seqs) * ((max_q_len + 32 * (8 / ghh) - 1) / (32 * (8 / ghh))) *
+                          (Hq / ghh);
+      nw = 8;
+      ks = wg8 >= 512 ? 1 : 2;
+    }
+    if (ns == 0) ns = ks == 2 ? 2 : (nw == 8 ? 3 : 2);
+    if (G % ghh != 0 || nw % (ghh * ks) != 0) return -1;
+    const int bm = 32 * (nw / ghh / ks);
+    const int tps = (max_q_len + bm - 1) / bm;
+    const int n_hg = Hq / ghh;
+    const float sl2 = scale * 1.4426950408889634f;
+    dim3 grid(static_cast<unsigned>(static_cast<int64_t>(num_seqs) * tps * n_hg)), block(64 * nw);
+#define XGK_PF2(NW, GH, KS, NS)                                                                              \
+  hipLaunchKernelGGL((prefill_attn2_kernel<NW, GH, KS, NS>), grid, block, 0, st, q, q_stride, kc, vc, bt, \
+                     bt_stride, qsl, seq_lens, out, out_stride, num_seqs, Hq, Hkv, bs, sl2, tps, n_hg)
+    const int code = ((ks * 10 + ns) * 10 + nw) * 10 + ghh;
+    switch (code) {
+      case 1384: XGK_PF2(8, 4, 1, 3); break;
+      case 1382: XGK_PF2(8, 2, 1, 3); break;
+      case 1381: XGK_PF2(8, 1, 1, 3); break;
+      case 1388: XGK_PF2(8, 8, 1, 3); break;
+      case 1244: XGK_PF2(4, 4, 1, 2); break;
+      case 1242: XGK_PF2(4, 2, 1, 2); break;
+      case 1241: XGK_PF2(4, 1, 1, 2); break;
+      case 2284: XGK_PF2(8, 4, 2, 2); break;
+      case 2282: XGK_PF2(8, 2, 2, 2); break;
+      case 2281: XGK_PF2(8, 1, 2, 2); break;
+      default: return -1;
+    }
+#undef XGK_PF2
+    return 0;
+  }
   const int tps = (max_q_len + 63) / 64;
   if (gh <= 0) {
     gh = 1;

@@ -153,6 +153,44 @@ def test_prefill_attention(Hq, Hkv, D, gh, qlens, ctxs):
     torch.testing.assert_close(out.cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
 
 
+# gh < 0: prefill_attn2_kernel forced to -gh = 10 * waves + heads per workgroup (D = 128)
+@pytest.mark.parametrize("Hq,Hkv,gh", [(32, 8, -44), (32, 8, -84), (32, 8, -82), (32, 8, -81), (32, 8, -42),
+                                       (32, 8, -41), (32, 8, -244), (32, 8, -1284), (32, 8, -1282), (32, 8, -1281), (8, 1, -1284), (8, 1, -88), (8, 1, -84), (64, 8, 0)])
+@pytest.mark.parametrize("qlens,ctxs,bs", [([100], [0], 16), ([64, 1, 130, 7], [0, 5, 40, 300], 16),
+                                           ([5, 5], [1000, 17], 16), ([700, 33], [300, 0], 32),
+                                           ([513], [0], 64)])
+def test_prefill_attention_mfma32(Hq, Hkv, gh, qlens, ctxs, bs):
+    D = 128
+    lens = [q + c for q, c in zip(qlens, ctxs)]
+    kc, vc, bt = _paged(lens, Hkv, D, bs)
+    T = sum(qlens)
+    qkv = rnd(T, (Hq + 2 * Hkv) * D)
+    q = qkv[:, :Hq * D].view(T, Hq, D)
+    qsl = torch.tensor([0] + list(torch.cumsum(torch.tensor(qlens), 0)), dtype=torch.int32, device=DEV)
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    scale = 1.0 / math.sqrt(D)
+    out = ops.prefill_attention(q, kc, vc, bt, qsl, sl, max(qlens), scale, gh=gh)
+    ref = ops.prefill_attention_ref(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), qsl.cpu(), sl.cpu(), scale)
+    torch.testing.assert_close(out.cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_prefill_attention_nan_past_end():
+    """Cache rows past a sequence's end hold NaN: the clamped DMA rows must never reach the output."""
+    Hq, Hkv, D, bs = 32, 8, 128, 16
+    lens = [37]
+    kc, vc, bt = _paged(lens, Hkv, D, bs, extra_pages=0)
+    pg = int(bt[0, 2])  # last page: rows 5.. lie past the end (37 = 2 * 16 + 5)
+    kc[pg, :, 5:] = float("nan")
+    vc[pg, :, 5:] = float("nan")
+    q = rnd(37, Hq, D)
+    qsl = torch.tensor([0, 37], dtype=torch.int32, device=DEV)
+    sl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    for gh in (0, -44, -84, -1284):
+        out = ops.prefill_attention(q, kc, vc, bt, qsl, sl, 37, 0.088, gh=gh)
+        ref = ops.prefill_attention_ref(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), qsl.cpu(), sl.cpu(), 0.088)
+        torch.testing.assert_close(out.cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
+
+
 def test_prefill_attention_spike_forces_rescale():
     # one large key early then a larger one late: the online max must rescale
     Hq, Hkv, D, bs = 8, 8, 128, 16

@@ -122,6 +122,10 @@ class ModelRunner:
     def decode_splits(self, bs: int) -> int:
         wgs = max(1, bs * self.Hkv)
         target = self.DECODE_SPLIT_WGS
+        if 4 * wgs >= 3 * target:
+            # within a quarter of the target (e.g. the 63 decode rows of a mixed step):
+            # a second split would only add the combine launch
+            return 1
         return int(max(1, min(self.max_splits, (target + wgs - 1) // wgs)))
 
     # ------------------------------------------------------------------ graph buffers
