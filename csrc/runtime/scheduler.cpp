@@ -205,40 +205,6 @@ void StepScheduler::emit(Sequence& s, int q, bool prefill, bool sample) {
   plan_seqs_.push_back(&s);
 }
 
-// Trim the last emitted prefill chunk so the step's token count lands on a
-// multiple of align_tokens when it overshoots one by <= align_slack (see
-// SchedulerConfig). Only a plain prompt chunk that keeps >= 1 token is trimmed; a
-// chunk that would have completed its prompt no longer samples this step.
-void StepScheduler::align_step() {
-  StepPlan& p = plan_;
-  const int A = cfg_.align_tokens;
-  if (A <= 0 || p.num_seqs == 0 || p.num_tokens <= A) return;
-  const int r = p.num_tokens % A;
-  if (r == 0 || r > cfg_.align_slack) return;
-  const int i = p.num_seqs - 1;
-  Sequence* s = plan_seqs_.back();
-  if (s == nullptr || !p.is_prefill[i] || p.is_embed[i] || !s->draft.empty() || p.q_lens[i] <= r) return;
-  p.input_ids.resize(p.input_ids.size() - r);
-  p.positions.resize(p.positions.size() - r);
-  p.slot_mapping.resize(p.slot_mapping.size() - r);
-  p.q_lens[i] -= r;
-  p.seq_lens[i] -= r;
-  p.num_tokens -= r;
-  p.query_start_loc.back() -= r;
-  if (p.do_sample[i]) {  // the prompt no longer completes this step
-    p.do_sample[i] = 0;
-    p.logits_indices.pop_back();
-    p.sample_seq_index.pop_back();
-    --p.num_sample;
-  }
-  p.max_q_len = 0;
-  p.max_seq_len = 0;
-  for (int j = 0; j < p.num_seqs; ++j) {
-    p.max_q_len = std::max(p.max_q_len, p.q_lens[j]);
-    p.max_seq_len = std::max(p.max_seq_len, p.seq_lens[j]);
-  }
-}
-
 const StepPlan& StepScheduler::schedule() {
   plan_ = StepPlan{};
   plan_.query_start_loc.push_back(0);
@@ -310,9 +276,20 @@ const StepPlan& StepScheduler::schedule() {
                                 [](Sequence* s) { return s->status != SeqStatus::Running; }),
                  running_.end());
 
-  // Pass 3: admissions.
+  // Pass 3: admissions (behind the admission window, see SchedulerConfig).
   const int reserve_pages = static_cast<int>(cfg_.admit_watermark * cfg_.num_blocks);
-  while (!waiting_.empty() && budget > 0 && static_cast<int>(running_.size()) < cfg_.max_num_seqs &&
+  bool hold = false;
+  if (cfg_.coalesce_prompts > 1 && plan_.num_decodes > 0 && n_prefill == 0 && !waiting_.empty()) {
+    int ready = 0;
+    for (const Sequence* s : waiting_) {
+      if (s->tokens.back() == kPlaceholder) break;
+      if (++ready >= cfg_.coalesce_prompts) break;
+    }
+    const int room = cfg_.max_num_seqs - static_cast<int>(running_.size());
+    hold = ready < std::min(cfg_.coalesce_prompts, std::max(room, 1)) &&
+           waiting_.front()->wait_plans < cfg_.coalesce_max_wait;
+  }
+  while (!hold && !waiting_.empty() && budget > 0 && static_cast<int>(running_.size()) < cfg_.max_num_seqs &&
          n_prefill < cfg_.max_prefill_seqs) {
     Sequence* s = waiting_.front();
     if (s->tokens.back() == kPlaceholder) break;  // preempted by a lookahead plan: wait for commit()
@@ -359,8 +336,7 @@ const StepPlan& StepScheduler::schedule() {
     ++n_prefill;
     budget -= q;
   }
-
-  align_step();
+  for (Sequence* s : waiting_) ++s->wait_plans;
 
   // Block tables.
   int w = 1;

@@ -51,14 +51,15 @@ struct SchedulerConfig {
   // Stall-free batching: prompt chunks ride on the decode step's weight reads
   // instead of stalling every running stream behind one large prefill step.
   int decode_prefill_cap = 0;
-  // GEMM-tile alignment of mixed steps: when a step's token count exceeds a
-  // multiple of align_tokens by at most align_slack, its last prefill chunk is
-  // trimmed back to that multiple (the trimmed tokens run next step). The prefill
-  // projections (hipBLASLt) cost a step function of M with steps at multiples of
-  // 256 rows: Llama-3-8B M 575 costs 286 us/layer, M 512 221 us
-  // (profiles/r2_prefill_m_sweep.jsonl). 0: off.
-  int align_tokens = 0;
-  int align_slack = 0;
+  // Admission window for continuous batching (Req 2.1/2.2 batching window, applied to
+  // prompt admission): while decode rows are running, new prompts are held until
+  // coalesce_prompts of them are waiting or the oldest has been passed over by
+  // coalesce_max_wait plans, then admitted together into one mixed step (one larger
+  // prefill GEMM instead of several M ~ 575 ones). With no decode rows running a
+  // prompt is admitted at once. coalesce_prompts <= 1: off (every prompt admitted
+  // at the first plan that has room).
+  int coalesce_prompts = 1;
+  int coalesce_max_wait = 4;
   // lookahead() over prompt steps (1) or pure-decode plans only (0)
   int lookahead_mixed = 1;
   // a length-finishing row: released at lookahead() so the next plan can admit into
@@ -82,6 +83,7 @@ struct Sequence {
   bool ignore_eos = false;
   bool embed = false;  // prefill-only (embeddings endpoint)
   bool released_early = false;  // length-finishing row released at lookahead(); reported at commit()
+  int wait_plans = 0;            // plans that passed this waiting prompt over (admission window)
   std::vector<std::vector<int32_t>> stop_seqs;
   std::vector<int> blocks;
   std::vector<int32_t> draft;  // speculative tokens for the next step
@@ -177,7 +179,6 @@ class StepScheduler {
   void preempt(Sequence& s);
   void insert_waiting(Sequence* s);
   void emit(Sequence& s, int q_len, bool prefill, bool sample);
-  void align_step();
   int check_stop(Sequence& s);
   void forget(Sequence* s);  // drop s from the plan / lookahead records
 

@@ -227,59 +227,65 @@ def test_kv_usage_excludes_evictable_prefix_pages():
     assert st["kv_usage"] == 0.0
 
 
-def test_mixed_step_tile_alignment():
-    """align_tokens / align_slack: 63 decoding rows + a 512-token prompt (575 tokens,
-    63 past the 512 multiple) -> the prompt chunk is trimmed to 449 (no sample this
-    step), the remaining 63 prompt tokens run next step and that step samples it.
-    The token streams equal the unaligned run's (chunking never changes results)."""
-    def make(align):
-        c = R.SchedulerConfig()
-        c.block_size = 16
-        c.num_blocks = 512
-        c.max_num_seqs = 128
-        c.max_num_batched_tokens = 8192
-        c.max_model_len = 2048
-        c.enable_prefix_cache = False
-        c.align_tokens = 256 if align else 0
-        c.align_slack = 64
-        return R.StepScheduler(c)
+def _coalesce_sched(k, wait):
+    c = R.SchedulerConfig()
+    c.block_size = 16
+    c.num_blocks = 1024
+    c.max_num_seqs = 64
+    c.max_num_batched_tokens = 8192
+    c.max_model_len = 2048
+    c.enable_prefix_cache = False
+    c.coalesce_prompts = k
+    c.coalesce_max_wait = wait
+    return R.StepScheduler(c)
 
-    def run(align):
-        s = make(align)
-        for i in range(63):
-            assert s.add(i + 1, [7, 8, 9 + i], 50, 1, True, False, [], 0)
-        plan = s.schedule()  # the 63 prompts (189 tokens < 256: untouched)
-        assert plan["num_tokens"] == 189
-        s.update(np.full(63, 5, np.int32), np.ones(63, np.int32))
-        assert s.add(100, list(range(1000, 1512)), 4, 1, True, False, [], 0)
-        plans, outs = [], []
-        plan = s.schedule()
-        while plan["num_tokens"] > 0 and len(plans) < 60:
-            plans.append(plan)
-            toks = np.array([3 + int(plan["seq_ids"][j]) % 5 for j in plan["sample_seq_index"]], np.int32)
-            outs.append([(int(plan["seq_ids"][j]), int(t)) for j, t in zip(plan["sample_seq_index"], toks)])
-            s.update(toks, np.ones(len(toks), np.int32))
-            plan = s.schedule()
-        return plans, outs
 
-    p_al, o_al = run(True)
-    p_no, o_no = run(False)
-    assert p_no[0]["num_tokens"] == 575
-    first = p_al[0]
-    assert first["num_tokens"] == 512 and first["num_decodes"] == 63
-    assert int(first["q_lens"][-1]) == 449 and 100 not in [int(first["seq_ids"][j]) for j in first["sample_seq_index"]]
-    second = p_al[1]
-    assert second["num_tokens"] == 63 + 63 and int(second["q_lens"][-1]) == 63
-    assert 100 in [int(second["seq_ids"][j]) for j in second["sample_seq_index"]]
-    # same per-sequence token streams
-    def streams(outs):
-        d = {}
-        for step in outs:
-            for sid, t in step:
-                d.setdefault(sid, []).append(t)
-        return d
-    assert streams(o_al) == streams(o_no)
+def _step(s, plan):
+    n = int(plan["num_sample"])
+    s.update(np.full(n, 5, np.int32), np.ones(n, np.int32))
+    return s.schedule()
 
+
+def test_admission_window_coalesces_prompts():
+    """coalesce_prompts = 2: with decode rows running, a lone new prompt waits until a
+    second arrives, then both prefill in ONE mixed step; without decode rows running
+    (idle GPU) a prompt is admitted at once."""
+    s = _coalesce_sched(2, 100)
+    assert s.add(1, list(range(10, 30)), 50, 1, True, False, [], 0)
+    plan = s.schedule()
+    assert [int(x) for x in plan["seq_ids"]] == [1]          # nothing decoding: no hold
+    plan = _step(s, plan)
+    assert s.add(2, list(range(40, 60)), 50, 1, True, False, [], 0)
+    for _ in range(3):                                      # decode-only while 2 waits alone
+        plan = _step(s, plan)
+        assert int(plan["num_tokens"]) == 1 and s.num_waiting() == 1
+    assert s.add(3, list(range(70, 90)), 50, 1, True, False, [], 0)
+    plan = _step(s, plan)
+    ids = [int(x) for x in plan["seq_ids"]]
+    assert ids == [1, 2, 3] and int(plan["num_tokens"]) == 1 + 20 + 20 and s.num_waiting() == 0
+
+
+def test_admission_window_wait_bound():
+    """A lone prompt is admitted after coalesce_max_wait plans passed it over."""
+    s = _coalesce_sched(4, 3)
+    assert s.add(1, list(range(10, 30)), 50, 1, True, False, [], 0)
+    plan = _step(s, s.schedule())
+    assert s.add(2, list(range(40, 60)), 50, 1, True, False, [], 0)
+    waited = 0
+    while 2 not in [int(x) for x in plan["seq_ids"]]:
+        plan = _step(s, plan)
+        waited += 1
+        assert waited <= 4
+    assert waited == 4  # passed over by 3 plans, admitted by the 4th
+
+
+def test_admission_window_off_admits_at_once():
+    s = _coalesce_sched(1, 4)
+    assert s.add(1, list(range(10, 30)), 50, 1, True, False, [], 0)
+    plan = _step(s, s.schedule())
+    assert s.add(2, list(range(40, 60)), 50, 1, True, False, [], 0)
+    plan = _step(s, plan)
+    assert 2 in [int(x) for x in plan["seq_ids"]]
 
 def test_overlap_outputs_go_to_the_sink_immediately(monkeypatch):
     """A serving replica sets LLMEngine.output_sink: outputs detokenised in a step's

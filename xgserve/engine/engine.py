@@ -78,6 +78,11 @@ class EngineConfig:
     max_prefill_seqs: int = 1 << 30
     # prefill tokens allowed in a step that also decodes (0: only the token budget)
     decode_prefill_cap: int = 0
+    # admission window (continuous batching): while rows decode, hold new prompts until
+    # prompt_coalesce of them wait or the oldest was passed over by
+    # prompt_coalesce_max_wait steps, then prefill them in one mixed step (1: off)
+    prompt_coalesce: int = 1
+    prompt_coalesce_max_wait: int = 4
     # speculative decoding (Req 12)
     draft_model: Optional[str] = None
     num_speculative_tokens: int = 0
@@ -143,6 +148,8 @@ class LLMEngine:
         sc.cache_threshold = cfg.cache_threshold
         sc.max_prefill_seqs = cfg.max_prefill_seqs
         sc.decode_prefill_cap = cfg.decode_prefill_cap
+        sc.coalesce_prompts = max(1, int(cfg.prompt_coalesce))
+        sc.coalesce_max_wait = max(0, int(cfg.prompt_coalesce_max_wait))
         # asynchronous scheduling over prompt steps too (r2_async_mixed_ab.md)
         sc.lookahead_mixed = 1
         # release length-finishing rows at lookahead: the next step is planned before a

@@ -65,6 +65,10 @@ class BatcherSection:
     batch_timeout_ms: float = 50.0
     max_sequence_length: int = 8192
     padding_token_id: int = 0
+    # continuous mode: admission window over prompt admission (1: off); see
+    # EngineConfig.prompt_coalesce
+    coalesce_prompts: int = 1
+    coalesce_max_wait_steps: int = 4
 
 
 @dataclass
@@ -172,6 +176,8 @@ class ServerConfig:
             e.append("batcher.max_batch_size must be > 0")
         if b.batch_timeout_ms < 0:
             e.append("batcher.batch_timeout_ms must be >= 0")
+        if b.coalesce_prompts < 1 or b.coalesce_max_wait_steps < 0:
+            e.append("batcher.coalesce_prompts must be >= 1 and batcher.coalesce_max_wait_steps >= 0")
         s = self.scheduler
         if s.strategy not in ("round_robin", "least_loaded", "memory_aware"):
             e.append(f"scheduler.strategy must be round_robin|least_loaded|memory_aware, got {s.strategy!r}")

@@ -252,7 +252,7 @@ class InferenceServer:
 
     async def _spawn_set(self, cfg: ServerConfig, ready_timeout: Optional[float]) -> List[int]:
         w = cfg.worker
-        spec = engine_spec(w, cfg.cache, cfg.spec, self.fault)
+        spec = engine_spec(w, cfg.cache, cfg.spec, self.fault, cfg.batcher)
         gpus = self._gpu_list(w)
         n = 1 if self._engine is not None else w.replicas
         new: List[Replica] = []

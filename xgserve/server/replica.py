@@ -38,7 +38,7 @@ HEARTBEAT_S = 0.5
 # ---------------------------------------------------------------------------
 # engine construction (runs inside the replica)
 # ---------------------------------------------------------------------------
-def engine_spec(worker, cache=None, spec=None, fault: Optional[dict] = None) -> dict:
+def engine_spec(worker, cache=None, spec=None, fault: Optional[dict] = None, batcher=None) -> dict:
     """Plain-dict (picklable) description of one replica's engine. `fault` holds
     MockEngine fault-injection knobs (crash_after_steps, eos_every)."""
     dt = {"bf16": "bfloat16", "fp16": "float16", "fp32": "float32", "fp8": "bfloat16"}[worker.quantization]
@@ -54,6 +54,8 @@ def engine_spec(worker, cache=None, spec=None, fault: Optional[dict] = None) -> 
                 draft_model=None if spec is None else spec.draft_model,
                 num_speculative_tokens=0 if spec is None else spec.num_speculative_tokens,
                 min_acceptance_rate=0.5 if spec is None else spec.min_acceptance_rate,
+                prompt_coalesce=1 if batcher is None else batcher.coalesce_prompts,
+                prompt_coalesce_max_wait=4 if batcher is None else batcher.coalesce_max_wait_steps,
                 fault=dict(fault or {}))
 
 
