@@ -238,7 +238,7 @@ void moe_align(const int32_t* ids, int T, int k, int E, int expert_offset, int b
 template <int SP>
 __global__ void __launch_bounds__(256) combine_kernel(const void* __restrict__ y, int S, int P,
                                                       const int32_t* __restrict__ dest, const float* __restrict__ w,
-                                                      uint16_t* __restrict__ out, int k, int H) {
+                                                      void* __restrict__ out, int k, int H, int out_f32) {
   const int t = blockIdx.x;
   for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -267,7 +267,13 @@ __global__ void __launch_bounds__(256) combine_kernel(const void* __restrict__ y
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] += wt * f[i];
     }
-    st16(out + static_cast<int64_t>(t) * H + c * 8, pack8(acc));
+    if (out_f32) {  // fp32 rows for a TP all-reduce: no bf16 rounding, no cast launch
+      float* o = static_cast<float*>(out) + static_cast<int64_t>(t) * H + c * 8;
+      *reinterpret_cast<float4*>(o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      *reinterpret_cast<float4*>(o + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    } else {
+      st16(static_cast<uint16_t*>(out) + static_cast<int64_t>(t) * H + c * 8, pack8(acc));
+    }
   }
 }
 
@@ -342,16 +348,16 @@ int moe_combine_resid(const float* part, int S, int P, const int32_t* dest, cons
   }
 }
 
-int moe_combine(const void* y, int S, int P, const int32_t* dest, const float* w, uint16_t* out, int T, int k, int H,
-                hipStream_t st) {
+int moe_combine(const void* y, int S, int P, const int32_t* dest, const float* w, void* out, int T, int k, int H,
+                hipStream_t st, int out_f32) {
   if (T <= 0) return 0;
   if (H % 8) return 1;
   const dim3 g(T), b(256);
   switch (S) {
-    case 0: hipLaunchKernelGGL(combine_kernel<0>, g, b, 0, st, y, S, P, dest, w, out, k, H); return 0;
-    case 1: hipLaunchKernelGGL(combine_kernel<1>, g, b, 0, st, y, S, P, dest, w, out, k, H); return 0;
-    case 2: hipLaunchKernelGGL(combine_kernel<2>, g, b, 0, st, y, S, P, dest, w, out, k, H); return 0;
-    case 4: hipLaunchKernelGGL(combine_kernel<4>, g, b, 0, st, y, S, P, dest, w, out, k, H); return 0;
+    case 0: hipLaunchKernelGGL(combine_kernel<0>, g, b, 0, st, y, S, P, dest, w, out, k, H, out_f32); return 0;
+    case 1: hipLaunchKernelGGL(combine_kernel<1>, g, b, 0, st, y, S, P, dest, w, out, k, H, out_f32); return 0;
+    case 2: hipLaunchKernelGGL(combine_kernel<2>, g, b, 0, st, y, S, P, dest, w, out, k, H, out_f32); return 0;
+    case 4: hipLaunchKernelGGL(combine_kernel<4>, g, b, 0, st, y, S, P, dest, w, out, k, H, out_f32); return 0;
     default: return 1;
   }
 }

@@ -53,7 +53,7 @@ int gemm_w8(const uint16_t*, int, int, const uint8_t*, const float*, int, float*
             hipStream_t);
 void moe_topk_softmax(const void*, int, int, int, int, int, float*, int32_t*, hipStream_t);
 void moe_align(const int32_t*, int, int, int, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
-int moe_combine(const void*, int, int, const int32_t*, const float*, uint16_t*, int, int, int, hipStream_t);
+int moe_combine(const void*, int, int, const int32_t*, const float*, void*, int, int, int, hipStream_t, int);
 int moe_route(const uint16_t*, const uint16_t*, int, int, int, int, int, float*, int32_t*, hipStream_t,
               const uint16_t*, float, uint16_t*);
 int moe_combine_resid(const float*, int, int, const int32_t*, const float*, uint16_t*, float*, int, int, int,
@@ -331,11 +331,12 @@ PYBIND11_MODULE(_kernels, m) {
           "ep_scatter");
   });
   m.def("moe_combine", [](uintptr_t y, int splits, int P_, uintptr_t dest, uintptr_t w, uintptr_t out, int T, int k,
-                          int H, uintptr_t st) {
-    check(xgk::moe_combine(P<const void>(y), splits, P_, P<const int32_t>(dest), P<const float>(w), P<uint16_t>(out),
-                           T, k, H, S(st)),
+                          int H, uintptr_t st, int out_f32) {
+    check(xgk::moe_combine(P<const void>(y), splits, P_, P<const int32_t>(dest), P<const float>(w), P<void>(out),
+                           T, k, H, S(st), out_f32),
           "moe_combine");
-  });
+  }, py::arg("y"), py::arg("splits"), py::arg("P"), py::arg("dest"), py::arg("w"), py::arg("out"), py::arg("T"),
+     py::arg("k"), py::arg("H"), py::arg("st"), py::arg("out_f32") = 0);
   m.def("device_synchronize", []() {
     hipError_t e = hipDeviceSynchronize();
     if (e != hipSuccess) throw std::runtime_error(hipGetErrorString(e));

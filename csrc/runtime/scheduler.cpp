@@ -285,9 +285,9 @@ const StepPlan& StepScheduler::schedule() {
       if (s->tokens.back() == kPlaceholder) break;
       if (++ready >= cfg_.coalesce_prompts) break;
     }
-    const int room = cfg_.max_num_seqs - static_cast<int>(running_.size());
-    hold = ready < std::min(cfg_.coalesce_prompts, std::max(room, 1)) &&
-           waiting_.front()->wait_plans < cfg_.coalesce_max_wait;
+    // (free slots can be fewer than coalesce_prompts: rows finishing meanwhile make
+    // room, and the wait bound caps the hold either way)
+    hold = ready < cfg_.coalesce_prompts && waiting_.front()->wait_plans < cfg_.coalesce_max_wait;
   }
   while (!hold && !waiting_.empty() && budget > 0 && static_cast<int>(running_.size()) < cfg_.max_num_seqs &&
          n_prefill < cfg_.max_prefill_seqs) {

@@ -377,8 +377,8 @@ class LlamaLayer(nn.Module):
         hn, w, ids = ops.moe_route_norm(resid, self.post_norm, eps, self.router, self.cfg.experts_per_token)
         ss = ws.ss[site + 1]
         if self.tp > 1:
-            part = ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset)
-            comm.tp_allreduce_resid(part.float().unsqueeze(0), resid, ss)
+            part = ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, out_f32=True)
+            comm.tp_allreduce_resid(part.unsqueeze(0), resid, ss)
         else:
             ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, resid=resid, ss=ss)
         return RowStats(ss, H // 1024, T)

@@ -118,7 +118,7 @@ def moe_forward_ref(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w
 
 def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
               topk_ids: torch.Tensor, expert_offset: int = 0, resid: Optional[torch.Tensor] = None,
-              ss: Optional[torch.Tensor] = None):
+              ss: Optional[torch.Tensor] = None, out_f32: bool = False):
     """Local-expert MoE FFN: sum_j w_j * FFN_{e_j}(x) over choices owned locally
     (ids in [expert_offset, expert_offset + E_local)); others contribute nothing.
 
@@ -131,7 +131,7 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     if not use_native(x):
         out = moe_forward_ref(x, w13, w2, topk_w, topk_ids, expert_offset)
         if resid is None:
-            return out
+            return out.float() if out_f32 else out
         r = (resid.float() + out.float()).to(resid.dtype)
         resid.copy_(r)
         T, H = r.shape
@@ -169,9 +169,9 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
         kn.moe_combine_resid(part.data_ptr(), S, P, dest.data_ptr(), topk_w.float().contiguous().data_ptr(),
                              resid.data_ptr(), ss.data_ptr(), T, k, H, stream_ptr())
         return None
-    out = torch.empty(T, H, dtype=x.dtype, device=x.device)
+    out = torch.empty(T, H, dtype=torch.float32 if out_f32 else x.dtype, device=x.device)
     kn.moe_combine(part.data_ptr(), S, P, dest.data_ptr(), topk_w.float().contiguous().data_ptr(), out.data_ptr(), T,
-                   k, H, stream_ptr())
+                   k, H, stream_ptr(), 1 if out_f32 else 0)
     return out
 
 
