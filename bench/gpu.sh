@@ -72,7 +72,9 @@ prefill)
 serve)
   run bench_long 300 $B --steps 3000 --warmup 100
   run serve 400 python -u bench/serve_bench.py --launch "--model llama3-8b --max-num-seqs 64" --concurrency 64 \
-      --prompt-len 512 --output-len 256 --warmup 40 --duration 40 --out "$o/serve_8b_c64.jsonl" "$@" ;;
+      --prompt-len 512 --output-len 256 --warmup 40 --duration 40 --out "$o/serve_8b_c64.jsonl" "$@"
+  run serve_fe2 400 python -u bench/serve_bench.py --launch "--model llama3-8b --max-num-seqs 64 --frontends 2" \
+      --concurrency 64 --prompt-len 512 --output-len 256 --warmup 40 --duration 40 --out "$o/serve_8b_c64.jsonl" "$@" ;;
 tune)
   export PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_MAX_TUNING_DURATION_MS=100
   export XGS_GEMM_TUNING=0   # tune from scratch (do not replay the shipped table)

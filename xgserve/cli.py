@@ -73,10 +73,11 @@ def cmd_serve(a) -> int:
     from .server.app import serve
     from .server.orchestrator import InferenceServer
     try:
-        if cfg.api.frontends > 1:
+        nfe = cfg.api.resolved_frontends(cfg.worker)
+        if nfe > 1:
             import asyncio
             from .server.frontend import run_hub
-            asyncio.run(run_hub(InferenceServer(cfg), cfg.api.frontends))
+            asyncio.run(run_hub(InferenceServer(cfg), nfe))
         else:
             serve(InferenceServer(cfg))
     except ApiError as e:

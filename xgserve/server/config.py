@@ -34,8 +34,16 @@ class ApiConfig:
     max_request_size: int = 4 * 1024 * 1024
     request_timeout_s: float = 300.0
     # HTTP front-end processes (SO_REUSEPORT) over the one orchestrator process;
-    # 1 = HTTP on the orchestrator's own event loop (server/frontend.py)
-    frontends: int = 1
+    # 1 = HTTP on the orchestrator's own event loop (server/frontend.py); 0 = auto:
+    # 2 when GPU process replicas serve (one replica's ~10k token events/s: delivery
+    # p99 12.4 ms on one loop, 6.9 ms on two, profiles/r3_frontend.md), else 1
+    frontends: int = 0
+
+    def resolved_frontends(self, worker) -> int:
+        if self.frontends > 0:
+            return self.frontends
+        gpu = not worker.mock and not worker.in_process and (worker.device or "cuda") != "cpu"
+        return 2 if gpu else 1
 
 
 @dataclass
@@ -169,6 +177,8 @@ class ServerConfig:
             e.append("validator token limits must be > 0")
         if v.min_temperature > v.max_temperature or v.min_top_p > v.max_top_p:
             e.append("validator ranges must satisfy min <= max")
+        if self.api.frontends < 0:
+            e.append("api.frontends must be >= 0 (0: auto)")
         b = self.batcher
         if b.mode not in ("continuous", "static"):
             e.append(f"batcher.mode must be continuous|static, got {b.mode!r}")

@@ -181,7 +181,10 @@ class FrontendHub:
             elif op == "m":  # front-end HTTP metrics: (kind, args)
                 getattr(m, msg[1])(*msg[2])
             elif op == "eof":
-                log.error("front end %d exited", wid)
+                if getattr(self, "stopping", False):
+                    log.info("front end %d stopped", wid)
+                else:
+                    log.error("front end %d exited", wid)
                 self.conns.pop(wid, None)
 
     # admin calls whose bad input is a 400 on the single-process server (app.py)
@@ -201,6 +204,7 @@ class FrontendHub:
             self.send(wid, ("rpc", cid, False, error_to_tuple(e)))
 
     def stop(self, timeout: float = 10.0) -> None:
+        self.stopping = True  # front-end EOFs from here on are the requested shutdown
         for c in self.conns.values():
             c.send(("stop",))
             c.close()
