@@ -11,6 +11,7 @@ Sizing notes for MI355X (7 xGMI links x ~153 GB/s per GPU, point-to-point):
 """
 from __future__ import annotations
 
+import os
 import pickle
 from typing import List, Optional
 
@@ -52,17 +53,32 @@ def resid_allreduce_ok(T: int, H: int) -> bool:
     return _CUSTOM_AR is not None and _CUSTOM_AR.can_resid(T, H)
 
 
-def tp_allreduce_resid(part: torch.Tensor, resid: torch.Tensor, ss: torch.Tensor) -> None:
+# Simulated TP all-reduce (bench.py --tp-shard: one rank of a TP group in one process):
+# XGS_SIM_AR_US > 0 makes the local stand-in wait that long (the peer round trip of the
+# one-shot xGMI all-reduce) so the simulation exposes collective latency, and
+# XGS_SIM_AR_PREFETCH_WGS workgroups of the same launch meanwhile touch the next
+# projection's weights (profiles/r3_tp_ar_overlap.md). Both are measurement knobs.
+_SIM_AR_TICKS = int(float(os.environ.get("XGS_SIM_AR_US", "0")) * 100)  # 100 MHz wall clock
+_SIM_AR_PF_WGS = int(os.environ.get("XGS_SIM_AR_PREFETCH_WGS", "0"))
+
+
+def tp_allreduce_resid(part: torch.Tensor, resid: torch.Tensor, ss: torch.Tensor,
+                       prefetch: Optional[torch.Tensor] = None) -> None:
     """Row-parallel projection epilogue of the fused decode layer:
     resid += all-reduce(sum_s part[s]) in place (bf16), ss[chunk * T + t] <- the new
     residual's sum of squares per 1024 columns. `part` is this rank's fp32 split-K
     partials [S, T, H]. One launch on the custom all-reduce; a simulated TP shard
-    (single-rank process) reduces locally."""
+    (single-rank process) reduces locally. `prefetch`: the next projection's weights
+    (the simulated wait may overlap their stream)."""
     from ..ops._native import kernels, stream_ptr
     S, T, H = part.shape
     s = get_state()
     if s.tp_size == 1:
-        kernels().add_partials_resid(part.data_ptr(), S, T, resid.data_ptr(), ss.data_ptr(), H, stream_ptr())
+        pf = prefetch if (prefetch is not None and _SIM_AR_PF_WGS > 0) else None
+        kernels().add_partials_resid(part.data_ptr(), S, T, resid.data_ptr(), ss.data_ptr(), H, stream_ptr(),
+                                     _SIM_AR_TICKS, 0 if pf is None else pf.data_ptr(),
+                                     0 if pf is None else pf.numel() * pf.element_size(),
+                                     _SIM_AR_PF_WGS if pf is not None else 0)
         return
     _CUSTOM_AR.all_reduce_resid(part, resid, ss)
 
