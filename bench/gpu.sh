@@ -12,7 +12,7 @@
 #   serve    HTTP/SSE serve bench (64 streams) next to the in-process long bench
 #   tune     rebuild the shipped TunableOp GEMM tables (xgserve/tuning/)
 #   sweep    gemm_m64g configuration sweep at the TP shard shapes
-#   arsim    one rank of 70B TP8 at batch 1 under a simulated 8 us all-reduce, with / without weight prefetch
+#   arsim    one rank of 70B TP8 at batch 1 under a simulated 0 / 4 / 8 us all-reduce
 #   coalesce admission-window A/B: driver form + 1000 steps at --coalesce 1 / 2 / 3
 #   profile  rocprofv3 kernel + gap profile of the headline (bench/profile.sh)
 #   b1       persistent batch-1 decode: tests, batch-1 bench vs the multi-launch path, profile
@@ -91,8 +91,7 @@ sweep)
       qkv70t8 o70t8 gate_up70t8 down70t8 qkv8t2 o8t2 gate_up8t2 down8t2 qkv8t4 o8t4 gate_up8t4 down8t4 \
       qkv8t8 o8t8 gate_up8t8 down8t8 qkv70t2 o70t2 gate_up70t2 down70t2 qkv70t4 o70t4 gate_up70t4 down70t4 ;;
 arsim)  # simulated xGMI all-reduce latency on one rank of 70B TP8 (XGS_SIM_AR_US), with / without prefetch
-  for cfgv in "XGS_SIM_AR_US=0" "XGS_SIM_AR_US=8" "XGS_SIM_AR_US=8 XGS_SIM_AR_PREFETCH_WGS=128" \
-              "XGS_SIM_AR_US=8 XGS_SIM_AR_PREFETCH_WGS=240" "XGS_SIM_AR_US=0 XGS_SIM_AR_PREFETCH_WGS=128"; do
+  for cfgv in "XGS_SIM_AR_US=0" "XGS_SIM_AR_US=4" "XGS_SIM_AR_US=8"; do
     n=$(echo "$cfgv" | tr -c 'A-Za-z0-9_=\n' '_')
     run "c1_$n" 300 env $cfgv $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20 "$@"
   done ;;

@@ -23,8 +23,7 @@ int skinny_slab_kmax(int);
 int gemm_m64g(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 int gemm_m64g_ex(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, const float*,
                  int, int, float, uint16_t*, float*, int*, hipStream_t);
-void add_partials_resid(const float*, int, int, uint16_t*, float*, int, hipStream_t, uint64_t, const void*, int64_t,
-                        int);
+void add_partials_resid(const float*, int, int, uint16_t*, float*, int, hipStream_t, uint64_t);
 void row_sumsq(const uint16_t*, int, int, float*, hipStream_t);
 void embed_gather(const int32_t*, int, const uint16_t*, int, int, uint16_t*, float*, hipStream_t);
 void mean_l2norm_rows(float*, const int32_t*, const int32_t*, float*, int, int, hipStream_t);
@@ -249,14 +248,12 @@ PYBIND11_MODULE(_kernels, m) {
           "gemm_m64g_ex");
   });
   m.def("add_partials_resid", [](uintptr_t part, int S_, int T, uintptr_t res, uintptr_t ss_part, int H,
-                                 uintptr_t st, uint64_t sim_ticks, uintptr_t pf, int64_t pf_bytes, int n_pf) {
+                                 uintptr_t st, uint64_t sim_ticks) {
     if (H % 1024) throw std::invalid_argument("add_partials_resid: H % 1024 != 0");
-    if (n_pf < 0 || n_pf > 4096) throw std::invalid_argument("add_partials_resid: n_pf out of range");
-    xgk::add_partials_resid(P<const float>(part), S_, T, P<uint16_t>(res), P<float>(ss_part), H, S(st), sim_ticks,
-                            P<const void>(pf), pf_bytes, n_pf);
+    xgk::add_partials_resid(P<const float>(part), S_, T, P<uint16_t>(res), P<float>(ss_part), H, S(st), sim_ticks);
     check(0, "add_partials_resid");
   }, py::arg("part"), py::arg("S"), py::arg("T"), py::arg("res"), py::arg("ss_part"), py::arg("H"), py::arg("st"),
-     py::arg("sim_ticks") = 0, py::arg("pf") = 0, py::arg("pf_bytes") = 0, py::arg("n_pf") = 0);
+     py::arg("sim_ticks") = 0);
   m.def("embed_gather", [](uintptr_t ids, int T, uintptr_t table, int V, int H, uintptr_t out, uintptr_t ss,
                            uintptr_t st) {
     if (H % 8 || T < 0 || V < 1) throw std::invalid_argument("embed_gather: H % 8 != 0 or bad sizes");

@@ -427,45 +427,18 @@ void add_partials_rmsnorm(const float* part, int S, int T, uint16_t* residual, c
 // issued before the adds; 4-8x the workgroups of add_partials_rmsnorm.
 //
 // Simulated TP all-reduce (a --tp-shard run stands in for one rank of a TP group):
-// sim_ticks > 0 makes every reduce workgroup wait that many ticks of the 100 MHz wall
-// clock first -- the peer round trip of the one-shot xGMI all-reduce -- and n_pf extra
-// workgroups meanwhile touch pf_bytes of the NEXT projection's weights (one dword per
-// 64 B, results discarded), so that GEMM finds them in the L2 / Infinity Cache: the
-// peer wait overlaps part of the next weight stream (VERDICT r2 #6 experiment).
-struct ArSim {
-  uint64_t ticks;
-  const uint8_t* pf;
-  int64_t pf_bytes;
-  int n_pf;
-};
-
-__device__ __forceinline__ void prefetch_touch(const uint8_t* p, int64_t bytes, int part, int nparts) {
-  const int64_t per = (bytes / nparts + 8191) & ~static_cast<int64_t>(8191);
-  const int64_t lo = per * part, hi = min(bytes, lo + per);
-  for (int64_t o = lo + threadIdx.x * 64; o < hi; o += 128 * 64) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    uint32_t d;
-    asm volatile("global_load_dword %0, %1, off" : "=v"(d) : "v"(p + o) : "memory");
-#endif
-  }
-#if defined(__HIP_DEVICE_COMPILE__)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-}
-
+// sim_ticks > 0 makes every workgroup wait that many ticks of the 100 MHz wall clock
+// first -- the peer round trip of the one-shot xGMI all-reduce -- so the simulation
+// exposes collective latency (profiles/r3_tp_ar_overlap.md).
 template <int SP>
 __global__ void __launch_bounds__(128) add_partials_resid_kernel(const float* __restrict__ part, int S, int T,
                                                                   uint16_t* __restrict__ residual,
-                                                                  float* __restrict__ ss_part, int H, ArSim sim) {
+                                                                  float* __restrict__ ss_part, int H, uint64_t sim_ticks) {
   __shared__ float red[8];
   const int nchunk = H / 1024;
-  if (static_cast<int>(blockIdx.x) >= T * nchunk) {  // prefetch workgroup
-    prefetch_touch(sim.pf, sim.pf_bytes, blockIdx.x - T * nchunk, sim.n_pf);
-    return;
-  }
-  if (sim.ticks) {
+  if (sim_ticks) {
     const uint64_t t0 = wall_clock64();
-    while (wall_clock64() - t0 < sim.ticks) __builtin_amdgcn_s_sleep(1);
+    while (wall_clock64() - t0 < sim_ticks) __builtin_amdgcn_s_sleep(1);
   }
   const int t = blockIdx.x / nchunk, chunk = blockIdx.x % nchunk;
   const int col = (chunk * 128 + threadIdx.x) * 8;
@@ -505,13 +478,11 @@ __global__ void __launch_bounds__(128) add_partials_resid_kernel(const float* __
 }
 
 void add_partials_resid(const float* part, int S, int T, uint16_t* residual, float* ss_part, int H,
-                        hipStream_t st, uint64_t sim_ticks, const void* pf, int64_t pf_bytes, int n_pf) {
+                        hipStream_t st, uint64_t sim_ticks) {
   if (T <= 0) return;
-  if (pf == nullptr || pf_bytes <= 0) n_pf = 0;
-  const ArSim sim{sim_ticks, static_cast<const uint8_t*>(pf), pf_bytes, n_pf};
-  const dim3 g(T * (H / 1024) + n_pf);
+  const dim3 g(T * (H / 1024));
 #define XGK_APRS(SPV) \
-  hipLaunchKernelGGL((add_partials_resid_kernel<SPV>), g, dim3(128), 0, st, part, S, T, residual, ss_part, H, sim)
+  hipLaunchKernelGGL((add_partials_resid_kernel<SPV>), g, dim3(128), 0, st, part, S, T, residual, ss_part, H, sim_ticks)
   if (S == 1) XGK_APRS(1);
   else if (S == 2) XGK_APRS(2);
   else if (S == 4) XGK_APRS(4);

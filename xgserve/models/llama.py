@@ -40,7 +40,6 @@ from ..ops.linear import (MODE_PARTIAL, MODE_SILU, W8_MAX_M, W8_MIN_ELEMS, Resid
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
 from .config import ModelConfig
 
-_SPLITK_QKV = int(os.environ.get("XGS_SPLITK_QKV", "1"))  # A/B only
 
 
 FAST_M_SMALL = 16   # tokens per step handled entirely by the streaming skinny GEMM
@@ -91,7 +90,6 @@ class LlamaLayer(nn.Module):
         super().__init__()
         self.cfg = cfg
         self.tp, self.rank = tp, rank
-        self._next_layer = ()  # (next LlamaLayer,) once the model is assembled
         Hq, Hkv = local_heads(cfg, tp)
         D, H = cfg.head_dim, cfg.hidden_size
         self.Hq, self.Hkv = Hq, Hkv
@@ -305,10 +303,7 @@ class LlamaLayer(nn.Module):
             o = self._row_parallel_fast(a, self.o, self.split_o)
             h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
             return self.mlp(h), residual
-        if _SPLITK_QKV > 1 and splitk_prefill_ok(h, self.qkv, min_ratio=0) and h.shape[1] % (512 * _SPLITK_QKV) == 0:
-            a = self.attn.from_partials(splitk_linear(h, self.qkv, _SPLITK_QKV), meta, kv, cos_sin)
-        else:
-            a = self.attn(F.linear(h, self.qkv), meta, kv, cos_sin)
+        a = self.attn(F.linear(h, self.qkv), meta, kv, cos_sin)
         if self.tp > 1 and not self.moe and T >= TP_OVERLAP_MIN_TOKENS and TP_OVERLAP_CHUNKS > 1:
             return self._forward_tp_overlap(a, residual)
         o = self._ar(F.linear(a, self.o))
@@ -394,12 +389,11 @@ class LlamaLayer(nn.Module):
         SiLU-gate) -> down GEMM partials -> all-reduce + residual + statistics."""
         T, H = resid.shape
         po = m64_linear(a, self.o, MODE_PARTIAL)
-        comm.tp_allreduce_resid(po.part, resid, ws.ss[site], prefetch=self.gate_up)
+        comm.tp_allreduce_resid(po.part, resid, ws.ss[site])
         st = RowStats(ws.ss[site], H // 1024, T)
         act = m64_norm_linear(resid, self.gate_up, MODE_SILU, st, self.cfg.norm_eps)
         pd = m64_linear(act, self.down, MODE_PARTIAL)
-        nxt = self._next_layer[0].qkv if self._next_layer else None
-        comm.tp_allreduce_resid(pd.part, resid, ws.ss[site + 1], prefetch=nxt)
+        comm.tp_allreduce_resid(pd.part, resid, ws.ss[site + 1])
         return RowStats(ws.ss[site + 1], H // 1024, T)
 
 
@@ -418,8 +412,6 @@ class LlamaForCausalLM(nn.Module):
         self.embed = _p(torch.empty(V, H, device=device, dtype=dtype))
         self.layers = nn.ModuleList([LlamaLayer(cfg, self.tp, self.rank, device, dtype)
                                      for _ in range(cfg.num_layers)])
-        for i, l in enumerate(self.layers):  # a plain tuple: not a registered submodule
-            l._next_layer = (self.layers[i + 1],) if i + 1 < len(self.layers) else ()
         self.norm = _p(torch.ones(H, device=device, dtype=dtype))
         self.lm_head = None if (cfg.tie_embeddings and self.tp == 1) else \
             _p(torch.empty(self.V_pad // self.tp, H, device=device, dtype=dtype))

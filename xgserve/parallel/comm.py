@@ -55,30 +55,23 @@ def resid_allreduce_ok(T: int, H: int) -> bool:
 
 # Simulated TP all-reduce (bench.py --tp-shard: one rank of a TP group in one process):
 # XGS_SIM_AR_US > 0 makes the local stand-in wait that long (the peer round trip of the
-# one-shot xGMI all-reduce) so the simulation exposes collective latency, and
-# XGS_SIM_AR_PREFETCH_WGS workgroups of the same launch meanwhile touch the next
-# projection's weights (profiles/r3_tp_ar_overlap.md). Both are measurement knobs.
+# one-shot xGMI all-reduce), so the simulation exposes collective latency
+# (profiles/r3_tp_ar_overlap.md). A measurement knob.
 _SIM_AR_TICKS = int(float(os.environ.get("XGS_SIM_AR_US", "0")) * 100)  # 100 MHz wall clock
-_SIM_AR_PF_WGS = int(os.environ.get("XGS_SIM_AR_PREFETCH_WGS", "0"))
 
 
-def tp_allreduce_resid(part: torch.Tensor, resid: torch.Tensor, ss: torch.Tensor,
-                       prefetch: Optional[torch.Tensor] = None) -> None:
+def tp_allreduce_resid(part: torch.Tensor, resid: torch.Tensor, ss: torch.Tensor) -> None:
     """Row-parallel projection epilogue of the fused decode layer:
     resid += all-reduce(sum_s part[s]) in place (bf16), ss[chunk * T + t] <- the new
     residual's sum of squares per 1024 columns. `part` is this rank's fp32 split-K
     partials [S, T, H]. One launch on the custom all-reduce; a simulated TP shard
-    (single-rank process) reduces locally. `prefetch`: the next projection's weights
-    (the simulated wait may overlap their stream)."""
+    (single-rank process) reduces locally."""
     from ..ops._native import kernels, stream_ptr
     S, T, H = part.shape
     s = get_state()
     if s.tp_size == 1:
-        pf = prefetch if (prefetch is not None and _SIM_AR_PF_WGS > 0) else None
         kernels().add_partials_resid(part.data_ptr(), S, T, resid.data_ptr(), ss.data_ptr(), H, stream_ptr(),
-                                     _SIM_AR_TICKS, 0 if pf is None else pf.data_ptr(),
-                                     0 if pf is None else pf.numel() * pf.element_size(),
-                                     _SIM_AR_PF_WGS if pf is not None else 0)
+                                     _SIM_AR_TICKS)
         return
     _CUSTOM_AR.all_reduce_resid(part, resid, ss)
 
