@@ -42,8 +42,9 @@ def main():
     ap.add_argument("--caches", type=int, default=7)
     ap.add_argument("--splits", type=int, nargs="+", default=[1, 2])
     ap.add_argument("--iters", type=int, default=70)
+    ap.add_argument("--bs", type=int, default=16)
     a = ap.parse_args()
-    dev, Hq, Hkv, D, bs = "cuda", 32, 8, 128, 16
+    dev, Hq, Hkv, D, bs = "cuda", 32, 8, 128, a.bs
     B = a.B
     g = torch.Generator().manual_seed(0)
     lens = (a.L - torch.randint(0, max(a.stagger, 1), (B,), generator=g)).int()
@@ -77,7 +78,7 @@ def main():
             e.record()
             torch.cuda.synchronize()
             us = s.elapsed_time(e) / a.iters * 1000.0
-            print(json.dumps({"op": "decode_attention_fq", "cache": mode, "B": B, "L": a.L, "stagger": a.stagger,
+            print(json.dumps({"op": "decode_attention_fq", "cache": mode, "B": B, "L": a.L, "stagger": a.stagger, "bs": bs,
                               "splits": S, "us": round(us, 2), "TB/s": round(nbytes / us / 1e6, 3)}), flush=True)
 
 

@@ -48,7 +48,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, nargs="+", default=[32, 64])
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
-    ap.add_argument("--variants", type=int, nargs="+", default=[2, 4])
     ap.add_argument("--moe-sweep", action="store_true",
                     help="sweep the grouped (MoE) gemm_m64g configurations at Mixtral decode shapes")
     ap.add_argument("--w8-sweep", action="store_true",
@@ -91,8 +90,8 @@ def main():
                         S = 1
                     if K % (S * 256):
                         continue
-                    for var in a.variants:
-                        fn = lambda w, nw=nw, S=S, var=var: L.m64_linear(x, w, mode, S, nw, variant=var)  # noqa: E731
+                    for var in (0,):
+                        fn = lambda w, nw=nw, S=S: L.m64_linear(x, w, mode, S, nw)  # noqa: E731
                         us2 = timeit([lambda w=w, fn=fn: fn(w) for w in ws])
                         y = fn(ws[0])
                         if mode == L.MODE_PARTIAL:
@@ -104,7 +103,7 @@ def main():
                         else:
                             want = ref
                         err = float((y.float() - want).norm() / want.norm())
-                        rows.append((f"gemm_m64(nw={nw},S={S},mode={mode},var={var})", us2, err))
+                        rows.append((f"gemm_m64g(nw={nw},S={S},mode={mode},plan)", us2, err))
             if M <= 16 or plan is None:
                 pass
             for op, t, err in rows:
