@@ -156,8 +156,12 @@ class ModelRunner:
         self.h_samp_ss = [_pinned(B, torch.int64) for _ in range(2)]
         self.g_stage_events = [None, None]
         self.g_stage_idx = 0
-        self.g_out_tok = torch.zeros(B, dtype=torch.int32, device=self.device)
-        self.g_out_lp = torch.zeros(B, dtype=torch.float32, device=self.device)
+        # sampled tokens [0, B) and their logprobs [B, 2B) in one buffer: a graph step's
+        # outputs leave in ONE D2H copy (g_out[:B + n]) instead of two
+        self.g_out = torch.zeros(2 * B, dtype=torch.int32, device=self.device)
+        self.g_out_tok = self.g_out[:B]
+        self.g_out_lp = self.g_out[B:].view(torch.float32)
+        self.h_gout = [_pinned(2 * B, torch.int32) for _ in range(2)]
         self.g_greedy_graph: Dict[int, bool] = {}
 
     def _decode_body(self, bs: int, greedy: bool):
@@ -310,9 +314,13 @@ class ModelRunner:
                 torch.cuda.current_stream().synchronize()
             self._check_comm()
             return None, None, hidden
-        i, ev = out
+        i, ev = out[0], out[1]
         self._wait_event(ev)  # this step only: a step queued behind it keeps running
         self._check_comm()
+        if len(out) > 2:  # graph step: tokens and logprobs in one pinned buffer
+            B = out[2]
+            h = self.h_gout[i]
+            return h[:n].numpy().copy(), h[B:B + n].view(torch.float32).numpy().copy(), hidden
         return self.h_toks[i][:n].numpy().copy(), self.h_lps[i][:n].numpy().copy(), hidden
 
     def _execute_graph(self, plan, samp: Optional[SamplingRows], n: int, bs: int, src: Optional[np.ndarray]):
@@ -337,9 +345,8 @@ class ModelRunner:
             hi[4 * B:4 * B + n] = src
         bt = hi[5 * B:5 * B + bs * W].reshape(bs, W)
         bt[:n, :w] = plan["block_tables"].reshape(n, w)
-        # copy ids..src (5*B) and the first bs rows of bt
-        self.g_int[:5 * B].copy_(h_int[:5 * B], non_blocking=True)
-        self.g_int[5 * B:5 * B + bs * W].copy_(h_int[5 * B:5 * B + bs * W], non_blocking=True)
+        # ids..src (5*B) and the first bs rows of bt: one contiguous H2D copy
+        self.g_int[:5 * B + bs * W].copy_(h_int[:5 * B + bs * W], non_blocking=True)
         greedy = samp is None or samp.all_greedy
         if not greedy:
             hf, hsi, hss = self.h_samp_fs[si], self.h_samp_is[si], self.h_samp_ss[si]
@@ -362,7 +369,13 @@ class ModelRunner:
             ev = torch.cuda.Event()
             ev.record()
             return (n, None, None, None, True, ev)
-        return self._record_out(n, self.g_out_tok, self.g_out_lp, None, True)
+        self._poll_comm()
+        i = self.out_idx
+        self.out_idx ^= 1
+        self.h_gout[i][:B + n].copy_(self.g_out[:B + n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return (n, None, None, (i, ev, B), True)
 
     def _execute_eager(self, plan, samp: Optional[SamplingRows], need_hidden: bool, src: Optional[np.ndarray]):
         T = int(plan["num_tokens"])
