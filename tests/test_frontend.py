@@ -185,3 +185,25 @@ def test_client_disconnect_aborts(server):
 
     stats = _run(main())
     assert sum(r["active_requests"] for r in stats["replicas"]) == 0
+
+
+def test_frontend_count_auto():
+    """api.frontends = 0 (default): two front ends for GPU process replicas (Req 5.1 at one
+    replica's token rate, profiles/r3_frontend.md), one for mock / in-process / CPU serving;
+    an explicit count wins; negative counts are rejected."""
+    from xgserve.server.config import ServerConfig
+    c = ServerConfig()
+    assert c.api.frontends == 0
+    assert c.api.resolved_frontends(c.worker) == 2
+    c.worker.mock = True
+    assert c.api.resolved_frontends(c.worker) == 1
+    c.worker.mock = False
+    c.worker.in_process = True
+    assert c.api.resolved_frontends(c.worker) == 1
+    c.worker.in_process = False
+    c.worker.device = "cpu"
+    assert c.api.resolved_frontends(c.worker) == 1
+    c.api.frontends = 3
+    assert c.api.resolved_frontends(c.worker) == 3
+    c.api.frontends = -1
+    assert any("api.frontends" in e for e in c.validate())
