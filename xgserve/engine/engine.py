@@ -49,12 +49,6 @@ EARLY_OUTPUTS = True
 _MASK63 = (1 << 63) - 1
 
 
-def _mix(seed: int, n: int) -> int:
-    x = (seed * 6364136223846793005 + (n + 1) * 1442695040888963407) & _MASK63
-    x ^= x >> 29
-    return (x * 0xBF58476D1CE4E5B9) & _MASK63
-
-
 @dataclass
 class EngineConfig:
     model: str = "llama3-8b"

@@ -173,11 +173,6 @@ class MetricsCollector:
         with self._lock:
             self.rejected_total[reason] += 1
 
-    def record_spec(self, proposed: int, accepted: int):
-        with self._lock:
-            self.spec_proposed += proposed
-            self.spec_accepted += accepted
-
     def set_spec_totals(self, proposed: int, accepted: int, speedup: Optional[float] = None):
         """Absolute draft-token counters (summed over replicas' heartbeats) and the
         measured speculation speedup factor (mean over replicas that report one)."""

@@ -14,7 +14,6 @@ import torch
 from ._native import kernels, stream_ptr, use_native
 
 MODE_BF16, MODE_PARTIAL, MODE_SILU = 0, 1, 2
-SKINNY_MAX_M = 128
 _SPLITS = (1, 2, 4, 7, 8, 14, 16)
 
 
@@ -62,13 +61,6 @@ def choose_split(M: int, N: int, K: int, target_wgs: int = 512) -> int:
         if K % kmax == 0:  # the slab kernel takes exactly kmax of K per workgroup
             return K // kmax
     return pick_split(N, K, target_wgs)
-
-
-def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    M, K = x.shape
-    N = w.shape[0]
-    return (use_native(x) and M <= SKINNY_MAX_M and N % 64 == 0 and K % 256 == 0
-            and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.is_contiguous())
 
 
 def skinny_linear(x: torch.Tensor, w: torch.Tensor, split_k: Optional[int] = None, mode: int = MODE_BF16,
