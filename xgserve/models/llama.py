@@ -162,33 +162,41 @@ class LlamaLayer(nn.Module):
         return self._ar(out)
 
     def _moe_alltoall(self, h: torch.Tensor) -> torch.Tensor:
-        """Expert-parallel MoE with an all_to_all dispatch: this rank routes its token
-        slice, ep_plan/ep_scatter (HIP) pack each (token, choice) row for the rank that
-        owns the expert, the owners run their experts as one grouped GEMM (send_eid =
-        -1 rows are skipped by the align), the rows travel back and ep_combine
-        (HIP) applies the routing weights; an all_gather rebuilds the replicated
-        [T, H] the next layer's head-parallel attention reads.
+        """Expert-parallel MoE with an all_to_all dispatch on the replicated [T, H]
+        input: this rank's token slice goes through `_moe_alltoall_rows`, and an
+        all_gather rebuilds the replicated output. (Prefill-sized steps take the
+        sequence-parallel form instead, `forward_sp`, which never gathers it.)"""
+        T = h.shape[0]
+        per = (T + self.tp - 1) // self.tp
+        lo, hi = min(T, self.rank * per), min(T, (self.rank + 1) * per)
+        out_slice = self._moe_alltoall_rows(h[lo:hi], T, per)
+        return comm.tp_all_gather_rows(out_slice)[:T].contiguous()
+
+    def _moe_alltoall_rows(self, hs: torch.Tensor, T: int, per: int) -> torch.Tensor:
+        """The all_to_all MoE on this rank's rows hs [Ts <= per, H] of a T-token step
+        (rank r owns tokens [r * per, r * per + Ts)) -> [per, H], rows >= Ts zero.
+        ep_plan/ep_scatter (HIP) pack each (token, choice) row for the rank that owns
+        the expert, the owners run their experts as one grouped GEMM (send_eid = -1
+        rows are skipped by the align), the rows travel back and ep_combine (HIP)
+        applies the routing weights.
         Split policy: count-exact (packed layout, splits exchanged first: one host
         sync per layer) for eager steps of >= EP_EXACT_MIN_PAIRS pairs; fixed
         capacity (per * k rows per destination, no host sync) otherwise, which is
         what a captured decode graph needs."""
-        tp, r = self.tp, self.rank
-        T, H = h.shape
+        tp = self.tp
+        Ts, H = hs.shape
         k = self.cfg.experts_per_token
-        per = (T + tp - 1) // tp
-        lo, hi = min(T, r * per), min(T, (r + 1) * per)
-        Ts = hi - lo
         cap = per * k
         if Ts > 0:
-            w, ids = ops.moe_route(h[lo:hi], self.router, k)
+            w, ids = ops.moe_route(hs, self.router, k)
         else:
-            w = torch.empty(0, k, dtype=torch.float32, device=h.device)
-            ids = torch.empty(0, k, dtype=torch.int32, device=h.device)
-        capturing = h.is_cuda and torch.cuda.is_current_stream_capturing()
+            w = torch.empty(0, k, dtype=torch.float32, device=hs.device)
+            ids = torch.empty(0, k, dtype=torch.int32, device=hs.device)
+        capturing = hs.is_cuda and torch.cuda.is_current_stream_capturing()
         packed = not capturing and T * k >= EP_EXACT_MIN_PAIRS
         slot, send_eid, counts = ops.ep_plan(ids, self.E_local, tp, cap, packed)
         rows = Ts * k if packed else tp * cap
-        send = ops.ep_scatter(h[lo:hi], k, slot, rows)
+        send = ops.ep_scatter(hs, k, slot, rows)
         if packed:
             recv_counts = comm.tp_exchange_counts(counts)
             send_splits, recv_splits = counts.tolist(), recv_counts.tolist()
@@ -196,13 +204,38 @@ class LlamaLayer(nn.Module):
             send_splits = recv_splits = [cap] * tp
         recv = comm.tp_all_to_all(send, send_splits, recv_splits)
         recv_eid = comm.tp_all_to_all(send_eid.view(-1, 1), send_splits, recv_splits).view(-1, 1)
-        ones = torch.ones(recv.shape[0], 1, dtype=torch.float32, device=h.device)
+        ones = torch.ones(recv.shape[0], 1, dtype=torch.float32, device=hs.device)
         y = ops.fused_moe(recv, self.w13, self.w2, ones, recv_eid, 0)    # unused slots (eid -1) -> 0 rows
         back = comm.tp_all_to_all(y, recv_splits, send_splits)            # rows in this rank's send order
-        out_slice = torch.zeros(per, H, dtype=h.dtype, device=h.device)
+        out_slice = torch.zeros(per, H, dtype=hs.dtype, device=hs.device)
         ops.ep_combine(back, slot, w, out_slice)
-        full = comm.tp_all_gather_rows(out_slice)                         # [tp*per, H]
-        return full[:T].contiguous()
+        return out_slice
+
+    def forward_sp(self, x: torch.Tensor, residual: Optional[torch.Tensor], meta: AttnMeta,
+                   kv: Tuple[torch.Tensor, torch.Tensor], cos_sin: torch.Tensor, T: int, per: int):
+        """Sequence-parallel TP + EP layer (MoE layers on the all_to_all exchange): the
+        residual stream stays token-sliced, [per, H] per rank (rank r holds tokens
+        [r * per, r * per + per), zero-padded). The head-parallel attention reads
+        the all-gathered normed input; its row-parallel output is reduce-scattered
+        (half the bytes of the all-reduce) straight into this rank's rows, whose
+        post-attention norm feeds the expert dispatch, and the combined expert output
+        stays sliced. Per layer: all_gather(h) + reduce_scatter(o) + 2 all_to_all,
+        against all_reduce(o) + 2 all_to_all + all_gather(out) in the replicated form
+        (VERDICT r2 #8)."""
+        eps = self.cfg.norm_eps
+        Ts = max(0, min(T, (self.rank + 1) * per) - self.rank * per)
+        if residual is None:
+            residual = x
+            hs = ops.rmsnorm(x, self.input_norm, eps)
+        else:
+            hs, residual = ops.fused_add_rmsnorm(x, residual, self.input_norm, eps)
+        h = comm.tp_all_gather_rows(hs)[:T]
+        a = self.attn(F.linear(h, self.qkv), meta, kv, cos_sin)
+        o = F.linear(a, self.o)
+        if o.shape[0] < self.tp * per:
+            o = torch.cat([o, o.new_zeros(self.tp * per - o.shape[0], o.shape[1])])
+        hs, residual = ops.fused_add_rmsnorm(comm.tp_reduce_scatter_rows(o), residual, self.post_norm, eps)
+        return self._moe_alltoall_rows(hs[:Ts], T, per), residual
 
     def _moe_use_alltoall(self, h: torch.Tensor) -> bool:
         """Exchange choice for a TP > 1 MoE layer. "auto" (default): the activations
@@ -550,12 +583,30 @@ class LlamaForCausalLM(nn.Module):
         x = ops.embed_gather(input_ids, self.embed) if input_ids.dtype == torch.int32 else \
             F.embedding(input_ids, self.embed)
         residual = None
+        l0 = self.layers[0]
+        if self.tp > 1 and l0.moe and l0._moe_use_alltoall(x):
+            return self._forward_sp(x, meta, kv_caches)
         for i, layer in enumerate(self.layers):
             x, residual = layer(x, residual, meta, kv_caches[i], self.cos_sin)
         if residual is None:
             return ops.rmsnorm(x, self.norm, self.cfg.norm_eps)
         h, _ = ops.fused_add_rmsnorm(x, residual, self.norm, self.cfg.norm_eps)
         return h
+
+    def _forward_sp(self, x: torch.Tensor, meta: AttnMeta, kv_caches) -> torch.Tensor:
+        """Every layer in the sequence-parallel form (LlamaLayer.forward_sp): the
+        residual stream stays token-sliced from the embedding to the final norm,
+        whose rows are gathered once for the LM head."""
+        T, H = x.shape
+        per = (T + self.tp - 1) // self.tp
+        lo = min(T, self.rank * per)
+        xs = x.new_zeros(per, H)
+        xs[:min(T, lo + per) - lo] = x[lo:lo + per]
+        residual = None
+        for i, layer in enumerate(self.layers):
+            xs, residual = layer.forward_sp(xs, residual, meta, kv_caches[i], self.cos_sin, T, per)
+        hs, _ = ops.fused_add_rmsnorm(xs, residual, self.norm, self.cfg.norm_eps)
+        return comm.tp_all_gather_rows(hs)[:T]
 
     def compute_logits(self, h: torch.Tensor) -> torch.Tensor:
         w = self.embed if self.lm_head is None else self.lm_head

@@ -120,6 +120,22 @@ def tp_all_gather_rows(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def tp_reduce_scatter_rows(x: torch.Tensor) -> torch.Tensor:
+    """[tp * n, ..] partial sums per rank -> this rank's [n, ..] block of the sum
+    (rank-major rows). gloo builds without reduce_scatter: all-reduce + slice."""
+    s = get_state()
+    if s.tp_size == 1:
+        return x
+    x = x.contiguous()
+    n = x.shape[0] // s.tp_size
+    if s.backend == "gloo":
+        dist.all_reduce(x, group=s.tp_group)
+        return x[s.tp_rank * n:(s.tp_rank + 1) * n]
+    out = torch.empty((n,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.reduce_scatter_tensor(out, x, group=s.tp_group)
+    return out
+
+
 def tp_all_to_all(x: torch.Tensor, send_splits: List[int], recv_splits: List[int]) -> torch.Tensor:
     s = get_state()
     out = torch.empty((sum(recv_splits),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
