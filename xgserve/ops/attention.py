@@ -145,7 +145,11 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
                       query_start_loc: torch.Tensor, seq_lens: torch.Tensor, max_q_len: int, scale: float,
                       out: Optional[torch.Tensor] = None, gh: Optional[int] = None) -> torch.Tensor:
     """q: [T, Hq, D] packed varlen (rows may be strided); causal w.r.t. absolute
-    positions ctx+i where ctx = seq_len - q_len; keys read from the paged cache."""
+    positions ctx+i where ctx = seq_len - q_len; keys read from the paged cache.
+    gh (tests / A/B sweeps; None = the kernel's own choice): > 0 runs the 16-row
+    kernel with gh query heads per workgroup; < 0 forces a D = 128 prefill_attn2_kernel
+    configuration -gh = 1000 (KS - 1) + 100 NSLOT + 10 NW + GH (key phases, ring
+    slots, waves, heads per workgroup; NSLOT 0 = default), e.g. -82 or -1284."""
     if not use_native(q):
         r = prefill_attention_ref(q, k_cache, v_cache, block_tables, query_start_loc, seq_lens, scale)
         if out is not None:
