@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--output-len", type=int, default=256)
     ap.add_argument("--max-batched-tokens", type=int, default=8192)
     ap.add_argument("--block-size", type=int, default=16, help="KV page size in tokens (multiple of 16)")
+    ap.add_argument("--prefill-chunk", type=int, default=0,
+                    help="stall-free batching: prompt tokens per step that also decodes (decode_prefill_cap; "
+                         "mixed steps replay a graph on the gemm_mw path); 0 = whole prompts")
     ap.add_argument("--coalesce", type=int, default=1,
                     help="admission window: hold new prompts until this many wait (1: off)")
     ap.add_argument("--coalesce-max-wait", type=int, default=4, help="admission window bound, in steps")
@@ -144,7 +147,7 @@ def main():
                         max_num_batched_tokens=a.max_batched_tokens, max_model_len=max_len,
                         use_graphs=on_gpu and not a.no_graphs, enable_prefix_cache=not a.no_prefix_cache,
                         moe_comm=a.moe_comm, prompt_coalesce=a.coalesce, block_size=a.block_size,
-                        prompt_coalesce_max_wait=a.coalesce_max_wait,
+                        prompt_coalesce_max_wait=a.coalesce_max_wait, decode_prefill_cap=a.prefill_chunk,
                         weight_dtype=a.weight_dtype, dtype=None if on_gpu else "float32",
                         graph_batch_sizes=[b for b in [1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128]
                                            if b <= max(64, a.concurrency)], seed=st.dp_rank)

@@ -54,10 +54,15 @@ def main():
                     help="every gemm_w8 (fp8 weight) configuration per shape at M <= 16, cold weights")
     ap.add_argument("--m64g-sweep", action="store_true",
                     help="sweep gemm_m64g (nw, split, cfg) configurations instead of the shoot-out")
+    ap.add_argument("--mw-sweep", action="store_true",
+                    help="sweep gemm_mw (split, cfg) configurations at 64 < M <= 320 against hipBLASLt")
+    ap.add_argument("--top", type=int, default=6, help="--mw-sweep: configurations printed per (shape, M)")
     a = ap.parse_args()
     kernels()
     if a.m64g_sweep:
         return m64g_sweep(a)
+    if a.mw_sweep:
+        return mw_sweep(a)
     if a.w8_sweep:
         return w8_sweep(a)
     if a.moe_sweep:
@@ -201,6 +206,65 @@ def m64g_sweep(a):
                 print(json.dumps({"shape": name, "M": M, "op": f"m64g(nw={nw},S={S},cfg={cfg})", "us": round(us, 2),
                                   "TB/s": round(nbytes / us / 1e6, 3), "wgs": N // (16 * nw * waves[cfg]) * S,
                                   "rel_err": round(err, 6)}), flush=True)
+        del ws
+        torch.cuda.empty_cache()
+
+
+def mw_sweep(a):
+    """gemm_mw: every valid (split, cfg) per shape and M (cold weights), checked against
+    fp32; prints hipBLASLt and the fastest a.top configurations. TB/s counts the weight
+    bytes, TF/s the 2 M N K flops."""
+    k = kernels()
+    st = torch.cuda.current_stream().cuda_stream
+    for name in a.shapes:
+        N, K = SHAPES[name]
+        nbytes = N * K * 2
+        copies = max(2, min(8, (1 << 30) // nbytes + 1))
+        ws = [(torch.randn(N, K, device="cuda") * 0.02).bfloat16() for _ in range(copies)]
+        mode = L.MODE_SILU if name.startswith("gate_up") and not name.endswith("_p") else (
+            L.MODE_BF16 if name == "lm_head" else L.MODE_PARTIAL)
+        for M in a.M:
+            x = torch.randn(M, K, device="cuda").bfloat16()
+            if mode == L.MODE_SILU:
+                g, u = L.deinterleave_gate_up(ws[0])
+                want = F.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
+            else:
+                want = x.float() @ ws[0].float().t()
+            flops = 2.0 * M * N * K
+
+            def show(op, us, err, extra=None):
+                print(json.dumps({"shape": name, "M": M, "op": op, "us": round(us, 2),
+                                  "TB/s": round(nbytes / us / 1e6, 3), "TF/s": round(flops / us / 1e6, 1),
+                                  "rel_err": None if err is None else round(err, 6), **(extra or {})}), flush=True)
+            show("hipblaslt", timeit([lambda w=w: F.linear(x, w) for w in ws]), None)
+            rows = []
+            for cfg, (cols, _, _) in L.MW_CFGS.items():
+                if N % cols:
+                    continue
+                splits = (1,) if mode != L.MODE_PARTIAL else tuple(
+                    s for s in (1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 14, 16) if s <= K // 64 and (N // cols) * s <= 640)
+                for S in splits:
+                    part = torch.empty(S, M, N, dtype=torch.float32, device="cuda")
+                    out = torch.empty(M, N // 2 if mode == L.MODE_SILU else N, dtype=torch.bfloat16, device="cuda")
+
+                    def fn(w, S=S, cfg=cfg, part=part, out=out):
+                        k.gemm_mw(x.data_ptr(), M, K, w.data_ptr(), N,
+                                  part.data_ptr() if mode == L.MODE_PARTIAL else 0,
+                                  out.data_ptr() if mode != L.MODE_PARTIAL else 0, S, mode, cfg, st)
+                    try:
+                        fn(ws[0])
+                    except RuntimeError:
+                        continue  # configuration cannot take this M (LDS)
+                    torch.cuda.synchronize()
+                    y = part.sum(0) if mode == L.MODE_PARTIAL else out.float()
+                    err = float((y - want).norm() / want.norm())
+                    us = timeit([lambda w=w, fn=fn: fn(w) for w in ws])
+                    rows.append((us, S, cfg, err, (N // cols) * S))
+            for us, S, cfg, err, wgs in sorted(rows)[:a.top]:
+                show(f"mw(S={S},cfg={cfg})", us, err, {"wgs": wgs})
+            if M <= 64 and L.m64_plan(M, N, K, mode) is not None:
+                fn = lambda w: L.m64_linear(x, w, mode)  # noqa: E731
+                show("m64g(plan)", timeit([lambda w=w: fn(w) for w in ws]), None)
         del ws
         torch.cuda.empty_cache()
 

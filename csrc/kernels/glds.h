@@ -3,8 +3,11 @@
 //     not see it (with the builtin it serialises the DMAs of different slots:
 //     vmcnt(0) between them and before every fragment read), so completion is
 //     tracked ONLY by the explicit counted waits; "memory" keeps the compiler
-//     from moving LDS reads across them. M0 is written in the same statement
-//     that reads it (cdna_hip_programming.md §5.7);
+//     from moving LDS reads across them. The LDS base goes in through a "{m0}"
+//     operand, so the compiler writes M0 itself (no clobbered reserved register,
+//     which hipcc flags as undefined behaviour); the s_nop 0 at the head of the
+//     statement is the M0-write -> LDS-DMA wait state, which the hazard
+//     recognizer does not insert in front of inline asm (cdna_hip_programming.md §5.7);
 //   * counted s_waitcnt vmcnt(N) and a raw s_barrier (never __syncthreads inside
 //     a pipelined loop: its fence drains the DMA queue);
 //   * the write-through (sc1) 16-B store of in-launch hand-offs (Guideline 16 R1).
@@ -21,12 +24,11 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
   const uint32_t lds = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)(lds_base))));
   asm volatile(
-      "s_mov_b32 m0, %1\n\t"
       "s_nop 0\n\t"
       "global_load_lds_dwordx4 %0, off"
       :
-      : "v"(src), "s"(lds)
-      : "memory", "m0");
+      : "v"(src), "{m0}"(lds)
+      : "memory");
 #endif
 }
 
@@ -36,12 +38,11 @@ __device__ __forceinline__ void glds16_nt(const void* src, void* lds_base) {
   const uint32_t lds = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)(lds_base))));
   asm volatile(
-      "s_mov_b32 m0, %1\n\t"
       "s_nop 0\n\t"
       "global_load_lds_dwordx4 %0, off nt"
       :
-      : "v"(src), "s"(lds)
-      : "memory", "m0");
+      : "v"(src), "{m0}"(lds)
+      : "memory");
 #endif
 }
 

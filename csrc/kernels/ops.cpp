@@ -23,6 +23,7 @@ int skinny_slab_kmax(int);
 int gemm_m64g(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 int gemm_m64g_ex(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, const float*,
                  int, int, float, uint16_t*, float*, int*, hipStream_t);
+int gemm_mw(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, hipStream_t);
 void add_partials_resid(const float*, int, int, uint16_t*, float*, int, hipStream_t, uint64_t);
 void row_sumsq(const uint16_t*, int, int, float*, hipStream_t);
 void embed_gather(const int32_t*, int, const uint16_t*, int, int, uint16_t*, float*, hipStream_t);
@@ -237,6 +238,13 @@ PYBIND11_MODULE(_kernels, m) {
     check(xgk::gemm_m64g(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode, nw,
                          cfg, S(st)),
           "gemm_m64g");
+  });
+  // mid-M weight-streaming GEMM (gemm_mw.hip): 64 < M <= 256 mixed / prompt steps
+  m.def("gemm_mw", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
+                      int mode, int cfg, uintptr_t st) {
+    check(xgk::gemm_mw(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode, cfg,
+                       S(st)),
+          "gemm_mw");
   });
   // ---- fused decode layer (gemm_m64g.hip epilogues, decode_attention.hip FQ prologue)
   m.def("gemm_m64g_ex", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,

@@ -1,0 +1,120 @@
+"""Pinned code-generation invariants of the LDS-DMA kernels (CPU: hipcc -S, gfx950).
+
+The weight-streaming GEMMs issue global_load_lds_dwordx4 from inline asm and retire
+them with hand-counted `s_waitcnt vmcnt(N)` (csrc/kernels/glds.h): hipcc's waitcnt
+pass cannot see those loads, so a compiler update that re-schedules or re-waits the
+loop would silently de-pipeline (an extra vmcnt(0)) or break (a count that no longer
+matches the issue order) the kernels. This test compiles them and checks:
+  * no "reserved registers on the clobber list" warning (M0 goes in as a "{m0}"
+    operand, not a clobber);
+  * every vmcnt wait in each instantiation is one the pipeline's issue order allows
+    (gemm_mw: the ring formula of gemm_mw.hip; gemm_m64g: G = x + W instructions per
+    chunk, or 0);
+  * no VGPR / SGPR spills.
+"""
+from __future__ import annotations
+
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KDIR = os.path.join(ROOT, "csrc", "kernels")
+HIPCC = shutil.which("hipcc") or ("/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else None)
+
+pytestmark = pytest.mark.skipif(HIPCC is None, reason="hipcc not available")
+
+
+def _compile(name: str, tmp_path):
+    out = tmp_path / f"{name}.s"
+    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", f"-I{KDIR}", "-S", "--cuda-device-only",
+                        os.path.join(KDIR, f"{name}.hip"), "-o", str(out)],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-4000:]
+    return out.read_text(), r.stdout
+
+
+def _kernels(asm: str, prefix: str):
+    """{template args string: body} for every kernel symbol starting with prefix."""
+    parts = re.split(r"\n(_ZN3xgk\w+):[^\n]*\n", asm)
+    out = {}
+    for i in range(1, len(parts), 2):
+        name, body = parts[i], parts[i + 1].split(".Lfunc_end")[0]
+        if name.startswith(prefix):
+            out[name] = body
+    return out
+
+
+def _targs(name: str):
+    """Template arguments of a mangled xgk kernel: Li<int>E / Lb<0|1>E in order."""
+    inner = name[name.index("I") + 1:]
+    return [int(v) for v in re.findall(r"L[ib](\d+)E", inner)]
+
+
+def _vmcnts(body: str):
+    return {int(v) for v in re.findall(r"s_waitcnt[^\n]*vmcnt\((\d+)\)", body)}
+
+
+def _pipeline(body: str, through_barrier: bool = False) -> str:
+    """The weight-streaming span: first LDS-DMA issue .. last MFMA (the prologue's
+    statistics loads and the epilogue's hand-offs carry compiler-counted waits of
+    their own, outside this span); through_barrier: .. the later of the last MFMA
+    and the last s_barrier (a rotated loop keeps its wait + barrier below the MFMAs)."""
+    a = body.index("global_load_lds_dwordx4")
+    b = body.rindex("v_mfma")
+    if through_barrier and "s_barrier" in body:
+        b = max(b, body.rindex("s_barrier"))
+    return body[a:b]
+
+
+def _no_spills(asm: str):
+    v = [int(x) for x in re.findall(r"\.vgpr_spill_count:\s*(\d+)", asm)]
+    s = [int(x) for x in re.findall(r"\.sgpr_spill_count:\s*(\d+)", asm)]
+    assert v and s, "no spill metadata in the assembly"
+    assert max(v) == 0 and max(s) == 0, (max(v), max(s))
+
+
+def test_gemm_mw_waits_follow_the_ring(tmp_path):
+    asm, log = _compile("gemm_mw", tmp_path)
+    assert "reserved registers on the clobber list" not in log
+    ks = _kernels(asm, "_ZN3xgk14gemm_mw_kernel")
+    assert len(ks) >= 20, len(ks)
+    for name, body in ks.items():
+        WN, NWT, MTW, D, _nt = _targs(name)
+        WI = WN * 16 * NWT // 64
+        XI = (8 // WN) * 16 * MTW // 64
+        allowed = {0, WI + (XI if D >= 3 else 0)}
+        if D >= 3:
+            allowed.add(2 * WI + min(D - 2, 2) * XI)
+        if D >= 4:
+            allowed.add(3 * WI + 2 * XI)
+        got = _vmcnts(_pipeline(body, through_barrier=True))
+        assert got <= allowed, (name, sorted(got), sorted(allowed))
+        assert WI + (XI if D >= 3 else 0) in got, (name, sorted(got))  # the steady-state counted wait exists
+        n_glds = len(re.findall(r"global_load_lds_dwordx4", body))
+        assert n_glds >= WI + XI, name
+        assert len(re.findall(r"v_mfma_f32_16x16x32_bf16", body)) >= 2 * NWT * MTW, name
+    _no_spills(asm)
+
+
+def test_gemm_m64g_waits_are_counted(tmp_path):
+    asm, log = _compile("gemm_m64g", tmp_path)
+    assert "reserved registers on the clobber list" not in log
+    ks = _kernels(asm, "_ZN3xgk16gemm_m64g_kernel")
+    assert len(ks) >= 8, len(ks)
+    for name, body in ks.items():
+        NW, WV, KC, _nt, MT = _targs(name)
+        RPI = 1024 // (KC * 2)
+        G = 16 * MT // RPI // WV + 16 * NW // RPI
+        got = _vmcnts(_pipeline(body))
+        assert got <= {0, G}, (name, sorted(got), G)
+        assert G in got, (name, sorted(got))
+    _no_spills(asm)
+
+
+def test_prefill_attention_has_no_clobber_warning(tmp_path):
+    _, log = _compile("prefill_attention", tmp_path)
+    assert "reserved registers on the clobber list" not in log

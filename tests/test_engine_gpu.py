@@ -215,3 +215,54 @@ def test_async_schedule_staggered_tokens_are_reference_argmax(llama_small):
             row = ref[len(p) - 1 + i]
             assert float(row.max() - row[tok]) < 0.15, (rid, i)
     assert eng.sched.num_inflight() == 0 and eng.sched.num_running() == 0
+
+
+def _run_stall_free(model, chunk, temperature=0.0):
+    """16 rows decoding while prompts arrive: with decode_prefill_cap = chunk every
+    prompt is prefilled in chunk-sized pieces that ride on the decode steps."""
+    eng = _engine(model, decode_prefill_cap=chunk, graph_batch_sizes=[1, 2, 4, 8, 16, 24, 32],
+                  max_num_seqs=32)
+    prompts, outs = {}, {}
+    for i in range(16):
+        p = [128000] + list(range(900 + 3 * i, 940 + 3 * i))
+        prompts[f"d{i}"] = p
+        eng.add_request(f"d{i}", p, SamplingParams(max_tokens=24, temperature=temperature, ignore_eos=True,
+                                                  seed=5 + i))
+    n = 0
+    while eng.has_work():
+        for o in eng.step():
+            outs.setdefault(o.request_id, []).extend(o.new_token_ids)
+        n += 1
+        if n in (3, 6):  # long prompts arriving while the rows decode
+            for j in range(2):
+                rid = f"p{n}-{j}"
+                p = [128000] + list(range(2000 + 50 * n + 7 * j, 2000 + 50 * n + 7 * j + 300 + 37 * j))
+                prompts[rid] = p
+                eng.add_request(rid, p, SamplingParams(max_tokens=6, temperature=temperature, ignore_eos=True,
+                                                      seed=50 + n + j))
+    return prompts, outs, eng
+
+
+def test_stall_free_mixed_graphs_match_reference(llama_small):
+    """Mixed steps (decode rows + one <= 128-token prompt chunk) replay the captured
+    mixed graphs on the gemm_mw path; every greedy token is the fp32 reference's
+    argmax up to a bf16 near-tie, with exact lengths."""
+    prompts, outs, eng = _run_stall_free(llama_small, 128)
+    assert eng.runner.mixed_graphs, "no mixed graphs captured"
+    assert eng.runner.mixed_replays >= 6, eng.runner.mixed_replays
+    for rid, gen in outs.items():
+        assert len(gen) == (24 if rid.startswith("d") else 6), rid
+        p = prompts[rid]
+        ref = reference_logits(llama_small, p + gen[:-1]).float()
+        for i, tok in enumerate(gen):
+            row = ref[len(p) - 1 + i]
+            assert float(row.max() - row[tok]) < 0.15, (rid, i)
+    assert eng.sched.num_inflight() == 0 and eng.sched.num_running() == 0
+
+
+def test_stall_free_sampling_seeded(llama_small):
+    """Seeded sampling through the mixed graphs is reproducible run to run."""
+    _, a, _ = _run_stall_free(llama_small, 128, temperature=0.8)
+    _, b, eng = _run_stall_free(llama_small, 128, temperature=0.8)
+    assert a == b
+    assert eng.runner.mixed_replays >= 6

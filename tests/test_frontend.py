@@ -130,7 +130,7 @@ def test_queue_full_is_503_with_retry_after(server):
                 async with s.post(server + "/generate", json={"prompt": "q", "max_tokens": 400,
                                                               "ignore_eos": True}) as r:
                     return r.status, dict(r.headers)
-            tasks = [asyncio.create_task(post()) for _ in range(120)]
+            tasks = [asyncio.create_task(post()) for _ in range(240)]
             res = await asyncio.gather(*tasks)
         return res
 

@@ -152,3 +152,75 @@ def test_gemm_m64_rejects_bad_shapes():
         m64_linear(rnd(8, 256), rnd(256, 256), MODE_PARTIAL)   # M <= 16: not this kernel
     with pytest.raises(ValueError):
         m64_linear(rnd(32, 200), rnd(256, 200), MODE_PARTIAL)  # K % 256
+
+
+# ---------------------------------------------------------------- gemm_mw (64 < M <= 320)
+@pytest.mark.parametrize("M", [65, 100, 128, 192, 257, 320])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+def test_gemm_mw_partial_every_cfg(M, cfg):
+    """Every ring depth / tile width, incl. uneven split-K chunk ranges (K / 64 = 22
+    chunks over S = 3 and 5) and short splits (1-2 chunks per split)."""
+    from xgserve.ops.linear import MW_CFGS, mw_linear
+    cols = MW_CFGS[cfg][0]
+    N, K = 2 * cols, 1408
+    x, w = rnd(M, K), rnd(N, K, scale=0.02)
+    ref = x.float() @ w.float().t()
+    for S in (1, 3, 5, 16):
+        try:
+            pend = mw_linear(x, w, MODE_PARTIAL, plan=(S, cfg))
+        except RuntimeError:
+            assert M > 256 and cfg != 2, (M, cfg)  # 320-row x tiles fit the LDS on cfg 2 only
+            return
+        assert pend.part.shape == (S, M, N)
+        assert rel_err(pend.part.sum(0), ref) < 1e-5, (S,)
+
+
+@pytest.mark.parametrize("M", [65, 128, 192, 256, 320])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 4096), (4096, 14336)])
+def test_gemm_mw_llama_shapes(M, N, K):
+    from xgserve.ops.linear import mw_linear
+    x, w = rnd(M, K), rnd(N, K, scale=0.02)
+    pend = mw_linear(x, w, MODE_PARTIAL)
+    ref = x.float() @ w.float().t()
+    assert rel_err(pend.part.sum(0), ref) < 1e-5
+    assert rel_err(pend.materialize(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("M", [65, 192, 256, 320])
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+def test_gemm_mw_silu_and_bf16(M, cfg):
+    from xgserve.ops.linear import MW_CFGS, mw_linear
+    if M > 256 and cfg != 2:
+        pytest.skip("320-row x tiles fit the LDS on cfg 2 only")
+    F_, H = 2 * MW_CFGS[cfg][0], 1024
+    x = rnd(M, H)
+    g, u = rnd(F_, H, scale=0.05), rnd(F_, H, scale=0.05)
+    w = interleave_gate_up(g, u).contiguous()
+    got = mw_linear(x, w, MODE_SILU, plan=(1, cfg))
+    ref = torch.nn.functional.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
+    assert got.shape == (M, F_)
+    assert rel_err(got, ref) < 1e-2
+    w2 = rnd(2 * MW_CFGS[cfg][0], H, scale=0.02)
+    got2 = mw_linear(x, w2, MODE_BF16, plan=(1, cfg))
+    assert rel_err(got2, x.float() @ w2.float().t()) < 1e-2
+
+
+def test_gemm_mw_gate_up_8b():
+    from xgserve.ops.linear import mw_linear
+    M, F_, H = 191, 14336, 4096
+    x = rnd(M, H)
+    g, u = rnd(F_, H, scale=0.02), rnd(F_, H, scale=0.02)
+    w = interleave_gate_up(g, u).contiguous()
+    got = mw_linear(x, w, MODE_SILU)
+    ref = torch.nn.functional.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
+    assert rel_err(got, ref) < 1e-2
+
+
+def test_gemm_mw_rejects_bad_shapes():
+    from xgserve.ops.linear import mw_linear
+    with pytest.raises(ValueError):
+        mw_linear(rnd(321, 256), rnd(256, 256), MODE_PARTIAL)   # M > 320
+    with pytest.raises(ValueError):
+        mw_linear(rnd(100, 200), rnd(256, 200), MODE_PARTIAL)   # K % 64
+    with pytest.raises(RuntimeError):
+        mw_linear(rnd(100, 256), rnd(256, 256), MODE_SILU, plan=(2, 1))  # SiLU needs split 1

@@ -169,7 +169,8 @@ class LLMEngine:
         self.runner = ModelRunner(self.model, block_size=cfg.block_size, num_blocks=num_blocks,
                                   max_num_seqs=cfg.max_num_seqs, max_num_batched_tokens=cfg.max_num_batched_tokens,
                                   max_model_len=self.max_model_len, use_graphs=use_graphs,
-                                  graph_batch_sizes=graph_bs, is_driver=self.is_driver)
+                                  graph_batch_sizes=graph_bs, is_driver=self.is_driver,
+                                  mixed_chunk=cfg.decode_prefill_cap)
         self.runner.collective_timeout_s = cfg.collective_timeout_s
         self.runner.capture_graphs()
         H = self.mcfg.hidden_size

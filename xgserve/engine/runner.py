@@ -9,6 +9,13 @@
   graph covers embedding -> all layers -> LM head -> sampling, so a decode step
   is one graph launch + one small H2D + one D2H. Padding rows use slot -1
   (no KV write) and seq_len 0 (no attention work).
+* Mixed steps of the stall-free schedule -- the decode rows plus ONE prompt
+  chunk of at most `mixed_chunk` tokens (the scheduler's decode_prefill_cap) --
+  replay a graph too, captured per (padded decode rows, chunk): the eager
+  forward of such a step costs more host time than its ~5 ms of GPU work. The
+  chunk's rows are padded to the chunk size (slot -1, outside every sequence);
+  its last row's logits follow the decode rows', so the sampled tokens come out
+  in the plan's sample order.
 """
 from __future__ import annotations
 
@@ -59,7 +66,8 @@ def _pinned(n: int, dtype) -> torch.Tensor:
 class ModelRunner:
     def __init__(self, model, *, block_size: int, num_blocks: int, max_num_seqs: int,
                  max_num_batched_tokens: int, max_model_len: int, use_graphs: bool = True,
-                 graph_batch_sizes: Optional[List[int]] = None, is_driver: bool = True):
+                 graph_batch_sizes: Optional[List[int]] = None, is_driver: bool = True,
+                 mixed_chunk: int = 0):
         self.model = model
         self.cfg = model.cfg
         self.device = model.device
@@ -104,6 +112,18 @@ class ModelRunner:
             graph_batch_sizes = [1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 256]
         self.graph_bs = sorted(b for b in graph_batch_sizes if b <= max_num_seqs)
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        # mixed-step graphs: (decode bucket, chunk) -> graph; buckets of >= 16 decode rows
+        # whose step stays on the gemm_mw path (decode rows + chunk <= MW_MAX_TOKENS)
+        self.mixed_chunk = int(mixed_chunk) if (self.use_graphs and comm.get_state().tp_size == 1) else 0
+        self.mixed_graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+        self.mixed_bs: List[int] = []
+        self.mixed_replays = 0
+        if self.mixed_chunk > 0:
+            from ..models.llama import MW_MAX_TOKENS
+            lim = MW_MAX_TOKENS if getattr(model, "_mw_ok", False) else 0
+            self.mixed_bs = [b for b in self.graph_bs if b >= 16 and b + self.mixed_chunk <= lim]
+            if not self.mixed_bs:
+                self.mixed_chunk = 0
         self._graph_pool = None
         self._init_graph_buffers()
         # custom all-reduce peer-wait limit while serving (EngineConfig.collective_timeout_s);
@@ -144,25 +164,43 @@ class ModelRunner:
         self.g_sl = self.g_int[3 * B:4 * B]
         self.g_src = self.g_int[4 * B:5 * B]
         self.g_bt = self.g_int[5 * B:5 * B + B * W].view(B, W)
-        self.g_temp = torch.zeros(B, dtype=torch.float32, device=self.device)
-        self.g_topp = torch.ones(B, dtype=torch.float32, device=self.device)
-        self.g_topk = torch.zeros(B, dtype=torch.int32, device=self.device)
-        self.g_seed = torch.zeros(B, dtype=torch.int64, device=self.device)
+        # sampling parameters: one row more than the widest decode graph (mixed steps)
+        self.g_temp = torch.zeros(B + 1, dtype=torch.float32, device=self.device)
+        self.g_topp = torch.ones(B + 1, dtype=torch.float32, device=self.device)
+        self.g_topk = torch.zeros(B + 1, dtype=torch.int32, device=self.device)
+        self.g_seed = torch.zeros(B + 1, dtype=torch.int64, device=self.device)
         # two sets of pinned host inputs (event-guarded): the next step's inputs can be
         # written while this step's H2D copies are still queued behind the GPU
         self.h_ints = [_pinned(n, torch.int32) for _ in range(2)]
-        self.h_samp_fs = [_pinned(2 * B, torch.float32) for _ in range(2)]
-        self.h_samp_is = [_pinned(B, torch.int32) for _ in range(2)]
-        self.h_samp_ss = [_pinned(B, torch.int64) for _ in range(2)]
+        self.h_samp_fs = [_pinned(2 * (B + 1), torch.float32) for _ in range(2)]
+        self.h_samp_is = [_pinned(B + 1, torch.int32) for _ in range(2)]
+        self.h_samp_ss = [_pinned(B + 1, torch.int64) for _ in range(2)]
         self.g_stage_events = [None, None]
         self.g_stage_idx = 0
-        # sampled tokens [0, B) and their logprobs [B, 2B) in one buffer: a graph step's
-        # outputs leave in ONE D2H copy (g_out[:B + n]) instead of two
-        self.g_out = torch.zeros(2 * B, dtype=torch.int32, device=self.device)
-        self.g_out_tok = self.g_out[:B]
-        self.g_out_lp = self.g_out[B:].view(torch.float32)
-        self.h_gout = [_pinned(2 * B, torch.int32) for _ in range(2)]
+        # sampled tokens [0, OB) and their logprobs [OB, 2 OB) in one buffer: a graph step's
+        # outputs leave in ONE D2H copy (g_out[:OB + n]) instead of two; OB = B + 1 (a
+        # mixed step samples its decode rows + the chunk's last row)
+        OB = self.g_OB = B + 1
+        self.g_out = torch.zeros(2 * OB, dtype=torch.int32, device=self.device)
+        self.g_out_tok = self.g_out[:OB]
+        self.g_out_lp = self.g_out[OB:].view(torch.float32)
+        self.h_gout = [_pinned(2 * OB, torch.int32) for _ in range(2)]
         self.g_greedy_graph: Dict[int, bool] = {}
+        # mixed-step inputs: ids | pos | slot (B + C rows each) | sl (B + 1) | src (B) |
+        # qsl (2) | bt ((B + 1) x W) ; lidx (int64, B + 1)
+        C = self.mixed_chunk
+        if C > 0:
+            R = B + C
+            self.m_sec = (0, R, 2 * R, 3 * R, 3 * R + B + 1, 3 * R + 2 * B + 1, 3 * R + 2 * B + 3)
+            n_m = self.m_sec[-1] + (B + 1) * W
+            self.m_int = torch.zeros(n_m, dtype=torch.int32, device=self.device)
+            o = self.m_sec
+            self.m_ids, self.m_pos, self.m_slot = self.m_int[o[0]:o[1]], self.m_int[o[1]:o[2]], self.m_int[o[2]:o[3]]
+            self.m_sl, self.m_src, self.m_qsl = self.m_int[o[3]:o[4]], self.m_int[o[4]:o[5]], self.m_int[o[5]:o[6]]
+            self.m_bt = self.m_int[o[6]:].view(B + 1, W)
+            self.m_lidx = torch.zeros(B + 1, dtype=torch.int64, device=self.device)
+            self.h_mints = [_pinned(n_m, torch.int32) for _ in range(2)]
+            self.h_mlidx = [_pinned(B + 1, torch.int64) for _ in range(2)]
 
     def _decode_body(self, bs: int, greedy: bool):
         ops.subst_tokens(self.g_ids[:bs], self.g_src[:bs], self.g_out_tok)
@@ -178,6 +216,36 @@ class ModelRunner:
                                         self.g_seed[:bs], step=0)
             self.g_out_tok[:bs].copy_(tok)
             self.g_out_lp[:bs].copy_(lp)
+
+    def _mixed_body(self, nb: int, greedy: bool):
+        """nb decode rows (padded) + one prompt chunk of up to C rows (padded) -> the
+        sampled tokens of the decode rows and the chunk's last row (g_out_tok[:nb + 1])."""
+        B, C = self.g_B, self.mixed_chunk
+        T = nb + C
+        ops.subst_tokens(self.m_ids[:nb], self.m_src[:nb], self.g_out_tok)
+        ids, pos, slot = self.m_ids[:B + C], self.m_pos[:B + C], self.m_slot[:B + C]
+        # decode rows [0, nb) and the chunk [B, B + C) of the B + C row buffers, as one
+        # contiguous [nb + C] view when nb == B, else gathered into place
+        if nb == B:
+            ids_t, pos_t, slot_t = ids, pos, slot
+        else:
+            ids_t = torch.cat([ids[:nb], ids[B:]])
+            pos_t = torch.cat([pos[:nb], pos[B:]])
+            slot_t = torch.cat([slot[:nb], slot[B:]])
+        meta = AttnMeta(num_tokens=T, num_decodes=nb, positions=pos_t, slot_mapping=slot_t,
+                        dec_block_tables=self.m_bt[:nb], dec_seq_lens=self.m_sl[:nb],
+                        num_splits=self.decode_splits(nb), workspace=self.workspace,
+                        pre_block_tables=self.m_bt[B:B + 1], pre_qsl=self.m_qsl, pre_seq_lens=self.m_sl[B:B + 1],
+                        pre_max_q=C)
+        h = self.model(ids_t, meta, self.kv_caches)
+        logits = self.model.compute_logits(h.index_select(0, self.m_lidx[:nb + 1]))
+        if greedy:
+            ops.argmax_logprob(logits, self.g_out_tok[:nb + 1], self.g_out_lp[:nb + 1])
+        else:
+            tok, lp = ops.sample_tokens(logits, self.g_temp[:nb + 1], self.g_topp[:nb + 1], self.g_topk[:nb + 1],
+                                        self.g_seed[:nb + 1], step=0)
+            self.g_out_tok[:nb + 1].copy_(tok)
+            self.g_out_lp[:nb + 1].copy_(lp)
 
     # the first launches run under the generous peer-wait limit too (first-call RCCL
     # communicator setup of a subgroup, first-seen library GEMM shapes)
@@ -218,6 +286,45 @@ class ModelRunner:
                 self.graphs[(bs, greedy)] = g
         torch.cuda.synchronize()
         log.info("captured %d decode graphs (batch sizes %s)", len(self.graphs), self.graph_bs)
+        if self.mixed_chunk > 0:
+            self._capture_mixed()
+
+    def _capture_mixed(self):
+        # neutral inputs: padding decode rows, an empty chunk (q = 0: no attention rows)
+        self.m_int.zero_()
+        self.m_slot.fill_(-1)
+        self.m_src.fill_(-1)
+        self.m_lidx.zero_()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for nb in reversed(self.mixed_bs):
+                for greedy in (True, False):
+                    for _ in range(2):
+                        self._mixed_body(nb, greedy)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        for nb in reversed(self.mixed_bs):
+            for greedy in (True, False):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self._graph_pool):
+                    self._mixed_body(nb, greedy)
+                self.mixed_graphs[(nb, greedy)] = g
+        torch.cuda.synchronize()
+        log.info("captured %d mixed-step graphs (decode rows %s + a %d-token chunk)", len(self.mixed_graphs),
+                 self.mixed_bs, self.mixed_chunk)
+
+    def _mixed_bucket(self, plan, Nd: int, ns: int, T: int) -> Optional[int]:
+        """Decode bucket of a mixed-graph step, or None: Nd decode rows + exactly one
+        prefill chunk of <= mixed_chunk tokens (no verify rows, no embeddings)."""
+        if not self.mixed_graphs or ns != Nd + 1 or T - Nd > self.mixed_chunk or T - Nd < 1:
+            return None
+        if not plan["is_prefill"][Nd] or plan["is_embed"][Nd]:
+            return None
+        for b in self.mixed_bs:
+            if b >= Nd:
+                return b
+        return None
 
     def _graph_bucket(self, n: int) -> Optional[int]:
         for b in self.graph_bs:
@@ -253,6 +360,10 @@ class ModelRunner:
         bucket = self._graph_bucket(Nd) if (Nd == ns and T == Nd and not need_hidden) else None
         if bucket is not None and self.graphs:
             return self._execute_graph(plan, samp, Nd, bucket, src)
+        if not need_hidden and self.mixed_chunk > 0:
+            mb = self._mixed_bucket(plan, Nd, ns, T)
+            if mb is not None:
+                return self._execute_mixed(plan, samp, Nd, mb, src)
         return self._execute_eager(plan, samp, need_hidden, src)
 
     def launched_as_graph(self, handle) -> bool:
@@ -318,9 +429,9 @@ class ModelRunner:
         self._wait_event(ev)  # this step only: a step queued behind it keeps running
         self._check_comm()
         if len(out) > 2:  # graph step: tokens and logprobs in one pinned buffer
-            B = out[2]
+            OB = out[2]
             h = self.h_gout[i]
-            return h[:n].numpy().copy(), h[B:B + n].view(torch.float32).numpy().copy(), hidden
+            return h[:n].numpy().copy(), h[OB:OB + n].view(torch.float32).numpy().copy(), hidden
         return self.h_toks[i][:n].numpy().copy(), self.h_lps[i][:n].numpy().copy(), hidden
 
     def _execute_graph(self, plan, samp: Optional[SamplingRows], n: int, bs: int, src: Optional[np.ndarray]):
@@ -349,16 +460,7 @@ class ModelRunner:
         self.g_int[:5 * B + bs * W].copy_(h_int[:5 * B + bs * W], non_blocking=True)
         greedy = samp is None or samp.all_greedy
         if not greedy:
-            hf, hsi, hss = self.h_samp_fs[si], self.h_samp_is[si], self.h_samp_ss[si]
-            f = hf.numpy()
-            f[:n] = samp.temps
-            f[B:B + n] = samp.top_ps
-            hsi.numpy()[:n] = samp.top_ks
-            hss.numpy()[:n] = samp.seeds
-            self.g_temp[:n].copy_(hf[:n], non_blocking=True)
-            self.g_topp[:n].copy_(hf[B:B + n], non_blocking=True)
-            self.g_topk[:n].copy_(hsi[:n], non_blocking=True)
-            self.g_seed[:n].copy_(hss[:n], non_blocking=True)
+            self._stage_sampling(si, samp, n)
         ev = self.g_stage_events[si] or torch.cuda.Event()
         ev.record()
         self.g_stage_events[si] = ev
@@ -369,13 +471,87 @@ class ModelRunner:
             ev = torch.cuda.Event()
             ev.record()
             return (n, None, None, None, True, ev)
+        return self._graph_out(n)
+
+    def _stage_sampling(self, si: int, samp: SamplingRows, n: int) -> None:
+        """Per-row sampling parameters of a graph step -> g_temp / g_topp / g_topk / g_seed."""
+        hf, hsi, hss = self.h_samp_fs[si], self.h_samp_is[si], self.h_samp_ss[si]
+        OB = self.g_OB
+        f = hf.numpy()
+        f[:n] = samp.temps
+        f[OB:OB + n] = samp.top_ps
+        hsi.numpy()[:n] = samp.top_ks
+        hss.numpy()[:n] = samp.seeds
+        self.g_temp[:n].copy_(hf[:n], non_blocking=True)
+        self.g_topp[:n].copy_(hf[OB:OB + n], non_blocking=True)
+        self.g_topk[:n].copy_(hsi[:n], non_blocking=True)
+        self.g_seed[:n].copy_(hss[:n], non_blocking=True)
+
+    def _graph_out(self, n: int):
+        """Queue a graph step's D2H of its n sampled tokens + logprobs (g_out)."""
+        OB = self.g_OB
         self._poll_comm()
         i = self.out_idx
         self.out_idx ^= 1
-        self.h_gout[i][:B + n].copy_(self.g_out[:B + n], non_blocking=True)
+        self.h_gout[i][:OB + n].copy_(self.g_out[:OB + n], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        return (n, None, None, (i, ev, B), True)
+        return (n, None, None, (i, ev, OB), True)
+
+    def _execute_mixed(self, plan, samp: Optional[SamplingRows], Nd: int, nb: int, src: Optional[np.ndarray]):
+        """Replay the (nb, chunk) mixed graph: Nd decode rows at [0, Nd), the prompt
+        chunk's q rows at [B, B + q) of the static input buffers."""
+        B, W, C = self.g_B, self.g_W, self.mixed_chunk
+        T = int(plan["num_tokens"])
+        q = T - Nd
+        n = int(plan["num_sample"])
+        si = self.g_stage_idx
+        self.g_stage_idx ^= 1
+        if self.g_stage_events[si] is not None:
+            self.g_stage_events[si].synchronize()
+        hi = self.h_mints[si].numpy()
+        hl = self.h_mlidx[si].numpy()
+        o = self.m_sec
+        ids, pos, slots = plan["input_ids"], plan["positions"], plan["slot_mapping"]
+        for k, arr, pad in ((0, ids, 0), (1, pos, 0), (2, slots, -1)):
+            base = o[k]
+            hi[base:base + Nd] = arr[:Nd]
+            hi[base + Nd:base + nb] = pad
+            hi[base + B:base + B + q] = arr[Nd:T]
+            hi[base + B + q:base + B + C] = pad
+        sl = plan["seq_lens"]
+        hi[o[3]:o[3] + Nd] = sl[:Nd]
+        hi[o[3] + Nd:o[3] + nb] = 0
+        hi[o[3] + B] = sl[Nd]
+        hi[o[4]:o[4] + nb] = -1
+        if src is not None:
+            hi[o[4]:o[4] + src.shape[0]] = src
+        hi[o[5]] = 0
+        hi[o[5] + 1] = q
+        w = int(plan["bt_width"])
+        bt = hi[o[6]:o[6] + (B + 1) * W].reshape(B + 1, W)
+        pbt = plan["block_tables"].reshape(Nd + 1, w)
+        bt[:Nd, :w] = pbt[:Nd]
+        bt[B, :w] = pbt[Nd]
+        hl[:Nd] = np.arange(Nd)
+        hl[Nd] = nb + q - 1
+        hl[Nd + 1:nb + 1] = 0
+        self.m_int.copy_(self.h_mints[si], non_blocking=True)
+        self.m_lidx[:nb + 1].copy_(self.h_mlidx[si][:nb + 1], non_blocking=True)
+        greedy = samp is None or samp.all_greedy
+        if not greedy:
+            self._stage_sampling(si, samp, n)
+        ev = self.g_stage_events[si] or torch.cuda.Event()
+        ev.record()
+        self.g_stage_events[si] = ev
+        self.mixed_graphs[(nb, greedy)].replay()
+        self.mixed_replays += 1
+        if not self.is_driver:
+            self._poll_comm()
+            ev = torch.cuda.Event()
+            ev.record()
+            return (n, None, None, None, True, ev)
+        return self._graph_out(n)
 
     def _execute_eager(self, plan, samp: Optional[SamplingRows], need_hidden: bool, src: Optional[np.ndarray]):
         T = int(plan["num_tokens"])

@@ -34,9 +34,9 @@ from .. import ops
 from ..parallel import comm
 from ..parallel.state import get_state
 from ..ops import linear as linear_mod
-from ..ops.linear import (MODE_PARTIAL, MODE_SILU, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace, RowStats, m64_linear,
-                          m64_norm_linear, m64_plan, m64_resid_linear, pick_split, quantize_fp8, skinny_linear,
-                          splitk_linear, splitk_prefill_ok, w8_linear, w8_plan)
+from ..ops.linear import (MODE_PARTIAL, MODE_SILU, MW_MAX_M, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace, RowStats,
+                          m64_linear, m64_norm_linear, m64_plan, m64_resid_linear, mw_linear, mw_plan, pick_split,
+                          quantize_fp8, skinny_linear, splitk_linear, splitk_prefill_ok, w8_linear, w8_plan)
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
 from .config import ModelConfig
 
@@ -57,6 +57,11 @@ FUSED_DECODE = os.environ.get("XGS_FUSED_DECODE", "1") != "0"
 # batch-1 decode steps of dense TP=1 models on the persistent all-layer kernel
 # (csrc/kernels/decode_b1.hip); 0 keeps the per-layer fused launches
 PERSISTENT_DECODE = os.environ.get("XGS_PERSISTENT_DECODE", "0") == "1"
+# 64 < T <= this many tokens (the mixed step: decode rows + one bounded prefill chunk)
+# run every projection on gemm_mw (csrc/kernels/gemm_mw.hip): weight-stream-bound
+# MFMA GEMMs whose split-K partials go to the consumers, SiLU-gate in gate_up.
+# 0 = hipBLASLt for every step above 64 tokens.
+MW_MAX_TOKENS = min(MW_MAX_M, int(os.environ.get("XGS_MW_MAX_TOKENS", str(MW_MAX_M))))
 # TP > 1 prefill-sized steps: the row-parallel all-reduces are pipelined over this
 # many token chunks and overlapped with the next chunk's GEMMs (RCCL stream); a
 # 2k-token 8B step moves 16 MiB per all-reduce -- ~100 us on 7 xGMI links, a
@@ -136,6 +141,12 @@ class LlamaLayer(nn.Module):
             for n, k in ((Nqkv, H), (H, Hq * D)) + (() if self.moe else ((H, cfg.intermediate_size // tp),)))
         self.m64_silu_ok = self.m64_ok and not self.moe and m64_plan(64, 2 * (cfg.intermediate_size // tp), H,
                                                                      MODE_SILU) is not None
+        # 64 < M <= MW_MAX_TOKENS: gemm_mw for every projection (dense layers)
+        self.mw_ok = self.fast_ok and not self.moe and MW_MAX_TOKENS > FAST_M_SLAB and all(
+            mw_plan(MW_MAX_TOKENS, n, k, mode) is not None and mw_plan(FAST_M_SLAB + 1, n, k, mode) is not None
+            for n, k, mode in ((Nqkv, H, MODE_PARTIAL), (H, Hq * D, MODE_PARTIAL),
+                               (2 * (cfg.intermediate_size // tp), H, MODE_SILU),
+                               (H, cfg.intermediate_size // tp, MODE_PARTIAL)))
         # M <= 16 too, when every projection has a measured small-M plan
         self.w8 = None  # FP8 weight copies for batch <= 16 decode (LlamaForCausalLM.quantize_fp8)
         self.m64_small_ok = self.m64_ok and all(
@@ -327,6 +338,19 @@ class LlamaLayer(nn.Module):
                 act = ops.silu_and_mul(F.linear(h, self.gate_up), interleave16=True)
             d = m64_linear(act, self.down, MODE_PARTIAL)
             return (d if self.tp == 1 else self._ar(d.materialize())), residual
+        if self.mw_ok and T <= MW_MAX_TOKENS:
+            # 64 < M <= 320 (decode rows + a prefill chunk): gemm_mw streams each weight
+            # once with the MFMA work under the stream; split-K partials go to the
+            # consumers (rope_cache_partials / add + rmsnorm), SiLU-gate in gate_up
+            pqkv = mw_linear(h, self.qkv, MODE_PARTIAL)
+            a = self.attn.from_partials(pqkv, meta, kv, cos_sin)
+            o = mw_linear(a, self.o, MODE_PARTIAL)
+            if self.tp > 1:
+                o = self._ar(o.materialize())
+            h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
+            act = mw_linear(h, self.gate_up, MODE_SILU)
+            d = mw_linear(act, self.down, MODE_PARTIAL)
+            return (d if self.tp == 1 else self._ar(d.materialize())), residual
         if self.fast_ok and T <= FAST_M_SLAB:
             # 16 < M <= 64: measured per shape on MI355X -- only the O projection
             # (N = H) is faster on the LDS-slab kernel; its split-K partials are
@@ -458,6 +482,8 @@ class LlamaForCausalLM(nn.Module):
                           and cfg.head_dim == 128 and l0.Hq % l0.Hkv == 0
                           and l0.Hq // l0.Hkv in (1, 2, 4, 8) and H % 1024 == 0 and H // 1024 <= 8)
         self._fused_small_ok = self._fused_ok and l0.m64_small_ok
+        # every layer on gemm_mw for 64 < T <= MW_MAX_TOKENS (the runner's mixed-step graphs)
+        self._mw_ok = self.device.type == "cuda" and all(l.mw_ok for l in self.layers)
         self._fused_ws = ResidWorkspace(2 * cfg.num_layers + 1, FAST_M_SLAB, H, device) if self._fused_ok else None
         self._b1 = None        # persistent batch-1 decoder (built on first use)
         self._b1_failed = False

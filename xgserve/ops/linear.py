@@ -217,6 +217,75 @@ def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split
     return out
 
 
+# ---------------------------------------------------------------------------- gemm_mw (64 < M <= 256)
+# csrc/kernels/gemm_mw.hip: one 8-wave workgroup per CU owns a 128- or 256-column
+# weight tile and every x row (x bytes per weight byte = M / columns), W and x both
+# by LDS-DMA, split-K partials for grids that would not fill the chip.
+# cfg -> (columns per workgroup, weight ring depth, non-temporal weight DMA)
+MW_CFGS = {0: (256, 2, True), 1: (128, 3, True), 2: (128, 2, True), 3: (256, 2, False), 4: (128, 3, False)}
+MW_MAX_M = 320   # M > 256 (a 320-row x tile) fits the LDS on cfg 2 only
+# (N, K, mode) -> {M bucket (128 / 192 / 256 / 320): (split_k, cfg)}, measured on MI355X with cold
+# weights (bench/gemm_bench.py --mw-sweep); other shapes take the default rule in mw_plan
+_MW_TUNED = {}
+
+
+def _mw_bucket(M: int) -> int:
+    return 128 if M <= 128 else (192 if M <= 192 else (256 if M <= 256 else 320))
+
+
+def mw_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL):
+    """(split_k, cfg) for gemm_mw, or None when the shape is unsupported. Default: the
+    128-column, 3-deep tile; split-K (PARTIAL only) to the split nearest 256 workgroups."""
+    if not (1 <= M <= MW_MAX_M) or K % 64:
+        return None
+    t = _MW_TUNED.get((N, K, mode), {}).get(_mw_bucket(M))
+    if t is not None:
+        return t
+    cfg = 1 if M <= 256 else 2
+    cols = MW_CFGS[cfg][0]
+    if N % cols:
+        return None
+    if mode != MODE_PARTIAL:
+        return 1, cfg
+    tiles = N // cols
+    S = max(1, min(K // 64, round(256 / tiles)))
+    return S, cfg
+
+
+def mw_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, plan=None,
+              out: Optional[torch.Tensor] = None):
+    """gemm_mw for 1 <= M <= 320 (built for the mixed decode + prefill-chunk step):
+    PendingSum (MODE_PARTIAL, reduced by the consumer), bf16 [M, N] (MODE_BF16) or
+    silu(gate) * up [M, N / 2] of a block-16 interleaved gate|up weight (MODE_SILU)."""
+    M, K = x.shape
+    N = w.shape[0]
+    p = plan or mw_plan(M, N, K, mode)
+    if p is None or not x.is_contiguous():
+        raise ValueError(f"gemm_mw: unsupported M={M} N={N} K={K} mode={mode}")
+    S, cfg = p
+    if mode == MODE_PARTIAL:
+        part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+        kernels().gemm_mw(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, cfg,
+                          stream_ptr())
+        return PendingSum(part, S)
+    if out is None:
+        out = torch.empty(M, N // 2 if mode == MODE_SILU else N, dtype=torch.bfloat16, device=x.device)
+    kernels().gemm_mw(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, cfg, stream_ptr())
+    return out
+
+
+def _apply_mw_overrides(spec: str) -> None:
+    """XGS_MW_PLANS="NxKxMODE@BUCKET=S,cfg;..." replaces gemm_mw plans (A/B sweeps)."""
+    for item in filter(None, (t.strip() for t in spec.split(";"))):
+        key, plan = item.split("=")
+        shape, bucket = key.split("@")
+        n, k, mode = (int(v) for v in shape.split("x"))
+        _MW_TUNED.setdefault((n, k, mode), {})[int(bucket)] = tuple(int(v) for v in plan.split(","))
+
+
+_apply_mw_overrides(__import__("os").environ.get("XGS_MW_PLANS", ""))
+
+
 # ---------------------------------------------------------------------------- fused decode layer
 MODE_RESID = 3
 # (A cooperative in-launch reduce of the larger slabs -- every split workgroup of a

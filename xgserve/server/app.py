@@ -141,7 +141,10 @@ async def _sse(request: web.Request, srv: InferenceServer, sreq: ServerRequest, 
             n += len(batch)
             if batch[-1].type in ("done", "error"):
                 break
-            if sreq.sse_native and sreq.wire is None and request.transport is not None:
+            if (sreq.sse_native and sreq.wire is None and request.transport is not None
+                    and resp.headers.get("Transfer-Encoding", "").lower() == "chunked"):
+                # (the wire bytes are pre-framed HTTP/1.1 chunks: an HTTP/1.0 client gets an
+                # unchunked, close-delimited body, so it stays on the queued resp.write path)
                 # the response has started (headers flushed): from here on the server's
                 # output handler writes this stream's token chunks straight to the
                 # socket; only the final done / error event comes through the queue.

@@ -31,7 +31,9 @@ import logging
 import multiprocessing as mp
 import os
 import pickle
+import select
 import signal
+import struct
 import threading
 import time
 from typing import Any, Dict, List, Optional
@@ -64,31 +66,79 @@ def _unframe(chunk: bytes) -> bytes:
     return chunk[i + 2:len(chunk) - 2]
 
 
+_HDR = struct.Struct("<I")
+
+
 class _Conn:
     """One duplex pipe end, serviced ON the event loop: a reader callback (no reader
     thread re-hopping onto the loop and contending for the GIL) hands decoded
     message batches to `on_msgs`; `send` batches messages and flushes once per loop
     iteration. (A writer thread doing the pickling and the pipe write measured
-    slower on an 8-core host: one more thread holding the GIL beside the loop.)"""
+    slower on an 8-core host: one more thread holding the GIL beside the loop.)
+
+    The socket is NON-BLOCKING with our own length-prefixed frames: a flush writes
+    what the kernel takes and leaves the rest to a loop writer callback, so a peer
+    that is itself busy writing (both ends flushing batches larger than the socket
+    buffer) can never block this loop -- each side keeps reading while its own
+    bytes wait (blocking send_bytes on both ends could deadlock)."""
+
+    READ_CHUNK = 1 << 20
 
     def __init__(self, conn, loop: asyncio.AbstractEventLoop, on_msgs, name: str):
-        self.conn = conn
+        self.conn = conn  # keeps the descriptor open
+        self.fd = conn.fileno()
+        os.set_blocking(self.fd, False)
         self.loop = loop
         self.on_msgs = on_msgs
         self.pending: List[tuple] = []
         self._flush_armed = False
         self.closed = False
         self.name = name
-        loop.add_reader(conn.fileno(), self._readable)
+        self._rbuf = bytearray()
+        self._wbuf = bytearray()
+        self._writer_on = False
+        loop.add_reader(self.fd, self._readable)
 
     def _readable(self) -> None:
-        try:
-            while self.conn.poll():
-                self.on_msgs(pickle.loads(self.conn.recv_bytes()))
-        except (EOFError, OSError):
-            self.closed = True
-            self.loop.remove_reader(self.conn.fileno())
-            self.on_msgs([("eof",)])
+        eof = False
+        while True:
+            try:
+                data = os.read(self.fd, self.READ_CHUNK)
+            except (BlockingIOError, InterruptedError):
+                break
+            except OSError:
+                eof = True
+                break
+            if not data:
+                eof = True
+                break
+            self._rbuf += data
+        self._deliver()
+        if eof:
+            self._eof()
+
+    def _deliver(self) -> None:
+        buf, off, n = self._rbuf, 0, len(self._rbuf)
+        frames = []
+        while n - off >= 4:
+            (ln,) = _HDR.unpack_from(buf, off)
+            if n - off - 4 < ln:
+                break
+            frames.append(bytes(buf[off + 4:off + 4 + ln]))
+            off += 4 + ln
+        if off:
+            del buf[:off]
+        for f in frames:
+            self.on_msgs(pickle.loads(f))
+
+    def _eof(self) -> None:
+        self.closed = True
+        self.loop.remove_reader(self.fd)
+        if self._writer_on:
+            self.loop.remove_writer(self.fd)
+            self._writer_on = False
+        self._wbuf.clear()
+        self.on_msgs([("eof",)])
 
     def send(self, msg: tuple) -> None:
         self.pending.append(msg)
@@ -102,13 +152,40 @@ class _Conn:
             self.pending = []
             return
         msgs, self.pending = self.pending, []
+        payload = pickle.dumps(msgs, protocol=pickle.HIGHEST_PROTOCOL)
+        self._wbuf += _HDR.pack(len(payload))
+        self._wbuf += payload
+        self._write_some()
+
+    def _write_some(self) -> None:
         try:
-            self.conn.send_bytes(pickle.dumps(msgs, protocol=pickle.HIGHEST_PROTOCOL))
-        except (OSError, ValueError):
+            while self._wbuf:
+                k = os.write(self.fd, self._wbuf)
+                del self._wbuf[:k]
+        except (BlockingIOError, InterruptedError):
+            pass
+        except OSError:  # peer gone: the reader sees the EOF
             self.closed = True
+            self._wbuf.clear()
+        if self._wbuf and not self._writer_on:
+            self.loop.add_writer(self.fd, self._write_some)
+            self._writer_on = True
+        elif not self._wbuf and self._writer_on:
+            self.loop.remove_writer(self.fd)
+            self._writer_on = False
+
+    @property
+    def buffered(self) -> int:
+        """Bytes flushed but not yet taken by the kernel."""
+        return len(self._wbuf)
 
     def close(self, timeout: float = 5.0) -> None:
+        """Flush, then give the socket up to `timeout` to take the rest (shutdown)."""
         self.flush()
+        t_end = time.monotonic() + timeout
+        while self._wbuf and not self.closed and time.monotonic() < t_end:
+            select.select([], [self.fd], [], 0.05)
+            self._write_some()
 
 
 # ---------------------------------------------------------------------------- hub
@@ -121,18 +198,54 @@ class FrontendHub:
         self.conns: Dict[int, _Conn] = {}
         self.procs: List[mp.Process] = []
 
+    # respawns of one front end within RESPAWN_WINDOW_S before the hub gives up and
+    # shuts the server down (a crash loop must not leave a healthy-looking hub that
+    # nothing listens for)
+    MAX_RESPAWNS = 5
+    RESPAWN_WINDOW_S = 60.0
+
     def start(self) -> None:
+        self.srv.hub = self
+        self.procs = [None] * self.n
+        self._respawns: Dict[int, List[float]] = {}
+        for wid in range(self.n):
+            self._spawn(wid)
+
+    def _spawn(self, wid: int) -> None:
         ctx = mp.get_context("spawn")
         loop = asyncio.get_running_loop()
-        self.srv.hub = self
-        for wid in range(self.n):
-            a, b = ctx.Pipe(duplex=True)
-            p = ctx.Process(target=frontend_main, args=(wid, self.srv.cfg, self._state(), b), daemon=True,
-                            name=f"xgs-frontend{wid}")
-            p.start()
-            b.close()
-            self.procs.append(p)
-            self.conns[wid] = _Conn(a, loop, lambda msgs, w=wid: self._on_msgs(w, msgs), f"hub-frontend{wid}")
+        a, b = ctx.Pipe(duplex=True)
+        p = ctx.Process(target=frontend_main, args=(wid, self.srv.cfg, self._state(), b), daemon=True,
+                        name=f"xgs-frontend{wid}")
+        p.start()
+        b.close()
+        self.procs[wid] = p
+        self.conns[wid] = _Conn(a, loop, lambda msgs, w=wid: self._on_msgs(w, msgs), f"hub-frontend{wid}")
+
+    def _front_end_lost(self, wid: int) -> None:
+        """An unexpected front-end exit: its clients' sockets died with it, so every
+        request it admitted is cancelled (queued ones leave the queue, running ones
+        are aborted in their engine -- no decoding for clients that are gone); then a
+        fresh front end takes the port share (bounded respawns, else shut down)."""
+        srv = self.srv
+        lost = [rid for rid, r in list(srv.queued.items()) + list(srv.inflight.items())
+                if getattr(r, "remote_wid", None) == wid]
+        for rid in lost:
+            srv.streamer.discard(rid)
+            srv.cancel(rid)
+        log.error("front end %d exited: cancelled %d of its requests", wid, len(lost))
+        now = time.monotonic()
+        hist = [t for t in self._respawns.get(wid, []) if now - t < self.RESPAWN_WINDOW_S]
+        if len(hist) >= self.MAX_RESPAWNS:
+            log.error("front end %d keeps exiting (%d respawns in %.0f s): shutting down", wid, len(hist),
+                      self.RESPAWN_WINDOW_S)
+            os.kill(os.getpid(), signal.SIGTERM)
+            return
+        self._respawns[wid] = hist + [now]
+        p = self.procs[wid]
+        if p is not None:
+            p.join(0.1)
+        self._spawn(wid)
 
     def _state(self) -> dict:
         s = self.srv
@@ -181,11 +294,11 @@ class FrontendHub:
             elif op == "m":  # front-end HTTP metrics: (kind, args)
                 getattr(m, msg[1])(*msg[2])
             elif op == "eof":
+                self.conns.pop(wid, None)
                 if getattr(self, "stopping", False):
                     log.info("front end %d stopped", wid)
                 else:
-                    log.error("front end %d exited", wid)
-                self.conns.pop(wid, None)
+                    self._front_end_lost(wid)
 
     # admin calls whose bad input is a 400 on the single-process server (app.py)
     _INVALID = {"areload_config": "config", "swap_model": "model", "add_replicas": "replicas",
@@ -210,6 +323,8 @@ class FrontendHub:
             c.close()
         t_end = time.monotonic() + timeout
         for p in self.procs:
+            if p is None:
+                continue
             p.join(max(0.1, t_end - time.monotonic()))
             if p.is_alive():
                 p.terminate()
@@ -445,11 +560,18 @@ class FrontendClient:
                     continue
                 w = p.wire
                 if w is not None:
-                    if not w.is_closing():
-                        w.write(chunk)
-                        if t_tok:
-                            dsum += now - t_tok
-                            dn += 1
+                    if w.is_closing():
+                        continue
+                    if w.get_write_buffer_size() > WIRE_MAX_BUFFERED:  # client not reading: cut the stream
+                        p.wire = None
+                        self.metrics.record_error("slow_consumer")
+                        self.streamer.fail_stream(rid, "client is not reading the stream", "slow_consumer")
+                        self.cancel(rid)
+                        continue
+                    w.write(chunk)
+                    if t_tok:
+                        dsum += now - t_tok
+                        dn += 1
                 elif p.sender is not None:
                     p.sender.send(_RawToken(_unframe(chunk), t_tok))
             elif op == "ev":
@@ -484,6 +606,9 @@ class FrontendClient:
                 os.kill(os.getpid(), signal.SIGINT)  # web.run_app's graceful exit
         if dn:  # Req 5.1 delay of the tokens written now (mean of this batch, weighted by count)
             self.metrics.record_delivery(dsum / dn, dn)
+
+
+from .orchestrator import WIRE_MAX_BUFFERED  # noqa: E402  (shared slow-consumer bound)
 
 
 def frontend_main(wid: int, cfg, state: dict, conn) -> None:

@@ -79,6 +79,10 @@ class RemoteSender:
             self.hub.send(self.wid, ("close", self.rid))
 
 
+# unread bytes a native SSE client may leave in its transport before the stream is cut
+WIRE_MAX_BUFFERED = 4 << 20
+
+
 class RemoteWire:
     """`ServerRequest.wire` of a native SSE stream held by a front-end process: token
     chunks are batched to that process, which writes them to the client socket."""
@@ -128,6 +132,7 @@ class ServerRequest:
         # (the client transport) -- no per-token queue hop or coroutine wake-up
         self.sse_native = False
         self.wire = None
+        self.remote_wid: Optional[int] = None  # admitting front-end process (server/frontend.py)
         self.future: Optional[asyncio.Future] = None if stream else loop.create_future()
         self.sender: Optional[StreamSender] = None
         self.token_stream = None
@@ -361,6 +366,7 @@ class InferenceServer:
         sreq = ServerRequest(rid or new_request_id(), kind, prompt_ids, params, int(priority), stream, self._loop)
         if remote is not None:
             hub, wid = remote
+            sreq.remote_wid = wid  # cancelled if that front end dies (FrontendHub._front_end_lost)
             if stream:
                 sreq.sender = RemoteSender(hub, wid, sreq.id)
                 self.streamer.register(sreq.id, sreq.sender)
@@ -543,6 +549,23 @@ class InferenceServer:
                 log.error("replica %d reported fatal error: %s", rid, payload)
                 self._on_replica_failure(r)
 
+    def _wire_ok(self, sreq: ServerRequest, w) -> bool:
+        """May a token chunk go straight to this client transport? Direct writes skip
+        aiohttp's drain, so a client that stays connected but stops reading would
+        grow the transport buffer for the whole generation: past WIRE_MAX_BUFFERED
+        unread bytes the stream fails as a slow consumer and its sequence is aborted."""
+        if w.is_closing():
+            return False
+        if w.get_write_buffer_size() <= WIRE_MAX_BUFFERED:
+            return True
+        log.warning("request %s: client not reading (%d bytes unsent), stream cut", sreq.id,
+                    w.get_write_buffer_size())
+        self.metrics.record_error("slow_consumer")
+        sreq.wire = None
+        self.streamer.fail_stream(sreq.id, "client is not reading the stream", "slow_consumer")
+        self.cancel(sreq.id)
+        return False
+
     def _handle_outputs(self, rid: int, outs: List[RequestOutput]) -> None:
         now = time.monotonic()
         n_tok = 0
@@ -564,7 +587,7 @@ class InferenceServer:
                 sreq.completion_tokens = o.completion_tokens
                 if w.__class__ is RemoteWire:
                     w.send(o.sse, o.t_tokens)
-                elif not w.is_closing():
+                elif self._wire_ok(sreq, w):
                     w.write(o.sse)
                     n_wire += 1
                     t_wire = o.t_tokens
@@ -596,7 +619,7 @@ class InferenceServer:
                                 o.new_text, sreq.completion_tokens - 1, o.logprobs[-1] if o.logprobs else None))
                             if w.__class__ is RemoteWire:
                                 w.send(chunk, o.t_tokens)  # the front end writes it and times the delivery
-                            elif not w.is_closing():
+                            elif self._wire_ok(sreq, w):
                                 w.write(chunk)
                                 n_wire += 1
                                 t_wire = o.t_tokens
@@ -613,7 +636,7 @@ class InferenceServer:
                     if sreq.wire is not None:
                         if sreq.wire.__class__ is RemoteWire:
                             sreq.wire.send(sse_chunk(ev), o.t_tokens)
-                        elif not sreq.wire.is_closing():
+                        elif self._wire_ok(sreq, sreq.wire):
                             sreq.wire.write(sse_chunk(ev))
                     else:
                         sreq.sender.send(ev)
