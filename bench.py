@@ -298,6 +298,8 @@ def main():
                        "preemptions": st_["preemptions"], "kv_blocks": st_["kv_blocks_total"],
                        "decode_steps_total": st_["decode_steps"], "steps_total": st_["steps"],
                        "gemm_table": bool(getattr(eng, "gemm_table", False)),
+                       "prefill_chunk": a.prefill_chunk,
+                       "mixed_graph_replays": getattr(eng.runner, "mixed_replays", 0),
                        **({"host_ms_per_step": {k: round(1000 * v / a.steps, 4)
                                                 for k, v in eng.step_timing().items()}}
                           if eng._timing is not None else {})},

@@ -15,7 +15,6 @@
 #   arsim    one rank of 70B TP8 at batch 1 under a simulated 0 / 4 / 8 us all-reduce
 #   coalesce admission-window A/B: driver form + 1000 steps at --coalesce 1 / 2 / 3
 #   profile  rocprofv3 kernel + gap profile of the headline (bench/profile.sh)
-#   b1       persistent batch-1 decode: tests, batch-1 bench vs the multi-launch path, profile
 # Each GPU step has its own time limit; the first failure ends the suite.
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -104,14 +103,6 @@ profile)
   bash bench/profile.sh "$o" "$@" ;;
 dmaprobe)
   run dma_probe 120 ./bench/dma_probe.bin ;;
-b1stamps)
-  run stamps 300 python -u bench/b1_stamps.py "$@" ;;
-b1)
-  pyt b1_tests 600 -v tests/test_persistent_gpu.py
-  run stamps 300 python -u bench/b1_stamps.py
-  run c1 200 env XGS_PERSISTENT_DECODE=1 $B --concurrency 1 --steps 200 --warmup 20 "$@"
-  run c1_multilaunch 200 env XGS_PERSISTENT_DECODE=0 $B --concurrency 1 --steps 200 --warmup 20 "$@"
-  XGS_PERSISTENT_DECODE=1 bash bench/profile.sh "$o/prof_c1" --concurrency 1 ;;
 *)
   echo "unknown suite $suite"; exit 2 ;;
 esac

@@ -69,11 +69,6 @@ int custom_allreduce_resid(const float*, int, int, uint16_t*, float*, int, int64
                            const uintptr_t*, int, int, uint32_t*, uint32_t*, hipStream_t);
 int custom_allgather_lastdim(const void*, void*, int64_t, int64_t, int64_t, const uintptr_t*, const uintptr_t*, int,
                              int, uint32_t*, uint32_t*, hipStream_t);
-int decode_b1_plan(int, int, int, int, int, int*);
-int decode_b1(const uint64_t*, const uint64_t*, const uint16_t*, const uint16_t*, uint16_t*, const int32_t*,
-              const int32_t*, const int32_t*, const int32_t*, const float*, uint64_t*, int*, const uint64_t*, int, int,
-              int, int, int, int, int, float, float, uint64_t*, hipStream_t);
-int decode_b1_build_runs(const uint64_t*, int, int, int, int, int, uint64_t*, int*, hipStream_t);
 int car_max_blocks();
 int car_wallclock_khz();
 int car_chunk();
@@ -352,30 +347,6 @@ PYBIND11_MODULE(_kernels, m) {
   });
 
   // ---- custom one-shot xGMI all-reduce (csrc/comm/custom_allreduce.hip)
-  m.def("decode_b1_plan", [](int L, int H, int F, int Hq, int Hkv) {
-    int pl[13];
-    const int ng = xgk::decode_b1_plan(L, H, F, Hq, Hkv, pl);
-    std::vector<int> r(pl, pl + 13);
-    r.insert(r.begin(), ng);
-    return r;  // [granules, S_att, ring_lines, off_xres, off_xbig, off_ctl, lds_bytes, g_* offsets...]; granules < 0: unsupported
-  });
-  m.def("decode_b1", [](uintptr_t wptr, uintptr_t kvptr, uintptr_t resid, uintptr_t fnorm, uintptr_t out, uintptr_t pos,
-                        uintptr_t slots, uintptr_t bt, uintptr_t sl, uintptr_t cs, uintptr_t gran, uintptr_t ctl,
-                        uintptr_t runs, int L, int H, int F, int Hq, int Hkv, int bs, int apply_rope, float eps,
-                        float scale, uintptr_t stamps, uintptr_t st) {
-    check(xgk::decode_b1(P<const uint64_t>(wptr), P<const uint64_t>(kvptr), P<const uint16_t>(resid),
-                         P<const uint16_t>(fnorm), P<uint16_t>(out), P<const int32_t>(pos), P<const int32_t>(slots),
-                         P<const int32_t>(bt), P<const int32_t>(sl), P<const float>(cs), P<uint64_t>(gran), P<int>(ctl),
-                         P<const uint64_t>(runs), L, H, F, Hq, Hkv, bs, apply_rope, eps, scale, P<uint64_t>(stamps),
-                         S(st)),
-          "decode_b1");
-  });
-  m.def("decode_b1_build_runs", [](uintptr_t wptr, int L, int H, int F, int Hq, int Hkv, uintptr_t runs,
-                                   uintptr_t overflow, uintptr_t st) {
-    check(xgk::decode_b1_build_runs(P<const uint64_t>(wptr), L, H, F, Hq, Hkv, P<uint64_t>(runs), P<int>(overflow),
-                                    S(st)),
-          "decode_b1_build_runs");
-  });
   m.def("car_wallclock_khz", []() { return xgk::car_wallclock_khz(); });
   m.def("car_limits", []() { return py::make_tuple(xgk::car_max_ranks(), xgk::car_max_blocks(), xgk::car_chunk()); });
   m.def("car_alloc_uncached", [](int64_t bytes) {

@@ -232,6 +232,7 @@ PYBIND11_MODULE(_runtime, m) {
       .def_readwrite("admit_watermark", &SchedulerConfig::admit_watermark)
       .def_readwrite("max_prefill_seqs", &SchedulerConfig::max_prefill_seqs)
       .def_readwrite("decode_prefill_cap", &SchedulerConfig::decode_prefill_cap)
+      .def_readwrite("decode_prefill_seqs", &SchedulerConfig::decode_prefill_seqs)
       .def_readwrite("coalesce_prompts", &SchedulerConfig::coalesce_prompts)
       .def_readwrite("coalesce_max_wait", &SchedulerConfig::coalesce_max_wait)
       .def_readwrite("lookahead_mixed", &SchedulerConfig::lookahead_mixed)

@@ -242,6 +242,8 @@ const StepPlan& StepScheduler::schedule() {
   }
   plan_.num_decodes = plan_.num_seqs;
   if (cfg_.decode_prefill_cap > 0 && plan_.num_decodes > 0) budget = std::min(budget, cfg_.decode_prefill_cap);
+  int max_pf = cfg_.max_prefill_seqs;
+  if (cfg_.decode_prefill_seqs > 0 && plan_.num_decodes > 0) max_pf = std::min(max_pf, cfg_.decode_prefill_seqs);
 
   // Pass 2: verify steps (decode + draft) and continuing prefill chunks.
   int n_prefill = 0;
@@ -253,7 +255,7 @@ const StepPlan& StepScheduler::schedule() {
     int q = verify ? 1 + static_cast<int>(s->draft.size()) : std::min(remaining, budget);
     if (verify && q > budget) continue;
     if (!verify && q < remaining && !cfg_.chunked_prefill && plan_.num_seqs > 0) continue;
-    if (!verify && n_prefill >= cfg_.max_prefill_seqs) continue;
+    if (!verify && n_prefill >= max_pf) continue;
     bool ok = true;
     while (!ensure_blocks(*s, s->num_computed + q)) {
       int v = plan_.num_seqs == 0 ? pick_victim(i) : -1;
@@ -290,7 +292,7 @@ const StepPlan& StepScheduler::schedule() {
     hold = ready < cfg_.coalesce_prompts && waiting_.front()->wait_plans < cfg_.coalesce_max_wait;
   }
   while (!hold && !waiting_.empty() && budget > 0 && static_cast<int>(running_.size()) < cfg_.max_num_seqs &&
-         n_prefill < cfg_.max_prefill_seqs) {
+         n_prefill < max_pf) {
     Sequence* s = waiting_.front();
     if (s->tokens.back() == kPlaceholder) break;  // preempted by a lookahead plan: wait for commit()
     int matched_pages = 0;

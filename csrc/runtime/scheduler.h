@@ -51,6 +51,10 @@ struct SchedulerConfig {
   // Stall-free batching: prompt chunks ride on the decode step's weight reads
   // instead of stalling every running stream behind one large prefill step.
   int decode_prefill_cap = 0;
+  // cap on prefill sequences in a step that also carries decode rows (0: max_prefill_seqs
+  // only). 1 keeps every stall-free mixed step at ONE prompt chunk (the runner's
+  // mixed-step graphs take exactly that shape).
+  int decode_prefill_seqs = 0;
   // Admission window for continuous batching (Req 2.1/2.2 batching window, applied to
   // prompt admission): while decode rows are running, new prompts are held until
   // coalesce_prompts of them are waiting or the oldest has been passed over by

@@ -308,3 +308,27 @@ def test_overlap_outputs_go_to_the_sink_immediately(monkeypatch):
     monkeypatch.setattr(E, "EARLY_OUTPUTS", False)
     eng.output_sink = got.append
     assert E.LLMEngine._emit_early(eng, list(outs)) == outs and len(got) == 2
+
+
+def test_stall_free_one_chunk_per_decode_step():
+    """decode_prefill_cap = 128, decode_prefill_seqs = 1 (stall-free batching): while
+    rows decode, every step carries at most ONE prompt chunk of <= 128 tokens, so a
+    200-token prompt and a 60-token prompt take 2 + 1 steps -- never two prompts in
+    one step (the runner's mixed-step graphs take exactly that shape)."""
+    c = R.SchedulerConfig()
+    c.block_size, c.num_blocks, c.max_num_seqs = 16, 1024, 64
+    c.max_num_batched_tokens, c.max_model_len, c.enable_prefix_cache = 8192, 2048, False
+    c.decode_prefill_cap, c.decode_prefill_seqs = 128, 1
+    s = R.StepScheduler(c)
+    assert s.add(1, list(range(10, 30)), 50, 1, True, False, [], 0)
+    plan = s.schedule()
+    assert int(plan["num_tokens"]) == 20          # nothing decoding: the whole prompt at once
+    plan = _step(s, plan)
+    assert s.add(2, list(range(100, 300)), 50, 1, True, False, [], 0)
+    assert s.add(3, list(range(400, 460)), 50, 1, True, False, [], 0)
+    shapes = []
+    for _ in range(4):
+        plan = _step(s, plan)
+        nd, ns = int(plan["num_decodes"]), int(plan["num_seqs"])
+        shapes.append((nd, ns - nd, int(plan["num_tokens"]) - nd))
+    assert shapes == [(1, 1, 128), (1, 1, 72), (2, 1, 60), (3, 0, 0)], shapes

@@ -49,7 +49,22 @@ def _rank_main(rank, world, port, ck, moe_comm, q, env=None):
                                      num_blocks=256, max_num_seqs=8, max_num_batched_tokens=1024,
                                      max_model_len=512, moe_comm=moe_comm))
         if rank == 0:
-            outs = eng.generate(PROMPTS, SamplingParams(max_tokens=N_GEN, temperature=0.0, ignore_eos=True))
+            sp = SamplingParams(max_tokens=N_GEN, temperature=0.0, ignore_eos=True)
+            if os.environ.get("XGS_TEST_STAGGER") == "1":
+                # the second prompt arrives while the first decodes: its prompt step is an
+                # eager MIXED step, launched asynchronously under TP (followers sample too)
+                res = {"a": [], "b": []}
+                eng.add_request("a", PROMPTS[0], sp)
+                n = 0
+                while eng.has_work() or n < 3:
+                    for o in eng.step():
+                        res[o.request_id].extend(o.new_token_ids)
+                    n += 1
+                    if n == 3:
+                        eng.add_request("b", PROMPTS[1], sp)
+                outs = [res["a"], res["b"]]
+            else:
+                outs = eng.generate(PROMPTS, sp)
             eng.stop_followers()
             mode = {"custom_ar": eng.custom_ar is not None, "graphs": bool(eng.runner.graphs), "async": eng._async,
                     "fused": eng.model._fused_ok}
@@ -73,7 +88,9 @@ _UNFUSED = {"XGS_FUSED_DECODE": "0", "XGS_ASYNC_SCHED": "0"}
     # share the GPU with one hardware queue each, so every rank's kernels are co-resident
     ("llama", "alltoall", 8, {"GPU_MAX_HW_QUEUES": "1"}),
     ("mixtral", "alltoall", 2, None), ("mixtral", "allreduce", 2, None), ("mixtral", "auto", 2, None),
-    ("mixtral", "alltoall", 2, {"XGS_EP_EXACT_MIN_PAIRS": "0"})])
+    ("mixtral", "alltoall", 2, {"XGS_EP_EXACT_MIN_PAIRS": "0"}),
+    # an arrival while decoding: the asynchronous eager mixed step under TP
+    ("llama", "alltoall", 2, {"XGS_TEST_STAGGER": "1"}), ("llama", "alltoall", 4, {"XGS_TEST_STAGGER": "1"})])
 def test_tp2_on_one_gpu_matches_fp32_reference(tmp_path, model, moe_comm, world, env):
     """Llama: TP attention + MLP shards; by default the fused TP decode layer (one
     custom all-reduce launch per row-parallel projection reduces the split-K
@@ -109,7 +126,7 @@ def test_tp2_on_one_gpu_matches_fp32_reference(tmp_path, model, moe_comm, world,
     assert kind == "ok", outs
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert mode["custom_ar"], mode  # decode all-reduces on the IPC kernels
-    if model == "llama" and env is None:
+    if model == "llama" and (env is None or "XGS_TEST_STAGGER" in env):
         assert mode["graphs"] and mode["async"] and mode["fused"], mode
 
     base = None

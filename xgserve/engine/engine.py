@@ -142,6 +142,8 @@ class LLMEngine:
         sc.cache_threshold = cfg.cache_threshold
         sc.max_prefill_seqs = cfg.max_prefill_seqs
         sc.decode_prefill_cap = cfg.decode_prefill_cap
+        # stall-free batching: one prompt chunk per decoding step (the mixed-step graphs)
+        sc.decode_prefill_seqs = 1 if cfg.decode_prefill_cap > 0 else 0
         sc.coalesce_prompts = max(1, int(cfg.prompt_coalesce))
         sc.coalesce_max_wait = max(0, int(cfg.prompt_coalesce_max_wait))
         # asynchronous scheduling over prompt steps too (r2_async_mixed_ab.md)

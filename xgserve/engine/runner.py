@@ -31,7 +31,6 @@ import torch
 
 from .. import ops
 from ..models.base import AttnMeta
-from ..ops import persistent
 from ..ops.attention import DecodeWorkspace
 from ..parallel import comm
 
@@ -255,7 +254,6 @@ class ModelRunner:
         ar = comm.custom_allreduce()
         if ar is not None:
             ar.set_timeout(seconds)
-        persistent.set_timeout_all(seconds)
 
     @torch.no_grad()
     def capture_graphs(self):
@@ -379,14 +377,12 @@ class ModelRunner:
         ar = comm.custom_allreduce()
         if ar is not None:
             ar.poll_async()
-        persistent.poll_all()
 
     @staticmethod
     def _check_comm():
         ar = comm.custom_allreduce()
         if ar is not None:
             ar.check()
-        persistent.check_all()
 
     def _record_out(self, n: int, tok: torch.Tensor, lp: torch.Tensor, hidden, graph: bool):
         """Tokens / logprobs D2H into the next of the two pinned buffers + an event."""
@@ -611,13 +607,29 @@ class ModelRunner:
             self.last_logits = logits.float().cpu()
         if not self.is_driver:
             if self.is_cuda:
+                # asynchronous prompt steps under TP: when the leader leaves this step's
+                # tokens on the device, so does every follower -- the same all-gathered
+                # logits and the leader's broadcast sampling rows give the same tokens, and
+                # the successor's decode rows substitute their ids from this rank's
+                # g_out_tok exactly as after a graph step
+                on_dev = self._async_ok(S, plan)
+                if on_dev:
+                    tok, _ = self._sample(logits, samp)
+                    self.g_out_tok[:S].copy_(tok[:S])
                 # an event of THIS step: a follower that queued its successor waits
                 # for this launch only (engine.follower_loop), not the whole stream
                 self._poll_comm()
                 ev = torch.cuda.Event()
                 ev.record()
-                return (S, hid, None, None, False, ev)
+                return (S, hid, None, None, on_dev, ev)
             return (S, hid, (None, None, hid), None)
+        tok, lp = self._sample(logits, samp)
+        if self.is_cuda:
+            on_dev = self.tokens_to_device(S, tok, plan)
+            return self._record_out(S, tok, lp, hid, on_dev)
+        return (S, hid, (tok.numpy().astype(np.int32), lp.numpy().astype(np.float32), hid), None)
+
+    def _sample(self, logits: torch.Tensor, samp: Optional[SamplingRows]):
         if samp is None or samp.all_greedy:
             tok, lp = ops.argmax_logprob(logits)
         else:
@@ -628,18 +640,21 @@ class ModelRunner:
             if not self.is_cuda:
                 gen = torch.Generator().manual_seed(int(samp.seeds[0]) & 0x7FFFFFFF)
             tok, lp = ops.sample_tokens(logits, dev_f[0], dev_f[1], topk, seeds, step=0, generator=gen)
-        if self.is_cuda:
-            on_dev = self.tokens_to_device(S, tok, plan)
-            return self._record_out(S, tok, lp, hid, on_dev)
-        return (S, hid, (tok.numpy().astype(np.int32), lp.numpy().astype(np.float32), hid), None)
+        return tok, lp
+
+    def _async_ok(self, S: int, plan: dict) -> bool:
+        """May an eager step's successor be planned before its tokens reach the host?
+        The same answer on every TP rank (it depends on the plan only)."""
+        return not (not ASYNC_MIXED or not self.graphs or S > self.g_B or bool(plan["is_embed"].any())
+                    or int(plan["num_sample"]) != S)
 
     def tokens_to_device(self, S: int, tok: torch.Tensor, plan: dict) -> bool:
-        """Eager step (TP = 1): also leave the sampled tokens in g_out_tok, in sample
-        order, so the engine can plan and launch the next step before this one ends
-        (its decode rows substitute their ids from there). Verify / embedding steps
-        and batches wider than the graph buffers stay synchronous."""
-        if (not ASYNC_MIXED or not self.graphs or S > self.g_B or comm.get_state().tp_size > 1
-                or bool(plan["is_embed"].any()) or int(plan["num_sample"]) != S):
+        """Eager step: also leave the sampled tokens in g_out_tok, in sample order, so
+        the engine can plan and launch the next step before this one ends (its decode
+        rows substitute their ids from there; TP followers do the same from their own
+        sampling, _execute_eager). Verify / embedding steps and batches wider than the
+        graph buffers stay synchronous."""
+        if not self._async_ok(S, plan):
             return False
         self.g_out_tok[:S].copy_(tok[:S])
         return True

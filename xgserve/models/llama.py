@@ -54,9 +54,6 @@ FAST_M_SLAB = 64    # tokens per step for the O-projection slab kernel
 # statistics (comm.tp_allreduce_resid): 6 launches + attention per layer instead
 # of 11. XGS_FUSED_DECODE=0 restores the unfused chain (A/B measurements, tests).
 FUSED_DECODE = os.environ.get("XGS_FUSED_DECODE", "1") != "0"
-# batch-1 decode steps of dense TP=1 models on the persistent all-layer kernel
-# (csrc/kernels/decode_b1.hip); 0 keeps the per-layer fused launches
-PERSISTENT_DECODE = os.environ.get("XGS_PERSISTENT_DECODE", "0") == "1"
 # 64 < T <= this many tokens (the mixed step: decode rows + one bounded prefill chunk)
 # run every projection on gemm_mw (csrc/kernels/gemm_mw.hip): weight-stream-bound
 # MFMA GEMMs whose split-K partials go to the consumers, SiLU-gate in gate_up.
@@ -485,8 +482,6 @@ class LlamaForCausalLM(nn.Module):
         # every layer on gemm_mw for 64 < T <= MW_MAX_TOKENS (the runner's mixed-step graphs)
         self._mw_ok = self.device.type == "cuda" and all(l.mw_ok for l in self.layers)
         self._fused_ws = ResidWorkspace(2 * cfg.num_layers + 1, FAST_M_SLAB, H, device) if self._fused_ok else None
-        self._b1 = None        # persistent batch-1 decoder (built on first use)
-        self._b1_failed = False
 
     @torch.no_grad()
     def fold_norms(self):
@@ -539,34 +534,6 @@ class LlamaForCausalLM(nn.Module):
             return False
         return T > FAST_M_SMALL or self._fused_small_ok
 
-    def _b1_decoder(self):
-        """The persistent batch-1 decoder when this model can use it: dense, TP=1, bf16
-        weights with folded norms, head_dim 128, a 256-CU device (one workgroup per CU
-        must be co-resident). None otherwise."""
-        if self._b1 is not None or self._b1_failed:
-            return self._b1
-        l0 = self.layers[0]
-        # a TP shard runs it only as the single-process rank simulation (bench.py --tp-shard:
-        # no peers, the row-parallel all-reduces are identities there too)
-        ok = (PERSISTENT_DECODE and FUSED_DECODE and self.device.type == "cuda" and self.norms_folded
-              and (self.tp == 1 or get_state().tp_size == 1) and not l0.moe and l0.w8 is None
-              and self.cfg.head_dim == 128 and self.weight_dtype == "bf16" and self.dtype == torch.bfloat16
-              and torch.cuda.get_device_properties(self.device).multi_processor_count == 256)
-        if ok:
-            from ..ops.persistent import B1Decoder, b1_plan
-            H, F = self.cfg.hidden_size, l0.gate_up.shape[0] // 2
-            if b1_plan(self.cfg.num_layers, H, F, l0.Hq, l0.Hkv) is not None:
-                self._b1 = B1Decoder(self.layers, self.norm, H, F, l0.Hq, l0.Hkv, self.cfg.norm_eps, l0.attn.scale,
-                                     l0.attn.use_rope)
-        self._b1_failed = self._b1 is None
-        return self._b1
-
-    def _forward_b1(self, input_ids: torch.Tensor, meta: AttnMeta,
-                    kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
-        resid = ops.embed_gather(input_ids, self.embed)
-        return self._b1(resid, meta.positions, meta.slot_mapping, meta.dec_block_tables, meta.dec_seq_lens,
-                        self.cos_sin, kv_caches)
-
     def _forward_fused(self, input_ids: torch.Tensor, meta: AttnMeta,
                        kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         ws = self._fused_ws
@@ -601,9 +568,6 @@ class LlamaForCausalLM(nn.Module):
     # ------------------------------------------------------------------ forward
     def forward(self, input_ids: torch.Tensor, meta: AttnMeta,
                 kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
-        if (meta.num_tokens == 1 and meta.num_decodes == 1 and input_ids.dtype == torch.int32
-                and self._b1_decoder() is not None):
-            return self._forward_b1(input_ids, meta, kv_caches)
         if self.fused_decode_ok(meta):
             return self._forward_fused(input_ids, meta, kv_caches)
         x = ops.embed_gather(input_ids, self.embed) if input_ids.dtype == torch.int32 else \
