@@ -15,6 +15,8 @@
 #   arsim    one rank of 70B TP8 at batch 1 under a simulated 0 / 4 / 8 us all-reduce
 #   coalesce admission-window A/B: driver form + 1000 steps at --coalesce 1 / 2 / 3
 #   profile  rocprofv3 kernel + gap profile of the headline (bench/profile.sh)
+#   mw       gemm_mw numerics + sweep, stall-free mixed-step tests, headline with prompt chunks
+#   ar       custom all-reduce push vs pull: tests + per-call latency (bench/ar_bench.py)
 # Each GPU step has its own time limit; the first failure ends the suite.
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -101,6 +103,17 @@ coalesce)  # admission window A/B (EngineConfig.prompt_coalesce)
   done ;;
 profile)
   bash bench/profile.sh "$o" "$@" ;;
+mw)  # gemm_mw: numerics, shape sweep, stall-free mixed-step engine tests, headline with / without chunks
+  pyt mw_tests 300 tests/test_skinny_gpu.py -k mw
+  run mw_sweep 500 python -u bench/gemm_bench.py --mw-sweep --M 64 128 192 256 320 --shapes qkv o gate_up down
+  pyt stall_free 300 tests/test_engine_gpu.py -k "stall_free or graph_decode or chunked or async"
+  run c64_chunk128 200 $B --steps 20 --warmup 5 --prefill-chunk 128 "$@"
+  run c64_chunk128_long 300 env XGS_STEP_LOG="$o/steps_chunk128.jsonl" $B --steps 1000 --warmup 100 --prefill-chunk 128 "$@"
+  run c64_chunk256_long 300 $B --steps 1000 --warmup 100 --prefill-chunk 256 "$@"
+  run c64_base_long 300 $B --steps 1000 --warmup 100 "$@" ;;
+ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
+  pyt ar_tests 600 tests/test_custom_ar_gpu.py
+  run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;
 dmaprobe)
   run dma_probe 120 ./bench/dma_probe.bin ;;
 *)

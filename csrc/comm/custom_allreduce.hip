@@ -295,6 +295,216 @@ __global__ void __launch_bounds__(128) car_resid_kernel(const float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Push ("LL") protocol for latency-bound TP decode messages.
+//
+// The pull kernels above put a full synchronisation in front of the data: stage the
+// message locally, fence system-wide, raise a flag in each peer, spin, fence again,
+// then READ every peer's copy over xGMI -- a remote read round trip after the last
+// flag arrives. Here each rank WRITES its contribution straight into every peer's
+// receive region as 16-byte lines {d0, gen, d1, gen} (two 4-byte payload words, each
+// carrying the generation): the receiver polls its OWN memory until both flags of a
+// line equal the current generation. The flag travels in the same store as the data,
+// so there is no fence, no separate flag word and no remote read; the cost is 2x the
+// bytes on the wire, which is nothing at decode sizes (T * H * 2 bytes per rank).
+//
+// Receive region per rank: [2 parities][CAR_MAX_RANKS sources][lines]; a block's
+// lines are at a fixed offset in every launch and parity = gen & 1, so the
+// double-buffering argument of the pull kernels holds unchanged: before rank X writes
+// parity p of block b at generation g into Y, X has received Y's generation g-1 of
+// block b, which Y sent only after it finished reading generation g-2 (the previous
+// user of parity p). The generation (not a toggling bit) in every line means a stale
+// line of generation g-2 never matches.
+struct LLLine {
+  uint32_t d0, f0, d1, f1;
+};
+
+__device__ __forceinline__ void ll_store(uint8_t* dst, uint32_t d0, uint32_t d1, uint32_t gen) {
+  u32x4_t v = {d0, gen, d1, gen};
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(dst));
+}
+
+// Poll `n` lines at src (stride 16 B) until every flag equals gen; returns the
+// payload words. Timeouts as car_wait (ctl[0] error counter, ctl[1] limit).
+template <int N>
+__device__ __forceinline__ bool ll_recv(const uint8_t* src, uint32_t gen, uint32_t* ctl, uint32_t (&d)[2 * N]) {
+  uint32_t got = 0;  // bit i: line i has arrived
+  uint64_t t0 = 0, limit = 0;
+  uint32_t spins = 0;
+  while (true) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      if (got & (1u << i)) continue;
+      const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(src + 16 * i));
+      if (v[1] == gen && v[3] == gen) {
+        d[2 * i] = v[0];
+        d[2 * i + 1] = v[2];
+        got |= 1u << i;
+      }
+    }
+    if (got == (1u << N) - 1) return true;
+    if (spins == 0) {
+      if (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+      limit = __hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t0 = wall_clock64();
+    }
+    if ((++spins & 63) == 0) {
+      if (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+      if (wall_clock64() - t0 > limit) {
+        atomicAdd(ctl, 1u);
+        return false;
+      }
+    }
+  }
+}
+
+// Fused residual all-reduce on the push protocol (same contract as car_resid_kernel:
+// rank-ordered sum, bit-identical on every rank). Block (t, chunk), 128 lanes x 8
+// elements; lane's 8 bf16 = 4 payload words = 2 lines per peer.
+template <int SP>
+__global__ void __launch_bounds__(128) car_ll_resid_kernel(const float* __restrict__ part, int S, int T,
+                                                           uint16_t* __restrict__ resid, float* __restrict__ ss_part,
+                                                           int H, int64_t region_bytes, CarPtrs p, int rank, int world,
+                                                           uint32_t* __restrict__ gens, uint32_t* __restrict__ err) {
+  __shared__ float red[2];
+  const int t = blockIdx.x, chunk = blockIdx.y;
+  const int b = t * gridDim.y + chunk;
+  const int lane = threadIdx.x;
+  const uint32_t gen = gens[b] + 1;
+  const int64_t e = static_cast<int64_t>(t) * H + (chunk * 128 + lane) * 8;  // element offset
+  // 1. local split-K reduction -> bf16 contribution (4 payload words)
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int ns = SP > 0 ? SP : S;
+#pragma unroll
+  for (int s = 0; s < ns; ++s) {
+    const float* pp = part + static_cast<int64_t>(s) * T * H + e;
+    const float4 a = *reinterpret_cast<const float4*>(pp);
+    const float4 c = *reinterpret_cast<const float4*>(pp + 4);
+    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+    v[4] += c.x; v[5] += c.y; v[6] += c.z; v[7] += c.w;
+  }
+  const uint4 mine = pack8(v);
+  const uint4 r_old = ld16(resid + e);
+  // 2. push to every peer: lines at [parity][my rank][e / 4 .. + 2) of the peer's region
+  const int64_t src_bytes = region_bytes / (2 * CAR_MAX_RANKS);  // per (parity, source)
+  const int64_t line_off = (gen & 1) * (region_bytes / 2) + (e / 4) * 16;
+  for (int r = 0; r < world; ++r) {
+    if (r == rank) continue;
+    uint8_t* dst = p.data[r] + line_off + static_cast<int64_t>(rank) * src_bytes;
+    ll_store(dst, mine.x, mine.y, gen);
+    ll_store(dst + 16, mine.z, mine.w, gen);
+  }
+  // 3. receive every peer's lines from my own region, sum in rank order
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  bool ok = true;
+  for (int r = 0; r < world; ++r) {
+    uint4 pv = mine;
+    if (r != rank && ok) {
+      uint32_t d[4];
+      ok = ll_recv<2>(p.data[rank] + line_off + static_cast<int64_t>(r) * src_bytes, gen, err, d);
+      pv = make_uint4(d[0], d[1], d[2], d[3]);
+    }
+    acc8<uint16_t>(acc, pv);
+  }
+  float ro[8];
+  unpack8(r_old, ro);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ro[i] += acc[i];
+  const uint4 pk = pack8(ro);
+  st16(resid + e, pk);
+  unpack8(pk, ro);
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ss += ro[i] * ro[i];
+  ss = block_sum(ss, red);
+  if (lane == 0) {
+    ss_part[static_cast<int64_t>(chunk) * T + t] = ss;
+    gens[b] = gen;
+  }
+}
+
+// Plain all-reduce (bf16, nbytes % 16 == 0) on the push protocol: block b owns the
+// 16-byte groups [b * 256, b * 256 + 256) -- 4 KiB of message per block, 2 lines per
+// group per peer.
+constexpr int CAR_LL_GROUPS = 256;
+
+__global__ void __launch_bounds__(CAR_LL_GROUPS) car_ll_kernel(const uint8_t* __restrict__ in,
+                                                                uint8_t* __restrict__ out, int64_t nbytes,
+                                                                int64_t region_bytes, CarPtrs p, int rank, int world,
+                                                                uint32_t* __restrict__ gens,
+                                                                uint32_t* __restrict__ err) {
+  const int b = blockIdx.x;
+  const uint32_t gen = gens[b] + 1;
+  const int64_t grp = static_cast<int64_t>(b) * CAR_LL_GROUPS + threadIdx.x;
+  const bool live = grp * 16 < nbytes;
+  const int64_t src_bytes = region_bytes / (2 * CAR_MAX_RANKS);
+  const int64_t line_off = (gen & 1) * (region_bytes / 2) + grp * 32;
+  uint4 mine = make_uint4(0, 0, 0, 0);
+  if (live) {
+    mine = ld16(in + grp * 16);
+    for (int r = 0; r < world; ++r) {
+      if (r == rank) continue;
+      uint8_t* dst = p.data[r] + line_off + static_cast<int64_t>(rank) * src_bytes;
+      ll_store(dst, mine.x, mine.y, gen);
+      ll_store(dst + 16, mine.z, mine.w, gen);
+    }
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    bool ok = true;
+    for (int r = 0; r < world; ++r) {
+      uint4 pv = mine;
+      if (r != rank && ok) {
+        uint32_t d[4];
+        ok = ll_recv<2>(p.data[rank] + line_off + static_cast<int64_t>(r) * src_bytes, gen, err, d);
+        pv = make_uint4(d[0], d[1], d[2], d[3]);
+      }
+      acc8<uint16_t>(acc, pv);
+    }
+    st16(out + grp * 16, pack8(acc));
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) gens[b] = gen;
+}
+
+int car_ll_max_bytes(int64_t region_bytes) {
+  return static_cast<int>(region_bytes / (2 * CAR_MAX_RANKS) / 2);  // payload bytes per source line region
+}
+
+int custom_allreduce_resid_ll(const float* part, int S, int T, uint16_t* resid, float* ss_part, int H,
+                              int64_t region_bytes, const uintptr_t* data_ptrs, int rank, int world, uint32_t* gens,
+                              uint32_t* err, hipStream_t st) {
+  if (world < 2 || world > CAR_MAX_RANKS || rank < 0 || rank >= world) return 1;
+  if (T <= 0 || S <= 0 || H <= 0 || H % 1024) return 1;
+  if (static_cast<int64_t>(T) * (H / 1024) > CAR_MAX_BLOCKS) return 1;
+  if (static_cast<int64_t>(T) * H * 2 > car_ll_max_bytes(region_bytes)) return 1;
+  CarPtrs p{};
+  for (int r = 0; r < world; ++r) p.data[r] = reinterpret_cast<uint8_t*>(data_ptrs[r]);
+  const dim3 g(T, H / 1024);
+#define XGK_CARLL(SPV)                                                                                           \
+  hipLaunchKernelGGL((car_ll_resid_kernel<SPV>), g, dim3(128), 0, st, part, S, T, resid, ss_part, H, region_bytes, \
+                     p, rank, world, gens, err)
+  if (S == 1) XGK_CARLL(1);
+  else if (S == 2) XGK_CARLL(2);
+  else if (S == 4) XGK_CARLL(4);
+  else if (S == 8) XGK_CARLL(8);
+  else XGK_CARLL(0);
+#undef XGK_CARLL
+  return 0;
+}
+
+int custom_allreduce_ll(const void* in, void* out, int64_t nbytes, int64_t region_bytes, const uintptr_t* data_ptrs,
+                        int rank, int world, uint32_t* gens, uint32_t* err, hipStream_t st) {
+  if (world < 2 || world > CAR_MAX_RANKS || rank < 0 || rank >= world) return 1;
+  if (nbytes <= 0 || nbytes % 16 || nbytes > car_ll_max_bytes(region_bytes)) return 1;
+  const int64_t blocks = (nbytes / 16 + CAR_LL_GROUPS - 1) / CAR_LL_GROUPS;
+  if (blocks > CAR_MAX_BLOCKS) return 1;
+  CarPtrs p{};
+  for (int r = 0; r < world; ++r) p.data[r] = reinterpret_cast<uint8_t*>(data_ptrs[r]);
+  hipLaunchKernelGGL(car_ll_kernel, dim3(static_cast<unsigned>(blocks)), dim3(CAR_LL_GROUPS), 0, st,
+                     static_cast<const uint8_t*>(in), static_cast<uint8_t*>(out), nbytes, region_bytes, p, rank, world,
+                     gens, err);
+  return 0;
+}
+
 int custom_allreduce_resid(const float* part, int S, int T, uint16_t* resid, float* ss_part, int H,
                            int64_t slot_bytes, const uintptr_t* data_ptrs, const uintptr_t* sig_ptrs, int rank,
                            int world, uint32_t* gens, uint32_t* err, hipStream_t st) {

@@ -69,6 +69,11 @@ int custom_allreduce_resid(const float*, int, int, uint16_t*, float*, int, int64
                            const uintptr_t*, int, int, uint32_t*, uint32_t*, hipStream_t);
 int custom_allgather_lastdim(const void*, void*, int64_t, int64_t, int64_t, const uintptr_t*, const uintptr_t*, int,
                              int, uint32_t*, uint32_t*, hipStream_t);
+int custom_allreduce_ll(const void*, void*, int64_t, int64_t, const uintptr_t*, int, int, uint32_t*, uint32_t*,
+                        hipStream_t);
+int custom_allreduce_resid_ll(const float*, int, int, uint16_t*, float*, int, int64_t, const uintptr_t*, int, int,
+                              uint32_t*, uint32_t*, hipStream_t);
+int car_ll_max_bytes(int64_t);
 int car_max_blocks();
 int car_wallclock_khz();
 int car_chunk();
@@ -385,6 +390,22 @@ PYBIND11_MODULE(_kernels, m) {
     check(xgk::custom_allreduce_2shot(P<void>(in), P<void>(out), nbytes, slot_bytes, data.data(), sig.data(), rank,
                                       static_cast<int>(data.size()), P<uint32_t>(gens), P<uint32_t>(err), S(st)),
           "custom_allreduce_2shot");
+  });
+  // push ("LL") protocol: flag-in-payload lines written into the peers' receive regions
+  m.def("car_ll_max_bytes", [](int64_t region) { return xgk::car_ll_max_bytes(region); });
+  m.def("custom_allreduce_ll", [](uintptr_t in, uintptr_t out, int64_t nbytes, int64_t region,
+                                  std::vector<uintptr_t> data, int rank, uintptr_t gens, uintptr_t err, uintptr_t st) {
+    check(xgk::custom_allreduce_ll(P<void>(in), P<void>(out), nbytes, region, data.data(), rank,
+                                   static_cast<int>(data.size()), P<uint32_t>(gens), P<uint32_t>(err), S(st)),
+          "custom_allreduce_ll");
+  });
+  m.def("custom_allreduce_resid_ll", [](uintptr_t part, int S_, int T, uintptr_t resid, uintptr_t ss_part, int H,
+                                        int64_t region, std::vector<uintptr_t> data, int rank, uintptr_t gens,
+                                        uintptr_t err, uintptr_t st) {
+    check(xgk::custom_allreduce_resid_ll(P<const float>(part), S_, T, P<uint16_t>(resid), P<float>(ss_part), H,
+                                         region, data.data(), rank, static_cast<int>(data.size()), P<uint32_t>(gens),
+                                         P<uint32_t>(err), S(st)),
+          "custom_allreduce_resid_ll");
   });
   m.def("custom_allreduce_resid", [](uintptr_t part, int S_, int T, uintptr_t resid, uintptr_t ss_part, int H,
                                      int64_t slot_bytes, std::vector<uintptr_t> data, std::vector<uintptr_t> sig,

@@ -19,14 +19,14 @@ def _port():
 SIZES = (8, 512, 4096, 8192, 24584, 65536, 1 << 20, 2 << 20, 6 << 20)
 
 
-def _worker(rank, world, port, q, two_shot_min=None, sizes=SIZES):
+def _worker(rank, world, port, q, two_shot_min=None, sizes=SIZES, ll_max=None):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
     import torch.distributed as dist
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
         from xgserve.parallel.custom_ar import CustomAllReduce
-        ar = CustomAllReduce(rank, world, torch.device("cuda:0"), two_shot_min=two_shot_min)
+        ar = CustomAllReduce(rank, world, torch.device("cuda:0"), two_shot_min=two_shot_min, ll_max=ll_max)
         ar.set_timeout(ar.WARMUP_TIMEOUT_S)  # ranks share one GPU and arrive seconds apart
         errs = []
         for n in sizes:  # elements (bf16)
@@ -79,17 +79,19 @@ def _run(target, world, *args):
     return res
 
 
-@pytest.mark.parametrize("world,two_shot_min", [(2, None), (2, 0), (4, None), (4, 0), (8, None), (8, 0)])
-def test_custom_allreduce_one_gpu(world, two_shot_min):
+@pytest.mark.parametrize("world,two_shot_min,ll_max", [(2, None, None), (2, 0, 0), (4, None, None), (4, 0, 0),
+                                                       (8, None, None), (8, 0, 0), (2, None, 0), (8, None, 0)])
+def test_custom_allreduce_one_gpu(world, two_shot_min, ll_max):
     """world ranks share the GPU; two_shot_min=0 forces the two-shot kernel for
-    every size, None is the production choice (one-shot small, two-shot large at 4 ranks).
+    every size, None is the production choice (push protocol up to 256 KiB, one-shot
+    pull above, two-shot large at 4 ranks); ll_max=0 forces the pull kernels.
     world=8 is the Llama-3-70B TP8 group's protocol (8 peers, 7 remote slots per block)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
     sizes = SIZES if world < 8 else SIZES[:7]
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, two_shot_min, sizes)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, two_shot_min, sizes, ll_max)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=240) for _ in ps]
@@ -100,7 +102,7 @@ def test_custom_allreduce_one_gpu(world, two_shot_min):
         assert tmo == 0
 
 
-def _resid_worker(rank, world, port, q):
+def _resid_worker(rank, world, port, q, ll_max=None):
     """custom_allreduce_resid against an fp32 loop reference with the kernel's
     summation order: local split-K slices in order, bf16 contribution per rank,
     rank-order sum, + residual, one bf16 rounding."""
@@ -111,7 +113,7 @@ def _resid_worker(rank, world, port, q):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
         from xgserve.parallel.custom_ar import CustomAllReduce
-        ar = CustomAllReduce(rank, world, torch.device("cuda:0"))
+        ar = CustomAllReduce(rank, world, torch.device("cuda:0"), ll_max=ll_max)
         # 8 ranks time-share one GPU and each builds its fp32 reference on the CPU
         # between collectives: peers arrive seconds apart, as in engine warmup
         ar.set_timeout(ar.WARMUP_TIMEOUT_S)
@@ -163,9 +165,10 @@ def _resid_worker(rank, world, port, q):
 # 128 blocks per rank so all 8 grids are co-resident (8 x 512 blocks of the T=64,
 # H=8192 shape are not: the first grids spin until the wait limit while the last
 # rank's blocks cannot be placed -- an artifact of sharing one GPU).
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_custom_allreduce_resid_one_gpu(world):
-    for rank, errs, tmo in _run(_resid_worker, world):
+@pytest.mark.parametrize("world,ll_max", [(2, None), (4, None), (8, None), (2, 0), (8, 0)])
+def test_custom_allreduce_resid_one_gpu(world, ll_max):
+    """ll_max None: the push protocol (production); 0: the pull kernel."""
+    for rank, errs, tmo in _run(_resid_worker, world, ll_max):
         assert errs == [], (rank, errs)
         assert tmo == 0
 

@@ -19,6 +19,15 @@ bf16 contributions over IPC, adds the sum to the replicated residual stream and
 writes the new residual's RMSNorm statistics (custom_allreduce_resid). It has
 its own slots, signals and generation counters.
 
+Push protocol ("LL", the default for decode-sized messages): instead of staging
+the message locally, fencing, raising flags and then READING every peer's copy
+over xGMI (the pull kernels), each rank writes its contribution straight into
+every peer's receive region as 16-byte lines {data, gen, data, gen}; the receiver
+polls its own memory until the generations match -- no fence, no flag word, no
+remote read round trip after the synchronisation. It serves the fused residual
+all-reduce and plain all-reduces up to `ll_max` bytes (XGS_AR_LL_MAX, 0 = pull
+kernels everywhere).
+
 Failure semantics: a peer that does not arrive within the wait limit makes the
 kernels bump a device error counter and give up (the GPU never hangs); once the
 counter is non-zero every later wait returns at once, so a dead peer costs one
@@ -52,12 +61,15 @@ class CustomAllReduce:
     RESID_SLOT = 1 << 20
     # last-dim all-gather (vocab-parallel LM head of decode steps): T * V/W bf16 per rank
     GATHER_SLOT = 16 << 20
+    # push-protocol receive regions: [2 parities][8 sources][2 x payload] per rank
+    RESID_LL_REGION = 32 << 20   # fused residual: T * H bf16 <= 1 MiB of payload
+    LL_REGION = 8 << 20          # plain all-reduce: <= 256 KiB of payload
     # peer-wait limits: while serving, and around warmup / graph capture
     SERVE_TIMEOUT_S = 2.0
     WARMUP_TIMEOUT_S = 20.0  # (the 32-bit tick word caps the limit at ~21 s at 100 MHz)
 
     def __init__(self, rank: int, world: int, device: torch.device, cpu_group=None, max_bytes: int = 8 << 20,
-                 two_shot_min: Optional[int] = None, two_shot_max: int = 32 << 20):
+                 two_shot_min: Optional[int] = None, two_shot_max: int = 32 << 20, ll_max: Optional[int] = None):
         k = kernels()
         max_ranks, self.max_blocks, chunk = k.car_limits()
         if not (2 <= world <= max_ranks):
@@ -77,10 +89,11 @@ class CustomAllReduce:
         # failure anywhere disables the path everywhere instead of hanging peers
         mine = None
         try:
-            # [one-shot 2 x slot | two-shot 2 x slot2 | resid 2 x RESID_SLOT | gather 2 x GATHER_SLOT]
-            # and [one-shot | two-shot phase 0 | phase 1 | resid | gather] signals
+            # [one-shot 2 x slot | two-shot 2 x slot2 | resid 2 x RESID_SLOT | gather 2 x GATHER_SLOT
+            #  | resid LL region | LL region] and [one-shot | two-shot phase 0 | phase 1 | resid |
+            # gather] signals
             self.data = k.car_alloc_uncached(2 * self.slot + 2 * self.slot2 + 2 * self.RESID_SLOT
-                                             + 2 * self.GATHER_SLOT)
+                                             + 2 * self.GATHER_SLOT + self.RESID_LL_REGION + self.LL_REGION)
             self.sig = k.car_alloc_uncached(5 * nsig)
             mine = (k.car_ipc_handle(self.data), k.car_ipc_handle(self.sig))
         except RuntimeError as e:
@@ -119,6 +132,16 @@ class CustomAllReduce:
         self.sig_ptrs3 = [s_ + 3 * nsig for s_ in self.sig_ptrs]
         self.data_ptrs4 = [d + 2 * self.slot + 2 * self.slot2 + 2 * self.RESID_SLOT for d in self.data_ptrs]
         self.sig_ptrs4 = [s_ + 4 * nsig for s_ in self.sig_ptrs]
+        ll0 = 2 * self.slot + 2 * self.slot2 + 2 * self.RESID_SLOT + 2 * self.GATHER_SLOT
+        self.data_ptrs_rll = [d + ll0 for d in self.data_ptrs]
+        self.data_ptrs_ll = [d + ll0 + self.RESID_LL_REGION for d in self.data_ptrs]
+        self.gens_rll = torch.zeros(self.max_blocks + 1, dtype=torch.int32, device=device)
+        self.gens_ll = torch.zeros(self.max_blocks + 1, dtype=torch.int32, device=device)
+        import os
+        if ll_max is None:
+            ll_max = int(os.environ.get("XGS_AR_LL_MAX", str(256 << 10)))
+        self.ll_max = min(ll_max, k.car_ll_max_bytes(self.LL_REGION))
+        self.resid_ll = self.ll_max > 0
         self.chunk = chunk
         self.gens = torch.zeros(self.max_blocks + 1, dtype=torch.int32, device=device)
         self.gens2 = torch.zeros(self.max_blocks + 1, dtype=torch.int32, device=device)
@@ -151,7 +174,10 @@ class CustomAllReduce:
     def all_reduce(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         out = x if out is None else out
         n = x.numel() * x.element_size()
-        if self._two_shot(n):
+        if n <= self.ll_max:
+            self._k.custom_allreduce_ll(x.data_ptr(), out.data_ptr(), n, self.LL_REGION, self.data_ptrs_ll,
+                                        self.rank, self.gens_ll.data_ptr(), self.err.data_ptr(), stream_ptr())
+        elif self._two_shot(n):
             self._k.custom_allreduce_2shot(x.data_ptr(), out.data_ptr(), n, self.slot2, self.data_ptrs2,
                                            self.sig_ptrs2, self.rank, self.gens2.data_ptr(), self.err.data_ptr(),
                                            stream_ptr())
@@ -171,6 +197,11 @@ class CustomAllReduce:
         if not (part.is_contiguous() and part.dtype == torch.float32 and resid.is_contiguous()
                 and tuple(resid.shape) == (T, H) and resid.dtype == torch.bfloat16 and ss.numel() >= T * (H // 1024)):
             raise ValueError(f"all_reduce_resid: bad operands part={tuple(part.shape)} resid={tuple(resid.shape)}")
+        if self.resid_ll:
+            self._k.custom_allreduce_resid_ll(part.data_ptr(), S, T, resid.data_ptr(), ss.data_ptr(), H,
+                                              self.RESID_LL_REGION, self.data_ptrs_rll, self.rank,
+                                              self.gens_rll.data_ptr(), self.err.data_ptr(), stream_ptr())
+            return
         self._k.custom_allreduce_resid(part.data_ptr(), S, T, resid.data_ptr(), ss.data_ptr(), H, self.RESID_SLOT,
                                        self.data_ptrs3, self.sig_ptrs3, self.rank, self.gens3.data_ptr(),
                                        self.err.data_ptr(), stream_ptr())
