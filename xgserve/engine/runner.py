@@ -62,6 +62,42 @@ def _pinned(n: int, dtype) -> torch.Tensor:
     return t.pin_memory() if torch.cuda.is_available() else t
 
 
+def stage_mixed_inputs(plan: dict, Nd: int, nb: int, B: int, C: int, W: int, src: Optional[np.ndarray],
+                       sec: tuple, hi: np.ndarray, hl: np.ndarray) -> None:
+    """Host staging of a mixed-graph step (ModelRunner._execute_mixed): the plan's Nd
+    decode rows go to rows [0, Nd) and its prompt chunk's q rows to [B, B + q) of the
+    static ids / positions / slot buffers (padding: id 0, position 0, slot -1); seq
+    lens [0, Nd) + the chunk's at B; the chunk's query_start_loc [0, q]; block-table
+    rows likewise; lidx = the logits rows in sample order (decode rows, then the
+    chunk's last row). sec: the section offsets of the int32 buffer `hi`."""
+    T = int(plan["num_tokens"])
+    q = T - Nd
+    o = sec
+    for k, arr, pad in ((0, plan["input_ids"], 0), (1, plan["positions"], 0), (2, plan["slot_mapping"], -1)):
+        base = o[k]
+        hi[base:base + Nd] = arr[:Nd]
+        hi[base + Nd:base + nb] = pad
+        hi[base + B:base + B + q] = arr[Nd:T]
+        hi[base + B + q:base + B + C] = pad
+    sl = plan["seq_lens"]
+    hi[o[3]:o[3] + Nd] = sl[:Nd]
+    hi[o[3] + Nd:o[3] + nb] = 0
+    hi[o[3] + B] = sl[Nd]
+    hi[o[4]:o[4] + nb] = -1
+    if src is not None:
+        hi[o[4]:o[4] + src.shape[0]] = src
+    hi[o[5]] = 0
+    hi[o[5] + 1] = q
+    w = int(plan["bt_width"])
+    bt = hi[o[6]:o[6] + (B + 1) * W].reshape(B + 1, W)
+    pbt = plan["block_tables"].reshape(Nd + 1, w)
+    bt[:Nd, :w] = pbt[:Nd]
+    bt[B, :w] = pbt[Nd]
+    hl[:Nd] = np.arange(Nd)
+    hl[Nd] = nb + q - 1
+    hl[Nd + 1:nb + 1] = 0
+
+
 class ModelRunner:
     def __init__(self, model, *, block_size: int, num_blocks: int, max_num_seqs: int,
                  max_num_batched_tokens: int, max_model_len: int, use_graphs: bool = True,
@@ -498,40 +534,13 @@ class ModelRunner:
         """Replay the (nb, chunk) mixed graph: Nd decode rows at [0, Nd), the prompt
         chunk's q rows at [B, B + q) of the static input buffers."""
         B, W, C = self.g_B, self.g_W, self.mixed_chunk
-        T = int(plan["num_tokens"])
-        q = T - Nd
         n = int(plan["num_sample"])
         si = self.g_stage_idx
         self.g_stage_idx ^= 1
         if self.g_stage_events[si] is not None:
             self.g_stage_events[si].synchronize()
-        hi = self.h_mints[si].numpy()
-        hl = self.h_mlidx[si].numpy()
-        o = self.m_sec
-        ids, pos, slots = plan["input_ids"], plan["positions"], plan["slot_mapping"]
-        for k, arr, pad in ((0, ids, 0), (1, pos, 0), (2, slots, -1)):
-            base = o[k]
-            hi[base:base + Nd] = arr[:Nd]
-            hi[base + Nd:base + nb] = pad
-            hi[base + B:base + B + q] = arr[Nd:T]
-            hi[base + B + q:base + B + C] = pad
-        sl = plan["seq_lens"]
-        hi[o[3]:o[3] + Nd] = sl[:Nd]
-        hi[o[3] + Nd:o[3] + nb] = 0
-        hi[o[3] + B] = sl[Nd]
-        hi[o[4]:o[4] + nb] = -1
-        if src is not None:
-            hi[o[4]:o[4] + src.shape[0]] = src
-        hi[o[5]] = 0
-        hi[o[5] + 1] = q
-        w = int(plan["bt_width"])
-        bt = hi[o[6]:o[6] + (B + 1) * W].reshape(B + 1, W)
-        pbt = plan["block_tables"].reshape(Nd + 1, w)
-        bt[:Nd, :w] = pbt[:Nd]
-        bt[B, :w] = pbt[Nd]
-        hl[:Nd] = np.arange(Nd)
-        hl[Nd] = nb + q - 1
-        hl[Nd + 1:nb + 1] = 0
+        stage_mixed_inputs(plan, Nd, nb, B, C, W, src, self.m_sec, self.h_mints[si].numpy(),
+                           self.h_mlidx[si].numpy())
         self.m_int.copy_(self.h_mints[si], non_blocking=True)
         self.m_lidx[:nb + 1].copy_(self.h_mlidx[si][:nb + 1], non_blocking=True)
         greedy = samp is None or samp.all_greedy
