@@ -138,12 +138,15 @@ class LlamaLayer(nn.Module):
             for n, k in ((Nqkv, H), (H, Hq * D)) + (() if self.moe else ((H, cfg.intermediate_size // tp),)))
         self.m64_silu_ok = self.m64_ok and not self.moe and m64_plan(64, 2 * (cfg.intermediate_size // tp), H,
                                                                      MODE_SILU) is not None
-        # 64 < M <= MW_MAX_TOKENS: gemm_mw for every projection (dense layers)
-        self.mw_ok = self.fast_ok and not self.moe and MW_MAX_TOKENS > FAST_M_SLAB and all(
+        # 64 < M <= MW_MAX_TOKENS: gemm_mw for every projection (MoE layers: the attention
+        # projections; the experts stay on the grouped gemm_m64g)
+        mw_shapes = ((Nqkv, H, MODE_PARTIAL), (H, Hq * D, MODE_PARTIAL))
+        if not self.moe:
+            mw_shapes += ((2 * (cfg.intermediate_size // tp), H, MODE_SILU),
+                          (H, cfg.intermediate_size // tp, MODE_PARTIAL))
+        self.mw_ok = self.fast_ok and MW_MAX_TOKENS > FAST_M_SLAB and all(
             mw_plan(MW_MAX_TOKENS, n, k, mode) is not None and mw_plan(FAST_M_SLAB + 1, n, k, mode) is not None
-            for n, k, mode in ((Nqkv, H, MODE_PARTIAL), (H, Hq * D, MODE_PARTIAL),
-                               (2 * (cfg.intermediate_size // tp), H, MODE_SILU),
-                               (H, cfg.intermediate_size // tp, MODE_PARTIAL)))
+            for n, k, mode in mw_shapes)
         # M <= 16 too, when every projection has a measured small-M plan
         self.w8 = None  # FP8 weight copies for batch <= 16 decode (LlamaForCausalLM.quantize_fp8)
         self.m64_small_ok = self.m64_ok and all(
@@ -345,6 +348,8 @@ class LlamaLayer(nn.Module):
             if self.tp > 1:
                 o = self._ar(o.materialize())
             h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
+            if self.moe:
+                return self.mlp(h), residual
             act = mw_linear(h, self.gate_up, MODE_SILU)
             d = mw_linear(act, self.down, MODE_PARTIAL)
             return (d if self.tp == 1 else self._ar(d.materialize())), residual
