@@ -215,45 +215,59 @@ __global__ void __launch_bounds__(512, 1) gemm_mw_kernel(const uint16_t* __restr
   }
 }
 
-// cfg -> (NWT, D, NT); WN = 4 (4 x 2 waves): 0 = 256 columns, ring 2, nt weights;
-// 1 = 128 columns, ring 3, nt; 2 = 128 columns, ring 2, nt; 3 / 4 = 0 / 1 with
-// default-policy weight loads. The x tile (64 / 128 / 192 / 256 rows) follows M.
-int mw_cfg_cols(int cfg) { return (cfg == 0 || cfg == 3) ? 256 : 128; }
+// cfg -> (WN, NWT, D, NT): 0 = 4 x 2 waves, 256 columns, ring 2, nt weights;
+// 1 = 4 x 2, 128 columns, ring 3, nt; 2 = 4 x 2, 128 columns, ring 2, nt; 3 / 4 = 0 / 1
+// with default-policy weight loads; 5 = 2 x 4 waves, 128 columns, ring 3, nt;
+// 6 = 2 x 4 waves, 256 columns, ring 2, nt. The x tile follows M: 32-row steps on the
+// 4 x 2 layouts (64 .. 320 rows), 64-row steps on the 2 x 4 ones (64 .. 256).
+int mw_cfg_cols(int cfg) { return (cfg == 0 || cfg == 3 || cfg == 6) ? 256 : 128; }
+static int mw_cfg_wn(int cfg) { return cfg >= 5 ? 2 : 4; }
 
-template <int NWT, int MTW, int D>
+template <int WN, int NWT, int MTW, int D>
 constexpr bool mw_fits() {
-  return (D + 1) * (64 * NWT * 128) + D * (32 * MTW * 128) <= 160 * 1024;
+  constexpr int WM = 8 / WN;
+  return (WM * 16 * MTW) % 64 == 0 && (D + 1) * (WN * 16 * NWT * 128) + D * (WM * 16 * MTW * 128) <= 160 * 1024;
 }
 
-template <int NWT, int D, bool NT>
+template <int WN, int NWT, int D, bool NT>
 static int launch_mw(int mtw, dim3 grid, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N,
                      int S, float* part, uint16_t* out, int mode) {
-#define XGK_MW(MTW)                                                                                          \
-  do {                                                                                                       \
-    if constexpr (mw_fits<NWT, MTW, D>()) {                                                                  \
-      hipLaunchKernelGGL((gemm_mw_kernel<4, NWT, MTW, D, NT>), grid, dim3(512), 0, st, x, M, K, w, N, S, part, \
-                         out, mode);                                                                         \
-      return 0;                                                                                              \
-    }                                                                                                        \
-    return 1;                                                                                                \
-  } while (0)
-  switch (mtw) {
-    case 2: XGK_MW(2);
-    case 4: XGK_MW(4);
-    case 6: XGK_MW(6);
-    case 8: XGK_MW(8);
-    default: XGK_MW(10);
+#define XGK_MW(MTW)                                                                                             \
+  case MTW:                                                                                                     \
+    if constexpr (mw_fits<WN, NWT, MTW, D>()) {                                                                 \
+      hipLaunchKernelGGL((gemm_mw_kernel<WN, NWT, MTW, D, NT>), grid, dim3(512), 0, st, x, M, K, w, N, S, part, \
+                         out, mode);                                                                            \
+      return 0;                                                                                                 \
+    }                                                                                                           \
+    return 1;
+  if constexpr (WN == 4) {
+    switch (mtw) {
+      XGK_MW(2)
+      XGK_MW(4)
+      XGK_MW(6)
+      XGK_MW(8)
+      XGK_MW(10)
+      default: return 1;
+    }
+  } else {
+    switch (mtw) {
+      XGK_MW(1)
+      XGK_MW(2)
+      XGK_MW(3)
+      XGK_MW(4)
+      default: return 1;
+    }
   }
 #undef XGK_MW
 }
 
 // x [M, K] bf16 row-major, w [N, K] bf16 row-major. mode MW_PARTIAL: part [S, M, N]
-// fp32; MW_BF16: out [M, N]; MW_SILU: out [M, N / 2] (S = 1). 0 = launched.
-// M <= 256 on every configuration, M <= 320 on those whose rings fit the LDS with a
-// 320-row x tile (cfg 2).
+// fp32; MW_BF16: out [M, N]; MW_SILU: out [M, N / 2] (S = 1). 0 = launched, 1 = a
+// shape / configuration this kernel does not take (M beyond the cfg's LDS budget:
+// M <= 256 everywhere, 320 on cfg 2).
 int gemm_mw(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
             int cfg, hipStream_t st) {
-  if (M < 1 || M > 320 || cfg < 0 || cfg > 4 || S < 1 || K % 64 || S > K / 64) return 1;
+  if (M < 1 || M > 320 || cfg < 0 || cfg > 6 || S < 1 || K % 64 || S > K / 64) return 1;
   const int cols = mw_cfg_cols(cfg);
   if (N % cols) return 1;
   if (mode == MW_PARTIAL) {
@@ -263,14 +277,18 @@ int gemm_mw(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* pa
   } else {
     return 1;
   }
-  const int mtw = M <= 64 ? 2 : M <= 128 ? 4 : M <= 192 ? 6 : M <= 256 ? 8 : 10;
+  int mtw;
+  if (mw_cfg_wn(cfg) == 4) mtw = M <= 64 ? 2 : M <= 128 ? 4 : M <= 192 ? 6 : M <= 256 ? 8 : 10;
+  else mtw = (M + 63) / 64;
   const dim3 grid((N / cols) * S);
   switch (cfg) {
-    case 0: return launch_mw<4, 2, true>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
-    case 1: return launch_mw<2, 3, true>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
-    case 2: return launch_mw<2, 2, true>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
-    case 3: return launch_mw<4, 2, false>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
-    default: return launch_mw<2, 3, false>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+    case 0: return launch_mw<4, 4, 2, true>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+    case 1: return launch_mw<4, 2, 3, true>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+    case 2: return launch_mw<4, 2, 2, true>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+    case 3: return launch_mw<4, 4, 2, false>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+    case 4: return launch_mw<4, 2, 3, false>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+    case 5: return launch_mw<2, 4, 3, true>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+    default: return launch_mw<2, 8, 2, true>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
   }
 }
 

@@ -156,7 +156,7 @@ def test_gemm_m64_rejects_bad_shapes():
 
 # ---------------------------------------------------------------- gemm_mw (64 < M <= 320)
 @pytest.mark.parametrize("M", [65, 100, 128, 192, 257, 320])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
 def test_gemm_mw_partial_every_cfg(M, cfg):
     """Every ring depth / tile width, incl. uneven split-K chunk ranges (K / 64 = 22
     chunks over S = 3 and 5) and short splits (1-2 chunks per split)."""
@@ -187,7 +187,7 @@ def test_gemm_mw_llama_shapes(M, N, K):
 
 
 @pytest.mark.parametrize("M", [65, 192, 256, 320])
-@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 5, 6])
 def test_gemm_mw_silu_and_bf16(M, cfg):
     from xgserve.ops.linear import MW_CFGS, mw_linear
     if M > 256 and cfg != 2:
