@@ -253,7 +253,7 @@ def mw_sweep(a):
                                   out.data_ptr() if mode != L.MODE_PARTIAL else 0, S, mode, cfg, st)
                     try:
                         fn(ws[0])
-                    except RuntimeError:
+                    except (RuntimeError, ValueError):
                         continue  # configuration cannot take this M (LDS)
                     torch.cuda.synchronize()
                     y = part.sum(0) if mode == L.MODE_PARTIAL else out.float()
