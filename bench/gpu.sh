@@ -112,6 +112,14 @@ mw)  # gemm_mw: numerics, shape sweep, stall-free mixed-step engine tests, headl
   run c64_chunk128_long 300 env XGS_STEP_LOG="$o/steps_chunk128.jsonl" $B --steps 1000 --warmup 100 --prefill-chunk 128 "$@"
   run c64_chunk256_long 300 $B --steps 1000 --warmup 100 --prefill-chunk 256 "$@"
   run c64_base_long 300 $B --steps 1000 --warmup 100 "$@" ;;
+r4b)  # round 4 second pass: all-reduce protocols, TP tests (async mixed steps), MoE, profile of the chunked headline
+  pyt ar_tests 600 tests/test_custom_ar_gpu.py
+  run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8
+  pyt tp_tests 600 tests/test_tp_gpu.py
+  run mixtral_c1 300 $B --model mixtral-8x7b --concurrency 1 --steps 60 --warmup 10
+  run mixtral_c64_chunk 300 $B --model mixtral-8x7b --steps 120 --warmup 20 --prefill-chunk 128
+  run mixtral_c64 300 $B --model mixtral-8x7b --steps 120 --warmup 20
+  bash bench/profile.sh "$o/prof_chunk128" --prefill-chunk 128 ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;
