@@ -178,6 +178,8 @@ def m64g_sweep(a):
                 want = x.float() @ ws[0].float().t()
             rows = []
             for cfg in L.M64G_CFGS:
+                if cfg in L.M64G_SMALL_ONLY and M > 16:
+                    continue
                 for nw in ((2,) if mode == L.MODE_SILU else (1, 2)):
                     for S in ((1, 2, 4) if mode == L.MODE_SILU else (1,) if mode != L.MODE_PARTIAL else (1, 2, 4, 8)):
                         cols = 16 * nw * waves[cfg]

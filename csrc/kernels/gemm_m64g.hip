@@ -189,7 +189,10 @@ __device__ __forceinline__ void m64g_silu_tail(const float* __restrict__ part, i
 //   NT  non-temporal weight DMA (streamed once; keeps x resident in L2)
 //   MT  16-row x tiles (4: 16 < M <= 64; 1: M <= 16 -- a quarter of the x DMA and
 //       LDS per chunk, so the weight stream owns the load path at batch 1)
-template <int NW, int WV, int KC, bool NT, int MT>
+//   NS  LDS ring slots (NS - 1 chunks in flight across each barrier): 3, or deeper
+//       for the one-x-tile (M <= 16) configurations, whose slots are small -- a
+//       single workgroup per CU then keeps ~80 KB of weights in flight instead of 40
+template <int NW, int WV, int KC, bool NT, int MT, int NS = 3>
 __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* __restrict__ x, int M, int K,
                                                                const uint16_t* __restrict__ w, int N,
                                                                float* __restrict__ part, uint16_t* __restrict__ out,
@@ -206,9 +209,10 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   constexpr int SLOT = XBYTES + WV * WBYTES;
   constexpr int G = XI + WI;
   static_assert(XI >= 1 && WI >= 1 && XROWS % (RPI * WV) == 0, "bad m64g geometry");
-  __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
-  __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
-  __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
+  static_assert(NS >= 3 && NS * SLOT <= 160 * 1024, "ring");
+  __shared__ __attribute__((aligned(1024))) uint8_t lds0[NS == 3 ? SLOT : NS * SLOT];
+  __shared__ __attribute__((aligned(1024))) uint8_t lds1[NS == 3 ? SLOT : 16];
+  __shared__ __attribute__((aligned(1024))) uint8_t lds2[NS == 3 ? SLOT : 16];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -301,16 +305,41 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
     }
   }
 
-  issue(lds0, 0);
-  if (nchunks > 1) issue(lds1, 1);
-  int c = 0;
-  for (; c + 3 <= nchunks; c += 3) {
-    step(lds0, lds2, c);
-    step(lds1, lds0, c + 1);
-    step(lds2, lds1, c + 2);
+  if constexpr (NS == 3) {
+    issue(lds0, 0);
+    if (nchunks > 1) issue(lds1, 1);
+    int c = 0;
+    for (; c + 3 <= nchunks; c += 3) {
+      step(lds0, lds2, c);
+      step(lds1, lds0, c + 1);
+      step(lds2, lds1, c + 2);
+    }
+    if (c < nchunks) step(lds0, lds2, c);
+    if (c + 1 < nchunks) step(lds1, lds0, c + 1);
+  } else {
+    // NS-slot ring: chunk c in slot c % NS; before chunk c the chunks after it that
+    // are already issued (rem = min(nchunks - 1 - c, NS - 2)) stay in flight
+#pragma unroll
+    for (int j = 0; j < NS - 1; ++j)
+      if (j < nchunks) issue(lds0 + j * SLOT, j);
+    for (int c = 0; c < nchunks; ++c) {
+      const int rem = min(nchunks - 1 - c, NS - 2);
+      if constexpr (NS >= 6) {
+        if (rem >= 4) wait_vmcnt<4 * G>();
+      }
+      if constexpr (NS >= 5) {
+        if (rem == 3) wait_vmcnt<3 * G>();
+      }
+      if constexpr (NS >= 4) {
+        if (rem == 2) wait_vmcnt<2 * G>();
+      }
+      if (rem == 1) wait_vmcnt<G>();
+      if (rem == 0) wait_vmcnt<0>();
+      raw_barrier();
+      if (c + NS - 1 < nchunks) issue(lds0 + ((c + NS - 1) % NS) * SLOT, c + NS - 1);
+      compute(lds0 + (c % NS) * SLOT);
+    }
   }
-  if (c < nchunks) step(lds0, lds2, c);
-  if (c + 1 < nchunks) step(lds1, lds0, c + 1);
 
   if (has_ss) {  // input RMSNorm as a row scale of the (linear) output
     float tot[MT];
@@ -737,6 +766,10 @@ static void launch_m64g(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, i
 #define XGK_M64G4(WV, KC, NT)                                                                                      \
   hipLaunchKernelGGL((gemm_m64g_kernel<NW, WV, KC, NT, 4>), grid, dim3(64 * WV), 0, st, x, M, K, w, N, part, out, \
                      mode, epi)
+// deep-ring one-x-tile configurations (M <= 16 only)
+#define XGK_M64G_DEEP(WV, KC, NT, NSV)                                                                             \
+  hipLaunchKernelGGL((gemm_m64g_kernel<NW, WV, KC, NT, 1, NSV>), grid, dim3(64 * WV), 0, st, x, M, K, w, N, part, \
+                     out, mode, epi)
   switch (cfg) {
     case 1: XGK_M64G(4, 128, true); break;
     case 2: XGK_M64G4(4, 64, false); break;
@@ -745,19 +778,26 @@ static void launch_m64g(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, i
     case 5: XGK_M64G(2, 64, true); break;
     case 6: XGK_M64G(2, 128, true); break;
     case 7: XGK_M64G4(8, 64, true); break;
+    case 8: XGK_M64G_DEEP(2, 128, true, 5); break;
+    case 9: XGK_M64G_DEEP(4, 128, true, 4); break;
+    case 10: XGK_M64G_DEEP(2, 64, true, 6); break;
     default: XGK_M64G(4, 128, false); break;
   }
 #undef XGK_M64G
 #undef XGK_M64G4
+#undef XGK_M64G_DEEP
 }
 
-int m64g_cfg_waves(int cfg) { return cfg == 7 ? 8 : (cfg >= 4 ? 2 : 4); }
-int m64g_cfg_kc(int cfg) { return (cfg == 2 || cfg == 3 || cfg == 4 || cfg == 5 || cfg == 7) ? 64 : 128; }
+int m64g_cfg_waves(int cfg) { return cfg == 7 ? 8 : cfg == 9 ? 4 : (cfg >= 4 ? 2 : 4); }
+int m64g_cfg_kc(int cfg) {
+  return (cfg == 2 || cfg == 3 || cfg == 4 || cfg == 5 || cfg == 7 || cfg == 10) ? 64 : 128;
+}
 
 // Host-side shape / operand checks shared by both entry points (0 = valid).
 static int m64g_check(int M, int K, int N, const float* part, const uint16_t* out, int S, int mode, int nw, int cfg,
                       const M64Epi& epi) {
-  if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 7) return 1;
+  if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 10) return 1;
+  if (cfg >= 8 && M > 16) return 1;  // deep-ring configurations: one x tile only
   if (mode < GG_BF16 || mode > GG_RESID) return 1;
   const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
   if (K % (S * kc) || N % cols) return 1;

@@ -106,12 +106,21 @@ def test_gemm_m64g_waits_are_counted(tmp_path):
     ks = _kernels(asm, "_ZN3xgk16gemm_m64g_kernel")
     assert len(ks) >= 8, len(ks)
     for name, body in ks.items():
-        NW, WV, KC, _nt, MT = _targs(name)
+        NW, WV, KC, _nt, MT, *rest = _targs(name)
+        NS = rest[0] if rest else 3
         RPI = 1024 // (KC * 2)
         G = 16 * MT // RPI // WV + 16 * NW // RPI
-        got = _vmcnts(_pipeline(body))
-        assert got <= {0, G}, (name, sorted(got), G)
-        assert G in got, (name, sorted(got))
+        counted = {k * G for k in range(1, NS - 1)}  # 1 .. NS - 2 chunks left in flight
+        if NS == 3:
+            got = _vmcnts(_pipeline(body))
+            assert got <= {0, G}, (name, sorted(got), G)
+        else:
+            # deep rings: the rotated loop may be laid out ahead of the prologue, so the
+            # whole body is checked -- the counted waits are all there and no other wait
+            # reaches G (smaller ones are the compiler's own, for the epilogue's loads)
+            got = _vmcnts(body)
+            assert not {v for v in got if v >= G} - counted, (name, sorted(got), sorted(counted))
+        assert counted <= got, (name, sorted(got), sorted(counted))
     _no_spills(asm)
 
 

@@ -224,3 +224,35 @@ def test_gemm_mw_rejects_bad_shapes():
         mw_linear(rnd(100, 200), rnd(256, 200), MODE_PARTIAL)   # K % 64
     with pytest.raises(ValueError):
         mw_linear(rnd(100, 256), rnd(256, 256), MODE_SILU, plan=(2, 1))  # SiLU needs split 1
+
+
+@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("cfg", [8, 9, 10])
+@pytest.mark.parametrize("N,K,S", [(4096, 14336, 4), (6144, 4096, 8), (4096, 4096, 4), (512, 1280, 1),
+                                   (1024, 768, 3)])
+def test_gemm_m64g_deep_ring(M, cfg, N, K, S):
+    """The 4- / 5- / 6-slot LDS rings of the one-x-tile kernel (M <= 16), every
+    chunk count phase (incl. fewer chunks than slots), partial and SiLU epilogues."""
+    from xgserve.ops.linear import M64G_CFGS, m64_linear
+    wv, kc, _ = M64G_CFGS[cfg]
+    nw = 2 if N % (32 * wv) == 0 else 1
+    if N % (16 * nw * wv) or K % (S * kc):
+        pytest.skip("shape not tileable")
+    x, w = rnd(M, K), rnd(N, K, scale=0.02)
+    pend = m64_linear(x, w, MODE_PARTIAL, split_k=S, nw=nw, cfg=cfg)
+    assert rel_err(pend.part.sum(0), x.float() @ w.float().t()) < 1e-5
+    if nw == 2:
+        g, u = rnd(N // 2, K, scale=0.02), rnd(N // 2, K, scale=0.02)
+        wi = interleave_gate_up(g, u).contiguous()
+        got = m64_linear(x, wi, MODE_SILU, split_k=1, nw=2, cfg=cfg)
+        ref = torch.nn.functional.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
+        assert rel_err(got, ref) < 1e-2
+
+
+def test_gemm_m64g_deep_ring_rejects_m_above_16():
+    from xgserve.ops._native import stream_ptr
+    x, w = rnd(17, 4096), rnd(4096, 4096, scale=0.02)
+    part = torch.empty(4, 17, 4096, device=DEV)
+    with pytest.raises(ValueError):
+        _native.kernels().gemm_m64g(x.data_ptr(), 17, 4096, w.data_ptr(), 4096, part.data_ptr(), 0, 4, MODE_PARTIAL,
+                                    1, 8, stream_ptr())

@@ -83,8 +83,11 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, split_k: Optional[int] = Non
 
 # gemm_m64g launch configurations (csrc/kernels/gemm_m64g.hip launch_m64g):
 # cfg -> (waves per workgroup, k chunk, non-temporal weight DMA)
+# 8-10: deep LDS rings (5 / 4 / 6 slots) for M <= 16 -- more weight bytes in flight per CU
 M64G_CFGS = {0: (4, 128, False), 1: (4, 128, True), 2: (4, 64, False), 3: (4, 64, True),
-             4: (2, 64, False), 5: (2, 64, True), 6: (2, 128, True), 7: (8, 64, True)}
+             4: (2, 64, False), 5: (2, 64, True), 6: (2, 128, True), 7: (8, 64, True),
+             8: (2, 128, True), 9: (4, 128, True), 10: (2, 64, True)}
+M64G_SMALL_ONLY = (8, 9, 10)
 
 # Measured on MI355X with cold weights (bench/gemm_bench.py --m64g-sweep,
 # profiles/r1_m64g_sweep.jsonl; bucket 16 re-swept with the MT=1 kernel: r1_m64g_mt1_sweep.jsonl): (N, K, mode) -> {M bucket: (nw, split_k, cfg)}.
@@ -147,7 +150,9 @@ def _apply_plan_overrides(spec: str) -> None:
 _apply_plan_overrides(__import__("os").environ.get("XGS_M64_PLANS", ""))
 
 
-def _m64_valid(N: int, K: int, mode: int, nw: int, S: int, cfg: int) -> bool:
+def _m64_valid(N: int, K: int, mode: int, nw: int, S: int, cfg: int, M: int = 1) -> bool:
+    if cfg in M64G_SMALL_ONLY and M > 16:
+        return False
     wv, kc, _ = M64G_CFGS[cfg]
     if N % (16 * nw * wv) or K % (S * kc):
         return False
@@ -165,10 +170,10 @@ def m64_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL):
     t = _M64_TUNED.get((N, K, mode))
     if M <= 16:
         p = t.get(16) if t is not None else None
-        return p if (p is not None and _m64_valid(N, K, mode, *p)) else None
+        return p if (p is not None and _m64_valid(N, K, mode, *p, M=M)) else None
     if t is not None:
         p = t.get(32) if (M <= 40 and 32 in t) else t.get(64)
-        if p is not None and _m64_valid(N, K, mode, *p):
+        if p is not None and _m64_valid(N, K, mode, *p, M=M):
             return p
     if mode == MODE_SILU:
         return (2, 1, 1) if N % 128 == 0 else None
@@ -198,7 +203,7 @@ def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split
         nw = nw or plan[0]
         S = split_k or plan[1]
         cfg = plan[2] if cfg is None else cfg
-        if not _m64_valid(N, K, mode, nw, S, cfg):
+        if not _m64_valid(N, K, mode, nw, S, cfg, M):
             cfg = 0
     k = kernels()
     if mode == MODE_PARTIAL:
