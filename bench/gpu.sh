@@ -121,7 +121,8 @@ r4b)  # round 4 second pass: all-reduce protocols, TP tests (async mixed steps),
   run mixtral_c1 300 $B --model mixtral-8x7b --concurrency 1 --steps 60 --warmup 10
   run mixtral_c64_chunk 300 $B --model mixtral-8x7b --steps 120 --warmup 20 --prefill-chunk 128
   run mixtral_c64 300 $B --model mixtral-8x7b --steps 120 --warmup 20
-  bash bench/profile.sh "$o/prof_chunk128" --prefill-chunk 128 ;;
+  bash bench/profile.sh "$o/prof_chunk128" --prefill-chunk 128
+  bash bench/profile.sh "$o/prof_mixtral_c1" --model mixtral-8x7b --concurrency 1 ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;
