@@ -65,6 +65,10 @@ tp)
 moe)
   pyt moe_tests 400 tests/test_kernels_gpu.py tests/test_engine_gpu.py -k "moe or mixtral or expert"
   run mixtral_c64 300 $B --model mixtral-8x7b --steps 60 --warmup 20 "$@"
+  pyt prefetch_test 200 tests/test_engine_gpu.py -k mall_prefetch
+  for pf in 0 48 120; do
+    run c1_pf$pf 200 env XGS_MALL_PREFETCH=$pf $B --concurrency 1 --steps 200 --warmup 20
+  done
   run mixtral_c1 300 $B --model mixtral-8x7b --concurrency 1 --steps 60 --warmup 10 "$@"
   run mixtral_tp2_c64 300 $B --model mixtral-8x7b --tp-shard 2 --steps 60 --warmup 20 "$@" ;;
 prefill)
@@ -118,6 +122,10 @@ r4b)  # round 4 second pass: all-reduce protocols, TP tests (async mixed steps),
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8
   pyt tp_tests 600 tests/test_tp_gpu.py
+  pyt prefetch_test 200 tests/test_engine_gpu.py -k mall_prefetch
+  for pf in 0 48 120; do
+    run c1_pf$pf 200 env XGS_MALL_PREFETCH=$pf $B --concurrency 1 --steps 200 --warmup 20
+  done
   run mixtral_c1 300 $B --model mixtral-8x7b --concurrency 1 --steps 60 --warmup 10
   run mixtral_c64_chunk 300 $B --model mixtral-8x7b --steps 120 --warmup 20 --prefill-chunk 128
   run mixtral_c64 300 $B --model mixtral-8x7b --steps 120 --warmup 20
