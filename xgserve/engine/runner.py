@@ -154,8 +154,10 @@ class ModelRunner:
         self.mixed_bs: List[int] = []
         self.mixed_replays = 0
         if self.mixed_chunk > 0:
+            # decode rows + chunk on gemm_mw when every layer has it (<= MW_MAX_TOKENS rows),
+            # else the library GEMMs (graph-capturable too)
             from ..models.llama import MW_MAX_TOKENS
-            lim = MW_MAX_TOKENS if getattr(model, "_mw_ok", False) else 0
+            lim = MW_MAX_TOKENS if getattr(model, "_mw_ok", False) else max_num_batched_tokens
             self.mixed_bs = [b for b in self.graph_bs if b >= 16 and b + self.mixed_chunk <= lim]
             if not self.mixed_bs:
                 self.mixed_chunk = 0
