@@ -116,6 +116,7 @@ mw)  # gemm_mw: numerics, shape sweep, stall-free mixed-step engine tests, headl
   pyt stall_free 300 tests/test_engine_gpu.py -k "stall_free or graph_decode or chunked or async"
   run c64_chunk128 200 $B --steps 20 --warmup 5 --prefill-chunk 128 "$@"
   run c64_chunk128_long 300 env XGS_STEP_LOG="$o/steps_chunk128.jsonl" $B --steps 1000 --warmup 100 --prefill-chunk 128 "$@"
+  run c64_chunk128_lib 300 env XGS_MW_MAX_TOKENS=0 $B --steps 1000 --warmup 100 --prefill-chunk 128 "$@"
   run c64_chunk256_long 300 $B --steps 1000 --warmup 100 --prefill-chunk 256 "$@"
   run c64_base_long 300 $B --steps 1000 --warmup 100 "$@" ;;
 r4b)  # round 4 second pass: all-reduce protocols, TP tests (async mixed steps), MoE, profile of the chunked headline
