@@ -181,9 +181,10 @@ def m64g_sweep(a):
                 if cfg in L.M64G_SMALL_ONLY and M > 16:
                     continue
                 for nw in ((2,) if mode == L.MODE_SILU else (1, 2)):
-                    for S in ((1, 2, 4) if mode == L.MODE_SILU else (1,) if mode != L.MODE_PARTIAL else (1, 2, 4, 8)):
+                    for S in ((1, 2, 4) if mode == L.MODE_SILU else (1,) if mode != L.MODE_PARTIAL else
+                              (1, 2, 3, 4, 5, 6, 8)):
                         cols = 16 * nw * waves[cfg]
-                        if N % cols or K % (S * kcs[cfg]):
+                        if N % cols or K % kcs[cfg] or S > K // kcs[cfg] or (mode == L.MODE_SILU and K % (S * kcs[cfg])):
                             continue
                         part = torch.empty(S, M, N, dtype=torch.float32, device="cuda")
                         out = torch.empty(M, N // 2 if mode == L.MODE_SILU else N, dtype=torch.bfloat16,

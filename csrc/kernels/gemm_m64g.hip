@@ -217,9 +217,12 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int S = gridDim.y, s = blockIdx.y;
-  const int kws = K / S;
-  const int k0 = s * kws;
-  const int nchunks = kws / KC;
+  // split s takes chunks [s * nch / S, (s + 1) * nch / S): any S <= K / KC (uneven
+  // splits fill the chip where K / KC has no divisor near 256 / column tiles)
+  const int nch_all = K / KC;
+  const int c_lo = s * nch_all / S;
+  const int k0 = c_lo * KC;
+  const int nchunks = (s + 1) * nch_all / S - c_lo;
   const int nbase = blockIdx.x * (16 * NW * WV) + wid * WROWS;
 
   const int dr = lane / GPR, dj = lane % GPR;    // row within a DMA instruction, granule
@@ -800,7 +803,7 @@ static int m64g_check(int M, int K, int N, const float* part, const uint16_t* ou
   if (cfg >= 8 && M > 16) return 1;  // deep-ring configurations: one x tile only
   if (mode < GG_BF16 || mode > GG_RESID) return 1;
   const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
-  if (K % (S * kc) || N % cols) return 1;
+  if (K % kc || S > K / kc || N % cols) return 1;
   // split-K SiLU: fp32 slabs + one zeroed arrival ticket per column tile (m64g_silu_tail)
   if (mode == GG_SILU && (nw != 2 || (S > 1 && (part == nullptr || epi.counters == nullptr)))) return 1;
   if (mode == GG_BF16 && S != 1) return 1;

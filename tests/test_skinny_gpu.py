@@ -256,3 +256,15 @@ def test_gemm_m64g_deep_ring_rejects_m_above_16():
     with pytest.raises(ValueError):
         _native.kernels().gemm_m64g(x.data_ptr(), 17, 4096, w.data_ptr(), 4096, part.data_ptr(), 0, 4, MODE_PARTIAL,
                                     1, 8, stream_ptr())
+
+
+@pytest.mark.parametrize("M", [1, 16, 40, 64])
+@pytest.mark.parametrize("N,K,nw,S,cfg", [(6144, 4096, 2, 5, 3), (6144, 4096, 1, 3, 0), (4096, 14336, 2, 3, 1),
+                                          (4096, 14336, 2, 7, 3), (1024, 768, 1, 5, 4)])
+def test_gemm_m64g_uneven_splits(M, N, K, nw, S, cfg):
+    """Split-K ranges of unequal chunk counts (K / KC not a multiple of S)."""
+    from xgserve.ops.linear import m64_linear
+    x, w = rnd(M, K), rnd(N, K, scale=0.02)
+    pend = m64_linear(x, w, MODE_PARTIAL, split_k=S, nw=nw, cfg=cfg)
+    assert pend.part.shape == (S, M, N)
+    assert rel_err(pend.part.sum(0), x.float() @ w.float().t()) < 1e-5

@@ -154,7 +154,7 @@ def _m64_valid(N: int, K: int, mode: int, nw: int, S: int, cfg: int, M: int = 1)
     if cfg in M64G_SMALL_ONLY and M > 16:
         return False
     wv, kc, _ = M64G_CFGS[cfg]
-    if N % (16 * nw * wv) or K % (S * kc):
+    if N % (16 * nw * wv) or K % kc or S > K // kc:  # uneven split-K ranges are fine
         return False
     # split-K SiLU reduces its slabs in the GEMM's tail (m64g_silu_tail): NW = 2 pairs only
     return not (mode == MODE_SILU and nw != 2) and not (mode == MODE_BF16 and S != 1)
