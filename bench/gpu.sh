@@ -112,7 +112,7 @@ mw)  # gemm_mw: numerics, shape sweep, stall-free mixed-step engine tests, headl
   run mw_sweep 500 python -u bench/gemm_bench.py --mw-sweep --M 64 128 192 256 320 --shapes qkv o gate_up down
   run mw_sweep_lm 200 python -u bench/gemm_bench.py --mw-sweep --M 64 65 --shapes lm_head --top 3
   pyt deep_ring 200 tests/test_skinny_gpu.py -k "deep_ring or uneven"
-  run m64g_c1_sweep 400 python -u bench/gemm_bench.py --m64g-sweep --M 1 --shapes qkv o gate_up down
+  run m64g_c1_sweep 700 python -u bench/gemm_bench.py --m64g-sweep --M 1 64 --shapes qkv o gate_up down
   pyt stall_free 300 tests/test_engine_gpu.py -k "stall_free or graph_decode or chunked or async"
   run c64_chunk128 200 $B --steps 20 --warmup 5 --prefill-chunk 128 "$@"
   run c64_chunk128_long 300 env XGS_STEP_LOG="$o/steps_chunk128.jsonl" $B --steps 1000 --warmup 100 --prefill-chunk 128 "$@"
