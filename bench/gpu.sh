@@ -16,6 +16,7 @@
 #   coalesce admission-window A/B: driver form + 1000 steps at --coalesce 1 / 2 / 3
 #   profile  rocprofv3 kernel + gap profile of the headline (bench/profile.sh)
 #   mw       gemm_mw numerics + sweep, stall-free mixed-step tests, headline with prompt chunks
+#   m64      LM head on gemm_mw, deep-ring / uneven-split gemm_m64g tests + sweeps
 #   ar       custom all-reduce push vs pull: tests + per-call latency (bench/ar_bench.py)
 # Each GPU step has its own time limit; the first failure ends the suite.
 set -o pipefail
@@ -109,16 +110,16 @@ profile)
   bash bench/profile.sh "$o" "$@" ;;
 mw)  # gemm_mw: numerics, shape sweep, stall-free mixed-step engine tests, headline with / without chunks
   pyt mw_tests 300 tests/test_skinny_gpu.py -k mw
-  run mw_sweep 500 python -u bench/gemm_bench.py --mw-sweep --M 64 128 192 256 320 --shapes qkv o gate_up down
-  run mw_sweep_lm 200 python -u bench/gemm_bench.py --mw-sweep --M 64 65 --shapes lm_head --top 3
-  pyt deep_ring 200 tests/test_skinny_gpu.py -k "deep_ring or uneven"
-  run m64g_c1_sweep 700 python -u bench/gemm_bench.py --m64g-sweep --M 1 64 --shapes qkv o gate_up down
+  run mw_sweep 420 python -u bench/gemm_bench.py --mw-sweep --M 64 128 192 256 320 --shapes qkv o gate_up down
   pyt stall_free 300 tests/test_engine_gpu.py -k "stall_free or graph_decode or chunked or async"
   run c64_chunk128 200 $B --steps 20 --warmup 5 --prefill-chunk 128 "$@"
-  run c64_chunk128_long 300 env XGS_STEP_LOG="$o/steps_chunk128.jsonl" $B --steps 1000 --warmup 100 --prefill-chunk 128 "$@"
-  run c64_chunk128_lib 300 env XGS_MW_MAX_TOKENS=0 $B --steps 1000 --warmup 100 --prefill-chunk 128 "$@"
-  run c64_chunk256_long 300 $B --steps 1000 --warmup 100 --prefill-chunk 256 "$@"
-  run c64_base_long 300 $B --steps 1000 --warmup 100 "$@" ;;
+  run c64_chunk128_long 240 env XGS_STEP_LOG="$o/steps_chunk128.jsonl" $B --steps 600 --warmup 60 --prefill-chunk 128 "$@"
+  run c64_chunk128_lib 240 env XGS_MW_MAX_TOKENS=0 $B --steps 600 --warmup 60 --prefill-chunk 128 "$@"
+  run c64_base_long 240 $B --steps 600 --warmup 60 "$@" ;;
+m64)  # decode GEMM plans: LM head on gemm_mw, deep-ring / uneven-split gemm_m64g tests and sweeps
+  run mw_sweep_lm 200 python -u bench/gemm_bench.py --mw-sweep --M 64 65 --shapes lm_head --top 3
+  pyt deep_ring 200 tests/test_skinny_gpu.py -k "deep_ring or uneven"
+  run m64g_sweep 700 python -u bench/gemm_bench.py --m64g-sweep --M 1 64 --shapes qkv o gate_up down ;;
 r4b)  # round 4 second pass: all-reduce protocols, TP tests (async mixed steps), MoE, profile of the chunked headline
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8
