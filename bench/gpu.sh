@@ -18,6 +18,7 @@
 #   mw       gemm_mw numerics + sweep, stall-free mixed-step tests, headline with prompt chunks
 #   m64      LM head on gemm_mw, deep-ring / uneven-split gemm_m64g tests + sweeps
 #   ar       custom all-reduce push vs pull: tests + per-call latency (bench/ar_bench.py)
+#   r4b/r4c  round-4 passes: AR + TP + prefetch A/B; Mixtral + profiles
 # Each GPU step has its own time limit; the first failure ends the suite.
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -120,14 +121,15 @@ m64)  # decode GEMM plans: LM head on gemm_mw, deep-ring / uneven-split gemm_m64
   run mw_sweep_lm 200 python -u bench/gemm_bench.py --mw-sweep --M 64 65 --shapes lm_head --top 3
   pyt deep_ring 200 tests/test_skinny_gpu.py -k "deep_ring or uneven"
   run m64g_sweep 700 python -u bench/gemm_bench.py --m64g-sweep --M 1 64 --shapes qkv o gate_up down ;;
-r4b)  # round 4 second pass: all-reduce protocols, TP tests (async mixed steps), MoE, profile of the chunked headline
+r4b)  # round 4: all-reduce protocols, TP tests (async mixed steps), batch-1 Infinity-Cache prefetch A/B
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
-  run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8
-  pyt tp_tests 600 tests/test_tp_gpu.py
+  run ar_bench 240 python -u bench/ar_bench.py --world 2 4 8
+  pyt tp_tests 500 tests/test_tp_gpu.py
   pyt prefetch_test 200 tests/test_engine_gpu.py -k mall_prefetch
   for pf in 0 48 120; do
-    run c1_pf$pf 200 env XGS_MALL_PREFETCH=$pf $B --concurrency 1 --steps 200 --warmup 20
-  done
+    run c1_pf$pf 150 env XGS_MALL_PREFETCH=$pf $B --concurrency 1 --steps 200 --warmup 20 "$@"
+  done ;;
+r4c)  # round 4: Mixtral with / without prompt chunks, profiles of the chunked headline and Mixtral batch 1
   run mixtral_c1 300 $B --model mixtral-8x7b --concurrency 1 --steps 60 --warmup 10
   run mixtral_c64_chunk 300 $B --model mixtral-8x7b --steps 120 --warmup 20 --prefill-chunk 128
   run mixtral_c64 300 $B --model mixtral-8x7b --steps 120 --warmup 20
