@@ -335,7 +335,10 @@ __device__ __forceinline__ bool ll_recv(const uint8_t* src, uint32_t gen, uint32
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       if (got & (1u << i)) continue;
-      const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(src + 16 * i));
+      // volatile: one real 16-B load per poll (a plain load may be hoisted out of the
+      // spin and served from a register forever)
+      typedef __attribute__((address_space(1))) const volatile u32x4_t gvec_t;
+      const u32x4_t v = *(gvec_t*)(src + 16 * i);
       if (v[1] == gen && v[3] == gen) {
         d[2 * i] = v[0];
         d[2 * i + 1] = v[2];
@@ -394,6 +397,7 @@ __global__ void __launch_bounds__(128) car_ll_resid_kernel(const float* __restri
     ll_store(dst, mine.x, mine.y, gen);
     ll_store(dst + 16, mine.z, mine.w, gen);
   }
+  asm volatile("" ::: "memory");  // the pushes are issued before any poll
   // 3. receive every peer's lines from my own region, sum in rank order
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   bool ok = true;
@@ -448,6 +452,7 @@ __global__ void __launch_bounds__(CAR_LL_GROUPS) car_ll_kernel(const uint8_t* __
       ll_store(dst, mine.x, mine.y, gen);
       ll_store(dst + 16, mine.z, mine.w, gen);
     }
+    asm volatile("" ::: "memory");  // the pushes are issued before any poll
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     bool ok = true;
     for (int r = 0; r < world; ++r) {
