@@ -277,7 +277,7 @@ def mw_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, plan=N
         return PendingSum(part, S)
     if out is None:
         out = torch.empty(M, N // 2 if mode == MODE_SILU else N, dtype=torch.bfloat16, device=x.device)
-    kernels().gemm_mw(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, cfg, stream_ptr())
+    kernels().gemm_mw(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), S, mode, cfg, stream_ptr())
     return out
 
 
