@@ -111,7 +111,7 @@ profile)
   bash bench/profile.sh "$o" "$@" ;;
 mw)  # gemm_mw: numerics, shape sweep, stall-free mixed-step engine tests, headline with / without chunks
   pyt mw_tests 300 tests/test_skinny_gpu.py -k mw
-  run mw_sweep 420 python -u bench/gemm_bench.py --mw-sweep --M 64 128 192 256 320 --shapes qkv o gate_up down
+  run mw_sweep 700 python -u bench/gemm_bench.py --mw-sweep --M 64 128 192 256 320 --shapes qkv o gate_up down
   pyt stall_free 300 tests/test_engine_gpu.py -k "stall_free or graph_decode or chunked or async"
   run c64_chunk128 200 $B --steps 20 --warmup 5 --prefill-chunk 128 "$@"
   run c64_chunk128_long 240 env XGS_STEP_LOG="$o/steps_chunk128.jsonl" $B --steps 600 --warmup 60 --prefill-chunk 128 "$@"

@@ -215,6 +215,197 @@ __global__ void __launch_bounds__(512, 1) gemm_mw_kernel(const uint16_t* __restr
   }
 }
 
+// Split-role rings (cfg >= 7). The single-ring kernel above issues x and W from every
+// wave, so vmcnt's in-order retirement ties x's lead to the weights' and the x
+// slots eat the LDS that deeper weight rings need -- at M = 192 it keeps ~56 KB in
+// flight per CU, and measured per-CU ingest (~42 GB/s) is exactly that over a
+// ~1.3 us loaded latency (profiles/r4_mw_sweep.md). vmcnt is PER WAVE: here waves
+// 0-3 issue only weight DMAs (DW-slot ring, DW-1 chunks ahead) and waves 4-7 only x
+// DMAs (DX slots, DX-1 ahead, L2-resident), so each role's counted wait sees its own
+// stream only, and the weight ring gets the LDS: e.g. 128 columns x DW = 6 keeps 80
+// KB of weights in flight. Every wave still computes its (wn, wm) tile.
+template <int WN, int NWT, int MTW, int DW, int DX, bool NT>
+__global__ void __launch_bounds__(512, 1) gemm_mw2_kernel(const uint16_t* __restrict__ x, int M, int K,
+                                                           const uint16_t* __restrict__ w, int N, int S,
+                                                           float* __restrict__ part, uint16_t* __restrict__ out,
+                                                           int mode) {
+  constexpr int WM = 8 / WN;
+  constexpr int KC = 64, RB = 128, RPI = 8;
+  constexpr int WCOLS = WN * 16 * NWT;
+  constexpr int XROWS = WM * 16 * MTW;
+  constexpr int WSLOT = WCOLS * RB;
+  constexpr int XSLOT = XROWS * RB;
+  constexpr int WI = WCOLS / RPI / 4;           // weight DMA instructions per W-wave per chunk
+  constexpr int XI = XROWS / RPI / 4;           // x DMA instructions per x-wave per chunk
+  static_assert(WN * WM == 8 && WI >= 1 && XI >= 1 && WCOLS % 32 == 0 && XROWS % 32 == 0, "bad gemm_mw2 geometry");
+  static_assert(DW >= 2 && DW <= 9 && DX >= 2 && DX <= 4, "ring depths");
+  static_assert(DW * WSLOT + DX * XSLOT <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[DW * WSLOT + DX * XSLOT];
+  uint8_t* const wring = smem;
+  uint8_t* const xring = smem + DW * WSLOT;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int wn = wid % WN, wm = wid / WN;
+  const bool wload = wid < 4;                   // DMA role: weights (waves 0-3) or x (4-7)
+  const int rw = wid & 3;                       // index within the role
+
+  const int nb = gridDim.x, bid = blockIdx.x;
+  const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7;
+  const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int ntiles = N / WCOLS;
+  const int s = v / ntiles, tile = v - s * ntiles;
+  const int nch_all = K / KC;
+  const int c_lo = s * nch_all / S, c_hi = (s + 1) * nch_all / S;
+  const int nch = c_hi - c_lo;
+  const int k0 = c_lo * KC;
+  const int n0 = tile * WCOLS;
+
+  const int dr = lane >> 3, dj = lane & 7;
+  constexpr int NI = WI > XI ? WI : XI;
+  const uint16_t* src[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    if (wload) {
+      const int row = 8 * (rw * WI + (i < WI ? i : 0)) + dr;
+      src[i] = w + static_cast<int64_t>(n0 + row) * K + k0 + 8 * (dj ^ dr);
+    } else {
+      const int row = 8 * (rw * XI + (i < XI ? i : 0)) + dr;
+      src[i] = x + static_cast<int64_t>(min(row, M - 1)) * K + k0 + 8 * (dj ^ dr);
+    }
+  }
+  auto issue_w = [&](int c) {
+    uint8_t* slot = wring + (c % DW) * WSLOT;
+    const int kk = c * KC;
+#pragma unroll
+    for (int i = 0; i < WI; ++i) {
+      if constexpr (NT) glds16_nt(src[i] + kk, slot + (rw * WI + i) * 1024);
+      else glds16(src[i] + kk, slot + (rw * WI + i) * 1024);
+    }
+  };
+  auto issue_x = [&](int c) {
+    uint8_t* slot = xring + (c % DX) * XSLOT;
+    const int kk = c * KC;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) glds16(src[i] + kk, slot + (rw * XI + i) * 1024);
+  };
+
+  f32x4_t acc[NWT][MTW];
+#pragma unroll
+  for (int nt = 0; nt < NWT; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt) acc[nt][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int wrow0 = wn * 16 * NWT, xrow0 = wm * 16 * MTW;
+  auto compute = [&](int c) {
+    const uint8_t* ws = wring + (c % DW) * WSLOT;
+    const uint8_t* xs = xring + (c % DX) * XSLOT;
+#pragma unroll
+    for (int t = 0; t < KC / 32; ++t) {
+      const int phys = (4 * t + g) ^ (li & 7);
+      uint4 a[NWT], b[MTW];
+#pragma unroll
+      for (int nt = 0; nt < NWT; ++nt)
+        a[nt] = *reinterpret_cast<const uint4*>(ws + (wrow0 + 16 * nt + li) * RB + phys * 16);
+#pragma unroll
+      for (int mt = 0; mt < MTW; ++mt)
+        b[mt] = *reinterpret_cast<const uint4*>(xs + (xrow0 + 16 * mt + li) * RB + phys * 16);
+#pragma unroll
+      for (int nt = 0; nt < NWT; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < MTW; ++mt) acc[nt][mt] = mfma16x16x32(as_frag(a[nt]), as_frag(b[mt]), acc[nt][mt]);
+    }
+  };
+
+  // each role leaves the chunks after c that it already issued in flight:
+  // rem = min(nch - 1 - c, ring depth - 2) groups of its own instructions
+  auto wait_role = [&](int c) {
+    if (wload) {
+      const int rem = min(nch - 1 - c, DW - 2);
+      if constexpr (DW >= 9) { if (rem == 7) { wait_vmcnt<7 * WI>(); return; } }
+      if constexpr (DW >= 8) { if (rem == 6) { wait_vmcnt<6 * WI>(); return; } }
+      if constexpr (DW >= 7) { if (rem == 5) { wait_vmcnt<5 * WI>(); return; } }
+      if constexpr (DW >= 6) { if (rem == 4) { wait_vmcnt<4 * WI>(); return; } }
+      if constexpr (DW >= 5) { if (rem == 3) { wait_vmcnt<3 * WI>(); return; } }
+      if constexpr (DW >= 4) { if (rem == 2) { wait_vmcnt<2 * WI>(); return; } }
+      if constexpr (DW >= 3) { if (rem == 1) { wait_vmcnt<WI>(); return; } }
+      wait_vmcnt<0>();
+    } else {
+      const int rem = min(nch - 1 - c, DX - 2);
+      if constexpr (DX >= 4) { if (rem == 2) { wait_vmcnt<2 * XI>(); return; } }
+      if constexpr (DX >= 3) { if (rem == 1) { wait_vmcnt<XI>(); return; } }
+      wait_vmcnt<0>();
+    }
+  };
+
+  if (wload) {
+#pragma unroll
+    for (int j = 0; j < DW - 1; ++j)
+      if (j < nch) issue_w(j);
+  } else {
+#pragma unroll
+    for (int j = 0; j < DX - 1; ++j)
+      if (j < nch) issue_x(j);
+  }
+  for (int c = 0; c < nch; ++c) {
+    wait_role(c);
+    raw_barrier();
+    // refill the slots chunk c - 1 used (every wave is past the barrier)
+    if (wload) {
+      if (c + DW - 1 < nch) issue_w(c + DW - 1);
+    } else {
+      if (c + DX - 1 < nch) issue_x(c + DX - 1);
+    }
+    compute(c);
+  }
+
+  if (mode == MW_PARTIAL) {
+    float* pp = part + static_cast<int64_t>(s) * M * N;
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt) {
+      const int m = xrow0 + 16 * mt + li;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < NWT; ++nt)
+        *reinterpret_cast<float4*>(pp + static_cast<int64_t>(m) * N + n0 + wrow0 + 16 * nt + 4 * g) =
+            make_float4(acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]);
+    }
+  } else if (mode == MW_BF16) {
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt) {
+      const int m = xrow0 + 16 * mt + li;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < NWT; ++nt) {
+        uint2 o;
+        o.x = pack2(acc[nt][mt][0], acc[nt][mt][1]);
+        o.y = pack2(acc[nt][mt][2], acc[nt][mt][3]);
+        *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * N + n0 + wrow0 + 16 * nt + 4 * g) = o;
+      }
+    }
+  } else if constexpr (NWT % 2 == 0) {
+    const int F = N / 2, f0 = (n0 + wrow0) / 2 + 4 * g;
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt) {
+      const int m = xrow0 + 16 * mt + li;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < NWT / 2; ++j) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gt = acc[2 * j][mt][r];
+          o[r] = gt / (1.f + __expf(-gt)) * acc[2 * j + 1][mt][r];
+        }
+        uint2 v2;
+        v2.x = pack2(o[0], o[1]);
+        v2.y = pack2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * F + f0 + 16 * j) = v2;
+      }
+    }
+  }
+}
+
 // cfg -> (WN, NWT, D, NT): 0 = 4 x 2 waves, 256 columns, ring 2, nt weights;
 // 1 = 4 x 2, 128 columns, ring 3, nt; 2 = 4 x 2, 128 columns, ring 2, nt; 3 / 4 = 0 / 1
 // with default-policy weight loads; 5 = 2 x 4 waves, 128 columns, ring 3, nt;
@@ -261,14 +452,65 @@ static int launch_mw(int mtw, dim3 grid, hipStream_t st, const uint16_t* x, int 
 #undef XGK_MW
 }
 
+template <int WN, int NWT, int MTW, int DW, int DX>
+constexpr bool mw2_fits() {
+  constexpr int WM = 8 / WN;
+  return DW * (WN * 16 * NWT * 128) + DX * (WM * 16 * MTW * 128) <= 160 * 1024;
+}
+
+template <int WN, int NWT, int DW, int DX>
+static int launch_mw2(int mtw, dim3 grid, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N,
+                      int S, float* part, uint16_t* out, int mode) {
+#define XGK_MW2(MTW)                                                                                              \
+  case MTW:                                                                                                       \
+    if constexpr (mw2_fits<WN, NWT, MTW, DW, DX>()) {                                                             \
+      hipLaunchKernelGGL((gemm_mw2_kernel<WN, NWT, MTW, DW, DX, true>), grid, dim3(512), 0, st, x, M, K, w, N, S, \
+                         part, out, mode);                                                                        \
+      return 0;                                                                                                   \
+    }                                                                                                             \
+    return 1;
+  switch (mtw) {
+    XGK_MW2(1)
+    XGK_MW2(2)
+    XGK_MW2(3)
+    XGK_MW2(4)
+    XGK_MW2(5)
+    XGK_MW2(6)
+    XGK_MW2(7)
+    XGK_MW2(8)
+    XGK_MW2(9)
+    XGK_MW2(10)
+    default: return 1;
+  }
+#undef XGK_MW2
+}
+
+// split-role configurations: (WN, NWT, DW, DX)
+struct Mw2Cfg { int wn, nwt, dw, dx; };
+static constexpr Mw2Cfg kMw2[] = {
+    {4, 2, 6, 2},   // 7: 128 columns, 5 weight chunks ahead
+    {2, 4, 6, 2},   // 8: same, 2 x 4 waves
+    {4, 2, 5, 3},   // 9: 128 columns, 4 ahead, x 2 ahead
+    {4, 4, 3, 2},   // 10: 256 columns, 2 ahead
+    {2, 8, 3, 2},   // 11: same, 2 x 4 waves
+    {4, 2, 8, 2},   // 12: 128 columns, 7 ahead (M <= 128)
+    {2, 4, 8, 2},   // 13: same, 2 x 4 waves
+    {4, 4, 4, 2},   // 14: 256 columns, 3 ahead (M <= 128)
+};
+constexpr int kMwCfgs = 7 + static_cast<int>(sizeof(kMw2) / sizeof(kMw2[0]));
+
+int mw_cfg_cols_any(int cfg) {
+  if (cfg < 7) return mw_cfg_cols(cfg);
+  return kMw2[cfg - 7].wn * 16 * kMw2[cfg - 7].nwt;
+}
+
 // x [M, K] bf16 row-major, w [N, K] bf16 row-major. mode MW_PARTIAL: part [S, M, N]
 // fp32; MW_BF16: out [M, N]; MW_SILU: out [M, N / 2] (S = 1). 0 = launched, 1 = a
-// shape / configuration this kernel does not take (M beyond the cfg's LDS budget:
-// M <= 256 everywhere, 320 on cfg 2).
+// shape / configuration this kernel does not take (M beyond the cfg's LDS budget).
 int gemm_mw(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
             int cfg, hipStream_t st) {
-  if (M < 1 || M > 320 || cfg < 0 || cfg > 6 || S < 1 || K % 64 || S > K / 64) return 1;
-  const int cols = mw_cfg_cols(cfg);
+  if (M < 1 || M > 320 || cfg < 0 || cfg >= kMwCfgs || S < 1 || K % 64 || S > K / 64) return 1;
+  const int cols = mw_cfg_cols_any(cfg);
   if (N % cols) return 1;
   if (mode == MW_PARTIAL) {
     if (part == nullptr) return 1;
@@ -277,10 +519,25 @@ int gemm_mw(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* pa
   } else {
     return 1;
   }
+  const dim3 grid((N / cols) * S);
+  if (cfg >= 7) {
+    const Mw2Cfg c = kMw2[cfg - 7];
+    const int rows_per = (8 / c.wn) * 16;
+    const int mtw = (M + rows_per - 1) / rows_per;
+    switch (cfg) {
+      case 7: return launch_mw2<4, 2, 6, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+      case 8: return launch_mw2<2, 4, 6, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+      case 9: return launch_mw2<4, 2, 5, 3>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+      case 10: return launch_mw2<4, 4, 3, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+      case 11: return launch_mw2<2, 8, 3, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+      case 12: return launch_mw2<4, 2, 8, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+      case 13: return launch_mw2<2, 4, 8, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+      default: return launch_mw2<4, 4, 4, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+    }
+  }
   int mtw;
   if (mw_cfg_wn(cfg) == 4) mtw = M <= 64 ? 2 : M <= 128 ? 4 : M <= 192 ? 6 : M <= 256 ? 8 : 10;
   else mtw = (M + 63) / 64;
-  const dim3 grid((N / cols) * S);
   switch (cfg) {
     case 0: return launch_mw<4, 4, 2, true>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
     case 1: return launch_mw<4, 2, 3, true>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);

@@ -100,6 +100,23 @@ def test_gemm_mw_waits_follow_the_ring(tmp_path):
     _no_spills(asm)
 
 
+def test_gemm_mw2_role_waits(tmp_path):
+    """Split-role rings: the weight waves' counted waits are multiples of their
+    per-chunk instruction count, the x waves' of theirs; both steady-state waits exist."""
+    asm, log = _compile("gemm_mw", tmp_path)
+    ks = _kernels(asm, "_ZN3xgk15gemm_mw2_kernel")
+    assert len(ks) >= 30, len(ks)
+    for name, body in ks.items():
+        WN, NWT, MTW, DW, DX, _nt = _targs(name)
+        WI = WN * 16 * NWT // 32
+        XI = (8 // WN) * 16 * MTW // 32
+        allowed = {k * WI for k in range(DW - 1)} | {k * XI for k in range(DX - 1)}
+        got = _vmcnts(body)
+        assert got <= allowed, (name, sorted(got), sorted(allowed))
+        assert (DW - 2) * WI in got and (DX - 2) * XI in got, (name, sorted(got))
+    _no_spills(asm)
+
+
 def test_gemm_m64g_waits_are_counted(tmp_path):
     asm, log = _compile("gemm_m64g", tmp_path)
     assert "reserved registers on the clobber list" not in log
