@@ -224,11 +224,22 @@ __global__ void __launch_bounds__(512, 1) gemm_mw_kernel(const uint16_t* __restr
 // DMAs (DX slots, DX-1 ahead, L2-resident), so each role's counted wait sees its own
 // stream only, and the weight ring gets the LDS: e.g. 128 columns x DW = 6 keeps 80
 // KB of weights in flight. Every wave still computes its (wn, wm) tile.
+// Input RMSNorm as an epilogue row scale (the fused decode layer's contract, see
+// gemm_m64g.hip M64Epi): x is the raw bf16 residual stream, the norm weight is folded
+// into W, and output row m is scaled by rsqrt(sum_j ss_in[j * ss_stride + m] / K + eps)
+// (ss_n partial sums of squares, added in order). ss_in == nullptr: no scale.
+struct MwEpi {
+  const float* ss_in;
+  int ss_n;
+  int ss_stride;
+  float eps;
+};
+
 template <int WN, int NWT, int MTW, int DW, int DX, bool NT>
 __global__ void __launch_bounds__(512, 1) gemm_mw2_kernel(const uint16_t* __restrict__ x, int M, int K,
                                                            const uint16_t* __restrict__ w, int N, int S,
                                                            float* __restrict__ part, uint16_t* __restrict__ out,
-                                                           int mode) {
+                                                           int mode, MwEpi epi) {
   constexpr int WM = 8 / WN;
   constexpr int KC = 64, RB = 128, RPI = 8;
   constexpr int WCOLS = WN * 16 * NWT;
@@ -338,6 +349,18 @@ __global__ void __launch_bounds__(512, 1) gemm_mw2_kernel(const uint16_t* __rest
     }
   };
 
+  // norm statistics of this lane's rows: lane group g sums j = g, g + 4, ... (loaded
+  // before the weight stream starts; older than every DMA, so the counted waits hold)
+  constexpr int SQ = 4;  // up to 4 * SQ = 16 partial sums per row
+  const bool has_ss = epi.ss_in != nullptr;
+  float ssv[MTW][SQ];
+  if (has_ss) {
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+      for (int q = 0; q < SQ; ++q)
+        ssv[mt][q] = epi.ss_in[min(g + 4 * q, epi.ss_n - 1) * epi.ss_stride + min(xrow0 + 16 * mt + li, M - 1)];
+  }
   if (wload) {
 #pragma unroll
     for (int j = 0; j < DW - 1; ++j)
@@ -357,6 +380,23 @@ __global__ void __launch_bounds__(512, 1) gemm_mw2_kernel(const uint16_t* __rest
       if (c + DX - 1 < nch) issue_x(c + DX - 1);
     }
     compute(c);
+  }
+
+  if (has_ss) {  // input RMSNorm as a row scale of the (linear) output
+    const float inv_k = 1.f / static_cast<float>(K);
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < SQ; ++q) v += g + 4 * q < epi.ss_n ? ssv[mt][q] : 0.f;
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const float sc = rsqrtf(v * inv_k + epi.eps);
+#pragma unroll
+      for (int nt = 0; nt < NWT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[nt][mt][r] *= sc;
+    }
   }
 
   if (mode == MW_PARTIAL) {
@@ -460,12 +500,12 @@ constexpr bool mw2_fits() {
 
 template <int WN, int NWT, int DW, int DX>
 static int launch_mw2(int mtw, dim3 grid, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N,
-                      int S, float* part, uint16_t* out, int mode) {
+                      int S, float* part, uint16_t* out, int mode, const MwEpi& epi) {
 #define XGK_MW2(MTW)                                                                                              \
   case MTW:                                                                                                       \
     if constexpr (mw2_fits<WN, NWT, MTW, DW, DX>()) {                                                             \
       hipLaunchKernelGGL((gemm_mw2_kernel<WN, NWT, MTW, DW, DX, true>), grid, dim3(512), 0, st, x, M, K, w, N, S, \
-                         part, out, mode);                                                                        \
+                         part, out, mode, epi);                                                                   \
       return 0;                                                                                                   \
     }                                                                                                             \
     return 1;
@@ -507,9 +547,10 @@ int mw_cfg_cols_any(int cfg) {
 // x [M, K] bf16 row-major, w [N, K] bf16 row-major. mode MW_PARTIAL: part [S, M, N]
 // fp32; MW_BF16: out [M, N]; MW_SILU: out [M, N / 2] (S = 1). 0 = launched, 1 = a
 // shape / configuration this kernel does not take (M beyond the cfg's LDS budget).
-int gemm_mw(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
-            int cfg, hipStream_t st) {
+static int gemm_mw_impl(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S,
+                        int mode, int cfg, const MwEpi& epi, hipStream_t st) {
   if (M < 1 || M > 320 || cfg < 0 || cfg >= kMwCfgs || S < 1 || K % 64 || S > K / 64) return 1;
+  if (epi.ss_in != nullptr && (cfg < 7 || epi.ss_n < 1 || epi.ss_n > 16 || epi.ss_stride < M)) return 1;
   const int cols = mw_cfg_cols_any(cfg);
   if (N % cols) return 1;
   if (mode == MW_PARTIAL) {
@@ -525,14 +566,14 @@ int gemm_mw(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* pa
     const int rows_per = (8 / c.wn) * 16;
     const int mtw = (M + rows_per - 1) / rows_per;
     switch (cfg) {
-      case 7: return launch_mw2<4, 2, 6, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
-      case 8: return launch_mw2<2, 4, 6, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
-      case 9: return launch_mw2<4, 2, 5, 3>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
-      case 10: return launch_mw2<4, 4, 3, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
-      case 11: return launch_mw2<2, 8, 3, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
-      case 12: return launch_mw2<4, 2, 8, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
-      case 13: return launch_mw2<2, 4, 8, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
-      default: return launch_mw2<4, 4, 4, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+      case 7: return launch_mw2<4, 2, 6, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode, epi);
+      case 8: return launch_mw2<2, 4, 6, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode, epi);
+      case 9: return launch_mw2<4, 2, 5, 3>(mtw, grid, st, x, M, K, w, N, S, part, out, mode, epi);
+      case 10: return launch_mw2<4, 4, 3, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode, epi);
+      case 11: return launch_mw2<2, 8, 3, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode, epi);
+      case 12: return launch_mw2<4, 2, 8, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode, epi);
+      case 13: return launch_mw2<2, 4, 8, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode, epi);
+      default: return launch_mw2<4, 4, 4, 2>(mtw, grid, st, x, M, K, w, N, S, part, out, mode, epi);
     }
   }
   int mtw;
@@ -547,6 +588,17 @@ int gemm_mw(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* pa
     case 5: return launch_mw<2, 4, 3, true>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
     default: return launch_mw<2, 8, 2, true>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
   }
+}
+
+int gemm_mw(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
+            int cfg, hipStream_t st) {
+  return gemm_mw_impl(x, M, K, w, N, part, out, S, mode, cfg, MwEpi{nullptr, 0, 0, 0.f}, st);
+}
+
+// with the input RMSNorm as a row scale (split-role configurations only; ss_n <= 16)
+int gemm_mw_ss(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
+               int cfg, const float* ss_in, int ss_n, int ss_stride, float eps, hipStream_t st) {
+  return gemm_mw_impl(x, M, K, w, N, part, out, S, mode, cfg, MwEpi{ss_in, ss_n, ss_stride, eps}, st);
 }
 
 }  // namespace xgk

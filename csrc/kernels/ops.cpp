@@ -24,6 +24,8 @@ int gemm_m64g(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*
 int gemm_m64g_ex(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, const float*,
                  int, int, float, uint16_t*, float*, int*, hipStream_t);
 int gemm_mw(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, hipStream_t);
+int gemm_mw_ss(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, const float*, int,
+               int, float, hipStream_t);
 void add_partials_resid(const float*, int, int, uint16_t*, float*, int, hipStream_t, uint64_t);
 void row_sumsq(const uint16_t*, int, int, float*, hipStream_t);
 void embed_gather(const int32_t*, int, const uint16_t*, int, int, uint16_t*, float*, hipStream_t);
@@ -250,6 +252,12 @@ PYBIND11_MODULE(_kernels, m) {
     check(xgk::gemm_mw(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode, cfg,
                        S(st)),
           "gemm_mw");
+  });
+  m.def("gemm_mw_ss", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
+                         int mode, int cfg, uintptr_t ss_in, int ss_n, int ss_stride, float eps, uintptr_t st) {
+    check(xgk::gemm_mw_ss(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode, cfg,
+                          P<const float>(ss_in), ss_n, ss_stride, eps, S(st)),
+          "gemm_mw_ss");
   });
   // ---- fused decode layer (gemm_m64g.hip epilogues, decode_attention.hip FQ prologue)
   m.def("gemm_m64g_ex", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,

@@ -111,7 +111,7 @@ def test_gemm_mw2_role_waits(tmp_path):
         WI = WN * 16 * NWT // 32
         XI = (8 // WN) * 16 * MTW // 32
         allowed = {k * WI for k in range(DW - 1)} | {k * XI for k in range(DX - 1)}
-        got = _vmcnts(body)
+        got = _vmcnts(_pipeline(body, through_barrier=True))  # the epilogue's RMS-statistics waits lie outside
         assert got <= allowed, (name, sorted(got), sorted(allowed))
         assert (DW - 2) * WI in got and (DX - 2) * XI in got, (name, sorted(got))
     _no_spills(asm)

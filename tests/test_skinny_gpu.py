@@ -271,3 +271,31 @@ def test_gemm_m64g_uneven_splits(M, N, K, nw, S, cfg):
     pend = m64_linear(x, w, MODE_PARTIAL, split_k=S, nw=nw, cfg=cfg)
     assert pend.part.shape == (S, M, N)
     assert rel_err(pend.part.sum(0), x.float() @ w.float().t()) < 1e-5
+
+
+@pytest.mark.parametrize("M", [1, 64, 192])
+@pytest.mark.parametrize("cfg,ss_n", [(7, 4), (8, 16), (10, 1), (12, 4)])
+def test_gemm_mw_norm_row_scale(M, cfg, ss_n):
+    """gemm_mw's input-RMSNorm row scale (split-role configurations): the raw residual
+    rows times (W diag(g))^T, scaled by rsqrt(sum of ss_n partial squares / K + eps),
+    equals rmsnorm(x, g) @ W^T -- partial and SiLU epilogues."""
+    from xgserve.ops.linear import MW_CFGS, RowStats, mw_norm_linear
+    if M > {12: 128}.get(cfg, 256):
+        pytest.skip("x tile beyond the LDS budget")
+    H, N = 1024, 2 * MW_CFGS[cfg][0]
+    x = rnd(M, H)
+    xf = x.float()
+    parts = (xf * xf).view(M, ss_n, H // ss_n).sum(-1).t().contiguous()  # [ss_n, M]
+    stride = M + 3
+    ss = torch.zeros(ss_n, stride, device=DEV)
+    ss[:, :M] = parts
+    st = RowStats(ss.view(-1), ss_n, stride)
+    w = rnd(N, H, scale=0.05)
+    xn = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)
+    pend = mw_norm_linear(x, w, MODE_PARTIAL, st, 1e-5, plan=(3, cfg))
+    assert rel_err(pend.part.sum(0), xn @ w.float().t()) < 1e-4
+    g, u = rnd(N // 2, H, scale=0.05), rnd(N // 2, H, scale=0.05)
+    wi = interleave_gate_up(g, u).contiguous()
+    got = mw_norm_linear(x, wi, MODE_SILU, st, 1e-5, plan=(1, cfg))
+    ref = torch.nn.functional.silu(xn @ g.float().t()) * (xn @ u.float().t())
+    assert rel_err(got, ref) < 1e-2

@@ -285,6 +285,29 @@ def mw_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, plan=N
     return out
 
 
+def mw_norm_linear(x: torch.Tensor, w: torch.Tensor, mode: int, stats: "RowStats", eps: float, plan=None,
+                   out: Optional[torch.Tensor] = None):
+    """gemm_mw (split-role configurations) on the raw residual stream x with its RMSNorm
+    as a per-row epilogue scale rsqrt(sum_sq / K + eps) (norm weight folded into w):
+    PendingSum (MODE_PARTIAL) or bf16 silu(gate) * up (MODE_SILU)."""
+    M, K = x.shape
+    N = w.shape[0]
+    p = plan or mw_plan(M, N, K, mode)
+    if p is None or p[1] < 7 or stats.n > 16:
+        raise ValueError(f"gemm_mw_ss: unsupported M={M} N={N} K={K} plan={p} stats={stats.n}")
+    S, cfg = p
+    k = kernels()
+    st = (stats.ss.data_ptr(), stats.n, stats.stride, float(eps))
+    if mode == MODE_PARTIAL:
+        part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+        k.gemm_mw_ss(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, cfg, *st, stream_ptr())
+        return PendingSum(part, S)
+    if out is None:
+        out = torch.empty(M, N // 2 if mode == MODE_SILU else N, dtype=torch.bfloat16, device=x.device)
+    k.gemm_mw_ss(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), S, mode, cfg, *st, stream_ptr())
+    return out
+
+
 def _apply_mw_overrides(spec: str) -> None:
     """XGS_MW_PLANS="NxKxMODE@BUCKET=S,cfg;..." replaces gemm_mw plans (A/B sweeps)."""
     for item in filter(None, (t.strip() for t in spec.split(";"))):
