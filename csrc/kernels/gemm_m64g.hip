@@ -88,56 +88,76 @@ __device__ __forceinline__ bool agent_ticket(int* cnt, int last_value, int* flag
 // Reduction of one column tile [tile*COLS, +COLS) x [0, M): the S fp32 slabs + the
 // bf16 residual -> new residual and the tile's per-row sum of squares. The threads
 // of one row are C4 = COLS/4 consecutive lanes of one wave (row sum = xor butterfly
-// over them); every lane runs every butterfly.
+// over them); every lane runs every butterfly. IB row-chunk passes share one batch
+// of loads (IB x 4 slab reads + IB residual reads in flight before the first add):
+// the slabs were written by other XCDs, so every read is a MALL round trip and a
+// pass-by-pass loop paid one per NTHR x 16 B (~1 us per 16 KB at M = 64).
 template <int COLS, int NTHR>
 __device__ __forceinline__ void m64g_resid_reduce(const float* __restrict__ part, int S, int M, int N, int tile,
                                                   const M64Epi& epi, int r0 = 0, int r1 = -1) {
   constexpr int C4 = COLS / 4;
+  constexpr int IB = 4;
   static_assert(64 % C4 == 0 && NTHR % C4 == 0, "row groups must not straddle waves");
   const int tid = threadIdx.x;
   const int n0 = tile * COLS;
   const int64_t slab = static_cast<int64_t>(M) * N;
   if (r1 < 0) r1 = M;
   const int nr = r1 - r0;
-  for (int base = 0; base < nr * C4; base += NTHR) {
-    const int idx = base + tid;
-    const bool ok = idx < nr * C4;
-    const int m = r0 + (ok ? idx / C4 : 0), c = idx % C4;
-    const int64_t off = static_cast<int64_t>(m) * N + n0 + 4 * c;
-    float y[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int base = 0; base < nr * C4; base += IB * NTHR) {
+    bool ok[IB];
+    int m[IB], c[IB];
+    int64_t off[IB];
+    float y[IB][4];
+    uint2 rv[IB];
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {  // clamped unconditional addresses, masked after
+      const int idx = base + i * NTHR + tid;
+      ok[i] = idx < nr * C4;
+      m[i] = r0 + (ok[i] ? idx / C4 : 0);
+      c[i] = idx % C4;
+      off[i] = static_cast<int64_t>(m[i]) * N + n0 + 4 * c[i];
+      rv[i] = *reinterpret_cast<const uint2*>(epi.resid + off[i]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[i][j] = 0.f;
+    }
     for (int s0 = 0; s0 < S; s0 += 4) {
-      float4 v[4];
+      float4 v[IB][4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)  // clamped unconditional loads, masked after (no branch per load)
-        v[i] = *reinterpret_cast<const float4*>(part + min(s0 + i, S - 1) * slab + off);
+      for (int i = 0; i < IB; ++i)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float k = s0 + i < S ? 1.f : 0.f;
-        y[0] += k * v[i].x;
-        y[1] += k * v[i].y;
-        y[2] += k * v[i].z;
-        y[3] += k * v[i].w;
+        for (int j = 0; j < 4; ++j) v[i][j] = *reinterpret_cast<const float4*>(part + min(s0 + j, S - 1) * slab + off[i]);
+#pragma unroll
+      for (int i = 0; i < IB; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float k = s0 + j < S ? 1.f : 0.f;
+          y[i][0] += k * v[i][j].x;
+          y[i][1] += k * v[i][j].y;
+          y[i][2] += k * v[i][j].z;
+          y[i][3] += k * v[i][j].w;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      float sq = 0.f;
+      if (ok[i]) {
+        y[i][0] += __uint_as_float(rv[i].x << 16);
+        y[i][1] += __uint_as_float(rv[i].x & 0xFFFF0000u);
+        y[i][2] += __uint_as_float(rv[i].y << 16);
+        y[i][3] += __uint_as_float(rv[i].y & 0xFFFF0000u);
+        uint2 o;
+        o.x = pack2(y[i][0], y[i][1]);
+        o.y = pack2(y[i][2], y[i][3]);
+        *reinterpret_cast<uint2*>(epi.resid + off[i]) = o;
+        // the residual stream is bf16: the norm statistics use the rounded values
+        const float a0 = __uint_as_float(o.x << 16), a1 = __uint_as_float(o.x & 0xFFFF0000u);
+        const float a2 = __uint_as_float(o.y << 16), a3 = __uint_as_float(o.y & 0xFFFF0000u);
+        sq = a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
       }
-    }
-    float sq = 0.f;
-    if (ok) {
-      const uint2 r = *reinterpret_cast<const uint2*>(epi.resid + off);
-      y[0] += __uint_as_float(r.x << 16);
-      y[1] += __uint_as_float(r.x & 0xFFFF0000u);
-      y[2] += __uint_as_float(r.y << 16);
-      y[3] += __uint_as_float(r.y & 0xFFFF0000u);
-      uint2 o;
-      o.x = pack2(y[0], y[1]);
-      o.y = pack2(y[2], y[3]);
-      *reinterpret_cast<uint2*>(epi.resid + off) = o;
-      // the residual stream is bf16: the norm statistics use the rounded values
-      const float r0 = __uint_as_float(o.x << 16), r1 = __uint_as_float(o.x & 0xFFFF0000u);
-      const float r2 = __uint_as_float(o.y << 16), r3 = __uint_as_float(o.y & 0xFFFF0000u);
-      sq = r0 * r0 + r1 * r1 + r2 * r2 + r3 * r3;
-    }
 #pragma unroll
-    for (int o = C4 / 2; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
-    if (ok && c == 0) epi.ss_out[tile * M + m] = sq;
+      for (int o = C4 / 2; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+      if (ok[i] && c[i] == 0) epi.ss_out[tile * M + m[i]] = sq;
+    }
   }
 }
 

@@ -329,8 +329,9 @@ MODE_RESID = 3
 # column tile in-launch while its split-K slab (S x M x columns fp32) is at most
 # this many bytes -- the tile's last arriver reads it serially (~1 us per 16 KB,
 # cdna_hip_programming.md §5); larger slabs (M ~ 64) go through the wide
-# add_partials_resid kernel instead.
-RESID_INLAUNCH_MAX_BYTES = 32 << 10
+# add_partials_resid kernel instead. XGS_RESID_INLAUNCH_KB overrides (A/B of the
+# batched last-arriver reduce at M = 64, whose slabs are 64-256 KB).
+RESID_INLAUNCH_MAX_BYTES = int(__import__("os").environ.get("XGS_RESID_INLAUNCH_KB", "32")) << 10
 
 
 @dataclass
