@@ -224,10 +224,16 @@ def main():
 
     # population fill (untimed setup, before the W warmup steps): prefill the initial
     # population until every initial request has produced its first token
+    # (stall-free batching is lifted while the initial population prefills: admitting
+    # 64 prompts one chunk per step would leave the timed window in a transient --
+    # finished requests' replacements queued behind the fill -- instead of the
+    # steady state of one prompt chunk per step)
     fill_steps = 0
+    eng.set_decode_prefill_cap(0)
     while any(r not in first_tok for r in initial) and fill_steps < 10_000:
         run_step()
         fill_steps += 1
+    eng.set_decode_prefill_cap(None)
     for _ in range(a.warmup):
         run_step()
     sync()

@@ -277,6 +277,7 @@ PYBIND11_MODULE(_runtime, m) {
       .def("num_evictable_blocks", &StepScheduler::num_evictable_blocks)
       .def("total_preemptions", &StepScheduler::total_preemptions)
       .def("set_limits", &StepScheduler::set_limits)
+      .def("set_decode_prefill", &StepScheduler::set_decode_prefill)
       .def("clear_prefix_cache", &StepScheduler::clear_prefix_cache)
       .def("cached_prefix", &StepScheduler::cached_prefix)
       .def("install_prefix", &StepScheduler::install_prefix)

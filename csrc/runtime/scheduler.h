@@ -169,6 +169,12 @@ class StepScheduler {
   BlockAllocator& allocator() { return alloc_; }
   int64_t total_preemptions() const { return total_preemptions_; }
   void set_limits(int max_num_seqs, int max_num_batched_tokens);
+  // stall-free batching limits of decoding steps (SchedulerConfig::decode_prefill_*);
+  // 0 lifts them
+  void set_decode_prefill(int cap, int seqs) {
+    cfg_.decode_prefill_cap = std::max(0, cap);
+    cfg_.decode_prefill_seqs = std::max(0, seqs);
+  }
   void clear_prefix_cache() { cache_.clear(); }
   // KV export/import (cache entry serialisation, design.md:400-401):
   // pages currently caching the page-aligned prefix of tokens (no stats, no incref)

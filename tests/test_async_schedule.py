@@ -332,3 +332,25 @@ def test_stall_free_one_chunk_per_decode_step():
         nd, ns = int(plan["num_decodes"]), int(plan["num_seqs"])
         shapes.append((nd, ns - nd, int(plan["num_tokens"]) - nd))
     assert shapes == [(1, 1, 128), (1, 1, 72), (2, 1, 60), (3, 0, 0)], shapes
+
+
+def test_decode_prefill_cap_can_be_lifted():
+    """set_decode_prefill(0, 0) lifts the stall-free limits at run time (bench.py's
+    untimed population fill); restoring them chunks the next prompt again."""
+    c = R.SchedulerConfig()
+    c.block_size, c.num_blocks, c.max_num_seqs = 16, 1024, 64
+    c.max_num_batched_tokens, c.max_model_len, c.enable_prefix_cache = 8192, 2048, False
+    c.decode_prefill_cap, c.decode_prefill_seqs = 128, 1
+    s = R.StepScheduler(c)
+    assert s.add(1, list(range(10, 30)), 50, 1, True, False, [], 0)
+    plan = _step(s, s.schedule())
+    s.set_decode_prefill(0, 0)
+    assert s.add(2, list(range(100, 300)), 50, 1, True, False, [], 0)
+    assert s.add(3, list(range(400, 460)), 50, 1, True, False, [], 0)
+    plan = _step(s, plan)
+    assert (int(plan["num_decodes"]), int(plan["num_tokens"])) == (1, 1 + 200 + 60)
+    s.set_decode_prefill(128, 1)
+    assert s.add(4, list(range(500, 800)), 50, 1, True, False, [], 0)
+    plan = _step(s, plan)
+    plan = _step(s, plan)
+    assert int(plan["num_tokens"]) - int(plan["num_decodes"]) <= 128

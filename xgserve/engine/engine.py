@@ -788,6 +788,15 @@ class LLMEngine:
                 self.runner.kv.index_copy_(2, idx, src)
         return len(blocks) - before
 
+    def set_decode_prefill_cap(self, cap: Optional[int] = None) -> None:
+        """Stall-free batching limit of decoding steps: at most `cap` prompt tokens of
+        one prompt per step that also decodes; 0 lifts it (whole prompts, as many as
+        the token budget takes); None restores the configured value. The mixed-step
+        graphs captured for the configured cap stay valid for any smaller one."""
+        cap = self.cfg.decode_prefill_cap if cap is None else max(0, min(int(cap), self.cfg.decode_prefill_cap or 1 << 30))
+        with self._lock:
+            self.sched.set_decode_prefill(cap, 1 if cap > 0 else 0)
+
     def set_limits(self, max_num_seqs: int, max_num_batched_tokens: int):
         """Runtime batch limits (degradation / hot reload), clamped to the sizes the
         runner's buffers and graphs were built for."""
