@@ -44,10 +44,12 @@ def main():
         print(f"| {shape} | {M} | {lib['us'] if lib else '-'} | S={S} cfg={cfg} | {best['us']} | {best['TB/s']} | "
               f"{best['TF/s']} | {lib['us'] / best['us']:.2f}x | {m64['us'] if m64 else '-'} |" if lib else
               f"| {shape} | {M} | - | S={S} cfg={cfg} | {best['us']} | {best['TB/s']} | {best['TF/s']} | - | - |")
-        if shape in SHAPES and M > 64:
+        if shape in SHAPES and (M > 64 or shape == "lm_head"):
             n, k, mode = SHAPES[shape]
             bucket = 128 if M <= 128 else 192 if M <= 192 else 256 if M <= 256 else 320
-            tuned[(n, k, mode)][bucket] = (S, cfg)
+            if shape == "lm_head" and lib and best["us"] >= lib["us"]:
+                continue  # the LM head keeps hipBLASLt unless gemm_mw wins
+            tuned[(n, k, mode)].setdefault(bucket, (S, cfg))  # ascending M: a bucket's smallest M decides
     print()
     print("_MW_TUNED = {")
     for key, v in tuned.items():

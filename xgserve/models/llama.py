@@ -35,7 +35,7 @@ from ..parallel import comm
 from ..parallel.state import get_state
 from ..ops import linear as linear_mod
 from ..ops.linear import (MODE_PARTIAL, MODE_SILU, MW_MAX_M, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace, RowStats,
-                          m64_linear, m64_norm_linear, m64_plan, m64_resid_linear, mw_linear, mw_plan, pick_split,
+                          lm_head_linear, m64_linear, m64_norm_linear, m64_plan, m64_resid_linear, mw_linear, mw_plan, pick_split,
                           quantize_fp8, skinny_linear, splitk_linear, splitk_prefill_ok, w8_linear, w8_plan)
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
 from .config import ModelConfig
@@ -644,7 +644,7 @@ class LlamaForCausalLM(nn.Module):
 
     def compute_logits(self, h: torch.Tensor) -> torch.Tensor:
         w = self.embed if self.lm_head is None else self.lm_head
-        logits = F.linear(h, w)
+        logits = lm_head_linear(h, w)
         if self.tp > 1:
             logits = comm.tp_all_gather_lastdim(logits)
         return logits[:, :self.cfg.vocab_size]

@@ -285,6 +285,17 @@ def mw_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, plan=N
     return out
 
 
+def lm_head_linear(h: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """bf16 logits h . w^T for the LM head: gemm_mw where the sweep measured a plan for
+    this row bucket (_MW_TUNED, mode bf16), else hipBLASLt."""
+    M, K = h.shape
+    N = w.shape[0]
+    if (h.is_cuda and 1 <= M <= MW_MAX_M and h.is_contiguous() and w.is_contiguous()
+            and _mw_bucket(M) in _MW_TUNED.get((N, K, MODE_BF16), {})):
+        return mw_linear(h, w, MODE_BF16)
+    return torch.nn.functional.linear(h, w)
+
+
 def mw_norm_linear(x: torch.Tensor, w: torch.Tensor, mode: int, stats: "RowStats", eps: float, plan=None,
                    out: Optional[torch.Tensor] = None):
     """gemm_mw (split-role configurations) on the raw residual stream x with its RMSNorm
