@@ -178,7 +178,7 @@ def test_gemm_mw_partial_every_cfg(M, cfg):
         assert rel_err(pend.part.sum(0), ref) < 1e-5, (S,)
 
 
-@pytest.mark.parametrize("M", [65, 128, 192, 256, 320])
+@pytest.mark.parametrize("M", [65, 128, 192, 256, 257, 320])
 @pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 4096), (4096, 14336)])
 def test_gemm_mw_llama_shapes(M, N, K):
     from xgserve.ops.linear import mw_linear
@@ -189,8 +189,8 @@ def test_gemm_mw_llama_shapes(M, N, K):
     assert rel_err(pend.materialize(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("M", [65, 192, 256, 320])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 5, 6, 7, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("M", [65, 128, 192, 257, 320])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
 def test_gemm_mw_silu_and_bf16(M, cfg):
     from xgserve.ops.linear import MW_CFGS, mw_linear
     if M > {2: 320, 9: 192, 12: 128, 13: 128, 14: 128}.get(cfg, 256):
