@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--splits", type=int, nargs="+", default=[1, 2])
     ap.add_argument("--iters", type=int, default=70)
     ap.add_argument("--bs", type=int, default=16)
+    ap.add_argument("--depth", type=int, nargs="+", default=[2])
     a = ap.parse_args()
     dev, Hq, Hkv, D, bs = "cuda", 32, 8, 128, a.bs
     B = a.B
@@ -61,13 +62,14 @@ def main():
     for kc, vc, bt in caches:
         slots.append((bt.gather(1, (pos // bs).long().view(B, 1)).view(B) * bs + pos % bs).int())
 
-    def run(i, S):
+    def run(i, S, dp):
         kc, vc, bt = caches[i % len(caches)]
-        ops.decode_attention_fused(pend, pos, slots[i % len(caches)], cs, kc, vc, bt, lens, Hq, sc, S, ws, out=out)
+        ops.decode_attention_fused(pend, pos, slots[i % len(caches)], cs, kc, vc, bt, lens, Hq, sc, S, ws, out=out,
+                                   depth=dp)
 
-    for S in a.splits:
-        for mode in ("warm", "cold"):
-            f = (lambda i: run(0, S)) if mode == "warm" else (lambda i: run(i, S))
+    for S, dp, mode in [(S, dp, m) for S in a.splits for dp in a.depth for m in ("warm", "cold")]:
+        if True:
+            f = (lambda i: run(0, S, dp)) if mode == "warm" else (lambda i: run(i, S, dp))
             for i in range(2 * len(caches)):
                 f(i)
             torch.cuda.synchronize()
@@ -79,7 +81,7 @@ def main():
             torch.cuda.synchronize()
             us = s.elapsed_time(e) / a.iters * 1000.0
             print(json.dumps({"op": "decode_attention_fq", "cache": mode, "B": B, "L": a.L, "stagger": a.stagger, "bs": bs,
-                              "splits": S, "us": round(us, 2), "TB/s": round(nbytes / us / 1e6, 3)}), flush=True)
+                              "splits": S, "depth": dp, "us": round(us, 2), "TB/s": round(nbytes / us / 1e6, 3)}), flush=True)
 
 
 if __name__ == "__main__":

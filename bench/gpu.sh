@@ -19,7 +19,7 @@
 #   m64      LM head on gemm_mw, deep-ring / uneven-split gemm_m64g tests + sweeps
 #   ar       custom all-reduce push vs pull: tests + per-call latency (bench/ar_bench.py)
 #   r4b/r4c  round-4 passes: AR + TP + prefetch A/B; Mixtral + profiles
-#   r4d      in-launch residual reduce A/B at 64 rows (step logs)
+#   r4d      in-launch residual reduce + decode-attention depth A/Bs at 64 rows (step logs)
 # Each GPU step has its own time limit; the first failure ends the suite.
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -136,10 +136,14 @@ r4c)  # round 4: Mixtral with / without prompt chunks, profiles of the chunked h
   run mixtral_c64 300 $B --model mixtral-8x7b --steps 120 --warmup 20
   bash bench/profile.sh "$o/prof_chunk128" --prefill-chunk 128
   bash bench/profile.sh "$o/prof_mixtral_c1" --model mixtral-8x7b --concurrency 1 ;;
-r4d)  # round 4: batched in-launch residual reduce at M = 64 (GG_RESID) vs add_partials_resid
+r4d)  # round 4: batched in-launch residual reduce at M = 64 (GG_RESID) vs add_partials_resid;
+      # decode attention with 2 / 3 register tiles in flight per wave (cold cache)
   pyt fused_tests 400 tests/test_fused_decode_gpu.py
-  for kb in 32 1024; do
-    run "steplog_kb$kb" 240 env XGS_RESID_INLAUNCH_KB=$kb XGS_STEP_LOG="$o/steps_kb$kb.jsonl" $B --steps 400 --warmup 40 "$@"
+  run attn_cold 200 python -u bench/decode_cold.py --L 768 --splits 1 --depth 2 3
+  run attn_cold_2k 200 python -u bench/decode_cold.py --L 2048 --caches 3 --splits 1 --depth 2 3
+  for v in "XGS_RESID_INLAUNCH_KB=32" "XGS_RESID_INLAUNCH_KB=1024" "XGS_DECODE_DEPTH=3"; do
+    n=$(echo "$v" | tr -c 'A-Za-z0-9_=\n' '_')
+    run "steplog_$n" 240 env $v XGS_STEP_LOG="$o/steps_$n.jsonl" $B --steps 400 --warmup 40 "$@"
   done ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py

@@ -189,7 +189,7 @@ __device__ __forceinline__ float combine_splits(const float* __restrict__ lse, c
 // (Measured and removed, A/B records in profiles/: an in-launch split combine by the
 // last-arriving split, r1_inlaunch_combine_ab.md; O-weight prefetch workgroups inside
 // this launch, r1_attn_prefetch_ab.md; 8 waves per workgroup, r1_decode_waves_c1.md.)
-template <int D, int G, bool FQ, bool KL = false>
+template <int D, int G, bool FQ, bool KL = false, int NB = 2>
 __global__ void __launch_bounds__(256) decode_attn_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ seq_lens,
@@ -214,10 +214,10 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 
   const int32_t* bt = block_tables + static_cast<int64_t>(b) * bt_stride;
   const int64_t head_stride = static_cast<int64_t>(bs) * D;
-  // two register tiles per wave (K fragments + V rows): tile t+W and t+2W are in
+  // NB register tiles per wave (K fragments + V rows): tiles t+W .. t+NB*W are in
   // flight while tile t is processed (one tile of lookahead left HBM idle between
   // a wave's tiles at 64 concurrent sequences)
-  uint4 kfA[C::KK], vrA[C::VLD], kfB[C::KK], vrB[C::VLD];
+  uint4 kf[NB][C::KK], vr[NB][C::VLD];
   auto load_tile = [&](int t, uint4 (&kf)[C::KK], uint4 (&vr)[C::VLD]) {
     const int key0 = t * 16;
     const int page = bt[key0 / bs];
@@ -241,14 +241,17 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     }
   };
   const int t0 = t_begin + wid;
-  // FQ: the first two tiles of each wave are requested BEFORE the prologue (their
+  // FQ: the first NB tiles of each wave are requested BEFORE the prologue (their
   // bytes do not depend on q), so the K/V latency overlaps the QKV-partial reads --
   // except the tile holding the key the prologue appends (the last one), which is
   // loaded after the prologue's barrier as before
-  const bool preA = FQ && t0 < t_end && t0 != ntiles - 1;
-  const bool preB = FQ && t0 + C::WAVES < t_end && t0 + C::WAVES != ntiles - 1;
-  if (preA) load_tile(t0, kfA, vrA);
-  if (preB) load_tile(t0 + C::WAVES, kfB, vrB);
+  bool pre[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int tj = t0 + j * C::WAVES;
+    pre[j] = FQ && tj < t_end && tj != ntiles - 1;
+    if (pre[j]) load_tile(tj, kf[j], vr[j]);
+  }
   if constexpr (FQ) {
     if (L > 0) decode_qkv_prologue<D, G>(fq, b, kvh, Hq, Hkv, bs, split == (ntiles - 1) / tps, q_lds);
     __syncthreads();
@@ -275,27 +278,27 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   uint16_t* my_v = v_lds[wid];
   uint16_t* my_k = k_lds[KL ? wid : 0];
 
-  auto process = [&](int t, uint4 (&kf)[C::KK], uint4 (&vr)[C::VLD]) {
+  auto process = [&](int t, uint4 (&kfb)[C::KK], uint4 (&vrb)[C::VLD]) {
     uint4 kcur[C::KK];
     if constexpr (KL) {  // stage K rows, chunk ch of row r at granule ch ^ r (r < 16)
 #pragma unroll
       for (int i = 0; i < C::KK; ++i) {
         const int c = lane + 64 * i;
         const int row = c / C::NCH, ch = c % C::NCH;
-        st16(my_k + row * D + (ch ^ row) * 8, kf[i]);
+        st16(my_k + row * D + (ch ^ row) * 8, kfb[i]);
       }
     } else {
 #pragma unroll
-      for (int kk = 0; kk < C::KK; ++kk) kcur[kk] = kf[kk];
+      for (int kk = 0; kk < C::KK; ++kk) kcur[kk] = kfb[kk];
     }
     // stage this tile's V rows into the wave-private LDS image (swizzled)
 #pragma unroll
     for (int i = 0; i < C::VLD; ++i) {
       const int c = lane + 64 * i;
       const int row = c / C::NCH, ch = c % C::NCH;
-      st16(my_v + row * D + dswz<D>(row, ch) * 8, vr[i]);
+      st16(my_v + row * D + dswz<D>(row, ch) * 8, vrb[i]);
     }
-    if (t + 2 * C::WAVES < t_end) load_tile(t + 2 * C::WAVES, kf, vr);  // refill this register tile
+    if (t + NB * C::WAVES < t_end) load_tile(t + NB * C::WAVES, kfb, vrb);  // refill this register tile
     if constexpr (KL) {  // A fragment: key li, dims 32 kk + 8 g .. +8 (same wave wrote it: LDS order)
 #pragma unroll
       for (int kk = 0; kk < C::KK; ++kk)
@@ -345,13 +348,18 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     }
   };
 
-  int t = t0;
-  if (t < t_end && !preA) load_tile(t, kfA, vrA);
-  if (t + C::WAVES < t_end && !preB) load_tile(t + C::WAVES, kfB, vrB);
-  for (; t < t_end; t += 2 * C::WAVES) {
-    process(t, kfA, vrA);
-    if (t + C::WAVES >= t_end) break;
-    process(t + C::WAVES, kfB, vrB);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int tj = t0 + j * C::WAVES;
+    if (tj < t_end && !pre[j]) load_tile(tj, kf[j], vr[j]);
+  }
+  for (int t = t0; t < t_end; t += NB * C::WAVES) {
+    bool done = false;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if (!done && t + j * C::WAVES < t_end) process(t + j * C::WAVES, kf[j], vr[j]);
+      else done = true;
+    }
   }
 
   // ---- merge the 4 wave states: O^T[d = 16mt + 4g + r][h = li]
@@ -409,9 +417,18 @@ template <int D, int G, bool FQ>
 static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, const uint16_t* vc,
                           const int32_t* bt, int bts, const int32_t* sl, float* po, float* pl, uint16_t* out,
                           int64_t os, int B, int Hq, int Hkv, int bs, float scale, int S, const QkvFuse& fq,
-                          hipStream_t st) {
+                          hipStream_t st, int depth = 2) {
   // K through LDS for G <= 4; at G = 8 (one kv head per TP-8 rank of the 70B) the
-  // fragment-shaped K loads measured 0.5-6 % faster
+  // fragment-shaped K loads measured 0.5-6 % faster. depth 3: three register tiles
+  // in flight per wave (fused form, G <= 4)
+  if constexpr (D == 128 && G <= 4 && FQ) {
+    if (depth == 3) {
+      hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, true, 3>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc,
+                         bt, bts, sl, po, pl, out, os, Hq, Hkv, bs, scale, S, fq);
+      if (S > 1) hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
+      return;
+    }
+  }
   if constexpr (D == 128 && G <= 4)
     hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, true>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt,
                        bts, sl, po, pl, out, os, Hq, Hkv, bs, scale, S, fq);
@@ -447,17 +464,17 @@ int decode_attention_fq(const float* part, int S_qkv, const int32_t* positions, 
                         const int32_t* slots, uint16_t* kc, uint16_t* vc, const int32_t* bt, int bt_stride,
                         const int32_t* seq_lens, float* part_out, float* part_lse, uint16_t* out,
                         int64_t out_stride, int B, int Hq, int Hkv, int D, int bs, float scale, int num_splits,
-                        int apply_rope, hipStream_t st) {
+                        int apply_rope, hipStream_t st, int depth) {
   if (B <= 0) return 0;
   if (part == nullptr || S_qkv < 1 || bs % 16 != 0 || Hq % Hkv != 0 || D != 128 || num_splits < 1) return -1;
   if (num_splits > 1 && (part_out == nullptr || part_lse == nullptr)) return -1;
-  if (out == nullptr) return -1;
+  if (out == nullptr || depth < 2 || depth > 3) return -1;
   const QkvFuse fq{part, S_qkv, positions, cos_sin, slots, kc, vc, apply_rope};
   const int G = Hq / Hkv;
 #define XGK_DECF(GG)                                                                                         \
   if (G == GG) {                                                                                             \
     launch_decode<128, GG, true>(nullptr, 0, kc, vc, bt, bt_stride, seq_lens, part_out, part_lse, out,       \
-                                 out_stride, B, Hq, Hkv, bs, scale, num_splits, fq, st);                     \
+                                 out_stride, B, Hq, Hkv, bs, scale, num_splits, fq, st, depth);              \
     return 0;                                                                                                \
   }
   XGK_DECF(1) XGK_DECF(2) XGK_DECF(4) XGK_DECF(8)

@@ -32,7 +32,7 @@ void embed_gather(const int32_t*, int, const uint16_t*, int, int, uint16_t*, flo
 void mean_l2norm_rows(float*, const int32_t*, const int32_t*, float*, int, int, hipStream_t);
 int decode_attention_fq(const float*, int, const int32_t*, const float*, const int32_t*, uint16_t*, uint16_t*,
                         const int32_t*, int, const int32_t*, float*, float*, uint16_t*, int64_t, int, int, int, int,
-                        int, float, int, int, hipStream_t);
+                        int, float, int, int, hipStream_t, int);
 int moe_gemm_m64g(const uint16_t*, const int32_t*, const int32_t*, int, int, const uint16_t*, int, int, float*,
                   uint16_t*, int, int, int, int, int, hipStream_t, const int32_t*);
 void add_partials_rmsnorm(const float*, int, int, uint16_t*, const uint16_t*, uint16_t*, int, float, hipStream_t);
@@ -295,13 +295,16 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("decode_attention_fq", [](uintptr_t part, int S_, uintptr_t pos, uintptr_t cs, uintptr_t slots, uintptr_t kc,
                                   uintptr_t vc, uintptr_t bt, int bts, uintptr_t sl, uintptr_t po, uintptr_t pl,
                                   uintptr_t out, int64_t os, int B, int Hq, int Hkv, int D, int bs, float scale,
-                                  int splits, int apply_rope, uintptr_t st) {
+                                  int splits, int apply_rope, uintptr_t st, int depth) {
     check(xgk::decode_attention_fq(P<const float>(part), S_, P<const int32_t>(pos), P<const float>(cs),
                                    P<const int32_t>(slots), P<uint16_t>(kc), P<uint16_t>(vc), P<const int32_t>(bt),
                                    bts, P<const int32_t>(sl), P<float>(po), P<float>(pl), P<uint16_t>(out), os, B, Hq,
-                                   Hkv, D, bs, scale, splits, apply_rope, S(st)),
+                                   Hkv, D, bs, scale, splits, apply_rope, S(st), depth),
           "decode_attention_fq");
-  });
+  }, py::arg("part"), py::arg("S"), py::arg("pos"), py::arg("cs"), py::arg("slots"), py::arg("kc"), py::arg("vc"),
+     py::arg("bt"), py::arg("bts"), py::arg("sl"), py::arg("po"), py::arg("pl"), py::arg("out"), py::arg("os"),
+     py::arg("B"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"), py::arg("bs"), py::arg("scale"), py::arg("splits"),
+     py::arg("apply_rope"), py::arg("st"), py::arg("depth") = 2);
   m.def("moe_gemm_m64g", [](uintptr_t x, uintptr_t rows, uintptr_t offs, int E, int K, uintptr_t w, int N, int P_,
                             uintptr_t part, uintptr_t out, int splits, int mode, int nw, int cfg, uintptr_t st) {
     check(xgk::moe_gemm_m64g(P<const uint16_t>(x), P<const int32_t>(rows), P<const int32_t>(offs), E, K,

@@ -151,7 +151,8 @@ def _paged(lens, Hkv, D, bs, extra_pages=8):
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 8)])
 @pytest.mark.parametrize("S", [1, 4, 8])
 @pytest.mark.parametrize("splits", [1, 3, 16])
-def test_decode_attention_fused_prologue(Hq, Hkv, S, splits):
+@pytest.mark.parametrize("depth", [2, 3])
+def test_decode_attention_fused_prologue(Hq, Hkv, S, splits, depth):
     import xgserve.ops.attention as A
     D, bs = 128, 16
     lens = [1, 17, 300, 64, 0, 129]  # row 4: a graph padding row (no KV write, no attention)
@@ -167,7 +168,7 @@ def test_decode_attention_fused_prologue(Hq, Hkv, S, splits):
     kc1, vc1, kc2, vc2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
     ws = A.DecodeWorkspace(B, Hq, D, splits, DEV)
     out = ops.decode_attention_fused(PendingSum(part, S), pos, slots, cs, kc1, vc1, bt, sl, Hq, scale, splits,
-                                     workspace=ws)
+                                     workspace=ws, depth=depth)
     # reference: the unfused chain (rope_cache_partials -> fp32 attention reference)
     q = torch.empty(B, Hq * D, dtype=torch.bfloat16, device=DEV)
     ops.rope_cache_partials(PendingSum(part, S), q, pos, cs, kc2, vc2, slots, Hq, Hkv, D)

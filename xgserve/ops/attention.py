@@ -9,6 +9,11 @@ import torch
 
 from ._native import kernels, stream_ptr, use_native
 
+# register K/V tiles in flight per wave of the fused decode attention (2 or 3; 3 only
+# for G <= 4): XGS_DECODE_DEPTH A/B (bench/decode_cold.py --depth)
+DECODE_DEPTH = int(__import__("os").environ.get("XGS_DECODE_DEPTH", "2"))
+
+
 def choose_num_splits(batch: int, num_kv_heads: int, max_seq_len: int, num_cus: int = 256) -> int:
     """Split-K factor so the decode grid has >= ~2 workgroups per CU, but every
     split still owns >= 256 keys (16 pages)."""
@@ -115,7 +120,7 @@ def decode_attention_fused(pend, positions: torch.Tensor, slot_mapping: torch.Te
                            k_cache: torch.Tensor, v_cache: torch.Tensor, block_tables: torch.Tensor,
                            seq_lens: torch.Tensor, num_heads: int, scale: float, num_splits: int = 1,
                            workspace: Optional[DecodeWorkspace] = None, apply_rope: bool = True,
-                           out: Optional[torch.Tensor] = None):
+                           out: Optional[torch.Tensor] = None, depth: Optional[int] = None):
     """Paged decode attention on the QKV projection's split-K partials (PendingSum
     [S, B, (Hq + 2 Hkv) D]): each workgroup's prologue reduces its (sequence, kv
     head) slice, applies RoPE and appends the new K/V row to the cache -- the work
@@ -137,7 +142,7 @@ def decode_attention_fused(pend, positions: torch.Tensor, slot_mapping: torch.Te
                                   slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                   block_tables.data_ptr(), block_tables.stride(0), seq_lens.data_ptr(), po, pl,
                                   out.data_ptr(), out.stride(0), B, Hq, Hkv, D, bs, float(scale), int(num_splits),
-                                  1 if apply_rope else 0, stream_ptr())
+                                  1 if apply_rope else 0, stream_ptr(), DECODE_DEPTH if depth is None else depth)
     return out
 
 
