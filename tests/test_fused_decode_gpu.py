@@ -287,7 +287,13 @@ def test_mixtral_decode_step_logits_match_reference(mixtral_small, fused, monkey
     assert len(toks) == 2
     got = eng.runner.last_logits[-1]
     ref = reference_logits(mixtral_small, prompt + toks[:1])[-1].float().cpu()
-    assert float((got - ref).norm() / ref.norm()) < 3e-2
+    # top-2 routing is discontinuous: a near-tie expert choice of one prompt token that
+    # flips between the bf16 engine and the fp32 reference moves the logits by a few %
+    # (bench/diag_moe_mw.py: 1.5-4.8 % across prompts, the same with the prompt step on
+    # gemm_mw or on the library GEMMs), so the bound is looser than the dense model's
+    # and the greedy choice must agree
+    assert float((got - ref).norm() / ref.norm()) < 6e-2
+    assert int(got.argmax()) == int(ref.argmax())
 
 
 def test_mixtral_fused_batch_decode_matches_unfused(mixtral_small, monkeypatch):

@@ -195,6 +195,9 @@ def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split
     M, K = x.shape
     N = w.shape[0]
     plan = m64_plan(M, N, K, mode)
+    if plan is None and None not in (nw, split_k, cfg) and 1 <= M <= 64 and _m64_valid(N, K, mode, nw, split_k,
+                                                                                     cfg, M):
+        plan = (nw, split_k, cfg)  # a fully explicit configuration (sweeps, tests) needs no measured plan
     if plan is None:
         raise ValueError(f"gemm_m64: unsupported shape M={M} N={N} K={K} mode={mode}")
     if nw is None and split_k is None and cfg is None:
