@@ -161,6 +161,11 @@ r4e)  # round 4 re-entry: MoE/mw numerics diagnostic, GPU tests, headline, mw2 s
   run mw_sweep 500 python -u bench/gemm_bench.py --mw-sweep --M 64 128 192 256 --shapes qkv o gate_up down --top 8
   run c64_chunk128 240 env XGS_STEP_LOG="$o/steps_chunk128.jsonl" $B --steps 600 --warmup 60 --prefill-chunk 128 "$@"
   run c64_base 240 env XGS_STEP_LOG="$o/steps_base.jsonl" $B --steps 600 --warmup 60 "$@" ;;
+r4f)  # round 4: decode / prompt GEMM overlap probe, then the r4d and r4b A/Bs
+  run overlap 200 python -u bench/overlap_probe.py --prompt 256 512 1024
+  run overlap_prio 200 python -u bench/overlap_probe.py --prompt 512 --prio
+  bash "$0" r4d r4f_d "$@" || exit $?
+  bash "$0" r4b r4f_b "$@" || exit $? ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;

@@ -39,7 +39,10 @@ namespace xgk {
 
 enum : int { MW_BF16 = 0, MW_PARTIAL = 1, MW_SILU = 2 };
 
-template <int WN, int NWT, int MTW, int D, bool NT>
+// PR (anatomy probes, bench/gemm_bench.py --mw-probe; results are garbage): 0 = the
+// kernel; 1 = DMA + waits + barriers only (no fragment reads / MFMA); 2 = fragment
+// reads + MFMA + barriers only (no DMA); 3 = no x DMA (weights only); 4 = no weight DMA.
+template <int WN, int NWT, int MTW, int D, bool NT, int PR = 0>
 __global__ void __launch_bounds__(512, 1) gemm_mw_kernel(const uint16_t* __restrict__ x, int M, int K,
                                                           const uint16_t* __restrict__ w, int N, int S,
                                                           float* __restrict__ part, uint16_t* __restrict__ out,
@@ -91,6 +94,7 @@ __global__ void __launch_bounds__(512, 1) gemm_mw_kernel(const uint16_t* __restr
     xsrc[i] = x + static_cast<int64_t>(min(8 * (wid * XI + i) + dr, M - 1)) * K + k0 + 8 * (dj ^ dr);
 
   auto issue_w = [&](int c) {
+    if constexpr (PR == 2 || PR == 4) return;
     uint8_t* slot = wring + (c % (D + 1)) * WSLOT;
     const int kk = c * KC;
 #pragma unroll
@@ -100,6 +104,7 @@ __global__ void __launch_bounds__(512, 1) gemm_mw_kernel(const uint16_t* __restr
     }
   };
   auto issue_x = [&](int c) {
+    if constexpr (PR == 2 || PR == 3) return;
     uint8_t* slot = xring + (c % D) * XSLOT;
     const int kk = c * KC;
 #pragma unroll
@@ -163,7 +168,7 @@ __global__ void __launch_bounds__(512, 1) gemm_mw_kernel(const uint16_t* __restr
     // refills the slots read by chunk c - 1 (every wave is past the barrier)
     if (c + D - 1 < nch) issue_x(c + D - 1);
     if (c + D < nch) issue_w(c + D);
-    compute(c);
+    if constexpr (PR != 1) compute(c);
   }
 
   // acc[nt][mt][r] = out[m = xrow0 + 16 mt + li][n = n0 + wrow0 + 16 nt + 4 g + r]
@@ -587,6 +592,46 @@ static int gemm_mw_impl(const uint16_t* x, int M, int K, const uint16_t* w, int 
     case 4: return launch_mw<4, 2, 3, false>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
     case 5: return launch_mw<2, 4, 3, true>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
     default: return launch_mw<2, 8, 2, true>(mtw, grid, st, x, M, K, w, N, S, part, out, mode);
+  }
+}
+
+// Anatomy probes of the two best mid-M configurations (cfg 1: 4 x 2 waves, cfg 5: 2 x 4
+// waves; 128 columns, ring 3, nt weights) at 64-row steps of M (PR as above).
+template <int PR>
+static int launch_mw_probe(int cfg, int M, dim3 grid, hipStream_t st, const uint16_t* x, int K, const uint16_t* w,
+                           int N, int S, float* part, uint16_t* out, int mode) {
+#define XGK_MWP(WN, NWT, MTW)                                                                                   \
+  hipLaunchKernelGGL((gemm_mw_kernel<WN, NWT, MTW, 3, true, PR>), grid, dim3(512), 0, st, x, M, K, w, N, S, \
+                     part, out, mode);                                                                          \
+  return 0;
+  const int q = (M + 63) / 64;
+  if (cfg == 1) {
+    if (q == 1) { XGK_MWP(4, 2, 2) }
+    if (q == 2) { XGK_MWP(4, 2, 4) }
+    if (q == 3) { XGK_MWP(4, 2, 6) }
+    if (q == 4) { XGK_MWP(4, 2, 8) }
+  } else if (cfg == 5) {
+    if (q == 1) { XGK_MWP(2, 4, 1) }
+    if (q == 2) { XGK_MWP(2, 4, 2) }
+    if (q == 3) { XGK_MWP(2, 4, 3) }
+    if (q == 4) { XGK_MWP(2, 4, 4) }
+  }
+#undef XGK_MWP
+  return 1;
+}
+
+int gemm_mw_probe(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S,
+                  int mode, int cfg, int probe, hipStream_t st) {
+  if (M < 1 || M > 256 || S < 1 || K % 64 || S > K / 64 || N % 128 || (cfg != 1 && cfg != 5)) return 1;
+  if (mode == MW_PARTIAL ? part == nullptr : (out == nullptr || S != 1)) return 1;
+  const dim3 grid((N / 128) * S);
+  switch (probe) {
+    case 0: return launch_mw_probe<0>(cfg, M, grid, st, x, K, w, N, S, part, out, mode);
+    case 1: return launch_mw_probe<1>(cfg, M, grid, st, x, K, w, N, S, part, out, mode);
+    case 2: return launch_mw_probe<2>(cfg, M, grid, st, x, K, w, N, S, part, out, mode);
+    case 3: return launch_mw_probe<3>(cfg, M, grid, st, x, K, w, N, S, part, out, mode);
+    case 4: return launch_mw_probe<4>(cfg, M, grid, st, x, K, w, N, S, part, out, mode);
+    default: return 1;
   }
 }
 

@@ -24,6 +24,7 @@ int gemm_m64g(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*
 int gemm_m64g_ex(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, const float*,
                  int, int, float, uint16_t*, float*, int*, hipStream_t);
 int gemm_mw(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, hipStream_t);
+int gemm_mw_probe(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 int gemm_mw_ss(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, const float*, int,
                int, float, hipStream_t);
 void add_partials_resid(const float*, int, int, uint16_t*, float*, int, hipStream_t, uint64_t);
@@ -252,6 +253,12 @@ PYBIND11_MODULE(_kernels, m) {
     check(xgk::gemm_mw(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode, cfg,
                        S(st)),
           "gemm_mw");
+  });
+  m.def("gemm_mw_probe", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
+                            int mode, int cfg, int probe, uintptr_t st) {
+    check(xgk::gemm_mw_probe(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode,
+                             cfg, probe, S(st)),
+          "gemm_mw_probe");
   });
   m.def("gemm_mw_ss", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
                          int mode, int cfg, uintptr_t ss_in, int ss_n, int ss_stride, float eps, uintptr_t st) {

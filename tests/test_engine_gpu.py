@@ -279,3 +279,4 @@ def test_mall_prefetch_side_stream_changes_nothing(llama_small, monkeypatch):
     monkeypatch.setattr(L, "MALL_PREFETCH_MB", 64)
     b = _engine(llama_small).generate(p, sp)
     assert a == b
+

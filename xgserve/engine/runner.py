@@ -560,19 +560,9 @@ class ModelRunner:
             return (n, None, None, None, True, ev)
         return self._graph_out(n)
 
-    def _execute_eager(self, plan, samp: Optional[SamplingRows], need_hidden: bool, src: Optional[np.ndarray]):
-        T = int(plan["num_tokens"])
-        Nd = int(plan["num_decodes"])
-        ns = int(plan["num_seqs"])
-        w = int(plan["bt_width"])
-        Np = ns - Nd
-        li = plan["logits_indices"]
-        S = li.shape[0]
-        qsl = plan["query_start_loc"]
-        parts = [plan["input_ids"], plan["positions"], plan["slot_mapping"],
-                 plan["block_tables"], plan["seq_lens"], (qsl[Nd:] - Nd).astype(np.int32), li]
-        if src is not None:  # staged with the other inputs: no blocking copy ahead of the queued step
-            parts.append(np.ascontiguousarray(src, dtype=np.int32))
+    def _stage_parts(self, parts):
+        """The int32 arrays of an eager step -> ONE pinned host buffer -> ONE async H2D
+        copy (two buffers, event-guarded). Returns (device buffer, section offsets)."""
         sizes = [p.size for p in parts]
         total = sum(sizes)
         si = self.stage_idx
@@ -594,7 +584,22 @@ class ModelRunner:
             dev = d_stage
         else:
             dev = h_stage
-        o = np.cumsum([0] + sizes)
+        return dev, np.cumsum([0] + sizes)
+
+    def _execute_eager(self, plan, samp: Optional[SamplingRows], need_hidden: bool, src: Optional[np.ndarray]):
+        T = int(plan["num_tokens"])
+        Nd = int(plan["num_decodes"])
+        ns = int(plan["num_seqs"])
+        w = int(plan["bt_width"])
+        Np = ns - Nd
+        li = plan["logits_indices"]
+        S = li.shape[0]
+        qsl = plan["query_start_loc"]
+        parts = [plan["input_ids"], plan["positions"], plan["slot_mapping"],
+                 plan["block_tables"], plan["seq_lens"], (qsl[Nd:] - Nd).astype(np.int32), li]
+        if src is not None:  # staged with the other inputs: no blocking copy ahead of the queued step
+            parts.append(np.ascontiguousarray(src, dtype=np.int32))
+        dev, o = self._stage_parts(parts)
         ids = dev[o[0]:o[1]]
         pos = dev[o[1]:o[2]]
         slots = dev[o[2]:o[3]]
