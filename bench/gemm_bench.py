@@ -278,12 +278,14 @@ def mw_sweep(a):
 
 def mw_probe(a):
     """gemm_mw (cfg 1 / 5) with parts of its pipeline removed (csrc/kernels/gemm_mw.hip PR):
-    0 full, 1 DMA + waits only, 2 LDS reads + MFMA only, 3 no x DMA, 4 no weight DMA.
+    0 full, 1 DMA + waits only, 2 LDS reads + MFMA only, 3 no x DMA, 4 no weight DMA,
+    5 x DMA only, 6 weight DMA only; +8: K chunks walked from a rotated start per tile.
     Cold weights; us per call."""
     k = kernels()
     st = torch.cuda.current_stream().cuda_stream
     splits = {"qkv": 5, "o": 8, "gate_up": 1, "down": 8}
-    names = {0: "full", 1: "dma_only", 2: "compute_only", 3: "w_only", 4: "x_only"}
+    names = {0: "full", 1: "dma_only", 2: "compute_only", 3: "w_only", 4: "x_only", 5: "x_dma", 6: "w_dma",
+             8: "full_rot", 9: "dma_only_rot", 13: "x_dma_rot"}
     for name in a.shapes:
         N, K = SHAPES[name]
         S = splits.get(name, 1)
@@ -297,7 +299,7 @@ def mw_probe(a):
             out = torch.empty(M, N // 2 if mode == L.MODE_SILU else N, dtype=torch.bfloat16, device="cuda")
             for cfg in (1, 5):
                 row = {}
-                for pr in range(5):
+                for pr in names:
                     def fn(w, pr=pr, cfg=cfg):
                         k.gemm_mw_probe(x.data_ptr(), M, K, w.data_ptr(), N,
                                         part.data_ptr() if mode == L.MODE_PARTIAL else 0,

@@ -76,10 +76,6 @@ tp)
 moe)
   pyt moe_tests 400 tests/test_kernels_gpu.py tests/test_engine_gpu.py -k "moe or mixtral or expert"
   run mixtral_c64 300 $B --model mixtral-8x7b --steps 60 --warmup 20 "$@"
-  pyt prefetch_test 200 tests/test_engine_gpu.py -k mall_prefetch
-  for pf in 0 48 120; do
-    run c1_pf$pf 200 env XGS_MALL_PREFETCH=$pf $B --concurrency 1 --steps 200 --warmup 20
-  done
   run mixtral_c1 300 $B --model mixtral-8x7b --concurrency 1 --steps 60 --warmup 10 "$@"
   run mixtral_tp2_c64 300 $B --model mixtral-8x7b --tp-shard 2 --steps 60 --warmup 20 "$@" ;;
 prefill)
@@ -134,10 +130,7 @@ r4b)  # round 4: all-reduce protocols, TP tests (async mixed steps), batch-1 Inf
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 240 python -u bench/ar_bench.py --world 2 4 8
   pyt tp_tests 500 tests/test_tp_gpu.py
-  pyt prefetch_test 200 tests/test_engine_gpu.py -k mall_prefetch
-  for pf in 0 48 120; do
-    run c1_pf$pf 150 env XGS_MALL_PREFETCH=$pf $B --concurrency 1 --steps 200 --warmup 20 "$@"
-  done ;;
+ ;;
 r4c)  # round 4: Mixtral with / without prompt chunks, profiles of the chunked headline and Mixtral batch 1
   run mixtral_c1 300 $B --model mixtral-8x7b --concurrency 1 --steps 60 --warmup 10
   run mixtral_c64_chunk 300 $B --model mixtral-8x7b --steps 120 --warmup 20 --prefill-chunk 128
@@ -166,6 +159,20 @@ r4f)  # round 4: decode / prompt GEMM overlap probe, then the r4d and r4b A/Bs
   run overlap_prio 200 python -u bench/overlap_probe.py --prompt 512 --prio
   bash "$0" r4d r4f_d "$@" || exit $?
   bash "$0" r4b r4f_b "$@" || exit $? ;;
+r4g)  # round 4: gemm_mw anatomy probes, AR latency at world 4 / 8, batch-1 prefetch A/B, c64 profile
+  run mw_probe 300 python -u bench/gemm_bench.py --mw-probe --M 64 128 192 256 --shapes gate_up down qkv o
+  bash bench/profile.sh "$o/prof_c64" "$@" ;;
+r4h)  # round 4: K-chunk rotation -- kernel tests, m64g / mw / LM-head sweeps, engine A/B (XGS_KROT)
+  pyt kernel_tests 600 tests/test_skinny_gpu.py tests/test_fused_decode_gpu.py tests/test_kernels_gpu.py
+  run m64g_sweep 300 python -u bench/gemm_bench.py --m64g-sweep --M 64 --shapes gate_up qkv o down
+  run m64g_sweep_off 300 env XGS_KROT=0 python -u bench/gemm_bench.py --m64g-sweep --M 64 --shapes gate_up
+  run mw_sweep 400 python -u bench/gemm_bench.py --mw-sweep --M 64 128 192 --shapes gate_up lm_head --top 4
+  for v in "XGS_KROT=1" "XGS_KROT=0" "XGS_KROT=2"; do
+    n=$(echo "$v" | tr -c 'A-Za-z0-9_=\n' '_')
+    run "c64_$n" 240 env $v XGS_STEP_LOG="$o/steps_$n.jsonl" $B --steps 600 --warmup 60 "$@"
+  done
+  run c1 150 $B --concurrency 1 --steps 200 --warmup 20 "$@"
+  run c1_off 150 env XGS_KROT=0 $B --concurrency 1 --steps 200 --warmup 20 "$@" ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;

@@ -58,7 +58,19 @@ struct M64Epi {
   uint16_t* resid;
   float* ss_out;
   int* counters;
+  int krot = 0;  // set by m64g_launch (k_rotation): walk K chunks from a per-tile start
 };
+
+// K-chunk rotation. Workgroups that all start at K chunk 0 and walk in lockstep read the
+// same column offset of weight rows 2*K bytes apart at the same moment, so the HBM
+// requests of the whole grid pile onto a few channels: 8B gate_up at 64 rows streams at
+// 4.9 TB/s in order and 6.2 TB/s rotated (profiles/r4_mw_probe.md). Each workgroup walks
+// its chunk range from a tile-dependent start instead (the fp32 sum order changes, the
+// result does not). Split-K grids (S > 2) are already spread over K and stay in order.
+// Policy (set_k_rotation): 0 never, 1 when S <= 2 (default), 2 always.
+static int g_krot_mode = 1;
+void set_k_rotation(int mode) { g_krot_mode = mode; }
+int k_rotation(int S) { return g_krot_mode == 2 || (g_krot_mode == 1 && S <= 2) ? 1 : 0; }
 
 // Every wave drains its stores (write-through), then one relaxed agent-scope
 // ticket; returns in every thread whether this workgroup drew `last_value`. The
@@ -258,9 +270,11 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
     const int r = RPI * (wid * XI + i) + dr;     // x row 0..XROWS-1
     xsrc[i] = x + static_cast<int64_t>(min(r, M - 1)) * K + k0 + 8 * (dj ^ (r & (GPR - 1)));
   }
+  const int rot = epi.krot ? static_cast<int>((blockIdx.x * 37u) % static_cast<unsigned>(nchunks)) : 0;
 
   auto issue = [&](uint8_t* slot, int c) {
-    const int kk = c * KC;
+    const int cr = c + rot;
+    const int kk = (cr >= nchunks ? cr - nchunks : cr) * KC;
 #pragma unroll
     for (int i = 0; i < XI; ++i) glds16(xsrc[i] + kk, slot + RPI * (wid * XI + i) * RB);
 #pragma unroll
@@ -835,8 +849,10 @@ static int m64g_check(int M, int K, int N, const float* part, const uint16_t* ou
 }
 
 static void m64g_launch(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S,
-                        int mode, int nw, int cfg, const M64Epi& epi, hipStream_t st) {
+                        int mode, int nw, int cfg, const M64Epi& epi_in, hipStream_t st) {
   const dim3 grid(N / (16 * nw * m64g_cfg_waves(cfg)), S);
+  M64Epi epi = epi_in;
+  epi.krot = k_rotation(S);
   if (nw == 1) launch_m64g<1>(cfg, grid, st, x, M, K, w, N, part, out, mode, epi);
   else launch_m64g<2>(cfg, grid, st, x, M, K, w, N, part, out, mode, epi);
 }

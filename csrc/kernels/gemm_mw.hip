@@ -37,16 +37,21 @@
 
 namespace xgk {
 
+int k_rotation(int S);  // gemm_m64g.hip
+
 enum : int { MW_BF16 = 0, MW_PARTIAL = 1, MW_SILU = 2 };
 
-// PR (anatomy probes, bench/gemm_bench.py --mw-probe; results are garbage): 0 = the
-// kernel; 1 = DMA + waits + barriers only (no fragment reads / MFMA); 2 = fragment
-// reads + MFMA + barriers only (no DMA); 3 = no x DMA (weights only); 4 = no weight DMA.
+// PR (anatomy probes, bench/gemm_bench.py --mw-probe; results are garbage unless the
+// low bits are 0): PR & 7: 0 = the kernel; 1 = DMA + waits + barriers only (no
+// fragment reads / MFMA); 2 = fragment reads + MFMA + barriers only (no DMA); 3 = no x
+// DMA (weights only); 4 = no weight DMA; 5 = x DMA only; 6 = weight DMA only.
+// PR & 8: every workgroup walks its K chunks from a tile-dependent start (rotated), so
+// the workgroups of an XCD read different x lines at any moment (results exact).
 template <int WN, int NWT, int MTW, int D, bool NT, int PR = 0>
 __global__ void __launch_bounds__(512, 1) gemm_mw_kernel(const uint16_t* __restrict__ x, int M, int K,
                                                           const uint16_t* __restrict__ w, int N, int S,
                                                           float* __restrict__ part, uint16_t* __restrict__ out,
-                                                          int mode) {
+                                                          int mode, int krot) {
   constexpr int WM = 8 / WN;
   constexpr int KC = 64, RB = 128, RPI = 8;     // k per chunk, bytes per LDS row, rows per DMA instruction
   constexpr int WCOLS = WN * 16 * NWT;
@@ -93,10 +98,16 @@ __global__ void __launch_bounds__(512, 1) gemm_mw_kernel(const uint16_t* __restr
   for (int i = 0; i < XI; ++i)
     xsrc[i] = x + static_cast<int64_t>(min(8 * (wid * XI + i) + dr, M - 1)) * K + k0 + 8 * (dj ^ dr);
 
+  constexpr int PK = PR & 7;
+  const int rot = ((PR & 8) || krot) ? (tile * 37) % nch : 0;  // K-chunk rotation (gemm_m64g.hip k_rotation)
+  auto kof = [&](int c) {
+    const int cc = c + rot;
+    return (cc >= nch ? cc - nch : cc) * KC;
+  };
   auto issue_w = [&](int c) {
-    if constexpr (PR == 2 || PR == 4) return;
+    if constexpr (PK == 2 || PK == 4 || PK == 5) return;
     uint8_t* slot = wring + (c % (D + 1)) * WSLOT;
-    const int kk = c * KC;
+    const int kk = kof(c);
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
       if constexpr (NT) glds16_nt(wsrc[i] + kk, slot + (wid * WI + i) * 1024);
@@ -104,9 +115,9 @@ __global__ void __launch_bounds__(512, 1) gemm_mw_kernel(const uint16_t* __restr
     }
   };
   auto issue_x = [&](int c) {
-    if constexpr (PR == 2 || PR == 3) return;
+    if constexpr (PK == 2 || PK == 3 || PK == 6) return;
     uint8_t* slot = xring + (c % D) * XSLOT;
-    const int kk = c * KC;
+    const int kk = kof(c);
 #pragma unroll
     for (int i = 0; i < XI; ++i) glds16(xsrc[i] + kk, slot + (wid * XI + i) * 1024);
   };
@@ -168,7 +179,7 @@ __global__ void __launch_bounds__(512, 1) gemm_mw_kernel(const uint16_t* __restr
     // refills the slots read by chunk c - 1 (every wave is past the barrier)
     if (c + D - 1 < nch) issue_x(c + D - 1);
     if (c + D < nch) issue_w(c + D);
-    if constexpr (PR != 1) compute(c);
+    if constexpr (PK != 1 && PK != 5 && PK != 6) compute(c);
   }
 
   // acc[nt][mt][r] = out[m = xrow0 + 16 mt + li][n = n0 + wrow0 + 16 nt + 4 g + r]
@@ -244,7 +255,7 @@ template <int WN, int NWT, int MTW, int DW, int DX, bool NT>
 __global__ void __launch_bounds__(512, 1) gemm_mw2_kernel(const uint16_t* __restrict__ x, int M, int K,
                                                            const uint16_t* __restrict__ w, int N, int S,
                                                            float* __restrict__ part, uint16_t* __restrict__ out,
-                                                           int mode, MwEpi epi) {
+                                                           int mode, MwEpi epi, int krot) {
   constexpr int WM = 8 / WN;
   constexpr int KC = 64, RB = 128, RPI = 8;
   constexpr int WCOLS = WN * 16 * NWT;
@@ -290,9 +301,14 @@ __global__ void __launch_bounds__(512, 1) gemm_mw2_kernel(const uint16_t* __rest
       src[i] = x + static_cast<int64_t>(min(row, M - 1)) * K + k0 + 8 * (dj ^ dr);
     }
   }
+  const int rot = krot ? (tile * 37) % nch : 0;  // K-chunk rotation (gemm_m64g.hip k_rotation)
+  auto kof = [&](int c) {
+    const int cc = c + rot;
+    return (cc >= nch ? cc - nch : cc) * KC;
+  };
   auto issue_w = [&](int c) {
     uint8_t* slot = wring + (c % DW) * WSLOT;
-    const int kk = c * KC;
+    const int kk = kof(c);
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
       if constexpr (NT) glds16_nt(src[i] + kk, slot + (rw * WI + i) * 1024);
@@ -301,7 +317,7 @@ __global__ void __launch_bounds__(512, 1) gemm_mw2_kernel(const uint16_t* __rest
   };
   auto issue_x = [&](int c) {
     uint8_t* slot = xring + (c % DX) * XSLOT;
-    const int kk = c * KC;
+    const int kk = kof(c);
 #pragma unroll
     for (int i = 0; i < XI; ++i) glds16(src[i] + kk, slot + (rw * XI + i) * 1024);
   };
@@ -472,7 +488,7 @@ static int launch_mw(int mtw, dim3 grid, hipStream_t st, const uint16_t* x, int 
   case MTW:                                                                                                     \
     if constexpr (mw_fits<WN, NWT, MTW, D>()) {                                                                 \
       hipLaunchKernelGGL((gemm_mw_kernel<WN, NWT, MTW, D, NT>), grid, dim3(512), 0, st, x, M, K, w, N, S, part, \
-                         out, mode);                                                                            \
+                         out, mode, k_rotation(S));                                                             \
       return 0;                                                                                                 \
     }                                                                                                           \
     return 1;
@@ -510,7 +526,7 @@ static int launch_mw2(int mtw, dim3 grid, hipStream_t st, const uint16_t* x, int
   case MTW:                                                                                                       \
     if constexpr (mw2_fits<WN, NWT, MTW, DW, DX>()) {                                                             \
       hipLaunchKernelGGL((gemm_mw2_kernel<WN, NWT, MTW, DW, DX, true>), grid, dim3(512), 0, st, x, M, K, w, N, S, \
-                         part, out, mode, epi);                                                                   \
+                         part, out, mode, epi, k_rotation(S));                                                    \
       return 0;                                                                                                   \
     }                                                                                                             \
     return 1;
@@ -602,7 +618,7 @@ static int launch_mw_probe(int cfg, int M, dim3 grid, hipStream_t st, const uint
                            int N, int S, float* part, uint16_t* out, int mode) {
 #define XGK_MWP(WN, NWT, MTW)                                                                                   \
   hipLaunchKernelGGL((gemm_mw_kernel<WN, NWT, MTW, 3, true, PR>), grid, dim3(512), 0, st, x, M, K, w, N, S, \
-                     part, out, mode);                                                                          \
+                     part, out, mode, 0);                                                                       \
   return 0;
   const int q = (M + 63) / 64;
   if (cfg == 1) {
@@ -626,11 +642,11 @@ int gemm_mw_probe(const uint16_t* x, int M, int K, const uint16_t* w, int N, flo
   if (mode == MW_PARTIAL ? part == nullptr : (out == nullptr || S != 1)) return 1;
   const dim3 grid((N / 128) * S);
   switch (probe) {
-    case 0: return launch_mw_probe<0>(cfg, M, grid, st, x, K, w, N, S, part, out, mode);
-    case 1: return launch_mw_probe<1>(cfg, M, grid, st, x, K, w, N, S, part, out, mode);
-    case 2: return launch_mw_probe<2>(cfg, M, grid, st, x, K, w, N, S, part, out, mode);
-    case 3: return launch_mw_probe<3>(cfg, M, grid, st, x, K, w, N, S, part, out, mode);
-    case 4: return launch_mw_probe<4>(cfg, M, grid, st, x, K, w, N, S, part, out, mode);
+#define XGK_MWPC(P) \
+  case P: return launch_mw_probe<P>(cfg, M, grid, st, x, K, w, N, S, part, out, mode);
+    XGK_MWPC(0) XGK_MWPC(1) XGK_MWPC(2) XGK_MWPC(3) XGK_MWPC(4) XGK_MWPC(5) XGK_MWPC(6)
+    XGK_MWPC(8) XGK_MWPC(9) XGK_MWPC(13)
+#undef XGK_MWPC
     default: return 1;
   }
 }

@@ -24,6 +24,7 @@ int gemm_m64g(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*
 int gemm_m64g_ex(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, const float*,
                  int, int, float, uint16_t*, float*, int*, hipStream_t);
 int gemm_mw(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, hipStream_t);
+void set_k_rotation(int mode);
 int gemm_mw_probe(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 int gemm_mw_ss(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, const float*, int,
                int, float, hipStream_t);
@@ -77,7 +78,6 @@ int custom_allreduce_ll(const void*, void*, int64_t, int64_t, const uintptr_t*, 
 int custom_allreduce_resid_ll(const float*, int, int, uint16_t*, float*, int, int64_t, const uintptr_t*, int, int,
                               uint32_t*, uint32_t*, hipStream_t);
 int car_ll_max_bytes(int64_t);
-void mall_prefetch(const void*, int64_t, int, uint32_t*, hipStream_t);
 int car_max_blocks();
 int car_wallclock_khz();
 int car_chunk();
@@ -243,10 +243,6 @@ PYBIND11_MODULE(_kernels, m) {
                          cfg, S(st)),
           "gemm_m64g");
   });
-  m.def("mall_prefetch", [](uintptr_t p, int64_t bytes, int blocks, uintptr_t sink, uintptr_t st) {
-    xgk::mall_prefetch(P<const void>(p), bytes, blocks, P<uint32_t>(sink), S(st));
-    check(0, "mall_prefetch");
-  });
   // mid-M weight-streaming GEMM (gemm_mw.hip): 64 < M <= 256 mixed / prompt steps
   m.def("gemm_mw", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
                       int mode, int cfg, uintptr_t st) {
@@ -254,6 +250,7 @@ PYBIND11_MODULE(_kernels, m) {
                        S(st)),
           "gemm_mw");
   });
+  m.def("set_k_rotation", [](int mode) { xgk::set_k_rotation(mode); });
   m.def("gemm_mw_probe", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
                             int mode, int cfg, int probe, uintptr_t st) {
     check(xgk::gemm_mw_probe(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode,

@@ -94,7 +94,10 @@ def test_gemm_mw_waits_follow_the_ring(tmp_path):
     ks = _kernels(asm, "_ZN3xgk14gemm_mw_kernel")
     assert len(ks) >= 20, len(ks)
     for name, body in ks.items():
-        WN, NWT, MTW, D, _nt = _targs(name)
+        targs = _targs(name)
+        if len(targs) > 5 and targs[5] != 0:
+            continue  # anatomy probes (PR != 0): parts of the pipeline removed on purpose
+        WN, NWT, MTW, D, _nt = targs[:5]
         WI = WN * 16 * NWT // 64
         XI = (8 // WN) * 16 * MTW // 64
         allowed = {0, WI + (XI if D >= 3 else 0)}

@@ -266,17 +266,3 @@ def test_stall_free_sampling_seeded(llama_small):
     _, b, eng = _run_stall_free(llama_small, 128, temperature=0.8)
     assert a == b
     assert eng.runner.mixed_replays >= 6
-
-
-def test_mall_prefetch_side_stream_changes_nothing(llama_small, monkeypatch):
-    """XGS_MALL_PREFETCH: the batch-1 side-stream weight read (captured into the decode
-    graphs with a fork / join around the attention) leaves every token unchanged."""
-    from xgserve.models import llama as L
-    p = [[128000] + list(range(600, 640))]
-    sp = SamplingParams(max_tokens=10, temperature=0.0, ignore_eos=True)
-    monkeypatch.setattr(L, "MALL_PREFETCH_MB", 0)
-    a = _engine(llama_small).generate(p, sp)
-    monkeypatch.setattr(L, "MALL_PREFETCH_MB", 64)
-    b = _engine(llama_small).generate(p, sp)
-    assert a == b
-

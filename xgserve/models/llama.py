@@ -59,29 +59,6 @@ FUSED_DECODE = os.environ.get("XGS_FUSED_DECODE", "1") != "0"
 # MFMA GEMMs whose split-K partials go to the consumers, SiLU-gate in gate_up.
 # 0 = hipBLASLt for every step above 64 tokens.
 MW_MAX_TOKENS = min(MW_MAX_M, int(os.environ.get("XGS_MW_MAX_TOKENS", str(MW_MAX_M))))
-# Batch-1 decode (fused layer, T <= 16): while the latency-bound attention + split
-# combine run, a side-stream launch reads this many MiB of the O and gate_up weights
-# (in that order) so the Infinity Cache holds them when those GEMMs stream them
-# (csrc/kernels/prefetch.hip). 0 = off (A/B: profiles/).
-MALL_PREFETCH_MB = int(os.environ.get("XGS_MALL_PREFETCH", "0"))
-_SIDE_STREAMS = {}
-
-
-def _side_stream(device) -> "torch.cuda.Stream":
-    s = _SIDE_STREAMS.get(str(device))
-    if s is None:
-        s = _SIDE_STREAMS[str(device)] = torch.cuda.Stream(device=device)
-    return s
-
-
-def _prefetch_sink(device) -> torch.Tensor:
-    key = ("sink", str(device))
-    t = _SIDE_STREAMS.get(key)
-    if t is None:
-        t = _SIDE_STREAMS[key] = torch.zeros(4, dtype=torch.int32, device=device)
-    return t
-
-
 # TP > 1 prefill-sized steps: the row-parallel all-reduces are pipelined over this
 # many token chunks and overlapped with the next chunk's GEMMs (RCCL stream); a
 # 2k-token 8B step moves 16 MiB per all-reduce -- ~100 us on 7 xGMI links, a
@@ -433,23 +410,7 @@ class LlamaLayer(nn.Module):
         returns the statistics of the new residual for the next layer."""
         eps = self.cfg.norm_eps
         pqkv = m64_norm_linear(resid, self.qkv, MODE_PARTIAL, stats, eps)
-        side = None
-        if MALL_PREFETCH_MB > 0 and resid.shape[0] <= FAST_M_SMALL and not self.moe:
-            # the O / gate_up weights into the Infinity Cache under the attention
-            cur = torch.cuda.current_stream()
-            side = _side_stream(resid.device)
-            side.wait_stream(cur)
-            budget = MALL_PREFETCH_MB << 20
-            with torch.cuda.stream(side):
-                for w in (self.o, self.gate_up):
-                    n = min(budget, w.numel() * w.element_size())
-                    if n <= 0:
-                        break
-                    ops.mall_prefetch(w, n, _prefetch_sink(resid.device))
-                    budget -= n
         a = self.attn.fused_decode(pqkv, meta, kv, cos_sin)
-        if side is not None:
-            torch.cuda.current_stream().wait_stream(side)
         if self.moe:
             return self._fused_moe_tail(a, resid, ws, site)
         if self.tp > 1:

@@ -15,7 +15,6 @@ from .sampling import argmax_logprob, sample_tokens, argmax_logprob_ref, segment
 from .embedding import embed_gather, mean_l2norm_rows
 from .moe import (moe_topk_softmax, moe_route, moe_route_norm, moe_align, moe_forward_ref, fused_moe, ep_plan,
                   ep_scatter, ep_combine)
-from .prefetch import mall_prefetch
 from ._native import available as native_available
 
 __all__ = [
