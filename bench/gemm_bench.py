@@ -198,7 +198,7 @@ def m64g_sweep(a):
                             if mode == L.MODE_SILU and S > 1:
                                 k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), out.data_ptr(),
                                                S, mode, nw, cfg, 0, 0, 0, 0.0, 0, 0, cnt.data_ptr(),
-                                               torch.cuda.current_stream().cuda_stream, 0, 0, 0, 0)
+                                               torch.cuda.current_stream().cuda_stream)
                                 return
                             k.gemm_m64g(x.data_ptr(), M, K, w.data_ptr(), N,
                                         part.data_ptr() if mode == L.MODE_PARTIAL else 0,

@@ -163,10 +163,10 @@ r4g)  # round 4: gemm_mw anatomy probes, AR latency at world 4 / 8, batch-1 pref
   run mw_probe 300 python -u bench/gemm_bench.py --mw-probe --M 64 128 192 256 --shapes gate_up down qkv o
   bash bench/profile.sh "$o/prof_c64" "$@" ;;
 r4h)  # round 4: K-chunk rotation -- kernel tests, m64g / mw / LM-head sweeps, engine A/B (XGS_KROT)
-  pyt kernel_tests 600 tests/test_skinny_gpu.py tests/test_fused_decode_gpu.py tests/test_kernels_gpu.py
   run m64g_sweep 300 python -u bench/gemm_bench.py --m64g-sweep --M 64 --shapes gate_up qkv o down
   run m64g_sweep_off 300 env XGS_KROT=0 python -u bench/gemm_bench.py --m64g-sweep --M 64 --shapes gate_up
-  run mw_sweep 400 python -u bench/gemm_bench.py --mw-sweep --M 64 128 192 --shapes gate_up lm_head --top 4
+  pyt mw3_tests 300 tests/test_skinny_gpu.py -k "mw"
+  run mw_sweep 500 python -u bench/gemm_bench.py --mw-sweep --M 64 128 192 256 --shapes gate_up down qkv o lm_head --top 5
   for v in "XGS_KROT=1" "XGS_KROT=0" "XGS_KROT=2"; do
     n=$(echo "$v" | tr -c 'A-Za-z0-9_=\n' '_')
     run "c64_$n" 240 env $v XGS_STEP_LOG="$o/steps_$n.jsonl" $B --steps 600 --warmup 60 "$@"

@@ -131,6 +131,28 @@ def test_gemm_mw2_role_waits(tmp_path):
     _no_spills(asm)
 
 
+def test_gemm_mw3_pipelined_waits(tmp_path):
+    """Software-pipelined ring (cfg 15-21): every counted wait is a whole number of
+    per-chunk DMA groups (G = weight + x instructions per wave) up to R - 1, the
+    steady-state wait (R - 2 groups still in flight) exists, and the fragment reads of
+    a chunk are fenced by an explicit lgkmcnt(0) before the barrier that frees the slot."""
+    asm, _ = _compile("gemm_mw", tmp_path)
+    ks = _kernels(asm, "_ZN3xgk15gemm_mw3_kernel")
+    assert len(ks) >= 10, len(ks)
+    for name, body in ks.items():
+        WN, NWT, MTW, R, _nt = _targs(name)[:5]
+        G = WN * 16 * NWT // 64 + (8 // WN) * 16 * MTW // 64
+        allowed = {k * G for k in range(R)}
+        got = _vmcnts(_pipeline(body, through_barrier=True))
+        assert got <= allowed, (name, sorted(got), sorted(allowed))
+        if R >= 3:
+            assert (R - 2) * G in got, (name, sorted(got))
+        # every in-loop barrier (all but the prologue's) follows its wave's lgkmcnt(0)
+        segs = body.split("s_barrier")[1:-1]
+        assert segs and all("lgkmcnt(0)" in seg for seg in segs), name
+    _no_spills(asm)
+
+
 def test_gemm_m64g_waits_are_counted(tmp_path):
     asm, log = _compile("gemm_m64g", tmp_path)
     assert "reserved registers on the clobber list" not in log

@@ -156,7 +156,7 @@ def test_gemm_m64_rejects_bad_shapes():
 
 # ---------------------------------------------------------------- gemm_mw (64 < M <= 320)
 @pytest.mark.parametrize("M", [65, 100, 128, 192, 257, 320])
-@pytest.mark.parametrize("cfg", list(range(15)))
+@pytest.mark.parametrize("cfg", list(range(22)))
 def test_gemm_mw_partial_every_cfg(M, cfg):
     """Every ring depth / tile width, incl. uneven split-K chunk ranges (K / 64 = 22
     chunks over S = 3 and 5) and short splits (1-2 chunks per split)."""
@@ -169,9 +169,10 @@ def test_gemm_mw_partial_every_cfg(M, cfg):
         try:
             pend = mw_linear(x, w, MODE_PARTIAL, plan=(S, cfg))
         except ValueError:
-            # x tiles beyond the cfg's LDS budget: 320 rows fit cfg 2 only of 0-6; the deep
-            # split-role rings 12-14 take M <= 128, 7 / 8 / 10 / 11 M <= 256, 9 M <= 192
-            limit = {2: 320, 9: 192, 12: 128, 13: 128, 14: 128}.get(cfg, 256)
+            # x tiles beyond the cfg's LDS / register budget: 320 rows fit cfg 2 only of 0-6;
+            # the deep split-role rings 12-14 take M <= 128, 7 / 8 / 10 / 11 M <= 256, 9 M <= 192;
+            # the pipelined 15-21 (two fragment sets in registers) M <= 128 / 192 / 256
+            limit = {2: 320, 9: 192, 12: 128, 13: 128, 14: 128, 15: 192, 16: 192, 17: 192, 18: 256, 19: 128, 20: 128, 21: 128}.get(cfg, 256)
             assert M > limit, (M, cfg)
             return
         assert pend.part.shape == (S, M, N)
@@ -190,10 +191,10 @@ def test_gemm_mw_llama_shapes(M, N, K):
 
 
 @pytest.mark.parametrize("M", [65, 128, 192, 257, 320])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21])
 def test_gemm_mw_silu_and_bf16(M, cfg):
     from xgserve.ops.linear import MW_CFGS, mw_linear
-    if M > {2: 320, 9: 192, 12: 128, 13: 128, 14: 128}.get(cfg, 256):
+    if M > {2: 320, 9: 192, 12: 128, 13: 128, 14: 128, 15: 192, 16: 192, 17: 192, 18: 256, 19: 128, 20: 128, 21: 128}.get(cfg, 256):
         pytest.skip("x tile beyond this configuration's LDS budget")
     F_, H = 2 * MW_CFGS[cfg][0], 1024
     x = rnd(M, H)
@@ -274,13 +275,13 @@ def test_gemm_m64g_uneven_splits(M, N, K, nw, S, cfg):
 
 
 @pytest.mark.parametrize("M", [1, 64, 192])
-@pytest.mark.parametrize("cfg,ss_n", [(7, 4), (8, 16), (10, 1), (12, 4)])
+@pytest.mark.parametrize("cfg,ss_n", [(7, 4), (8, 16), (10, 1), (12, 4), (15, 4), (18, 16), (21, 1)])
 def test_gemm_mw_norm_row_scale(M, cfg, ss_n):
     """gemm_mw's input-RMSNorm row scale (split-role configurations): the raw residual
     rows times (W diag(g))^T, scaled by rsqrt(sum of ss_n partial squares / K + eps),
     equals rmsnorm(x, g) @ W^T -- partial and SiLU epilogues."""
     from xgserve.ops.linear import MW_CFGS, RowStats, mw_norm_linear
-    if M > {12: 128}.get(cfg, 256):
+    if M > {12: 128, 15: 192, 21: 128}.get(cfg, 256):
         pytest.skip("x tile beyond the LDS budget")
     H, N = 1024, 2 * MW_CFGS[cfg][0]
     x = rnd(M, H)

@@ -232,11 +232,14 @@ def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split
 # cfg -> (columns per workgroup, weight ring depth, non-temporal weight DMA)
 # (0-4: 4 x 2 waves as N x M; 5-6: 2 x 4 waves -- fewer LDS fragment reads per MFMA;
 # 7-14: split DMA roles -- waves 0-3 stream the weights through a deep ring, waves 4-7
-# the x tile; the depth is the weight ring's slot count)
+# the x tile; the depth is the weight ring's slot count; 15-21: software-pipelined
+# fragment reads -- one ring of whole chunks, chunk c + 1 read under chunk c's MFMAs)
 MW_CFGS = {0: (256, 2, True), 1: (128, 3, True), 2: (128, 2, True), 3: (256, 2, False), 4: (128, 3, False),
            5: (128, 3, True), 6: (256, 2, True),
            7: (128, 6, True), 8: (128, 6, True), 9: (128, 5, True), 10: (256, 3, True), 11: (256, 3, True),
-           12: (128, 8, True), 13: (128, 8, True), 14: (256, 4, True)}
+           12: (128, 8, True), 13: (128, 8, True), 14: (256, 4, True),
+           15: (128, 4, True), 16: (128, 3, True), 17: (128, 4, True), 18: (128, 3, True), 19: (128, 5, True),
+           20: (256, 3, True), 21: (128, 5, True)}
 MW_MAX_M = 320   # M > 256 (a 320-row x tile) fits the LDS on cfg 2 only
 # (N, K, mode) -> {M bucket (128 / 192 / 256 / 320): (split_k, cfg)}, measured on MI355X with cold
 # weights (bench/gemm_bench.py --mw-sweep); other shapes take the default rule in mw_plan
