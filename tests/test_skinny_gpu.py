@@ -300,3 +300,14 @@ def test_gemm_mw_norm_row_scale(M, cfg, ss_n):
     got = mw_norm_linear(x, wi, MODE_SILU, st, 1e-5, plan=(1, cfg))
     ref = torch.nn.functional.silu(xn @ g.float().t()) * (xn @ u.float().t())
     assert rel_err(got, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 17, 64, 65, 128, 192, 256])
+def test_lm_head_linear_matches_fp32(M):
+    """The LM head (Llama-3 vocab 128,256 x 4,096): gemm_mw where a measured plan exists
+    (M >= LM_HEAD_MW_MIN_M), hipBLASLt otherwise -- bf16 logits vs fp32."""
+    from xgserve.ops.linear import lm_head_linear
+    h, w = rnd(M, 4096), rnd(128256, 4096, scale=0.02)
+    got = lm_head_linear(h, w)
+    assert got.shape == (M, 128256) and got.dtype == torch.bfloat16
+    assert rel_err(got, h.float() @ w.float().t()) < 1e-2

@@ -243,7 +243,12 @@ MW_CFGS = {0: (256, 2, True), 1: (128, 3, True), 2: (128, 2, True), 3: (256, 2, 
 MW_MAX_M = 320   # M > 256 (a 320-row x tile) fits the LDS on cfg 2 only
 # (N, K, mode) -> {M bucket (128 / 192 / 256 / 320): (split_k, cfg)}, measured on MI355X with cold
 # weights (bench/gemm_bench.py --mw-sweep); other shapes take the default rule in mw_plan
-_MW_TUNED = {}
+_MW_TUNED = {
+    # Llama-3 LM head, bf16 logits (profiles/r4_mw_sweep_rot.jsonl, K-chunk rotation on):
+    # 64 rows 170.4 us (hipBLASLt 212), 128 rows 175.5 (237), 192 219.5 (257), 256 267 (299)
+    (128256, 4096, MODE_BF16): {128: (1, 0), 192: (1, 6), 256: (1, 6)},
+}
+LM_HEAD_MW_MIN_M = 17  # batch <= 16 keeps the library GEMM (not swept)
 
 
 def _mw_bucket(M: int) -> int:
@@ -296,7 +301,7 @@ def lm_head_linear(h: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     this row bucket (_MW_TUNED, mode bf16), else hipBLASLt."""
     M, K = h.shape
     N = w.shape[0]
-    if (h.is_cuda and 1 <= M <= MW_MAX_M and h.is_contiguous() and w.is_contiguous()
+    if (h.is_cuda and LM_HEAD_MW_MIN_M <= M <= MW_MAX_M and h.is_contiguous() and w.is_contiguous()
             and _mw_bucket(M) in _MW_TUNED.get((N, K, MODE_BF16), {})):
         return mw_linear(h, w, MODE_BF16)
     return torch.nn.functional.linear(h, w)
