@@ -173,6 +173,18 @@ r4h)  # round 4: K-chunk rotation -- kernel tests, m64g / mw / LM-head sweeps, e
   done
   run c1 150 $B --concurrency 1 --steps 200 --warmup 20 "$@"
   run c1_off 150 env XGS_KROT=0 $B --concurrency 1 --steps 200 --warmup 20 "$@" ;;
+r4i)  # round 4: full GPU tests + smoke + headline with rotation and the LM head on gemm_mw; MoE rotation A/B
+  pyt_soft gputests 900 tests -m gpu --maxfail=10
+  run smoke 150 python -u -c "import __graft_entry__ as g; g.smoke()"
+  run bench_driver 200 $B --steps 20 --warmup 5 "$@"
+  run c64_long 240 env XGS_STEP_LOG="$o/steps_c64.jsonl" $B --steps 600 --warmup 60 "$@"
+  run c1 150 $B --concurrency 1 --steps 200 --warmup 20 "$@"
+  for v in "XGS_KROT=1" "XGS_KROT=0"; do
+    n=$(echo "$v" | tr -c 'A-Za-z0-9_=\n' '_')
+    run "mixtral_c1_$n" 200 env $v $B --model mixtral-8x7b --concurrency 1 --steps 60 --warmup 10
+    run "mixtral_c64_$n" 240 env $v $B --model mixtral-8x7b --steps 120 --warmup 20
+  done
+  bash bench/profile.sh "$o/prof_c64" "$@" ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;

@@ -487,7 +487,7 @@ template <int NW, int WV, int KC, bool NT, int MT>
 __device__ __forceinline__ void grouped_body(const uint16_t* __restrict__ x, const int32_t* __restrict__ rows, int e,
                                              int p0, int p1, int rt0, int K, const uint16_t* __restrict__ w, int N,
                                              int P, float* __restrict__ part, uint16_t* __restrict__ out, int mode,
-                                             uint8_t* lds0, uint8_t* lds1, uint8_t* lds2) {
+                                             uint8_t* lds0, uint8_t* lds1, uint8_t* lds2, int krot) {
   constexpr int RB = KC * 2;
   constexpr int GPR = KC / 8;
   constexpr int RPI = 1024 / RB;
@@ -529,8 +529,11 @@ __device__ __forceinline__ void grouped_body(const uint16_t* __restrict__ x, con
       if (src < 0) src = first;
       xsrc[i] = x + static_cast<int64_t>(src) * K + k0 + 8 * (dj ^ (r & (GPR - 1)));
     }
+    // K-chunk rotation (k_rotation): expert e's column tiles spread over K
+    const int rot = krot ? static_cast<int>((blockIdx.x * 37u + e * 11u) % static_cast<unsigned>(nchunks)) : 0;
     auto issue = [&](uint8_t* slot, int c) {
-      const int kk = c * KC;
+      const int cr = c + rot;
+      const int kk = (cr >= nchunks ? cr - nchunks : cr) * KC;
 #pragma unroll
       for (int i = 0; i < XI; ++i) glds16(xsrc[i] + kk, slot + RPI * (wid * XI + i) * RB);
       if (nt) {
@@ -650,7 +653,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
                                                                        const int32_t* __restrict__ valid, int E,
                                                                        int K, const uint16_t* __restrict__ w, int N,
                                                                        int P, float* __restrict__ part,
-                                                                       uint16_t* __restrict__ out, int mode) {
+                                                                       uint16_t* __restrict__ out, int mode,
+                                                                       int krot) {
   constexpr int SLOT = 16 * MT_MAX * KC * 2 + WV * 16 * NW * KC * 2;
   __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
@@ -684,7 +688,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
       const int need = (real + 63) >> 6;           // tiles holding real rows (they lead the segment)
       if (need >= 2) {
         if (lt != gs) return;                      // the group leader takes the group's real tiles
-        grouped_body<NW, WV, KC, NT, 8>(x, rows, e, p0, p1, r0, K, w, N, P, part, out, mode, lds0, lds1, lds2);
+        grouped_body<NW, WV, KC, NT, 8>(x, rows, e, p0, p1, r0, K, w, N, P, part, out, mode, lds0, lds1, lds2, krot);
         return;
       }
     }
@@ -699,18 +703,18 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
   constexpr bool MT1_OK = (16 / RPI / WV) >= 1;  // one 16-row x sub-tile is >= one DMA per wave
   if constexpr (MT_MAX >= 4) {
     if (amt > 2) {
-      grouped_body<NW, WV, KC, NT, 4>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2);
+      grouped_body<NW, WV, KC, NT, 4>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2, krot);
       return;
     }
   }
   if constexpr (MT_MAX >= 2) {
     if (amt == 2 || !MT1_OK) {
-      grouped_body<NW, WV, KC, NT, 2>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2);
+      grouped_body<NW, WV, KC, NT, 2>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2, krot);
       return;
     }
   }
   if constexpr (MT1_OK)
-    grouped_body<NW, WV, KC, NT, 1>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2);
+    grouped_body<NW, WV, KC, NT, 1>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2, krot);
 }
 
 int m64g_cfg_kc(int cfg);
@@ -721,7 +725,7 @@ static void launch_m64g_grouped(int cfg, dim3 grid, hipStream_t st, const uint16
                                 int P, float* part, uint16_t* out, int mode, bool mt1, bool mt8) {
 #define XGK_GRP_MT(WV, KC, NT, MT)                                                                              \
   hipLaunchKernelGGL((gemm_m64g_grouped_kernel<NW, WV, KC, NT, MT>), grid, dim3(64 * WV), 0, st, x, rows, offs, \
-                     valid, E, K, w, N, P, part, out, mode)
+                     valid, E, K, w, N, P, part, out, mode, k_rotation(static_cast<int>(grid.y)))
 #define XGK_GRP(WV, KC, NT)              \
   do {                                   \
     if (mt1) XGK_GRP_MT(WV, KC, NT, 1);  \
