@@ -266,3 +266,20 @@ def test_stall_free_sampling_seeded(llama_small):
     _, b, eng = _run_stall_free(llama_small, 128, temperature=0.8)
     assert a == b
     assert eng.runner.mixed_replays >= 6
+
+
+def test_whole_prompt_mixed_graphs_on_library_gemms(llama_small):
+    """decode_prefill_cap = 512: a whole prompt (<= 512 tokens) rides one decode step as
+    a captured mixed graph whose GEMMs are the library ones (rows > MW_MAX_TOKENS); every
+    greedy token is the fp32 reference's argmax up to a bf16 near-tie."""
+    prompts, outs, eng = _run_stall_free(llama_small, 512)
+    assert eng.runner.mixed_chunk == 512 and eng.runner.mixed_graphs
+    assert eng.runner.mixed_replays >= 3, eng.runner.mixed_replays
+    for rid, gen in outs.items():
+        assert len(gen) == (24 if rid.startswith("d") else 6), rid
+        p = prompts[rid]
+        ref = reference_logits(llama_small, p + gen[:-1]).float()
+        for i, tok in enumerate(gen):
+            row = ref[len(p) - 1 + i]
+            assert float(row.max() - row[tok]) < 0.15, (rid, i)
+    assert eng.sched.num_inflight() == 0 and eng.sched.num_running() == 0

@@ -154,10 +154,13 @@ class ModelRunner:
         self.mixed_bs: List[int] = []
         self.mixed_replays = 0
         if self.mixed_chunk > 0:
-            # decode rows + chunk on gemm_mw when every layer has it (<= MW_MAX_TOKENS rows),
-            # else the library GEMMs (graph-capturable too)
+            # decode rows + chunk run on gemm_mw when every layer has it and they fit
+            # (<= MW_MAX_TOKENS rows), else on the library GEMMs (graph-capturable too): a
+            # chunk of a whole prompt (e.g. 512) replays as one graph instead of an eager
+            # step whose host-side launch of ~400 kernels the GPU would wait on
             from ..models.llama import MW_MAX_TOKENS
-            lim = MW_MAX_TOKENS if getattr(model, "_mw_ok", False) else max_num_batched_tokens
+            mw = getattr(model, "_mw_ok", False) and 16 + self.mixed_chunk <= MW_MAX_TOKENS
+            lim = MW_MAX_TOKENS if mw else max_num_batched_tokens
             self.mixed_bs = [b for b in self.graph_bs if b >= 16 and b + self.mixed_chunk <= lim]
             if not self.mixed_bs:
                 self.mixed_chunk = 0
