@@ -29,10 +29,12 @@ def _port() -> int:
         return s.getsockname()[1]
 
 
+import torch  # noqa: E402  (imported before the workers set their env, as in tests/test_custom_ar_gpu.py)
+
+
 def _rank(rank, world, port, calls, reps, q):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0",
                        "GPU_MAX_HW_QUEUES": "1"})
-    import torch
     import torch.distributed as dist
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)

@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--iters", type=int, default=70)
     ap.add_argument("--bs", type=int, default=16)
     ap.add_argument("--depth", type=int, nargs="+", default=[2])
+    ap.add_argument("--probe", action="store_true",
+                    help="anatomy: also time the kernel without its prologue (11), key loop (12), both (13)")
     a = ap.parse_args()
     dev, Hq, Hkv, D, bs = "cuda", 32, 8, 128, a.bs
     B = a.B
@@ -67,7 +69,8 @@ def main():
         ops.decode_attention_fused(pend, pos, slots[i % len(caches)], cs, kc, vc, bt, lens, Hq, sc, S, ws, out=out,
                                    depth=dp)
 
-    for S, dp, mode in [(S, dp, m) for S in a.splits for dp in a.depth for m in ("warm", "cold")]:
+    depths = list(a.depth) + ([11, 12, 13] if a.probe else [])
+    for S, dp, mode in [(S, dp, m) for S in a.splits for dp in depths for m in ("warm", "cold")]:
         if True:
             f = (lambda i: run(0, S, dp)) if mode == "warm" else (lambda i: run(i, S, dp))
             for i in range(2 * len(caches)):

@@ -185,6 +185,12 @@ r4i)  # round 4: full GPU tests + smoke + headline with rotation and the LM head
     run "mixtral_c64_$n" 240 env $v $B --model mixtral-8x7b --steps 120 --warmup 20
   done
   bash bench/profile.sh "$o/prof_c64" "$@" ;;
+r4j)  # round 4: whole-prompt mixed graphs (library GEMMs) A/B, decode-attention anatomy
+  pyt mixed_tests 300 tests/test_engine_gpu.py -k "whole_prompt or stall_free"
+  run attn_probe 200 python -u bench/decode_cold.py --L 768 --splits 1 --probe
+  run c64_chunk512 240 env XGS_STEP_LOG="$o/steps_chunk512.jsonl" $B --steps 600 --warmup 60 --prefill-chunk 512 "$@"
+  run c64_chunk512_driver 200 $B --steps 20 --warmup 5 --prefill-chunk 512 "$@"
+  run c64_base 240 env XGS_STEP_LOG="$o/steps_base.jsonl" $B --steps 600 --warmup 60 "$@" ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;

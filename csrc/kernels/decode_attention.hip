@@ -189,7 +189,10 @@ __device__ __forceinline__ float combine_splits(const float* __restrict__ lse, c
 // (Measured and removed, A/B records in profiles/: an in-launch split combine by the
 // last-arriving split, r1_inlaunch_combine_ab.md; O-weight prefetch workgroups inside
 // this launch, r1_attn_prefetch_ab.md; 8 waves per workgroup, r1_decode_waves_c1.md.)
-template <int D, int G, bool FQ, bool KL = false, int NB = 2>
+// PR (anatomy probes, bench/decode_cold.py --probe; output garbage): 0 = the kernel;
+// 1 = no fused prologue (no QKV-partial reads / RoPE / KV append); 2 = no key loop;
+// 3 = neither (launch + merge + store only).
+template <int D, int G, bool FQ, bool KL = false, int NB = 2, int PR = 0>
 __global__ void __launch_bounds__(256) decode_attn_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ seq_lens,
@@ -245,15 +248,18 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   // bytes do not depend on q), so the K/V latency overlaps the QKV-partial reads --
   // except the tile holding the key the prologue appends (the last one), which is
   // loaded after the prologue's barrier as before
+  constexpr bool LOOP = PR != 2 && PR != 3;
   bool pre[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int tj = t0 + j * C::WAVES;
-    pre[j] = FQ && tj < t_end && tj != ntiles - 1;
+    pre[j] = LOOP && FQ && tj < t_end && tj != ntiles - 1;
     if (pre[j]) load_tile(tj, kf[j], vr[j]);
   }
   if constexpr (FQ) {
-    if (L > 0) decode_qkv_prologue<D, G>(fq, b, kvh, Hq, Hkv, bs, split == (ntiles - 1) / tps, q_lds);
+    if constexpr (PR != 1 && PR != 3) {
+      if (L > 0) decode_qkv_prologue<D, G>(fq, b, kvh, Hq, Hkv, bs, split == (ntiles - 1) / tps, q_lds);
+    }
     __syncthreads();
   }
 
@@ -351,9 +357,9 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int tj = t0 + j * C::WAVES;
-    if (tj < t_end && !pre[j]) load_tile(tj, kf[j], vr[j]);
+    if (LOOP && tj < t_end && !pre[j]) load_tile(tj, kf[j], vr[j]);
   }
-  for (int t = t0; t < t_end; t += NB * C::WAVES) {
+  for (int t = t0; LOOP && t < t_end; t += NB * C::WAVES) {
     bool done = false;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -422,6 +428,17 @@ static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, con
   // fragment-shaped K loads measured 0.5-6 % faster. depth 3: three register tiles
   // in flight per wave (fused form, G <= 4)
   if constexpr (D == 128 && G <= 4 && FQ) {
+    if (depth >= 11 && depth <= 13) {  // anatomy probes (depth = 10 + PR)
+#define XGK_DECP(P)                                                                                                 \
+  hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, true, 2, P>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt, \
+                     bts, sl, po, pl, out, os, Hq, Hkv, bs, scale, S, fq)
+      if (depth == 11) XGK_DECP(1);
+      else if (depth == 12) XGK_DECP(2);
+      else XGK_DECP(3);
+#undef XGK_DECP
+      if (S > 1) hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
+      return;
+    }
     if (depth == 3) {
       hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, true, 3>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc,
                          bt, bts, sl, po, pl, out, os, Hq, Hkv, bs, scale, S, fq);
@@ -468,7 +485,7 @@ int decode_attention_fq(const float* part, int S_qkv, const int32_t* positions, 
   if (B <= 0) return 0;
   if (part == nullptr || S_qkv < 1 || bs % 16 != 0 || Hq % Hkv != 0 || D != 128 || num_splits < 1) return -1;
   if (num_splits > 1 && (part_out == nullptr || part_lse == nullptr)) return -1;
-  if (out == nullptr || depth < 2 || depth > 3) return -1;
+  if (out == nullptr || depth < 2 || (depth > 3 && (depth < 11 || depth > 13))) return -1;
   const QkvFuse fq{part, S_qkv, positions, cos_sin, slots, kc, vc, apply_rope};
   const int G = Hq / Hkv;
 #define XGK_DECF(GG)                                                                                         \
