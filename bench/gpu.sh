@@ -191,6 +191,18 @@ r4j)  # round 4: whole-prompt mixed graphs (library GEMMs) A/B, decode-attention
   run c64_chunk512 240 env XGS_STEP_LOG="$o/steps_chunk512.jsonl" $B --steps 600 --warmup 60 --prefill-chunk 512 "$@"
   run c64_chunk512_driver 200 $B --steps 20 --warmup 5 --prefill-chunk 512 "$@"
   run c64_base 240 env XGS_STEP_LOG="$o/steps_base.jsonl" $B --steps 600 --warmup 60 "$@" ;;
+r4k)  # round 4: Mixtral profiles (batch 1, 64 concurrent, TP2 shard), AR latency at world 4 / 8
+  bash bench/profile.sh "$o/prof_mixtral_c1" --model mixtral-8x7b --concurrency 1
+  bash bench/profile.sh "$o/prof_mixtral_c64" --model mixtral-8x7b
+  run mixtral_tp2_c64 300 $B --model mixtral-8x7b --tp-shard 2 --steps 60 --warmup 20
+  run ar_w4 200 python -u bench/ar_bench.py --world 4
+  run ar_w8 240 python -u bench/ar_bench.py --world 8 ;;
+r4l)  # round 4: one-round-trip MoE router -- MoE tests, Mixtral batch 1 / 64 concurrent / TP2 shard
+  pyt moe_tests 400 tests/test_kernels_gpu.py tests/test_fused_decode_gpu.py tests/test_engine_gpu.py -k "moe or mixtral or expert or route"
+  run mixtral_c1 200 $B --model mixtral-8x7b --concurrency 1 --steps 100 --warmup 10
+  run mixtral_c64 240 $B --model mixtral-8x7b --steps 120 --warmup 20
+  run mixtral_tp2_c64 300 $B --model mixtral-8x7b --tp-shard 2 --steps 60 --warmup 20
+  run mixtral_tp2_c1 200 $B --model mixtral-8x7b --tp-shard 2 --concurrency 1 --steps 100 --warmup 10 ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;

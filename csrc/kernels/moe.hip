@@ -164,12 +164,139 @@ __global__ void __launch_bounds__(256) route_kernel(const uint16_t* __restrict__
   }
 }
 
+// One-round-trip router (route2): 512 threads, each owning CPT 8-element chunks of the
+// hidden row; every load the workgroup needs (the row, the norm weight, all E router
+// rows) is issued before any arithmetic, so the launch costs one memory latency instead
+// of route_kernel's three dependent rounds (norm pass, then per-chunk router loads):
+// Mixtral batch 1 spent 10.8 us per layer in route_kernel<8, true> (profiles/
+// r4_mixtral_c1_kernels.md) on 8 KB of activations + 64 KB of router weights.
+template <int EM, bool NORM, int CPT>
+__global__ void __launch_bounds__(512) route2_kernel(const uint16_t* __restrict__ h, const uint16_t* __restrict__ wr,
+                                                     int H, int E, int k, int renorm, float* __restrict__ w,
+                                                     int32_t* __restrict__ ids, const uint16_t* __restrict__ norm_w,
+                                                     float eps, uint16_t* __restrict__ hn) {
+  constexpr int NWV = 8;
+  __shared__ float red[NWV][EM + 1];
+  const int t = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nch = H / 8;
+  const uint16_t* hr = h + static_cast<int64_t>(t) * H;
+  uint4 xv[CPT], gv[CPT], rv[CPT][EM];
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int c = min(threadIdx.x + 512 * i, nch - 1);
+    xv[i] = ld16(hr + c * 8);
+    if constexpr (NORM) gv[i] = ld16(norm_w + c * 8);
+#pragma unroll
+    for (int e = 0; e < EM; ++e) rv[i][e] = ld16(wr + static_cast<int64_t>(min(e, E - 1)) * H + c * 8);
+  }
+  float scale = 1.f;
+  if constexpr (NORM) {
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      if (threadIdx.x + 512 * i >= nch) break;
+      float x[8];
+      unpack8(xv[i], x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += x[j] * x[j];
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) red[wid][EM] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int v = 0; v < NWV; ++v) tot += red[v][EM];
+    scale = rsqrtf(tot / static_cast<float>(H) + eps);
+  }
+  float acc[EM];
+#pragma unroll
+  for (int e = 0; e < EM; ++e) acc[e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int c = threadIdx.x + 512 * i;
+    if (c >= nch) break;
+    float x[8];
+    unpack8(xv[i], x);
+    if constexpr (NORM) {
+      float g[8];
+      unpack8(gv[i], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = x[j] * scale * g[j];
+      const uint4 q = pack8(x);
+      st16(hn + static_cast<int64_t>(t) * H + c * 8, q);
+      unpack8(q, x);  // route on the bf16 values the experts will see
+    }
+#pragma unroll
+    for (int e = 0; e < EM; ++e) {
+      float r[8];
+      unpack8(rv[i][e], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[e] += x[j] * r[j];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EM; ++e) {
+    const float v = wave_sum(acc[e]);
+    if (lane == 0) red[wid][e] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  float v[EM];
+  float mx = -INFINITY;
+  for (int e = 0; e < E; ++e) {
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < NWV; ++q) sum += red[q][e];
+    v[e] = sum;
+    mx = fmaxf(mx, v[e]);
+  }
+  float den = 0.f;
+  for (int e = 0; e < E; ++e) den += __expf(v[e] - mx);
+  unsigned long long used = 0;
+  float sel[16];
+  int sid[16];
+  float ssum = 0.f;
+  for (int j = 0; j < k; ++j) {
+    int best = -1;
+    float bv = -INFINITY;
+    for (int e = 0; e < E; ++e)
+      if (!((used >> e) & 1ull) && (best < 0 || v[e] > bv)) { best = e; bv = v[e]; }
+    used |= 1ull << best;
+    sid[j] = best;
+    sel[j] = __expf(bv - mx) / den;
+    ssum += sel[j];
+  }
+  for (int j = 0; j < k; ++j) {
+    w[static_cast<int64_t>(t) * k + j] = renorm ? sel[j] / ssum : sel[j];
+    ids[static_cast<int64_t>(t) * k + j] = sid[j];
+  }
+}
+
 int moe_route(const uint16_t* h, const uint16_t* wr, int T, int H, int E, int k, int renorm, float* w, int32_t* ids,
               hipStream_t st, const uint16_t* norm_w, float eps, uint16_t* hn) {
   if (T <= 0) return 0;
   if (H % 8 || E < 1 || E > 64 || k < 1 || k > 16 || k > E) return 1;
   if ((norm_w == nullptr) != (hn == nullptr)) return 1;
   const dim3 g(T), b(256);
+  // up to 8 experts and 4 chunks per thread (H <= 16384): the one-round-trip router
+  if (E <= 8 && H <= 8 * 512 * 4) {
+    const int cpt = (H / 8 + 511) / 512;
+#define XGK_R2(NORM, CPT)                                                                                         \
+  hipLaunchKernelGGL((route2_kernel<8, NORM, CPT>), g, dim3(512), 0, st, h, wr, H, E, k, renorm, w, ids, norm_w, \
+                     eps, hn)
+    if (norm_w != nullptr) {
+      if (cpt == 1) XGK_R2(true, 1);
+      else if (cpt == 2) XGK_R2(true, 2);
+      else XGK_R2(true, 4);
+    } else {
+      if (cpt == 1) XGK_R2(false, 1);
+      else if (cpt == 2) XGK_R2(false, 2);
+      else XGK_R2(false, 4);
+    }
+#undef XGK_R2
+    return 0;
+  }
   if (norm_w != nullptr) {
     if (E <= 8) hipLaunchKernelGGL((route_kernel<8, true>), g, b, 0, st, h, wr, H, E, k, renorm, w, ids, norm_w, eps, hn);
     else if (E <= 16) hipLaunchKernelGGL((route_kernel<16, true>), g, b, 0, st, h, wr, H, E, k, renorm, w, ids, norm_w, eps, hn);

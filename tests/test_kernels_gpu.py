@@ -397,7 +397,8 @@ def test_fused_moe_expert_parallel_shard():
     torch.testing.assert_close(half0 + half1, full, atol=4e-2, rtol=4e-2)
 
 
-@pytest.mark.parametrize("T,E,k,H", [(1, 8, 2, 4096), (64, 8, 2, 4096), (5, 16, 4, 512), (3, 64, 6, 1024)])
+@pytest.mark.parametrize("T,E,k,H", [(1, 8, 2, 4096), (64, 8, 2, 4096), (5, 16, 4, 512), (3, 64, 6, 1024),
+                                     (2, 4, 1, 8192), (7, 8, 2, 14336), (1, 6, 2, 1000)])
 def test_moe_route_matches_fp32(T, E, k, H):
     h = rnd(T, H)
     router = rnd(E, H, scale=0.05)
@@ -461,3 +462,19 @@ def test_ep_dispatch_kernels_match_torch(Ts, k, E_local, tp, packed):
     want = (back.cpu().float()[s.long().cpu()] * w.cpu().reshape(-1, 1)).view(Ts, k, H).sum(1)
     torch.testing.assert_close(out[:Ts].cpu().float(), want, atol=2e-2, rtol=1e-2)
     assert bool((out[Ts:] == 0).all())
+
+
+@pytest.mark.parametrize("T,E,k,H", [(1, 8, 2, 4096), (33, 8, 2, 4096), (2, 4, 1, 8192), (3, 8, 2, 14336)])
+def test_moe_route_norm_matches_fp32(T, E, k, H):
+    """Router with the RMSNorm prologue (one-round-trip route2 kernel, 1 / 2 / 4 chunks
+    per thread): normalised rows vs fp32 up to one bf16 rounding, routing on them."""
+    h = rnd(T, H)
+    g = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16()
+    router = rnd(E, H, scale=0.05)
+    hn, w, ids = ops.moe_route_norm(h, g, 1e-5, router, k)
+    hf = h.float()
+    want = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()
+    torch.testing.assert_close(hn.float(), want, atol=2e-2, rtol=1e-2)
+    rw, rids = ops.moe_topk_softmax((hn.float() @ router.float().t()).cpu(), k)
+    assert torch.equal(ids.cpu().long().sort(-1).values, rids.long().sort(-1).values)
+    torch.testing.assert_close(w.cpu().sort(-1).values, rw.sort(-1).values, atol=1e-4, rtol=1e-4)
