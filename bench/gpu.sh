@@ -203,6 +203,10 @@ r4l)  # round 4: one-round-trip MoE router -- MoE tests, Mixtral batch 1 / 64 co
   run mixtral_c64 240 $B --model mixtral-8x7b --steps 120 --warmup 20
   run mixtral_tp2_c64 300 $B --model mixtral-8x7b --tp-shard 2 --steps 60 --warmup 20
   run mixtral_tp2_c1 200 $B --model mixtral-8x7b --tp-shard 2 --concurrency 1 --steps 100 --warmup 10 ;;
+r4m)  # round 4: re-sweep the batch-1 / 32-row gemm_m64g plans with K rotation, then the headline and batch 1
+  run m64g_sweep_1 400 python -u bench/gemm_bench.py --m64g-sweep --M 1 32 --shapes qkv o gate_up down
+  run c64 240 $B --steps 600 --warmup 60 "$@"
+  run c1 150 $B --concurrency 1 --steps 200 --warmup 20 "$@" ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;
