@@ -170,13 +170,25 @@ __global__ void __launch_bounds__(256) route_kernel(const uint16_t* __restrict__
 // of route_kernel's three dependent rounds (norm pass, then per-chunk router loads):
 // Mixtral batch 1 spent 10.8 us per layer in route_kernel<8, true> (profiles/
 // r4_mixtral_c1_kernels.md) on 8 KB of activations + 64 KB of router weights.
+// Single-token steps (batch-1 decode) can take the expert layout of moe_align in the
+// same launch (RA.sorted_rows != nullptr): the one workgroup that routed the token
+// writes offsets / sorted_rows / dest exactly as align_kernel would for T = 1 (top-k
+// experts are distinct, so each holds at most one row) -- one launch less per layer.
+struct RouteAlign {
+  int32_t* sorted_rows;  // [cap]
+  int32_t* offsets;      // [E_local + 1]
+  int32_t* dest;         // [k]
+  int E_local, expert_offset, block_m, cap;
+};
+
 template <int EM, bool NORM, int CPT>
 __global__ void __launch_bounds__(512) route2_kernel(const uint16_t* __restrict__ h, const uint16_t* __restrict__ wr,
                                                      int H, int E, int k, int renorm, float* __restrict__ w,
                                                      int32_t* __restrict__ ids, const uint16_t* __restrict__ norm_w,
-                                                     float eps, uint16_t* __restrict__ hn) {
+                                                     float eps, uint16_t* __restrict__ hn, RouteAlign ra) {
   constexpr int NWV = 8;
   __shared__ float red[NWV][EM + 1];
+  __shared__ int s_off[EM + 1], s_pos[16];
   const int t = blockIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nch = H / 8;
@@ -241,7 +253,8 @@ __global__ void __launch_bounds__(512) route2_kernel(const uint16_t* __restrict_
     if (lane == 0) red[wid][e] = v;
   }
   __syncthreads();
-  if (threadIdx.x != 0) return;
+  const bool align = ra.sorted_rows != nullptr;  // T == 1 (host-checked)
+  if (threadIdx.x == 0) {
   float v[EM];
   float mx = -INFINITY;
   for (int e = 0; e < E; ++e) {
@@ -271,20 +284,52 @@ __global__ void __launch_bounds__(512) route2_kernel(const uint16_t* __restrict_
     w[static_cast<int64_t>(t) * k + j] = renorm ? sel[j] / ssum : sel[j];
     ids[static_cast<int64_t>(t) * k + j] = sid[j];
   }
+  if (align) {  // align_kernel's layout for the k pairs of this one token
+    int cnt[EM];
+    for (int e = 0; e < ra.E_local; ++e) cnt[e] = 0;
+    for (int j = 0; j < k; ++j) {
+      const int e = sid[j] - ra.expert_offset;
+      if (e >= 0 && e < ra.E_local) ++cnt[e];
+    }
+    s_off[0] = 0;
+    for (int e = 0; e < ra.E_local; ++e) s_off[e + 1] = s_off[e] + (cnt[e] + ra.block_m - 1) / ra.block_m * ra.block_m;
+    for (int j = 0; j < k; ++j) {
+      const int e = sid[j] - ra.expert_offset;
+      s_pos[j] = (e >= 0 && e < ra.E_local) ? s_off[e] : -1;  // distinct experts: one row each
+    }
+  }
+  }
+  if (!align) return;
+  __syncthreads();
+  for (int e = threadIdx.x; e <= ra.E_local; e += blockDim.x) ra.offsets[e] = s_off[e];
+  for (int j = threadIdx.x; j < k; j += blockDim.x) ra.dest[j] = s_pos[j];
+  for (int p = threadIdx.x; p < ra.cap; p += blockDim.x) {
+    int r = -1;
+    for (int j = 0; j < k; ++j)
+      if (s_pos[j] == p) r = 0;
+    ra.sorted_rows[p] = r;
+  }
 }
 
 int moe_route(const uint16_t* h, const uint16_t* wr, int T, int H, int E, int k, int renorm, float* w, int32_t* ids,
-              hipStream_t st, const uint16_t* norm_w, float eps, uint16_t* hn) {
+              hipStream_t st, const uint16_t* norm_w, float eps, uint16_t* hn, int32_t* al_rows, int32_t* al_offs,
+              int32_t* al_dest, int al_E, int al_eoff, int al_bm) {
   if (T <= 0) return 0;
   if (H % 8 || E < 1 || E > 64 || k < 1 || k > 16 || k > E) return 1;
   if ((norm_w == nullptr) != (hn == nullptr)) return 1;
   const dim3 g(T), b(256);
+  RouteAlign ra{nullptr, nullptr, nullptr, 0, 0, 1, 0};
+  if (al_rows != nullptr) {  // the layout in the same launch: one token, <= 8 local experts
+    if (T != 1 || E > 8 || al_E < 1 || al_E > 8 || al_bm < 1 || al_offs == nullptr || al_dest == nullptr) return 1;
+    const int cap = (k + al_E * (al_bm - 1) + al_bm - 1) / al_bm * al_bm;
+    ra = RouteAlign{al_rows, al_offs, al_dest, al_E, al_eoff, al_bm, cap};
+  }
   // up to 8 experts and 4 chunks per thread (H <= 16384): the one-round-trip router
   if (E <= 8 && H <= 8 * 512 * 4) {
     const int cpt = (H / 8 + 511) / 512;
 #define XGK_R2(NORM, CPT)                                                                                         \
   hipLaunchKernelGGL((route2_kernel<8, NORM, CPT>), g, dim3(512), 0, st, h, wr, H, E, k, renorm, w, ids, norm_w, \
-                     eps, hn)
+                     eps, hn, ra)
     if (norm_w != nullptr) {
       if (cpt == 1) XGK_R2(true, 1);
       else if (cpt == 2) XGK_R2(true, 2);
@@ -297,6 +342,7 @@ int moe_route(const uint16_t* h, const uint16_t* wr, int T, int H, int E, int k,
 #undef XGK_R2
     return 0;
   }
+  if (ra.sorted_rows != nullptr) return 1;
   if (norm_w != nullptr) {
     if (E <= 8) hipLaunchKernelGGL((route_kernel<8, true>), g, b, 0, st, h, wr, H, E, k, renorm, w, ids, norm_w, eps, hn);
     else if (E <= 16) hipLaunchKernelGGL((route_kernel<16, true>), g, b, 0, st, h, wr, H, E, k, renorm, w, ids, norm_w, eps, hn);

@@ -60,7 +60,7 @@ void moe_topk_softmax(const void*, int, int, int, int, int, float*, int32_t*, hi
 void moe_align(const int32_t*, int, int, int, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
 int moe_combine(const void*, int, int, const int32_t*, const float*, void*, int, int, int, hipStream_t, int);
 int moe_route(const uint16_t*, const uint16_t*, int, int, int, int, int, float*, int32_t*, hipStream_t,
-              const uint16_t*, float, uint16_t*);
+              const uint16_t*, float, uint16_t*, int32_t*, int32_t*, int32_t*, int, int, int);
 int moe_combine_resid(const float*, int, int, const int32_t*, const float*, uint16_t*, float*, int, int, int,
                       hipStream_t);
 int ep_plan(const int32_t*, int, int, int, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
@@ -329,13 +329,18 @@ PYBIND11_MODULE(_kernels, m) {
      py::arg("P"), py::arg("part"), py::arg("out"), py::arg("splits"), py::arg("mode"), py::arg("nw"), py::arg("cfg"),
      py::arg("max_rows"), py::arg("st"), py::arg("valid") = 0);
   m.def("moe_route", [](uintptr_t h, uintptr_t wr, int T, int H, int E, int k, int renorm, uintptr_t w, uintptr_t ids,
-                        uintptr_t st, uintptr_t norm_w, float eps, uintptr_t hn) {
-    // norm_w / hn != 0: h is the raw residual stream, normalised in-kernel (fused decode layer)
+                        uintptr_t st, uintptr_t norm_w, float eps, uintptr_t hn, uintptr_t al_rows, uintptr_t al_offs,
+                        uintptr_t al_dest, int al_E, int al_eoff, int al_bm) {
+    // norm_w / hn != 0: h is the raw residual stream, normalised in-kernel (fused decode layer);
+    // al_rows != 0 (T == 1): also moe_align's layout of this rank's al_E experts
     check(xgk::moe_route(P<const uint16_t>(h), P<const uint16_t>(wr), T, H, E, k, renorm, P<float>(w),
-                         P<int32_t>(ids), S(st), P<const uint16_t>(norm_w), eps, P<uint16_t>(hn)),
+                         P<int32_t>(ids), S(st), P<const uint16_t>(norm_w), eps, P<uint16_t>(hn), P<int32_t>(al_rows),
+                         P<int32_t>(al_offs), P<int32_t>(al_dest), al_E, al_eoff, al_bm),
           "moe_route");
   }, py::arg("h"), py::arg("wr"), py::arg("T"), py::arg("H"), py::arg("E"), py::arg("k"), py::arg("renorm"),
-     py::arg("w"), py::arg("ids"), py::arg("st"), py::arg("norm_w") = 0, py::arg("eps") = 0.f, py::arg("hn") = 0);
+     py::arg("w"), py::arg("ids"), py::arg("st"), py::arg("norm_w") = 0, py::arg("eps") = 0.f, py::arg("hn") = 0,
+     py::arg("al_rows") = 0, py::arg("al_offs") = 0, py::arg("al_dest") = 0, py::arg("al_E") = 0,
+     py::arg("al_eoff") = 0, py::arg("al_bm") = 64);
   m.def("moe_combine_resid", [](uintptr_t part, int splits, int P_, uintptr_t dest, uintptr_t w, uintptr_t resid,
                                 uintptr_t ss, int T, int k, int H, uintptr_t st) {
     if (H % 1024 || H > 8192) throw std::invalid_argument("moe_combine_resid: H % 1024 == 0, H <= 8192");

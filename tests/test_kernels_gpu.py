@@ -478,3 +478,19 @@ def test_moe_route_norm_matches_fp32(T, E, k, H):
     rw, rids = ops.moe_topk_softmax((hn.float() @ router.float().t()).cpu(), k)
     assert torch.equal(ids.cpu().long().sort(-1).values, rids.long().sort(-1).values)
     torch.testing.assert_close(w.cpu().sort(-1).values, rw.sort(-1).values, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("T,E_local,eoff", [(1, 8, 0), (1, 4, 4), (1, 4, 0), (1, 2, 6), (5, 8, 0)])
+def test_moe_route_norm_align_matches_moe_align(T, E_local, eoff):
+    """moe_route_norm(align=...): for one token the router launch writes moe_align's
+    layout itself (sorted_rows, offsets, dest), bit-identical to the align kernel's;
+    more tokens fall back to moe_align."""
+    H, E, k = 4096, 8, 2
+    h = rnd(T, H)
+    g = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16()
+    router = rnd(E, H, scale=0.05)
+    hn, w, ids, (rows, offs, dest) = ops.moe_route_norm(h, g, 1e-5, router, k, align=(E_local, eoff))
+    rows2, offs2, dest2 = ops.moe_align(ids, E_local, eoff)
+    assert torch.equal(offs.cpu(), offs2.cpu())
+    assert torch.equal(dest.cpu(), dest2.cpu())
+    assert torch.equal(rows.cpu(), rows2.cpu())

@@ -433,13 +433,15 @@ class LlamaLayer(nn.Module):
             comm.tp_allreduce_resid(po.part, resid, ws.ss[site])
         else:
             m64_resid_linear(a, self.o, resid, ws, site, eps)  # its statistics go unused: the router renorms
-        hn, w, ids = ops.moe_route_norm(resid, self.post_norm, eps, self.router, self.cfg.experts_per_token)
+        # one token (batch 1): the router launch also writes the expert layout
+        hn, w, ids, layout = ops.moe_route_norm(resid, self.post_norm, eps, self.router, self.cfg.experts_per_token,
+                                                align=(self.E_local, self.expert_offset))
         ss = ws.ss[site + 1]
         if self.tp > 1:
-            part = ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, out_f32=True)
+            part = ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, out_f32=True, layout=layout)
             comm.tp_allreduce_resid(part.unsqueeze(0), resid, ss)
         else:
-            ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, resid=resid, ss=ss)
+            ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, resid=resid, ss=ss, layout=layout)
         return RowStats(ss, H // 1024, T)
 
     def _fused_tp_tail(self, a: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace, site: int) -> RowStats:

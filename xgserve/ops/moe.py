@@ -57,22 +57,37 @@ def moe_route(h: torch.Tensor, router: torch.Tensor, k: int, renorm: bool = True
 
 
 def moe_route_norm(resid: torch.Tensor, norm_w: torch.Tensor, eps: float, router: torch.Tensor, k: int,
-                   renorm: bool = True):
+                   renorm: bool = True, align: Optional[Tuple[int, int]] = None):
     """Fused decode layer: RMSNorm of the raw residual stream + router + top-k in one
-    launch -> (hn = bf16 normalised rows for the experts, weights, expert ids)."""
+    launch -> (hn = bf16 normalised rows for the experts, weights, expert ids).
+    align = (E_local, expert_offset) and a single token: the same launch also writes
+    moe_align's expert layout, returned as a fourth value (fused_moe(layout=...))."""
     T, H = resid.shape
     if not use_native(resid):
         rf = resid.float()
         hn = (rf * torch.rsqrt(rf.pow(2).mean(-1, keepdim=True) + eps) * norm_w.float()).to(resid.dtype)
         w, ids = moe_route(hn, router, k, renorm)
-        return hn, w, ids
+        return (hn, w, ids) if align is None else (hn, w, ids, None)  # CPU: fused_moe runs the reference
     E = router.shape[0]
     hn = torch.empty_like(resid)
     w = torch.empty(T, k, dtype=torch.float32, device=resid.device)
     ids = torch.empty(T, k, dtype=torch.int32, device=resid.device)
+    fuse = align is not None and T == 1 and E <= 8 and align[0] <= 8
+    if fuse:
+        El, eoff = align
+        cap = (T * k + El * (BLOCK_M - 1) + BLOCK_M - 1) // BLOCK_M * BLOCK_M
+        layout = (torch.empty(cap, dtype=torch.int32, device=resid.device),
+                  torch.empty(El + 1, dtype=torch.int32, device=resid.device),
+                  torch.empty(T * k, dtype=torch.int32, device=resid.device))
+        al = dict(al_rows=layout[0].data_ptr(), al_offs=layout[1].data_ptr(), al_dest=layout[2].data_ptr(), al_E=El,
+                  al_eoff=eoff, al_bm=BLOCK_M)
+    else:
+        al = {}
     kernels().moe_route(resid.data_ptr(), router.data_ptr(), T, H, E, k, 1 if renorm else 0, w.data_ptr(),
-                        ids.data_ptr(), stream_ptr(), norm_w.data_ptr(), float(eps), hn.data_ptr())
-    return hn, w, ids
+                        ids.data_ptr(), stream_ptr(), norm_w.data_ptr(), float(eps), hn.data_ptr(), **al)
+    if align is None:
+        return hn, w, ids
+    return hn, w, ids, (layout if fuse else moe_align(ids, align[0], align[1]))
 
 
 def moe_align(ids: torch.Tensor, num_experts: int, expert_offset: int = 0, block_m: int = BLOCK_M):
@@ -118,7 +133,7 @@ def moe_forward_ref(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w
 
 def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
               topk_ids: torch.Tensor, expert_offset: int = 0, resid: Optional[torch.Tensor] = None,
-              ss: Optional[torch.Tensor] = None, out_f32: bool = False):
+              ss: Optional[torch.Tensor] = None, out_f32: bool = False, layout=None):
     """Local-expert MoE FFN: sum_j w_j * FFN_{e_j}(x) over choices owned locally
     (ids in [expert_offset, expert_offset + E_local)); others contribute nothing.
 
@@ -140,7 +155,8 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     T, k = topk_ids.shape
     E, F2, H = w13.shape
     F = F2 // 2
-    sorted_rows, offs, dest = moe_align(topk_ids, E, expert_offset)
+    # layout: moe_align's (sorted_rows, offsets, dest), e.g. from moe_route_norm(align=...)
+    sorted_rows, offs, dest = layout if layout is not None else moe_align(topk_ids, E, expert_offset)
     P = sorted_rows.shape[0]
     act = torch.empty(P, F, dtype=x.dtype, device=x.device)
     kn = kernels()
