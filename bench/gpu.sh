@@ -207,6 +207,18 @@ r4m)  # round 4: re-sweep the batch-1 / 32-row gemm_m64g plans with K rotation, 
   run m64g_sweep_1 400 python -u bench/gemm_bench.py --m64g-sweep --M 1 32 --shapes qkv o gate_up down
   run c64 240 $B --steps 600 --warmup 60 "$@"
   run c1 150 $B --concurrency 1 --steps 200 --warmup 20 "$@" ;;
+r4n)  # round 4: re-swept batch-1 / 32-row plans vs the round-3 ones, decode splits at batch 1, QKV S=4 vs 5 at 64 rows
+  pyt plan_tests 300 tests/test_skinny_gpu.py tests/test_fused_decode_gpu.py -k "m64 or deep_ring or uneven or logits"
+  OLD16="6144x4096x1@16=2,8,5;4096x4096x1@16=2,4,4;28672x4096x2@16=2,1,6;4096x14336x1@16=2,4,6"
+  run c1_new 150 $B --concurrency 1 --steps 300 --warmup 20
+  run c1_old 150 env XGS_M64_PLANS="$OLD16" $B --concurrency 1 --steps 300 --warmup 20
+  for sp in 1 4; do
+    run c1_splits$sp 150 env XGS_DECODE_MAX_SPLITS=$sp $B --concurrency 1 --steps 300 --warmup 20
+  done
+  run c8 150 $B --concurrency 8 --steps 200 --warmup 20
+  run c64_qkv5 240 $B --steps 600 --warmup 60
+  run c64_qkv4 240 env XGS_M64_PLANS="6144x4096x1@64=2,4,3" $B --steps 600 --warmup 60
+  run mixtral_c1 200 $B --model mixtral-8x7b --concurrency 1 --steps 100 --warmup 10 ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;

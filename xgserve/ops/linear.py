@@ -97,10 +97,11 @@ M64G_SMALL_ONLY = (8, 9, 10)
 # down 22.9 -> 19.2 us); the rest keep the skinny kernel.
 _M64_TUNED = {
     # Llama-3-8B / Mixtral attention, TP1
-    (6144, 4096, MODE_PARTIAL): {64: (2, 5, 3), 32: (2, 8, 5), 16: (2, 8, 5)},  # 64: S 5 12.2 vs S 4 ~15 us (r4_m64g_sweep_rot)
-    (4096, 4096, MODE_PARTIAL): {64: (1, 4, 0), 32: (1, 4, 0), 16: (2, 4, 4)},
-    (28672, 4096, MODE_SILU): {64: (2, 1, 1), 32: (2, 1, 5), 16: (2, 1, 6)},
-    (4096, 14336, MODE_PARTIAL): {64: (2, 8, 3), 32: (1, 4, 1), 16: (2, 4, 6)},
+    # 16 / 32 re-swept with K rotation in round 4 (profiles/r4_m64g_sweep_m1.jsonl; 64: r4_m64g_sweep_rot.jsonl)
+    (6144, 4096, MODE_PARTIAL): {64: (2, 5, 3), 32: (1, 5, 7), 16: (1, 2, 9)},
+    (4096, 4096, MODE_PARTIAL): {64: (1, 4, 0), 32: (1, 4, 0), 16: (1, 3, 0)},
+    (28672, 4096, MODE_SILU): {64: (2, 1, 1), 32: (2, 1, 3), 16: (2, 1, 5)},
+    (4096, 14336, MODE_PARTIAL): {64: (2, 8, 3), 32: (1, 4, 1), 16: (1, 4, 9)},
     # Llama-3-70B TP1
     (10240, 8192, MODE_PARTIAL): {64: (2, 2, 1), 16: (2, 8, 5)},
     (8192, 8192, MODE_PARTIAL): {64: (2, 8, 7), 32: (2, 8, 7), 16: (2, 8, 7)},  # 8-wave tile: 23.3 vs 24.8-25.7 us
