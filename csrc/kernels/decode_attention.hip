@@ -68,10 +68,29 @@ struct QkvFuse {
 // f[0..4) = sum_s part[s * slab + off + 0..4): batches of 4 clamped loads issued
 // before the adds (a runtime trip count with one load per iteration would chain S
 // dependent L2 round trips); masked partials add exactly 0.
+// S <= 8 (the decode QKV plans use 2-8 splits) takes ONE batch of loads, so the
+// prologue pays one L2 round trip whatever the split.
 __device__ __forceinline__ void sum_partials4(const float* __restrict__ part, int S, int64_t slab, int64_t off,
                                               float* f) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) f[i] = 0.f;
+  if (S > 4 && S <= 8) {
+    // per-lane pointers stepped by one slab while i < S (clamped to the last split):
+    // no per-split 64-bit scalar offsets (SGPR pressure)
+    const float* p = part + off;
+    float4 a[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a[i] = *reinterpret_cast<const float4*>(p);
+      if (i + 1 < S) p += slab;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float k = i < S ? 1.f : 0.f;
+      f[0] += k * a[i].x; f[1] += k * a[i].y; f[2] += k * a[i].z; f[3] += k * a[i].w;
+    }
+    return;
+  }
   for (int s0 = 0; s0 < S; s0 += 4) {
     float4 a[4];
 #pragma unroll
