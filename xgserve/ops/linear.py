@@ -107,29 +107,30 @@ _M64_TUNED = {
     (8192, 8192, MODE_PARTIAL): {64: (2, 8, 7), 32: (2, 8, 7), 16: (2, 8, 7)},  # 8-wave tile: 23.3 vs 24.8-25.7 us
     (57344, 8192, MODE_SILU): {64: (2, 1, 7), 32: (2, 1, 7), 16: (2, 1, 7)},  # 8-wave tile: 148 vs 166-178 us
     (8192, 28672, MODE_PARTIAL): {64: (2, 4, 3), 16: (2, 4, 5)},
+    # 70B shards re-swept with K rotation in round 4 at M = 1 / 64 (profiles/r4_m64g_sweep_tp.jsonl)
     # TP shards (Llama-3-8B / Mixtral attention TP2/4/8, Llama-3-70B TP2/4/8), re-swept at
     # M = 1 / 16 (bucket 16: best sum), 32, 64 (profiles/r2_tp_shard_sweep.jsonl); gate_up
     # shards with split-K SiLU (S > 1) and the 8-wave cfg 7: profiles/r2_silu_split_sweep.jsonl
-    (8192, 14336, MODE_PARTIAL): {64: (2, 4, 1), 32: (2, 4, 1), 16: (2, 4, 5)},  # down70t2
-    (8192, 7168, MODE_PARTIAL): {64: (2, 4, 1), 32: (2, 4, 1), 16: (1, 2, 1)},  # down70t4
-    (8192, 3584, MODE_PARTIAL): {64: (2, 4, 3), 32: (1, 2, 1), 16: (2, 4, 6)},  # down70t8
+    (8192, 14336, MODE_PARTIAL): {64: (2, 4, 1), 32: (2, 4, 1), 16: (1, 2, 9)},  # down70t2
+    (8192, 7168, MODE_PARTIAL): {64: (2, 4, 1), 32: (2, 4, 1), 16: (1, 4, 6)},  # down70t4
+    (8192, 3584, MODE_PARTIAL): {64: (1, 4, 7), 32: (1, 2, 1), 16: (2, 4, 6)},  # down70t8
     (4096, 7168, MODE_PARTIAL): {64: (2, 8, 3), 32: (1, 4, 1), 16: (1, 8, 5)},  # down8t2
     (4096, 3584, MODE_PARTIAL): {64: (1, 4, 2), 32: (1, 8, 4), 16: (1, 8, 5)},  # down8t4
     (4096, 1792, MODE_PARTIAL): {64: (1, 4, 2), 32: (1, 4, 4), 16: (1, 2, 2)},  # down8t8
-    (28672, 8192, MODE_SILU): {64: (2, 1, 3), 32: (2, 1, 3), 16: (2, 2, 5)},  # gate_up70t2
-    (14336, 8192, MODE_SILU): {64: (2, 1, 6), 32: (2, 2, 5), 16: (2, 2, 6)},  # gate_up70t4
+    (28672, 8192, MODE_SILU): {64: (2, 1, 1), 32: (2, 1, 3), 16: (2, 1, 3)},  # gate_up70t2
+    (14336, 8192, MODE_SILU): {64: (2, 1, 6), 32: (2, 2, 5), 16: (2, 1, 6)},  # gate_up70t4
     (7168, 8192, MODE_SILU): {64: (2, 2, 6), 32: (2, 2, 6), 16: (2, 2, 6)},  # gate_up70t8
     (14336, 4096, MODE_SILU): {64: (2, 1, 6), 32: (2, 1, 6), 16: (2, 4, 7)},  # gate_up8t2
     (7168, 4096, MODE_SILU): {64: (2, 2, 6), 32: (2, 4, 3), 16: (2, 4, 1)},  # gate_up8t4
     (3584, 4096, MODE_SILU): {64: (2, 4, 6), 32: (2, 4, 0), 16: (2, 4, 0)},  # gate_up8t8
-    (8192, 4096, MODE_PARTIAL): {64: (2, 4, 3), 32: (2, 4, 3), 16: (1, 4, 5)},  # o70t2
-    (8192, 2048, MODE_PARTIAL): {64: (1, 2, 2), 32: (1, 2, 0), 16: (1, 2, 0)},  # o70t4
-    (8192, 1024, MODE_PARTIAL): {64: (1, 2, 2), 32: (2, 2, 4), 16: (2, 4, 0)},  # o70t8
+    (8192, 4096, MODE_PARTIAL): {64: (2, 4, 3), 32: (2, 4, 3), 16: (2, 4, 1)},  # o70t2
+    (8192, 2048, MODE_PARTIAL): {64: (1, 2, 0), 32: (1, 2, 0), 16: (1, 2, 0)},  # o70t4
+    (8192, 1024, MODE_PARTIAL): {64: (1, 2, 2), 32: (2, 2, 4), 16: (1, 1, 9)},  # o70t8
     (4096, 2048, MODE_PARTIAL): {64: (1, 4, 2), 32: (1, 4, 4), 16: (1, 2, 0)},  # o8t2
     (4096, 1024, MODE_PARTIAL): {64: (1, 4, 2), 32: (2, 4, 4), 16: (1, 4, 5)},  # o8t4
     (4096, 512, MODE_PARTIAL): {64: (2, 2, 6), 32: (1, 2, 3), 16: (2, 1, 6)},  # o8t8
-    (5120, 8192, MODE_PARTIAL): {64: (2, 8, 7), 32: (2, 8, 5), 16: (2, 8, 5)},  # qkv70t2
-    (2560, 8192, MODE_PARTIAL): {64: (2, 8, 1), 32: (2, 8, 1), 16: (1, 8, 6)},  # qkv70t4
+    (5120, 8192, MODE_PARTIAL): {64: (2, 6, 1), 32: (2, 8, 5), 16: (1, 6, 6)},  # qkv70t2
+    (2560, 8192, MODE_PARTIAL): {64: (1, 6, 1), 32: (2, 8, 1), 16: (1, 6, 0)},  # qkv70t4
     (1280, 8192, MODE_PARTIAL): {64: (1, 8, 0), 32: (1, 8, 0), 16: (2, 8, 4)},  # qkv70t8
     (3072, 4096, MODE_PARTIAL): {64: (1, 8, 4), 32: (1, 4, 2), 16: (1, 8, 6)},  # qkv8t2
     (1536, 4096, MODE_PARTIAL): {64: (1, 8, 2), 32: (1, 4, 1), 16: (1, 8, 4)},  # qkv8t4
