@@ -219,6 +219,19 @@ r4n)  # round 4: re-swept batch-1 / 32-row plans vs the round-3 ones, decode spl
   run c64_qkv5 240 $B --steps 600 --warmup 60
   run c64_qkv4 240 env XGS_M64_PLANS="6144x4096x1@64=2,4,3" $B --steps 600 --warmup 60
   run mixtral_c1 200 $B --model mixtral-8x7b --concurrency 1 --steps 100 --warmup 10 ;;
+r4o)  # round 4: kernel profiles of batch 1 and 64 concurrent on the final plans; TP-shard plan re-sweep (K rotation)
+  bash bench/profile.sh "$o/prof_c1" --concurrency 1
+  bash bench/profile.sh "$o/prof_c64"
+  run sweep_tp 600 python -u bench/gemm_bench.py --m64g-sweep --M 1 64 --shapes \
+      qkv70t8 o70t8 gate_up70t8 down70t8 qkv70t2 o70t2 gate_up70t2 down70t2 qkv70t4 o70t4 gate_up70t4 down70t4 ;;
+final)  # round-end gate: every GPU test, smoke, the driver form twice, a 3000-step window, batch 1, the c64 profile
+  pyt_soft gputests 900 tests -m gpu --maxfail=10
+  run smoke 150 python -u -c "import __graft_entry__ as g; g.smoke()"
+  run driver_a 200 $B --steps 20 --warmup 5 "$@"
+  run driver_b 200 $B --steps 20 --warmup 5 "$@"
+  run long 300 $B --steps 3000 --warmup 100 "$@"
+  run c1 150 $B --concurrency 1 --steps 300 --warmup 20 "$@"
+  bash bench/profile.sh "$o/prof_c64" "$@" ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;
