@@ -181,6 +181,58 @@ struct RouteAlign {
   int E_local, expert_offset, block_m, cap;
 };
 
+// Thread 0 of route2_kernel: softmax over the E router sums (red[wave][e]), top-k,
+// optional renormalisation -> w / ids of token t; with ra.sorted_rows (one token) also
+// align_kernel's layout offsets s_off / rows s_pos, published by the caller.
+template <int EM, int NWV>
+__device__ __forceinline__ void route_select(const float (*red)[EM + 1], int E, int k, int renorm, int t,
+                                             float* __restrict__ w, int32_t* __restrict__ ids, const RouteAlign& ra,
+                                             bool align, int* s_off, int* s_pos) {
+  float v[EM];
+  float mx = -INFINITY;
+  for (int e = 0; e < E; ++e) {
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < NWV; ++q) sum += red[q][e];
+    v[e] = sum;
+    mx = fmaxf(mx, v[e]);
+  }
+  float den = 0.f;
+  for (int e = 0; e < E; ++e) den += __expf(v[e] - mx);
+  unsigned long long used = 0;
+  float sel[16];
+  int sid[16];
+  float ssum = 0.f;
+  for (int j = 0; j < k; ++j) {
+    int best = -1;
+    float bv = -INFINITY;
+    for (int e = 0; e < E; ++e)
+      if (!((used >> e) & 1ull) && (best < 0 || v[e] > bv)) { best = e; bv = v[e]; }
+    used |= 1ull << best;
+    sid[j] = best;
+    sel[j] = __expf(bv - mx) / den;
+    ssum += sel[j];
+  }
+  for (int j = 0; j < k; ++j) {
+    w[static_cast<int64_t>(t) * k + j] = renorm ? sel[j] / ssum : sel[j];
+    ids[static_cast<int64_t>(t) * k + j] = sid[j];
+  }
+  if (align) {  // align_kernel's layout for the k pairs of this one token
+    int cnt[EM];
+    for (int e = 0; e < ra.E_local; ++e) cnt[e] = 0;
+    for (int j = 0; j < k; ++j) {
+      const int e = sid[j] - ra.expert_offset;
+      if (e >= 0 && e < ra.E_local) ++cnt[e];
+    }
+    s_off[0] = 0;
+    for (int e = 0; e < ra.E_local; ++e) s_off[e + 1] = s_off[e] + (cnt[e] + ra.block_m - 1) / ra.block_m * ra.block_m;
+    for (int j = 0; j < k; ++j) {
+      const int e = sid[j] - ra.expert_offset;
+      s_pos[j] = (e >= 0 && e < ra.E_local) ? s_off[e] : -1;  // distinct experts: one row each
+    }
+  }
+}
+
 template <int EM, bool NORM, int CPT>
 __global__ void __launch_bounds__(512) route2_kernel(const uint16_t* __restrict__ h, const uint16_t* __restrict__ wr,
                                                      int H, int E, int k, int renorm, float* __restrict__ w,
@@ -254,51 +306,7 @@ __global__ void __launch_bounds__(512) route2_kernel(const uint16_t* __restrict_
   }
   __syncthreads();
   const bool align = ra.sorted_rows != nullptr;  // T == 1 (host-checked)
-  if (threadIdx.x == 0) {
-  float v[EM];
-  float mx = -INFINITY;
-  for (int e = 0; e < E; ++e) {
-    float sum = 0.f;
-#pragma unroll
-    for (int q = 0; q < NWV; ++q) sum += red[q][e];
-    v[e] = sum;
-    mx = fmaxf(mx, v[e]);
-  }
-  float den = 0.f;
-  for (int e = 0; e < E; ++e) den += __expf(v[e] - mx);
-  unsigned long long used = 0;
-  float sel[16];
-  int sid[16];
-  float ssum = 0.f;
-  for (int j = 0; j < k; ++j) {
-    int best = -1;
-    float bv = -INFINITY;
-    for (int e = 0; e < E; ++e)
-      if (!((used >> e) & 1ull) && (best < 0 || v[e] > bv)) { best = e; bv = v[e]; }
-    used |= 1ull << best;
-    sid[j] = best;
-    sel[j] = __expf(bv - mx) / den;
-    ssum += sel[j];
-  }
-  for (int j = 0; j < k; ++j) {
-    w[static_cast<int64_t>(t) * k + j] = renorm ? sel[j] / ssum : sel[j];
-    ids[static_cast<int64_t>(t) * k + j] = sid[j];
-  }
-  if (align) {  // align_kernel's layout for the k pairs of this one token
-    int cnt[EM];
-    for (int e = 0; e < ra.E_local; ++e) cnt[e] = 0;
-    for (int j = 0; j < k; ++j) {
-      const int e = sid[j] - ra.expert_offset;
-      if (e >= 0 && e < ra.E_local) ++cnt[e];
-    }
-    s_off[0] = 0;
-    for (int e = 0; e < ra.E_local; ++e) s_off[e + 1] = s_off[e] + (cnt[e] + ra.block_m - 1) / ra.block_m * ra.block_m;
-    for (int j = 0; j < k; ++j) {
-      const int e = sid[j] - ra.expert_offset;
-      s_pos[j] = (e >= 0 && e < ra.E_local) ? s_off[e] : -1;  // distinct experts: one row each
-    }
-  }
-  }
+  if (threadIdx.x == 0) route_select<EM, NWV>(red, E, k, renorm, t, w, ids, ra, align, s_off, s_pos);
   if (!align) return;
   __syncthreads();
   for (int e = threadIdx.x; e <= ra.E_local; e += blockDim.x) ra.offsets[e] = s_off[e];
