@@ -232,6 +232,11 @@ final)  # round-end gate: every GPU test, smoke, the driver form twice, a 3000-s
   run long 300 $B --steps 3000 --warmup 100 "$@"
   run c1 150 $B --concurrency 1 --steps 300 --warmup 20 "$@"
   bash bench/profile.sh "$o/prof_c64" "$@" ;;
+r4p)  # round 4: one rank of the Llama-3-70B TP8 group (config 4 proxy), 70B TP1, batch 1 and 64 concurrent
+  run tp8_c1 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+  run tp8_c64 300 $B --model llama3-70b --tp-shard 8 --steps 60 --warmup 20
+  run tp1_c1 300 $B --model llama3-70b --concurrency 1 --steps 40 --warmup 10
+  run tp1_c64 300 $B --model llama3-70b --steps 40 --warmup 10 ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;
