@@ -122,11 +122,12 @@ __global__ void __launch_bounds__(256) route_kernel(const uint16_t* __restrict__
     }
 #pragma unroll
     for (int e = 0; e < EM; ++e) {
-      if (e >= E) break;
-      float r[8];
-      unpack8(ld16(wr + static_cast<int64_t>(e) * H + c * 8), r);
+      if (e < E) {
+        float r[8];
+        unpack8(ld16(wr + static_cast<int64_t>(e) * H + c * 8), r);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[e] += x[i] * r[i];
+        for (int i = 0; i < 8; ++i) acc[e] += x[i] * r[i];
+      }
     }
   }
 #pragma unroll

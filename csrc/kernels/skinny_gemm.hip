@@ -288,10 +288,11 @@ static int launch_slab(const uint16_t* x, int M, int K, const uint16_t* w, int N
   dim3 grid(N / 64, split_k);
   static bool attr_set = false;  // opt in to > 64 KiB dynamic LDS once (not a stream op: graph-safe)
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_slab_kernel<2>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, SL_MAX_LDS);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_slab_kernel<4>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, SL_MAX_LDS);
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_slab_kernel<2>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, SL_MAX_LDS) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_slab_kernel<4>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, SL_MAX_LDS) != hipSuccess)
+      return -1;  // the LDS opt-in failed: the caller reports the unsupported launch
     attr_set = true;
   }
   if (MT == 2)
