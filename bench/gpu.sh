@@ -237,6 +237,10 @@ r4p)  # round 4: one rank of the Llama-3-70B TP8 group (config 4 proxy), 70B TP1
   run tp8_c64 300 $B --model llama3-70b --tp-shard 8 --steps 60 --warmup 20
   run tp1_c1 300 $B --model llama3-70b --concurrency 1 --steps 40 --warmup 10
   run tp1_c64 300 $B --model llama3-70b --steps 40 --warmup 10 ;;
+r4q)  # round 4: two-stream overlap with the decode GEMMs on 72-KB-LDS (KC 64) configurations
+  run overlap_kc64 200 env XGS_M64_PLANS="4096x4096x1@64=1,4,2;28672x4096x2@64=2,1,3" \
+      python -u bench/overlap_probe.py --prompt 512 1024
+  run overlap_base 200 python -u bench/overlap_probe.py --prompt 512 1024 ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;
