@@ -241,6 +241,21 @@ r4q)  # round 4: two-stream overlap with the decode GEMMs on 72-KB-LDS (KC 64) c
   run overlap_kc64 200 env XGS_M64_PLANS="4096x4096x1@64=1,4,2;28672x4096x2@64=2,1,3" \
       python -u bench/overlap_probe.py --prompt 512 1024
   run overlap_base 200 python -u bench/overlap_probe.py --prompt 512 1024 ;;
+r4r)  # round 4: decode attention with non-temporal K/V loads (depth 14 = PR 4), kernel + engine A/B
+  run dnt_768 200 python -u bench/decode_cold.py --depth 2 14 --splits 1 2
+  run dnt_2k 200 python -u bench/decode_cold.py --L 2048 --depth 2 14 --splits 1
+  run eng_base 300 python -u bench.py --steps 600 --warmup 50
+  run eng_nt 300 env XGS_DECODE_DEPTH=14 python -u bench.py --steps 600 --warmup 50
+  run eng_base2 300 python -u bench.py --steps 600 --warmup 50 ;;
+r4s)  # round 4: non-temporal K/V loads as the default -- numerics, then batch 1 / 64 / 70B A/Bs (14 = cached loads)
+  pyt attn_tests 400 tests/test_fused_decode_gpu.py tests/test_kernels_gpu.py -k "decode or attention"
+  run c1_nt 300 $B --concurrency 1 --steps 300 --warmup 30
+  run c1_cached 300 env XGS_DECODE_DEPTH=14 $B --concurrency 1 --steps 300 --warmup 30
+  run c1_nt2 300 $B --concurrency 1 --steps 300 --warmup 30
+  run c64_nt 300 $B --steps 1000 --warmup 100
+  run c64_cached 300 env XGS_DECODE_DEPTH=14 $B --steps 1000 --warmup 100
+  run tp8_c1 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+  run tp8_c64 300 $B --model llama3-70b --tp-shard 8 --steps 60 --warmup 20 ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;

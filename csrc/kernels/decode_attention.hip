@@ -210,7 +210,7 @@ __device__ __forceinline__ float combine_splits(const float* __restrict__ lse, c
 // this launch, r1_attn_prefetch_ab.md; 8 waves per workgroup, r1_decode_waves_c1.md.)
 // PR (anatomy probes, bench/decode_cold.py --probe; output garbage): 0 = the kernel;
 // 1 = no fused prologue (no QKV-partial reads / RoPE / KV append); 2 = no key loop;
-// 3 = neither (launch + merge + store only).
+// 3 = neither (launch + merge + store only); 4 = the kernel with cached (temporal) K/V loads.
 template <int D, int G, bool FQ, bool KL = false, int NB = 2, int PR = 0>
 __global__ void __launch_bounds__(256) decode_attn_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
@@ -244,22 +244,25 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     const int key0 = t * 16;
     const int page = bt[key0 / bs];
     const int64_t base = (static_cast<int64_t>(page) * Hkv + kvh) * head_stride + static_cast<int64_t>(key0 % bs) * D;
+    // K/V are read once per step and a step's cache (GBs at 64 sequences) never fits the
+    // L2 / Infinity Cache: non-temporal loads, 5.3 -> 6.1 TB/s at 2K keys (r4_decode_nt.md)
+    auto ldkv = [](const uint16_t* p) { return PR == 4 ? ld16(p) : ld16_nt(p); };
     if constexpr (KL) {
       static_assert(C::KK == C::VLD, "K and V tiles split into the same chunks per lane");
 #pragma unroll
       for (int i = 0; i < C::KK; ++i) {
         const int c = lane + 64 * i;  // chunk id in the 16 x NCH tile (4 full rows per instruction)
-        kf[i] = ld16(kc + base + (c / C::NCH) * D + (c % C::NCH) * 8);
+        kf[i] = ldkv(kc + base + (c / C::NCH) * D + (c % C::NCH) * 8);
       }
     } else {
       const uint16_t* kp = kc + base + li * D + 8 * g;
 #pragma unroll
-      for (int kk = 0; kk < C::KK; ++kk) kf[kk] = ld16(kp + kk * 32);
+      for (int kk = 0; kk < C::KK; ++kk) kf[kk] = ldkv(kp + kk * 32);
     }
 #pragma unroll
     for (int i = 0; i < C::VLD; ++i) {
       const int c = lane + 64 * i;  // chunk id in the 16 x NCH tile
-      vr[i] = ld16(vc + base + (c / C::NCH) * D + (c % C::NCH) * 8);
+      vr[i] = ldkv(vc + base + (c / C::NCH) * D + (c % C::NCH) * 8);
     }
   };
   const int t0 = t_begin + wid;
@@ -447,13 +450,14 @@ static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, con
   // fragment-shaped K loads measured 0.5-6 % faster. depth 3: three register tiles
   // in flight per wave (fused form, G <= 4)
   if constexpr (D == 128 && G <= 4 && FQ) {
-    if (depth >= 11 && depth <= 13) {  // anatomy probes (depth = 10 + PR)
+    if (depth >= 11 && depth <= 14) {  // anatomy probes (depth = 10 + PR)
 #define XGK_DECP(P)                                                                                                 \
   hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, true, 2, P>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt, \
                      bts, sl, po, pl, out, os, Hq, Hkv, bs, scale, S, fq)
       if (depth == 11) XGK_DECP(1);
       else if (depth == 12) XGK_DECP(2);
-      else XGK_DECP(3);
+      else if (depth == 13) XGK_DECP(3);
+      else XGK_DECP(4);
 #undef XGK_DECP
       if (S > 1) hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
       return;
@@ -504,7 +508,7 @@ int decode_attention_fq(const float* part, int S_qkv, const int32_t* positions, 
   if (B <= 0) return 0;
   if (part == nullptr || S_qkv < 1 || bs % 16 != 0 || Hq % Hkv != 0 || D != 128 || num_splits < 1) return -1;
   if (num_splits > 1 && (part_out == nullptr || part_lse == nullptr)) return -1;
-  if (out == nullptr || depth < 2 || (depth > 3 && (depth < 11 || depth > 13))) return -1;
+  if (out == nullptr || depth < 2 || (depth > 3 && (depth < 11 || depth > 14))) return -1;
   const QkvFuse fq{part, S_qkv, positions, cos_sin, slots, kc, vc, apply_rope};
   const int G = Hq / Hkv;
 #define XGK_DECF(GG)                                                                                         \
