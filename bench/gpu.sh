@@ -256,6 +256,14 @@ r4s)  # round 4: non-temporal K/V loads as the default -- numerics, then batch 1
   run c64_cached 300 env XGS_DECODE_DEPTH=14 $B --steps 1000 --warmup 100
   run tp8_c1 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
   run tp8_c64 300 $B --model llama3-70b --tp-shard 8 --steps 60 --warmup 20 ;;
+r4t)  # round 4: all-reduce prologue in the next GEMM (gemm_m64g_arx): tests, then simulated-TP8 70B batch 1 A/B
+  pyt arx_tests 400 tests/test_ar_prologue_gpu.py
+  pyt fused_tests 400 tests/test_fused_decode_gpu.py
+  run tp8_ar0_base 300 env XGS_SIM_AR_US=0 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+  run tp8_ar0_arx 300 env XGS_SIM_AR_US=0 XGS_AR_PROLOGUE=1 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+  run tp8_ar8_base 300 env XGS_SIM_AR_US=8 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+  run tp8_ar8_arx 300 env XGS_SIM_AR_US=8 XGS_AR_PROLOGUE=1 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+  run c64_default 300 $B --steps 600 --warmup 50 ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;

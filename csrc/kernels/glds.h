@@ -46,6 +46,21 @@ __device__ __forceinline__ void glds16_nt(const void* src, void* lds_base) {
 #endif
 }
 
+// device-coherent (sc1) LDS-DMA: reads data another workgroup of the same launch
+// published with write-through stores, past this XCD's possibly stale L2 lines
+__device__ __forceinline__ void glds16_sc1(const void* src, void* lds_base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)(lds_base))));
+  asm volatile(
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off sc1"
+      :
+      : "v"(src), "{m0}"(lds)
+      : "memory");
+#endif
+}
+
 // s_waitcnt vmcnt(N) (expcnt, lgkmcnt left at max)
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -67,6 +82,26 @@ __device__ __forceinline__ void raw_barrier() {
 __device__ __forceinline__ void st16_sc1(float* p, f32x4_t v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+#endif
+}
+
+// 8-B and 4-B write-through stores (same contract as st16_sc1)
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
+__device__ __forceinline__ void st8_sc1(void* p, uint2 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const u32x2_t w = {v.x, v.y};
+  asm volatile("global_store_dwordx2 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+#endif
+}
+__device__ __forceinline__ void st16u_sc1(void* p, uint4 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const u32x4_t w = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+#endif
+}
+__device__ __forceinline__ void st4_sc1(float* p, float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("global_store_dword %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 #endif
 }
 

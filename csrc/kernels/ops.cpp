@@ -23,6 +23,8 @@ int skinny_slab_kmax(int);
 int gemm_m64g(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 int gemm_m64g_ex(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, const float*,
                  int, int, float, uint16_t*, float*, int*, hipStream_t);
+int gemm_m64g_arx(uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, float*, float,
+                  int*, const float*, int, int, int*, uint64_t, hipStream_t);
 int gemm_mw(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, hipStream_t);
 void set_k_rotation(int mode);
 int gemm_mw_probe(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
@@ -271,6 +273,14 @@ PYBIND11_MODULE(_kernels, m) {
                             nw, cfg, P<const float>(ss_in), ss_n, ss_stride, eps, P<uint16_t>(resid),
                             P<float>(ss_out), P<int>(counters), S(st)),
           "gemm_m64g_ex");
+  });
+  m.def("gemm_m64g_arx", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
+                            int mode, int nw, int cfg, uintptr_t ss, float eps, uintptr_t counters, uintptr_t ar_part,
+                            int ar_S, int ar_wgs, uintptr_t flags, uint64_t ar_ticks, uintptr_t st) {
+    check(xgk::gemm_m64g_arx(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode,
+                             nw, cfg, P<float>(ss), eps, P<int>(counters), P<const float>(ar_part), ar_S, ar_wgs,
+                             P<int>(flags), ar_ticks, S(st)),
+          "gemm_m64g_arx");
   });
   m.def("add_partials_resid", [](uintptr_t part, int S_, int T, uintptr_t res, uintptr_t ss_part, int H,
                                  uintptr_t st, uint64_t sim_ticks) {

@@ -162,11 +162,15 @@ def test_gemm_m64g_waits_are_counted(tmp_path):
         NW, WV, KC, _nt, MT, *rest = _targs(name)
         NS = rest[0] if rest else 3
         RPI = 1024 // (KC * 2)
-        G = 16 * MT // RPI // WV + 16 * NW // RPI
+        XI = 16 * MT // RPI // WV
+        G = XI + 16 * NW // RPI
         counted = {k * G for k in range(1, NS - 1)}  # 1 .. NS - 2 chunks left in flight
         if NS == 3:
-            got = _vmcnts(_pipeline(body))
-            assert got <= {0, G}, (name, sorted(got), G)
+            # blocks with ordinary loads (the all-reduce prologue's reducer path, the
+            # statistics loads) carry the compiler's own waits and are skipped
+            got = _vmcnts(_without_epilogue_blocks(_pipeline(body)))
+            # XI: the all-reduce prologue leaves chunk 1's x DMAs in flight
+            assert got <= {0, XI, G}, (name, sorted(got), G)
         else:
             # deep rings: the rotated loop may be laid out ahead of the prologue, so every
             # block without ordinary global memory ops is checked -- the counted waits are

@@ -35,7 +35,8 @@ from ..parallel import comm
 from ..parallel.state import get_state
 from ..ops import linear as linear_mod
 from ..ops.linear import (MODE_PARTIAL, MODE_SILU, MW_MAX_M, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace, RowStats,
-                          lm_head_linear, m64_linear, m64_norm_linear, m64_plan, m64_resid_linear, mw_linear, mw_plan, pick_split,
+                          lm_head_linear, m64_arx_linear, m64_arx_ok, m64_linear, m64_norm_linear, m64_plan, m64_resid_linear,
+                          mw_linear, mw_plan, pick_split,
                           quantize_fp8, skinny_linear, splitk_linear, splitk_prefill_ok, w8_linear, w8_plan)
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
 from .config import ModelConfig
@@ -71,6 +72,13 @@ EP_EXACT_MIN_PAIRS = int(os.environ.get("XGS_EP_EXACT_MIN_PAIRS", "256"))
 # moe_comm "auto": steps of at most this many tokens use the allreduce form when the
 # custom IPC all-reduce can take the [T, H] message
 EP_AR_MAX_TOKENS = 64
+# One rank of a TP group simulated in one process (--tp-shard), decode steps of <= 16
+# tokens: the residual all-reduce of the O / down partials runs as the reducer
+# workgroups of the NEXT GEMM's launch (gemm_m64g_arx) while its weight stream starts,
+# instead of a launch of its own -- the exposed-latency A/B of
+# profiles/r4_ar_prologue.md. XGS_AR_PROLOGUE=0 keeps the separate launch.
+AR_PROLOGUE = os.environ.get("XGS_AR_PROLOGUE", "0") != "0"
+AR_PROLOGUE_MAX_M = 16
 
 
 @torch.no_grad()
@@ -409,7 +417,11 @@ class LlamaLayer(nn.Module):
         (+ residual, + next statistics). `resid` (bf16 [T, H]) is updated in place;
         returns the statistics of the new residual for the next layer."""
         eps = self.cfg.norm_eps
-        pqkv = m64_norm_linear(resid, self.qkv, MODE_PARTIAL, stats, eps)
+        if stats.pending is not None:  # the previous layer's down all-reduce, folded in here
+            pqkv = m64_arx_linear(resid, stats.pending, self.qkv, MODE_PARTIAL, stats.ss, eps, ws.ar_flags,
+                                  comm.sim_ar_ticks())
+        else:
+            pqkv = m64_norm_linear(resid, self.qkv, MODE_PARTIAL, stats, eps)
         a = self.attn.fused_decode(pqkv, meta, kv, cos_sin)
         if self.moe:
             return self._fused_moe_tail(a, resid, ws, site)
@@ -449,13 +461,29 @@ class LlamaLayer(nn.Module):
         all-reduce + residual + statistics (one launch) -> gate_up (norm row scale,
         SiLU-gate) -> down GEMM partials -> all-reduce + residual + statistics."""
         T, H = resid.shape
+        eps = self.cfg.norm_eps
         po = m64_linear(a, self.o, MODE_PARTIAL)
+        if self._ar_prologue(T):
+            act = m64_arx_linear(resid, po, self.gate_up, MODE_SILU, ws.ss[site], eps, ws.ar_flags,
+                                 comm.sim_ar_ticks())
+            pd = m64_linear(act, self.down, MODE_PARTIAL)
+            return RowStats(ws.ss[site + 1], H // 1024, T, pending=pd)  # folded in by the next QKV GEMM
         comm.tp_allreduce_resid(po.part, resid, ws.ss[site])
         st = RowStats(ws.ss[site], H // 1024, T)
-        act = m64_norm_linear(resid, self.gate_up, MODE_SILU, st, self.cfg.norm_eps)
+        act = m64_norm_linear(resid, self.gate_up, MODE_SILU, st, eps)
         pd = m64_linear(act, self.down, MODE_PARTIAL)
         comm.tp_allreduce_resid(pd.part, resid, ws.ss[site + 1])
         return RowStats(ws.ss[site + 1], H // 1024, T)
+
+    def _ar_prologue(self, T: int) -> bool:
+        """The simulated-TP residual all-reduces as GEMM prologues (AR_PROLOGUE): a
+        single-rank process (the all-reduce is the local fold), T <= 16, and plans for
+        gate_up and QKV that take the prologue."""
+        if not (AR_PROLOGUE and get_state().tp_size == 1 and T <= AR_PROLOGUE_MAX_M):
+            return False
+        H = self.cfg.hidden_size
+        return (m64_arx_ok(T, self.gate_up.shape[0], H, MODE_SILU)
+                and m64_arx_ok(T, self.qkv.shape[0], H, MODE_PARTIAL))
 
 
 class LlamaForCausalLM(nn.Module):
@@ -548,6 +576,8 @@ class LlamaForCausalLM(nn.Module):
         st = RowStats(ws.ss[0], 1, meta.num_tokens)
         for i, layer in enumerate(self.layers):
             st = layer.forward_fused(resid, st, meta, kv_caches[i], self.cos_sin, ws, 2 * i + 1)
+        if st.pending is not None:  # the last layer's down all-reduce
+            comm.tp_allreduce_resid(st.pending.part, resid, st.ss)
         return ops.rmsnorm(resid, self.norm, self.cfg.norm_eps)
 
     def set_moe_comm(self, mode: str):

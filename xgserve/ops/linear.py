@@ -365,6 +365,10 @@ class RowStats:
     ss: torch.Tensor
     n: int
     stride: int
+    # the residual add these statistics describe has not run yet: the consuming GEMM
+    # folds these split-K partials in first (m64_arx_linear), or they are reduced
+    # by comm.tp_allreduce_resid before anything else reads the residual
+    pending: Optional["PendingSum"] = None
 
 
 class ResidWorkspace:
@@ -382,6 +386,8 @@ class ResidWorkspace:
         # arrival tickets (GG_RESID: one word per tile): zero here, and every launch
         # re-arms the words it used
         self.counters = torch.zeros(n_sites, 2 * self.MAX_TILES, dtype=torch.int32, device=device)
+        # all-reduce prologue (m64_arx_linear): arrival + pass count, re-armed by each launch
+        self.ar_flags = torch.zeros(2, dtype=torch.int32, device=device)
 
 
 # Prefill-sized down projections (K = 3.5 N) have too few output tiles for the chip at
@@ -454,6 +460,46 @@ def m64_norm_linear(x: torch.Tensor, w: torch.Tensor, mode: int, stats: RowStats
         return out
     k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, cfg, *st, 0, 0, 0,
                    stream_ptr())
+    return out
+
+
+def m64_arx_ok(M: int, N: int, K: int, mode: int) -> bool:
+    """Can m64_arx_linear run this GEMM (a plan whose workgroups are 128 / 256 threads,
+    K a multiple of 1024 up to 8192)?"""
+    plan = m64_plan(M, N, K, mode)
+    return plan is not None and plan[2] != 7 and K % 1024 == 0 and K // 1024 <= 8
+
+
+def m64_arx_linear(resid: torch.Tensor, prev: PendingSum, w: torch.Tensor, mode: int, ss: torch.Tensor,
+                   eps: float, flags: torch.Tensor, ticks: int = 0, wgs: Optional[int] = None):
+    """resid += sum_s prev.part[s] (the previous projection's split-K partials) and then
+    the norm-scaled GEMM of the new residual, in ONE gemm_m64g launch: reducer
+    workgroups fold the partials (after `ticks` of simulated all-reduce latency) while
+    the GEMM workgroups already stream their first weight chunks, then read the
+    residual and its statistics (written to `ss`, [K / 1024, M]). Returns what
+    m64_norm_linear returns: PendingSum (MODE_PARTIAL) or bf16 silu(gate) * up."""
+    M, K = resid.shape
+    N = w.shape[0]
+    plan = m64_plan(M, N, K, mode)
+    if plan is None or not m64_arx_ok(M, N, K, mode):
+        raise ValueError(f"gemm_m64g_arx: unsupported shape M={M} N={N} K={K} mode={mode}")
+    nw, S, cfg = plan
+    if wgs is None:
+        wgs = min(M * (K // 1024), 32)
+    k = kernels()
+    ar = (prev.part.data_ptr(), prev.part.shape[0], wgs, flags.data_ptr(), int(ticks), stream_ptr())
+    if mode == MODE_PARTIAL:
+        part = torch.empty(S, M, N, dtype=torch.float32, device=resid.device)
+        k.gemm_m64g_arx(resid.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, mode, nw, cfg, ss.data_ptr(),
+                        float(eps), 0, *ar)
+        return PendingSum(part, S)
+    out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=resid.device)
+    part, cnt = 0, 0
+    if S > 1:  # split-K SiLU: slabs + tile tickets, reduced in the GEMM tail
+        pt = torch.empty(S, M, N, dtype=torch.float32, device=resid.device)
+        part, cnt = pt.data_ptr(), tile_counters(resid.device, N).data_ptr()
+    k.gemm_m64g_arx(resid.data_ptr(), M, K, w.data_ptr(), N, part, out.data_ptr(), S, mode, nw, cfg, ss.data_ptr(),
+                    float(eps), cnt, *ar)
     return out
 
 

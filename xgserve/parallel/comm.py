@@ -60,6 +60,11 @@ def resid_allreduce_ok(T: int, H: int) -> bool:
 _SIM_AR_TICKS = int(float(os.environ.get("XGS_SIM_AR_US", "0")) * 100)  # 100 MHz wall clock
 
 
+def sim_ar_ticks() -> int:
+    """The simulated all-reduce wait (XGS_SIM_AR_US) in 100 MHz ticks; 0 in a real TP group."""
+    return _SIM_AR_TICKS if get_state().tp_size == 1 else 0
+
+
 def tp_allreduce_resid(part: torch.Tensor, resid: torch.Tensor, ss: torch.Tensor) -> None:
     """Row-parallel projection epilogue of the fused decode layer:
     resid += all-reduce(sum_s part[s]) in place (bf16), ss[chunk * T + t] <- the new
