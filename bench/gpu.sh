@@ -264,6 +264,10 @@ r4t)  # round 4: all-reduce prologue in the next GEMM (gemm_m64g_arx): tests, th
   run tp8_ar8_base 300 env XGS_SIM_AR_US=8 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
   run tp8_ar8_arx 300 env XGS_SIM_AR_US=8 XGS_AR_PROLOGUE=1 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
   run c64_default 300 $B --steps 600 --warmup 50 ;;
+r4u)  # round 4: decode-attention depth / page size with the non-temporal K/V loads
+  run dnt_depth 200 python -u bench/decode_cold.py --depth 2 3 --splits 1
+  run dnt_depth_2k 200 python -u bench/decode_cold.py --L 2048 --depth 2 3 --splits 1
+  run dnt_bs32 200 python -u bench/decode_cold.py --bs 32 --depth 2 3 --splits 1 ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;
