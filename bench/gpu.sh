@@ -268,6 +268,14 @@ r4u)  # round 4: decode-attention depth / page size with the non-temporal K/V lo
   run dnt_depth 200 python -u bench/decode_cold.py --depth 2 3 --splits 1
   run dnt_depth_2k 200 python -u bench/decode_cold.py --L 2048 --depth 2 3 --splits 1
   run dnt_bs32 200 python -u bench/decode_cold.py --bs 32 --depth 2 3 --splits 1 ;;
+r4v)  # round 4: K rotation for every split (XGS_KROT=2) and non-temporal O-projection plans, c64 / c1 A/B
+  run c64_base 300 $B --steps 600 --warmup 50
+  run c64_krot2 300 env XGS_KROT=2 $B --steps 600 --warmup 50
+  run c64_ont 300 env XGS_M64_PLANS="4096x4096x1@64=1,4,1;4096x4096x1@32=1,4,1" $B --steps 600 --warmup 50
+  run c64_base2 300 $B --steps 600 --warmup 50
+  run c1_base 300 $B --concurrency 1 --steps 300 --warmup 30
+  run c1_krot2 300 env XGS_KROT=2 $B --concurrency 1 --steps 300 --warmup 30
+  run c1_ont 300 env XGS_M64_PLANS="4096x4096x1@16=1,3,1" $B --concurrency 1 --steps 300 --warmup 30 ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;
