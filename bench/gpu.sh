@@ -276,6 +276,14 @@ r4v)  # round 4: K rotation for every split (XGS_KROT=2) and non-temporal O-proj
   run c1_base 300 $B --concurrency 1 --steps 300 --warmup 30
   run c1_krot2 300 env XGS_KROT=2 $B --concurrency 1 --steps 300 --warmup 30
   run c1_ont 300 env XGS_M64_PLANS="4096x4096x1@16=1,3,1" $B --concurrency 1 --steps 300 --warmup 30 ;;
+r4w)  # round 4: split attention combine inside the O GEMM (gemm_m64g_xl): tests, batch-1 / batch-8 A/B
+  pyt xl_tests 400 tests/test_fused_decode_gpu.py -k "xl or combines or logits"
+  run c1_base 300 $B --concurrency 1 --steps 300 --warmup 30
+  run c1_xl 300 env XGS_XL_COMBINE=1 $B --concurrency 1 --steps 300 --warmup 30
+  run c1_base2 300 $B --concurrency 1 --steps 300 --warmup 30
+  run c1_xl2 300 env XGS_XL_COMBINE=1 $B --concurrency 1 --steps 300 --warmup 30
+  run c8_base 300 $B --concurrency 8 --steps 200 --warmup 30
+  run c8_xl 300 env XGS_XL_COMBINE=1 $B --concurrency 8 --steps 200 --warmup 30 ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;
