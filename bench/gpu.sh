@@ -284,6 +284,13 @@ r4w)  # round 4: split attention combine inside the O GEMM (gemm_m64g_xl): tests
   run c1_xl2 300 env XGS_XL_COMBINE=1 $B --concurrency 1 --steps 300 --warmup 30
   run c8_base 300 $B --concurrency 8 --steps 200 --warmup 30
   run c8_xl 300 env XGS_XL_COMBINE=1 $B --concurrency 8 --steps 200 --warmup 30 ;;
+r4x)  # round 4: decode-attention split target at batch 1 / 8 (16 / 8 / 4 splits at batch 1; needed a temporary XGS_DECODE_SPLIT_WGS override of ModelRunner.DECODE_SPLIT_WGS)
+  run c1_512 300 $B --concurrency 1 --steps 300 --warmup 30
+  run c1_64 300 env XGS_DECODE_SPLIT_WGS=64 $B --concurrency 1 --steps 300 --warmup 30
+  run c1_32 300 env XGS_DECODE_SPLIT_WGS=32 $B --concurrency 1 --steps 300 --warmup 30
+  run c1_512b 300 $B --concurrency 1 --steps 300 --warmup 30
+  run c8_512 300 $B --concurrency 8 --steps 200 --warmup 30
+  run c8_128 300 env XGS_DECODE_SPLIT_WGS=128 $B --concurrency 8 --steps 200 --warmup 30 ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;
