@@ -291,6 +291,14 @@ r4x)  # round 4: decode-attention split target at batch 1 / 8 (16 / 8 / 4 splits
   run c1_512b 300 $B --concurrency 1 --steps 300 --warmup 30
   run c8_512 300 $B --concurrency 8 --steps 200 --warmup 30
   run c8_128 300 env XGS_DECODE_SPLIT_WGS=128 $B --concurrency 8 --steps 200 --warmup 30 ;;
+r4y)  # round 4: re-tune the config-3 library GEMMs with a 5x longer TunableOp budget per shape
+  export PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_MAX_TUNING_DURATION_MS=500
+  export XGS_GEMM_TUNING=0
+  run t_c64_long 900 env PYTORCH_TUNABLEOP_FILENAME="$o/t_c64_long.csv" $B --steps 120 --warmup 40 ;;
+r4z)  # round 4: the re-tuned mixed-step QKV entry in the shipped TunableOp table
+  run c64_a 300 $B --steps 600 --warmup 50
+  run driver 200 $B --steps 20 --warmup 5
+  run c64_b 300 $B --steps 600 --warmup 50 ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;
