@@ -63,7 +63,8 @@ struct M64Epi {
   // 1-D grid fold the previous projection's split-K partials ar_part [ar_S, M, K] into
   // the residual stream x (in place) and write its statistics to ss_in; the other
   // workgroups (ar_tiles x ar_splits GEMM tiles) issue their first weight chunks, then
-  // wait for them (ar_flag: arrival count + pass count, zero between launches).
+  // wait for them (ar_flag: arrival count + pass count, zero between launches; word 2
+  // counts waits that timed out -- a sticky fault the host checks, m64_arx_fault).
   const float* ar_part = nullptr;
   int ar_S = 0;
   int ar_wgs = 0;  // 0: no prologue (2-D grid)
@@ -314,7 +315,10 @@ __device__ __forceinline__ void m64g_ar_wait(const M64Epi& epi, int ngemm) {
     const uint64_t t0 = wall_clock64();
     while (__hip_atomic_load(epi.ar_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epi.ar_wgs) {
       __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > 200000000ull) break;  // 2 s
+      if (wall_clock64() - t0 > 200000000ull) {  // 2 s: record the fault (sticky word 2), never hang
+        __hip_atomic_fetch_add(epi.ar_flag + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
     }
     if (__hip_atomic_fetch_add(epi.ar_flag + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngemm - 1) {
       __hip_atomic_store(epi.ar_flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1053,8 +1057,9 @@ int gemm_m64g_ex(const uint16_t* x, int M, int K, const uint16_t* w, int N, floa
 // projection's split-K partials ar_part [ar_S, M, K] into it, in the same launch
 // (m64g_ar_role / m64g_ar_wait): the weight stream starts under the fold (and under a
 // simulated all-reduce wait of ar_ticks). ss [K / 1024, M] receives the residual's
-// statistics and is this GEMM's input-norm row scale. flags: 2 ints, zero before the
-// first launch (each launch leaves them zero). PARTIAL / SiLU modes.
+// statistics and is this GEMM's input-norm row scale. flags: 3 ints, zero before the
+// first launch (each launch leaves words 0-1 zero; word 2 counts timed-out waits).
+// PARTIAL / SiLU modes.
 int gemm_m64g_arx(uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
                   int nw, int cfg, float* ss, float eps, int* counters, const float* ar_part, int ar_S, int ar_wgs,
                   int* flags, uint64_t ar_ticks, hipStream_t st) {

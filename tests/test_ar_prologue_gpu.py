@@ -63,7 +63,7 @@ def test_arx_matches_separate_fold(M, shape, ticks):
     key = (N, K, mode)
     old = lin._M64_TUNED.get(key)
     lin._M64_TUNED[key] = {16: p_small, 32: p_big, 64: p_big}
-    flags = torch.zeros(2, dtype=torch.int32, device=DEV)
+    flags = torch.zeros(3, dtype=torch.int32, device=DEV)
     try:
         runs = []
         for _ in range(3):  # the flags are re-armed by each launch
@@ -75,7 +75,7 @@ def test_arx_matches_separate_fold(M, shape, ticks):
             assert torch.equal(r, r_ref)
             assert rel_err(ss, ss_ref) < 1e-5
             assert rel_err(y, ref) < (2e-3 if mode == MODE_PARTIAL else 1e-2)
-            assert int(flags.abs().sum()) == 0
+            assert int(flags.abs().sum()) == 0  # re-armed, and no wait timed out (word 2)
             runs.append(y.clone())
         assert all(torch.equal(runs[0], t) for t in runs)
     finally:
@@ -120,4 +120,5 @@ def test_tp_shard_decode_with_ar_prologue(llama_tp4_shard, n_seqs, monkeypatch):
         eng.generate(prompts, sp)
         logits[on] = eng.runner.last_logits[-1].float().cpu()
         assert (calls[0] > 0) is on  # the fused decode layer ran the prologue form
+        assert lin.m64_arx_fault(llama_tp4_shard._fused_ws.ar_flags) == 0
     assert rel_err(logits[True], logits[False]) < 1e-2

@@ -386,8 +386,9 @@ class ResidWorkspace:
         # arrival tickets (GG_RESID: one word per tile): zero here, and every launch
         # re-arms the words it used
         self.counters = torch.zeros(n_sites, 2 * self.MAX_TILES, dtype=torch.int32, device=device)
-        # all-reduce prologue (m64_arx_linear): arrival + pass count, re-armed by each launch
-        self.ar_flags = torch.zeros(2, dtype=torch.int32, device=device)
+        # all-reduce prologue (m64_arx_linear): arrival + pass count, re-armed by each launch;
+        # word 2 counts timed-out waits (m64_arx_fault)
+        self.ar_flags = torch.zeros(3, dtype=torch.int32, device=device)
 
 
 # Prefill-sized down projections (K = 3.5 N) have too few output tiles for the chip at
@@ -487,6 +488,8 @@ def m64_arx_linear(resid: torch.Tensor, prev: PendingSum, w: torch.Tensor, mode:
     if wgs is None:
         wgs = min(M * (K // 1024), 32)
     k = kernels()
+    if flags.numel() < 3 or flags.dtype != torch.int32:
+        raise ValueError("gemm_m64g_arx: flags must be 3 int32 words")
     ar = (prev.part.data_ptr(), prev.part.shape[0], wgs, flags.data_ptr(), int(ticks), stream_ptr())
     if mode == MODE_PARTIAL:
         part = torch.empty(S, M, N, dtype=torch.float32, device=resid.device)
@@ -501,6 +504,12 @@ def m64_arx_linear(resid: torch.Tensor, prev: PendingSum, w: torch.Tensor, mode:
     k.gemm_m64g_arx(resid.data_ptr(), M, K, w.data_ptr(), N, part, out.data_ptr(), S, mode, nw, cfg, ss.data_ptr(),
                     float(eps), cnt, *ar)
     return out
+
+
+def m64_arx_fault(flags: torch.Tensor) -> int:
+    """Waits of the all-reduce prologue that gave up (2 s) since `flags` was zeroed:
+    non-zero means a reducer never arrived and those launches computed on stale x."""
+    return int(flags[2].item())
 
 
 def m64_resid_linear(x, w: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace, site: int,
