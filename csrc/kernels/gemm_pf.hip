@@ -1,0 +1,520 @@
+// gemm_pf: prompt-sized MFMA GEMM (M ~ 256 .. 8192) for the projections of mixed
+// continuous-batching steps and prefill:
+//
+//   out[M, N] = x[M, K] . W[N, K]^T        (bf16 in, fp32 accumulate)
+//
+// Replaces the library GEMM of the mixed step (VERDICT r4 "next round" #1): at
+// M ~ 575 the four projections of a Llama-3-8B layer are ~250 GFLOP, compute-
+// bound, so the kernel is built around keeping the matrix pipe busy
+// (cdna_hip_programming.md §5 "The 256² 8-phase template", §5.5 T1-T5):
+//
+//   * one 512-thread workgroup per CU owns a BM x 256 output tile (BM = 128 / 192
+//     / 256) over 64-deep K tiles; 8 waves as 2 (M) x 4 (N): wave (wr, wc) owns
+//     BM/2 rows x 64 columns, v_mfma_f32_16x16x32_bf16 (the DVFS-favourable shape,
+//     MI355X_MICROARCH.md "DVFS give-back" item 7) with the W fragment as the MFMA
+//     A operand, so each lane ends with 4 consecutive output columns of one row;
+//   * a K tile is consumed in P = BM/64 PHASES; phase q covers 32 rows of each
+//     wave's half (64 A rows of the tile), so its A rows are free for restaging as
+//     soon as phase q is over. The W tile (256 rows) is read into registers once,
+//     in phase 0. Two LDS slots (K tiles t and t+1); the pieces of tile t+2 are
+//     re-staged into tile t's slot phase by phase as they are released, so ~1.5 K
+//     tiles of LDS-DMA stay in flight across the barriers under counted
+//     s_waitcnt vmcnt(N) (never 0 in steady state; §5 "Pipelining across
+//     barriers") -- the counts come from a constexpr simulation of the issue
+//     order (pf_wait_count);
+//   * both operands by global_load_lds_dwordx4 (8 rows x 128 B per wave
+//     instruction) into lane-linear images, 16-B granule XOR-swizzle (granule ^
+//     row & 7) on the global SOURCE address and on the ds_read_b128 fragment
+//     reads (rule 21 / T2);
+//   * ping-pong: waves 4-7 (wr = 1) run one barrier behind waves 0-3, so on every
+//     SIMD (waves w and w + 4 share one) one wave's MFMA segment overlaps its
+//     partner's fragment reads + DMA issue. Every piece is waited for one barrier
+//     earlier than its first reader needs ("one barrier MORE when two wave groups
+//     run staggered", §5 "Read a staged buffer one phase AFTER the wait"), and the
+//     fragment reads retire (lgkmcnt(0)) before the barrier that ends their
+//     segment, so a slot region can be re-staged in the very next phase (WAR);
+//   * XCD-bijective block order with the M tiles of one W tile adjacent, so a W
+//     tile's M tiles run on one XCD and read it through one L2 (T1); optional
+//     K-tile rotation per W tile (the lock-step HBM stream of r4_mw_probe.md);
+//   * split-K (uneven ranges) for grids that would not fill the chip: fp32
+//     partials [S, M, N] reduced by the consumer (rope_cache_partials /
+//     add_partials_rmsnorm), like every other projection kernel here.
+// Epilogues: bf16, fp32 partials, or silu(gate) * up of a block-16 interleaved
+// gate|up weight (the SiLU-gate fused: no [M, 2F] intermediate).
+#include <type_traits>
+
+#include "glds.h"
+
+namespace xgk {
+
+int k_rotation(int S);  // gemm_m64g.hip
+
+enum : int { PF_BF16 = 0, PF_PARTIAL = 1, PF_SILU = 2 };
+constexpr int PF_GROUP_M = 8;  // M tiles per group of the tile order
+// K-tile rotation per W tile (XGS_PF_KROT=1; off by default): it spreads the
+// lock-step HBM stream of the weight-streaming kernels, but here it would put the
+// N tiles that share an A panel on different K tiles and lose that panel's L2 reuse
+static int pf_krot = 0;
+void set_pf_krot(int on) { pf_krot = on; }
+
+namespace pf {
+constexpr int BN = 256;  // output columns per workgroup (4 waves x 64)
+constexpr int NBW = 4;   // W-tile DMA instructions per wave per K tile (256 rows x 128 B / 8 waves / 1 KB)
+
+// Steady-state DMA issue order per wave (P phases per K tile, NA = A-piece DMA
+// instructions per wave per phase). Tile t, phase 0 issues A piece P-1 of tile
+// t+1; phase p >= 1 issues A piece p-1 of tile t+2. W piece i of tile u goes in
+// position i % P of the P phases from (u-2, phase 1) to (u-1, phase 0): phases
+// 1..P-1 of tile u-2, then phase 0 of tile u-1 (its W image is free after phase 0
+// of tile u-2). Within a phase: the A pieces first, then the W pieces.
+constexpr int b_phase(int P, int i) { return (i % P + 1) % P; }
+constexpr int nb_in_phase(int P, int ph) {
+  int c = 0;
+  for (int i = 0; i < NBW; ++i) c += b_phase(P, i) == ph ? 1 : 0;
+  return c;
+}
+constexpr int n_issue(int P, int NA, int ph) { return NA + nb_in_phase(P, ph); }
+constexpr int tile_issues(int P, int NA) {
+  int s = 0;
+  for (int ph = 0; ph < P; ++ph) s += n_issue(P, NA, ph);
+  return s;
+}
+constexpr int pos(int P, int NA, int tau, int ph, int j) {
+  int o = 0;
+  for (int q = 0; q < ph; ++q) o += n_issue(P, NA, q);
+  return tau * tile_issues(P, NA) + o + j;
+}
+// the last A DMA of A piece q of tile u
+constexpr int pos_a(int P, int NA, int u, int q) {
+  return q <= P - 2 ? pos(P, NA, u - 2, q + 1, NA - 1) : pos(P, NA, u - 1, 0, NA - 1);
+}
+constexpr int pos_b(int P, int NA, int u, int i) {
+  const int ph = b_phase(P, i);
+  int j = NA;
+  for (int i2 = 0; i2 < i; ++i2) j += b_phase(P, i2) == ph ? 1 : 0;
+  return pos(P, NA, ph == 0 ? u - 1 : u - 2, ph, j);
+}
+// vmcnt that retires everything phase p of a steady-state tile reads (A piece p,
+// plus the whole W tile at p = 0), counted where the wait sits: after the issues
+// of the previous phase, before those of phase p
+constexpr int wait_count(int P, int NA, int p) {
+  const int t = 8;
+  int latest = pos_a(P, NA, t, p);
+  if (p == 0)
+    for (int i = 0; i < NBW; ++i) latest = latest > pos_b(P, NA, t, i) ? latest : pos_b(P, NA, t, i);
+  return pos(P, NA, t, p, 0) - 1 - latest;
+}
+static_assert(wait_count(4, 1, 0) == 6 && wait_count(4, 1, 1) == 13 && wait_count(4, 1, 2) == 13 &&
+                  wait_count(4, 1, 3) == 13, "pf wait counts (P = 4)");
+static_assert(wait_count(2, 2, 0) == 4 && wait_count(2, 2, 1) == 10, "pf wait counts (P = 2, NA = 2)");
+}  // namespace pf
+
+template <int P, int NA, int PH>
+__device__ __forceinline__ void pf_wait(bool steady) {
+  if (steady) wait_vmcnt<pf::wait_count(P, NA, PH)>();
+  else wait_vmcnt<0>();
+}
+
+// Stream-K (sk_grid > 0): `sk_grid` persistent workgroups split the TM x TN x nk
+// K-tile iterations evenly, so a grid whose tile count is not a multiple of the CU
+// count (336 tiles of the 8B gate_up at M = 575 on 256 CUs) runs ~1.3 tile-times
+// instead of 2. Workgroup g owns iterations [start(g), start(g+1)), start(g) =
+// floor(g I / G): a suffix of one tile, whole tiles, a prefix of another. A tile
+// finished by several workgroups is combined by the last arriver: every other
+// contributor writes its fp32 accumulators (lane-major, write-through sc1) to its
+// workspace slot (g, 0) if the tile holds the START of its range, else (g, 1), then
+// adds its iteration count to the tile's ticket (relaxed, agent scope); the one
+// whose add completes nk acquires, adds every other contributor's slot into its
+// registers and runs the epilogue (Guideline 16 / §5 "In-launch split-K
+// reduction", sc1 form). Tickets re-arm themselves (the last arriver zeroes them).
+struct PfSk {
+  float* ws;      // [sk_grid][2][512 threads x ACC floats]
+  int* tickets;   // [tiles], zero between launches
+  int grid;       // 0: data-parallel (grid = tiles x S)
+};
+
+template <int BM, int MTP, bool NT, int PR = 0, bool SKM = false>
+__global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restrict__ x, int M, int K,
+                                                          const uint16_t* __restrict__ w, int N, int S,
+                                                          float* __restrict__ part, uint16_t* __restrict__ out,
+                                                          int mode, int krot, PfSk sk) {
+  // MTP: 16-row m tiles per wave per phase -> a phase is MTP x 4 x 2 MFMAs per wave
+  // and releases 32 MTP A rows (NA = MTP / 2 DMA instructions per wave)
+  constexpr int P = BM / (32 * MTP);
+  constexpr int NA = MTP / 2;
+  constexpr int PB = 32 * MTP * 128;       // bytes of one A phase block
+  constexpr int BN = pf::BN;
+  constexpr int ASZ = BM * 128;            // A image: P phase blocks
+  constexpr int SLOT = ASZ + BN * 128;     // + the W image
+  constexpr int NACC = P * MTP * 4;        // f32x4 accumulators per lane
+  static_assert(P >= 2 && P * 32 * MTP == BM && (MTP == 2 || MTP == 4), "gemm_pf geometry");
+  static_assert(2 * SLOT + 16 <= 160 * 1024, "LDS");
+  // ONE __shared__ object (cdna_hip_programming.md §5 "Three .s-level traps" (a));
+  // the last 16 bytes hold the stream-K "last arriver" flag
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * SLOT + 16];
+  int* const sk_flag = reinterpret_cast<int*>(smem + 2 * SLOT);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;   // wave-uniform (scalar): guards barriers below
+  const int g = lane >> 4, li = lane & 15;
+
+  // XCD-bijective virtual block id (T1)
+  const int TM = (M + BM - 1) / BM, TN = N / BN;
+  const int nb = gridDim.x, bid = blockIdx.x;
+  const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7;
+  const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int per_split = TM * TN;
+  const int nk_all = K / 64;
+  // grouped order: GM M tiles x every N tile per group, M fastest inside a group, so
+  // the ~32 workgroups an XCD runs at once share a few A and W panels (L2 hits)
+  const int GM = TM < PF_GROUP_M ? TM : PF_GROUP_M;
+  auto tile_mn = [&](int u, int& m0, int& n0) {
+    const int gsz = GM * TN, gid = u / gsz, first_m = gid * GM;
+    const int gm = TM - first_m < GM ? TM - first_m : GM;
+    const int ug = u - gid * gsz;
+    m0 = (first_m + ug % gm) * BM;
+    n0 = (ug / gm) * BN;
+  };
+
+  // DMA lanes: row dr of an 8-row piece, physical granule dj holding logical dj ^ dr
+  const int dr = lane >> 3, dj = lane & 7;
+  const int sw = 8 * (dj ^ dr);
+  const int wrow = wc * 64;          // W rows of this wave within the W image
+  const int arl = wr * 16 * MTP;     // this wave's rows within an A phase block
+  const int sl = li & 7;             // swizzle key of every fragment row this lane reads
+
+  f32x4_t acc[P][MTP][4];
+  uint4 bfr[4][2];
+  uint4 afr[MTP][2];
+
+  // ---- one K range [kt_lo, kt_lo + nk) of the tile at (m0, n0) into acc
+  auto compute = [&](int m0, int n0, int kt_lo, int nk) {
+    const int rot = krot ? ((n0 / BN) * 37) % nk : 0;
+    // A phase block q: rows [wr 0: 16 MTP rows][wr 1: 16 MTP rows]; DMA a of wave wid
+    // fills block rows 8 (NA wid + a) .. + 7
+    const uint16_t* asrc[P][NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      const int br = 8 * (NA * wid + a) + dr;
+      const int half = br / (16 * MTP);
+      const int r = half * (BM / 2) + br - half * 16 * MTP;
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+        asrc[q][a] = x + static_cast<int64_t>(min(m0 + r + 16 * MTP * q, M - 1)) * K + sw;
+    }
+    const uint16_t* bsrc = w + static_cast<int64_t>(n0 + 32 * wid + dr) * K + sw;  // + 8 i rows per piece
+    auto kof = [&](int t) {
+      const int tt = t + rot;
+      return (kt_lo + (tt >= nk ? tt - nk : tt)) * 64;
+    };
+    auto issue_a = [&](int t, int q) {
+      if constexpr (PR == 1) return;
+#pragma unroll
+      for (int a = 0; a < NA; ++a)
+        glds16(asrc[q][a] + kof(t), smem + (t & 1) * SLOT + q * PB + (NA * wid + a) * 1024);
+    };
+    auto issue_b = [&](int t, int i) {
+      if constexpr (PR == 1) return;
+      const uint16_t* src = bsrc + static_cast<int64_t>(8 * i) * K + kof(t);
+      uint8_t* dst = smem + (t & 1) * SLOT + ASZ + (4 * wid + i) * 1024;
+      if constexpr (NT) glds16_nt(src, dst);
+      else glds16(src, dst);
+    };
+    // the DMA of phase PH of tile t (steady-state order, pf:: above)
+    auto issue_phase = [&](int t, auto ph_c) {
+      constexpr int PH = decltype(ph_c)::value;
+      if constexpr (PH == 0) {
+        if (t + 1 < nk) {
+          issue_a(t + 1, P - 1);
+#pragma unroll
+          for (int i = 0; i < pf::NBW; ++i)
+            if (pf::b_phase(P, i) == 0) issue_b(t + 1, i);
+        }
+      } else {
+        if (t + 2 < nk) {
+          issue_a(t + 2, PH - 1);
+#pragma unroll
+          for (int i = 0; i < pf::NBW; ++i)
+            if (pf::b_phase(P, i) == PH) issue_b(t + 2, i);
+        }
+      }
+    };
+
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+#pragma unroll
+      for (int mt = 0; mt < MTP; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[q][mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    // every wave is past the previous range's LDS reads before its slots are refilled
+    __syncthreads();
+    // prologue: the issues of (virtual) tiles -2 and -1, in steady-state order
+#pragma unroll
+    for (int ph = 1; ph < P; ++ph) {
+      issue_a(0, ph - 1);
+#pragma unroll
+      for (int i = 0; i < pf::NBW; ++i)
+        if (pf::b_phase(P, i) == ph) issue_b(0, i);
+    }
+    issue_a(0, P - 1);
+#pragma unroll
+    for (int i = 0; i < pf::NBW; ++i)
+      if (pf::b_phase(P, i) == 0) issue_b(0, i);
+    if (nk > 1) {
+#pragma unroll
+      for (int ph = 1; ph < P; ++ph) {
+        issue_a(1, ph - 1);
+#pragma unroll
+        for (int i = 0; i < pf::NBW; ++i)
+          if (pf::b_phase(P, i) == ph) issue_b(1, i);
+      }
+    }
+    // wait for what (tile 0, phase 0) reads; the steady count holds iff every issue
+    // between that piece and the wait exists: target tile tt <= nk - 3, or tt == nk - 2
+    // with phase <= 1
+    pf_wait<P, NA, 0>(nk >= 2);
+    if (wr == 1) raw_barrier();  // the stagger: waves 4-7 one barrier behind
+
+    auto phase = [&](int t, auto ph_c) {
+      constexpr int p = decltype(ph_c)::value;
+      const uint8_t* slot = smem + (t & 1) * SLOT;
+      // the wait at the end of this phase retires what the NEXT phase reads
+      constexpr int PN = (p + 1 < P) ? p + 1 : 0;
+      const int tt = (p + 1 < P) ? t : t + 1;
+      const bool need = tt < nk;
+      const bool steady = (tt <= nk - 3) || (tt == nk - 2 && PN <= 1);
+      // ---- load segment: this phase's DMA, then the fragment reads
+      raw_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      issue_phase(t, ph_c);
+      if constexpr (p == 0) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            bfr[nt][ks] = *reinterpret_cast<const uint4*>(slot + ASZ + (wrow + 16 * nt + li) * 128 +
+                                                           (((4 * ks + g) ^ sl) << 4));
+      }
+#pragma unroll
+      for (int mt = 0; mt < MTP; ++mt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          afr[mt][ks] = *reinterpret_cast<const uint4*>(slot + p * PB + (arl + 16 * mt + li) * 128 +
+                                                         (((4 * ks + g) ^ sl) << 4));
+      // fragment reads retire before the barrier: the region may be re-staged next phase
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (wr == 1 && need) pf_wait<P, NA, PN>(steady);
+      raw_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- MFMA segment
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < (PR == 2 ? 0 : 2); ++ks)
+#pragma unroll
+        for (int mt = 0; mt < MTP; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+            acc[p][mt][nt] = mfma16x16x32(as_frag(bfr[nt][ks]), as_frag(afr[mt][ks]), acc[p][mt][nt]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (wr == 0 && need) pf_wait<P, NA, PN>(steady);
+    };
+    for (int t = 0; t < nk; ++t) {
+      phase(t, std::integral_constant<int, 0>{});
+      phase(t, std::integral_constant<int, 1>{});
+      if constexpr (P > 2) phase(t, std::integral_constant<int, (P > 2 ? 2 : 0)>{});
+      if constexpr (P > 3) phase(t, std::integral_constant<int, (P > 3 ? 3 : 0)>{});
+    }
+    if (wr == 0) raw_barrier();  // equal barrier counts in both groups
+  };
+
+  // ---- epilogue of a finished tile (split s of S for PF_PARTIAL)
+  // acc[q][mt][nt][r] = out[m = m0 + wr BM/2 + 16 MTP q + 16 mt + li][n = n0 + wrow + 16 nt + 4 g + r]
+  auto epilogue = [&](int m0, int n0, int s) {
+    const int mb = m0 + wr * (BM / 2) + li;
+    const int nb0 = n0 + wrow + 4 * g;
+    if (mode == PF_PARTIAL) {
+      float* pp = part + static_cast<int64_t>(s) * M * N;
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int mt = 0; mt < MTP; ++mt) {
+          const int m = mb + 16 * MTP * q + 16 * mt;
+          if (m >= M) continue;
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+            *reinterpret_cast<float4*>(pp + static_cast<int64_t>(m) * N + nb0 + 16 * nt) =
+                make_float4(acc[q][mt][nt][0], acc[q][mt][nt][1], acc[q][mt][nt][2], acc[q][mt][nt][3]);
+        }
+    } else if (mode == PF_BF16) {
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int mt = 0; mt < MTP; ++mt) {
+          const int m = mb + 16 * MTP * q + 16 * mt;
+          if (m >= M) continue;
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            uint2 o;
+            o.x = pack2(acc[q][mt][nt][0], acc[q][mt][nt][1]);
+            o.y = pack2(acc[q][mt][nt][2], acc[q][mt][nt][3]);
+            *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * N + nb0 + 16 * nt) = o;
+          }
+        }
+    } else {
+      // SiLU gate: n tiles 2j (gate) / 2j + 1 (up) are one interleaved 16-row block pair
+      const int F = N / 2, f0 = (n0 + wrow) / 2 + 4 * g;
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int mt = 0; mt < MTP; ++mt) {
+          const int m = mb + 16 * MTP * q + 16 * mt;
+          if (m >= M) continue;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            float o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float gt = acc[q][mt][2 * j][r];
+              o[r] = gt / (1.f + __expf(-gt)) * acc[q][mt][2 * j + 1][r];
+            }
+            uint2 v2;
+            v2.x = pack2(o[0], o[1]);
+            v2.y = pack2(o[2], o[3]);
+            *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * F + f0 + 16 * j) = v2;
+          }
+        }
+    }
+  };
+
+  if constexpr (!SKM) {  // data-parallel: one (tile, split) per workgroup
+    const int s = v / per_split;
+    int m0, n0;
+    tile_mn(v - s * per_split, m0, n0);
+    const int kt_lo = s * nk_all / S;
+    compute(m0, n0, kt_lo, (s + 1) * nk_all / S - kt_lo);
+    epilogue(m0, n0, s);
+  } else {  // stream-K
+    const int64_t I = static_cast<int64_t>(per_split) * nk_all;
+    const int G = sk.grid;
+    auto start = [&](int gg) { return static_cast<int64_t>(gg) * I / G; };
+    auto slot_of = [&](int gg, int tile) {  // workspace slot of contributor gg to `tile`
+      return sk.ws + (static_cast<int64_t>(gg) * 2 + (start(gg) >= static_cast<int64_t>(tile) * nk_all ? 0 : 1)) *
+                         (512 * NACC * 4);
+    };
+    const int64_t it_hi = start(v + 1);
+    for (int64_t it = start(v); it < it_hi;) {
+      const int tile = static_cast<int>(it / nk_all);
+      const int k0 = static_cast<int>(it - static_cast<int64_t>(tile) * nk_all);
+      const int k1 = static_cast<int>(min(static_cast<int64_t>(nk_all), k0 + (it_hi - it)));
+      it += k1 - k0;
+      int m0, n0;
+      tile_mn(tile, m0, n0);
+      compute(m0, n0, k0, k1 - k0);
+      if (k0 != 0 || k1 != nk_all) {
+        // a shared tile: publish, then the last arriver combines
+        float* mine = slot_of(v, tile) + tid * 4;
+#pragma unroll
+        for (int q = 0; q < P; ++q)
+#pragma unroll
+          for (int mt = 0; mt < MTP; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) st16_sc1(mine + ((q * MTP + mt) * 4 + nt) * 512 * 4, acc[q][mt][nt]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains (write-through)
+        __syncthreads();
+        if (tid == 0) {
+          const int prev = __hip_atomic_fetch_add(sk.tickets + tile, k1 - k0, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+          const int last = prev + (k1 - k0) == nk_all;
+          if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(sk.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          *sk_flag = last;
+        }
+        __syncthreads();
+        if (*sk_flag == 0) continue;
+        // contributors: the workgroups owning iterations [tile nk, tile nk + nk)
+        const int64_t t_lo = static_cast<int64_t>(tile) * nk_all;
+        const int g_lo = static_cast<int>(((t_lo + 1) * G - 1) / I);
+        const int g_hi = static_cast<int>(((t_lo + nk_all) * G - 1) / I);
+        for (int gg = g_lo; gg <= g_hi; ++gg) {
+          if (gg == v) continue;
+          const float* other = slot_of(gg, tile) + tid * 4;
+#pragma unroll
+          for (int q = 0; q < P; ++q)
+#pragma unroll
+            for (int mt = 0; mt < MTP; ++mt)
+#pragma unroll
+              for (int nt = 0; nt < 4; ++nt) {
+                const float4 o = *reinterpret_cast<const float4*>(other + ((q * MTP + mt) * 4 + nt) * 512 * 4);
+                acc[q][mt][nt] += f32x4_t{o.x, o.y, o.z, o.w};
+              }
+        }
+      }
+      epilogue(m0, n0, 0);
+    }
+  }
+}
+
+template <int BM, int MTP, bool NT, int PR = 0>
+static int launch_pf(int tiles, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N, int S,
+                     float* part, uint16_t* out, int mode, PfSk sk) {
+  if (sk.grid)
+    hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, true>), dim3(sk.grid), dim3(512), 0, st, x, M, K, w, N, S,
+                       part, out, mode, pf_krot, sk);
+  else
+    hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, false>), dim3(tiles * S), dim3(512), 0, st, x, M, K, w, N,
+                       S, part, out, mode, pf_krot, sk);
+  return static_cast<int>(hipGetLastError());
+}
+
+// cfg % 8 -> (BM, MTP, NT): 0 (256, 2, -) 1 (192, 2, -) 2 (128, 2, -) 3 (256, 4, -)
+// 4 (256, 2, nt) 5 (192, 2, nt) 6 (128, 2, nt) 7 (256, 4, nt); cfg / 8: 0 the kernel,
+// 1 no DMA, 2 no MFMA (anatomy probes, bench/pf_gemm_bench.py --probe: garbage results)
+int pf_cfg_bm(int cfg) { return (cfg & 3) == 1 ? 192 : ((cfg & 3) == 2 ? 128 : 256); }
+
+template <int PR>
+static int launch_pf_cfg(int c, int tiles, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N,
+                         int S, float* part, uint16_t* out, int mode, PfSk sk) {
+  switch (c) {
+    case 0: return launch_pf<256, 2, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 1: return launch_pf<192, 2, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 2: return launch_pf<128, 2, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 3: return launch_pf<256, 4, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 4: return launch_pf<256, 2, true, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 5: return launch_pf<192, 2, true, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 6: return launch_pf<128, 2, true, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    default: return launch_pf<256, 4, true, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+  }
+}
+
+// sk_grid > 0: stream-K over sk_grid persistent workgroups (S must be 1); ws holds
+// sk_grid x 2 x pf_sk_slot_floats(cfg) floats, tickets one zeroed int per tile
+int pf_sk_slot_floats(int cfg) { return 512 * (pf_cfg_bm(cfg) / 32) * 4 * 4; }
+
+int gemm_pf(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
+            int cfg, int sk_grid, float* sk_ws, int* sk_tickets, hipStream_t st) {
+  if (M < 1 || K < 64 || K % 64 || N < pf::BN || N % pf::BN || S < 1 || S > K / 64 || cfg < 0 || cfg >= 24) return 1;
+  if (sk_grid < 0 || (sk_grid > 0 && (S != 1 || sk_ws == nullptr || sk_tickets == nullptr))) return 1;
+  if (mode == PF_PARTIAL) {
+    if (part == nullptr) return 1;
+  } else if (mode == PF_BF16 || mode == PF_SILU) {
+    if (out == nullptr || S != 1) return 1;
+  } else {
+    return 1;
+  }
+  const int bm = pf_cfg_bm(cfg);
+  const int tiles = ((M + bm - 1) / bm) * (N / pf::BN);
+  const PfSk sk{sk_ws, sk_tickets, sk_grid};
+  switch (cfg / 8) {
+    case 0: return launch_pf_cfg<0>(cfg % 8, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 1: return launch_pf_cfg<1>(cfg % 8, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    default: return launch_pf_cfg<2>(cfg % 8, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+  }
+}
+
+}  // namespace xgk

@@ -26,6 +26,10 @@ int gemm_m64g_ex(const uint16_t*, int, int, const uint16_t*, int, float*, uint16
 int gemm_m64g_arx(uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, float*, float,
                   int*, const float*, int, int, int*, uint64_t, hipStream_t);
 int gemm_mw(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, hipStream_t);
+int gemm_pf(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, float*, int*,
+            hipStream_t);
+int pf_sk_slot_floats(int);
+void set_pf_krot(int);
 void set_k_rotation(int mode);
 int gemm_mw_probe(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 int gemm_mw_ss(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, const float*, int,
@@ -252,6 +256,15 @@ PYBIND11_MODULE(_kernels, m) {
                        S(st)),
           "gemm_mw");
   });
+  // prompt-sized MFMA GEMM (gemm_pf.hip): mixed steps above gemm_mw's range, prefill
+  m.def("gemm_pf", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
+                      int mode, int cfg, int sk_grid, uintptr_t sk_ws, uintptr_t sk_tickets, uintptr_t st) {
+    check(xgk::gemm_pf(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode, cfg,
+                       sk_grid, P<float>(sk_ws), P<int>(sk_tickets), S(st)),
+          "gemm_pf");
+  });
+  m.def("pf_sk_slot_floats", &xgk::pf_sk_slot_floats);
+  m.def("set_pf_krot", [](int on) { xgk::set_pf_krot(on); });
   m.def("set_k_rotation", [](int mode) { xgk::set_k_rotation(mode); });
   m.def("gemm_mw_probe", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
                             int mode, int cfg, int probe, uintptr_t st) {

@@ -298,6 +298,111 @@ def mw_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, plan=N
     return out
 
 
+# ---------------------------------------------------------------------------- gemm_pf (prompt-sized M)
+# csrc/kernels/gemm_pf.hip: BM x 256 output tiles (BM 256 / 192 / 128) on 8 waves,
+# 64-deep K tiles consumed in BM / 64 phases with the next tiles' LDS-DMA in flight
+# across the barriers, waves 4-7 one barrier behind waves 0-3 (MFMA / load
+# ping-pong per SIMD). cfg -> (BM, m tiles per wave per phase, non-temporal W):
+# 0 (256, 2) 1 (192, 2) 2 (128, 2) 3 (256, 4); 4-7 the same with non-temporal W DMA.
+PF_BM = (256, 192, 128)
+PF_CFG_BM = {0: 256, 1: 192, 2: 128, 3: 256}
+PF_MIN_M = 65
+PF_SK_MIN_TAIL = 0.15   # stream-K when the data-parallel grid's last round is this empty
+
+
+def pf_bm(M: int) -> int:
+    """The tile height that pads M least (ties -> the taller tile)."""
+    return min(PF_BM, key=lambda b: (-(-M // b) * b, -b))
+
+
+_CU_COUNT = {}
+
+
+def cu_count(device=None) -> int:
+    d = torch.cuda.current_device() if device is None else torch.device(device).index or 0
+    n = _CU_COUNT.get(d)
+    if n is None:
+        n = _CU_COUNT[d] = torch.cuda.get_device_properties(d).multi_processor_count
+    return n
+
+
+def pf_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL, cus: int = 256):
+    """(split_k, cfg, sk_grid) for gemm_pf, or None when the shape is unsupported.
+    PARTIAL: split-K (fp32 partials reduced by the consumer) until the grid reaches
+    ~`cus` workgroups. bf16 / SiLU: data-parallel, or stream-K over `cus`
+    persistent workgroups when the last data-parallel round would run mostly empty."""
+    if M < 1 or N % 256 or K % 64 or K < 64:
+        return None
+    bm = pf_bm(M)
+    cfg = PF_BM.index(bm)
+    if bm == 256:
+        cfg = 3  # 4 m tiles per wave per phase (32 MFMAs per segment)
+    tiles = -(-M // bm) * (N // 256)
+    if mode == MODE_PARTIAL:
+        S = 1
+        while tiles * (S + 1) <= cus * 1.15 and (S + 1) <= K // 256:
+            S += 1
+        return S, cfg, 0
+    rounds = tiles / cus
+    tail = -(-tiles // cus) - rounds
+    if tail > PF_SK_MIN_TAIL and rounds < 6:
+        return 1, cfg, cus
+    return 1, cfg, 0
+
+
+class _SkWorkspace:
+    def __init__(self):
+        self.ws = {}
+        self.tickets = {}
+        self.retired = []
+
+    def get(self, device, grid: int, cfg: int, tiles: int):
+        key = str(device)
+        need = grid * 2 * kernels().pf_sk_slot_floats(cfg)
+        w = self.ws.get(key)
+        if w is None or w.numel() < need:
+            if w is not None:
+                self.retired.append(w)  # captured graphs may still point at it
+            w = self.ws[key] = torch.empty(need, dtype=torch.float32, device=device)
+        t = self.tickets.get(key)
+        if t is None or t.numel() < tiles:
+            if t is not None:
+                self.retired.append(t)
+            t = self.tickets[key] = torch.zeros(max(tiles, 4096), dtype=torch.int32, device=device)
+        return w, t
+
+
+_PF_SK = _SkWorkspace()
+
+
+def pf_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_BF16, plan=None,
+              out: Optional[torch.Tensor] = None):
+    """gemm_pf: bf16 [M, N] (MODE_BF16), PendingSum (MODE_PARTIAL, reduced by the
+    consumer) or silu(gate) * up [M, N / 2] of a block-16 interleaved gate|up weight
+    (MODE_SILU)."""
+    M, K = x.shape
+    N = w.shape[0]
+    p = plan or pf_plan(M, N, K, mode, cu_count(x.device) if x.is_cuda else 256)
+    if p is None or not x.is_contiguous() or not w.is_contiguous():
+        raise ValueError(f"gemm_pf: unsupported M={M} N={N} K={K} mode={mode}")
+    S, cfg, skg = p if len(p) == 3 else (p[0], p[1], 0)
+    k = kernels()
+    wsp = tk = 0
+    if skg:
+        bm = PF_CFG_BM[cfg % 4]
+        wt, tt = _PF_SK.get(x.device, skg, cfg, -(-M // bm) * (N // 256))
+        wsp, tk = wt.data_ptr(), tt.data_ptr()
+    if mode == MODE_PARTIAL:
+        part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+        k.gemm_pf(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, cfg, skg, wsp, tk,
+                  stream_ptr())
+        return PendingSum(part, S)
+    if out is None:
+        out = torch.empty(M, N // 2 if mode == MODE_SILU else N, dtype=torch.bfloat16, device=x.device)
+    k.gemm_pf(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), S, mode, cfg, skg, wsp, tk, stream_ptr())
+    return out
+
+
 def lm_head_linear(h: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """bf16 logits h . w^T for the LM head: gemm_mw where the sweep measured a plan for
     this row bucket (_MW_TUNED, mode bf16), else hipBLASLt."""
