@@ -57,6 +57,9 @@ def parse():
                     help="sampling temperature of every request (0 = greedy, the headline)")
     ap.add_argument("--top-p", type=float, default=1.0)
     ap.add_argument("--top-k", type=int, default=0)
+    ap.add_argument("--allow-rccl-decode", action="store_true",
+                    help="with --tp > 1, report even if the custom xGMI all-reduce did not register (TP decode "
+                         "all-reduces on RCCL); without it such a run exits 3")
     ap.add_argument("--tp-shard", type=int, default=1,
                     help="single-GPU simulation of ONE rank of a TP group of this degree: the rank's weight / "
                          "KV shards and kernels, collectives replaced by local reductions (not a TP measurement: "
@@ -101,6 +104,41 @@ def launch_ranks(n: int) -> int:
         if live:
             time.sleep(0.05)
     return rc
+
+
+def preflight(st, world: int, tp: int, dev, eng) -> dict:
+    """First contact with a multi-GPU node, before anything is timed (every rank
+    takes part): the collective backend forms the N-rank
+    communicator and sums correctly, every GPU pair can reach the other (peer
+    access, what the custom all-reduce's IPC mappings need), and each TP group's
+    decode all-reduce is the self-tested custom kernel or, visibly, RCCL. The
+    result goes into the JSON line."""
+    import torch
+    import torch.distributed as dist
+    info = {"backend": None, "rccl_world": None, "tp_groups": None, "p2p_ok": None, "decode_ar": None,
+            "custom_ar_selftest": None}
+    if world > 1:
+        info["backend"] = str(dist.get_backend())
+        x = torch.full((4096,), float(st.rank + 1), dtype=torch.float32, device=dev)
+        dist.all_reduce(x)
+        ok = bool((x == world * (world + 1) / 2).all())
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        info["rccl_world"] = dist.get_world_size() if int(flag.item()) == 1 else -1
+        info["tp_groups"] = [list(range(r, r + tp)) for r in range(0, world, tp)]
+    if dev.type == "cuda":
+        n = torch.cuda.device_count()
+        info["p2p_ok"] = all(torch.cuda.can_device_access_peer(i, j) for i in range(n) for j in range(n) if i != j) \
+            if n > 1 else None
+    if tp > 1:
+        ar = getattr(eng, "custom_ar", None)
+        lib = "rccl" if info["backend"] == "nccl" else info["backend"]  # the library collective
+        info["custom_ar_selftest"] = getattr(ar, "verified", None)
+        # every rank must agree on the protocol (a refusal below is collective)
+        mine = torch.tensor([1 if ar is not None else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(mine, op=dist.ReduceOp.MIN)
+        info["decode_ar"] = ar.protocol() if (ar is not None and int(mine.item()) == 1) else lib
+    return info
 
 
 def main():
@@ -160,6 +198,18 @@ def main():
         shard_model = build_model(get_config(a.model), device=dev, tp=a.tp_shard, rank=0,
                                   weight_dtype=a.weight_dtype)
     eng = LLMEngine(ecfg, model=shard_model)
+    pre = preflight(st, world, a.tp, dev, eng)
+    if a.tp > 1 and pre["decode_ar"] not in ("ll", "pull") and not a.allow_rccl_decode:
+        if rank == 0:
+            print(f"bench.py: --tp {a.tp} but the custom xGMI all-reduce did not register (TP decode all-reduces "
+                  f"would run on {pre['decode_ar']}); pass --allow-rccl-decode to measure that anyway",
+                  file=sys.stderr)
+        dist.barrier()
+        dist.destroy_process_group()
+        return 3
+    if world > 1 and pre["rccl_world"] != world:
+        print(f"bench.py: collective check failed on the {world}-rank communicator: {pre}", file=sys.stderr)
+        return 3
     leader = st.tp_rank == 0
     # timing collectives run among the TP leaders only (followers sit in follower_loop)
     leaders = [r for r in range(world) if r % a.tp == 0]
@@ -298,7 +348,12 @@ def main():
                        "concurrency_per_replica": a.concurrency,
                        "sampling": ("greedy" if a.temperature <= 0 else
                                     f"temperature {a.temperature}, top_p {a.top_p}, top_k {a.top_k}")},
+            "rccl_world": pre["rccl_world"], "tp_groups": pre["tp_groups"], "p2p_ok": pre["p2p_ok"],
+            "decode_ar": pre["decode_ar"],
             "detail": {"initial_population": "steady-state (ages uniform on [0, output_len))",
+                       "backend": pre["backend"], "custom_ar_selftest": pre["custom_ar_selftest"],
+                       "prompt_gemm": "gemm_pf" if getattr(eng.model, "layers", None) is not None and
+                       getattr(eng.model.layers[0], "pf_ok", False) else "library",
                        "fill_steps": fill_steps, "window_engine_steps": window_steps,
                        "window_prompt_steps": window_mixed, "ttft_samples": len(ttfts),
                        "preemptions": st_["preemptions"], "kv_blocks": st_["kv_blocks_total"],

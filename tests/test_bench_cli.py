@@ -47,14 +47,32 @@ def _run(nproc, *args, launcher=True):
 @pytest.mark.parametrize("nproc,tp,model,par", [(2, 1, "llama-tiny", "dp2"), (2, 2, "llama-tiny", "tp2"),
                                                 (4, 2, "mixtral-tiny", "dp2xtp2")])
 def test_bench_multi_rank_json_contract(nproc, tp, model, par):
-    r = _run(nproc, "--tp", str(tp), "--model", model)
+    r = _run(nproc, "--tp", str(tp), "--model", model, *(["--allow-rccl-decode"] if tp > 1 else []))
     _check_contract(r, nproc, model, par, tp)
+    # pre-flight evidence: the communicator formed at world N and summed
+    # correctly, the TP groups, and which library carried the TP decode all-reduce
+    assert r["rccl_world"] == nproc
+    assert r["tp_groups"] == [list(range(g, g + tp)) for g in range(0, nproc, tp)]
+    assert r["p2p_ok"] is None  # no GPUs here
+    assert r["decode_ar"] == ("gloo" if tp > 1 else None)
+    assert r["detail"]["backend"] == "gloo"
+
+
+def test_bench_refuses_tp_without_custom_allreduce():
+    """--tp > 1 whose decode all-reduce would not be the custom xGMI kernel exits 3
+    unless --allow-rccl-decode says that is what is being measured."""
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", *SMALL, "--tp", "2", "--model", "llama-tiny"]
+    p = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=240)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert "allow-rccl-decode" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
 
 
 @pytest.mark.parametrize("nproc,tp,par", [(2, 1, "dp2"), (4, 2, "dp2xtp2")])
 def test_bench_self_launches_ranks(nproc, tp, par):
     """`python bench.py --gpus N` with no external launcher starts N ranks itself."""
-    r = _run(nproc, "--tp", str(tp), "--model", "llama-tiny", launcher=False)
+    r = _run(nproc, "--tp", str(tp), "--model", "llama-tiny", *(["--allow-rccl-decode"] if tp > 1 else []),
+             launcher=False)
     _check_contract(r, nproc, "llama-tiny", par, tp)
 
 

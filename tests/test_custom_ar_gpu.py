@@ -255,3 +255,34 @@ def test_dead_peer_costs_one_limit_not_one_per_collective():
     n0, dt0, _ = res[0]
     assert n0 >= 1, res
     assert dt0 < 2.5, res  # ten full limits would be >= 5 s
+
+
+def _selftest_worker(rank, world, port, q, ll_max):
+    """maybe_enable's first-contact check on the ranks of this box: every protocol
+    agrees with the reference all-reduce, so nothing is switched off."""
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    import torch.distributed as dist
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from xgserve.parallel.custom_ar import CustomAllReduce
+        ar = CustomAllReduce(rank, world, torch.device("cuda:0"), ll_max=ll_max)
+        res = ar.self_test(dist.group.WORLD, dist.group.WORLD)
+        q.put((rank, res, ar.protocol(), ar.timeouts()))
+        dist.barrier()
+        ar.close()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), None, -1))
+
+
+@pytest.mark.parametrize("world,ll_max", [(2, None), (2, 0), (4, None)])
+def test_custom_allreduce_self_test(world, ll_max):
+    for rank, res, proto, tmo in _run(_selftest_worker, world, ll_max):
+        assert isinstance(res, dict), res
+        assert res["pull"] and res["pull_resid"], res
+        if ll_max == 0:
+            assert res["ll"] is None and proto == "pull"
+        else:
+            assert res["ll"] and res["ll_resid"] and proto == "ll", res
+        assert tmo == 0

@@ -36,7 +36,7 @@ from ..parallel.state import get_state
 from ..ops import linear as linear_mod
 from ..ops.linear import (MODE_PARTIAL, MODE_SILU, MW_MAX_M, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace, RowStats,
                           lm_head_linear, m64_arx_linear, m64_arx_ok, m64_linear, m64_norm_linear, m64_plan, m64_resid_linear,
-                          mw_linear, mw_plan, pick_split,
+                          mw_linear, mw_plan, pf_linear, pf_plan, pick_split,
                           quantize_fp8, skinny_linear, splitk_linear, splitk_prefill_ok, w8_linear, w8_plan)
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
 from .config import ModelConfig
@@ -60,6 +60,11 @@ FUSED_DECODE = os.environ.get("XGS_FUSED_DECODE", "1") != "0"
 # MFMA GEMMs whose split-K partials go to the consumers, SiLU-gate in gate_up.
 # 0 = hipBLASLt for every step above 64 tokens.
 MW_MAX_TOKENS = min(MW_MAX_M, int(os.environ.get("XGS_MW_MAX_TOKENS", str(MW_MAX_M))))
+# T > MW_MAX_TOKENS tokens (a mixed step carrying a whole 512-token prompt chunk,
+# prefill) on TP = 1: every projection on gemm_pf (csrc/kernels/gemm_pf.hip) --
+# QKV / O / down as split-K partials into their consumers, gate_up with the SiLU
+# gate in its epilogue (stream-K grid). XGS_PF=0 keeps the library GEMMs.
+PF_PROMPT = os.environ.get("XGS_PF", "1") != "0"
 # TP > 1 prefill-sized steps: the row-parallel all-reduces are pipelined over this
 # many token chunks and overlapped with the next chunk's GEMMs (RCCL stream); a
 # 2k-token 8B step moves 16 MiB per all-reduce -- ~100 us on 7 xGMI links, a
@@ -155,6 +160,9 @@ class LlamaLayer(nn.Module):
         self.mw_ok = self.fast_ok and MW_MAX_TOKENS > FAST_M_SLAB and all(
             mw_plan(MW_MAX_TOKENS, n, k, mode) is not None and mw_plan(FAST_M_SLAB + 1, n, k, mode) is not None
             for n, k, mode in mw_shapes)
+        # T > MW_MAX_TOKENS on TP = 1: gemm_pf for every projection (MoE layers: attention)
+        self.pf_ok = self.fast_ok and PF_PROMPT and tp == 1 and all(
+            pf_plan(1024, n, k, mode) is not None for n, k, mode in mw_shapes)
         # M <= 16 too, when every projection has a measured small-M plan
         self.w8 = None  # FP8 weight copies for batch <= 16 decode (LlamaForCausalLM.quantize_fp8)
         self.m64_small_ok = self.m64_ok and all(
@@ -361,6 +369,18 @@ class LlamaLayer(nn.Module):
             act = mw_linear(h, self.gate_up, MODE_SILU)
             d = mw_linear(act, self.down, MODE_PARTIAL)
             return (d if self.tp == 1 else self._ar(d.materialize())), residual
+        if self.pf_ok and T > MW_MAX_TOKENS:
+            # prompt-sized steps: gemm_pf (MFMA tiles, LDS-DMA ring, stream-K); split-K
+            # partials go to the consumers (rope_cache_partials / add + rmsnorm), the
+            # SiLU gate rides in the gate_up epilogue
+            pqkv = pf_linear(h, self.qkv, MODE_PARTIAL)
+            a = self.attn.from_partials(pqkv, meta, kv, cos_sin)
+            o = pf_linear(a, self.o, MODE_PARTIAL)
+            h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
+            if self.moe:
+                return self.mlp(h), residual
+            act = pf_linear(h, self.gate_up, MODE_SILU)
+            return pf_linear(act, self.down, MODE_PARTIAL), residual
         if self.fast_ok and T <= FAST_M_SLAB:
             # 16 < M <= 64: measured per shape on MI355X -- only the O projection
             # (N = H) is faster on the LDS-slab kernel; its split-K partials are

@@ -28,6 +28,19 @@ remote read round trip after the synchronisation. It serves the fused residual
 all-reduce and plain all-reduces up to `ll_max` bytes (XGS_AR_LL_MAX, 0 = pull
 kernels everywhere).
 
+First contact (`self_test`, run by `maybe_enable` on every start): before the
+instance is registered, every protocol it would use -- push (LL) and pull plain
+all-reduces at decode sizes, the fused residual all-reduce in both forms, the
+two-shot form when TP >= 4 -- runs on the real links against an RCCL all-reduce
+of the same data. A protocol whose result differs is switched off on every rank
+(the group agrees through a MIN all-reduce), and if the pull kernels themselves
+fail the custom path is not registered at all (RCCL serves). The outcome is
+kept in `self.verified` ({"ll": bool, "pull": bool, ...}) and reported by
+bench.py. This is the gate for the push protocol on multi-GPU nodes: it has
+only been measured with every rank on one GPU (profiles/r4_ar_protocols.md),
+and its correctness depends on each peer's 8-byte {data, gen} halves landing
+intact over xGMI.
+
 Failure semantics: a peer that does not arrive within the wait limit makes the
 kernels bump a device error counter and give up (the GPU never hangs); once the
 counter is non-zero every later wait returns at once, so a dead peer costs one
@@ -155,6 +168,7 @@ class CustomAllReduce:
         self._khz = max(1, int(k.car_wallclock_khz()) or 100_000)
         self.timeout_s = 0.0
         self.set_timeout(self.SERVE_TIMEOUT_S)
+        self.verified = None  # self_test() outcome
         log.info("custom all-reduce ready: rank %d/%d, one-shot <= %d KiB, two-shot <= %d MiB", rank, world,
                  min(self.slot, self.two_shot_min) >> 10, self.slot2 >> 20)
 
@@ -220,6 +234,86 @@ class CustomAllReduce:
                                          self.err.data_ptr(), stream_ptr())
         return out
 
+    def self_test(self, group, cpu_group) -> dict:
+        """Run every protocol this instance would use against RCCL on the real links
+        (module docstring, "First contact"); switch off the ones that disagree on any
+        rank. Returns {"ll", "ll_resid", "pull", "pull_resid", "two_shot"} -> bool
+        (None: protocol not in use)."""
+        dev = self.device
+        g = torch.Generator(device=dev).manual_seed(4321 + self.rank)
+        res = {"ll": None, "ll_resid": None, "pull": None, "pull_resid": None, "two_shot": None}
+
+        def close_enough(got: torch.Tensor, ref: torch.Tensor) -> bool:
+            return bool(torch.isfinite(got).all()) and float((got.float() - ref).abs().max()) <= \
+                2e-2 * max(1e-3, float(ref.abs().max()))
+
+        def plain(nbytes: int, ll: bool) -> bool:
+            x = (torch.randn(nbytes // 2, generator=g, device=dev) * 0.5).bfloat16()
+            ref = x.float()
+            dist.all_reduce(ref, group=group)
+            keep = self.ll_max
+            if not ll:
+                self.ll_max = 0
+            try:
+                y = self.all_reduce(x.clone())
+            finally:
+                self.ll_max = keep
+            torch.cuda.synchronize(dev)
+            return close_enough(y, ref)
+
+        def resid(ll: bool) -> bool:
+            T, H, S = 8, 4096, 2
+            part = torch.randn(S, T, H, generator=g, device=dev) * 0.25
+            base = torch.randn(T, H, generator=torch.Generator(device=dev).manual_seed(99), device=dev).bfloat16()
+            ref = part.sum(0)
+            dist.all_reduce(ref, group=group)
+            ref = base.float() + ref
+            r = base.clone()
+            ss = torch.zeros(T * (H // 1024), dtype=torch.float32, device=dev)
+            keep = self.resid_ll
+            self.resid_ll = ll
+            try:
+                self.all_reduce_resid(part, r, ss)
+            finally:
+                self.resid_ll = keep
+            torch.cuda.synchronize(dev)
+            ss_ref = (r.float().view(T, H // 1024, 1024) ** 2).sum(-1).t().reshape(-1)
+            return close_enough(r, ref) and bool(torch.allclose(ss, ss_ref, rtol=2e-2, atol=1e-2))
+
+        checks = {"pull": lambda: plain(16 << 10, False) and plain(min(self.slot, 256 << 10), False),
+                  "pull_resid": lambda: resid(False)}
+        if self.ll_max > 0:
+            checks["ll"] = lambda: plain(min(self.ll_max, 16 << 10), True) and plain(self.ll_max, True)
+        if self.resid_ll:
+            checks["ll_resid"] = lambda: resid(True)
+        if self.world >= 4 and self._two_shot(1 << 20):
+            checks["two_shot"] = lambda: plain(1 << 20, False)
+        self.set_timeout(self.WARMUP_TIMEOUT_S)
+        for name, fn in checks.items():
+            try:
+                ok = int(fn() and self.timeouts() == 0)
+            except Exception as e:  # noqa: BLE001 - a protocol that raises is a failed protocol
+                log.warning("custom all-reduce self-test %s raised: %s", name, e)
+                ok = 0
+            self.reset_errors()
+            flag = torch.tensor([ok], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=cpu_group)
+            res[name] = bool(flag.item())
+        self.set_timeout(self.SERVE_TIMEOUT_S)
+        if res["ll"] is False or res["ll_resid"] is False:
+            log.warning("custom all-reduce: push (LL) protocol disagreed with RCCL on this node (%s); "
+                        "using the pull kernels", res)
+            self.ll_max = 0
+            self.resid_ll = False
+        if res["two_shot"] is False:
+            self.two_shot_min = self.slot2 + 1  # one-shot up to its slot, RCCL above
+        self.verified = res
+        return res
+
+    def protocol(self) -> str:
+        """The decode all-reduce protocol in use: "ll" (push) or "pull"."""
+        return "ll" if self.resid_ll else "pull"
+
     def set_timeout(self, seconds: float) -> None:
         """Peer-wait limit of every later launch (stream-ordered; captured graphs read
         the word at replay). Clamped to the 32-bit tick range."""
@@ -267,6 +361,11 @@ def maybe_enable(state, device: torch.device) -> Optional[CustomAllReduce]:
         ar = CustomAllReduce(state.tp_rank, state.tp_size, device, cpu_group=state.tp_cpu_group)
     except Exception as e:  # noqa: BLE001 - RCCL remains correct
         log.warning("custom all-reduce unavailable (%s); using RCCL", e)
+        return None
+    res = ar.self_test(state.tp_group, state.tp_cpu_group)
+    if not (res["pull"] and res["pull_resid"]):
+        log.warning("custom all-reduce: pull kernels disagreed with RCCL (%s); using RCCL", res)
+        ar.close()
         return None
     comm.register_custom_allreduce(ar)
     return ar
