@@ -204,7 +204,9 @@ class ServerConfig:
             e.append("worker.block_size must be a multiple of 16")
         if not w.mock and not w.random_init and not w.checkpoint:
             e.append("worker.checkpoint is required unless random_init or mock")
-        if w.checkpoint and not w.checkpoint.startswith(("http://", "https://")) and not os.path.isdir(w.checkpoint):
+        if w.checkpoint and w.checkpoint.startswith(("http://", "https://")) and not w.mock:
+            e.append(f"worker.checkpoint {w.checkpoint!r}: remote checkpoints are fetched by load_config")
+        elif w.checkpoint and not w.checkpoint.startswith(("http://", "https://")) and not os.path.isdir(w.checkpoint):
             e.append(f"worker.checkpoint {w.checkpoint!r} is not a directory")
         if not w.mock:
             try:
@@ -368,6 +370,15 @@ def load_config(file: Optional[str] = None, env: Optional[Dict[str, str]] = None
         for k, v in kv.items():
             if v is not None:
                 _set(cfg, sec, k, v, errors, "cli")
+    w = cfg.worker
+    if not errors and not w.mock and w.checkpoint and w.checkpoint.startswith(("http://", "https://")):
+        # Req 10.2: a remote checkpoint directory is fetched once into the local cache
+        # and loaded from there; an unreachable URL is a configuration error (exit != 0)
+        from ..models.fetch import FetchError, fetch_checkpoint
+        try:
+            w.checkpoint = fetch_checkpoint(w.checkpoint)
+        except FetchError as ex:
+            errors.append(f"worker.checkpoint: cannot fetch {w.checkpoint}: {ex}")
     errors += cfg.validate()
     if errors:
         raise ConfigError("; ".join(errors))
