@@ -48,8 +48,10 @@ def _rank_main(rank, world, port, ck, moe_comm, q, env=None):
         eng = LLMEngine(EngineConfig(model="tp-test", checkpoint=ck, tp=world, device="cuda:0",
                                      num_blocks=256, max_num_seqs=8, max_num_batched_tokens=1024,
                                      max_model_len=512, moe_comm=moe_comm))
+        temp = float(os.environ.get("XGS_TEST_TEMPERATURE", "0"))
         if rank == 0:
-            sp = SamplingParams(max_tokens=N_GEN, temperature=0.0, ignore_eos=True)
+            sp = SamplingParams(max_tokens=N_GEN, temperature=temp, top_p=0.95 if temp > 0 else 1.0, seed=11,
+                                ignore_eos=True)
             if os.environ.get("XGS_TEST_STAGGER") == "1":
                 # the second prompt arrives while the first decodes: its prompt step is an
                 # eager MIXED step, launched asynchronously under TP (followers sample too)
@@ -67,10 +69,12 @@ def _rank_main(rank, world, port, ck, moe_comm, q, env=None):
                 outs = eng.generate(PROMPTS, sp)
             eng.stop_followers()
             mode = {"custom_ar": eng.custom_ar is not None, "graphs": bool(eng.runner.graphs), "async": eng._async,
-                    "fused": eng.model._fused_ok}
+                    "fused": eng.model._fused_ok, "samples": eng.runner.sample_log}
             q.put(("ok", outs, mode))
         else:
             eng.follower_loop()
+            if eng.runner.sample_log is not None:
+                q.put(("samples", rank, eng.runner.sample_log))
         torch.cuda.synchronize()
         destroy_distributed()
     except Exception as e:  # noqa: BLE001 - reported to the parent
@@ -149,3 +153,45 @@ def test_tp2_on_one_gpu_matches_fp32_reference(tmp_path, model, moe_comm, world,
             assert gap < 0.15, (i, tok, int(row.argmax()), gap)
             if base is not None:
                 break  # diverged from TP=1 at a near-tie: later tokens have other prefixes
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_tp_followers_sample_the_leaders_tokens(tmp_path, world):
+    """Asynchronous scheduling under TP at temperature > 0: every rank
+    samples the decode ids of the next step itself (graph steps and asynchronous
+    eager mixed steps), from the same all-gathered logits, the leader's broadcast
+    sampling rows and per-request seeds -- so every rank must draw exactly the
+    leader's tokens, step by step, or the ranks' KV caches would silently diverge."""
+    from xgserve.models import build_model, save_checkpoint
+    from xgserve.ops import _native
+    _native.kernels()
+    cfg = _cfg("llama")
+    ck = str(tmp_path / "ckpt")
+    save_checkpoint(build_model(cfg, device="cuda:0", seed=7), ck)
+    ctx = torch.multiprocessing.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    env = {"XGS_TEST_STAGGER": "1", "XGS_TEST_TEMPERATURE": "0.8", "XGS_TEST_SAMPLE_LOG": "1"}
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, ck, "alltoall", q, env)) for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = []
+    try:
+        for _ in range(world):
+            msgs.append(q.get(timeout=240))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    lead = [m for m in msgs if m[0] == "ok"]
+    assert len(lead) == 1, msgs
+    _, outs, mode = lead[0]
+    assert all(len(g) == N_GEN for g in outs)
+    assert mode["graphs"] and mode["async"], mode
+    logs = {m[1]: m[2] for m in msgs if m[0] == "samples"}
+    assert sorted(logs) == list(range(1, world)), msgs
+    ref = mode["samples"]
+    assert len(ref) >= N_GEN // 2  # graph + async steps were logged
+    for r, lg in logs.items():
+        assert lg == ref, (r, next((i, a, b) for i, (a, b) in enumerate(zip(lg, ref)) if a != b) if lg != ref else None)

@@ -141,6 +141,12 @@ class ModelRunner:
         self.h_toks = [_pinned(nt, torch.int32) for _ in range(2)]
         self.h_lps = [_pinned(nt, torch.float32) for _ in range(2)]
         self.out_idx = 0
+        self._es_pin = [None, None]   # eager-step sampling rows: pinned stagings + events
+        self._es_ev = [None, None]
+        self._es_idx = 0
+        # XGS_TEST_SAMPLE_LOG=1 (tests): every eager sample of this rank, to check that TP
+        # followers draw exactly the leader's tokens at temperature > 0
+        self.sample_log = [] if os.environ.get("XGS_TEST_SAMPLE_LOG") == "1" else None
         # graphs
         self.use_graphs = use_graphs and self.is_cuda
         if graph_batch_sizes is None:
@@ -502,6 +508,7 @@ class ModelRunner:
         ev.record()
         self.g_stage_events[si] = ev
         self.graphs[(bs, greedy)].replay()
+        self._log_samples(n)
         if not self.is_driver:
             # no D2H to wait on; wait() still drains before the pinned inputs get rewritten
             self._poll_comm()
@@ -556,6 +563,7 @@ class ModelRunner:
         self.g_stage_events[si] = ev
         self.mixed_graphs[(nb, greedy)].replay()
         self.mixed_replays += 1
+        self._log_samples(n)
         if not self.is_driver:
             self._poll_comm()
             ev = torch.cuda.Event()
@@ -635,6 +643,7 @@ class ModelRunner:
                 if on_dev:
                     tok, _ = self._sample(logits, samp)
                     self.g_out_tok[:S].copy_(tok[:S])
+                    self._log_samples(S)
                 # an event of THIS step: a follower that queued its successor waits
                 # for this launch only (engine.follower_loop), not the whole stream
                 self._poll_comm()
@@ -651,15 +660,44 @@ class ModelRunner:
     def _sample(self, logits: torch.Tensor, samp: Optional[SamplingRows]):
         if samp is None or samp.all_greedy:
             tok, lp = ops.argmax_logprob(logits)
+        elif self.is_cuda:
+            # eager-step sampling rows through two event-guarded pinned stagings (async
+            # H2D; a follower samples every asynchronous eager step, so no pageable copy
+            # or host sync on its step path)
+            n = len(samp.temps)
+            i = self._es_idx
+            self._es_idx ^= 1
+            if self._es_ev[i] is not None:
+                self._es_ev[i].synchronize()
+            if self._es_pin[i] is None or self._es_pin[i][1].numel() < n:
+                m = max(n, 64)
+                self._es_pin[i] = (_pinned(2 * m, torch.float32), _pinned(m, torch.int32), _pinned(m, torch.int64))
+            hf, hk, hs = self._es_pin[i]
+            f = hf.numpy()
+            f[:n] = samp.temps
+            f[n:2 * n] = samp.top_ps
+            hk.numpy()[:n] = samp.top_ks
+            hs.numpy()[:n] = samp.seeds
+            dev_f = hf[:2 * n].to(self.device, non_blocking=True).view(2, n)
+            topk = hk[:n].to(self.device, non_blocking=True)
+            seeds = hs[:n].to(self.device, non_blocking=True)
+            ev = self._es_ev[i] or torch.cuda.Event()
+            ev.record()
+            self._es_ev[i] = ev
+            tok, lp = ops.sample_tokens(logits, dev_f[0], dev_f[1], topk, seeds, step=0)
         else:
-            dev_f = torch.from_numpy(np.stack([samp.temps, samp.top_ps]).astype(np.float32)).to(self.device)
-            topk = torch.from_numpy(samp.top_ks.astype(np.int32)).to(self.device)
-            seeds = torch.from_numpy(samp.seeds.astype(np.int64)).to(self.device)
-            gen = None
-            if not self.is_cuda:
-                gen = torch.Generator().manual_seed(int(samp.seeds[0]) & 0x7FFFFFFF)
+            dev_f = torch.from_numpy(np.stack([samp.temps, samp.top_ps]).astype(np.float32))
+            topk = torch.from_numpy(samp.top_ks.astype(np.int32))
+            seeds = torch.from_numpy(samp.seeds.astype(np.int64))
+            gen = torch.Generator().manual_seed(int(samp.seeds[0]) & 0x7FFFFFFF)
             tok, lp = ops.sample_tokens(logits, dev_f[0], dev_f[1], topk, seeds, step=0, generator=gen)
         return tok, lp
+
+    def _log_samples(self, n: int) -> None:
+        """(tests) the tokens of a step this rank sampled into g_out_tok -- the steps
+        whose successor reads its decode ids from there on EVERY rank"""
+        if self.sample_log is not None:
+            self.sample_log.append(self.g_out_tok[:n].cpu().tolist())
 
     def _async_ok(self, S: int, plan: dict) -> bool:
         """May an eager step's successor be planned before its tokens reach the host?
@@ -676,4 +714,5 @@ class ModelRunner:
         if not self._async_ok(S, plan):
             return False
         self.g_out_tok[:S].copy_(tok[:S])
+        self._log_samples(S)
         return True
