@@ -354,3 +354,28 @@ def test_decode_prefill_cap_can_be_lifted():
     plan = _step(s, plan)
     plan = _step(s, plan)
     assert int(plan["num_tokens"]) - int(plan["num_decodes"]) <= 128
+
+
+@pytest.mark.parametrize("seqs,expect_steps", [(None, 1), (1, 3)])
+def test_decode_prefill_burst_without_mixed_graphs(seqs, expect_steps):
+    """with decode_prefill_cap set but no mixed-step graphs captured (here:
+    CPU, no graphs), a burst of short prompts arriving while a request decodes is
+    admitted in ONE step (the one-prompt limit exists only for the graphs' shape);
+    decode_prefill_seqs=1 restores one prompt per step."""
+    from xgserve.engine import EngineConfig, LLMEngine, SamplingParams
+    eng = LLMEngine(EngineConfig(model="llama-tiny", device="cpu", dtype="float32", num_blocks=64, max_num_seqs=8,
+                                 max_num_batched_tokens=256, max_model_len=128, use_graphs=False,
+                                 decode_prefill_cap=64, decode_prefill_seqs=seqs))
+    sp = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True)
+    eng.add_request("long", list(range(5, 21)), sp)
+    for _ in range(3):
+        eng.step()
+    first_step = {}
+    for i in range(3):
+        eng.add_request(f"b{i}", list(range(30 + i, 38 + i)), SamplingParams(max_tokens=2, ignore_eos=True))
+    for k in range(8):
+        for o in eng.step():
+            if o.new_token_ids and o.request_id.startswith("b") and o.request_id not in first_step:
+                first_step[o.request_id] = k
+    assert sorted(first_step) == ["b0", "b1", "b2"]
+    assert len(set(first_step.values())) == expect_steps, first_step

@@ -72,6 +72,10 @@ class EngineConfig:
     max_prefill_seqs: int = 1 << 30
     # prefill tokens allowed in a step that also decodes (0: only the token budget)
     decode_prefill_cap: int = 0
+    # prompts per decoding step under decode_prefill_cap: None = 1 when the runner
+    # captured mixed-step graphs (their shape holds one chunk), else no limit (a burst
+    # of short prompts shares a step)
+    decode_prefill_seqs: Optional[int] = None
     # admission window (continuous batching): while rows decode, hold new prompts until
     # prompt_coalesce of them wait or the oldest was passed over by
     # prompt_coalesce_max_wait steps, then prefill them in one mixed step (1: off)
@@ -174,6 +178,9 @@ class LLMEngine:
                                   graph_batch_sizes=graph_bs, is_driver=self.is_driver,
                                   mixed_chunk=cfg.decode_prefill_cap)
         self.runner.collective_timeout_s = cfg.collective_timeout_s
+        self._dp_seqs = cfg.decode_prefill_seqs if cfg.decode_prefill_seqs is not None else \
+            (1 if self.runner.mixed_chunk > 0 else 0)
+        self.sched.set_decode_prefill(cfg.decode_prefill_cap, self._dp_seqs if cfg.decode_prefill_cap > 0 else 0)
         self.runner.capture_graphs()
         H = self.mcfg.hidden_size
         self.embed_acc = torch.zeros(cfg.max_num_seqs, H, dtype=torch.float32, device=self.device)
@@ -795,7 +802,7 @@ class LLMEngine:
         graphs captured for the configured cap stay valid for any smaller one."""
         cap = self.cfg.decode_prefill_cap if cap is None else max(0, min(int(cap), self.cfg.decode_prefill_cap or 1 << 30))
         with self._lock:
-            self.sched.set_decode_prefill(cap, 1 if cap > 0 else 0)
+            self.sched.set_decode_prefill(cap, self._dp_seqs if cap > 0 else 0)
 
     def set_limits(self, max_num_seqs: int, max_num_batched_tokens: int):
         """Runtime batch limits (degradation / hot reload), clamped to the sizes the
