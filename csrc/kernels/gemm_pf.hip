@@ -185,8 +185,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
   const int sl = li & 7;             // swizzle key of every fragment row this lane reads
 
   f32x4_t acc[P][MTP][4];
-  uint4 bfr[4][2];
-  uint4 afr[MTP][2];
+  // fragments read straight into the MFMA operand type (a uint4 -> bf16x8 bit_cast made
+  // hipcc shuffle every fragment's middle dwords through VALU moves before each MFMA)
+  bf16x8_t bfr[4][2];
+  bf16x8_t afr[MTP][2];
 
   // ---- one K range [kt_lo, kt_lo + nk) of the tile at (m0, n0) into acc
   auto compute = [&](int m0, int n0, int kt_lo, int nk) {
@@ -294,15 +296,15 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
         for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
-            bfr[nt][ks] = *reinterpret_cast<const uint4*>(slot + ASZ + (wrow + 16 * nt + li) * 128 +
-                                                           (((4 * ks + g) ^ sl) << 4));
+            bfr[nt][ks] = *reinterpret_cast<const bf16x8_t*>(slot + ASZ + (wrow + 16 * nt + li) * 128 +
+                                                              (((4 * ks + g) ^ sl) << 4));
       }
 #pragma unroll
       for (int mt = 0; mt < MTP; ++mt)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          afr[mt][ks] = *reinterpret_cast<const uint4*>(slot + p * PB + (arl + 16 * mt + li) * 128 +
-                                                         (((4 * ks + g) ^ sl) << 4));
+          afr[mt][ks] = *reinterpret_cast<const bf16x8_t*>(slot + p * PB + (arl + 16 * mt + li) * 128 +
+                                                            (((4 * ks + g) ^ sl) << 4));
       // fragment reads retire before the barrier: the region may be re-staged next phase
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (wr == 1 && need) pf_wait<P, NA, PN>(steady);
@@ -316,7 +318,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
         for (int mt = 0; mt < MTP; ++mt)
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt)
-            acc[p][mt][nt] = mfma16x16x32(as_frag(bfr[nt][ks]), as_frag(afr[mt][ks]), acc[p][mt][nt]);
+            acc[p][mt][nt] = mfma16x16x32(bfr[nt][ks], afr[mt][ks], acc[p][mt][nt]);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       if (wr == 0 && need) pf_wait<P, NA, PN>(steady);

@@ -339,8 +339,10 @@ def pf_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL, cus: int = 256):
         cfg = 3  # 4 m tiles per wave per phase (32 MFMAs per segment)
     tiles = -(-M // bm) * (N // 256)
     if mode == MODE_PARTIAL:
+        # the most splits that still run in ONE round (a second, mostly empty round
+        # costs a whole split's time)
         S = 1
-        while tiles * (S + 1) <= cus * 1.15 and (S + 1) <= K // 256:
+        while tiles * (S + 1) <= cus and (S + 1) <= K // 256:
             S += 1
         return S, cfg, 0
     rounds = tiles / cus
