@@ -56,8 +56,6 @@ def main():
                     help="sweep gemm_m64g (nw, split, cfg) configurations instead of the shoot-out")
     ap.add_argument("--mw-sweep", action="store_true",
                     help="sweep gemm_mw (split, cfg) configurations at 64 < M <= 320 against hipBLASLt")
-    ap.add_argument("--mw-probe", action="store_true",
-                    help="gemm_mw anatomy: full kernel vs DMA-only / compute-only / W-only / x-only variants")
     ap.add_argument("--top", type=int, default=6, help="--mw-sweep: configurations printed per (shape, M)")
     a = ap.parse_args()
     kernels()
@@ -65,8 +63,6 @@ def main():
         return m64g_sweep(a)
     if a.mw_sweep:
         return mw_sweep(a)
-    if a.mw_probe:
-        return mw_probe(a)
     if a.w8_sweep:
         return w8_sweep(a)
     if a.moe_sweep:
@@ -272,40 +268,6 @@ def mw_sweep(a):
             if M <= 64 and L.m64_plan(M, N, K, mode) is not None:
                 fn = lambda w: L.m64_linear(x, w, mode)  # noqa: E731
                 show("m64g(plan)", timeit([lambda w=w: fn(w) for w in ws]), None)
-        del ws
-        torch.cuda.empty_cache()
-
-
-def mw_probe(a):
-    """gemm_mw (cfg 1 / 5) with parts of its pipeline removed (csrc/kernels/gemm_mw.hip PR):
-    0 full, 1 DMA + waits only, 2 LDS reads + MFMA only, 3 no x DMA, 4 no weight DMA,
-    5 x DMA only, 6 weight DMA only; +8: K chunks walked from a rotated start per tile.
-    Cold weights; us per call."""
-    k = kernels()
-    st = torch.cuda.current_stream().cuda_stream
-    splits = {"qkv": 5, "o": 8, "gate_up": 1, "down": 8}
-    names = {0: "full", 1: "dma_only", 2: "compute_only", 3: "w_only", 4: "x_only", 5: "x_dma", 6: "w_dma",
-             8: "full_rot", 9: "dma_only_rot", 13: "x_dma_rot"}
-    for name in a.shapes:
-        N, K = SHAPES[name]
-        S = splits.get(name, 1)
-        nbytes = N * K * 2
-        copies = max(2, min(8, (1 << 30) // nbytes + 1))
-        ws = [(torch.randn(N, K, device="cuda") * 0.02).bfloat16() for _ in range(copies)]
-        mode = L.MODE_SILU if name.startswith("gate_up") else L.MODE_PARTIAL
-        for M in a.M:
-            x = torch.randn(M, K, device="cuda").bfloat16()
-            part = torch.empty(S, M, N, dtype=torch.float32, device="cuda")
-            out = torch.empty(M, N // 2 if mode == L.MODE_SILU else N, dtype=torch.bfloat16, device="cuda")
-            for cfg in (1, 5):
-                row = {}
-                for pr in names:
-                    def fn(w, pr=pr, cfg=cfg):
-                        k.gemm_mw_probe(x.data_ptr(), M, K, w.data_ptr(), N,
-                                        part.data_ptr() if mode == L.MODE_PARTIAL else 0,
-                                        out.data_ptr() if mode != L.MODE_PARTIAL else 0, S, mode, cfg, pr, st)
-                    row[names[pr]] = round(timeit([lambda w=w, fn=fn: fn(w) for w in ws]), 2)
-                print(json.dumps({"shape": name, "M": M, "S": S, "cfg": cfg, **row}), flush=True)
         del ws
         torch.cuda.empty_cache()
 

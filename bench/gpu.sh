@@ -103,7 +103,7 @@ sweep)
       qkv70t8 o70t8 gate_up70t8 down70t8 qkv8t2 o8t2 gate_up8t2 down8t2 qkv8t4 o8t4 gate_up8t4 down8t4 \
       qkv8t8 o8t8 gate_up8t8 down8t8 qkv70t2 o70t2 gate_up70t2 down70t2 qkv70t4 o70t4 gate_up70t4 down70t4 ;;
 arsim)  # simulated xGMI all-reduce latency on one rank of 70B TP8 (XGS_SIM_AR_US), with / without prefetch
-  for cfgv in "XGS_SIM_AR_US=0" "XGS_SIM_AR_US=4" "XGS_SIM_AR_US=8"; do
+  for cfgv in "XGS_TUNE=sim_ar_us=0" "XGS_TUNE=sim_ar_us=4" "XGS_TUNE=sim_ar_us=8"; do
     n=$(echo "$cfgv" | tr -c 'A-Za-z0-9_=\n' '_')
     run "c1_$n" 300 env $cfgv $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20 "$@"
   done ;;
@@ -120,7 +120,7 @@ mw)  # gemm_mw: numerics, shape sweep, stall-free mixed-step engine tests, headl
   pyt stall_free 300 tests/test_engine_gpu.py -k "stall_free or graph_decode or chunked or async"
   run c64_chunk128 200 $B --steps 20 --warmup 5 --prefill-chunk 128 "$@"
   run c64_chunk128_long 240 env XGS_STEP_LOG="$o/steps_chunk128.jsonl" $B --steps 600 --warmup 60 --prefill-chunk 128 "$@"
-  run c64_chunk128_lib 240 env XGS_MW_MAX_TOKENS=0 $B --steps 600 --warmup 60 --prefill-chunk 128 "$@"
+  run c64_chunk128_lib 240 env XGS_TUNE=mw_max_tokens=0 $B --steps 600 --warmup 60 --prefill-chunk 128 "$@"
   run c64_base_long 240 $B --steps 600 --warmup 60 "$@" ;;
 m64)  # decode GEMM plans: LM head on gemm_mw, deep-ring / uneven-split gemm_m64g tests and sweeps
   run mw_sweep_lm 200 python -u bench/gemm_bench.py --mw-sweep --M 64 65 --shapes lm_head --top 3
@@ -142,7 +142,7 @@ r4d)  # round 4: batched in-launch residual reduce at M = 64 (GG_RESID) vs add_p
   pyt fused_tests 400 tests/test_fused_decode_gpu.py
   run attn_cold 200 python -u bench/decode_cold.py --L 768 --splits 1 --depth 2 3
   run attn_cold_2k 200 python -u bench/decode_cold.py --L 2048 --caches 3 --splits 1 --depth 2 3
-  for v in "XGS_RESID_INLAUNCH_KB=32" "XGS_RESID_INLAUNCH_KB=1024" "XGS_DECODE_DEPTH=3"; do
+  for v in "XGS_TUNE=resid_inlaunch_kb=32" "XGS_TUNE=resid_inlaunch_kb=1024" "XGS_TUNE=decode_depth=3"; do
     n=$(echo "$v" | tr -c 'A-Za-z0-9_=\n' '_')
     run "steplog_$n" 240 env $v XGS_STEP_LOG="$o/steps_$n.jsonl" $B --steps 400 --warmup 40 "$@"
   done ;;
@@ -164,22 +164,22 @@ r4g)  # round 4: gemm_mw anatomy probes, AR latency at world 4 / 8, batch-1 pref
   bash bench/profile.sh "$o/prof_c64" "$@" ;;
 r4h)  # round 4: K-chunk rotation -- kernel tests, m64g / mw / LM-head sweeps, engine A/B (XGS_KROT)
   run m64g_sweep 300 python -u bench/gemm_bench.py --m64g-sweep --M 64 --shapes gate_up qkv o down
-  run m64g_sweep_off 300 env XGS_KROT=0 python -u bench/gemm_bench.py --m64g-sweep --M 64 --shapes gate_up
+  run m64g_sweep_off 300 env XGS_TUNE=krot=0 python -u bench/gemm_bench.py --m64g-sweep --M 64 --shapes gate_up
   pyt mw3_tests 300 tests/test_skinny_gpu.py -k "mw"
   run mw_sweep 500 python -u bench/gemm_bench.py --mw-sweep --M 64 128 192 256 --shapes gate_up down qkv o lm_head --top 5
-  for v in "XGS_KROT=1" "XGS_KROT=0" "XGS_KROT=2"; do
+  for v in "XGS_TUNE=krot=1" "XGS_TUNE=krot=0" "XGS_TUNE=krot=2"; do
     n=$(echo "$v" | tr -c 'A-Za-z0-9_=\n' '_')
     run "c64_$n" 240 env $v XGS_STEP_LOG="$o/steps_$n.jsonl" $B --steps 600 --warmup 60 "$@"
   done
   run c1 150 $B --concurrency 1 --steps 200 --warmup 20 "$@"
-  run c1_off 150 env XGS_KROT=0 $B --concurrency 1 --steps 200 --warmup 20 "$@" ;;
+  run c1_off 150 env XGS_TUNE=krot=0 $B --concurrency 1 --steps 200 --warmup 20 "$@" ;;
 r4i)  # round 4: full GPU tests + smoke + headline with rotation and the LM head on gemm_mw; MoE rotation A/B
   pyt_soft gputests 900 tests -m gpu --maxfail=10
   run smoke 150 python -u -c "import __graft_entry__ as g; g.smoke()"
   run bench_driver 200 $B --steps 20 --warmup 5 "$@"
   run c64_long 240 env XGS_STEP_LOG="$o/steps_c64.jsonl" $B --steps 600 --warmup 60 "$@"
   run c1 150 $B --concurrency 1 --steps 200 --warmup 20 "$@"
-  for v in "XGS_KROT=1" "XGS_KROT=0"; do
+  for v in "XGS_TUNE=krot=1" "XGS_TUNE=krot=0"; do
     n=$(echo "$v" | tr -c 'A-Za-z0-9_=\n' '_')
     run "mixtral_c1_$n" 200 env $v $B --model mixtral-8x7b --concurrency 1 --steps 60 --warmup 10
     run "mixtral_c64_$n" 240 env $v $B --model mixtral-8x7b --steps 120 --warmup 20
@@ -211,13 +211,13 @@ r4n)  # round 4: re-swept batch-1 / 32-row plans vs the round-3 ones, decode spl
   pyt plan_tests 300 tests/test_skinny_gpu.py tests/test_fused_decode_gpu.py -k "m64 or deep_ring or uneven or logits"
   OLD16="6144x4096x1@16=2,8,5;4096x4096x1@16=2,4,4;28672x4096x2@16=2,1,6;4096x14336x1@16=2,4,6"
   run c1_new 150 $B --concurrency 1 --steps 300 --warmup 20
-  run c1_old 150 env XGS_M64_PLANS="$OLD16" $B --concurrency 1 --steps 300 --warmup 20
+  run c1_old 150 env XGS_TUNE=m64_plans="$OLD16" $B --concurrency 1 --steps 300 --warmup 20
   for sp in 1 4; do
-    run c1_splits$sp 150 env XGS_DECODE_MAX_SPLITS=$sp $B --concurrency 1 --steps 300 --warmup 20
+    run c1_splits$sp 150 env XGS_TUNE=decode_max_splits=$sp $B --concurrency 1 --steps 300 --warmup 20
   done
   run c8 150 $B --concurrency 8 --steps 200 --warmup 20
   run c64_qkv5 240 $B --steps 600 --warmup 60
-  run c64_qkv4 240 env XGS_M64_PLANS="6144x4096x1@64=2,4,3" $B --steps 600 --warmup 60
+  run c64_qkv4 240 env XGS_TUNE=m64_plans="6144x4096x1@64=2,4,3" $B --steps 600 --warmup 60
   run mixtral_c1 200 $B --model mixtral-8x7b --concurrency 1 --steps 100 --warmup 10 ;;
 r4o)  # round 4: kernel profiles of batch 1 and 64 concurrent on the final plans; TP-shard plan re-sweep (K rotation)
   bash bench/profile.sh "$o/prof_c1" --concurrency 1
@@ -238,44 +238,42 @@ r4p)  # round 4: one rank of the Llama-3-70B TP8 group (config 4 proxy), 70B TP1
   run tp1_c1 300 $B --model llama3-70b --concurrency 1 --steps 40 --warmup 10
   run tp1_c64 300 $B --model llama3-70b --steps 40 --warmup 10 ;;
 r4q)  # round 4: two-stream overlap with the decode GEMMs on 72-KB-LDS (KC 64) configurations
-  run overlap_kc64 200 env XGS_M64_PLANS="4096x4096x1@64=1,4,2;28672x4096x2@64=2,1,3" \
+  run overlap_kc64 200 env XGS_TUNE=m64_plans="4096x4096x1@64=1,4,2;28672x4096x2@64=2,1,3" \
       python -u bench/overlap_probe.py --prompt 512 1024
   run overlap_base 200 python -u bench/overlap_probe.py --prompt 512 1024 ;;
 r4r)  # round 4: decode attention with non-temporal K/V loads (depth 14 = PR 4), kernel + engine A/B
   run dnt_768 200 python -u bench/decode_cold.py --depth 2 14 --splits 1 2
   run dnt_2k 200 python -u bench/decode_cold.py --L 2048 --depth 2 14 --splits 1
   run eng_base 300 python -u bench.py --steps 600 --warmup 50
-  run eng_nt 300 env XGS_DECODE_DEPTH=14 python -u bench.py --steps 600 --warmup 50
+  run eng_nt 300 env XGS_TUNE=decode_depth=14 python -u bench.py --steps 600 --warmup 50
   run eng_base2 300 python -u bench.py --steps 600 --warmup 50 ;;
 r4s)  # round 4: non-temporal K/V loads as the default -- numerics, then batch 1 / 64 / 70B A/Bs (14 = cached loads)
   pyt attn_tests 400 tests/test_fused_decode_gpu.py tests/test_kernels_gpu.py -k "decode or attention"
   run c1_nt 300 $B --concurrency 1 --steps 300 --warmup 30
-  run c1_cached 300 env XGS_DECODE_DEPTH=14 $B --concurrency 1 --steps 300 --warmup 30
+  run c1_cached 300 env XGS_TUNE=decode_depth=14 $B --concurrency 1 --steps 300 --warmup 30
   run c1_nt2 300 $B --concurrency 1 --steps 300 --warmup 30
   run c64_nt 300 $B --steps 1000 --warmup 100
-  run c64_cached 300 env XGS_DECODE_DEPTH=14 $B --steps 1000 --warmup 100
+  run c64_cached 300 env XGS_TUNE=decode_depth=14 $B --steps 1000 --warmup 100
   run tp8_c1 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
   run tp8_c64 300 $B --model llama3-70b --tp-shard 8 --steps 60 --warmup 20 ;;
 r4t)  # round 4: all-reduce prologue in the next GEMM (gemm_m64g_arx): tests, then simulated-TP8 70B batch 1 A/B
   pyt arx_tests 400 tests/test_ar_prologue_gpu.py
   pyt fused_tests 400 tests/test_fused_decode_gpu.py
-  run tp8_ar0_base 300 env XGS_SIM_AR_US=0 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
-  run tp8_ar0_arx 300 env XGS_SIM_AR_US=0 XGS_AR_PROLOGUE=1 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
-  run tp8_ar8_base 300 env XGS_SIM_AR_US=8 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
-  run tp8_ar8_arx 300 env XGS_SIM_AR_US=8 XGS_AR_PROLOGUE=1 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+  run tp8_ar0_base 300 env XGS_TUNE=sim_ar_us=0 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+  run tp8_ar8_base 300 env XGS_TUNE=sim_ar_us=8 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
   run c64_default 300 $B --steps 600 --warmup 50 ;;
 r4u)  # round 4: decode-attention depth / page size with the non-temporal K/V loads
   run dnt_depth 200 python -u bench/decode_cold.py --depth 2 3 --splits 1
   run dnt_depth_2k 200 python -u bench/decode_cold.py --L 2048 --depth 2 3 --splits 1
   run dnt_bs32 200 python -u bench/decode_cold.py --bs 32 --depth 2 3 --splits 1 ;;
-r4v)  # round 4: K rotation for every split (XGS_KROT=2) and non-temporal O-projection plans, c64 / c1 A/B
+r4v)  # round 4: K rotation for every split (XGS_TUNE=krot=2) and non-temporal O-projection plans, c64 / c1 A/B
   run c64_base 300 $B --steps 600 --warmup 50
-  run c64_krot2 300 env XGS_KROT=2 $B --steps 600 --warmup 50
-  run c64_ont 300 env XGS_M64_PLANS="4096x4096x1@64=1,4,1;4096x4096x1@32=1,4,1" $B --steps 600 --warmup 50
+  run c64_krot2 300 env XGS_TUNE=krot=2 $B --steps 600 --warmup 50
+  run c64_ont 300 env XGS_TUNE=m64_plans="4096x4096x1@64=1,4,1;4096x4096x1@32=1,4,1" $B --steps 600 --warmup 50
   run c64_base2 300 $B --steps 600 --warmup 50
   run c1_base 300 $B --concurrency 1 --steps 300 --warmup 30
-  run c1_krot2 300 env XGS_KROT=2 $B --concurrency 1 --steps 300 --warmup 30
-  run c1_ont 300 env XGS_M64_PLANS="4096x4096x1@16=1,3,1" $B --concurrency 1 --steps 300 --warmup 30 ;;
+  run c1_krot2 300 env XGS_TUNE=krot=2 $B --concurrency 1 --steps 300 --warmup 30
+  run c1_ont 300 env XGS_TUNE=m64_plans="4096x4096x1@16=1,3,1" $B --concurrency 1 --steps 300 --warmup 30 ;;
 r4w)  # round 4: split attention combine inside the O GEMM (gemm_m64g_xl): tests, batch-1 / batch-8 A/B
   pyt xl_tests 400 tests/test_fused_decode_gpu.py -k "xl or combines or logits"
   run c1_base 300 $B --concurrency 1 --steps 300 --warmup 30

@@ -59,19 +59,6 @@ struct M64Epi {
   float* ss_out;
   int* counters;
   int krot = 0;  // set by m64g_launch (k_rotation): walk K chunks from a per-tile start
-  // All-reduce prologue (gemm_m64g_arx, m64g_ar_role): the first ar_wgs workgroups of a
-  // 1-D grid fold the previous projection's split-K partials ar_part [ar_S, M, K] into
-  // the residual stream x (in place) and write its statistics to ss_in; the other
-  // workgroups (ar_tiles x ar_splits GEMM tiles) issue their first weight chunks, then
-  // wait for them (ar_flag: arrival count + pass count, zero between launches; word 2
-  // counts waits that timed out -- a sticky fault the host checks, m64_arx_fault).
-  const float* ar_part = nullptr;
-  int ar_S = 0;
-  int ar_wgs = 0;  // 0: no prologue (2-D grid)
-  int ar_tiles = 0;
-  int ar_splits = 0;
-  int* ar_flag = nullptr;
-  uint64_t ar_ticks = 0;  // simulated peer round trip (XGS_SIM_AR_US), 100 MHz ticks
 };
 
 // K-chunk rotation. Workgroups that all start at K chunk 0 and walk in lockstep read the
@@ -226,108 +213,6 @@ __device__ __forceinline__ void m64g_silu_tail(const float* __restrict__ part, i
   }
 }
 
-// All-reduce prologue, reducer side. Workgroup r of the first ar_wgs folds 1024-column
-// pieces (row t, chunk c) = r, r + ar_wgs, ... of the previous projection's split-K
-// partials into the bf16 residual stream, resid[t] += sum_s part[s, t] (fp32, s in
-// order), and writes the new residual's sum of squares per piece to ss[c * M + t] (the
-// GEMM's ss_in, ss_n = K / 1024). A --tp-shard simulation waits ar_ticks first (the
-// xGMI round trip of the rank's all-reduce). Write-through (sc1) stores, so the
-// arrival count needs no release fence: drain them, then count (guide §5, projection
-// GEMM item 2, the sc1 form).
-template <int NTHR>
-__device__ __forceinline__ void m64g_ar_role(uint16_t* __restrict__ resid, int M, int K, const M64Epi& epi,
-                                             float* red) {
-  constexpr int CPT = 1024 / NTHR;  // columns per thread: 4 (256 threads) or 8 (128)
-  static_assert(CPT == 4 || CPT == 8, "AR prologue geometry");
-  if (epi.ar_ticks) {
-    const uint64_t t0 = wall_clock64();
-    while (wall_clock64() - t0 < epi.ar_ticks) __builtin_amdgcn_s_sleep(1);
-  }
-  const int nch = K / 1024, S = epi.ar_S;
-  const int64_t slab = static_cast<int64_t>(M) * K;
-  float* ss = const_cast<float*>(epi.ss_in);
-  for (int job = blockIdx.x; job < M * nch; job += epi.ar_wgs) {
-    const int t = job / nch, c = job % nch;
-    const int64_t off = static_cast<int64_t>(t) * K + c * 1024 + threadIdx.x * CPT;
-    float v[CPT];
-    if constexpr (CPT == 8) {
-      unpack8(ld16(resid + off), v);
-    } else {
-      const uint2 r = *reinterpret_cast<const uint2*>(resid + off);
-      v[0] = __uint_as_float(r.x << 16);
-      v[1] = __uint_as_float(r.x & 0xFFFF0000u);
-      v[2] = __uint_as_float(r.y << 16);
-      v[3] = __uint_as_float(r.y & 0xFFFF0000u);
-    }
-    for (int s0 = 0; s0 < S; s0 += 4) {  // 4 slabs' loads in flight before their adds
-      float4 a[4][CPT / 4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int q = 0; q < CPT / 4; ++q)
-          a[j][q] = *reinterpret_cast<const float4*>(epi.ar_part + min(s0 + j, S - 1) * slab + off + 4 * q);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float k = s0 + j < S ? 1.f : 0.f;
-#pragma unroll
-        for (int q = 0; q < CPT / 4; ++q) {
-          v[4 * q] += k * a[j][q].x;
-          v[4 * q + 1] += k * a[j][q].y;
-          v[4 * q + 2] += k * a[j][q].z;
-          v[4 * q + 3] += k * a[j][q].w;
-        }
-      }
-    }
-    if constexpr (CPT == 8) {
-      const uint4 pk = pack8(v);
-      st16u_sc1(resid + off, pk);
-      unpack8(pk, v);  // statistics of the rounded (stored) residual
-    } else {
-      uint2 o;
-      o.x = pack2(v[0], v[1]);
-      o.y = pack2(v[2], v[3]);
-      st8_sc1(resid + off, o);
-      v[0] = __uint_as_float(o.x << 16);
-      v[1] = __uint_as_float(o.x & 0xFFFF0000u);
-      v[2] = __uint_as_float(o.y << 16);
-      v[3] = __uint_as_float(o.y & 0xFFFF0000u);
-    }
-    float sq = 0.f;
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) sq += v[i] * v[i];
-    sq = block_sum(sq, red);
-    if (threadIdx.x == 0) st4_sc1(ss + c * M + t, sq);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(epi.ar_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// All-reduce prologue, GEMM side: one lane polls the arrival count (relaxed, agent
-// scope; a bounded wait, so a lost reducer can never hang the GPU) and counts this
-// workgroup past (no acquire fence: everything the reducers wrote is read with sc1
-// loads -- the x DMAs and the statistics); the last of the ngemm re-arms both words for the next
-// launch. The reducers hold the lowest workgroup ids, so they are dispatched first and
-// never wait on a GEMM workgroup. A plain __syncthreads: it drains this workgroup's
-// pre-issued weight DMAs, which have landed during the wait.
-__device__ __forceinline__ void m64g_ar_wait(const M64Epi& epi, int ngemm) {
-  if (threadIdx.x == 0) {
-    const uint64_t t0 = wall_clock64();
-    while (__hip_atomic_load(epi.ar_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epi.ar_wgs) {
-      __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > 200000000ull) {  // 2 s: record the fault (sticky word 2), never hang
-        __hip_atomic_fetch_add(epi.ar_flag + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    if (__hip_atomic_fetch_add(epi.ar_flag + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngemm - 1) {
-      __hip_atomic_store(epi.ar_flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(epi.ar_flag + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-}
-
 // Dense kernel, parametrised for the decode shapes (bench/gemm_bench.py picks):
 //   NW  16-column MFMA tiles per wave (2 = 32 columns; required by the SiLU epilogue)
 //   WV  waves per workgroup (4 or 2): fewer waves = more, smaller workgroups, so a
@@ -363,20 +248,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  // tile bx of split s; with the all-reduce prologue the grid is 1-D, reducers first
-  const bool arx = epi.ar_wgs > 0;
-  int bx = blockIdx.x, S = gridDim.y, s = blockIdx.y;
-  if (arx) {
-    if (static_cast<int>(blockIdx.x) < epi.ar_wgs) {
-      if constexpr (WV == 2 || WV == 4)  // the host rejects the 8-wave configurations
-        m64g_ar_role<64 * WV>(const_cast<uint16_t*>(x), M, K, epi, reinterpret_cast<float*>(lds0));
-      return;
-    }
-    const int lin = blockIdx.x - epi.ar_wgs;
-    bx = lin % epi.ar_tiles;
-    s = lin / epi.ar_tiles;
-    S = epi.ar_splits;
-  }
+  // tile bx of split s
+  const int bx = blockIdx.x, S = gridDim.y, s = blockIdx.y;
   // split s takes chunks [s * nch / S, (s + 1) * nch / S): any S <= K / KC (uneven
   // splits fill the chip where K / KC has no divisor near 256 / column tiles)
   const int nch_all = K / KC;
@@ -407,10 +280,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   auto issue_x = [&](uint8_t* slot, int c) {
     const int kk = chunk_k(c);
 #pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      if (arx) glds16_sc1(xsrc[i] + kk, slot + RPI * (wid * XI + i) * RB);  // published this launch
-      else glds16(xsrc[i] + kk, slot + RPI * (wid * XI + i) * RB);
-    }
+    for (int i = 0; i < XI; ++i) glds16(xsrc[i] + kk, slot + RPI * (wid * XI + i) * RB);
   };
   auto issue_w = [&](uint8_t* slot, int c) {
     const int kk = chunk_k(c);
@@ -469,24 +339,12 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   constexpr int TQ = MT > 1 ? 64 / WV : 1;
   float ssv[8];
   float ssb[TQ];
-  // ring prologue: chunks 0 .. NS - 2 into their slots. With the all-reduce prologue
-  // their weight parts stream in while the reducers run; x (the reduced residual) and
-  // its statistics are read after the wait, and that prologue is drained once, so the
-  // ring's counted waits hold from chunk 0 on
+  // ring prologue: chunks 0 .. NS - 2 into their slots
   auto slot_of = [&](int j) -> uint8_t* {
     if constexpr (NS == 3) return j == 0 ? lds0 : lds1;
     else return lds0 + j * SLOT;
   };
-  if (arx) {
-#pragma unroll
-    for (int j = 0; j < NS - 1; ++j)
-      if (j < nchunks) issue_w(slot_of(j), j);
-    m64g_ar_wait(epi, epi.ar_tiles * epi.ar_splits);
-  }
-  // (all-reduce prologue: the reducers' write-through statistics, read device-coherent)
-  auto ld_ss = [&](int idx) {
-    return arx ? __hip_atomic_load(epi.ss_in + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : epi.ss_in[idx];
-  };
+  auto ld_ss = [&](int idx) { return epi.ss_in[idx]; };
   if (tall_ss) {
 #pragma unroll
     for (int q = 0; q < TQ; ++q) ssb[q] = ld_ss(min(wid + WV * q, epi.ss_n - 1) * epi.ss_stride + min(lane, M - 1));
@@ -499,20 +357,9 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
       ssv[i] = ld_ss(min(j, epi.ss_n - 1) * epi.ss_stride + min(16 * mt + li, M - 1));
     }
   }
-  if (arx) {
 #pragma unroll
-    for (int j = 0; j < NS - 1; ++j)
-      if (j < nchunks) issue_x(slot_of(j), j);
-    // the weight DMAs were drained by the wait's barrier: only x chunks are in flight.
-    // Three slots: chunk 1's x may stay in flight (the loop's first counted wait
-    // retires it in order); deeper rings drain here
-    if constexpr (NS == 3) wait_vmcnt<XI>();
-    else wait_vmcnt<0>();
-  } else {
-#pragma unroll
-    for (int j = 0; j < NS - 1; ++j)
-      if (j < nchunks) issue(slot_of(j), j);
-  }
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < nchunks) issue(slot_of(j), j);
 
   if constexpr (NS == 3) {
     int c = 0;
@@ -1024,12 +871,7 @@ static void m64g_launch(const uint16_t* x, int M, int K, const uint16_t* w, int 
   const int tiles = N / (16 * nw * m64g_cfg_waves(cfg));
   M64Epi epi = epi_in;
   epi.krot = k_rotation(S);
-  dim3 grid(tiles, S);
-  if (epi.ar_wgs > 0) {  // all-reduce prologue: 1-D grid, the reducers first
-    epi.ar_tiles = tiles;
-    epi.ar_splits = S;
-    grid = dim3(epi.ar_wgs + tiles * S, 1);
-  }
+  const dim3 grid(tiles, S);
   if (nw == 1) launch_m64g<1>(cfg, grid, st, x, M, K, w, N, part, out, mode, epi);
   else launch_m64g<2>(cfg, grid, st, x, M, K, w, N, part, out, mode, epi);
 }
@@ -1049,32 +891,6 @@ int gemm_m64g_ex(const uint16_t* x, int M, int K, const uint16_t* w, int N, floa
                  float* ss_out, int* counters, hipStream_t st) {
   const M64Epi epi{ss_in, ss_n, ss_stride, eps, resid, ss_out, counters};
   if (m64g_check(M, K, N, part, out, S, mode, nw, cfg, epi)) return 1;
-  m64g_launch(x, M, K, w, N, part, out, S, mode, nw, cfg, epi, st);
-  return 0;
-}
-
-// gemm_m64g_ex on x = the residual stream [M, K] AFTER folding the previous
-// projection's split-K partials ar_part [ar_S, M, K] into it, in the same launch
-// (m64g_ar_role / m64g_ar_wait): the weight stream starts under the fold (and under a
-// simulated all-reduce wait of ar_ticks). ss [K / 1024, M] receives the residual's
-// statistics and is this GEMM's input-norm row scale. flags: 3 ints, zero before the
-// first launch (each launch leaves words 0-1 zero; word 2 counts timed-out waits).
-// PARTIAL / SiLU modes.
-int gemm_m64g_arx(uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
-                  int nw, int cfg, float* ss, float eps, int* counters, const float* ar_part, int ar_S, int ar_wgs,
-                  int* flags, uint64_t ar_ticks, hipStream_t st) {
-  M64Epi epi{ss, K / 1024, M, eps, nullptr, nullptr, counters};
-  if (mode != GG_PARTIAL && mode != GG_SILU) return 1;
-  if (K % 1024 || K / 1024 > 8 || ar_part == nullptr || ar_S < 1 || ar_wgs < 1 || ar_wgs > 64 || flags == nullptr)
-    return 1;
-  const int nthr = 64 * m64g_cfg_waves(cfg);
-  if (nthr != 128 && nthr != 256) return 1;  // the reducers' 1024-column pieces
-  if (m64g_check(M, K, N, part, out, S, mode, nw, cfg, epi)) return 1;
-  epi.ar_part = ar_part;
-  epi.ar_S = ar_S;
-  epi.ar_wgs = ar_wgs;
-  epi.ar_flag = flags;
-  epi.ar_ticks = ar_ticks;
   m64g_launch(x, M, K, w, N, part, out, S, mode, nw, cfg, epi, st);
   return 0;
 }

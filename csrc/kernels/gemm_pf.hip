@@ -51,7 +51,7 @@ int k_rotation(int S);  // gemm_m64g.hip
 
 enum : int { PF_BF16 = 0, PF_PARTIAL = 1, PF_SILU = 2 };
 constexpr int PF_GROUP_M = 8;  // M tiles per group of the tile order
-// K-tile rotation per W tile (XGS_PF_KROT=1; off by default): it spreads the
+// K-tile rotation per W tile (set_pf_krot(1); off by default): it spreads the
 // lock-step HBM stream of the weight-streaming kernels, but here it would put the
 // N tiles that share an A panel on different K tiles and lose that panel's L2 reuse
 static int pf_krot = 0;

@@ -23,17 +23,12 @@ int skinny_slab_kmax(int);
 int gemm_m64g(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
 int gemm_m64g_ex(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, const float*,
                  int, int, float, uint16_t*, float*, int*, hipStream_t);
-int gemm_m64g_arx(uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, float*, float,
-                  int*, const float*, int, int, int*, uint64_t, hipStream_t);
 int gemm_mw(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, hipStream_t);
 int gemm_pf(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, float*, int*,
             hipStream_t);
 int pf_sk_slot_floats(int);
 void set_pf_krot(int);
 void set_k_rotation(int mode);
-int gemm_mw_probe(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, hipStream_t);
-int gemm_mw_ss(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, const float*, int,
-               int, float, hipStream_t);
 void add_partials_resid(const float*, int, int, uint16_t*, float*, int, hipStream_t, uint64_t);
 void row_sumsq(const uint16_t*, int, int, float*, hipStream_t);
 void embed_gather(const int32_t*, int, const uint16_t*, int, int, uint16_t*, float*, hipStream_t);
@@ -266,19 +261,6 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("pf_sk_slot_floats", &xgk::pf_sk_slot_floats);
   m.def("set_pf_krot", [](int on) { xgk::set_pf_krot(on); });
   m.def("set_k_rotation", [](int mode) { xgk::set_k_rotation(mode); });
-  m.def("gemm_mw_probe", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
-                            int mode, int cfg, int probe, uintptr_t st) {
-    check(xgk::gemm_mw_probe(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode,
-                             cfg, probe, S(st)),
-          "gemm_mw_probe");
-  });
-  m.def("gemm_mw_ss", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
-                         int mode, int cfg, uintptr_t ss_in, int ss_n, int ss_stride, float eps, uintptr_t st) {
-    check(xgk::gemm_mw_ss(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode, cfg,
-                          P<const float>(ss_in), ss_n, ss_stride, eps, S(st)),
-          "gemm_mw_ss");
-  });
-  // ---- fused decode layer (gemm_m64g.hip epilogues, decode_attention.hip FQ prologue)
   m.def("gemm_m64g_ex", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
                            int mode, int nw, int cfg, uintptr_t ss_in, int ss_n, int ss_stride, float eps,
                            uintptr_t resid, uintptr_t ss_out, uintptr_t counters, uintptr_t st) {
@@ -286,14 +268,6 @@ PYBIND11_MODULE(_kernels, m) {
                             nw, cfg, P<const float>(ss_in), ss_n, ss_stride, eps, P<uint16_t>(resid),
                             P<float>(ss_out), P<int>(counters), S(st)),
           "gemm_m64g_ex");
-  });
-  m.def("gemm_m64g_arx", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
-                            int mode, int nw, int cfg, uintptr_t ss, float eps, uintptr_t counters, uintptr_t ar_part,
-                            int ar_S, int ar_wgs, uintptr_t flags, uint64_t ar_ticks, uintptr_t st) {
-    check(xgk::gemm_m64g_arx(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode,
-                             nw, cfg, P<float>(ss), eps, P<int>(counters), P<const float>(ar_part), ar_S, ar_wgs,
-                             P<int>(flags), ar_ticks, S(st)),
-          "gemm_m64g_arx");
   });
   m.def("add_partials_resid", [](uintptr_t part, int S_, int T, uintptr_t res, uintptr_t ss_part, int H,
                                  uintptr_t st, uint64_t sim_ticks) {

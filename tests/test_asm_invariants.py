@@ -114,43 +114,54 @@ def test_gemm_mw_waits_follow_the_ring(tmp_path):
     _no_spills(asm)
 
 
-def test_gemm_mw2_role_waits(tmp_path):
-    """Split-role rings: the weight waves' counted waits are multiples of their
-    per-chunk instruction count, the x waves' of theirs; both steady-state waits exist."""
-    asm, log = _compile("gemm_mw", tmp_path)
-    ks = _kernels(asm, "_ZN3xgk15gemm_mw2_kernel")
-    assert len(ks) >= 30, len(ks)
-    for name, body in ks.items():
-        WN, NWT, MTW, DW, DX, _nt = _targs(name)
-        WI = WN * 16 * NWT // 32
-        XI = (8 // WN) * 16 * MTW // 32
-        allowed = {k * WI for k in range(DW - 1)} | {k * XI for k in range(DX - 1)}
-        got = _vmcnts(_pipeline(body, through_barrier=True))  # the epilogue's RMS-statistics waits lie outside
-        assert got <= allowed, (name, sorted(got), sorted(allowed))
-        assert (DW - 2) * WI in got and (DX - 2) * XI in got, (name, sorted(got))
-    _no_spills(asm)
+def _pf_wait_counts(P: int, NA: int):
+    """Python twin of pf::wait_count (csrc/kernels/gemm_pf.hip): the steady-state
+    vmcnt before phase p = every DMA issued after the last piece phase p reads."""
+    NBW = 4
+    b_phase = lambda i: (i % P + 1) % P  # noqa: E731
+    n_issue = [NA + sum(1 for i in range(NBW) if b_phase(i) == ph) for ph in range(P)]
+    T = sum(n_issue)
+
+    def pos(tau, ph, j):
+        return tau * T + sum(n_issue[:ph]) + j
+
+    def pos_a(u, q):
+        return pos(u - 2, q + 1, NA - 1) if q <= P - 2 else pos(u - 1, 0, NA - 1)
+
+    def pos_b(u, i):
+        ph = b_phase(i)
+        j = NA + sum(1 for i2 in range(i) if b_phase(i2) == ph)
+        return pos(u - 1 if ph == 0 else u - 2, ph, j)
+
+    t = 8
+    out = []
+    for p in range(P):
+        latest = pos_a(t, p)
+        if p == 0:
+            latest = max([latest] + [pos_b(t, i) for i in range(NBW)])
+        out.append(pos(t, p, 0) - 1 - latest)
+    return out
 
 
-def test_gemm_mw3_pipelined_waits(tmp_path):
-    """Software-pipelined ring (cfg 15-21): every counted wait is a whole number of
-    per-chunk DMA groups (G = weight + x instructions per wave) up to R - 1, the
-    steady-state wait (R - 2 groups still in flight) exists, and the fragment reads of
-    a chunk are fenced by an explicit lgkmcnt(0) before the barrier that frees the slot."""
-    asm, _ = _compile("gemm_mw", tmp_path)
-    ks = _kernels(asm, "_ZN3xgk15gemm_mw3_kernel")
-    assert len(ks) >= 10, len(ks)
+def test_gemm_pf_waits_and_fragments(tmp_path):
+    """gemm_pf: every vmcnt is a count of its DMA issue order (or 0 at a range's
+    tail), the MFMA operands come straight from ds_read_b128 (no VALU shuffles of the
+    fragments between the reads and the MFMAs), and nothing spills."""
+    asm, log = _compile("gemm_pf", tmp_path)
+    assert "reserved registers" not in log
+    assert _pf_wait_counts(4, 1) == [6, 13, 13, 13] and _pf_wait_counts(2, 2) == [4, 10]
+    ks = _kernels(asm, "_ZN3xgk14gemm_pf_kernel")
+    assert len(ks) >= 8
     for name, body in ks.items():
-        WN, NWT, MTW, R, _nt = _targs(name)[:5]
-        G = WN * 16 * NWT // 64 + (8 // WN) * 16 * MTW // 64
-        allowed = {k * G for k in range(R)}
-        got = _vmcnts(_pipeline(body, through_barrier=True))
+        bm, mtp, _nt, pr = _targs(name)[:4]
+        if pr:  # anatomy-probe builds (no DMA / no MFMA)
+            continue
+        allowed = {0} | set(_pf_wait_counts(bm // (32 * mtp), mtp // 2))
+        got = _vmcnts(_without_epilogue_blocks(_pipeline(body)))
         assert got <= allowed, (name, sorted(got), sorted(allowed))
-        if R >= 3:
-            assert (R - 2) * G in got, (name, sorted(got))
-        # every in-loop barrier (all but the prologue's) follows its wave's lgkmcnt(0)
-        segs = body.split("s_barrier")[1:-1]
-        assert segs and all("lgkmcnt(0)" in seg for seg in segs), name
-    _no_spills(asm)
+        assert "v_pk_mov_b32" not in _pipeline(body), name
+    meta = asm[asm.index("amdhsa.kernels"):]
+    assert ".vgpr_spill_count: 0" in meta and not re.search(r"\.vgpr_spill_count:\s+[1-9]", meta)
 
 
 def test_gemm_m64g_waits_are_counted(tmp_path):

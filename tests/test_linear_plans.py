@@ -55,20 +55,3 @@ def test_split_silu_needs_slabs_and_tickets():
         _check(L.MODE_SILU, nw=1, counters=1)
 
 
-def test_arx_gate_follows_the_plans():
-    assert L.m64_arx_ok(1, 7168, 4096, L.MODE_SILU)         # gate_up8t4: (2, 4, 1), 4 waves
-    assert L.m64_arx_ok(1, 1536, 4096, L.MODE_PARTIAL)      # qkv8t4: (1, 8, 4), 2 waves
-    assert not L.m64_arx_ok(1, 14336, 4096, L.MODE_SILU)    # gate_up8t2 at 16 rows: 8-wave cfg 7
-    assert not L.m64_arx_ok(1, 6144, 3072, L.MODE_PARTIAL)  # K not a multiple of 1024
-
-
-def _arx(mode=L.MODE_PARTIAL, M=1, K=4096, N=6144, S=2, nw=1, cfg=0, ar_part=1, ar_S=4, wgs=4, flags=1):
-    return kernels().gemm_m64g_arx(1, M, K, 1, N, 1, 1, S, mode, nw, cfg, 1, 1e-5, 1, ar_part, ar_S, wgs, flags, 0, 0)
-
-
-@pytest.mark.parametrize("bad", [dict(mode=3), dict(mode=0, S=1), dict(K=4096 + 256), dict(K=16384, N=1024),
-                                 dict(wgs=0), dict(wgs=65), dict(flags=0), dict(ar_part=0), dict(ar_S=0),
-                                 dict(cfg=7, nw=2, N=8192)])
-def test_arx_host_checks_reject_before_launch(bad):
-    with pytest.raises(Exception):
-        _arx(**bad)

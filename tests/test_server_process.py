@@ -94,8 +94,7 @@ def test_tp2_process_replica_gloo_matches_tp1(tmp_path, monkeypatch, model, moe_
     `overlap`: every step takes the chunk-pipelined all-reduce path
     (LlamaLayer._forward_tp_overlap, 3 token chunks, async all-reduces)."""
     if overlap:  # read by the replica processes at import
-        monkeypatch.setenv("XGS_TP_OVERLAP_MIN_TOKENS", "1")
-        monkeypatch.setenv("XGS_TP_OVERLAP_CHUNKS", "3")
+        monkeypatch.setenv("XGS_TUNE", "tp_overlap_min_tokens=1|tp_overlap_chunks=3")
     import torch
     from xgserve.engine import EngineConfig, LLMEngine, SamplingParams
     from xgserve.models import build_model, get_config, save_checkpoint

@@ -156,7 +156,7 @@ def test_gemm_m64_rejects_bad_shapes():
 
 # ---------------------------------------------------------------- gemm_mw (64 < M <= 320)
 @pytest.mark.parametrize("M", [65, 100, 128, 192, 257, 320])
-@pytest.mark.parametrize("cfg", list(range(22)))
+@pytest.mark.parametrize("cfg", list(range(7)))
 def test_gemm_mw_partial_every_cfg(M, cfg):
     """Every ring depth / tile width, incl. uneven split-K chunk ranges (K / 64 = 22
     chunks over S = 3 and 5) and short splits (1-2 chunks per split)."""
@@ -169,10 +169,8 @@ def test_gemm_mw_partial_every_cfg(M, cfg):
         try:
             pend = mw_linear(x, w, MODE_PARTIAL, plan=(S, cfg))
         except ValueError:
-            # x tiles beyond the cfg's LDS / register budget: 320 rows fit cfg 2 only of 0-6;
-            # the deep split-role rings 12-14 take M <= 128, 7 / 8 / 10 / 11 M <= 256, 9 M <= 192;
-            # the pipelined 15-21 (two fragment sets in registers) M <= 128 / 192 / 256
-            limit = {2: 320, 9: 192, 12: 128, 13: 128, 14: 128, 15: 192, 16: 192, 17: 192, 18: 256, 19: 128, 20: 128, 21: 128}.get(cfg, 256)
+            # x tiles beyond the cfg's LDS budget: 320 rows fit cfg 2 only
+            limit = {2: 320}.get(cfg, 256)
             assert M > limit, (M, cfg)
             return
         assert pend.part.shape == (S, M, N)
@@ -191,10 +189,10 @@ def test_gemm_mw_llama_shapes(M, N, K):
 
 
 @pytest.mark.parametrize("M", [65, 128, 192, 257, 320])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 5, 6])
 def test_gemm_mw_silu_and_bf16(M, cfg):
     from xgserve.ops.linear import MW_CFGS, mw_linear
-    if M > {2: 320, 9: 192, 12: 128, 13: 128, 14: 128, 15: 192, 16: 192, 17: 192, 18: 256, 19: 128, 20: 128, 21: 128}.get(cfg, 256):
+    if M > {2: 320}.get(cfg, 256):
         pytest.skip("x tile beyond this configuration's LDS budget")
     F_, H = 2 * MW_CFGS[cfg][0], 1024
     x = rnd(M, H)
@@ -272,34 +270,6 @@ def test_gemm_m64g_uneven_splits(M, N, K, nw, S, cfg):
     pend = m64_linear(x, w, MODE_PARTIAL, split_k=S, nw=nw, cfg=cfg)
     assert pend.part.shape == (S, M, N)
     assert rel_err(pend.part.sum(0), x.float() @ w.float().t()) < 1e-5
-
-
-@pytest.mark.parametrize("M", [1, 64, 192])
-@pytest.mark.parametrize("cfg,ss_n", [(7, 4), (8, 16), (10, 1), (12, 4), (15, 4), (18, 16), (21, 1)])
-def test_gemm_mw_norm_row_scale(M, cfg, ss_n):
-    """gemm_mw's input-RMSNorm row scale (split-role configurations): the raw residual
-    rows times (W diag(g))^T, scaled by rsqrt(sum of ss_n partial squares / K + eps),
-    equals rmsnorm(x, g) @ W^T -- partial and SiLU epilogues."""
-    from xgserve.ops.linear import MW_CFGS, RowStats, mw_norm_linear
-    if M > {12: 128, 15: 192, 21: 128}.get(cfg, 256):
-        pytest.skip("x tile beyond the LDS budget")
-    H, N = 1024, 2 * MW_CFGS[cfg][0]
-    x = rnd(M, H)
-    xf = x.float()
-    parts = (xf * xf).view(M, ss_n, H // ss_n).sum(-1).t().contiguous()  # [ss_n, M]
-    stride = M + 3
-    ss = torch.zeros(ss_n, stride, device=DEV)
-    ss[:, :M] = parts
-    st = RowStats(ss.view(-1), ss_n, stride)
-    w = rnd(N, H, scale=0.05)
-    xn = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)
-    pend = mw_norm_linear(x, w, MODE_PARTIAL, st, 1e-5, plan=(3, cfg))
-    assert rel_err(pend.part.sum(0), xn @ w.float().t()) < 1e-4
-    g, u = rnd(N // 2, H, scale=0.05), rnd(N // 2, H, scale=0.05)
-    wi = interleave_gate_up(g, u).contiguous()
-    got = mw_norm_linear(x, wi, MODE_SILU, st, 1e-5, plan=(1, cfg))
-    ref = torch.nn.functional.silu(xn @ g.float().t()) * (xn @ u.float().t())
-    assert rel_err(got, ref) < 1e-2
 
 
 @pytest.mark.parametrize("M", [1, 17, 64, 65, 128, 192, 256])

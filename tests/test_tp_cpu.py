@@ -40,7 +40,7 @@ def _rank_main(rank, world, port, ck, moe_comm, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     if moe_comm == "alltoall-exact":  # every step on the count-exact (packed) EP dispatch
-        os.environ["XGS_EP_EXACT_MIN_PAIRS"] = "0"
+        os.environ["XGS_TUNE"] = "ep_exact_min_pairs=0"
         moe_comm = "alltoall"
     torch.set_num_threads(1)
     try:

@@ -83,7 +83,7 @@ def _rank_main(rank, world, port, ck, moe_comm, q, env=None):
         raise
 
 
-_UNFUSED = {"XGS_FUSED_DECODE": "0", "XGS_ASYNC_SCHED": "0"}
+_UNFUSED = {"XGS_TUNE": "fused_decode=0|async_sched=0"}
 
 
 @pytest.mark.parametrize("model,moe_comm,world,env", [
@@ -92,7 +92,7 @@ _UNFUSED = {"XGS_FUSED_DECODE": "0", "XGS_ASYNC_SCHED": "0"}
     # share the GPU with one hardware queue each, so every rank's kernels are co-resident
     ("llama", "alltoall", 8, {"GPU_MAX_HW_QUEUES": "1"}),
     ("mixtral", "alltoall", 2, None), ("mixtral", "allreduce", 2, None), ("mixtral", "auto", 2, None),
-    ("mixtral", "alltoall", 2, {"XGS_EP_EXACT_MIN_PAIRS": "0"}),
+    ("mixtral", "alltoall", 2, {"XGS_TUNE": "ep_exact_min_pairs=0"}),
     # an arrival while decoding: the asynchronous eager mixed step under TP
     ("llama", "alltoall", 2, {"XGS_TEST_STAGGER": "1"}), ("llama", "alltoall", 4, {"XGS_TEST_STAGGER": "1"})])
 def test_tp2_on_one_gpu_matches_fp32_reference(tmp_path, model, moe_comm, world, env):

@@ -28,6 +28,7 @@ import numpy as np
 import torch
 
 from .. import _runtime as R
+from .. import tune
 from ..models import build_model, get_config
 from ..parallel import comm
 from ..parallel.state import get_state
@@ -156,8 +157,8 @@ class LLMEngine:
         # finishing row's last token reaches the host, so the GPU never waits for the
         # host at a finish (a request arriving just then is admitted one step later).
         # Steady state 64 concurrent: +1.3 % tok/s, p50 TTFT 12.4 -> 16.6 ms
-        # (profiles/r3_steady_state.md). XGS_EARLY_RELEASE=0: synchronous finishing steps.
-        sc.early_release = int(os.environ.get("XGS_EARLY_RELEASE", "1" if cfg.early_release else "0"))
+        # (profiles/r3_steady_state.md). XGS_TUNE early_release=0: synchronous finishing steps.
+        sc.early_release = int(tune.get_bool("early_release", bool(cfg.early_release)))
         sc.eos_ids = list(self.mcfg.eos_token_ids)
         self.sched = R.StepScheduler(sc)
         # decode graphs capture the TP collectives: RCCL (and the IPC all-reduce) can be
@@ -213,7 +214,7 @@ class LLMEngine:
             self.spec = SpeculativeDecoder(self, cfg.draft_model, cfg.num_speculative_tokens,
                                            cfg.spec_min_acceptance_rate)
         self._inflight = None  # (plan, handle): launched by the previous step() (async scheduling)
-        self._async = (cfg.async_schedule and os.environ.get("XGS_ASYNC_SCHED", "1") != "0"
+        self._async = (cfg.async_schedule and tune.get_bool("async_sched", True)
                        and self.device.type == "cuda" and self.spec is None and bool(self.runner.graphs))
         log.info("engine ready: model=%s tp=%d blocks=%d (%.1f GiB KV) load=%.1fs", self.mcfg.name, get_state().tp_size,
                  num_blocks, self.runner.kv_bytes() / 2**30, self.load_time)

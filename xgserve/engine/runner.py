@@ -29,6 +29,7 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 import torch
 
+from .. import tune
 from .. import ops
 from ..models.base import AttnMeta
 from ..ops.attention import DecodeWorkspace
@@ -36,9 +37,9 @@ from ..parallel import comm
 
 # eager (prompt) steps leave their sampled tokens on the device for a looked-ahead successor
 ASYNC_MIXED = True
-# host wait for a step's results: poll the event (default; XGS_SPIN_WAIT=0: a
+# host wait for a step's results: poll the event (default; XGS_TUNE spin_wait=0: a
 # blocking synchronize) for at most 50 ms before blocking (profiles/r2_spin_wait.md)
-SPIN_WAIT = os.environ.get("XGS_SPIN_WAIT", "1") != "0"
+SPIN_WAIT = tune.get_bool("spin_wait", True)
 SPIN_MAX_S = 0.050
 
 log = logging.getLogger("xgserve.runner")
@@ -123,7 +124,7 @@ class ModelRunner:
         self.kv_caches = [(self.kv[i, 0], self.kv[i, 1]) for i in range(cfg.num_layers)]
         self.is_cuda = self.device.type == "cuda"
         Hq_local = cfg.num_heads // model.tp
-        self.max_splits = int(os.environ.get("XGS_DECODE_MAX_SPLITS", "16"))
+        self.max_splits = tune.get_int("decode_max_splits", 16)
         self.workspace = DecodeWorkspace(max(max_num_seqs, 1), Hq_local, cfg.head_dim, self.max_splits,
                                          self.device) if self.is_cuda else None
         # pinned staging for eager steps

@@ -30,12 +30,12 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .. import ops
+from .. import ops, tune
 from ..parallel import comm
 from ..parallel.state import get_state
 from ..ops import linear as linear_mod
 from ..ops.linear import (MODE_PARTIAL, MODE_SILU, MW_MAX_M, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace, RowStats,
-                          lm_head_linear, m64_arx_linear, m64_arx_ok, m64_linear, m64_norm_linear, m64_plan, m64_resid_linear,
+                          lm_head_linear, m64_linear, m64_norm_linear, m64_plan, m64_resid_linear,
                           mw_linear, mw_plan, pf_linear, pf_plan, pick_split,
                           quantize_fp8, skinny_linear, splitk_linear, splitk_prefill_ok, w8_linear, w8_plan)
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
@@ -53,37 +53,30 @@ FAST_M_SLAB = 64    # tokens per step for the O-projection slab kernel
 # split-K partials and ONE custom all-reduce launch per projection reduces them,
 # sums across ranks over xGMI, adds the residual and writes the next norm's
 # statistics (comm.tp_allreduce_resid): 6 launches + attention per layer instead
-# of 11. XGS_FUSED_DECODE=0 restores the unfused chain (A/B measurements, tests).
-FUSED_DECODE = os.environ.get("XGS_FUSED_DECODE", "1") != "0"
+# of 11. XGS_TUNE fused_decode=0 restores the unfused chain (A/B measurements, tests).
+FUSED_DECODE = tune.get_bool("fused_decode", True)
 # 64 < T <= this many tokens (the mixed step: decode rows + one bounded prefill chunk)
 # run every projection on gemm_mw (csrc/kernels/gemm_mw.hip): weight-stream-bound
 # MFMA GEMMs whose split-K partials go to the consumers, SiLU-gate in gate_up.
 # 0 = hipBLASLt for every step above 64 tokens.
-MW_MAX_TOKENS = min(MW_MAX_M, int(os.environ.get("XGS_MW_MAX_TOKENS", str(MW_MAX_M))))
+MW_MAX_TOKENS = min(MW_MAX_M, tune.get_int("mw_max_tokens", MW_MAX_M))
 # T > MW_MAX_TOKENS tokens (a mixed step carrying a whole 512-token prompt chunk,
 # prefill) on TP = 1: every projection on gemm_pf (csrc/kernels/gemm_pf.hip) --
 # QKV / O / down as split-K partials into their consumers, gate_up with the SiLU
-# gate in its epilogue (stream-K grid). XGS_PF=0 keeps the library GEMMs.
-PF_PROMPT = os.environ.get("XGS_PF", "1") != "0"
+# gate in its epilogue (stream-K grid). XGS_TUNE pf=0 keeps the library GEMMs.
+PF_PROMPT = tune.get_bool("pf", True)
 # TP > 1 prefill-sized steps: the row-parallel all-reduces are pipelined over this
 # many token chunks and overlapped with the next chunk's GEMMs (RCCL stream); a
 # 2k-token 8B step moves 16 MiB per all-reduce -- ~100 us on 7 xGMI links, a
-# GEMM-sized share of the layer. XGS_TP_OVERLAP_CHUNKS=1 disables it.
-TP_OVERLAP_CHUNKS = int(os.environ.get("XGS_TP_OVERLAP_CHUNKS", "2"))
-TP_OVERLAP_MIN_TOKENS = int(os.environ.get("XGS_TP_OVERLAP_MIN_TOKENS", "256"))
+# GEMM-sized share of the layer. XGS_TUNE tp_overlap_chunks=1 disables it.
+TP_OVERLAP_CHUNKS = tune.get_int("tp_overlap_chunks", 2)
+TP_OVERLAP_MIN_TOKENS = tune.get_int("tp_overlap_min_tokens", 256)
 # EP all_to_all: steps with at least this many (token, choice) pairs (and not under
 # graph capture) exchange exact per-destination counts first and send only real rows
-EP_EXACT_MIN_PAIRS = int(os.environ.get("XGS_EP_EXACT_MIN_PAIRS", "256"))
+EP_EXACT_MIN_PAIRS = tune.get_int("ep_exact_min_pairs", 256)
 # moe_comm "auto": steps of at most this many tokens use the allreduce form when the
 # custom IPC all-reduce can take the [T, H] message
 EP_AR_MAX_TOKENS = 64
-# One rank of a TP group simulated in one process (--tp-shard), decode steps of <= 16
-# tokens: the residual all-reduce of the O / down partials runs as the reducer
-# workgroups of the NEXT GEMM's launch (gemm_m64g_arx) while its weight stream starts,
-# instead of a launch of its own -- the exposed-latency A/B of
-# profiles/r4_ar_prologue.md. XGS_AR_PROLOGUE=0 keeps the separate launch.
-AR_PROLOGUE = os.environ.get("XGS_AR_PROLOGUE", "0") != "0"
-AR_PROLOGUE_MAX_M = 16
 
 
 @torch.no_grad()
@@ -437,11 +430,7 @@ class LlamaLayer(nn.Module):
         (+ residual, + next statistics). `resid` (bf16 [T, H]) is updated in place;
         returns the statistics of the new residual for the next layer."""
         eps = self.cfg.norm_eps
-        if stats.pending is not None:  # the previous layer's down all-reduce, folded in here
-            pqkv = m64_arx_linear(resid, stats.pending, self.qkv, MODE_PARTIAL, stats.ss, eps, ws.ar_flags,
-                                  comm.sim_ar_ticks())
-        else:
-            pqkv = m64_norm_linear(resid, self.qkv, MODE_PARTIAL, stats, eps)
+        pqkv = m64_norm_linear(resid, self.qkv, MODE_PARTIAL, stats, eps)
         a = self.attn.fused_decode(pqkv, meta, kv, cos_sin)
         if self.moe:
             return self._fused_moe_tail(a, resid, ws, site)
@@ -483,27 +472,12 @@ class LlamaLayer(nn.Module):
         T, H = resid.shape
         eps = self.cfg.norm_eps
         po = m64_linear(a, self.o, MODE_PARTIAL)
-        if self._ar_prologue(T):
-            act = m64_arx_linear(resid, po, self.gate_up, MODE_SILU, ws.ss[site], eps, ws.ar_flags,
-                                 comm.sim_ar_ticks())
-            pd = m64_linear(act, self.down, MODE_PARTIAL)
-            return RowStats(ws.ss[site + 1], H // 1024, T, pending=pd)  # folded in by the next QKV GEMM
         comm.tp_allreduce_resid(po.part, resid, ws.ss[site])
         st = RowStats(ws.ss[site], H // 1024, T)
         act = m64_norm_linear(resid, self.gate_up, MODE_SILU, st, eps)
         pd = m64_linear(act, self.down, MODE_PARTIAL)
         comm.tp_allreduce_resid(pd.part, resid, ws.ss[site + 1])
         return RowStats(ws.ss[site + 1], H // 1024, T)
-
-    def _ar_prologue(self, T: int) -> bool:
-        """The simulated-TP residual all-reduces as GEMM prologues (AR_PROLOGUE): a
-        single-rank process (the all-reduce is the local fold), T <= 16, and plans for
-        gate_up and QKV that take the prologue."""
-        if not (AR_PROLOGUE and get_state().tp_size == 1 and T <= AR_PROLOGUE_MAX_M):
-            return False
-        H = self.cfg.hidden_size
-        return (m64_arx_ok(T, self.gate_up.shape[0], H, MODE_SILU)
-                and m64_arx_ok(T, self.qkv.shape[0], H, MODE_PARTIAL))
 
 
 class LlamaForCausalLM(nn.Module):
@@ -596,8 +570,6 @@ class LlamaForCausalLM(nn.Module):
         st = RowStats(ws.ss[0], 1, meta.num_tokens)
         for i, layer in enumerate(self.layers):
             st = layer.forward_fused(resid, st, meta, kv_caches[i], self.cos_sin, ws, 2 * i + 1)
-        if st.pending is not None:  # the last layer's down all-reduce
-            comm.tp_allreduce_resid(st.pending.part, resid, st.ss)
         return ops.rmsnorm(resid, self.norm, self.cfg.norm_eps)
 
     def set_moe_comm(self, mode: str):

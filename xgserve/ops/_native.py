@@ -26,8 +26,9 @@ def kernels():
     try:
         from .. import _kernels as k  # noqa: WPS433
         # weight-streaming GEMMs: K-chunk rotation policy (csrc/kernels/gemm_m64g.hip
-        # k_rotation; XGS_KROT 0 never, 1 grids of split <= 2 (default), 2 always)
-        k.set_k_rotation(int(os.environ.get("XGS_KROT", "1")))
+        # k_rotation; XGS_TUNE krot: 0 never, 1 grids of split <= 2 (default), 2 always)
+        from .. import tune
+        k.set_k_rotation(tune.get_int("krot", 1))
         _K = k
         return k
     except Exception as e:  # pragma: no cover - depends on build

@@ -10,8 +10,8 @@ import torch
 from ._native import kernels, stream_ptr, use_native
 
 # register K/V tiles in flight per wave of the fused decode attention (2 or 3; 3 only
-# for G <= 4): XGS_DECODE_DEPTH A/B (bench/decode_cold.py --depth)
-DECODE_DEPTH = int(__import__("os").environ.get("XGS_DECODE_DEPTH", "2"))
+# for G <= 4): XGS_TUNE decode_depth A/B (bench/decode_cold.py --depth)
+DECODE_DEPTH = __import__("xgserve.tune", fromlist=["get_int"]).get_int("decode_depth", 2)
 
 
 def choose_num_splits(batch: int, num_kv_heads: int, max_seq_len: int, num_cus: int = 256) -> int:

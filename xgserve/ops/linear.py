@@ -11,6 +11,7 @@ from typing import Optional
 
 import torch
 
+from .. import tune
 from ._native import kernels, stream_ptr, use_native
 
 MODE_BF16, MODE_PARTIAL, MODE_SILU = 0, 1, 2
@@ -141,7 +142,7 @@ _M64_TUNED = {
 
 
 def _apply_plan_overrides(spec: str) -> None:
-    """XGS_M64_PLANS="NxKxMODE@BUCKET=nw,S,cfg;..." replaces tuned plans (A/B sweeps)."""
+    """XGS_TUNE m64_plans="NxKxMODE@BUCKET=nw,S,cfg;..." replaces tuned plans (A/B sweeps)."""
     for item in filter(None, (t.strip() for t in spec.split(";"))):
         key, plan = item.split("=")
         shape, bucket = key.split("@")
@@ -149,7 +150,7 @@ def _apply_plan_overrides(spec: str) -> None:
         _M64_TUNED.setdefault((n, k, mode), {})[int(bucket)] = tuple(int(v) for v in plan.split(","))
 
 
-_apply_plan_overrides(__import__("os").environ.get("XGS_M64_PLANS", ""))
+_apply_plan_overrides(tune.get_str("m64_plans", ""))
 
 
 def _m64_valid(N: int, K: int, mode: int, nw: int, S: int, cfg: int, M: int = 1) -> bool:
@@ -232,16 +233,11 @@ def m64_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, split
 # weight tile and every x row (x bytes per weight byte = M / columns), W and x both
 # by LDS-DMA, split-K partials for grids that would not fill the chip.
 # cfg -> (columns per workgroup, weight ring depth, non-temporal weight DMA)
-# (0-4: 4 x 2 waves as N x M; 5-6: 2 x 4 waves -- fewer LDS fragment reads per MFMA;
-# 7-14: split DMA roles -- waves 0-3 stream the weights through a deep ring, waves 4-7
-# the x tile; the depth is the weight ring's slot count; 15-21: software-pipelined
-# fragment reads -- one ring of whole chunks, chunk c + 1 read under chunk c's MFMAs)
+# (0-4: 4 x 2 waves as N x M; 5-6: 2 x 4 waves -- fewer LDS fragment reads per MFMA.
+# The split-role and software-pipelined families of round 4 (cfg 7-21) never won a
+# default plan and were removed in round 5; their sweeps stay in profiles/r4_mw*.)
 MW_CFGS = {0: (256, 2, True), 1: (128, 3, True), 2: (128, 2, True), 3: (256, 2, False), 4: (128, 3, False),
-           5: (128, 3, True), 6: (256, 2, True),
-           7: (128, 6, True), 8: (128, 6, True), 9: (128, 5, True), 10: (256, 3, True), 11: (256, 3, True),
-           12: (128, 8, True), 13: (128, 8, True), 14: (256, 4, True),
-           15: (128, 4, True), 16: (128, 3, True), 17: (128, 4, True), 18: (128, 3, True), 19: (128, 5, True),
-           20: (256, 3, True), 21: (128, 5, True)}
+           5: (128, 3, True), 6: (256, 2, True)}
 MW_MAX_M = 320   # M > 256 (a 320-row x tile) fits the LDS on cfg 2 only
 # (N, K, mode) -> {M bucket (128 / 192 / 256 / 320): (split_k, cfg)}, measured on MI355X with cold
 # weights (bench/gemm_bench.py --mw-sweep); other shapes take the default rule in mw_plan
@@ -416,31 +412,8 @@ def lm_head_linear(h: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return torch.nn.functional.linear(h, w)
 
 
-def mw_norm_linear(x: torch.Tensor, w: torch.Tensor, mode: int, stats: "RowStats", eps: float, plan=None,
-                   out: Optional[torch.Tensor] = None):
-    """gemm_mw (split-role configurations) on the raw residual stream x with its RMSNorm
-    as a per-row epilogue scale rsqrt(sum_sq / K + eps) (norm weight folded into w):
-    PendingSum (MODE_PARTIAL) or bf16 silu(gate) * up (MODE_SILU)."""
-    M, K = x.shape
-    N = w.shape[0]
-    p = plan or mw_plan(M, N, K, mode)
-    if p is None or p[1] < 7 or stats.n > 16:
-        raise ValueError(f"gemm_mw_ss: unsupported M={M} N={N} K={K} plan={p} stats={stats.n}")
-    S, cfg = p
-    k = kernels()
-    st = (stats.ss.data_ptr(), stats.n, stats.stride, float(eps))
-    if mode == MODE_PARTIAL:
-        part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
-        k.gemm_mw_ss(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, cfg, *st, stream_ptr())
-        return PendingSum(part, S)
-    if out is None:
-        out = torch.empty(M, N // 2 if mode == MODE_SILU else N, dtype=torch.bfloat16, device=x.device)
-    k.gemm_mw_ss(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), S, mode, cfg, *st, stream_ptr())
-    return out
-
-
 def _apply_mw_overrides(spec: str) -> None:
-    """XGS_MW_PLANS="NxKxMODE@BUCKET=S,cfg;..." replaces gemm_mw plans (A/B sweeps)."""
+    """XGS_TUNE mw_plans="NxKxMODE@BUCKET=S,cfg;..." replaces gemm_mw plans (A/B sweeps)."""
     for item in filter(None, (t.strip() for t in spec.split(";"))):
         key, plan = item.split("=")
         shape, bucket = key.split("@")
@@ -448,7 +421,7 @@ def _apply_mw_overrides(spec: str) -> None:
         _MW_TUNED.setdefault((n, k, mode), {})[int(bucket)] = tuple(int(v) for v in plan.split(","))
 
 
-_apply_mw_overrides(__import__("os").environ.get("XGS_MW_PLANS", ""))
+_apply_mw_overrides(tune.get_str("mw_plans", ""))
 
 
 # ---------------------------------------------------------------------------- fused decode layer
@@ -460,9 +433,9 @@ MODE_RESID = 3
 # column tile in-launch while its split-K slab (S x M x columns fp32) is at most
 # this many bytes -- the tile's last arriver reads it serially (~1 us per 16 KB,
 # cdna_hip_programming.md §5); larger slabs (M ~ 64) go through the wide
-# add_partials_resid kernel instead. XGS_RESID_INLAUNCH_KB overrides (A/B of the
+# add_partials_resid kernel instead. XGS_TUNE resid_inlaunch_kb overrides (A/B of the
 # batched last-arriver reduce at M = 64, whose slabs are 64-256 KB).
-RESID_INLAUNCH_MAX_BYTES = int(__import__("os").environ.get("XGS_RESID_INLAUNCH_KB", "32")) << 10
+RESID_INLAUNCH_MAX_BYTES = tune.get_int("resid_inlaunch_kb", 32) << 10
 
 
 @dataclass
@@ -472,10 +445,6 @@ class RowStats:
     ss: torch.Tensor
     n: int
     stride: int
-    # the residual add these statistics describe has not run yet: the consuming GEMM
-    # folds these split-K partials in first (m64_arx_linear), or they are reduced
-    # by comm.tp_allreduce_resid before anything else reads the residual
-    pending: Optional["PendingSum"] = None
 
 
 class ResidWorkspace:
@@ -493,9 +462,6 @@ class ResidWorkspace:
         # arrival tickets (GG_RESID: one word per tile): zero here, and every launch
         # re-arms the words it used
         self.counters = torch.zeros(n_sites, 2 * self.MAX_TILES, dtype=torch.int32, device=device)
-        # all-reduce prologue (m64_arx_linear): arrival + pass count, re-armed by each launch;
-        # word 2 counts timed-out waits (m64_arx_fault)
-        self.ar_flags = torch.zeros(3, dtype=torch.int32, device=device)
 
 
 # Prefill-sized down projections (K = 3.5 N) have too few output tiles for the chip at
@@ -569,54 +535,6 @@ def m64_norm_linear(x: torch.Tensor, w: torch.Tensor, mode: int, stats: RowStats
     k.gemm_m64g_ex(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), 1, mode, nw, cfg, *st, 0, 0, 0,
                    stream_ptr())
     return out
-
-
-def m64_arx_ok(M: int, N: int, K: int, mode: int) -> bool:
-    """Can m64_arx_linear run this GEMM (a plan whose workgroups are 128 / 256 threads,
-    K a multiple of 1024 up to 8192)?"""
-    plan = m64_plan(M, N, K, mode)
-    return plan is not None and plan[2] != 7 and K % 1024 == 0 and K // 1024 <= 8
-
-
-def m64_arx_linear(resid: torch.Tensor, prev: PendingSum, w: torch.Tensor, mode: int, ss: torch.Tensor,
-                   eps: float, flags: torch.Tensor, ticks: int = 0, wgs: Optional[int] = None):
-    """resid += sum_s prev.part[s] (the previous projection's split-K partials) and then
-    the norm-scaled GEMM of the new residual, in ONE gemm_m64g launch: reducer
-    workgroups fold the partials (after `ticks` of simulated all-reduce latency) while
-    the GEMM workgroups already stream their first weight chunks, then read the
-    residual and its statistics (written to `ss`, [K / 1024, M]). Returns what
-    m64_norm_linear returns: PendingSum (MODE_PARTIAL) or bf16 silu(gate) * up."""
-    M, K = resid.shape
-    N = w.shape[0]
-    plan = m64_plan(M, N, K, mode)
-    if plan is None or not m64_arx_ok(M, N, K, mode):
-        raise ValueError(f"gemm_m64g_arx: unsupported shape M={M} N={N} K={K} mode={mode}")
-    nw, S, cfg = plan
-    if wgs is None:
-        wgs = min(M * (K // 1024), 32)
-    k = kernels()
-    if flags.numel() < 3 or flags.dtype != torch.int32:
-        raise ValueError("gemm_m64g_arx: flags must be 3 int32 words")
-    ar = (prev.part.data_ptr(), prev.part.shape[0], wgs, flags.data_ptr(), int(ticks), stream_ptr())
-    if mode == MODE_PARTIAL:
-        part = torch.empty(S, M, N, dtype=torch.float32, device=resid.device)
-        k.gemm_m64g_arx(resid.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, mode, nw, cfg, ss.data_ptr(),
-                        float(eps), 0, *ar)
-        return PendingSum(part, S)
-    out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=resid.device)
-    part, cnt = 0, 0
-    if S > 1:  # split-K SiLU: slabs + tile tickets, reduced in the GEMM tail
-        pt = torch.empty(S, M, N, dtype=torch.float32, device=resid.device)
-        part, cnt = pt.data_ptr(), tile_counters(resid.device, N).data_ptr()
-    k.gemm_m64g_arx(resid.data_ptr(), M, K, w.data_ptr(), N, part, out.data_ptr(), S, mode, nw, cfg, ss.data_ptr(),
-                    float(eps), cnt, *ar)
-    return out
-
-
-def m64_arx_fault(flags: torch.Tensor) -> int:
-    """Waits of the all-reduce prologue that gave up (2 s) since `flags` was zeroed:
-    non-zero means a reducer never arrived and those launches computed on stale x."""
-    return int(flags[2].item())
 
 
 def m64_resid_linear(x, w: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace, site: int,

@@ -54,14 +54,14 @@ def resid_allreduce_ok(T: int, H: int) -> bool:
 
 
 # Simulated TP all-reduce (bench.py --tp-shard: one rank of a TP group in one process):
-# XGS_SIM_AR_US > 0 makes the local stand-in wait that long (the peer round trip of the
+# XGS_TUNE sim_ar_us > 0 makes the local stand-in wait that long (the peer round trip of the
 # one-shot xGMI all-reduce), so the simulation exposes collective latency
 # (profiles/r3_tp_ar_overlap.md). A measurement knob.
-_SIM_AR_TICKS = int(float(os.environ.get("XGS_SIM_AR_US", "0")) * 100)  # 100 MHz wall clock
+_SIM_AR_TICKS = int(__import__("xgserve.tune", fromlist=["get_float"]).get_float("sim_ar_us", 0.0) * 100)  # 100 MHz
 
 
 def sim_ar_ticks() -> int:
-    """The simulated all-reduce wait (XGS_SIM_AR_US) in 100 MHz ticks; 0 in a real TP group."""
+    """The simulated all-reduce wait (XGS_TUNE sim_ar_us) in 100 MHz ticks; 0 in a real TP group."""
     return _SIM_AR_TICKS if get_state().tp_size == 1 else 0
 
 

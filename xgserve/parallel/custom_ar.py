@@ -25,7 +25,7 @@ over xGMI (the pull kernels), each rank writes its contribution straight into
 every peer's receive region as 16-byte lines {data, gen, data, gen}; the receiver
 polls its own memory until the generations match -- no fence, no flag word, no
 remote read round trip after the synchronisation. It serves the fused residual
-all-reduce and plain all-reduces up to `ll_max` bytes (XGS_AR_LL_MAX, 0 = pull
+all-reduce and plain all-reduces up to `ll_max` bytes (XGS_TUNE ar_ll_max, 0 = pull
 kernels everywhere).
 
 First contact (`self_test`, run by `maybe_enable` on every start): before the
@@ -152,7 +152,8 @@ class CustomAllReduce:
         self.gens_ll = torch.zeros(self.max_blocks + 1, dtype=torch.int32, device=device)
         import os
         if ll_max is None:
-            ll_max = int(os.environ.get("XGS_AR_LL_MAX", str(256 << 10)))
+            from .. import tune
+            ll_max = tune.get_int("ar_ll_max", 256 << 10)
         self.ll_max = min(ll_max, k.car_ll_max_bytes(self.LL_REGION))
         self.resid_ll = self.ll_max > 0
         self.chunk = chunk

@@ -1,0 +1,67 @@
+"""Measurement knobs: the A/B switches and plan overrides the profiles in
+`profiles/` were measured with, behind ONE environment variable instead of one
+variable per knob:
+
+  XGS_TUNE="key=value|key=value|..."      e.g.  XGS_TUNE="krot=0|decode_depth=3"
+
+Keys (default in brackets; every default is the production setting):
+  fused_decode [1]         fused decode layer (GEMM epilogue norms / residuals)
+  async_sched [1]          plan + launch step N+1 before step N's tokens reach the host
+  early_release [config]   release length-finishing rows at lookahead
+  spin_wait [1]            host polls the step event instead of blocking
+  pf [1]                   gemm_pf for prompt-sized steps (0: library GEMMs)
+  krot [1]                 K-chunk rotation of the weight-streaming GEMMs (0 / 1 / 2)
+  m64_plans / mw_plans     gemm_m64g / gemm_mw plan overrides, "NxKxMODE@BUCKET=...;..."
+  mw_max_tokens [320]      largest step on gemm_mw
+  resid_inlaunch_kb [32]   in-launch residual reduce bound of the fused decode GEMMs
+  decode_depth [2]         decode attention K/V register pipeline depth
+  decode_max_splits [16]   split-K cap of decode attention
+  ar_ll_max [262144]       push (LL) all-reduce up to this many bytes (0: pull kernels)
+  sim_ar_us [0]            --tp-shard simulation: stand-in all-reduce latency
+  tp_overlap_chunks [2]    TP prefill: all-reduces pipelined over this many chunks
+  tp_overlap_min_tokens [256]
+  ep_exact_min_pairs [256] EP all_to_all: count-exact splits from this many pairs
+Unknown keys are an error (a typo must not silently measure the default).
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict
+
+KEYS = {"fused_decode", "async_sched", "early_release", "spin_wait", "pf", "krot", "m64_plans", "mw_plans",
+        "mw_max_tokens", "resid_inlaunch_kb", "decode_depth", "decode_max_splits", "ar_ll_max", "sim_ar_us",
+        "tp_overlap_chunks", "tp_overlap_min_tokens", "ep_exact_min_pairs"}
+
+
+def _parse(spec: str) -> Dict[str, str]:
+    out = {}
+    for item in filter(None, (t.strip() for t in spec.split("|"))):
+        if "=" not in item:
+            raise ValueError(f"XGS_TUNE: expected key=value, got {item!r}")
+        k, v = item.split("=", 1)
+        k = k.strip()
+        if k not in KEYS:
+            raise ValueError(f"XGS_TUNE: unknown key {k!r} (known: {sorted(KEYS)})")
+        out[k] = v.strip()
+    return out
+
+
+def knobs() -> Dict[str, str]:
+    return _parse(os.environ.get("XGS_TUNE", ""))
+
+
+def get_str(key: str, default: str) -> str:
+    assert key in KEYS, key
+    return knobs().get(key, default)
+
+
+def get_int(key: str, default: int) -> int:
+    return int(float(get_str(key, str(default))))
+
+
+def get_float(key: str, default: float) -> float:
+    return float(get_str(key, str(default)))
+
+
+def get_bool(key: str, default: bool) -> bool:
+    return get_str(key, "1" if default else "0") not in ("0", "false", "False", "off", "")
