@@ -139,15 +139,20 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
                                                           float* __restrict__ part, uint16_t* __restrict__ out,
                                                           int mode, int krot, PfSk sk) {
   // MTP: 16-row m tiles per wave per phase -> a phase is MTP x 4 x 2 MFMAs per wave
-  // and releases 32 MTP A rows (NA = MTP / 2 DMA instructions per wave)
+  // and releases 32 MTP A rows = 4 MTP DMA pieces of 8 rows; wave w issues pieces
+  // w, w + 8, ... (MTP = 3: 12 pieces -> waves 0-3 two, waves 4-7 one; NA0 / NA1 are
+  // the per-wave counts of the two groups, and each group's waits count its own)
   constexpr int P = BM / (32 * MTP);
-  constexpr int NA = MTP / 2;
+  constexpr int NPC = 4 * MTP;                       // pieces per A phase block
+  constexpr int NA0 = (NPC + 7) / 8;                 // pieces per wave, waves 0-3
+  constexpr int NA1 = NPC / 8;                       // waves 4-7
+  constexpr int NA = NA0;
   constexpr int PB = 32 * MTP * 128;       // bytes of one A phase block
   constexpr int BN = pf::BN;
   constexpr int ASZ = BM * 128;            // A image: P phase blocks
   constexpr int SLOT = ASZ + BN * 128;     // + the W image
   constexpr int NACC = P * MTP * 4;        // f32x4 accumulators per lane
-  static_assert(P >= 2 && P * 32 * MTP == BM && (MTP == 2 || MTP == 4), "gemm_pf geometry");
+  static_assert(P >= 2 && P * 32 * MTP == BM && MTP >= 2 && MTP <= 4 && NA1 >= 1, "gemm_pf geometry");
   static_assert(2 * SLOT + 16 <= 160 * 1024, "LDS");
   // ONE __shared__ object (cdna_hip_programming.md §5 "Three .s-level traps" (a));
   // the last 16 bytes hold the stream-K "last arriver" flag
@@ -193,12 +198,13 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
   // ---- one K range [kt_lo, kt_lo + nk) of the tile at (m0, n0) into acc
   auto compute = [&](int m0, int n0, int kt_lo, int nk) {
     const int rot = krot ? ((n0 / BN) * 37) % nk : 0;
-    // A phase block q: rows [wr 0: 16 MTP rows][wr 1: 16 MTP rows]; DMA a of wave wid
-    // fills block rows 8 (NA wid + a) .. + 7
+    // A phase block q: rows [wr 0: 16 MTP rows][wr 1: 16 MTP rows]; piece pc = wid + 8 a
+    // of wave wid fills block rows 8 pc .. 8 pc + 7
     const uint16_t* asrc[P][NA];
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-      const int br = 8 * (NA * wid + a) + dr;
+      const int pc = wid + 8 * a < NPC ? wid + 8 * a : wid;   // (an unused slot of waves 4-7)
+      const int br = 8 * pc + dr;
       const int half = br / (16 * MTP);
       const int r = half * (BM / 2) + br - half * 16 * MTP;
 #pragma unroll
@@ -214,7 +220,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
       if constexpr (PR == 1) return;
 #pragma unroll
       for (int a = 0; a < NA; ++a)
-        glds16(asrc[q][a] + kof(t), smem + (t & 1) * SLOT + q * PB + (NA * wid + a) * 1024);
+        if (a < NA1 || wr == 0)
+          glds16(asrc[q][a] + kof(t), smem + (t & 1) * SLOT + q * PB + (wid + 8 * a) * 1024);
     };
     auto issue_b = [&](int t, int i) {
       if constexpr (PR == 1) return;
@@ -276,7 +283,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
     // wait for what (tile 0, phase 0) reads; the steady count holds iff every issue
     // between that piece and the wait exists: target tile tt <= nk - 3, or tt == nk - 2
     // with phase <= 1
-    pf_wait<P, NA, 0>(nk >= 2);
+    if (wr == 0) pf_wait<P, NA0, 0>(nk >= 2);
+    else pf_wait<P, NA1, 0>(nk >= 2);
     if (wr == 1) raw_barrier();  // the stagger: waves 4-7 one barrier behind
 
     auto phase = [&](int t, auto ph_c) {
@@ -307,7 +315,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
                                                             (((4 * ks + g) ^ sl) << 4));
       // fragment reads retire before the barrier: the region may be re-staged next phase
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (wr == 1 && need) pf_wait<P, NA, PN>(steady);
+      if (wr == 1 && need) pf_wait<P, NA1, PN>(steady);
       raw_barrier();
       __builtin_amdgcn_sched_barrier(0);
       // ---- MFMA segment
@@ -321,7 +329,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
             acc[p][mt][nt] = mfma16x16x32(bfr[nt][ks], afr[mt][ks], acc[p][mt][nt]);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
-      if (wr == 0 && need) pf_wait<P, NA, PN>(steady);
+      if (wr == 0 && need) pf_wait<P, NA0, PN>(steady);
     };
     for (int t = 0; t < nk; ++t) {
       phase(t, std::integral_constant<int, 0>{});
@@ -474,10 +482,18 @@ static int launch_pf(int tiles, hipStream_t st, const uint16_t* x, int M, int K,
   return static_cast<int>(hipGetLastError());
 }
 
-// cfg % 8 -> (BM, MTP, NT): 0 (256, 2, -) 1 (192, 2, -) 2 (128, 2, -) 3 (256, 4, -)
-// 4 (256, 2, nt) 5 (192, 2, nt) 6 (128, 2, nt) 7 (256, 4, nt); cfg / 8: 0 the kernel,
-// 1 no DMA, 2 no MFMA (anatomy probes, bench/pf_gemm_bench.py --probe: garbage results)
-int pf_cfg_bm(int cfg) { return (cfg & 3) == 1 ? 192 : ((cfg & 3) == 2 ? 128 : 256); }
+// cfg % 8 -> (BM, MTP): 0 (256, 2)  1 (192, 2)  2 (128, 2)  3 (256, 4)  4 (192, 3)  5 (288, 3);
+// cfg / 8: 0 the kernel, 1 no DMA, 2 no MFMA (anatomy probes, bench/pf_gemm_bench.py
+// --probe: garbage results). W stays on cached DMA (non-temporal measured slower: the
+// M tiles of a W tile re-read it through L2).
+int pf_cfg_bm(int cfg) {
+  switch (cfg & 7) {
+    case 1: case 4: return 192;
+    case 2: return 128;
+    case 5: return 288;
+    default: return 256;
+  }
+}
 
 template <int PR>
 static int launch_pf_cfg(int c, int tiles, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N,
@@ -487,10 +503,9 @@ static int launch_pf_cfg(int c, int tiles, hipStream_t st, const uint16_t* x, in
     case 1: return launch_pf<192, 2, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
     case 2: return launch_pf<128, 2, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
     case 3: return launch_pf<256, 4, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    case 4: return launch_pf<256, 2, true, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    case 5: return launch_pf<192, 2, true, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    case 6: return launch_pf<128, 2, true, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    default: return launch_pf<256, 4, true, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 4: return launch_pf<192, 3, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 5: return launch_pf<288, 3, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    default: return 1;
   }
 }
 
@@ -500,7 +515,9 @@ int pf_sk_slot_floats(int cfg) { return 512 * (pf_cfg_bm(cfg) / 32) * 4 * 4; }
 
 int gemm_pf(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
             int cfg, int sk_grid, float* sk_ws, int* sk_tickets, hipStream_t st) {
-  if (M < 1 || K < 64 || K % 64 || N < pf::BN || N % pf::BN || S < 1 || S > K / 64 || cfg < 0 || cfg >= 24) return 1;
+  if (M < 1 || K < 64 || K % 64 || N < pf::BN || N % pf::BN || S < 1 || S > K / 64 || cfg < 0 || cfg >= 24 ||
+      (cfg & 7) > 5)
+    return 1;
   if (sk_grid < 0 || (sk_grid > 0 && (S != 1 || sk_ws == nullptr || sk_tickets == nullptr))) return 1;
   if (mode == PF_PARTIAL) {
     if (part == nullptr) return 1;

@@ -295,20 +295,24 @@ def mw_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, plan=N
 
 
 # ---------------------------------------------------------------------------- gemm_pf (prompt-sized M)
-# csrc/kernels/gemm_pf.hip: BM x 256 output tiles (BM 256 / 192 / 128) on 8 waves,
-# 64-deep K tiles consumed in BM / 64 phases with the next tiles' LDS-DMA in flight
-# across the barriers, waves 4-7 one barrier behind waves 0-3 (MFMA / load
-# ping-pong per SIMD). cfg -> (BM, m tiles per wave per phase, non-temporal W):
-# 0 (256, 2) 1 (192, 2) 2 (128, 2) 3 (256, 4); 4-7 the same with non-temporal W DMA.
-PF_BM = (256, 192, 128)
-PF_CFG_BM = {0: 256, 1: 192, 2: 128, 3: 256}
+# csrc/kernels/gemm_pf.hip: BM x 256 output tiles on 8 waves, 64-deep K tiles consumed
+# in phases with the next tiles' LDS-DMA in flight across the barriers, waves 4-7 one
+# barrier behind waves 0-3 (MFMA / load ping-pong per SIMD), stream-K option.
+# cfg -> (BM, m tiles per wave per phase): 0 (256, 2) 1 (192, 2) 2 (128, 2) 3 (256, 4)
+# 4 (192, 3) 5 (288, 3).
+PF_CFG_BM = {0: 256, 1: 192, 2: 128, 3: 256, 4: 192, 5: 288}
 PF_MIN_M = 65
-PF_SK_MIN_TAIL = 0.15   # stream-K when the data-parallel grid's last round is this empty
+# per-CU cost of one 64-deep K tile (us) by tile height: max(LDS-DMA at ~55 GB/s per CU,
+# MFMA at ~1.45 PFLOP/s chip-wide); the planner's model, refined by measurement
+_PF_KT_US = {128: 0.89, 192: 1.12, 256: 1.50, 288: 1.69}
+_PF_DEFAULT_CFG = {128: 2, 192: 4, 256: 3, 288: 5}
+PF_SK_OVERHEAD = 1.06    # stream-K fixup (partial slots of the shared tiles) relative cost
+PF_SK_MAX_BM = 256       # the 288-row tile has no register room for the stream-K loop
 
 
 def pf_bm(M: int) -> int:
     """The tile height that pads M least (ties -> the taller tile)."""
-    return min(PF_BM, key=lambda b: (-(-M // b) * b, -b))
+    return min((256, 192, 128), key=lambda b: (-(-M // b) * b, -b))
 
 
 _CU_COUNT = {}
@@ -324,28 +328,31 @@ def cu_count(device=None) -> int:
 
 def pf_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL, cus: int = 256):
     """(split_k, cfg, sk_grid) for gemm_pf, or None when the shape is unsupported.
-    PARTIAL: split-K (fp32 partials reduced by the consumer) until the grid reaches
-    ~`cus` workgroups. bf16 / SiLU: data-parallel, or stream-K over `cus`
-    persistent workgroups when the last data-parallel round would run mostly empty."""
+    Every tile height is priced with the per-K-tile model (_PF_KT_US): data-parallel
+    rounds x K tiles, or stream-K (bf16 / SiLU) K tiles spread over `cus` workgroups;
+    PARTIAL adds split-K (fp32 partials reduced by the consumer) up to one round."""
     if M < 1 or N % 256 or K % 64 or K < 64:
         return None
-    bm = pf_bm(M)
-    cfg = PF_BM.index(bm)
-    if bm == 256:
-        cfg = 3  # 4 m tiles per wave per phase (32 MFMAs per segment)
-    tiles = -(-M // bm) * (N // 256)
-    if mode == MODE_PARTIAL:
-        # the most splits that still run in ONE round (a second, mostly empty round
-        # costs a whole split's time)
-        S = 1
-        while tiles * (S + 1) <= cus and (S + 1) <= K // 256:
-            S += 1
-        return S, cfg, 0
-    rounds = tiles / cus
-    tail = -(-tiles // cus) - rounds
-    if tail > PF_SK_MIN_TAIL and rounds < 6:
-        return 1, cfg, cus
-    return 1, cfg, 0
+    nk = K // 64
+    best = None
+    for bm, kt in _PF_KT_US.items():
+        tiles = -(-M // bm) * (N // 256)
+        cands = []
+        if mode == MODE_PARTIAL:
+            S = 1
+            while tiles * (S + 1) <= cus and (S + 1) <= K // 256:
+                S += 1
+            # + the fp32 partials' round trip through the consumer (written here, read
+            # there; ~8 TB/s through the Infinity Cache)
+            cands.append(((-(-tiles * S // cus)) * (-(-nk // S)) * kt + S * M * N * 8 / 8e6, S, 0))
+        else:
+            cands.append((-(-tiles // cus) * nk * kt, 1, 0))
+            if bm <= PF_SK_MAX_BM and tiles % cus:
+                cands.append((tiles * nk / cus * kt * PF_SK_OVERHEAD, 1, cus))
+        for t, S, skg in cands:
+            if best is None or t < best[0]:
+                best = (t, S, _PF_DEFAULT_CFG[bm], skg)
+    return best[1], best[2], best[3]
 
 
 class _SkWorkspace:
@@ -387,7 +394,7 @@ def pf_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_BF16, plan=None
     k = kernels()
     wsp = tk = 0
     if skg:
-        bm = PF_CFG_BM[cfg % 4]
+        bm = PF_CFG_BM[cfg % 8]
         wt, tt = _PF_SK.get(x.device, skg, cfg, -(-M // bm) * (N // 256))
         wsp, tk = wt.data_ptr(), tt.data_ptr()
     if mode == MODE_PARTIAL:
