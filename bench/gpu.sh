@@ -301,12 +301,20 @@ r4z)  # round 4: the re-tuned mixed-step QKV entry in the shipped TunableOp tabl
 r5a)  # round 5: gemm_pf (prompt-sized MFMA GEMM) -- numerics, per-projection A/B vs the library at the
       # mixed-step rows, then the headline with gemm_pf on / off and its kernel profile
   pyt pf_tests 300 tests/test_pf_gpu.py
-  run pf_gate_up 300 python -u bench/pf_gemm_bench.py --shapes gate_up --M 575 1024 --cfgs 1 3 4 5 --sk 0 256 --rounds 3 --iters 10
+  pyt moe_resid 200 tests/test_fused_decode_gpu.py -k "combine_resid or mixtral"
+  run pf_gate_up 300 python -u bench/pf_gemm_bench.py --shapes gate_up --M 575 1024 --cfgs 1 3 4 --sk 0 256 --rounds 3 --iters 10
+  run pf_gate_up288 300 python -u bench/pf_gemm_bench.py --shapes gate_up --M 575 1024 --cfgs 5 --sk 0 --rounds 3 --iters 10
   run pf_proj 300 python -u bench/pf_gemm_bench.py --shapes qkv_p o_p down_p --M 575 --cfgs 4 5 --splits 1 2 3 5 8 --rounds 3 --iters 10
   run pf_proj_sk 300 python -u bench/pf_gemm_bench.py --shapes qkv o down --M 575 --cfgs 2 4 --sk 0 256 --rounds 3 --iters 10
   run c64_pf 300 $B --steps 400 --warmup 40 "$@"
   run c64_lib 300 env XGS_TUNE=pf=0 $B --steps 400 --warmup 40 "$@"
   run c64_pf_driver 200 $B --steps 20 --warmup 5 "$@"
+  bash bench/profile.sh "$o/prof_c64" "$@" ;;
+r5b)  # r5a after the gate_up sweep
+  run pf_proj 300 python -u bench/pf_gemm_bench.py --shapes qkv_p o_p down_p --M 575 --cfgs 4 5 --splits 1 2 3 5 8 --rounds 3 --iters 10
+  run pf_proj_sk 300 python -u bench/pf_gemm_bench.py --shapes qkv o down --M 575 --cfgs 2 4 --sk 0 256 --rounds 3 --iters 10
+  run c64_pf 300 $B --steps 400 --warmup 40 "$@"
+  run c64_lib 300 env XGS_TUNE=pf=0 $B --steps 400 --warmup 40 "$@"
   bash bench/profile.sh "$o/prof_c64" "$@" ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py

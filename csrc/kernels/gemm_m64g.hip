@@ -35,7 +35,7 @@
 
 namespace xgk {
 
-enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2, GG_RESID = 3 };
+enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2, GG_RESID = 3, GG_MOE_RESID = 4 };
 
 // Fused-decode epilogue operands (all null / 0 for a plain GEMM).
 //   ss_in / ss_n / ss_stride: RMSNorm statistics of the input rows as ss_n
@@ -59,6 +59,23 @@ struct M64Epi {
   float* ss_out;
   int* counters;
   int krot = 0;  // set by m64g_launch (k_rotation): walk K chunks from a per-tile start
+};
+
+// GG_MOE_RESID (grouped w2 of the fused decode layer, TP = 1): the MoE combine inside
+// the w2 launch. Every workgroup stores its fp32 partial rows write-through and takes a
+// ticket on its column tile; the tile's last arriver (all real row tiles x S splits
+// have stored) adds, per token t, sum_j w[t, j] * sum_s part[s, dest[t, j]] over the
+// tile's columns into the bf16 residual stream and writes the new residual's sum of
+// squares ss_out[tile * T + t] (the next RMSNorm reads N / cols partial sums per row).
+// Replaces the separate combine_resid launch (6 us per layer at Mixtral batch 1).
+struct MoeResidEpi {
+  const int32_t* dest;   // [T * k] padded row of each (token, choice), -1 = not local
+  const float* w;        // [T * k] routing weights
+  uint16_t* resid;       // [T, N] bf16 residual stream, updated in place
+  float* ss_out;         // [N / cols, T]
+  int* counters;         // one ticket per column tile, zero between launches
+  int T;
+  int k;
 };
 
 // K-chunk rotation. Workgroups that all start at K chunk 0 and walk in lockstep read the
@@ -497,11 +514,62 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   }
 }
 
+// GG_MOE_RESID tail (MoeResidEpi): the column tile's last arriver combines every
+// (token, choice) row's S partials into the residual stream.
+template <int COLS, int NTHR>
+__device__ __forceinline__ void moe_resid_tail(const float* __restrict__ part, int S, int P, int N,
+                                               const MoeResidEpi& mre, int contributors, int* flag, int bx) {
+  if (!agent_ticket(mre.counters + bx, contributors - 1, flag)) return;
+  constexpr int G4 = COLS / 4;  // 4-column groups of the tile
+  const int n0 = bx * COLS;
+  const int64_t slab = static_cast<int64_t>(P) * N;
+  const int lane = threadIdx.x & 63;
+  // one row per G4 consecutive threads (G4 = 32: two rows per wave); the sum of
+  // squares of a row is a reduction over its G4 lanes
+  static_assert(64 % G4 == 0 && NTHR % G4 == 0, "moe_resid_tail geometry");
+  for (int base = 0; base < mre.T * G4; base += NTHR) {
+    const int idx = base + static_cast<int>(threadIdx.x);
+    const int t = idx / G4, c = 4 * (idx % G4);
+    const bool ok = t < mre.T;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    float sq = 0.f;
+    if (ok) {
+      for (int j = 0; j < mre.k; ++j) {
+        const int p = mre.dest[t * mre.k + j];
+        if (p < 0) continue;
+        const float wt = mre.w[t * mre.k + j];
+        float f[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < S; ++s) {
+          const float4 v = *reinterpret_cast<const float4*>(part + s * slab + static_cast<int64_t>(p) * N + n0 + c);
+          f[0] += v.x; f[1] += v.y; f[2] += v.z; f[3] += v.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] += wt * f[i];
+      }
+      uint16_t* rp = mre.resid + static_cast<int64_t>(t) * N + n0 + c;
+      const uint2 rv = *reinterpret_cast<const uint2*>(rp);
+      float r[4] = {__uint_as_float(rv.x << 16), __uint_as_float(rv.x & 0xFFFF0000u),
+                    __uint_as_float(rv.y << 16), __uint_as_float(rv.y & 0xFFFF0000u)};
+      uint2 o;
+      o.x = pack2(r[0] + a[0], r[1] + a[1]);
+      o.y = pack2(r[2] + a[2], r[3] + a[3]);
+      *reinterpret_cast<uint2*>(rp) = o;
+      const float q[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xFFFF0000u),
+                          __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xFFFF0000u)};
+      sq = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];  // statistics of the rounded residual
+    }
+#pragma unroll
+    for (int o = G4 / 2; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+    if (ok && (lane % G4) == 0) mre.ss_out[static_cast<int64_t>(bx) * mre.T + t] = sq;
+  }
+}
+
 template <int NW, int WV, int KC, bool NT, int MT>
 __device__ __forceinline__ void grouped_body(const uint16_t* __restrict__ x, const int32_t* __restrict__ rows, int e,
                                              int p0, int p1, int rt0, int K, const uint16_t* __restrict__ w, int N,
                                              int P, float* __restrict__ part, uint16_t* __restrict__ out, int mode,
-                                             uint8_t* lds0, uint8_t* lds1, uint8_t* lds2, int krot) {
+                                             uint8_t* lds0, uint8_t* lds1, uint8_t* lds2, int krot,
+                                             const MoeResidEpi& mre, int contributors) {
   constexpr int RB = KC * 2;
   constexpr int GPR = KC / 8;
   constexpr int RPI = 1024 / RB;
@@ -600,16 +668,21 @@ __device__ __forceinline__ void grouped_body(const uint16_t* __restrict__ x, con
     if (c < nchunks) step(lds0, lds2, c);
     if (c + 1 < nchunks) step(lds1, lds0, c + 1);
 
-    if (mode == GG_PARTIAL) {
+    if (mode == GG_PARTIAL || mode == GG_MOE_RESID) {
       float* pp = part + static_cast<int64_t>(s) * P * N;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int m = rt + 16 * mt + li;
 #pragma unroll
-        for (int nt_ = 0; nt_ < NW; ++nt_)
-          *reinterpret_cast<float4*>(pp + static_cast<int64_t>(m) * N + nbase + 16 * nt_ + 4 * g) =
-              make_float4(acc[nt_][mt][0], acc[nt_][mt][1], acc[nt_][mt][2], acc[nt_][mt][3]);
+        for (int nt_ = 0; nt_ < NW; ++nt_) {
+          float* dst = pp + static_cast<int64_t>(m) * N + nbase + 16 * nt_ + 4 * g;
+          if (mode == GG_MOE_RESID) st16_sc1(dst, acc[nt_][mt]);
+          else *reinterpret_cast<float4*>(dst) = make_float4(acc[nt_][mt][0], acc[nt_][mt][1], acc[nt_][mt][2],
+                                                             acc[nt_][mt][3]);
+        }
       }
+      if (mode == GG_MOE_RESID) moe_resid_tail<16 * NW * WV, 64 * WV>(part, S, P, N, mre, contributors,
+                                                                       reinterpret_cast<int*>(lds0), blockIdx.x);
     } else if (mode == GG_BF16) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
@@ -668,7 +741,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
                                                                        int K, const uint16_t* __restrict__ w, int N,
                                                                        int P, float* __restrict__ part,
                                                                        uint16_t* __restrict__ out, int mode,
-                                                                       int krot) {
+                                                                       int krot, MoeResidEpi mre) {
   constexpr int SLOT = 16 * MT_MAX * KC * 2 + WV * 16 * NW * KC * 2;
   __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
@@ -679,6 +752,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
     if (rt0 >= offs[i] && rt0 < offs[i + 1]) e = i;
   if (e < 0) return;  // capacity padding past the last segment
   const int p0 = offs[e], p1 = offs[e + 1];
+  // GG_MOE_RESID: every real row tile x split stores, then tickets (offs is 64-aligned)
+  const int contributors = (offs[E] >> 6) * static_cast<int>(gridDim.y);
   // MT_MAX 8 (prefill-sized steps): the 64-row tiles of an aligned pair within the
   // expert's segment run as ONE 128-row workgroup when both of them hold real rows -- the expert's weight tile is streamed once per
   // group instead of once per 64 rows (at ~144 rows per expert the re-reads are
@@ -702,7 +777,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
       const int need = (real + 63) >> 6;           // tiles holding real rows (they lead the segment)
       if (need >= 2) {
         if (lt != gs) return;                      // the group leader takes the group's real tiles
-        grouped_body<NW, WV, KC, NT, 8>(x, rows, e, p0, p1, r0, K, w, N, P, part, out, mode, lds0, lds1, lds2, krot);
+        grouped_body<NW, WV, KC, NT, 8>(x, rows, e, p0, p1, r0, K, w, N, P, part, out, mode, lds0, lds1, lds2, krot, mre, contributors);
         return;
       }
     }
@@ -717,18 +792,18 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_grouped_kernel(const uin
   constexpr bool MT1_OK = (16 / RPI / WV) >= 1;  // one 16-row x sub-tile is >= one DMA per wave
   if constexpr (MT_MAX >= 4) {
     if (amt > 2) {
-      grouped_body<NW, WV, KC, NT, 4>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2, krot);
+      grouped_body<NW, WV, KC, NT, 4>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2, krot, mre, contributors);
       return;
     }
   }
   if constexpr (MT_MAX >= 2) {
     if (amt == 2 || !MT1_OK) {
-      grouped_body<NW, WV, KC, NT, 2>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2, krot);
+      grouped_body<NW, WV, KC, NT, 2>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2, krot, mre, contributors);
       return;
     }
   }
   if constexpr (MT1_OK)
-    grouped_body<NW, WV, KC, NT, 1>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2, krot);
+    grouped_body<NW, WV, KC, NT, 1>(x, rows, e, p0, p1, rt0, K, w, N, P, part, out, mode, lds0, lds1, lds2, krot, mre, contributors);
 }
 
 int m64g_cfg_kc(int cfg);
@@ -736,10 +811,11 @@ int m64g_cfg_kc(int cfg);
 template <int NW>
 static void launch_m64g_grouped(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, const int32_t* rows,
                                 const int32_t* offs, const int32_t* valid, int E, int K, const uint16_t* w, int N,
-                                int P, float* part, uint16_t* out, int mode, bool mt1, bool mt8) {
+                                int P, float* part, uint16_t* out, int mode, bool mt1, bool mt8,
+                                const MoeResidEpi& mre) {
 #define XGK_GRP_MT(WV, KC, NT, MT)                                                                              \
   hipLaunchKernelGGL((gemm_m64g_grouped_kernel<NW, WV, KC, NT, MT>), grid, dim3(64 * WV), 0, st, x, rows, offs, \
-                     valid, E, K, w, N, P, part, out, mode, k_rotation(static_cast<int>(grid.y)))
+                     valid, E, K, w, N, P, part, out, mode, k_rotation(static_cast<int>(grid.y)), mre)
 #define XGK_GRP(WV, KC, NT)              \
   do {                                   \
     if (mt1) XGK_GRP_MT(WV, KC, NT, 1);  \
@@ -781,22 +857,27 @@ int m64g_cfg_kc(int cfg);
 // valid: the sorted rows (-1 = pad) for the row-occupancy dispatch, or nullptr (all 64 rows).
 int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, int E, int K, const uint16_t* w, int N,
                   int P, float* part, uint16_t* out, int S, int mode, int nw, int cfg, int max_rows, hipStream_t st,
-                  const int32_t* valid) {
+                  const int32_t* valid, const MoeResidEpi* mre_in) {
   if (E < 1 || P < 0 || P % 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 6) return 1;
-  if (mode != GG_BF16 && mode != GG_PARTIAL && mode != GG_SILU) return 1;
+  if (mode != GG_BF16 && mode != GG_PARTIAL && mode != GG_SILU && mode != GG_MOE_RESID) return 1;
+  const MoeResidEpi mre = mre_in ? *mre_in : MoeResidEpi{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
+  if (mode == GG_MOE_RESID && (mre.dest == nullptr || mre.w == nullptr || mre.resid == nullptr ||
+                               mre.ss_out == nullptr || mre.counters == nullptr || mre.T < 1 || mre.k < 1 ||
+                               max_rows > 256 || (16 * nw * m64g_cfg_waves(cfg)) % 4))
+    return 1;
   const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
   if (K % (S * kc) || N % cols) return 1;
   if (mode == GG_SILU && (nw != 2 || S != 1)) return 1;
-  if (mode == GG_PARTIAL && part == nullptr) return 1;
-  if (mode != GG_PARTIAL && out == nullptr) return 1;
+  if ((mode == GG_PARTIAL || mode == GG_MOE_RESID) && part == nullptr) return 1;
+  if (mode != GG_PARTIAL && mode != GG_MOE_RESID && out == nullptr) return 1;
   if (P == 0) return 0;
   const dim3 grid(N / cols, S, P / 64);
   const bool mt1 = max_rows <= 16 && cfg != 2 && cfg != 3;  // 16 x rows >= one DMA per wave
   // 128-row pairs for prefill-sized steps (> 256 pairs; decode keeps the 48 KB-slot
   // kernel and its occupancy), KC 64 configs only
   const bool mt8 = max_rows > 256 && m64g_cfg_kc(cfg) == 64;
-  if (nw == 1) launch_m64g_grouped<1>(cfg, grid, st, x, rows, offs, valid, E, K, w, N, P, part, out, mode, mt1, mt8);
-  else launch_m64g_grouped<2>(cfg, grid, st, x, rows, offs, valid, E, K, w, N, P, part, out, mode, mt1, mt8);
+  if (nw == 1) launch_m64g_grouped<1>(cfg, grid, st, x, rows, offs, valid, E, K, w, N, P, part, out, mode, mt1, mt8, mre);
+  else launch_m64g_grouped<2>(cfg, grid, st, x, rows, offs, valid, E, K, w, N, P, part, out, mode, mt1, mt8, mre);
   return 0;
 }
 

@@ -448,11 +448,12 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
         __syncthreads();
         if (*sk_flag == 0) continue;
         // contributors: the workgroups owning iterations [tile nk, tile nk + nk)
+        // (grid > iterations: workgroups between them may own none and never stored)
         const int64_t t_lo = static_cast<int64_t>(tile) * nk_all;
         const int g_lo = static_cast<int>(((t_lo + 1) * G - 1) / I);
         const int g_hi = static_cast<int>(((t_lo + nk_all) * G - 1) / I);
         for (int gg = g_lo; gg <= g_hi; ++gg) {
-          if (gg == v) continue;
+          if (gg == v || start(gg) == start(gg + 1)) continue;
           const float* other = slot_of(gg, tile) + tid * 4;
 #pragma unroll
           for (int q = 0; q < P; ++q)
@@ -473,12 +474,18 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
 template <int BM, int MTP, bool NT, int PR = 0>
 static int launch_pf(int tiles, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N, int S,
                      float* part, uint16_t* out, int mode, PfSk sk) {
-  if (sk.grid)
-    hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, true>), dim3(sk.grid), dim3(512), 0, st, x, M, K, w, N, S,
-                       part, out, mode, pf_krot, sk);
-  else
-    hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, false>), dim3(tiles * S), dim3(512), 0, st, x, M, K, w, N,
-                       S, part, out, mode, pf_krot, sk);
+  // stream-K: tiles up to 256 rows (the 288-row variant spills the combine's registers)
+  if constexpr (BM <= 256) {
+    if (sk.grid) {
+      hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, true>), dim3(sk.grid), dim3(512), 0, st, x, M, K, w, N, S,
+                         part, out, mode, pf_krot, sk);
+      return static_cast<int>(hipGetLastError());
+    }
+  } else if (sk.grid) {
+    return 1;
+  }
+  hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, false>), dim3(tiles * S), dim3(512), 0, st, x, M, K, w, N, S,
+                     part, out, mode, pf_krot, sk);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -127,7 +127,7 @@ def test_queue_full_is_503_with_retry_after(server):
     async def main():
         async with aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=0)) as s:
             async def post():
-                async with s.post(server + "/generate", json={"prompt": "q", "max_tokens": 400,
+                async with s.post(server + "/generate", json={"prompt": "q", "max_tokens": 1500,
                                                               "ignore_eos": True}) as r:
                     return r.status, dict(r.headers)
             tasks = [asyncio.create_task(post()) for _ in range(240)]

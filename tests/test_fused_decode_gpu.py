@@ -256,13 +256,21 @@ def test_moe_route_norm_and_combine_resid(T):
     w13 = torch.stack([interleave_gate_up(rnd(F, H, scale=0.05), rnd(F, H, scale=0.05)) for _ in range(E)])
     w2 = rnd(E, H, F, scale=0.05)
     out = ops.fused_moe(hn, w13, w2, w, ids)
-    r = resid.clone()
-    ss = torch.full((H // 1024 * T,), -1.0, device=DEV)
-    assert ops.fused_moe(hn, w13, w2, w, ids, resid=r, ss=ss) is None
-    want = (resid.float() + out.float()).bfloat16()
-    assert rel_err(r, want) < 1e-2
-    want_ss = r.float().view(T, H // 1024, 1024).pow(2).sum(-1).t().reshape(-1)
-    torch.testing.assert_close(ss, want_ss, rtol=1e-4, atol=1e-2)
+    # separate combine kernel (1024-column statistics), then the combine inside the
+    # w2 launch (per-128-column-tile statistics; twice: the tickets must re-arm)
+    counters = torch.zeros(128, dtype=torch.int32, device=DEV)
+    for use_ctr, reps in ((False, 1), (True, 2)):
+        for _ in range(reps):
+            r = resid.clone()
+            ss = torch.full((64 * T,), -1.0, device=DEV)
+            n = ops.fused_moe(hn, w13, w2, w, ids, resid=r, ss=ss, counters=counters if use_ctr else None)
+            assert n == (H // 128 if use_ctr else H // 1024)
+            want = (resid.float() + out.float()).bfloat16()
+            assert rel_err(r, want) < 1e-2
+            want_ss = r.float().view(T, n, H // n).pow(2).sum(-1).t().reshape(-1)
+            torch.testing.assert_close(ss[: n * T], want_ss, rtol=1e-4, atol=1e-2)
+        torch.cuda.synchronize()
+        assert int(counters.abs().sum()) == 0
 
 
 @pytest.mark.parametrize("fused", [True, False])

@@ -462,7 +462,8 @@ class LlamaLayer(nn.Module):
             part = ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, out_f32=True, layout=layout)
             comm.tp_allreduce_resid(part.unsqueeze(0), resid, ss)
         else:
-            ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, resid=resid, ss=ss, layout=layout)
+            return RowStats(ss, ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, resid=resid, ss=ss,
+                                              layout=layout, counters=ws.counters[site + 1]), T)
         return RowStats(ss, H // 1024, T)
 
     def _fused_tp_tail(self, a: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace, site: int) -> RowStats:

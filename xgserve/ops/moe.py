@@ -22,6 +22,8 @@ MOE_CFG_W2 = 1
 # removed.
 MOE_PREFILL_PAIRS = 256
 MOE_CFG_W2_PREFILL = 3
+# waves per workgroup of each gemm_m64g cfg (csrc/kernels/gemm_m64g.hip m64g_cfg_waves)
+M64G_CFG_WAVES = {0: 4, 1: 4, 2: 4, 3: 4, 4: 2, 5: 2, 6: 2, 7: 8}
 MOE_CFG_W13_PREFILL = 3
 
 
@@ -133,7 +135,8 @@ def moe_forward_ref(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w
 
 def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
               topk_ids: torch.Tensor, expert_offset: int = 0, resid: Optional[torch.Tensor] = None,
-              ss: Optional[torch.Tensor] = None, out_f32: bool = False, layout=None):
+              ss: Optional[torch.Tensor] = None, out_f32: bool = False, layout=None,
+              counters: Optional[torch.Tensor] = None):
     """Local-expert MoE FFN: sum_j w_j * FFN_{e_j}(x) over choices owned locally
     (ids in [expert_offset, expert_offset + E_local)); others contribute nothing.
 
@@ -141,8 +144,13 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     (x gathered through the sorted rows) -> grouped gemm_m64 on w2 (split-K
     partials when few experts are active) -> combine (weights, partial sums).
     resid / ss given (fused decode layer): the combine adds into the bf16 residual
-    stream in place and writes the next RMSNorm's per-1024-column statistics
-    ss[c * T + t]; returns None."""
+    stream in place and writes the next RMSNorm's per-column-tile statistics
+    ss[c * T + t]; returns the number of partial sums per row. With `counters`
+    (>= H / 128 zeroed int32 words, re-armed by every launch) and a decode-sized
+    step the combine runs inside the w2 launch (GG_MOE_RESID: the last workgroup to
+    store into a column tile adds that tile's weighted rows into the residual), one
+    launch fewer per layer; otherwise a separate combine kernel with 1024-column
+    statistics."""
     if not use_native(x):
         out = moe_forward_ref(x, w13, w2, topk_w, topk_ids, expert_offset)
         if resid is None:
@@ -151,7 +159,7 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
         resid.copy_(r)
         T, H = r.shape
         ss[: (H // 1024) * T].copy_(r.float().view(T, H // 1024, 1024).pow(2).sum(-1).t().reshape(-1))
-        return None
+        return H // 1024
     T, k = topk_ids.shape
     E, F2, H = w13.shape
     F = F2 // 2
@@ -179,12 +187,20 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
             S = sk
             break
     part = torch.empty(S, P, H, dtype=torch.float32, device=x.device)
+    cols2 = 16 * nw2 * M64G_CFG_WAVES[cfg2]
+    if (resid is not None and counters is not None and max_rows <= MOE_PREFILL_PAIRS and H // cols2 <= counters.numel()
+            and (H // cols2) * T <= ss.numel()):
+        kn.moe_gemm_m64g_resid(act.data_ptr(), 0, offs.data_ptr(), E, F, w2.data_ptr(), H, P, part.data_ptr(), S, nw2,
+                               cfg2, max_rows, stream_ptr(), valid, dest.data_ptr(),
+                               topk_w.float().contiguous().data_ptr(), resid.data_ptr(), ss.data_ptr(),
+                               counters.data_ptr(), T, k)
+        return H // cols2
     gemm(act.data_ptr(), 0, offs.data_ptr(), E, F, w2.data_ptr(), H, P, part.data_ptr(), 0, S, 1, nw2, stream_ptr(),
          cfg=cfg2)
     if resid is not None:
         kn.moe_combine_resid(part.data_ptr(), S, P, dest.data_ptr(), topk_w.float().contiguous().data_ptr(),
                              resid.data_ptr(), ss.data_ptr(), T, k, H, stream_ptr())
-        return None
+        return H // 1024
     out = torch.empty(T, H, dtype=torch.float32 if out_f32 else x.dtype, device=x.device)
     kn.moe_combine(part.data_ptr(), S, P, dest.data_ptr(), topk_w.float().contiguous().data_ptr(), out.data_ptr(), T,
                    k, H, stream_ptr(), 1 if out_f32 else 0)
