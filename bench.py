@@ -106,6 +106,16 @@ def launch_ranks(n: int) -> int:
     return rc
 
 
+def prompt_gemm(eng) -> str:
+    """Which projections of the prompt-sized mixed steps run on gemm_pf (and for which
+    step sizes); the rest stay on the library GEMMs."""
+    layers = getattr(eng.model, "layers", None)
+    if layers is None or not getattr(layers[0], "pf_ok", False):
+        return "library"
+    from xgserve.models import llama
+    return f"gemm_pf[{','.join(sorted(llama.PF_SET))}] for {llama.PF_MIN_M}-{llama.PF_MAX_M} tokens"
+
+
 def preflight(st, world: int, tp: int, dev, eng) -> dict:
     """First contact with a multi-GPU node, before anything is timed (every rank
     takes part): the collective backend forms the N-rank
@@ -352,8 +362,7 @@ def main():
             "decode_ar": pre["decode_ar"],
             "detail": {"initial_population": "steady-state (ages uniform on [0, output_len))",
                        "backend": pre["backend"], "custom_ar_selftest": pre["custom_ar_selftest"],
-                       "prompt_gemm": "gemm_pf" if getattr(eng.model, "layers", None) is not None and
-                       getattr(eng.model.layers[0], "pf_ok", False) else "library",
+                       "prompt_gemm": prompt_gemm(eng),
                        "fill_steps": fill_steps, "window_engine_steps": window_steps,
                        "window_prompt_steps": window_mixed, "ttft_samples": len(ttfts),
                        "preemptions": st_["preemptions"], "kv_blocks": st_["kv_blocks_total"],

@@ -311,11 +311,33 @@ r5a)  # round 5: gemm_pf (prompt-sized MFMA GEMM) -- numerics, per-projection A/
   run c64_pf_driver 200 $B --steps 20 --warmup 5 "$@"
   bash bench/profile.sh "$o/prof_c64" "$@" ;;
 r5b)  # r5a after the gate_up sweep
+  run pf_gate_up288 300 python -u bench/pf_gemm_bench.py --shapes gate_up --M 575 1024 --cfgs 5 --sk 0 --rounds 3 --iters 10
   run pf_proj 300 python -u bench/pf_gemm_bench.py --shapes qkv_p o_p down_p --M 575 --cfgs 4 5 --splits 1 2 3 5 8 --rounds 3 --iters 10
   run pf_proj_sk 300 python -u bench/pf_gemm_bench.py --shapes qkv o down --M 575 --cfgs 2 4 --sk 0 256 --rounds 3 --iters 10
   run c64_pf 300 $B --steps 400 --warmup 40 "$@"
   run c64_lib 300 env XGS_TUNE=pf=0 $B --steps 400 --warmup 40 "$@"
   bash bench/profile.sh "$o/prof_c64" "$@" ;;
+r5c)  # gemm_pf anatomy at the mixed-step shapes (tuned library baselines)
+  run pf_probe 300 python -u bench/pf_gemm_bench.py --shapes gate_up --M 575 --cfgs 5 --sk 0 --probe --rounds 3 --iters 10
+  run pf_probe2 300 python -u bench/pf_gemm_bench.py --shapes qkv_p o_p down_p --M 575 --cfgs 4 5 --splits 3 5 8 --probe --rounds 3 --iters 10
+  run pf_sq 300 python -u bench/pf_gemm_bench.py --shapes sq8k --M 8192 --cfgs 3 --sk 0 --probe --rounds 2 --iters 5 ;;
+r5d)  # gemm_pf DMA lag 2 (template-form fragment waits) vs lag 1
+  pyt pf_tests 300 tests/test_pf_gpu.py -k "cfgs or streamk"
+  run pf_lag 300 python -u bench/pf_gemm_bench.py --shapes gate_up --M 575 --cfgs 5 6 3 7 0 --sk 0 --probe --rounds 3 --iters 10
+  run pf_lag_sq 300 python -u bench/pf_gemm_bench.py --shapes sq8k --M 8192 --cfgs 3 7 0 --sk 0 --rounds 2 --iters 5 ;;
+r5e)  # gemm_pf cfg sweep for the planner fit (lag-2 configs), then the headline on / off
+  pyt pf_tests 300 tests/test_pf_gpu.py
+  run pf_gu 300 python -u bench/pf_gemm_bench.py --shapes gate_up --M 512 575 1024 --cfgs 3 4 6 8 --sk 0 256 --rounds 3 --iters 10 --no-check
+  run pf_pr 300 python -u bench/pf_gemm_bench.py --shapes qkv_p o_p down_p --M 575 1024 --cfgs 2 4 6 8 --splits 2 3 4 5 8 --rounds 3 --iters 10 --no-check
+  run c64_pf 300 $B --steps 400 --warmup 40 "$@"
+  run c64_lib 300 env XGS_TUNE=pf=0 $B --steps 400 --warmup 40 "$@" ;;
+r5f)  # gemm_pf per-projection A/B in the headline (400 steps each, then the driver form)
+  run c64_gu 300 env XGS_TUNE=pf=gate_up $B --steps 400 --warmup 40 "$@"
+  run c64_gud 300 env XGS_TUNE=pf=gate_up,down $B --steps 400 --warmup 40 "$@"
+  run c64_all 300 env XGS_TUNE=pf=qkv,o,gate_up,down $B --steps 400 --warmup 40 "$@"
+  run c64_lib 300 env XGS_TUNE=pf=0 $B --steps 400 --warmup 40 "$@"
+  run c64_gud2 300 env XGS_TUNE=pf=gate_up,down $B --steps 400 --warmup 40 "$@"
+  run c64_gu2 300 env XGS_TUNE=pf=gate_up $B --steps 400 --warmup 40 "$@" ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;

@@ -77,6 +77,9 @@ def main():
     kernels()
     torch.manual_seed(0)
     dev = "cuda"
+    # the library baselines run with the shipped TunableOp table, as in the engine
+    from xgserve.tuning import enable_gemm_table
+    print(json.dumps({"gemm_table": enable_gemm_table(torch.device(dev))}), flush=True)
     for name in a.shapes:
         N, K, mode = SHAPES[name]
         nbytes = N * K * 2
@@ -92,12 +95,14 @@ def main():
             for cfg in cfgs:
                 for S in splits:
                     for skg in (sks if S == 1 else [0]):
+                        if skg and L.PF_CFG_BM[cfg % 16] > L.PF_SK_MAX_BM:
+                            continue
                         variants[f"pf_c{cfg}_s{S}" + (f"_sk{skg}" if skg else "")] = (S, cfg, skg)
             probes = {}
             if a.probe:
                 for k, (S, cfg, skg) in list(variants.items()):
-                    probes[k + "_nodma"] = (S, cfg % 8 + 8, skg)
-                    probes[k + "_nomfma"] = (S, cfg % 8 + 16, skg)
+                    probes[k + "_nodma"] = (S, cfg % 16 + 16, skg)
+                    probes[k + "_nomfma"] = (S, cfg % 16 + 32, skg)
             if not a.no_check:
                 r = ref(x, ws[0], mode)
                 for k, p in variants.items():

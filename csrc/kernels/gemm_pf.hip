@@ -62,56 +62,76 @@ constexpr int BN = 256;  // output columns per workgroup (4 waves x 64)
 constexpr int NBW = 4;   // W-tile DMA instructions per wave per K tile (256 rows x 128 B / 8 waves / 1 KB)
 
 // Steady-state DMA issue order per wave (P phases per K tile, NA = A-piece DMA
-// instructions per wave per phase). Tile t, phase 0 issues A piece P-1 of tile
-// t+1; phase p >= 1 issues A piece p-1 of tile t+2. W piece i of tile u goes in
-// position i % P of the P phases from (u-2, phase 1) to (u-1, phase 0): phases
-// 1..P-1 of tile u-2, then phase 0 of tile u-1 (its W image is free after phase 0
-// of tile u-2). Within a phase: the A pieces first, then the W pieces.
-constexpr int b_phase(int P, int i) { return (i % P + 1) % P; }
-constexpr int nb_in_phase(int P, int ph) {
+// instructions per wave per phase, lag L). Global phase of (tile t, phase p) is
+// tP + p. A piece q of tile u is read in global phase uP + q and its LDS region is
+// re-staged (for tile u + 2) L phases later: issued in global phase uP + q + L.
+// L = 1: the phase right after the last read -- the fragment reads retire before that
+// phase's first barrier (lgkmcnt(0) ahead of the barrier); L = 2: the template form,
+// the reads retire after the barrier, just ahead of the MFMAs (one phase less of DMA
+// in flight). W piece i of tile u (the W image is read in phase 0 of tile u - 2) is
+// issued in global phase (u - 2)P + L + i % P. Within a phase: A pieces, then W.
+constexpr int b_rel(int P, int L, int i) { return L + i % P; }      // global phase offset from (u - 2)P
+constexpr int b_phase(int P, int L, int i) { return b_rel(P, L, i) % P; }
+constexpr int nb_in_phase(int P, int L, int ph) {
   int c = 0;
-  for (int i = 0; i < NBW; ++i) c += b_phase(P, i) == ph ? 1 : 0;
+  for (int i = 0; i < NBW; ++i) c += b_phase(P, L, i) == ph ? 1 : 0;
   return c;
 }
-constexpr int n_issue(int P, int NA, int ph) { return NA + nb_in_phase(P, ph); }
-constexpr int tile_issues(int P, int NA) {
+// the A piece issued in phase ph and how many tiles ahead its target is (1 or 2)
+constexpr int a_piece(int P, int L, int ph) { return (ph - L % P + P) % P; }
+constexpr int a_ahead(int P, int L, int ph) { return 2 - (a_piece(P, L, ph) + L) / P; }
+constexpr int b_ahead(int P, int L, int i) { return 2 - b_rel(P, L, i) / P; }
+constexpr int n_issue(int P, int L, int NA, int ph) { return NA + nb_in_phase(P, L, ph); }
+constexpr int tile_issues(int P, int L, int NA) {
   int s = 0;
-  for (int ph = 0; ph < P; ++ph) s += n_issue(P, NA, ph);
+  for (int ph = 0; ph < P; ++ph) s += n_issue(P, L, NA, ph);
   return s;
 }
-constexpr int pos(int P, int NA, int tau, int ph, int j) {
+constexpr int pos(int P, int L, int NA, int tau, int ph, int j) {
   int o = 0;
-  for (int q = 0; q < ph; ++q) o += n_issue(P, NA, q);
-  return tau * tile_issues(P, NA) + o + j;
+  for (int q = 0; q < ph; ++q) o += n_issue(P, L, NA, q);
+  return tau * tile_issues(P, L, NA) + o + j;
 }
 // the last A DMA of A piece q of tile u
-constexpr int pos_a(int P, int NA, int u, int q) {
-  return q <= P - 2 ? pos(P, NA, u - 2, q + 1, NA - 1) : pos(P, NA, u - 1, 0, NA - 1);
+constexpr int pos_a(int P, int L, int NA, int u, int q) {
+  return pos(P, L, NA, u - 2 + (q + L) / P, (q + L) % P, NA - 1);
 }
-constexpr int pos_b(int P, int NA, int u, int i) {
-  const int ph = b_phase(P, i);
+constexpr int pos_b(int P, int L, int NA, int u, int i) {
+  const int ph = b_phase(P, L, i);
   int j = NA;
-  for (int i2 = 0; i2 < i; ++i2) j += b_phase(P, i2) == ph ? 1 : 0;
-  return pos(P, NA, ph == 0 ? u - 1 : u - 2, ph, j);
+  for (int i2 = 0; i2 < i; ++i2) j += b_phase(P, L, i2) == ph ? 1 : 0;
+  return pos(P, L, NA, u - 2 + b_rel(P, L, i) / P, ph, j);
 }
 // vmcnt that retires everything phase p of a steady-state tile reads (A piece p,
 // plus the whole W tile at p = 0), counted where the wait sits: after the issues
 // of the previous phase, before those of phase p
-constexpr int wait_count(int P, int NA, int p) {
+constexpr int wait_count(int P, int L, int NA, int p) {
   const int t = 8;
-  int latest = pos_a(P, NA, t, p);
+  int latest = pos_a(P, L, NA, t, p);
   if (p == 0)
-    for (int i = 0; i < NBW; ++i) latest = latest > pos_b(P, NA, t, i) ? latest : pos_b(P, NA, t, i);
-  return pos(P, NA, t, p, 0) - 1 - latest;
+    for (int i = 0; i < NBW; ++i) latest = latest > pos_b(P, L, NA, t, i) ? latest : pos_b(P, L, NA, t, i);
+  return pos(P, L, NA, t, p, 0) - 1 - latest;
 }
-static_assert(wait_count(4, 1, 0) == 6 && wait_count(4, 1, 1) == 13 && wait_count(4, 1, 2) == 13 &&
-                  wait_count(4, 1, 3) == 13, "pf wait counts (P = 4)");
-static_assert(wait_count(2, 2, 0) == 4 && wait_count(2, 2, 1) == 10, "pf wait counts (P = 2, NA = 2)");
+// the largest tile an issue of phase ph targets, relative to the phase's tile
+constexpr int max_ahead(int P, int L, int ph) {
+  int m = a_ahead(P, L, ph);
+  for (int i = 0; i < NBW; ++i)
+    if (b_phase(P, L, i) == ph && b_ahead(P, L, i) > m) m = b_ahead(P, L, i);
+  return m;
+}
+static_assert(wait_count(4, 1, 1, 0) == 6 && wait_count(4, 1, 1, 1) == 13 && wait_count(4, 1, 1, 2) == 13 &&
+                  wait_count(4, 1, 1, 3) == 13, "pf wait counts (P = 4)");
+static_assert(wait_count(2, 1, 2, 0) == 4 && wait_count(2, 1, 2, 1) == 10, "pf wait counts (P = 2, NA = 2)");
+static_assert(a_piece(3, 1, 0) == 2 && a_ahead(3, 1, 0) == 1 && a_piece(3, 1, 1) == 0 && a_ahead(3, 1, 1) == 2,
+              "pf lag-1 order");
+static_assert(a_piece(3, 2, 0) == 1 && a_ahead(3, 2, 0) == 1 && a_piece(3, 2, 1) == 2 && a_ahead(3, 2, 1) == 1 &&
+                  a_piece(3, 2, 2) == 0 && a_ahead(3, 2, 2) == 2,
+              "pf lag-2 order");
 }  // namespace pf
 
-template <int P, int NA, int PH>
+template <int P, int L, int NA, int PH>
 __device__ __forceinline__ void pf_wait(bool steady) {
-  if (steady) wait_vmcnt<pf::wait_count(P, NA, PH)>();
+  if (steady) wait_vmcnt<pf::wait_count(P, L, NA, PH)>();
   else wait_vmcnt<0>();
 }
 
@@ -133,7 +153,7 @@ struct PfSk {
   int grid;       // 0: data-parallel (grid = tiles x S)
 };
 
-template <int BM, int MTP, bool NT, int PR = 0, bool SKM = false>
+template <int BM, int MTP, bool NT, int PR = 0, bool SKM = false, int LAG = 1>
 __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restrict__ x, int M, int K,
                                                           const uint16_t* __restrict__ w, int N, int S,
                                                           float* __restrict__ part, uint16_t* __restrict__ out,
@@ -230,24 +250,24 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
       if constexpr (NT) glds16_nt(src, dst);
       else glds16(src, dst);
     };
-    // the DMA of phase PH of tile t (steady-state order, pf:: above)
+    // the DMA of phase PH of tile t (steady-state order, pf:: above); targets outside
+    // [0, nk) are skipped (the prologue runs virtual tiles -2 and -1)
     auto issue_phase = [&](int t, auto ph_c) {
       constexpr int PH = decltype(ph_c)::value;
-      if constexpr (PH == 0) {
-        if (t + 1 < nk) {
-          issue_a(t + 1, P - 1);
+      constexpr int QA = pf::a_piece(P, LAG, PH), UA = pf::a_ahead(P, LAG, PH);
+      if (t + UA >= 0 && t + UA < nk) issue_a(t + UA, QA);
 #pragma unroll
-          for (int i = 0; i < pf::NBW; ++i)
-            if (pf::b_phase(P, i) == 0) issue_b(t + 1, i);
+      for (int i = 0; i < pf::NBW; ++i)
+        if (pf::b_phase(P, LAG, i) == PH) {
+          const int ub = t + pf::b_ahead(P, LAG, i);
+          if (ub >= 0 && ub < nk) issue_b(ub, i);
         }
-      } else {
-        if (t + 2 < nk) {
-          issue_a(t + 2, PH - 1);
-#pragma unroll
-          for (int i = 0; i < pf::NBW; ++i)
-            if (pf::b_phase(P, i) == PH) issue_b(t + 2, i);
-        }
-      }
+    };
+    auto issue_tile = [&](int t) {
+      issue_phase(t, std::integral_constant<int, 0>{});
+      issue_phase(t, std::integral_constant<int, 1>{});
+      if constexpr (P > 2) issue_phase(t, std::integral_constant<int, (P > 2 ? 2 : 0)>{});
+      if constexpr (P > 3) issue_phase(t, std::integral_constant<int, (P > 3 ? 3 : 0)>{});
     };
 
 #pragma unroll
@@ -260,31 +280,12 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
     // every wave is past the previous range's LDS reads before its slots are refilled
     __syncthreads();
     // prologue: the issues of (virtual) tiles -2 and -1, in steady-state order
-#pragma unroll
-    for (int ph = 1; ph < P; ++ph) {
-      issue_a(0, ph - 1);
-#pragma unroll
-      for (int i = 0; i < pf::NBW; ++i)
-        if (pf::b_phase(P, i) == ph) issue_b(0, i);
-    }
-    issue_a(0, P - 1);
-#pragma unroll
-    for (int i = 0; i < pf::NBW; ++i)
-      if (pf::b_phase(P, i) == 0) issue_b(0, i);
-    if (nk > 1) {
-#pragma unroll
-      for (int ph = 1; ph < P; ++ph) {
-        issue_a(1, ph - 1);
-#pragma unroll
-        for (int i = 0; i < pf::NBW; ++i)
-          if (pf::b_phase(P, i) == ph) issue_b(1, i);
-      }
-    }
+    issue_tile(-2);
+    issue_tile(-1);
     // wait for what (tile 0, phase 0) reads; the steady count holds iff every issue
-    // between that piece and the wait exists: target tile tt <= nk - 3, or tt == nk - 2
-    // with phase <= 1
-    if (wr == 0) pf_wait<P, NA0, 0>(nk >= 2);
-    else pf_wait<P, NA1, 0>(nk >= 2);
+    // between that piece and the wait exists (nk >= 2: every prologue target does)
+    if (wr == 0) pf_wait<P, LAG, NA0, 0>(nk >= 2);
+    else pf_wait<P, LAG, NA1, 0>(nk >= 2);
     if (wr == 1) raw_barrier();  // the stagger: waves 4-7 one barrier behind
 
     auto phase = [&](int t, auto ph_c) {
@@ -294,7 +295,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
       constexpr int PN = (p + 1 < P) ? p + 1 : 0;
       const int tt = (p + 1 < P) ? t : t + 1;
       const bool need = tt < nk;
-      const bool steady = (tt <= nk - 3) || (tt == nk - 2 && PN <= 1);
+      // the count holds iff the last phase before the wait (p of tile t) issued all
+      // its DMA (its largest target is below nk; targets grow with the phase)
+      const bool steady = t + pf::max_ahead(P, LAG, p) <= nk - 1;
       // ---- load segment: this phase's DMA, then the fragment reads
       raw_barrier();
       __builtin_amdgcn_sched_barrier(0);
@@ -313,9 +316,10 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
         for (int ks = 0; ks < 2; ++ks)
           afr[mt][ks] = *reinterpret_cast<const bf16x8_t*>(slot + p * PB + (arl + 16 * mt + li) * 128 +
                                                             (((4 * ks + g) ^ sl) << 4));
-      // fragment reads retire before the barrier: the region may be re-staged next phase
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (wr == 1 && need) pf_wait<P, NA1, PN>(steady);
+      // LAG 1: fragment reads retire before the barrier (the region is re-staged next
+      // phase); LAG 2: they retire ahead of the MFMAs that use them (compiler waits)
+      if constexpr (LAG == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (wr == 1 && need) pf_wait<P, LAG, NA1, PN>(steady);
       raw_barrier();
       __builtin_amdgcn_sched_barrier(0);
       // ---- MFMA segment
@@ -329,7 +333,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
             acc[p][mt][nt] = mfma16x16x32(bfr[nt][ks], afr[mt][ks], acc[p][mt][nt]);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
-      if (wr == 0 && need) pf_wait<P, NA0, PN>(steady);
+      if (wr == 0 && need) pf_wait<P, LAG, NA0, PN>(steady);
     };
     for (int t = 0; t < nk; ++t) {
       phase(t, std::integral_constant<int, 0>{});
@@ -471,33 +475,35 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
   }
 }
 
-template <int BM, int MTP, bool NT, int PR = 0>
+template <int BM, int MTP, bool NT, int PR = 0, int LAG = 1>
 static int launch_pf(int tiles, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N, int S,
                      float* part, uint16_t* out, int mode, PfSk sk) {
   // stream-K: tiles up to 256 rows (the 288-row variant spills the combine's registers)
   if constexpr (BM <= 256) {
     if (sk.grid) {
-      hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, true>), dim3(sk.grid), dim3(512), 0, st, x, M, K, w, N, S,
+      hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, true, LAG>), dim3(sk.grid), dim3(512), 0, st, x, M, K, w, N, S,
                          part, out, mode, pf_krot, sk);
       return static_cast<int>(hipGetLastError());
     }
   } else if (sk.grid) {
     return 1;
   }
-  hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, false>), dim3(tiles * S), dim3(512), 0, st, x, M, K, w, N, S,
+  hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, false, LAG>), dim3(tiles * S), dim3(512), 0, st, x, M, K, w, N, S,
                      part, out, mode, pf_krot, sk);
   return static_cast<int>(hipGetLastError());
 }
 
-// cfg % 8 -> (BM, MTP): 0 (256, 2)  1 (192, 2)  2 (128, 2)  3 (256, 4)  4 (192, 3)  5 (288, 3);
-// cfg / 8: 0 the kernel, 1 no DMA, 2 no MFMA (anatomy probes, bench/pf_gemm_bench.py
+// cfg % 16 -> (BM, MTP): 0 (256, 2)  1 (192, 2)  2 (128, 2)  3 (256, 4)  4 (192, 3)  5 (288, 3);
+// with DMA lag 2 (fragment reads retire after the barrier; 3+ phases only): 6 (288, 3)
+// 7 (256, 2)  8 (192, 2);
+// cfg / 16: 0 the kernel, 1 no DMA, 2 no MFMA (anatomy probes, bench/pf_gemm_bench.py
 // --probe: garbage results). W stays on cached DMA (non-temporal measured slower: the
 // M tiles of a W tile re-read it through L2).
 int pf_cfg_bm(int cfg) {
-  switch (cfg & 7) {
-    case 1: case 4: return 192;
+  switch (cfg & 15) {
+    case 1: case 4: case 8: return 192;
     case 2: return 128;
-    case 5: return 288;
+    case 5: case 6: return 288;
     default: return 256;
   }
 }
@@ -512,6 +518,9 @@ static int launch_pf_cfg(int c, int tiles, hipStream_t st, const uint16_t* x, in
     case 3: return launch_pf<256, 4, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
     case 4: return launch_pf<192, 3, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
     case 5: return launch_pf<288, 3, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 6: return launch_pf<288, 3, false, PR, 2>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 7: return launch_pf<256, 2, false, PR, 2>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 8: return launch_pf<192, 2, false, PR, 2>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
     default: return 1;
   }
 }
@@ -522,8 +531,7 @@ int pf_sk_slot_floats(int cfg) { return 512 * (pf_cfg_bm(cfg) / 32) * 4 * 4; }
 
 int gemm_pf(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
             int cfg, int sk_grid, float* sk_ws, int* sk_tickets, hipStream_t st) {
-  if (M < 1 || K < 64 || K % 64 || N < pf::BN || N % pf::BN || S < 1 || S > K / 64 || cfg < 0 || cfg >= 24 ||
-      (cfg & 7) > 5)
+  if (M < 1 || K < 64 || K % 64 || N < pf::BN || N % pf::BN || S < 1 || S > K / 64 || cfg < 0 || cfg >= 48)
     return 1;
   if (sk_grid < 0 || (sk_grid > 0 && (S != 1 || sk_ws == nullptr || sk_tickets == nullptr))) return 1;
   if (mode == PF_PARTIAL) {
@@ -536,10 +544,10 @@ int gemm_pf(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* pa
   const int bm = pf_cfg_bm(cfg);
   const int tiles = ((M + bm - 1) / bm) * (N / pf::BN);
   const PfSk sk{sk_ws, sk_tickets, sk_grid};
-  switch (cfg / 8) {
-    case 0: return launch_pf_cfg<0>(cfg % 8, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    case 1: return launch_pf_cfg<1>(cfg % 8, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    default: return launch_pf_cfg<2>(cfg % 8, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+  switch (cfg / 16) {
+    case 0: return launch_pf_cfg<0>(cfg % 16, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 1: return launch_pf_cfg<1>(cfg % 16, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    default: return launch_pf_cfg<2>(cfg % 16, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
   }
 }
 

@@ -114,11 +114,13 @@ def test_gemm_mw_waits_follow_the_ring(tmp_path):
     _no_spills(asm)
 
 
-def _pf_wait_counts(P: int, NA: int):
+def _pf_wait_counts(P: int, NA: int, L: int = 1):
     """Python twin of pf::wait_count (csrc/kernels/gemm_pf.hip): the steady-state
-    vmcnt before phase p = every DMA issued after the last piece phase p reads."""
+    vmcnt before phase p = every DMA issued after the last piece phase p reads.
+    A piece q of tile u is issued in global phase (u - 2)P + q + L, W piece i in
+    (u - 2)P + L + i % P (global phase of (tile t, phase p) = tP + p)."""
     NBW = 4
-    b_phase = lambda i: (i % P + 1) % P  # noqa: E731
+    b_phase = lambda i: (L + i % P) % P  # noqa: E731
     n_issue = [NA + sum(1 for i in range(NBW) if b_phase(i) == ph) for ph in range(P)]
     T = sum(n_issue)
 
@@ -126,12 +128,14 @@ def _pf_wait_counts(P: int, NA: int):
         return tau * T + sum(n_issue[:ph]) + j
 
     def pos_a(u, q):
-        return pos(u - 2, q + 1, NA - 1) if q <= P - 2 else pos(u - 1, 0, NA - 1)
+        g = (u - 2) * P + q + L
+        return pos(g // P, g % P, NA - 1)
 
     def pos_b(u, i):
-        ph = b_phase(i)
+        g = (u - 2) * P + L + i % P
+        ph = g % P
         j = NA + sum(1 for i2 in range(i) if b_phase(i2) == ph)
-        return pos(u - 1 if ph == 0 else u - 2, ph, j)
+        return pos(g // P, ph, j)
 
     t = 8
     out = []
@@ -153,12 +157,14 @@ def test_gemm_pf_waits_and_fragments(tmp_path):
     ks = _kernels(asm, "_ZN3xgk14gemm_pf_kernel")
     assert len(ks) >= 8
     for name, body in ks.items():
-        bm, mtp, _nt, pr = _targs(name)[:4]
+        ta = _targs(name)
+        bm, mtp, _nt, pr = ta[:4]
+        lag = ta[5] if len(ta) > 5 else 1
         if pr:  # anatomy-probe builds (no DMA / no MFMA)
             continue
         P = bm // (32 * mtp)
         na0, na1 = (4 * mtp + 7) // 8, (4 * mtp) // 8  # per-wave A pieces of the two wave groups
-        allowed = {0} | set(_pf_wait_counts(P, na0)) | set(_pf_wait_counts(P, na1))
+        allowed = {0} | set(_pf_wait_counts(P, na0, lag)) | set(_pf_wait_counts(P, na1, lag))
         got = _vmcnts(_without_epilogue_blocks(_pipeline(body)))
         assert got <= allowed, (name, sorted(got), sorted(allowed))
         assert "v_pk_mov_b32" not in _pipeline(body), name

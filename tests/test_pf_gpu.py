@@ -52,7 +52,7 @@ def test_pf_default_plan(M, mode):
     assert rel_err(got, ref(x, w, mode)) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("M", [1, 100, 575, 600])
 def test_pf_cfgs_bf16(cfg, M):
     x, w = rnd(M, 1024), rnd(1024, 1024, scale=0.05)
@@ -69,7 +69,7 @@ def test_pf_splitk_uneven(S, M):
     assert rel_err(got, ref(x, w, L.MODE_PARTIAL)) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", [1, 3, 4])
+@pytest.mark.parametrize("cfg", [1, 3, 4, 7])
 @pytest.mark.parametrize("M", [257, 575, 1024])
 @pytest.mark.parametrize("grid", [7, 100, 256])
 def test_pf_streamk(cfg, M, grid):

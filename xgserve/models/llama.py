@@ -60,11 +60,20 @@ FUSED_DECODE = tune.get_bool("fused_decode", True)
 # MFMA GEMMs whose split-K partials go to the consumers, SiLU-gate in gate_up.
 # 0 = hipBLASLt for every step above 64 tokens.
 MW_MAX_TOKENS = min(MW_MAX_M, tune.get_int("mw_max_tokens", MW_MAX_M))
-# T > MW_MAX_TOKENS tokens (a mixed step carrying a whole 512-token prompt chunk,
-# prefill) on TP = 1: every projection on gemm_pf (csrc/kernels/gemm_pf.hip) --
-# QKV / O / down as split-K partials into their consumers, gate_up with the SiLU
-# gate in its epilogue (stream-K grid). XGS_TUNE pf=0 keeps the library GEMMs.
-PF_PROMPT = tune.get_bool("pf", True)
+# PF_MIN_M <= T <= PF_MAX_M tokens (a mixed step carrying a whole 512-token prompt
+# chunk) on TP = 1: the projections named by XGS_TUNE pf (comma list of qkv, o,
+# gate_up, down; "1" = PF_DEFAULT, "0" = none) on gemm_pf (csrc/kernels/gemm_pf.hip)
+# -- QKV / O / down as split-K partials into their consumers, gate_up with the SiLU
+# gate in its epilogue. The window is where two 288-row tiles cover the step: one
+# round of workgroups on 256 CUs, where gemm_pf beats the tuned library GEMMs
+# (gate_up 121 vs 124 + 10 us at M = 575); above and below it the tuned library
+# tiles are ahead (profiles/r5_pf_gemm.md) and keep those steps.
+PF_DEFAULT = "gate_up,down"
+_pf_spec = tune.get_str("pf", "1")
+PF_SET = frozenset() if _pf_spec in ("0", "") else frozenset(
+    (PF_DEFAULT if _pf_spec == "1" else _pf_spec).replace("+", ",").split(","))
+assert PF_SET <= {"qkv", "o", "gate_up", "down"}, f"XGS_TUNE pf: {sorted(PF_SET)}"
+PF_MIN_M, PF_MAX_M = (int(v) for v in tune.get_str("pf_m", "513-576").split("-"))
 # TP > 1 prefill-sized steps: the row-parallel all-reduces are pipelined over this
 # many token chunks and overlapped with the next chunk's GEMMs (RCCL stream); a
 # 2k-token 8B step moves 16 MiB per all-reduce -- ~100 us on 7 xGMI links, a
@@ -154,8 +163,8 @@ class LlamaLayer(nn.Module):
             mw_plan(MW_MAX_TOKENS, n, k, mode) is not None and mw_plan(FAST_M_SLAB + 1, n, k, mode) is not None
             for n, k, mode in mw_shapes)
         # T > MW_MAX_TOKENS on TP = 1: gemm_pf for every projection (MoE layers: attention)
-        self.pf_ok = self.fast_ok and PF_PROMPT and tp == 1 and all(
-            pf_plan(1024, n, k, mode) is not None for n, k, mode in mw_shapes)
+        self.pf_ok = self.fast_ok and bool(PF_SET) and tp == 1 and all(
+            pf_plan(PF_MAX_M, n, k, mode) is not None for n, k, mode in mw_shapes)
         # M <= 16 too, when every projection has a measured small-M plan
         self.w8 = None  # FP8 weight copies for batch <= 16 decode (LlamaForCausalLM.quantize_fp8)
         self.m64_small_ok = self.m64_ok and all(
@@ -362,18 +371,27 @@ class LlamaLayer(nn.Module):
             act = mw_linear(h, self.gate_up, MODE_SILU)
             d = mw_linear(act, self.down, MODE_PARTIAL)
             return (d if self.tp == 1 else self._ar(d.materialize())), residual
-        if self.pf_ok and T > MW_MAX_TOKENS:
-            # prompt-sized steps: gemm_pf (MFMA tiles, LDS-DMA ring, stream-K); split-K
-            # partials go to the consumers (rope_cache_partials / add + rmsnorm), the
-            # SiLU gate rides in the gate_up epilogue
-            pqkv = pf_linear(h, self.qkv, MODE_PARTIAL)
-            a = self.attn.from_partials(pqkv, meta, kv, cos_sin)
-            o = pf_linear(a, self.o, MODE_PARTIAL)
+        if self.pf_ok and PF_MIN_M <= T <= PF_MAX_M:
+            # prompt-sized mixed steps: gemm_pf for the projections of PF_SET (split-K
+            # partials into the consumers: rope_cache_partials / add + rmsnorm; the SiLU
+            # gate in the gate_up epilogue), the library GEMMs for the others
+            if "qkv" in PF_SET:
+                a = self.attn.from_partials(pf_linear(h, self.qkv, MODE_PARTIAL), meta, kv, cos_sin)
+            else:
+                a = self.attn(F.linear(h, self.qkv), meta, kv, cos_sin)
+            o = pf_linear(a, self.o, MODE_PARTIAL) if "o" in PF_SET else F.linear(a, self.o)
             h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
             if self.moe:
                 return self.mlp(h), residual
-            act = pf_linear(h, self.gate_up, MODE_SILU)
-            return pf_linear(act, self.down, MODE_PARTIAL), residual
+            if "gate_up" in PF_SET:
+                act = pf_linear(h, self.gate_up, MODE_SILU)
+            else:
+                act = ops.silu_and_mul(F.linear(h, self.gate_up), interleave16=True)
+            if "down" in PF_SET:
+                return pf_linear(act, self.down, MODE_PARTIAL), residual
+            if splitk_prefill_ok(act, self.down):
+                return splitk_linear(act, self.down, linear_mod.SPLITK_PREFILL_S), residual
+            return F.linear(act, self.down), residual
         if self.fast_ok and T <= FAST_M_SLAB:
             # 16 < M <= 64: measured per shape on MI355X -- only the O projection
             # (N = H) is faster on the LDS-slab kernel; its split-K partials are

@@ -300,13 +300,17 @@ def mw_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, plan=N
 # barrier behind waves 0-3 (MFMA / load ping-pong per SIMD), stream-K option.
 # cfg -> (BM, m tiles per wave per phase): 0 (256, 2) 1 (192, 2) 2 (128, 2) 3 (256, 4)
 # 4 (192, 3) 5 (288, 3).
-PF_CFG_BM = {0: 256, 1: 192, 2: 128, 3: 256, 4: 192, 5: 288}
+PF_CFG_BM = {0: 256, 1: 192, 2: 128, 3: 256, 4: 192, 5: 288, 6: 288, 7: 256, 8: 192}
 PF_MIN_M = 65
-# per-CU cost of one 64-deep K tile (us) by tile height: max(LDS-DMA at ~55 GB/s per CU,
-# MFMA at ~1.45 PFLOP/s chip-wide); the planner's model, refined by measurement
-_PF_KT_US = {128: 0.89, 192: 1.12, 256: 1.50, 288: 1.69}
-_PF_DEFAULT_CFG = {128: 2, 192: 4, 256: 3, 288: 5}
-PF_SK_OVERHEAD = 1.06    # stream-K fixup (partial slots of the shared tiles) relative cost
+# The planner's cost model, fitted to bench/pf_gemm_bench.py at the 8B mixed-step
+# shapes (profiles/r5_pf_gemm.md): a workgroup costs PF_WG_US + its output bytes at
+# PF_WG_OUT_GBS (fp32 partials or bf16) + K tiles x the per-K-tile time of its cfg;
+# one workgroup per CU, so a grid of G costs ceil(G / CUs) of those.
+_PF_CFG_KT_US = {2: 1.07, 4: 1.34, 8: 1.29, 3: 1.75, 7: 1.51, 6: 1.77}   # cfg -> us per 64-deep K tile
+_PF_CFG_BM_ = {2: 128, 4: 192, 8: 192, 3: 256, 7: 256, 6: 288}
+PF_WG_US = 5.0
+PF_WG_OUT_GBS = 60.0
+PF_SK_OVERHEAD = 1.45    # stream-K (shared tiles: partial slots, pipeline restarts, lost W reuse)
 PF_SK_MAX_BM = 256       # the 288-row tile has no register room for the stream-K loop
 
 
@@ -328,30 +332,33 @@ def cu_count(device=None) -> int:
 
 def pf_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL, cus: int = 256):
     """(split_k, cfg, sk_grid) for gemm_pf, or None when the shape is unsupported.
-    Every tile height is priced with the per-K-tile model (_PF_KT_US): data-parallel
-    rounds x K tiles, or stream-K (bf16 / SiLU) K tiles spread over `cus` workgroups;
-    PARTIAL adds split-K (fp32 partials reduced by the consumer) up to one round."""
+    Every cfg of _PF_CFG_KT_US is priced with the model above: data-parallel (PARTIAL:
+    with split-K up to one round of workgroups; the fp32 partials' round trip through
+    the consumer is added), or stream-K over `cus` workgroups (bf16 / SiLU)."""
     if M < 1 or N % 256 or K % 64 or K < 64:
         return None
     nk = K // 64
     best = None
-    for bm, kt in _PF_KT_US.items():
+    for cfg, kt in _PF_CFG_KT_US.items():
+        bm = _PF_CFG_BM_[cfg]
         tiles = -(-M // bm) * (N // 256)
+        ob = bm * 256 * (4 if mode == MODE_PARTIAL else 2)      # output bytes per workgroup
+        wg = PF_WG_US + ob / (PF_WG_OUT_GBS * 1e3)
         cands = []
         if mode == MODE_PARTIAL:
             S = 1
             while tiles * (S + 1) <= cus and (S + 1) <= K // 256:
                 S += 1
-            # + the fp32 partials' round trip through the consumer (written here, read
-            # there; ~8 TB/s through the Infinity Cache)
-            cands.append(((-(-tiles * S // cus)) * (-(-nk // S)) * kt + S * M * N * 8 / 8e6, S, 0))
+            # + the partials' extra round trip through the consumer (~8 TB/s)
+            cands.append(((-(-tiles * S // cus)) * (wg + -(-nk // S) * kt) + (S - 1) * M * N * 8 / 8e6, S, 0))
         else:
-            cands.append((-(-tiles // cus) * nk * kt, 1, 0))
+            cands.append((-(-tiles // cus) * (wg + nk * kt), 1, 0))
             if bm <= PF_SK_MAX_BM and tiles % cus:
-                cands.append((tiles * nk / cus * kt * PF_SK_OVERHEAD, 1, cus))
-        for t, S, skg in cands:
+                cands.append((wg + tiles * nk / cus * kt * PF_SK_OVERHEAD, 1, cus))
+        for c in cands:
+            t, S_, skg = c[0], c[1], c[2]
             if best is None or t < best[0]:
-                best = (t, S, _PF_DEFAULT_CFG[bm], skg)
+                best = (t, S_, cfg, skg)
     return best[1], best[2], best[3]
 
 
@@ -394,7 +401,7 @@ def pf_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_BF16, plan=None
     k = kernels()
     wsp = tk = 0
     if skg:
-        bm = PF_CFG_BM[cfg % 8]
+        bm = PF_CFG_BM[cfg % 16]
         wt, tt = _PF_SK.get(x.device, skg, cfg, -(-M // bm) * (N // 256))
         wsp, tk = wt.data_ptr(), tt.data_ptr()
     if mode == MODE_PARTIAL:
