@@ -338,6 +338,13 @@ r5f)  # gemm_pf per-projection A/B in the headline (400 steps each, then the dri
   run c64_lib 300 env XGS_TUNE=pf=0 $B --steps 400 --warmup 40 "$@"
   run c64_gud2 300 env XGS_TUNE=pf=gate_up,down $B --steps 400 --warmup 40 "$@"
   run c64_gu2 300 env XGS_TUNE=pf=gate_up $B --steps 400 --warmup 40 "$@" ;;
+r5m)  # MoE with the combine in the w2 launch: tests, Mixtral c1 / c64 / TP2-EP2 rank, c1 profile; 8K prefill
+  pyt moe_tests 400 tests/test_kernels_gpu.py tests/test_engine_gpu.py tests/test_fused_decode_gpu.py -k "moe or mixtral or expert"
+  run mixtral_c1 300 $B --model mixtral-8x7b --concurrency 1 --steps 100 --warmup 10 "$@"
+  run mixtral_c64 300 $B --model mixtral-8x7b --steps 100 --warmup 20 "$@"
+  run mixtral_tp2_c64 300 $B --model mixtral-8x7b --tp-shard 2 --steps 100 --warmup 20 "$@"
+  bash bench/profile.sh "$o/prof_mixtral_c1" --model mixtral-8x7b --concurrency 1 "$@"
+  run prefill 300 python -u bench/prefill_bench.py ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;
