@@ -126,6 +126,7 @@ def preflight(st, world: int, tp: int, dev, eng) -> dict:
     import torch
     import torch.distributed as dist
     info = {"backend": None, "rccl_world": None, "tp_groups": None, "p2p_ok": None, "decode_ar": None,
+            "decode_ar_in_gemm": None,
             "custom_ar_selftest": None}
     if world > 1:
         info["backend"] = str(dist.get_backend())
@@ -148,6 +149,8 @@ def preflight(st, world: int, tp: int, dev, eng) -> dict:
         mine = torch.tensor([1 if ar is not None else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(mine, op=dist.ReduceOp.MIN)
         info["decode_ar"] = ar.protocol() if (ar is not None and int(mine.item()) == 1) else lib
+        # steps of <= 16 rows: the all-reduce inside the O / down GEMM launches
+        info["decode_ar_in_gemm"] = bool(ar is not None and ar.gemm_ar is not None and not ar.shared_device)
     return info
 
 
@@ -359,7 +362,7 @@ def main():
                        "sampling": ("greedy" if a.temperature <= 0 else
                                     f"temperature {a.temperature}, top_p {a.top_p}, top_k {a.top_k}")},
             "rccl_world": pre["rccl_world"], "tp_groups": pre["tp_groups"], "p2p_ok": pre["p2p_ok"],
-            "decode_ar": pre["decode_ar"],
+            "decode_ar": pre["decode_ar"], "decode_ar_in_gemm": pre["decode_ar_in_gemm"],
             "detail": {"initial_population": "steady-state (ages uniform on [0, output_len))",
                        "backend": pre["backend"], "custom_ar_selftest": pre["custom_ar_selftest"],
                        "prompt_gemm": prompt_gemm(eng),

@@ -345,6 +345,19 @@ r5m)  # MoE with the combine in the w2 launch: tests, Mixtral c1 / c64 / TP2-EP2
   run mixtral_tp2_c64 300 $B --model mixtral-8x7b --tp-shard 2 --steps 100 --warmup 20 "$@"
   bash bench/profile.sh "$o/prof_mixtral_c1" --model mixtral-8x7b --concurrency 1 "$@"
   run prefill 300 python -u bench/prefill_bench.py ;;
+r5t)  # TP decode: all-reduce inside the row-parallel GEMMs (GG_AR) -- loopback + self-test + TP engine
+      # tests, then one simulated 70B TP8 rank at batch 1 / 64 with it on / off, simulated links 0 / 8 us
+  pyt gar_tests 300 tests/test_gemm_ar_gpu.py
+  pyt ar_selftest 400 tests/test_custom_ar_gpu.py -k self_test
+  [ -n "$R5T_SKIP_TP" ] || pyt tp_tests 600 tests/test_tp_gpu.py
+  run tp8_c1 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 10 "$@"
+  run tp8_c1_off 300 env XGS_TUNE=gemm_ar=0 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 10 "$@"
+  run tp8_c1_ar8 300 env XGS_TUNE=sim_ar_us=8 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 10 "$@"
+  run tp8_c1_ar8_off 300 env "XGS_TUNE=sim_ar_us=8|gemm_ar=0" $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 10 "$@"
+  run tp8_c16 300 $B --model llama3-70b --tp-shard 8 --concurrency 16 --steps 100 --warmup 20 "$@"
+  run tp8_c16_off 300 env XGS_TUNE=gemm_ar=0 $B --model llama3-70b --tp-shard 8 --concurrency 16 --steps 100 --warmup 20 "$@"
+  run tp8_c64 300 $B --model llama3-70b --tp-shard 8 --steps 100 --warmup 20 "$@"
+  run tp8_c64_off 300 env XGS_TUNE=gemm_ar=0 $B --model llama3-70b --tp-shard 8 --steps 100 --warmup 20 "$@" ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;

@@ -40,10 +40,10 @@
 #include <stdint.h>
 
 #include "../kernels/common.h"
+#include "ll.h"
 
 namespace xgk {
 
-constexpr int CAR_MAX_RANKS = 8;
 constexpr int CAR_MAX_BLOCKS = 512;
 constexpr int CAR_CHUNK = 16384;    // bytes per block
 constexpr int CAR_THREADS = 256;    // 256 x 64 B = 16 KiB
@@ -315,52 +315,6 @@ __global__ void __launch_bounds__(128) car_resid_kernel(const float* __restrict_
 // block b, which Y sent only after it finished reading generation g-2 (the previous
 // user of parity p). The generation (not a toggling bit) in every line means a stale
 // line of generation g-2 never matches.
-struct LLLine {
-  uint32_t d0, f0, d1, f1;
-};
-
-__device__ __forceinline__ void ll_store(uint8_t* dst, uint32_t d0, uint32_t d1, uint32_t gen) {
-  u32x4_t v = {d0, gen, d1, gen};
-  __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t*>(dst));
-}
-
-// Poll `n` lines at src (stride 16 B) until every flag equals gen; returns the
-// payload words. Timeouts as car_wait (ctl[0] error counter, ctl[1] limit).
-template <int N>
-__device__ __forceinline__ bool ll_recv(const uint8_t* src, uint32_t gen, uint32_t* ctl, uint32_t (&d)[2 * N]) {
-  uint32_t got = 0;  // bit i: line i has arrived
-  uint64_t t0 = 0, limit = 0;
-  uint32_t spins = 0;
-  while (true) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      if (got & (1u << i)) continue;
-      // volatile: one real 16-B load per poll (a plain load may be hoisted out of the
-      // spin and served from a register forever)
-      typedef __attribute__((address_space(1))) const volatile u32x4_t gvec_t;
-      const u32x4_t v = *(gvec_t*)(src + 16 * i);
-      if (v[1] == gen && v[3] == gen) {
-        d[2 * i] = v[0];
-        d[2 * i + 1] = v[2];
-        got |= 1u << i;
-      }
-    }
-    if (got == (1u << N) - 1) return true;
-    if (spins == 0) {
-      if (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
-      limit = __hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      t0 = wall_clock64();
-    }
-    if ((++spins & 63) == 0) {
-      if (__hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
-      if (wall_clock64() - t0 > limit) {
-        atomicAdd(ctl, 1u);
-        return false;
-      }
-    }
-  }
-}
-
 // Fused residual all-reduce on the push protocol (same contract as car_resid_kernel:
 // rank-ordered sum, bit-identical on every rank). Block (t, chunk), 128 lanes x 8
 // elements; lane's 8 bf16 = 4 payload words = 2 lines per peer.
@@ -368,7 +322,11 @@ template <int SP>
 __global__ void __launch_bounds__(128) car_ll_resid_kernel(const float* __restrict__ part, int S, int T,
                                                            uint16_t* __restrict__ resid, float* __restrict__ ss_part,
                                                            int H, int64_t region_bytes, CarPtrs p, int rank, int world,
-                                                           uint32_t* __restrict__ gens, uint32_t* __restrict__ err) {
+                                                           uint32_t* __restrict__ gens, uint32_t* __restrict__ err,
+                                                           int loop) {
+  // loop (one-process --tp-shard simulation, comm.tp_allreduce_resid): every "peer"
+  // region is this rank's own, lines go to source slot r and are polled but not added;
+  // loop - 1 = a simulated link latency in wall-clock ticks
   __shared__ float red[2];
   const int t = blockIdx.x, chunk = blockIdx.y;
   const int b = t * gridDim.y + chunk;
@@ -393,11 +351,15 @@ __global__ void __launch_bounds__(128) car_ll_resid_kernel(const float* __restri
   const int64_t line_off = (gen & 1) * (region_bytes / 2) + (e / 4) * 16;
   for (int r = 0; r < world; ++r) {
     if (r == rank) continue;
-    uint8_t* dst = p.data[r] + line_off + static_cast<int64_t>(rank) * src_bytes;
+    uint8_t* dst = p.data[r] + line_off + static_cast<int64_t>(loop ? r : rank) * src_bytes;
     ll_store(dst, mine.x, mine.y, gen);
     ll_store(dst + 16, mine.z, mine.w, gen);
   }
   asm volatile("" ::: "memory");  // the pushes are issued before any poll
+  if (loop > 1) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < static_cast<uint64_t>(loop - 1)) __builtin_amdgcn_s_sleep(1);
+  }
   // 3. receive every peer's lines from my own region, sum in rank order
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   bool ok = true;
@@ -406,6 +368,7 @@ __global__ void __launch_bounds__(128) car_ll_resid_kernel(const float* __restri
     if (r != rank && ok) {
       uint32_t d[4];
       ok = ll_recv<2>(p.data[rank] + line_off + static_cast<int64_t>(r) * src_bytes, gen, err, d);
+      if (loop) continue;
       pv = make_uint4(d[0], d[1], d[2], d[3]);
     }
     acc8<uint16_t>(acc, pv);
@@ -476,7 +439,7 @@ int car_ll_max_bytes(int64_t region_bytes) {
 
 int custom_allreduce_resid_ll(const float* part, int S, int T, uint16_t* resid, float* ss_part, int H,
                               int64_t region_bytes, const uintptr_t* data_ptrs, int rank, int world, uint32_t* gens,
-                              uint32_t* err, hipStream_t st) {
+                              uint32_t* err, hipStream_t st, int loop) {
   if (world < 2 || world > CAR_MAX_RANKS || rank < 0 || rank >= world) return 1;
   if (T <= 0 || S <= 0 || H <= 0 || H % 1024) return 1;
   if (static_cast<int64_t>(T) * (H / 1024) > CAR_MAX_BLOCKS) return 1;
@@ -486,7 +449,7 @@ int custom_allreduce_resid_ll(const float* part, int S, int T, uint16_t* resid, 
   const dim3 g(T, H / 1024);
 #define XGK_CARLL(SPV)                                                                                           \
   hipLaunchKernelGGL((car_ll_resid_kernel<SPV>), g, dim3(128), 0, st, part, S, T, resid, ss_part, H, region_bytes, \
-                     p, rank, world, gens, err)
+                     p, rank, world, gens, err, loop)
   if (S == 1) XGK_CARLL(1);
   else if (S == 2) XGK_CARLL(2);
   else if (S == 4) XGK_CARLL(4);

@@ -32,10 +32,11 @@
 #include <cstdlib>
 
 #include "glds.h"
+#include "../comm/ll.h"
 
 namespace xgk {
 
-enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2, GG_RESID = 3, GG_MOE_RESID = 4 };
+enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2, GG_RESID = 3, GG_MOE_RESID = 4, GG_AR = 5 };
 
 // Fused-decode epilogue operands (all null / 0 for a plain GEMM).
 //   ss_in / ss_n / ss_stride: RMSNorm statistics of the input rows as ss_n
@@ -59,6 +60,29 @@ struct M64Epi {
   float* ss_out;
   int* counters;
   int krot = 0;  // set by m64g_launch (k_rotation): walk K chunks from a per-tile start
+  // GG_AR (TP decode, row-parallel O / down): GG_RESID with the tensor-parallel
+  // all-reduce inside the launch. The tile's last arriver sums its S slabs, rounds to
+  // bf16 (this rank's contribution, as in the unfused path) and pushes it to every
+  // peer as LL lines (comm/ll.h) at [parity][source rank][element / 4] of the peer's
+  // receive region, then polls its OWN region for the peers' lines of the same tile
+  // and adds all contributions in rank order to the residual (bit-identical on every
+  // rank), with the tile's statistics. Generation per column tile (ar_gens), so the
+  // pull-free double-buffering argument of the LL all-reduce holds per tile.
+  // ar_loop: one-process TP-shard simulation -- the "peers" are this rank's own region
+  // (lines pushed to source slot r, polled, not added): the traffic and the waits of
+  // an ar_world-rank group, the numerics of one rank; ar_loop - 1 = a simulated link
+  // latency in wall-clock ticks, waited once per tile between the pushes and the polls.
+  uint8_t* ar_data[CAR_MAX_RANKS] = {};
+  int64_t ar_region = 0;
+  int ar_rank = 0, ar_world = 0, ar_loop = 0;
+  uint32_t* ar_gens = nullptr;
+  uint32_t* ar_err = nullptr;  // [timeouts, wait limit] (the custom all-reduce's ctl)
+  // more than 64 column tiles: statistics per PAIR of tiles (the consumer combines
+  // <= 64 partial sums per row) -- each tile stores its row sums to ar_ss_tmp, the
+  // second of the pair to finish (ticket ar_pair[tile / 2]) adds the two in order
+  float* ar_ss_tmp = nullptr;
+  int* ar_pair = nullptr;
+  int ar_group = 1;
 };
 
 // GG_MOE_RESID (grouped w2 of the fused decode layer, TP = 1): the MoE combine inside
@@ -196,6 +220,104 @@ __device__ __forceinline__ void m64g_resid_tail(const float* __restrict__ part, 
                                                 const M64Epi& epi, int* flag, int bx) {
   if (S > 1 && !agent_ticket(epi.counters + bx, S - 1, flag)) return;
   m64g_resid_reduce<COLS, NTHR>(part, S, M, N, bx, epi);
+}
+
+// GG_AR tail (M64Epi::ar_*): tile ticket -> the last arriver reduces the S slabs,
+// exchanges the bf16 tile with the TP peers over LL lines and folds the sum into the
+// residual. One LL line = 4 columns of one row; the C4 = COLS / 4 lines of a row are
+// consecutive lanes of one wave (row statistics by xor butterfly; every lane runs
+// every butterfly).
+template <int COLS, int NTHR>
+__device__ __forceinline__ void m64g_ar_tail(const float* __restrict__ part, int S, int M, int N, const M64Epi& epi,
+                                             int* flag, int bx) {
+  if (S > 1) {
+    if (!agent_ticket(epi.counters + bx, S - 1, flag)) return;
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's own slab stores
+    __syncthreads();
+  }
+  constexpr int C4 = COLS / 4;
+  static_assert(64 % C4 == 0 && NTHR % C4 == 0, "row groups must not straddle waves");
+  const int tid = threadIdx.x;
+  const int n0 = bx * COLS;
+  const int64_t slab = static_cast<int64_t>(M) * N;
+  const uint32_t gen = epi.ar_gens[bx] + 1;
+  const int64_t src_bytes = epi.ar_region / (2 * CAR_MAX_RANKS);  // per (parity, source)
+  const int64_t par = static_cast<int64_t>(gen & 1) * (epi.ar_region / 2);
+  uint8_t* const own = epi.ar_data[epi.ar_rank];
+  bool ok = true;
+  for (int base = 0; base < M * C4; base += NTHR) {
+    const int idx = base + tid;
+    const bool act = idx < M * C4;
+    const int m = act ? idx / C4 : 0, c = idx % C4;
+    const int64_t e = static_cast<int64_t>(m) * N + n0 + 4 * c;  // element offset
+    float y[4] = {0.f, 0.f, 0.f, 0.f};
+    float sq = 0.f;
+    if (act) {
+      for (int s0 = 0; s0 < S; s0 += 4) {
+        float4 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const float4*>(part + min(s0 + j, S - 1) * slab + e);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float k = s0 + j < S ? 1.f : 0.f;
+          y[0] += k * v[j].x; y[1] += k * v[j].y; y[2] += k * v[j].z; y[3] += k * v[j].w;
+        }
+      }
+      const uint32_t w0 = pack2(y[0], y[1]), w1 = pack2(y[2], y[3]);  // this rank's bf16 contribution
+      const int64_t line = par + (e / 4) * 16;
+      for (int r = 0; r < epi.ar_world; ++r) {
+        if (r == epi.ar_rank) continue;
+        ll_store(epi.ar_data[r] + line + static_cast<int64_t>(epi.ar_loop ? r : epi.ar_rank) * src_bytes, w0, w1,
+                 gen);
+      }
+      asm volatile("" ::: "memory");  // every push is issued before the first poll
+      if (epi.ar_loop > 1) {  // loopback simulation of a link latency (ticks)
+        const uint64_t t0 = wall_clock64();
+        while (wall_clock64() - t0 < static_cast<uint64_t>(epi.ar_loop - 1)) __builtin_amdgcn_s_sleep(1);
+      }
+      uint32_t d[CAR_MAX_RANKS][2];
+      const uint32_t need = ((1u << epi.ar_world) - 1) & ~(1u << epi.ar_rank);
+      if (ok) ok = ll_recv_multi(own + line, src_bytes, need, gen, epi.ar_err, d);
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < epi.ar_world; ++r) {  // rank order: bit-identical on every rank
+        uint32_t d0 = w0, d1 = w1;
+        if (r != epi.ar_rank) {
+          if (epi.ar_loop || !ok) continue;  // loopback: polled, not added
+          d0 = d[r][0];
+          d1 = d[r][1];
+        }
+        acc[0] += __uint_as_float(d0 << 16);
+        acc[1] += __uint_as_float(d0 & 0xFFFF0000u);
+        acc[2] += __uint_as_float(d1 << 16);
+        acc[3] += __uint_as_float(d1 & 0xFFFF0000u);
+      }
+      uint2 rv = *reinterpret_cast<const uint2*>(epi.resid + e);
+      acc[0] += __uint_as_float(rv.x << 16);
+      acc[1] += __uint_as_float(rv.x & 0xFFFF0000u);
+      acc[2] += __uint_as_float(rv.y << 16);
+      acc[3] += __uint_as_float(rv.y & 0xFFFF0000u);
+      rv.x = pack2(acc[0], acc[1]);
+      rv.y = pack2(acc[2], acc[3]);
+      *reinterpret_cast<uint2*>(epi.resid + e) = rv;
+      const float a0 = __uint_as_float(rv.x << 16), a1 = __uint_as_float(rv.x & 0xFFFF0000u);
+      const float a2 = __uint_as_float(rv.y << 16), a3 = __uint_as_float(rv.y & 0xFFFF0000u);
+      sq = a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+    }
+#pragma unroll
+    for (int o = C4 / 2; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+    if (act && c == 0) {
+      if (epi.ar_group == 1) epi.ss_out[bx * M + m] = sq;
+      else st4_sc1(epi.ar_ss_tmp + bx * M + m, sq);
+    }
+  }
+  if (tid == 0) epi.ar_gens[bx] = gen;
+  if (epi.ar_group == 1) return;
+  // pair statistics: the later tile of the pair adds both row sums, in tile order
+  if (!agent_ticket(epi.ar_pair + bx / 2, 1, flag)) return;
+  const int p0 = bx & ~1;
+  for (int m = tid; m < M; m += NTHR)
+    epi.ss_out[(bx / 2) * M + m] = epi.ar_ss_tmp[p0 * M + m] + epi.ar_ss_tmp[(p0 + 1) * M + m];
 }
 
 // Split-K GG_SILU tail: every workgroup has stored its fp32 partial of the tile
@@ -464,7 +586,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
 
   // acc[nt][mt][r] = out[m = 16 mt + li][n = nbase + 16 nt + 4 g + r]
   const bool silu_split = NW == 2 && mode == GG_SILU && S > 1;
-  if (mode == GG_PARTIAL || mode == GG_RESID || silu_split) {
+  if (mode == GG_PARTIAL || mode == GG_RESID || mode == GG_AR || silu_split) {
     float* pp = part + static_cast<int64_t>(s) * M * N;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -479,6 +601,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
     }
     if (mode == GG_RESID)
       m64g_resid_tail<16 * NW * WV, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0), bx);
+    else if (mode == GG_AR)
+      m64g_ar_tail<16 * NW * WV, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0), bx);
     else if (silu_split)
       m64g_silu_tail<16 * NW * WV, 64 * WV>(part, S, M, N, out, epi.counters, reinterpret_cast<int*>(lds0), bx);
   } else if (mode == GG_BF16) {
@@ -934,15 +1058,28 @@ static int m64g_check(int M, int K, int N, const float* part, const uint16_t* ou
                       const M64Epi& epi) {
   if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 10) return 1;
   if (cfg >= 8 && M > 16) return 1;  // deep-ring configurations: one x tile only
-  if (mode < GG_BF16 || mode > GG_RESID) return 1;
+  if (mode < GG_BF16 || mode > GG_AR || mode == GG_MOE_RESID) return 1;
   const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
   if (K % kc || S > K / kc || N % cols) return 1;
   // split-K SiLU: fp32 slabs + one zeroed arrival ticket per column tile (m64g_silu_tail)
   if (mode == GG_SILU && (nw != 2 || (S > 1 && (part == nullptr || epi.counters == nullptr)))) return 1;
   if (mode == GG_BF16 && S != 1) return 1;
-  if ((mode == GG_PARTIAL || mode == GG_RESID) && part == nullptr) return 1;
+  if ((mode == GG_PARTIAL || mode == GG_RESID || mode == GG_AR) && part == nullptr) return 1;
   if ((mode == GG_BF16 || mode == GG_SILU) && out == nullptr) return 1;
-  if (mode == GG_RESID && (epi.resid == nullptr || epi.ss_out == nullptr || epi.counters == nullptr)) return 1;
+  if ((mode == GG_RESID || mode == GG_AR) && (epi.resid == nullptr || epi.ss_out == nullptr || epi.counters == nullptr))
+    return 1;
+  if (mode == GG_AR) {
+    if (epi.ar_world < 1 || epi.ar_world > CAR_MAX_RANKS || epi.ar_rank < 0 || epi.ar_rank >= epi.ar_world ||
+        epi.ar_gens == nullptr || epi.ar_err == nullptr || (N / cols) > 4096)
+      return 1;
+    if (epi.ar_group != 1 && (epi.ar_group != 2 || (N / cols) % 2 || epi.ar_ss_tmp == nullptr ||
+                              epi.ar_pair == nullptr))
+      return 1;
+    for (int r = 0; r < epi.ar_world; ++r)
+      if (epi.ar_data[r] == nullptr) return 1;
+    // every line of the [M, N] message fits a (parity, source) slice of the region
+    if (static_cast<int64_t>(M) * N * 4 > epi.ar_region / (2 * CAR_MAX_RANKS)) return 1;
+  }
   if (epi.ss_in != nullptr && (epi.ss_n < 1 || epi.ss_n > 64 || epi.ss_stride < M)) return 1;
   return 0;
 }
@@ -960,7 +1097,7 @@ static void m64g_launch(const uint16_t* x, int M, int K, const uint16_t* w, int 
 int gemm_m64g(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
               int nw, int cfg, hipStream_t st) {
   const M64Epi epi{nullptr, 0, 0, 0.f, nullptr, nullptr, nullptr};
-  if (mode == GG_RESID || m64g_check(M, K, N, part, out, S, mode, nw, cfg, epi)) return 1;
+  if (mode == GG_RESID || mode == GG_AR || m64g_check(M, K, N, part, out, S, mode, nw, cfg, epi)) return 1;
   m64g_launch(x, M, K, w, N, part, out, S, mode, nw, cfg, epi, st);
   return 0;
 }
@@ -973,6 +1110,29 @@ int gemm_m64g_ex(const uint16_t* x, int M, int K, const uint16_t* w, int N, floa
   const M64Epi epi{ss_in, ss_n, ss_stride, eps, resid, ss_out, counters};
   if (m64g_check(M, K, N, part, out, S, mode, nw, cfg, epi)) return 1;
   m64g_launch(x, M, K, w, N, part, out, S, mode, nw, cfg, epi, st);
+  return 0;
+}
+
+// Row-parallel GEMM with the TP all-reduce + residual + statistics in the launch
+// (GG_AR): data[r] = rank r's LL receive region (region bytes each; loop: all this
+// rank's own), gens one word per column tile, err = the custom all-reduce's ctl.
+int gemm_m64g_ar(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, int S, int nw, int cfg,
+                 uint16_t* resid, float* ss_out, int* counters, uint8_t* const* data, int64_t region, int rank,
+                 int world, int loop, uint32_t* gens, uint32_t* err, float* ss_tmp, int* pair, int group,
+                 hipStream_t st) {
+  M64Epi epi{nullptr, 0, 0, 0.f, resid, ss_out, counters};
+  epi.ar_ss_tmp = ss_tmp;
+  epi.ar_pair = pair;
+  epi.ar_group = group;
+  for (int r = 0; r < world && r < CAR_MAX_RANKS; ++r) epi.ar_data[r] = data[r];
+  epi.ar_region = region;
+  epi.ar_rank = rank;
+  epi.ar_world = world;
+  epi.ar_loop = loop;
+  epi.ar_gens = gens;
+  epi.ar_err = err;
+  if (m64g_check(M, K, N, part, nullptr, S, GG_AR, nw, cfg, epi)) return 1;
+  m64g_launch(x, M, K, w, N, part, nullptr, S, GG_AR, nw, cfg, epi, st);
   return 0;
 }
 

@@ -24,6 +24,8 @@ int gemm_m64g(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*
 int gemm_m64g_ex(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, const float*,
                  int, int, float, uint16_t*, float*, int*, hipStream_t);
 int gemm_mw(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, hipStream_t);
+int gemm_m64g_ar(const uint16_t*, int, int, const uint16_t*, int, float*, int, int, int, uint16_t*, float*, int*,
+                 uint8_t* const*, int64_t, int, int, int, uint32_t*, uint32_t*, float*, int*, int, hipStream_t);
 int gemm_pf(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, float*, int*,
             hipStream_t);
 int pf_sk_slot_floats(int);
@@ -86,7 +88,7 @@ int custom_allgather_lastdim(const void*, void*, int64_t, int64_t, int64_t, cons
 int custom_allreduce_ll(const void*, void*, int64_t, int64_t, const uintptr_t*, int, int, uint32_t*, uint32_t*,
                         hipStream_t);
 int custom_allreduce_resid_ll(const float*, int, int, uint16_t*, float*, int, int64_t, const uintptr_t*, int, int,
-                              uint32_t*, uint32_t*, hipStream_t);
+                              uint32_t*, uint32_t*, hipStream_t, int);
 int car_ll_max_bytes(int64_t);
 int car_max_blocks();
 int car_wallclock_khz();
@@ -278,6 +280,21 @@ PYBIND11_MODULE(_kernels, m) {
                             P<float>(ss_out), P<int>(counters), S(st)),
           "gemm_m64g_ex");
   });
+  // TP row-parallel GEMM with the all-reduce + residual + statistics in the launch
+  // (gemm_m64g.hip GG_AR); data = each rank's LL receive region (loop: this rank's own)
+  m.def("gemm_m64g_ar", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, int splits, int nw,
+                           int cfg, uintptr_t resid, uintptr_t ss_out, uintptr_t counters, std::vector<uintptr_t> data,
+                           int64_t region, int rank, int world, int loop, uintptr_t gens, uintptr_t err,
+                           uintptr_t ss_tmp, uintptr_t pair, int group, uintptr_t st) {
+    if (static_cast<int>(data.size()) != world || world < 1 || world > 8)
+      throw std::invalid_argument("gemm_m64g_ar: one region pointer per rank (<= 8)");
+    uint8_t* d[8] = {};
+    for (int r = 0; r < world; ++r) d[r] = reinterpret_cast<uint8_t*>(data[r]);
+    check(xgk::gemm_m64g_ar(P<const uint16_t>(x), M, K, P<const uint16_t>(w), N, P<float>(part), splits, nw, cfg,
+                            P<uint16_t>(resid), P<float>(ss_out), P<int>(counters), d, region, rank, world, loop,
+                            P<uint32_t>(gens), P<uint32_t>(err), P<float>(ss_tmp), P<int>(pair), group, S(st)),
+          "gemm_m64g_ar");
+  });
   m.def("add_partials_resid", [](uintptr_t part, int S_, int T, uintptr_t res, uintptr_t ss_part, int H,
                                  uintptr_t st, uint64_t sim_ticks) {
     if (H % 1024) throw std::invalid_argument("add_partials_resid: H % 1024 != 0");
@@ -449,12 +466,14 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("custom_allreduce_resid_ll", [](uintptr_t part, int S_, int T, uintptr_t resid, uintptr_t ss_part, int H,
                                         int64_t region, std::vector<uintptr_t> data, int rank, uintptr_t gens,
-                                        uintptr_t err, uintptr_t st) {
+                                        uintptr_t err, uintptr_t st, int loop) {
     check(xgk::custom_allreduce_resid_ll(P<const float>(part), S_, T, P<uint16_t>(resid), P<float>(ss_part), H,
                                          region, data.data(), rank, static_cast<int>(data.size()), P<uint32_t>(gens),
-                                         P<uint32_t>(err), S(st)),
+                                         P<uint32_t>(err), S(st), loop),
           "custom_allreduce_resid_ll");
-  });
+  }, py::arg("part"), py::arg("S"), py::arg("T"), py::arg("resid"), py::arg("ss_part"), py::arg("H"),
+     py::arg("region"), py::arg("data"), py::arg("rank"), py::arg("gens"), py::arg("err"), py::arg("st"),
+     py::arg("loop") = 0);
   m.def("custom_allreduce_resid", [](uintptr_t part, int S_, int T, uintptr_t resid, uintptr_t ss_part, int H,
                                      int64_t slot_bytes, std::vector<uintptr_t> data, std::vector<uintptr_t> sig,
                                      int rank, uintptr_t gens, uintptr_t err, uintptr_t st) {

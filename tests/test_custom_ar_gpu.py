@@ -281,6 +281,7 @@ def test_custom_allreduce_self_test(world, ll_max):
     for rank, res, proto, tmo in _run(_selftest_worker, world, ll_max):
         assert isinstance(res, dict), res
         assert res["pull"] and res["pull_resid"], res
+        assert res["gemm_ar"], res  # the all-reduce inside the row-parallel GEMM launch
         if ll_max == 0:
             assert res["ll"] is None and proto == "pull"
         else:

@@ -35,7 +35,8 @@ from ..parallel import comm
 from ..parallel.state import get_state
 from ..ops import linear as linear_mod
 from ..ops.linear import (MODE_PARTIAL, MODE_SILU, MW_MAX_M, W8_MAX_M, W8_MIN_ELEMS, ResidWorkspace, RowStats,
-                          lm_head_linear, m64_linear, m64_norm_linear, m64_plan, m64_resid_linear,
+                          lm_head_linear, m64_ar_resid_linear, m64_linear, m64_norm_linear, m64_plan,
+                          m64_resid_linear,
                           mw_linear, mw_plan, pf_linear, pf_plan, pick_split,
                           quantize_fp8, skinny_linear, splitk_linear, splitk_prefill_ok, w8_linear, w8_plan)
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
@@ -469,7 +470,7 @@ class LlamaLayer(nn.Module):
         eps = self.cfg.norm_eps
         if self.tp > 1:
             po = m64_linear(a, self.o, MODE_PARTIAL)
-            comm.tp_allreduce_resid(po.part, resid, ws.ss[site])
+            comm.tp_allreduce_resid(po.part, resid, ws.ss[site], self.tp)
         else:
             m64_resid_linear(a, self.o, resid, ws, site, eps)  # its statistics go unused: the router renorms
         # one token (batch 1): the router launch also writes the expert layout
@@ -478,7 +479,7 @@ class LlamaLayer(nn.Module):
         ss = ws.ss[site + 1]
         if self.tp > 1:
             part = ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, out_f32=True, layout=layout)
-            comm.tp_allreduce_resid(part.unsqueeze(0), resid, ss)
+            comm.tp_allreduce_resid(part.unsqueeze(0), resid, ss, self.tp)
         else:
             return RowStats(ss, ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, resid=resid, ss=ss,
                                               layout=layout, counters=ws.counters[site + 1]), T)
@@ -490,12 +491,18 @@ class LlamaLayer(nn.Module):
         SiLU-gate) -> down GEMM partials -> all-reduce + residual + statistics."""
         T, H = resid.shape
         eps = self.cfg.norm_eps
+        ar = comm.gemm_ar_args(self.tp, T, H, resid.device)
+        if ar is not None:
+            # the all-reduce inside the O / down launches (gemm_m64g GG_AR): 2 launches fewer
+            st = m64_ar_resid_linear(a, self.o, resid, ws, site, ar)
+            act = m64_norm_linear(resid, self.gate_up, MODE_SILU, st, eps)
+            return m64_ar_resid_linear(act, self.down, resid, ws, site + 1, ar)
         po = m64_linear(a, self.o, MODE_PARTIAL)
-        comm.tp_allreduce_resid(po.part, resid, ws.ss[site])
+        comm.tp_allreduce_resid(po.part, resid, ws.ss[site], self.tp)
         st = RowStats(ws.ss[site], H // 1024, T)
         act = m64_norm_linear(resid, self.gate_up, MODE_SILU, st, eps)
         pd = m64_linear(act, self.down, MODE_PARTIAL)
-        comm.tp_allreduce_resid(pd.part, resid, ws.ss[site + 1])
+        comm.tp_allreduce_resid(pd.part, resid, ws.ss[site + 1], self.tp)
         return RowStats(ws.ss[site + 1], H // 1024, T)
 
 

@@ -476,6 +476,10 @@ class ResidWorkspace:
         # arrival tickets (GG_RESID: one word per tile): zero here, and every launch
         # re-arms the words it used
         self.counters = torch.zeros(n_sites, 2 * self.MAX_TILES, dtype=torch.int32, device=device)
+        # GG_AR (TP decode, all-reduce in the GEMM launch): tile-pair statistics tickets
+        # and per-tile row sums for grids of more than MAX_TILES column tiles
+        self.ar_pair = torch.zeros(self.MAX_TILES, dtype=torch.int32, device=device)
+        self.ar_ss_tmp = torch.zeros(2 * self.MAX_TILES * self.IN_LAUNCH_MAX_M, dtype=torch.float32, device=device)
 
 
 # Prefill-sized down projections (K = 3.5 N) have too few output tiles for the chip at
@@ -577,6 +581,33 @@ def m64_resid_linear(x, w: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace
     k.gemm_m64g(xp, M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, nw, cfg, stream_ptr())
     k.add_partials_resid(part.data_ptr(), S, M, resid.data_ptr(), ss.data_ptr(), N, stream_ptr())
     return RowStats(ss, N // 1024, M)  # one partial sum per 1024-column chunk
+
+
+def m64_ar_resid_linear(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace, site: int,
+                        ar) -> RowStats:
+    """TP row-parallel projection of the fused decode layer in ONE launch: resid +=
+    all-reduce over the TP group of x . w^T (this rank's K shard), with the new
+    residual's statistics (gemm_m64g GG_AR: the tile's last arriver pushes its bf16
+    contribution to every peer as LL lines and folds the peers' lines in rank order).
+    `ar` = comm.GemmArArgs (the custom all-reduce's GEMM region, or the one-process
+    loopback of a --tp-shard simulation). x: bf16 [M, K], M <= 64."""
+    M, K = x.shape
+    N = w.shape[0]
+    plan = m64_plan(M, N, K, MODE_PARTIAL)
+    if plan is None or M > ws.IN_LAUNCH_MAX_M or tuple(resid.shape) != (M, N):
+        raise ValueError(f"gemm_m64g_ar: unsupported shape M={M} N={N} K={K}")
+    nw, S, cfg = plan
+    ntiles = N // (16 * nw * M64G_CFGS[cfg][0])
+    group = 1 if ntiles <= ws.MAX_TILES else 2
+    if ntiles > 2 * ws.MAX_TILES:
+        raise ValueError(f"gemm_m64g_ar: {ntiles} column tiles")
+    part = torch.empty(S, M, N, dtype=torch.float32, device=resid.device)
+    ss = ws.ss[site]
+    kernels().gemm_m64g_ar(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), S, nw, cfg, resid.data_ptr(),
+                           ss.data_ptr(), ws.counters[site].data_ptr(), ar.data, ar.region, ar.rank, ar.world,
+                           ar.loop, ar.gens.data_ptr(), ar.err.data_ptr(), ws.ar_ss_tmp.data_ptr(),
+                           ws.ar_pair.data_ptr(), group, stream_ptr())
+    return RowStats(ss, ntiles // group, M)
 
 
 def interleave_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:

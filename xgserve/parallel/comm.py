@@ -57,6 +57,13 @@ def resid_allreduce_ok(T: int, H: int) -> bool:
 # XGS_TUNE sim_ar_us > 0 makes the local stand-in wait that long (the peer round trip of the
 # one-shot xGMI all-reduce), so the simulation exposes collective latency
 # (profiles/r3_tp_ar_overlap.md). A measurement knob.
+# TP decode: the row-parallel O / down GEMMs all-reduce inside their own launch, for
+# steps of at most GEMM_AR_MAX_T rows. Above that one tail workgroup per column tile
+# has too many lines to push and poll; the separate LL kernel spreads them over
+# T x H / 1024 workgroups. One simulated 70B TP8 rank (profiles/r5_gemm_ar.md):
+# batch 1 6.14 vs 6.30 ms, 16 rows 7.91 vs 7.74, 64 rows 13.6 vs 11.0.
+GEMM_AR = __import__("xgserve.tune", fromlist=["get_bool"]).get_bool("gemm_ar", True)
+GEMM_AR_MAX_T = 4
 _SIM_AR_TICKS = int(__import__("xgserve.tune", fromlist=["get_float"]).get_float("sim_ar_us", 0.0) * 100)  # 100 MHz
 
 
@@ -65,20 +72,79 @@ def sim_ar_ticks() -> int:
     return _SIM_AR_TICKS if get_state().tp_size == 1 else 0
 
 
-def tp_allreduce_resid(part: torch.Tensor, resid: torch.Tensor, ss: torch.Tensor) -> None:
+def tp_allreduce_resid(part: torch.Tensor, resid: torch.Tensor, ss: torch.Tensor, sim_world: int = 1) -> None:
     """Row-parallel projection epilogue of the fused decode layer:
     resid += all-reduce(sum_s part[s]) in place (bf16), ss[chunk * T + t] <- the new
     residual's sum of squares per 1024 columns. `part` is this rank's fp32 split-K
-    partials [S, T, H]. One launch on the custom all-reduce; a simulated TP shard
-    (single-rank process) reduces locally."""
+    partials [S, T, H]. One launch on the custom all-reduce. A simulated TP shard
+    (single-rank process, layers built for sim_world > 1 ranks) runs the same LL
+    kernel in its loopback form (pushes / polls of sim_world ranks through its own
+    region, numerics of one rank; XGS_TUNE sim_ar_us adds a link latency)."""
     from ..ops._native import kernels, stream_ptr
     S, T, H = part.shape
     s = get_state()
+    if s.tp_size == 1 and sim_world > 1 and H % 1024 == 0 and T * (H // 1024) <= 512 and T * H * 4 <= (32 << 20) // 16:
+        a = _loopback_args(sim_world, part.device)
+        kernels().custom_allreduce_resid_ll(part.data_ptr(), S, T, resid.data_ptr(), ss.data_ptr(), H, a.region,
+                                            a.data2, 0, a.gens2.data_ptr(), a.err.data_ptr(), stream_ptr(), a.loop)
+        return
     if s.tp_size == 1:
         kernels().add_partials_resid(part.data_ptr(), S, T, resid.data_ptr(), ss.data_ptr(), H, stream_ptr(),
                                      _SIM_AR_TICKS)
         return
     _CUSTOM_AR.all_reduce_resid(part, resid, ss)
+
+
+class GemmArArgs:
+    """Operands of the all-reduce inside a row-parallel GEMM launch (gemm_m64g GG_AR):
+    each rank's LL receive region, this rank, the group size, one generation word per
+    column tile and the timeout control words. loop = 1: a one-process --tp-shard
+    simulation whose "peers" are its own region (the waits and traffic of `world`
+    ranks, the numerics of one)."""
+
+    REGION = 32 << 20
+
+    def __init__(self, data, region, rank, world, loop, gens, err):
+        self.data, self.region, self.rank, self.world, self.loop = data, region, rank, world, loop
+        self.gens, self.err = gens, err
+
+
+_LOOPBACK = {}
+
+
+def _loopback_args(world: int, device) -> GemmArArgs:
+    key = (str(device), world)
+    a = _LOOPBACK.get(key)
+    if a is None:
+        from ..ops._native import kernels
+        buf = torch.zeros(GemmArArgs.REGION, dtype=torch.uint8, device=device)
+        gens = torch.zeros(4096, dtype=torch.int32, device=device)
+        # [timeouts, wait limit in wall-clock ticks]: 20 s
+        khz = max(1, int(kernels().car_wallclock_khz()) or 100_000)
+        err = torch.tensor([0, min(2**31 - 1, 20 * khz * 1000)], dtype=torch.int32, device=device)
+        # loop = 1 + the simulated link latency (XGS_TUNE sim_ar_us) in wall-clock ticks
+        a = GemmArArgs([buf.data_ptr()] * world, GemmArArgs.REGION, 0, world, 1 + _SIM_AR_TICKS, gens, err)
+        a._buf = buf
+        # the unfused path's LL residual all-reduce: its own region and block generations
+        a._buf2 = torch.zeros(GemmArArgs.REGION, dtype=torch.uint8, device=device)
+        a.gens2 = torch.zeros(1024, dtype=torch.int32, device=device)
+        a.data2 = [a._buf2.data_ptr()] * world
+        _LOOPBACK[key] = a
+    return a
+
+
+def gemm_ar_args(layer_tp: int, T: int, H: int, device) -> Optional[GemmArArgs]:
+    """The GG_AR operands for a decode step of T rows, or None (the GEMM + all-reduce
+    launches then run as before): the verified custom all-reduce of a real TP group,
+    or the loopback of a simulated shard (tp_size 1, layer built for layer_tp ranks)."""
+    if not GEMM_AR or T > GEMM_AR_MAX_T or T * H * 4 > GemmArArgs.REGION // 16:
+        return None
+    s = get_state()
+    if s.tp_size == 1:
+        return _loopback_args(layer_tp, device) if layer_tp > 1 else None
+    if _CUSTOM_AR is None or not getattr(_CUSTOM_AR, "gemm_ar", None) or _CUSTOM_AR.shared_device:
+        return None
+    return _CUSTOM_AR.gemm_ar
 
 
 class _Done:

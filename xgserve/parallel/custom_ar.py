@@ -77,6 +77,7 @@ class CustomAllReduce:
     # push-protocol receive regions: [2 parities][8 sources][2 x payload] per rank
     RESID_LL_REGION = 32 << 20   # fused residual: T * H bf16 <= 1 MiB of payload
     LL_REGION = 8 << 20          # plain all-reduce: <= 256 KiB of payload
+    GEMM_LL_REGION = 32 << 20    # all-reduce inside the row-parallel GEMM (gemm_m64g GG_AR)
     # peer-wait limits: while serving, and around warmup / graph capture
     SERVE_TIMEOUT_S = 2.0
     WARMUP_TIMEOUT_S = 20.0  # (the 32-bit tick word caps the limit at ~21 s at 100 MHz)
@@ -101,18 +102,26 @@ class CustomAllReduce:
         # phase 1 (local): allocate + export; every rank reports success so a
         # failure anywhere disables the path everywhere instead of hanging peers
         mine = None
+        props = torch.cuda.get_device_properties(device)
+        self.device_id = (props.pci_domain_id, props.pci_bus_id, props.pci_device_id, str(props.uuid))
         try:
             # [one-shot 2 x slot | two-shot 2 x slot2 | resid 2 x RESID_SLOT | gather 2 x GATHER_SLOT
             #  | resid LL region | LL region] and [one-shot | two-shot phase 0 | phase 1 | resid |
             # gather] signals
             self.data = k.car_alloc_uncached(2 * self.slot + 2 * self.slot2 + 2 * self.RESID_SLOT
-                                             + 2 * self.GATHER_SLOT + self.RESID_LL_REGION + self.LL_REGION)
+                                             + 2 * self.GATHER_SLOT + self.RESID_LL_REGION + self.LL_REGION
+                                             + self.GEMM_LL_REGION)
             self.sig = k.car_alloc_uncached(5 * nsig)
             mine = (k.car_ipc_handle(self.data), k.car_ipc_handle(self.sig))
         except RuntimeError as e:
             log.warning("custom all-reduce: local setup failed: %s", e)
         handles: List = [None] * world
-        dist.all_gather_object(handles, mine, group=cpu_group)
+        dist.all_gather_object(handles, (mine, self.device_id), group=cpu_group)
+        # ranks sharing one GPU (the single-GPU test boxes): kernels that spin on peers
+        # must stay small enough to be co-resident with every peer's (the GEMM-fused
+        # all-reduce is not: comm.gemm_ar_args keeps the separate launches there)
+        self.shared_device = len({h[1] for h in handles}) < world
+        handles = [h[0] for h in handles]
         if any(h is None for h in handles):
             self.close()
             raise RuntimeError("custom all-reduce setup failed on some rank")
@@ -148,6 +157,8 @@ class CustomAllReduce:
         ll0 = 2 * self.slot + 2 * self.slot2 + 2 * self.RESID_SLOT + 2 * self.GATHER_SLOT
         self.data_ptrs_rll = [d + ll0 for d in self.data_ptrs]
         self.data_ptrs_ll = [d + ll0 + self.RESID_LL_REGION for d in self.data_ptrs]
+        self.data_ptrs_gll = [d + ll0 + self.RESID_LL_REGION + self.LL_REGION for d in self.data_ptrs]
+        self.gens_gll = torch.zeros(4096, dtype=torch.int32, device=device)
         self.gens_rll = torch.zeros(self.max_blocks + 1, dtype=torch.int32, device=device)
         self.gens_ll = torch.zeros(self.max_blocks + 1, dtype=torch.int32, device=device)
         import os
@@ -170,6 +181,12 @@ class CustomAllReduce:
         self.timeout_s = 0.0
         self.set_timeout(self.SERVE_TIMEOUT_S)
         self.verified = None  # self_test() outcome
+        # operands of the all-reduce inside the row-parallel GEMMs (comm.gemm_ar_args);
+        # None until self_test() has verified it against RCCL
+        from .comm import GemmArArgs
+        self._gemm_ar = GemmArArgs(self.data_ptrs_gll, self.GEMM_LL_REGION, rank, world, 0, self.gens_gll,
+                                   self.ctl)
+        self.gemm_ar = None
         log.info("custom all-reduce ready: rank %d/%d, one-shot <= %d KiB, two-shot <= %d MiB", rank, world,
                  min(self.slot, self.two_shot_min) >> 10, self.slot2 >> 20)
 
@@ -238,11 +255,11 @@ class CustomAllReduce:
     def self_test(self, group, cpu_group) -> dict:
         """Run every protocol this instance would use against RCCL on the real links
         (module docstring, "First contact"); switch off the ones that disagree on any
-        rank. Returns {"ll", "ll_resid", "pull", "pull_resid", "two_shot"} -> bool
+        rank. Returns {"ll", "ll_resid", "pull", "pull_resid", "two_shot", "gemm_ar"} -> bool
         (None: protocol not in use)."""
         dev = self.device
         g = torch.Generator(device=dev).manual_seed(4321 + self.rank)
-        res = {"ll": None, "ll_resid": None, "pull": None, "pull_resid": None, "two_shot": None}
+        res = {"ll": None, "ll_resid": None, "pull": None, "pull_resid": None, "two_shot": None, "gemm_ar": None}
 
         def close_enough(got: torch.Tensor, ref: torch.Tensor) -> bool:
             return bool(torch.isfinite(got).all()) and float((got.float() - ref).abs().max()) <= \
@@ -281,8 +298,34 @@ class CustomAllReduce:
             ss_ref = (r.float().view(T, H // 1024, 1024) ** 2).sum(-1).t().reshape(-1)
             return close_enough(r, ref) and bool(torch.allclose(ss, ss_ref, rtol=2e-2, atol=1e-2))
 
+        def gemm_ar() -> bool:
+            from ..ops.linear import ResidWorkspace, m64_ar_resid_linear
+            ok_all = True
+            for T, N, K in ((8, 4096, 1024), (1, 8192, 1024)):
+                x = (torch.randn(T, K, generator=g, device=dev) * 0.5).bfloat16()
+                w = (torch.randn(N, K, generator=g, device=dev) * 0.05).bfloat16()
+                base = torch.randn(T, N, generator=torch.Generator(device=dev).manual_seed(77), device=dev).bfloat16()
+                mine = (x.float() @ w.float().t()).bfloat16().float()
+                ref = mine.clone()
+                dist.all_reduce(ref, group=group)
+                ref = base.float() + ref
+                ws = ResidWorkspace(1, 64, N, dev)
+                for _ in range(2):  # a second launch on the advanced generations
+                    r = base.clone()
+                    st = m64_ar_resid_linear(x, w, r, ws, 0, self._gemm_ar)
+                    torch.cuda.synchronize(dev)
+                    n = st.n
+                    ss_ref = (r.float().view(T, n, N // n) ** 2).sum(-1).t().reshape(-1)
+                    ok_all = ok_all and close_enough(r, ref) and bool(
+                        torch.allclose(st.ss[: n * T], ss_ref, rtol=2e-2, atol=1e-2))
+            return ok_all
+
         checks = {"pull": lambda: plain(16 << 10, False) and plain(min(self.slot, 256 << 10), False),
                   "pull_resid": lambda: resid(False)}
+        # (ranks sharing one GPU never use it: a GEMM-sized grid spinning on its peers
+        # need not be co-resident with theirs there -- see shared_device)
+        if not self.shared_device or self.world <= 4:
+            checks["gemm_ar"] = gemm_ar
         if self.ll_max > 0:
             checks["ll"] = lambda: plain(min(self.ll_max, 16 << 10), True) and plain(self.ll_max, True)
         if self.resid_ll:
@@ -308,6 +351,10 @@ class CustomAllReduce:
             self.resid_ll = False
         if res["two_shot"] is False:
             self.two_shot_min = self.slot2 + 1  # one-shot up to its slot, RCCL above
+        # the all-reduce inside the row-parallel GEMMs only once it agreed with RCCL
+        self.gemm_ar = self._gemm_ar if res["gemm_ar"] else None
+        if res["gemm_ar"] is False:
+            log.warning("custom all-reduce: the GEMM-fused all-reduce disagreed with RCCL; separate launches")
         self.verified = res
         return res
 

@@ -18,6 +18,7 @@ Keys (default in brackets; every default is the production setting):
   resid_inlaunch_kb [32]   in-launch residual reduce bound of the fused decode GEMMs
   decode_depth [2]         decode attention K/V register pipeline depth
   decode_max_splits [16]   split-K cap of decode attention
+  gemm_ar [1]              TP decode: all-reduce inside the row-parallel O / down GEMM launches
   ar_ll_max [262144]       push (LL) all-reduce up to this many bytes (0: pull kernels)
   sim_ar_us [0]            --tp-shard simulation: stand-in all-reduce latency
   tp_overlap_chunks [2]    TP prefill: all-reduces pipelined over this many chunks
@@ -30,7 +31,7 @@ from __future__ import annotations
 import os
 from typing import Dict
 
-KEYS = {"fused_decode", "async_sched", "early_release", "spin_wait", "pf", "pf_m", "krot", "m64_plans", "mw_plans",
+KEYS = {"fused_decode", "async_sched", "early_release", "spin_wait", "pf", "pf_m", "gemm_ar", "krot", "m64_plans", "mw_plans",
         "mw_max_tokens", "resid_inlaunch_kb", "decode_depth", "decode_max_splits", "ar_ll_max", "sim_ar_us",
         "tp_overlap_chunks", "tp_overlap_min_tokens", "ep_exact_min_pairs"}
 
