@@ -354,10 +354,10 @@ r5t)  # TP decode: all-reduce inside the row-parallel GEMMs (GG_AR) -- loopback 
   run tp8_c1_off 300 env XGS_TUNE=gemm_ar=0 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 10 "$@"
   run tp8_c1_ar8 300 env XGS_TUNE=sim_ar_us=8 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 10 "$@"
   run tp8_c1_ar8_off 300 env "XGS_TUNE=sim_ar_us=8|gemm_ar=0" $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 10 "$@"
-  run tp8_c16 300 $B --model llama3-70b --tp-shard 8 --concurrency 16 --steps 100 --warmup 20 "$@"
-  run tp8_c16_off 300 env XGS_TUNE=gemm_ar=0 $B --model llama3-70b --tp-shard 8 --concurrency 16 --steps 100 --warmup 20 "$@"
+  run tp8_c4 300 $B --model llama3-70b --tp-shard 8 --concurrency 4 --steps 100 --warmup 20 "$@"
+  run tp8_c4_off 300 env XGS_TUNE=gemm_ar=0 $B --model llama3-70b --tp-shard 8 --concurrency 4 --steps 100 --warmup 20 "$@"
   run tp8_c64 300 $B --model llama3-70b --tp-shard 8 --steps 100 --warmup 20 "$@"
-  run tp8_c64_off 300 env XGS_TUNE=gemm_ar=0 $B --model llama3-70b --tp-shard 8 --steps 100 --warmup 20 "$@" ;;
+  run c64 300 $B --steps 400 --warmup 40 ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;

@@ -31,6 +31,8 @@
 //     stream instead of extending the tail.
 #include <cstdlib>
 
+#include <cstddef>
+
 #include "glds.h"
 #include "../comm/ll.h"
 
@@ -60,29 +62,34 @@ struct M64Epi {
   float* ss_out;
   int* counters;
   int krot = 0;  // set by m64g_launch (k_rotation): walk K chunks from a per-tile start
-  // GG_AR (TP decode, row-parallel O / down): GG_RESID with the tensor-parallel
-  // all-reduce inside the launch. The tile's last arriver sums its S slabs, rounds to
-  // bf16 (this rank's contribution, as in the unfused path) and pushes it to every
-  // peer as LL lines (comm/ll.h) at [parity][source rank][element / 4] of the peer's
-  // receive region, then polls its OWN region for the peers' lines of the same tile
-  // and adds all contributions in rank order to the residual (bit-identical on every
-  // rank), with the tile's statistics. Generation per column tile (ar_gens), so the
-  // pull-free double-buffering argument of the LL all-reduce holds per tile.
-  // ar_loop: one-process TP-shard simulation -- the "peers" are this rank's own region
-  // (lines pushed to source slot r, polled, not added): the traffic and the waits of
-  // an ar_world-rank group, the numerics of one rank; ar_loop - 1 = a simulated link
-  // latency in wall-clock ticks, waited once per tile between the pushes and the polls.
-  uint8_t* ar_data[CAR_MAX_RANKS] = {};
-  int64_t ar_region = 0;
-  int ar_rank = 0, ar_world = 0, ar_loop = 0;
-  uint32_t* ar_gens = nullptr;
-  uint32_t* ar_err = nullptr;  // [timeouts, wait limit] (the custom all-reduce's ctl)
-  // more than 64 column tiles: statistics per PAIR of tiles (the consumer combines
-  // <= 64 partial sums per row) -- each tile stores its row sums to ar_ss_tmp, the
-  // second of the pair to finish (ticket ar_pair[tile / 2]) adds the two in order
-  float* ar_ss_tmp = nullptr;
-  int* ar_pair = nullptr;
-  int ar_group = 1;
+  // GG_AR (TP decode, row-parallel O / down): the tensor-parallel all-reduce in the
+  // launch, operands in device memory (ArDesc below: kernel arguments stay in SGPRs)
+  const struct ArDesc* ar = nullptr;
+};
+
+// GG_AR: GG_RESID with the tensor-parallel all-reduce inside the launch. The tile's
+// last arriver sums its S slabs, rounds to bf16 (this rank's contribution, as in the
+// unfused path) and pushes it to every peer as LL lines (comm/ll.h) at [parity]
+// [source rank][element / 4] of the peer's receive region, then polls its OWN region
+// for the peers' lines of the same tile and adds all contributions in rank order to
+// the residual (bit-identical on every rank), with the tile's statistics. Generation
+// per column tile (gens), so the pull-free double-buffering argument of the LL
+// all-reduce holds per tile. loop: one-process TP-shard simulation -- the "peers" are
+// this rank's own region (lines pushed to source slot r, polled, not added): the
+// traffic and the waits of a `world`-rank group, the numerics of one rank; loop - 1 =
+// a simulated link latency in wall-clock ticks, waited once per tile between the
+// pushes and the polls. More than 64 column tiles (group 2): statistics per PAIR of
+// tiles (the consumer combines <= 64 partial sums per row) -- each tile stores its row
+// sums to ss_tmp, the second of the pair to finish (ticket pair[tile / 2]) adds the
+// two in order.
+struct ArDesc {
+  uint8_t* data[CAR_MAX_RANKS];  // each rank's LL receive region (loop: all this rank's own)
+  int64_t region;
+  int rank, world, loop, group;
+  uint32_t* gens;                // one generation per column tile
+  uint32_t* err;                 // [timeouts, wait limit] (the custom all-reduce's ctl)
+  float* ss_tmp;
+  int* pair;
 };
 
 // GG_MOE_RESID (grouped w2 of the fused decode layer, TP = 1): the MoE combine inside
@@ -229,7 +236,17 @@ __device__ __forceinline__ void m64g_resid_tail(const float* __restrict__ part, 
 // every butterfly).
 template <int COLS, int NTHR>
 __device__ __forceinline__ void m64g_ar_tail(const float* __restrict__ part, int S, int M, int N, const M64Epi& epi,
-                                             int* flag, int bx) {
+                                             int* flag, int bx, uint32_t dv) {
+  // the descriptor, loaded into lanes 0..29 of every wave at kernel start (dv): read
+  // back lane by lane (no global load in the tail, no SGPRs held across the loop)
+  auto d32 = [&](int i) { return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dv), i)); };
+  auto d64 = [&](int i) { return static_cast<uint64_t>(d32(i)) | (static_cast<uint64_t>(d32(i + 1)) << 32); };
+  // (fields read where they are used: few SGPRs live at once)
+  auto peer = [&](int r) { return reinterpret_cast<uint8_t*>(d64(2 * r)); };
+  auto region = [&] { return static_cast<int64_t>(d64(16)); };
+  auto gens = [&] { return reinterpret_cast<uint32_t*>(d64(22)); };
+  auto err = [&] { return reinterpret_cast<uint32_t*>(d64(24)); };
+  const int rank = static_cast<int>(d32(18)), world = static_cast<int>(d32(19)), loop = static_cast<int>(d32(20));
   if (S > 1) {
     if (!agent_ticket(epi.counters + bx, S - 1, flag)) return;
   } else {
@@ -241,10 +258,10 @@ __device__ __forceinline__ void m64g_ar_tail(const float* __restrict__ part, int
   const int tid = threadIdx.x;
   const int n0 = bx * COLS;
   const int64_t slab = static_cast<int64_t>(M) * N;
-  const uint32_t gen = epi.ar_gens[bx] + 1;
-  const int64_t src_bytes = epi.ar_region / (2 * CAR_MAX_RANKS);  // per (parity, source)
-  const int64_t par = static_cast<int64_t>(gen & 1) * (epi.ar_region / 2);
-  uint8_t* const own = epi.ar_data[epi.ar_rank];
+  const uint32_t gen = gens()[bx] + 1;
+  const int64_t src_bytes = region() / (2 * CAR_MAX_RANKS);  // per (parity, source)
+  const int64_t par = static_cast<int64_t>(gen & 1) * (region() / 2);
+  uint8_t* const own = peer(rank);
   bool ok = true;
   for (int base = 0; base < M * C4; base += NTHR) {
     const int idx = base + tid;
@@ -266,24 +283,24 @@ __device__ __forceinline__ void m64g_ar_tail(const float* __restrict__ part, int
       }
       const uint32_t w0 = pack2(y[0], y[1]), w1 = pack2(y[2], y[3]);  // this rank's bf16 contribution
       const int64_t line = par + (e / 4) * 16;
-      for (int r = 0; r < epi.ar_world; ++r) {
-        if (r == epi.ar_rank) continue;
-        ll_store(epi.ar_data[r] + line + static_cast<int64_t>(epi.ar_loop ? r : epi.ar_rank) * src_bytes, w0, w1,
+      for (int r = 0; r < world; ++r) {
+        if (r == rank) continue;
+        ll_store(peer(r) + line + static_cast<int64_t>(loop ? r : rank) * src_bytes, w0, w1,
                  gen);
       }
       asm volatile("" ::: "memory");  // every push is issued before the first poll
-      if (epi.ar_loop > 1) {  // loopback simulation of a link latency (ticks)
+      if (loop > 1) {  // loopback simulation of a link latency (ticks)
         const uint64_t t0 = wall_clock64();
-        while (wall_clock64() - t0 < static_cast<uint64_t>(epi.ar_loop - 1)) __builtin_amdgcn_s_sleep(1);
+        while (wall_clock64() - t0 < static_cast<uint64_t>(loop - 1)) __builtin_amdgcn_s_sleep(1);
       }
       uint32_t d[CAR_MAX_RANKS][2];
-      const uint32_t need = ((1u << epi.ar_world) - 1) & ~(1u << epi.ar_rank);
-      if (ok) ok = ll_recv_multi(own + line, src_bytes, need, gen, epi.ar_err, d);
+      const uint32_t need = ((1u << world) - 1) & ~(1u << rank);
+      if (ok) ok = ll_recv_multi(own + line, src_bytes, need, gen, err(), d);
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int r = 0; r < epi.ar_world; ++r) {  // rank order: bit-identical on every rank
+      for (int r = 0; r < world; ++r) {  // rank order: bit-identical on every rank
         uint32_t d0 = w0, d1 = w1;
-        if (r != epi.ar_rank) {
-          if (epi.ar_loop || !ok) continue;  // loopback: polled, not added
+        if (r != rank) {
+          if (loop || !ok) continue;  // loopback: polled, not added
           d0 = d[r][0];
           d1 = d[r][1];
         }
@@ -307,17 +324,17 @@ __device__ __forceinline__ void m64g_ar_tail(const float* __restrict__ part, int
 #pragma unroll
     for (int o = C4 / 2; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
     if (act && c == 0) {
-      if (epi.ar_group == 1) epi.ss_out[bx * M + m] = sq;
-      else st4_sc1(epi.ar_ss_tmp + bx * M + m, sq);
+      if (static_cast<int>(d32(21)) == 1) epi.ss_out[bx * M + m] = sq;
+      else st4_sc1(reinterpret_cast<float*>(d64(26)) + bx * M + m, sq);
     }
   }
-  if (tid == 0) epi.ar_gens[bx] = gen;
-  if (epi.ar_group == 1) return;
+  if (tid == 0) gens()[bx] = gen;
+  if (static_cast<int>(d32(21)) == 1) return;
   // pair statistics: the later tile of the pair adds both row sums, in tile order
-  if (!agent_ticket(epi.ar_pair + bx / 2, 1, flag)) return;
+  if (!agent_ticket(reinterpret_cast<int*>(d64(28)) + bx / 2, 1, flag)) return;
   const int p0 = bx & ~1;
-  for (int m = tid; m < M; m += NTHR)
-    epi.ss_out[(bx / 2) * M + m] = epi.ar_ss_tmp[p0 * M + m] + epi.ar_ss_tmp[(p0 + 1) * M + m];
+  const float* ss_tmp = reinterpret_cast<const float*>(d64(26));
+  for (int m = tid; m < M; m += NTHR) epi.ss_out[(bx / 2) * M + m] = ss_tmp[p0 * M + m] + ss_tmp[(p0 + 1) * M + m];
 }
 
 // Split-K GG_SILU tail: every workgroup has stored its fp32 partial of the tile
@@ -439,7 +456,6 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   for (int nt = 0; nt < NW; ++nt)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
   auto compute = [&](const uint8_t* slot) {
     const uint8_t* xs = slot;
     const uint8_t* ws = slot + XBYTES + wid * WBYTES;
@@ -584,6 +600,11 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
     }
   }
 
+  // GG_AR: the all-reduce descriptor (30 dwords) into lanes 0..29 of every wave, its
+  // latency under the slab stores and the tile ticket (m64g_ar_tail reads it back with
+  // readlane: no SGPRs held, no dependent load in the tail)
+  uint32_t ar_dv = 0;
+  if (mode == GG_AR) ar_dv = reinterpret_cast<const uint32_t*>(epi.ar)[lane < 30 ? lane : 29];
   // acc[nt][mt][r] = out[m = 16 mt + li][n = nbase + 16 nt + 4 g + r]
   const bool silu_split = NW == 2 && mode == GG_SILU && S > 1;
   if (mode == GG_PARTIAL || mode == GG_RESID || mode == GG_AR || silu_split) {
@@ -602,7 +623,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
     if (mode == GG_RESID)
       m64g_resid_tail<16 * NW * WV, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0), bx);
     else if (mode == GG_AR)
-      m64g_ar_tail<16 * NW * WV, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0), bx);
+      m64g_ar_tail<16 * NW * WV, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0), bx, ar_dv);
     else if (silu_split)
       m64g_silu_tail<16 * NW * WV, 64 * WV>(part, S, M, N, out, epi.counters, reinterpret_cast<int*>(lds0), bx);
   } else if (mode == GG_BF16) {
@@ -1068,19 +1089,7 @@ static int m64g_check(int M, int K, int N, const float* part, const uint16_t* ou
   if ((mode == GG_BF16 || mode == GG_SILU) && out == nullptr) return 1;
   if ((mode == GG_RESID || mode == GG_AR) && (epi.resid == nullptr || epi.ss_out == nullptr || epi.counters == nullptr))
     return 1;
-  if (mode == GG_AR) {
-    if (epi.ar_world < 1 || epi.ar_world > CAR_MAX_RANKS || epi.ar_rank < 0 || epi.ar_rank >= epi.ar_world ||
-        epi.ar_gens == nullptr || epi.ar_err == nullptr || (N / cols) > 4096)
-      return 1;
-    if (epi.ar_group != 1 && (epi.ar_group != 2 || (N / cols) % 2 || epi.ar_ss_tmp == nullptr ||
-                              epi.ar_pair == nullptr))
-      return 1;
-    for (int r = 0; r < epi.ar_world; ++r)
-      if (epi.ar_data[r] == nullptr) return 1;
-    // every line of the [M, N] message fits a (parity, source) slice of the region
-    if (static_cast<int64_t>(M) * N * 4 > epi.ar_region / (2 * CAR_MAX_RANKS)) return 1;
-  }
-  if (epi.ss_in != nullptr && (epi.ss_n < 1 || epi.ss_n > 64 || epi.ss_stride < M)) return 1;
+  if (mode == GG_AR && epi.ar == nullptr) return 1;  // (the descriptor is checked by the host wrapper)
   return 0;
 }
 
@@ -1114,26 +1123,19 @@ int gemm_m64g_ex(const uint16_t* x, int M, int K, const uint16_t* w, int N, floa
 }
 
 // Row-parallel GEMM with the TP all-reduce + residual + statistics in the launch
-// (GG_AR): data[r] = rank r's LL receive region (region bytes each; loop: all this
-// rank's own), gens one word per column tile, err = the custom all-reduce's ctl.
+// (GG_AR); desc: a device copy of ArDesc, validated by the host (linear.py
+// m64_ar_resid_linear / comm.GemmArArgs).
 int gemm_m64g_ar(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, int S, int nw, int cfg,
-                 uint16_t* resid, float* ss_out, int* counters, uint8_t* const* data, int64_t region, int rank,
-                 int world, int loop, uint32_t* gens, uint32_t* err, float* ss_tmp, int* pair, int group,
-                 hipStream_t st) {
+                 uint16_t* resid, float* ss_out, int* counters, const void* desc, hipStream_t st) {
   M64Epi epi{nullptr, 0, 0, 0.f, resid, ss_out, counters};
-  epi.ar_ss_tmp = ss_tmp;
-  epi.ar_pair = pair;
-  epi.ar_group = group;
-  for (int r = 0; r < world && r < CAR_MAX_RANKS; ++r) epi.ar_data[r] = data[r];
-  epi.ar_region = region;
-  epi.ar_rank = rank;
-  epi.ar_world = world;
-  epi.ar_loop = loop;
-  epi.ar_gens = gens;
-  epi.ar_err = err;
+  epi.ar = static_cast<const ArDesc*>(desc);
   if (m64g_check(M, K, N, part, nullptr, S, GG_AR, nw, cfg, epi)) return 1;
   m64g_launch(x, M, K, w, N, part, nullptr, S, GG_AR, nw, cfg, epi, st);
   return 0;
 }
+int m64g_ar_desc_bytes() { return static_cast<int>(sizeof(ArDesc)); }
+static_assert(sizeof(ArDesc) == 30 * 4 && offsetof(ArDesc, region) == 16 * 4 && offsetof(ArDesc, rank) == 18 * 4 &&
+                  offsetof(ArDesc, gens) == 22 * 4 && offsetof(ArDesc, pair) == 28 * 4,
+              "ArDesc: the tail reads it back by dword (m64g_ar_tail)");
 
 }  // namespace xgk

@@ -25,7 +25,8 @@ int gemm_m64g_ex(const uint16_t*, int, int, const uint16_t*, int, float*, uint16
                  int, int, float, uint16_t*, float*, int*, hipStream_t);
 int gemm_mw(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, hipStream_t);
 int gemm_m64g_ar(const uint16_t*, int, int, const uint16_t*, int, float*, int, int, int, uint16_t*, float*, int*,
-                 uint8_t* const*, int64_t, int, int, int, uint32_t*, uint32_t*, float*, int*, int, hipStream_t);
+                 const void*, hipStream_t);
+int m64g_ar_desc_bytes();
 int gemm_pf(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, float*, int*,
             hipStream_t);
 int pf_sk_slot_floats(int);
@@ -283,18 +284,13 @@ PYBIND11_MODULE(_kernels, m) {
   // TP row-parallel GEMM with the all-reduce + residual + statistics in the launch
   // (gemm_m64g.hip GG_AR); data = each rank's LL receive region (loop: this rank's own)
   m.def("gemm_m64g_ar", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, int splits, int nw,
-                           int cfg, uintptr_t resid, uintptr_t ss_out, uintptr_t counters, std::vector<uintptr_t> data,
-                           int64_t region, int rank, int world, int loop, uintptr_t gens, uintptr_t err,
-                           uintptr_t ss_tmp, uintptr_t pair, int group, uintptr_t st) {
-    if (static_cast<int>(data.size()) != world || world < 1 || world > 8)
-      throw std::invalid_argument("gemm_m64g_ar: one region pointer per rank (<= 8)");
-    uint8_t* d[8] = {};
-    for (int r = 0; r < world; ++r) d[r] = reinterpret_cast<uint8_t*>(data[r]);
+                           int cfg, uintptr_t resid, uintptr_t ss_out, uintptr_t counters, uintptr_t desc,
+                           uintptr_t st) {
     check(xgk::gemm_m64g_ar(P<const uint16_t>(x), M, K, P<const uint16_t>(w), N, P<float>(part), splits, nw, cfg,
-                            P<uint16_t>(resid), P<float>(ss_out), P<int>(counters), d, region, rank, world, loop,
-                            P<uint32_t>(gens), P<uint32_t>(err), P<float>(ss_tmp), P<int>(pair), group, S(st)),
+                            P<uint16_t>(resid), P<float>(ss_out), P<int>(counters), P<const void>(desc), S(st)),
           "gemm_m64g_ar");
   });
+  m.def("m64g_ar_desc_bytes", &xgk::m64g_ar_desc_bytes);
   m.def("add_partials_resid", [](uintptr_t part, int S_, int T, uintptr_t res, uintptr_t ss_part, int H,
                                  uintptr_t st, uint64_t sim_ticks) {
     if (H % 1024) throw std::invalid_argument("add_partials_resid: H % 1024 != 0");

@@ -480,6 +480,22 @@ class ResidWorkspace:
         # and per-tile row sums for grids of more than MAX_TILES column tiles
         self.ar_pair = torch.zeros(self.MAX_TILES, dtype=torch.int32, device=device)
         self.ar_ss_tmp = torch.zeros(2 * self.MAX_TILES * self.IN_LAUNCH_MAX_M, dtype=torch.float32, device=device)
+        self._ar_descs = {}
+
+    def ar_desc(self, ar, group: int) -> torch.Tensor:
+        """Device copy of gemm_m64g's ArDesc for these all-reduce operands (built once;
+        captured graphs keep pointing at it)."""
+        key = (id(ar), group)
+        d = self._ar_descs.get(key)
+        if d is None:
+            import struct
+            ptrs = list(ar.data) + [0] * (8 - len(ar.data))
+            raw = struct.pack("<8Qq4i4Q", *ptrs, ar.region, ar.rank, ar.world, ar.loop, group, ar.gens.data_ptr(),
+                              ar.err.data_ptr(), self.ar_ss_tmp.data_ptr(), self.ar_pair.data_ptr())
+            assert len(raw) == kernels().m64g_ar_desc_bytes(), "ArDesc layout"
+            d = (torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.ss.device), ar)  # (keeps ar alive)
+            self._ar_descs[key] = d
+        return d[0]
 
 
 # Prefill-sized down projections (K = 3.5 N) have too few output tiles for the chip at
@@ -604,9 +620,7 @@ def m64_ar_resid_linear(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, w
     part = torch.empty(S, M, N, dtype=torch.float32, device=resid.device)
     ss = ws.ss[site]
     kernels().gemm_m64g_ar(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), S, nw, cfg, resid.data_ptr(),
-                           ss.data_ptr(), ws.counters[site].data_ptr(), ar.data, ar.region, ar.rank, ar.world,
-                           ar.loop, ar.gens.data_ptr(), ar.err.data_ptr(), ws.ar_ss_tmp.data_ptr(),
-                           ws.ar_pair.data_ptr(), group, stream_ptr())
+                           ss.data_ptr(), ws.counters[site].data_ptr(), ws.ar_desc(ar, group).data_ptr(), stream_ptr())
     return RowStats(ss, ntiles // group, M)
 
 

@@ -364,7 +364,11 @@ class CustomAllReduce:
 
     def set_timeout(self, seconds: float) -> None:
         """Peer-wait limit of every later launch (stream-ordered; captured graphs read
-        the word at replay). Clamped to the 32-bit tick range."""
+        the word at replay). Clamped to the 32-bit tick range. Ranks that share one GPU
+        (test boxes: up to 8 processes time-share its queues) wait at least 10 s while
+        serving -- a peer process can be descheduled that long without being dead."""
+        if getattr(self, "shared_device", False):
+            seconds = max(seconds, 10.0)
         ticks = int(min(max(seconds, 1e-3) * self._khz * 1000, 0x7FFFFFFF))
         self.ctl[1].fill_(ticks)
         self.timeout_s = float(seconds)
