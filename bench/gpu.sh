@@ -358,6 +358,13 @@ r5t)  # TP decode: all-reduce inside the row-parallel GEMMs (GG_AR) -- loopback 
   run tp8_c4_off 300 env XGS_TUNE=gemm_ar=0 $B --model llama3-70b --tp-shard 8 --concurrency 4 --steps 100 --warmup 20 "$@"
   run tp8_c64 300 $B --model llama3-70b --tp-shard 8 --steps 100 --warmup 20 "$@"
   run c64 300 $B --steps 400 --warmup 40 ;;
+r5p)  # round-5 kernel tables of the defaults: 8B c64 / c1, 70B TP8 shard c1
+  bash bench/profile.sh "$o/prof_c64" "$@" &&
+  bash bench/profile.sh "$o/prof_c1" --concurrency 1 "$@" &&
+  bash bench/profile.sh "$o/prof_tp8_c1" --model llama3-70b --tp-shard 8 --concurrency 1 "$@" ;;
+r5s)  # host side of the headline: per-phase host timing and per-step wall log
+  run c64_t 300 env XGS_STEP_TIMING=1 XGS_STEP_LOG=$o/steps.jsonl $B --steps 400 --warmup 40 "$@"
+  run c64 300 $B --steps 400 --warmup 40 "$@" ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;

@@ -6,6 +6,8 @@ in their prologue, so a split-K GEMM costs no extra reduction launch.
 """
 from __future__ import annotations
 
+import functools
+
 from dataclasses import dataclass
 from typing import Optional
 
@@ -306,7 +308,7 @@ PF_MIN_M = 65
 # shapes (profiles/r5_pf_gemm.md): a workgroup costs PF_WG_US + its output bytes at
 # PF_WG_OUT_GBS (fp32 partials or bf16) + K tiles x the per-K-tile time of its cfg;
 # one workgroup per CU, so a grid of G costs ceil(G / CUs) of those.
-_PF_CFG_KT_US = {2: 1.07, 4: 1.34, 8: 1.29, 3: 1.75, 7: 1.51, 6: 1.77}   # cfg -> us per 64-deep K tile
+_PF_CFG_KT_US = {2: 1.07, 4: 1.34, 8: 1.37, 3: 1.75, 7: 1.51, 6: 1.77}   # cfg -> us per 64-deep K tile
 _PF_CFG_BM_ = {2: 128, 4: 192, 8: 192, 3: 256, 7: 256, 6: 288}
 PF_WG_US = 5.0
 PF_WG_OUT_GBS = 60.0
@@ -330,6 +332,7 @@ def cu_count(device=None) -> int:
     return n
 
 
+@functools.lru_cache(maxsize=4096)  # (eager mixed steps call it per projection: ~10 us of host time)
 def pf_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL, cus: int = 256):
     """(split_k, cfg, sk_grid) for gemm_pf, or None when the shape is unsupported.
     Every cfg of _PF_CFG_KT_US is priced with the model above: data-parallel (PARTIAL:
@@ -349,8 +352,8 @@ def pf_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL, cus: int = 256):
             S = 1
             while tiles * (S + 1) <= cus and (S + 1) <= K // 256:
                 S += 1
-            # + the partials' extra round trip through the consumer (~8 TB/s)
-            cands.append(((-(-tiles * S // cus)) * (wg + -(-nk // S) * kt) + (S - 1) * M * N * 8 / 8e6, S, 0))
+            # + the consumer's read of the extra fp32 slabs (~7 TB/s; their writes are in wg)
+            cands.append(((-(-tiles * S // cus)) * (wg + -(-nk // S) * kt) + (S - 1) * M * N * 4 / 7e6, S, 0))
         else:
             cands.append((-(-tiles // cus) * (wg + nk * kt), 1, 0))
             if bm <= PF_SK_MAX_BM and tiles % cus:
