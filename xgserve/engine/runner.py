@@ -299,9 +299,10 @@ class ModelRunner:
     WARM_LAUNCHES = 32
 
     def _set_comm_timeout(self, seconds: float) -> None:
+        from ..parallel.custom_ar import CustomAllReduce
         ar = comm.custom_allreduce()
         if ar is not None:
-            ar.set_timeout(seconds)
+            ar.set_timeout(seconds if seconds >= CustomAllReduce.WARMUP_TIMEOUT_S else ar.serve_timeout(seconds))
 
     @torch.no_grad()
     def capture_graphs(self):

@@ -179,7 +179,7 @@ class CustomAllReduce:
         self.h_err = torch.zeros(1, dtype=torch.int32).pin_memory()
         self._khz = max(1, int(k.car_wallclock_khz()) or 100_000)
         self.timeout_s = 0.0
-        self.set_timeout(self.SERVE_TIMEOUT_S)
+        self.set_timeout(self.serve_timeout())
         self.verified = None  # self_test() outcome
         # operands of the all-reduce inside the row-parallel GEMMs (comm.gemm_ar_args);
         # None until self_test() has verified it against RCCL
@@ -343,7 +343,7 @@ class CustomAllReduce:
             flag = torch.tensor([ok], dtype=torch.int32)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=cpu_group)
             res[name] = bool(flag.item())
-        self.set_timeout(self.SERVE_TIMEOUT_S)
+        self.set_timeout(self.serve_timeout())
         if res["ll"] is False or res["ll_resid"] is False:
             log.warning("custom all-reduce: push (LL) protocol disagreed with RCCL on this node (%s); "
                         "using the pull kernels", res)
@@ -362,13 +362,17 @@ class CustomAllReduce:
         """The decode all-reduce protocol in use: "ll" (push) or "pull"."""
         return "ll" if self.resid_ll else "pull"
 
+    def serve_timeout(self, seconds: Optional[float] = None) -> float:
+        """The peer-wait limit while serving: `seconds` (the configured collective
+        timeout, default SERVE_TIMEOUT_S), at least 10 s when the ranks share one GPU
+        (test boxes: up to 8 processes time-share its queues, so a live peer can be
+        descheduled that long)."""
+        s = self.SERVE_TIMEOUT_S if seconds is None else seconds
+        return max(s, 10.0) if getattr(self, "shared_device", False) else s
+
     def set_timeout(self, seconds: float) -> None:
         """Peer-wait limit of every later launch (stream-ordered; captured graphs read
-        the word at replay). Clamped to the 32-bit tick range. Ranks that share one GPU
-        (test boxes: up to 8 processes time-share its queues) wait at least 10 s while
-        serving -- a peer process can be descheduled that long without being dead."""
-        if getattr(self, "shared_device", False):
-            seconds = max(seconds, 10.0)
+        the word at replay). Clamped to the 32-bit tick range."""
         ticks = int(min(max(seconds, 1e-3) * self._khz * 1000, 0x7FFFFFFF))
         self.ctl[1].fill_(ticks)
         self.timeout_s = float(seconds)
