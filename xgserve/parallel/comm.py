@@ -67,11 +67,6 @@ GEMM_AR_MAX_T = 4
 _SIM_AR_TICKS = int(__import__("xgserve.tune", fromlist=["get_float"]).get_float("sim_ar_us", 0.0) * 100)  # 100 MHz
 
 
-def sim_ar_ticks() -> int:
-    """The simulated all-reduce wait (XGS_TUNE sim_ar_us) in 100 MHz ticks; 0 in a real TP group."""
-    return _SIM_AR_TICKS if get_state().tp_size == 1 else 0
-
-
 def tp_allreduce_resid(part: torch.Tensor, resid: torch.Tensor, ss: torch.Tensor, sim_world: int = 1) -> None:
     """Row-parallel projection epilogue of the fused decode layer:
     resid += all-reduce(sum_s part[s]) in place (bf16), ss[chunk * T + t] <- the new
