@@ -365,6 +365,13 @@ r5p)  # round-5 kernel tables of the defaults: 8B c64 / c1, 70B TP8 shard c1
 r5s)  # host side of the headline: per-phase host timing and per-step wall log
   run c64_t 300 env XGS_STEP_TIMING=1 XGS_STEP_LOG=$o/steps.jsonl $B --steps 400 --warmup 40 "$@"
   run c64 300 $B --steps 400 --warmup 40 "$@" ;;
+r5q)  # gemm_pf projection sets again after the planner refit (interleaved, two passes)
+  for pass in 1 2; do
+    run c64_def_$pass 300 $B --steps 400 --warmup 40 "$@"
+    run c64_qkv_$pass 300 env XGS_TUNE=pf=qkv,gate_up,down $B --steps 400 --warmup 40 "$@"
+    run c64_o_$pass 300 env XGS_TUNE=pf=o,gate_up,down $B --steps 400 --warmup 40 "$@"
+    run c64_all_$pass 300 env XGS_TUNE=pf=qkv,o,gate_up,down $B --steps 400 --warmup 40 "$@"
+  done ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;
