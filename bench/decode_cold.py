@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--probe", action="store_true",
                     help="anatomy: also time the kernel without its prologue (11), key loop (12), both (13)")
     a = ap.parse_args()
+    if a.probe:  # the probe kernels live only in a probe build of _kernels.so
+        from xgserve import _build
+        _build.build_kernels(probes=True)
     dev, Hq, Hkv, D, bs = "cuda", 32, 8, 128, a.bs
     B = a.B
     g = torch.Generator().manual_seed(0)

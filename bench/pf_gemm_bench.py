@@ -74,6 +74,9 @@ def main():
     ap.add_argument("--probe", action="store_true", help="also time the no-DMA / no-MFMA anatomy builds")
     ap.add_argument("--krot", action="store_true", help="also time each variant with K-tile rotation on")
     a = ap.parse_args()
+    if a.probe:  # the probe kernels live only in a probe build of _kernels.so
+        from xgserve import _build
+        _build.build_kernels(probes=True)
     kernels()
     torch.manual_seed(0)
     dev = "cuda"

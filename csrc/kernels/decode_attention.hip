@@ -450,7 +450,8 @@ static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, con
   // fragment-shaped K loads measured 0.5-6 % faster. depth 3: three register tiles
   // in flight per wave (fused form, G <= 4)
   if constexpr (D == 128 && G <= 4 && FQ) {
-    if (depth >= 11 && depth <= 14) {  // anatomy probes (depth = 10 + PR)
+#ifdef XGK_PROBES
+    if (depth >= 11 && depth <= 14) {  // anatomy probes (depth = 10 + PR): xgserve/_build.py --probes
 #define XGK_DECP(P)                                                                                                 \
   hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, true, 2, P>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt, \
                      bts, sl, po, pl, out, os, Hq, Hkv, bs, scale, S, fq)
@@ -462,6 +463,7 @@ static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, con
       if (S > 1) hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
       return;
     }
+#endif
     if (depth == 3) {
       hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, true, 3>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc,
                          bt, bts, sl, po, pl, out, os, Hq, Hkv, bs, scale, S, fq);
@@ -508,7 +510,11 @@ int decode_attention_fq(const float* part, int S_qkv, const int32_t* positions, 
   if (B <= 0) return 0;
   if (part == nullptr || S_qkv < 1 || bs % 16 != 0 || Hq % Hkv != 0 || D != 128 || num_splits < 1) return -1;
   if (num_splits > 1 && (part_out == nullptr || part_lse == nullptr)) return -1;
+#ifdef XGK_PROBES
   if (out == nullptr || depth < 2 || (depth > 3 && (depth < 11 || depth > 14))) return -1;
+#else
+  if (out == nullptr || depth < 2 || depth > 3) return -1;
+#endif
   const QkvFuse fq{part, S_qkv, positions, cos_sin, slots, kc, vc, apply_rope};
   const int G = Hq / Hkv;
 #define XGK_DECF(GG)                                                                                         \

@@ -546,8 +546,12 @@ int gemm_pf(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* pa
   const PfSk sk{sk_ws, sk_tickets, sk_grid};
   switch (cfg / 16) {
     case 0: return launch_pf_cfg<0>(cfg % 16, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+#ifdef XGK_PROBES  // anatomy probes (no DMA / no MFMA): measurement builds only (xgserve/_build.py --probes)
     case 1: return launch_pf_cfg<1>(cfg % 16, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
     default: return launch_pf_cfg<2>(cfg % 16, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+#else
+    default: return 1;
+#endif
   }
 }
 

@@ -93,13 +93,17 @@ def build_runtime(force: bool = False, jobs: int = 8, extra=()) -> Path:
     return out
 
 
-def build_kernels(force: bool = False, jobs: int = 8) -> Path:
+def build_kernels(force: bool = False, jobs: int = 8, probes: bool = False) -> Path:
+    """probes: also compile the anatomy-probe kernels (gemm_pf without DMA / MFMA,
+    decode attention without prologue / key loop). They are measurement builds
+    (bench/pf_gemm_bench.py --probe, bench/decode_cold.py --probe), never selected
+    by a plan, so the default library leaves them out."""
     srcs = sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "comm").glob("*.hip"))
     hdrs = sorted((CSRC / "kernels").glob("*.h")) + sorted((CSRC / "comm").glob("*.h"))
     cpp = sorted((CSRC / "kernels").glob("*.cpp"))
     out = PKG / f"_kernels{EXT}"
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fvisibility=hidden",
-             "-munsafe-fp-atomics", "-Wno-unused-result"]
+             "-munsafe-fp-atomics", "-Wno-unused-result"] + (["-DXGK_PROBES=1"] if probes else [])
     stamp = _digest(srcs + hdrs + cpp, flags)
     if not _needs(out, stamp, force):
         return out
@@ -130,11 +134,12 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--only", choices=["runtime", "kernels"], default=None)
+    ap.add_argument("--probes", action="store_true", help="include the anatomy-probe kernels (measurement builds)")
     a = ap.parse_args(argv)
     if a.only in (None, "runtime"):
         print("runtime:", build_runtime(a.force, a.jobs))
     if a.only in (None, "kernels"):
-        print("kernels:", build_kernels(a.force, a.jobs))
+        print("kernels:", build_kernels(a.force, a.jobs, a.probes))
 
 
 if __name__ == "__main__":
