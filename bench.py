@@ -370,6 +370,7 @@ def main():
                        "window_prompt_steps": window_mixed, "ttft_samples": len(ttfts),
                        "preemptions": st_["preemptions"], "kv_blocks": st_["kv_blocks_total"],
                        "decode_steps_total": st_["decode_steps"], "steps_total": st_["steps"],
+                       "window_lookahead_launches": c_after["lookahead_launches"] - c_before["lookahead_launches"],
                        "gemm_table": bool(getattr(eng, "gemm_table", False)),
                        "prefill_chunk": a.prefill_chunk,
                        "mixed_graph_replays": getattr(eng.runner, "mixed_replays", 0),

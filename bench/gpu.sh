@@ -372,6 +372,25 @@ r5q)  # gemm_pf projection sets again after the planner refit (interleaved, two 
     run c64_o_$pass 300 env XGS_TUNE=pf=o,gate_up,down $B --steps 400 --warmup 40 "$@"
     run c64_all_$pass 300 env XGS_TUNE=pf=qkv,o,gate_up,down $B --steps 400 --warmup 40 "$@"
   done ;;
+r5k)  # where the c64 step idles: kernel-trace-only profile (no HIP API trace), gaps by neighbouring kernels
+  run c64_plain 300 $B --steps 400 --warmup 40 "$@"
+  raw=$(mktemp -d "$TMPDIR/xgs_k.XXXXXX")
+  run c64_ktrace 400 rocprofv3 --kernel-trace --output-format csv -d "$raw" -o run -- \
+      python3 bench.py --steps 400 --warmup 40 "$@"
+  trace=$(find "$raw" -name '*kernel_trace.csv' | sort | tail -n 1)
+  python3 bench/prof_summary.py "$trace" --window-ms 600 --gap-us 8 --top 30 > "$o/c64_kernels_gaps.md"
+  run c1_plain 200 $B --concurrency 1 --steps 300 --warmup 30 "$@"
+  run c1_ktrace 300 rocprofv3 --kernel-trace --output-format csv -d "$raw/c1" -o run -- \
+      python3 bench.py --concurrency 1 --steps 300 --warmup 30 "$@"
+  trace=$(find "$raw/c1" -name '*kernel_trace.csv' | sort | tail -n 1)
+  python3 bench/prof_summary.py "$trace" --window-ms 300 --gap-us 4 --top 30 > "$o/c1_kernels_gaps.md"
+  rm -rf "$raw" ;;
+r5l)  # step-boundary gaps: kernel + HIP API trace, each gap's kernel matched to its enqueue call
+  raw=$(mktemp -d "$TMPDIR/xgs_l.XXXXXX")
+  run c64_htrace 400 rocprofv3 --kernel-trace --hip-trace --memory-copy-trace --output-format csv -d "$raw" -o run -- \
+      python3 bench.py --steps 300 --warmup 40 "$@"
+  python3 bench/gap_corr.py "$raw" --window-ms 400 --min-us 8 --dump 3 > "$o/c64_gap_corr.md"
+  rm -rf "$raw" ;;
 ar)  # custom all-reduce: push (LL) vs pull protocols, correctness + latency
   pyt ar_tests 600 tests/test_custom_ar_gpu.py
   run ar_bench 300 python -u bench/ar_bench.py --world 2 4 8 ;;

@@ -14,6 +14,8 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--window-ms", type=float, default=600.0)
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--gap-us", type=float, default=0.0,
+                    help="also list idle gaps longer than this, grouped by the kernels around them")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -48,6 +50,26 @@ def main():
         v = sorted(durs[n])
         med, mx = v[len(v) // 2] / 1e3, v[-1] / 1e3
         print(f"| `{short}` | {c} | {d / 1e6:.2f} | {d / c / 1e3:.1f} | {med:.1f} | {mx:.1f} | {100 * d / 1e6 / busy:.1f}% |")
+    if a.gap_us > 0:
+        ctx = collections.defaultdict(list)
+        prev_e, prev_n, small = None, None, 0.0
+        for r in win:
+            s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            n = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "")[:40]
+            if prev_e is not None and s > prev_e:
+                g = (s - prev_e) / 1e3
+                if g > a.gap_us:
+                    ctx[(prev_n, n)].append(g)
+                else:
+                    small += g
+            if prev_e is None or e >= prev_e:
+                prev_e, prev_n = e, n
+        tot = sum(sum(v) for v in ctx.values())
+        print(f"\n## Idle gaps > {a.gap_us:.0f} us: {sum(len(v) for v in ctx.values())}, {tot / 1e3:.2f} ms"
+              f" (shorter gaps: {small / 1e3:.2f} ms)\n")
+        print("| before | after | gaps | total ms | mean us | max us |\n|---|---|---:|---:|---:|---:|")
+        for (pn, nn), v in sorted(ctx.items(), key=lambda x: -sum(x[1]))[:a.top]:
+            print(f"| `{pn}` | `{nn}` | {len(v)} | {sum(v) / 1e3:.2f} | {sum(v) / len(v):.0f} | {max(v):.0f} |")
 
 
 if __name__ == "__main__":

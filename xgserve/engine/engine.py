@@ -207,7 +207,8 @@ class LLMEngine:
         self._pending_aborts: List[str] = []
         self.step_count = 0
         self.stats_counters = {"prompt_tokens": 0, "generation_tokens": 0, "steps": 0, "decode_steps": 0,
-                               "prefill_tokens_computed": 0, "requests_finished": 0, "preemptions": 0}
+                               "prefill_tokens_computed": 0, "requests_finished": 0, "preemptions": 0,
+                               "lookahead_launches": 0}
         self.spec = None
         if cfg.draft_model and cfg.num_speculative_tokens > 0:
             from .spec_decode import SpeculativeDecoder
@@ -448,6 +449,7 @@ class LLMEngine:
                     nsamp = self._sampling_rows(nplan)
                     src = self._lookahead_src(plan, nplan)
                     self._inflight = (nplan, self._launch(nplan, nsamp, src=src))
+                    self.stats_counters["lookahead_launches"] += 1
                 t = self._tick("launch", t)
         outs += self._emit_early(self._flush_deferred())  # previous step's outputs, while the GPU runs
         t = self._tick("emit_overlapped", t)
