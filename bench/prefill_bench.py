@@ -66,7 +66,7 @@ def ttft(L):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--lens", type=int, nargs="+", default=[512, 2048, 8192])
+    ap.add_argument("--lens", type=int, nargs="*", default=[512, 2048, 8192])
     ap.add_argument("--gh", type=int, nargs="+", default=[0, 4, -44, -84, -82, -1284, -1282, -1281])
     ap.add_argument("--ttft-len", type=int, default=8000)
     ap.add_argument("--no-ttft", action="store_true")

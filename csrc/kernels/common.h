@@ -31,8 +31,12 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 
+typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
+typedef float f32x2v_t __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16 pair (a low) in ONE v_cvt_pk_bf16_f32 (round to nearest
+// even, as f2bf); the scalar-cast form compiled to two converts + shift + or
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return static_cast<uint32_t>(f2bf(a)) | (static_cast<uint32_t>(f2bf(b)) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v_t{a, b}, bf16x2v_t));
 }
 
 __device__ __forceinline__ uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
