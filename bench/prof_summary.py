@@ -14,6 +14,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--window-ms", type=float, default=600.0)
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--by-grid", action="store_true", help="one row per (kernel, grid size)")
     ap.add_argument("--gap-us", type=float, default=0.0,
                     help="also list idle gaps longer than this, grouped by the kernels around them")
     a = ap.parse_args()
@@ -28,9 +29,12 @@ def main():
     durs = collections.defaultdict(list)
     for r in win:
         d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-        agg[r["Kernel_Name"]][0] += d
-        agg[r["Kernel_Name"]][1] += 1
-        durs[r["Kernel_Name"]].append(d)
+        key = r["Kernel_Name"]
+        if a.by_grid:
+            key = key.split("(")[0] + f" [grid {r['Grid_Size_X']}x{r['Grid_Size_Y']}x{r['Grid_Size_Z']}]"
+        agg[key][0] += d
+        agg[key][1] += 1
+        durs[key].append(d)
     gaps = []
     prev = None
     for r in win:
@@ -46,7 +50,7 @@ def main():
     # larger) mixed prefill launches of the same kernel
     print("\n| kernel | calls | total ms | avg us | median us | max us | share |\n|---|---:|---:|---:|---:|---:|---:|")
     for n, (d, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:a.top]:
-        short = n.split("(")[0][:90].replace("|", "/")
+        short = (n if a.by_grid else n.split("(")[0])[:110].replace("|", "/")
         v = sorted(durs[n])
         med, mx = v[len(v) // 2] / 1e3, v[-1] / 1e3
         print(f"| `{short}` | {c} | {d / 1e6:.2f} | {d / c / 1e3:.1f} | {med:.1f} | {mx:.1f} | {100 * d / 1e6 / busy:.1f}% |")

@@ -450,12 +450,13 @@ __global__ void __launch_bounds__(64 * NW, (NW == 4 && NSLOT <= 2 ? 2 : 1)) pref
     const bool need_mask = kv0 + C::BN - 1 > wave_lo || kv0 + C::BN > L;
     float mx = -INFINITY;
     if (need_mask) {
+      // key kv0 + 4 hf + c (c a per-register constant) is visible iff c <= lim - kv0 - 4 hf
+      const int vis = lim - kv0 - 4 * hf;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int key = kv0 + kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * hf;
-          if (key > lim) sacc[kb][e] = -INFINITY;
+          if (kb * 32 + (e & 3) + 8 * (e >> 2) > vis) sacc[kb][e] = -INFINITY;
           mx = fmaxf(mx, sacc[kb][e]);
         }
     } else {
@@ -477,16 +478,22 @@ __global__ void __launch_bounds__(64 * NW, (NW == 4 && NSLOT <= 2 ? 2 : 1)) pref
         for (int e = 0; e < 16; ++e) o[db][e] *= alpha;
       m = m_new;
     }
-    float rs = 0.f;
+    // pairwise: the fma / add pairs issue as packed v_pk_fma_f32 / v_pk_add_f32
+    f32x2v_t rs2 = {0.f, 0.f};
+    const f32x2v_t sc2 = {scale_log2, scale_log2}, nm2 = {nms, nms};
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const float pv = fast_exp2(fmaf(sacc[kb][e], scale_log2, nms));
-        sacc[kb][e] = pv;
-        rs += pv;
+      for (int e = 0; e < 16; e += 2) {
+        f32x2v_t x = {sacc[kb][e], sacc[kb][e + 1]};
+        x = x * sc2 + nm2;
+        x[0] = fast_exp2(x[0]);
+        x[1] = fast_exp2(x[1]);
+        sacc[kb][e] = x[0];
+        sacc[kb][e + 1] = x[1];
+        rs2 += x;
       }
-    l += xor32_sum(rs);
+    l += xor32_sum(rs2[0] + rs2[1]);
 
     // ---- O^T += V^T . P^T: k-step (kb, ss) takes accumulator registers 8 ss .. 8 ss + 7
 #pragma unroll
