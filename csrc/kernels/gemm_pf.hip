@@ -153,11 +153,25 @@ struct PfSk {
   int grid;       // 0: data-parallel (grid = tiles x S)
 };
 
-template <int BM, int MTP, bool NT, int PR = 0, bool SKM = false, int LAG = 1>
+// Grouped (MoE expert) form, GRP: the M dimension is moe_align's expert-sorted,
+// 64-padded row space [P]; expert e owns rows [offs[e], offs[e + 1]) and its own
+// weight w + e * w_stride. Tile slot mi of a column tile walks the experts' tiles in
+// order (expert e has ceil(segment / BM) of them); slots past the last tile exit.
+// A row p of a tile reads x row rows[p] (rows == nullptr: row p; -1 = a pad: row 0,
+// finite data never combined), rows past the segment end are not stored.
+struct PfGrp {
+  const int32_t* rows;
+  const int32_t* offs;
+  int E;
+  int mt;            // tile slots per column tile (host bound on the experts' tiles)
+  int64_t w_stride;  // elements between two experts' [N, K] weights
+};
+
+template <int BM, int MTP, bool NT, int PR = 0, bool SKM = false, int LAG = 1, bool GRP = false>
 __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restrict__ x, int M, int K,
                                                           const uint16_t* __restrict__ w, int N, int S,
                                                           float* __restrict__ part, uint16_t* __restrict__ out,
-                                                          int mode, int krot, PfSk sk) {
+                                                          int mode, int krot, PfSk sk, PfGrp grp) {
   // MTP: 16-row m tiles per wave per phase -> a phase is MTP x 4 x 2 MFMAs per wave
   // and releases 32 MTP A rows = 4 MTP DMA pieces of 8 rows; wave w issues pieces
   // w, w + 8, ... (MTP = 3: 12 pieces -> waves 0-3 two, waves 4-7 one; NA0 / NA1 are
@@ -189,7 +203,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
   const int nb = gridDim.x, bid = blockIdx.x;
   const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7;
   const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int per_split = TM * TN;
+  const int per_split = (GRP ? grp.mt : TM) * TN;
   const int nk_all = K / 64;
   // grouped order: GM M tiles x every N tile per group, M fastest inside a group, so
   // the ~32 workgroups an XCD runs at once share a few A and W panels (L2 hits)
@@ -216,7 +230,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
   bf16x8_t afr[MTP][2];
 
   // ---- one K range [kt_lo, kt_lo + nk) of the tile at (m0, n0) into acc
-  auto compute = [&](int m0, int n0, int kt_lo, int nk) {
+  auto compute = [&](int m0, int n0, int kt_lo, int nk, int m_hi, const uint16_t* wb) {
     const int rot = krot ? ((n0 / BN) * 37) % nk : 0;
     // A phase block q: rows [wr 0: 16 MTP rows][wr 1: 16 MTP rows]; piece pc = wid + 8 a
     // of wave wid fills block rows 8 pc .. 8 pc + 7
@@ -228,10 +242,15 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
       const int half = br / (16 * MTP);
       const int r = half * (BM / 2) + br - half * 16 * MTP;
 #pragma unroll
-      for (int q = 0; q < P; ++q)
-        asrc[q][a] = x + static_cast<int64_t>(min(m0 + r + 16 * MTP * q, M - 1)) * K + sw;
+      for (int q = 0; q < P; ++q) {
+        int row = min(m0 + r + 16 * MTP * q, m_hi - 1);
+        if constexpr (GRP) {
+          if (grp.rows != nullptr) row = max(grp.rows[row], 0);
+        }
+        asrc[q][a] = x + static_cast<int64_t>(row) * K + sw;
+      }
     }
-    const uint16_t* bsrc = w + static_cast<int64_t>(n0 + 32 * wid + dr) * K + sw;  // + 8 i rows per piece
+    const uint16_t* bsrc = wb + static_cast<int64_t>(n0 + 32 * wid + dr) * K + sw;  // + 8 i rows per piece
     auto kof = [&](int t) {
       const int tt = t + rot;
       return (kt_lo + (tt >= nk ? tt - nk : tt)) * 64;
@@ -346,7 +365,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
 
   // ---- epilogue of a finished tile (split s of S for PF_PARTIAL)
   // acc[q][mt][nt][r] = out[m = m0 + wr BM/2 + 16 MTP q + 16 mt + li][n = n0 + wrow + 16 nt + 4 g + r]
-  auto epilogue = [&](int m0, int n0, int s) {
+  auto epilogue = [&](int m0, int n0, int s, int m_hi) {
     const int mb = m0 + wr * (BM / 2) + li;
     const int nb0 = n0 + wrow + 4 * g;
     if (mode == PF_PARTIAL) {
@@ -356,7 +375,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
 #pragma unroll
         for (int mt = 0; mt < MTP; ++mt) {
           const int m = mb + 16 * MTP * q + 16 * mt;
-          if (m >= M) continue;
+          if (m >= m_hi) continue;
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt)
             *reinterpret_cast<float4*>(pp + static_cast<int64_t>(m) * N + nb0 + 16 * nt) =
@@ -368,7 +387,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
 #pragma unroll
         for (int mt = 0; mt < MTP; ++mt) {
           const int m = mb + 16 * MTP * q + 16 * mt;
-          if (m >= M) continue;
+          if (m >= m_hi) continue;
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) {
             uint2 o;
@@ -385,7 +404,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
 #pragma unroll
         for (int mt = 0; mt < MTP; ++mt) {
           const int m = mb + 16 * MTP * q + 16 * mt;
-          if (m >= M) continue;
+          if (m >= m_hi) continue;
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             float o[4];
@@ -404,12 +423,35 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
   };
 
   if constexpr (!SKM) {  // data-parallel: one (tile, split) per workgroup
-    const int s = v / per_split;
-    int m0, n0;
-    tile_mn(v - s * per_split, m0, n0);
+    // GRP: the tile slots past the experts' last tile are empty and sit at the end of
+    // the order, so the dispatch order itself (block b on XCD b % 8) spreads the real
+    // tiles over every XCD; the XCD-contiguous order v would leave whole XCDs idle
+    const int vg = GRP ? bid : v;
+    const int s = vg / per_split;
+    int m0, n0, m_hi = M;
+    const uint16_t* wb = w;
+    if constexpr (GRP) {
+      // tile slot mi of column tile n: the mi-th (expert, row tile) in expert order
+      const int u = vg - s * per_split, mi = u / TN;
+      n0 = (u - mi * TN) * BN;
+      int e = 0, base = 0, lo = 0, hi = 0;
+      for (; e < grp.E; ++e) {
+        lo = grp.offs[e];
+        hi = grp.offs[e + 1];
+        const int nt = (hi - lo + BM - 1) / BM;
+        if (mi < base + nt) break;
+        base += nt;
+      }
+      if (e == grp.E) return;  // past the last tile: the whole workgroup leaves (uniform)
+      m0 = lo + (mi - base) * BM;
+      m_hi = hi;
+      wb = w + static_cast<int64_t>(e) * grp.w_stride;
+    } else {
+      tile_mn(v - s * per_split, m0, n0);
+    }
     const int kt_lo = s * nk_all / S;
-    compute(m0, n0, kt_lo, (s + 1) * nk_all / S - kt_lo);
-    epilogue(m0, n0, s);
+    compute(m0, n0, kt_lo, (s + 1) * nk_all / S - kt_lo, m_hi, wb);
+    epilogue(m0, n0, s, m_hi);
   } else {  // stream-K
     const int64_t I = static_cast<int64_t>(per_split) * nk_all;
     const int G = sk.grid;
@@ -426,7 +468,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
       it += k1 - k0;
       int m0, n0;
       tile_mn(tile, m0, n0);
-      compute(m0, n0, k0, k1 - k0);
+      compute(m0, n0, k0, k1 - k0, M, w);
       if (k0 != 0 || k1 != nk_all) {
         // a shared tile: publish, then the last arriver combines
         float* mine = slot_of(v, tile) + tid * 4;
@@ -470,7 +512,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
               }
         }
       }
-      epilogue(m0, n0, 0);
+      epilogue(m0, n0, 0, M);
     }
   }
 }
@@ -478,18 +520,19 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
 template <int BM, int MTP, bool NT, int PR = 0, int LAG = 1>
 static int launch_pf(int tiles, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N, int S,
                      float* part, uint16_t* out, int mode, PfSk sk) {
+  const PfGrp ng{nullptr, nullptr, 0, 0, 0};
   // stream-K: tiles up to 256 rows (the 288-row variant spills the combine's registers)
   if constexpr (BM <= 256) {
     if (sk.grid) {
       hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, true, LAG>), dim3(sk.grid), dim3(512), 0, st, x, M, K, w, N, S,
-                         part, out, mode, pf_krot, sk);
+                         part, out, mode, pf_krot, sk, ng);
       return static_cast<int>(hipGetLastError());
     }
   } else if (sk.grid) {
     return 1;
   }
   hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, false, LAG>), dim3(tiles * S), dim3(512), 0, st, x, M, K, w, N, S,
-                     part, out, mode, pf_krot, sk);
+                     part, out, mode, pf_krot, sk, ng);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -528,6 +571,43 @@ static int launch_pf_cfg(int c, int tiles, hipStream_t st, const uint16_t* x, in
 // sk_grid > 0: stream-K over sk_grid persistent workgroups (S must be 1); ws holds
 // sk_grid x 2 x pf_sk_slot_floats(cfg) floats, tickets one zeroed int per tile
 int pf_sk_slot_floats(int cfg) { return 512 * (pf_cfg_bm(cfg) / 32) * 4 * 4; }
+
+// grouped (MoE): data-parallel only, no K rotation
+template <int BM, int MTP, int LAG>
+static int launch_pf_grp(int tiles, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N, int S,
+                         float* part, uint16_t* out, int mode, const PfGrp& grp) {
+  hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, false, 0, false, LAG, true>), dim3(tiles * S), dim3(512), 0, st, x, M, K,
+                     w, N, S, part, out, mode, 0, PfSk{nullptr, nullptr, 0}, grp);
+  return static_cast<int>(hipGetLastError());
+}
+
+// Grouped (MoE experts, moe_align layout): out / part rows are the P sorted rows; w is
+// [E, N, K]; rows gathers x (nullptr: x is already in sorted order); max_pairs bounds
+// the real rows over all experts (sizes the grid: sum over experts of ceil(segment / BM)
+// <= (max_pairs + 63 E) / BM + E). Lag-2 configs 6 / 7 / 8 only.
+int gemm_pf_grouped(const uint16_t* x, const int32_t* rows, const int32_t* offs, int E, int P, int K,
+                    const uint16_t* w, int N, int max_pairs, float* part, uint16_t* out, int S, int mode, int cfg,
+                    hipStream_t st) {
+  if (E < 1 || P < 1 || P % 64 || max_pairs < 1 || offs == nullptr || K < 64 || K % 64 || N < pf::BN ||
+      N % pf::BN || S < 1 || S > K / 64 || cfg < 6 || cfg > 8)
+    return 1;
+  if (mode == PF_PARTIAL) {
+    if (part == nullptr) return 1;
+  } else if (mode == PF_BF16 || mode == PF_SILU) {
+    if (out == nullptr || S != 1) return 1;
+  } else {
+    return 1;
+  }
+  const int bm = pf_cfg_bm(cfg);
+  const int mt = (max_pairs + 63 * E) / bm + E;
+  const PfGrp grp{rows, offs, E, mt, static_cast<int64_t>(N) * K};
+  const int tiles = mt * (N / pf::BN);
+  switch (cfg) {
+    case 6: return launch_pf_grp<288, 3, 2>(tiles, st, x, P, K, w, N, S, part, out, mode, grp);
+    case 7: return launch_pf_grp<256, 2, 2>(tiles, st, x, P, K, w, N, S, part, out, mode, grp);
+    default: return launch_pf_grp<192, 2, 2>(tiles, st, x, P, K, w, N, S, part, out, mode, grp);
+  }
+}
 
 int gemm_pf(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
             int cfg, int sk_grid, float* sk_ws, int* sk_tickets, hipStream_t st) {

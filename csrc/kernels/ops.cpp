@@ -27,6 +27,8 @@ int gemm_mw(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, 
 int gemm_m64g_ar(const uint16_t*, int, int, const uint16_t*, int, float*, int, int, int, uint16_t*, float*, int*,
                  const void*, hipStream_t);
 int m64g_ar_desc_bytes();
+int gemm_pf_grouped(const uint16_t*, const int32_t*, const int32_t*, int, int, int, const uint16_t*, int, int, float*,
+                    uint16_t*, int, int, int, hipStream_t);
 int gemm_pf(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, float*, int*,
             hipStream_t);
 int pf_sk_slot_floats(int);
@@ -269,6 +271,14 @@ PYBIND11_MODULE(_kernels, m) {
     check(xgk::gemm_pf(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode, cfg,
                        sk_grid, P<float>(sk_ws), P<int>(sk_tickets), S(st)),
           "gemm_pf");
+  });
+  // grouped form over moe_align's expert-sorted rows (the prompt-sized expert GEMMs)
+  m.def("gemm_pf_grouped", [](uintptr_t x, uintptr_t rows, uintptr_t offs, int E, int n_rows, int K, uintptr_t w, int N,
+                              int max_pairs, uintptr_t part, uintptr_t out, int splits, int mode, int cfg,
+                              uintptr_t st) {
+    check(xgk::gemm_pf_grouped(P<uint16_t>(x), P<int32_t>(rows), P<int32_t>(offs), E, n_rows, K, P<uint16_t>(w), N,
+                               max_pairs, P<float>(part), P<uint16_t>(out), splits, mode, cfg, S(st)),
+          "gemm_pf_grouped");
   });
   m.def("pf_sk_slot_floats", &xgk::pf_sk_slot_floats);
   m.def("set_pf_krot", [](int on) { xgk::set_pf_krot(on); });

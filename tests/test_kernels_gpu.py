@@ -421,6 +421,31 @@ def test_fused_moe_grouped(T):
     torch.testing.assert_close(out.cpu().float(), ref, atol=2e-2 * ref.std().item(), rtol=2e-2)
 
 
+@pytest.mark.parametrize("T,E,skew,eoff", [(300, 8, 0.0, 0), (575, 8, 6.0, 0), (700, 4, 3.0, 0), (575, 8, 0.0, 4)])
+def test_fused_moe_prefill_on_gemm_pf(T, E, skew, eoff, monkeypatch):
+    """Prefill-sized expert GEMMs on gemm_pf's grouped form (> 256 pairs): balanced and
+    skewed routing (an expert with several 192-288-row tiles), an EP shard (pairs of
+    another rank's experts are not placed), against fp32 and against the m64g path."""
+    from xgserve.ops import moe as MOE
+    k, H, F = 2, 1024, 512
+    x = rnd(T, H)
+    w13 = _w13(E, F, H)
+    w2 = rnd(E, H, F, scale=0.05)
+    logits = rnd(T, E, dtype=torch.float32)
+    logits[:, 0] += skew  # skew > 0: expert 0 takes most tokens
+    w, ids = ops.moe_topk_softmax(logits, k)
+    El = E // 2 if eoff else E
+    w13l, w2l = w13[eoff:eoff + El].contiguous(), w2[eoff:eoff + El].contiguous()
+    assert MOE.MOE_PF and MOE._moe_pf_ok(H, F)
+    out = ops.fused_moe(x, w13l, w2l, w, ids, expert_offset=eoff)
+    monkeypatch.setattr(MOE, "MOE_PF", False)
+    base = ops.fused_moe(x, w13l, w2l, w, ids, expert_offset=eoff)
+    ref = ops.moe_forward_ref(x.cpu(), w13l.cpu(), w2l.cpu(), w.cpu(), ids.cpu(), expert_offset=eoff).float()
+    tol = 2e-2 * ref.std().item()
+    torch.testing.assert_close(out.cpu().float(), ref, atol=tol, rtol=2e-2)
+    torch.testing.assert_close(out.cpu().float(), base.cpu().float(), atol=tol, rtol=2e-2)
+
+
 def test_decode_attention_split_combine_repeats():
     """Repeated split-K launches on one workspace (as graph replays do) with varying
     split counts stay correct."""

@@ -25,6 +25,21 @@ MOE_CFG_W2_PREFILL = 3
 # waves per workgroup of each gemm_m64g cfg (csrc/kernels/gemm_m64g.hip m64g_cfg_waves)
 M64G_CFG_WAVES = {0: 4, 1: 4, 2: 4, 3: 4, 4: 2, 5: 2, 6: 2, 7: 8}
 MOE_CFG_W13_PREFILL = 3
+# prefill-sized steps on gemm_pf's grouped form instead (csrc/kernels/gemm_pf.hip
+# gemm_pf_grouped): one MFMA tile of 192-288 rows covers an expert's rows, so each
+# expert's weights stream once per step (profiles/r5_moe_pf.md). XGS_TUNE moe_pf=0: off.
+MOE_PF = __import__("xgserve.tune", fromlist=["get_bool"]).get_bool("moe_pf", True)
+
+
+def _moe_pf_cfg(pairs: int, E: int) -> int:
+    """gemm_pf lag-2 tile (cfg 8 / 7 / 6 = 192 / 256 / 288 rows) covering the average
+    expert's 64-padded segment."""
+    seg = -(-max(1, pairs // max(1, E)) // BLOCK_M) * BLOCK_M
+    return 8 if seg <= 192 else 7 if seg <= 256 else 6
+
+
+def _moe_pf_ok(H: int, F: int) -> bool:
+    return H % 256 == 0 and (2 * F) % 256 == 0 and F % 64 == 0 and H >= 256
 
 
 def moe_topk_softmax(router_logits: torch.Tensor, k: int, renorm: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -171,6 +186,17 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     max_rows = T * k  # no expert holds more rows than (token, choice) pairs
     valid = sorted_rows.data_ptr()  # per-workgroup real-row count -> 16 / 32 / 64-row body
 
+    if MOE_PF and max_rows > MOE_PREFILL_PAIRS and _moe_pf_ok(H, F):
+        cfg = _moe_pf_cfg(max_rows, E)
+        kn.gemm_pf_grouped(x.contiguous().data_ptr(), sorted_rows.data_ptr(), offs.data_ptr(), E, P, H, w13.data_ptr(),
+                           F2, max_rows, 0, act.data_ptr(), 1, 2, cfg, stream_ptr())
+        # w2 has H / 256 column tiles per expert: 2 K splits (reduced by the combine)
+        S = 2 if F % 128 == 0 else 1
+        part = torch.empty(S, P, H, dtype=torch.float32, device=x.device)
+        kn.gemm_pf_grouped(act.data_ptr(), 0, offs.data_ptr(), E, P, F, w2.data_ptr(), H, max_rows, part.data_ptr(), 0,
+                           S, 1, cfg, stream_ptr())
+        return _moe_combine(kn, part, S, P, dest, topk_w, resid, ss, T, k, H, x, out_f32)
+
     def gemm(*a, cfg=0):
         kn.moe_gemm_m64g_rows(*a[:-1], cfg, max_rows, a[-1], valid)
     cfg13 = ((MOE_CFG_W13_PREFILL if T * k > MOE_PREFILL_PAIRS else MOE_CFG_W13)
@@ -197,6 +223,12 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
         return H // cols2
     gemm(act.data_ptr(), 0, offs.data_ptr(), E, F, w2.data_ptr(), H, P, part.data_ptr(), 0, S, 1, nw2, stream_ptr(),
          cfg=cfg2)
+    return _moe_combine(kn, part, S, P, dest, topk_w, resid, ss, T, k, H, x, out_f32)
+
+
+def _moe_combine(kn, part, S, P, dest, topk_w, resid, ss, T, k, H, x, out_f32):
+    """Weighted unpermute of the w2 partials: into the residual stream (+ statistics,
+    returns the partial-sum count) or a fresh [T, H] output."""
     if resid is not None:
         kn.moe_combine_resid(part.data_ptr(), S, P, dest.data_ptr(), topk_w.float().contiguous().data_ptr(),
                              resid.data_ptr(), ss.data_ptr(), T, k, H, stream_ptr())

@@ -12,6 +12,7 @@ Keys (default in brackets; every default is the production setting):
   pf [1]                   gemm_pf projections of prompt-sized mixed steps: 1 = the default set,
                            0 = library GEMMs, or a list "qkv,o,gate_up,down"
   pf_m [513-576]           the step sizes (tokens) that take gemm_pf
+  moe_pf [1]               prompt-sized expert GEMMs (> 256 token-expert pairs) on gemm_pf's grouped form
   krot [1]                 K-chunk rotation of the weight-streaming GEMMs (0 / 1 / 2)
   m64_plans / mw_plans     gemm_m64g / gemm_mw plan overrides, "NxKxMODE@BUCKET=...;..."
   mw_max_tokens [320]      largest step on gemm_mw
@@ -31,7 +32,7 @@ from __future__ import annotations
 import os
 from typing import Dict
 
-KEYS = {"fused_decode", "async_sched", "early_release", "spin_wait", "pf", "pf_m", "gemm_ar", "krot", "m64_plans", "mw_plans",
+KEYS = {"fused_decode", "async_sched", "early_release", "spin_wait", "pf", "pf_m", "moe_pf", "gemm_ar", "krot", "m64_plans", "mw_plans",
         "mw_max_tokens", "resid_inlaunch_kb", "decode_depth", "decode_max_splits", "ar_ll_max", "sim_ar_us",
         "tp_overlap_chunks", "tp_overlap_min_tokens", "ep_exact_min_pairs"}
 
