@@ -372,6 +372,20 @@ r5q)  # gemm_pf projection sets again after the planner refit (interleaved, two 
     run c64_o_$pass 300 env XGS_TUNE=pf=o,gate_up,down $B --steps 400 --warmup 40 "$@"
     run c64_all_$pass 300 env XGS_TUNE=pf=qkv,o,gate_up,down $B --steps 400 --warmup 40 "$@"
   done ;;
+r5z)  # round-5 closing gate: every GPU test, smoke, the headline (driver form x2, 3000 steps), batch 1,
+      # Mixtral c64 / c1 / TP2 shard, 70B TP8 shard c1, the 8K TTFT, a c64 kernel profile
+  pyt_soft gputests 900 tests -m gpu --maxfail=10
+  run smoke 150 python -u -c "import __graft_entry__ as g; g.smoke()"
+  run driver_a 200 $B --steps 20 --warmup 5
+  run driver_b 200 $B --steps 20 --warmup 5
+  run long 300 $B --steps 3000 --warmup 100
+  run c1 150 $B --concurrency 1 --steps 300 --warmup 30
+  run mx_c64 300 $B --model mixtral-8x7b --steps 100 --warmup 20
+  run mx_c1 300 $B --model mixtral-8x7b --concurrency 1 --steps 150 --warmup 20
+  run mx_tp2 300 $B --model mixtral-8x7b --tp-shard 2 --steps 100 --warmup 20
+  run tp8_c1 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 10
+  run ttft8k 300 python -u bench/prefill_bench.py --lens
+  bash bench/profile.sh "$o/prof_c64" ;;
 r5k)  # where the c64 step idles: kernel-trace-only profile (no HIP API trace), gaps by neighbouring kernels
   run c64_plain 300 $B --steps 400 --warmup 40 "$@"
   raw=$(mktemp -d "$TMPDIR/xgs_k.XXXXXX")
