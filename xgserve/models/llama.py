@@ -188,7 +188,8 @@ class LlamaLayer(nn.Module):
     # ------------------------------------------------------------------ MoE
     def _moe_allreduce(self, h: torch.Tensor) -> torch.Tensor:
         w, ids = ops.moe_route(h, self.router, self.cfg.experts_per_token)
-        out = ops.fused_moe(h, self.w13, self.w2, w, ids, self.expert_offset)
+        out = ops.fused_moe(h, self.w13, self.w2, w, ids, self.expert_offset,
+                              experts_total=self.router.shape[0])
         return self._ar(out)
 
     def _moe_alltoall(self, h: torch.Tensor) -> torch.Tensor:
@@ -478,7 +479,8 @@ class LlamaLayer(nn.Module):
                                                 align=(self.E_local, self.expert_offset))
         ss = ws.ss[site + 1]
         if self.tp > 1:
-            part = ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, out_f32=True, layout=layout)
+            part = ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, out_f32=True, layout=layout,
+                                 experts_total=self.router.shape[0])
             comm.tp_allreduce_resid(part.unsqueeze(0), resid, ss, self.tp)
         else:
             return RowStats(ss, ops.fused_moe(hn, self.w13, self.w2, w, ids, self.expert_offset, resid=resid, ss=ss,

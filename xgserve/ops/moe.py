@@ -151,7 +151,7 @@ def moe_forward_ref(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w
 def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
               topk_ids: torch.Tensor, expert_offset: int = 0, resid: Optional[torch.Tensor] = None,
               ss: Optional[torch.Tensor] = None, out_f32: bool = False, layout=None,
-              counters: Optional[torch.Tensor] = None):
+              counters: Optional[torch.Tensor] = None, experts_total: Optional[int] = None):
     """Local-expert MoE FFN: sum_j w_j * FFN_{e_j}(x) over choices owned locally
     (ids in [expert_offset, expert_offset + E_local)); others contribute nothing.
 
@@ -165,7 +165,8 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     step the combine runs inside the w2 launch (GG_MOE_RESID: the last workgroup to
     store into a column tile adds that tile's weighted rows into the residual), one
     launch fewer per layer; otherwise a separate combine kernel with 1024-column
-    statistics."""
+    statistics. experts_total (EP shards): the global expert count, so the prompt-sized
+    path sizes its tiles by this rank's expected share of the pairs."""
     if not use_native(x):
         out = moe_forward_ref(x, w13, w2, topk_w, topk_ids, expert_offset)
         if resid is None:
@@ -187,7 +188,8 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     valid = sorted_rows.data_ptr()  # per-workgroup real-row count -> 16 / 32 / 64-row body
 
     if MOE_PF and max_rows > MOE_PREFILL_PAIRS and _moe_pf_ok(H, F):
-        cfg = _moe_pf_cfg(max_rows, E)
+        share = max_rows * E // experts_total if experts_total else max_rows  # this rank's expected pairs
+        cfg = _moe_pf_cfg(share, E)
         kn.gemm_pf_grouped(x.contiguous().data_ptr(), sorted_rows.data_ptr(), offs.data_ptr(), E, P, H, w13.data_ptr(),
                            F2, max_rows, 0, act.data_ptr(), 1, 2, cfg, stream_ptr())
         # w2 has H / 256 column tiles per expert: 2 K splits (reduced by the combine)
