@@ -214,8 +214,12 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
         if F % (sk * kc2) == 0 and F % (sk * 256) == 0:
             S = sk
             break
-    part = torch.empty(S, P, H, dtype=torch.float32, device=x.device)
     cols2 = 16 * nw2 * M64G_CFG_WAVES[cfg2]
+    if S == 1 and (H // cols2) * E < 192 and F % (2 * kc2) == 0 and F % 512 == 0:
+        # few column tiles x local experts (EP shards: 4 experts x 32 tiles = 128
+        # workgroups on 256 CUs): 2 K splits fill the chip
+        S = 2
+    part = torch.empty(S, P, H, dtype=torch.float32, device=x.device)
     if (resid is not None and counters is not None and max_rows <= MOE_PREFILL_PAIRS and H // cols2 <= counters.numel()
             and (H // cols2) * T <= ss.numel()):
         kn.moe_gemm_m64g_resid(act.data_ptr(), 0, offs.data_ptr(), E, F, w2.data_ptr(), H, P, part.data_ptr(), S, nw2,
