@@ -41,6 +41,9 @@
 //     add_partials_rmsnorm), like every other projection kernel here.
 // Epilogues: bf16, fp32 partials, or silu(gate) * up of a block-16 interleaved
 // gate|up weight (the SiLU-gate fused: no [M, 2F] intermediate).
+// Grouped form (gemm_pf_grouped, GRP): the prompt-sized expert GEMMs of an MoE layer
+// over moe_align's expert-sorted rows -- one tile per expert segment, so each expert's
+// weights stream once per step (profiles/r5_moe_pf.md).
 #include <type_traits>
 
 #include "glds.h"
