@@ -236,7 +236,9 @@ __device__ __forceinline__ void m64g_resid_tail(const float* __restrict__ part, 
 // every butterfly).
 template <int COLS, int NTHR>
 __device__ __forceinline__ void m64g_ar_tail(const float* __restrict__ part, int S, int M, int N, const M64Epi& epi,
-                                             int* flag, int bx, uint32_t dv) {
+                                             int* flag, int bx, uint32_t dv, const float* ys = nullptr) {
+  // ys (S == 1, a few rows): this workgroup's tile staged in LDS [M][COLS] instead of
+  // the slab round trip through global memory
   // the descriptor, loaded into lanes 0..29 of every wave at kernel start (dv): read
   // back lane by lane (no global load in the tail, no SGPRs held across the loop)
   auto d32 = [&](int i) { return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dv), i)); };
@@ -249,6 +251,8 @@ __device__ __forceinline__ void m64g_ar_tail(const float* __restrict__ part, int
   const int rank = static_cast<int>(d32(18)), world = static_cast<int>(d32(19)), loop = static_cast<int>(d32(20));
   if (S > 1) {
     if (!agent_ticket(epi.counters + bx, S - 1, flag)) return;
+  } else if (ys != nullptr) {
+    __syncthreads();  // every wave's LDS stage
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's own slab stores
     __syncthreads();
@@ -271,14 +275,21 @@ __device__ __forceinline__ void m64g_ar_tail(const float* __restrict__ part, int
     float y[4] = {0.f, 0.f, 0.f, 0.f};
     float sq = 0.f;
     if (act) {
-      for (int s0 = 0; s0 < S; s0 += 4) {
-        float4 v[4];
+      // the residual row segment is needed last: its load flies under the pushes and polls
+      uint2 rv = *reinterpret_cast<const uint2*>(epi.resid + e);
+      if (ys != nullptr) {
+        const float4 v = *reinterpret_cast<const float4*>(ys + m * COLS + 4 * c);
+        y[0] = v.x; y[1] = v.y; y[2] = v.z; y[3] = v.w;
+      } else {
+        for (int s0 = 0; s0 < S; s0 += 4) {
+          float4 v[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const float4*>(part + min(s0 + j, S - 1) * slab + e);
+          for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const float4*>(part + min(s0 + j, S - 1) * slab + e);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float k = s0 + j < S ? 1.f : 0.f;
-          y[0] += k * v[j].x; y[1] += k * v[j].y; y[2] += k * v[j].z; y[3] += k * v[j].w;
+          for (int j = 0; j < 4; ++j) {
+            const float k = s0 + j < S ? 1.f : 0.f;
+            y[0] += k * v[j].x; y[1] += k * v[j].y; y[2] += k * v[j].z; y[3] += k * v[j].w;
+          }
         }
       }
       const uint32_t w0 = pack2(y[0], y[1]), w1 = pack2(y[2], y[3]);  // this rank's bf16 contribution
@@ -309,7 +320,6 @@ __device__ __forceinline__ void m64g_ar_tail(const float* __restrict__ part, int
         acc[2] += __uint_as_float(d1 << 16);
         acc[3] += __uint_as_float(d1 & 0xFFFF0000u);
       }
-      uint2 rv = *reinterpret_cast<const uint2*>(epi.resid + e);
       acc[0] += __uint_as_float(rv.x << 16);
       acc[1] += __uint_as_float(rv.x & 0xFFFF0000u);
       acc[2] += __uint_as_float(rv.y << 16);
@@ -607,7 +617,22 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   if (mode == GG_AR) ar_dv = reinterpret_cast<const uint32_t*>(epi.ar)[lane < 30 ? lane : 29];
   // acc[nt][mt][r] = out[m = 16 mt + li][n = nbase + 16 nt + 4 g + r]
   const bool silu_split = NW == 2 && mode == GG_SILU && S > 1;
-  if (mode == GG_PARTIAL || mode == GG_RESID || mode == GG_AR || silu_split) {
+  constexpr int TCOLS = 16 * NW * WV;
+  if (mode == GG_AR && S == 1 && 256 + M * TCOLS * 4 <= static_cast<int>(sizeof(lds0))) {
+    // one split: the tile goes through LDS to the all-reduce tail (no slab store + reload)
+    __syncthreads();  // every wave is past its last ring read
+    float* ys = reinterpret_cast<float*>(lds0 + 256);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = 16 * mt + li;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < NW; ++nt)
+        *reinterpret_cast<float4*>(ys + m * TCOLS + (nbase - bx * TCOLS) + 16 * nt + 4 * g) =
+            make_float4(acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]);
+    }
+    m64g_ar_tail<TCOLS, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0), bx, ar_dv, ys);
+  } else if (mode == GG_PARTIAL || mode == GG_RESID || mode == GG_AR || silu_split) {
     float* pp = part + static_cast<int64_t>(s) * M * N;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
