@@ -225,7 +225,12 @@ __device__ __forceinline__ void m64g_resid_reduce(const float* __restrict__ part
 template <int COLS, int NTHR>
 __device__ __forceinline__ void m64g_resid_tail(const float* __restrict__ part, int S, int M, int N,
                                                 const M64Epi& epi, int* flag, int bx) {
-  if (S > 1 && !agent_ticket(epi.counters + bx, S - 1, flag)) return;
+  if (S > 1) {
+    if (!agent_ticket(epi.counters + bx, S - 1, flag)) return;
+  } else {  // one split: the tile's own slab, written by every wave, read back in another layout
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   m64g_resid_reduce<COLS, NTHR>(part, S, M, N, bx, epi);
 }
 
