@@ -127,7 +127,7 @@ def preflight(st, world: int, tp: int, dev, eng) -> dict:
     import torch.distributed as dist
     info = {"backend": None, "rccl_world": None, "tp_groups": None, "p2p_ok": None, "decode_ar": None,
             "decode_ar_in_gemm": None,
-            "custom_ar_selftest": None}
+            "custom_ar_selftest": None, "custom_ar_selftest_passes": None}
     if world > 1:
         info["backend"] = str(dist.get_backend())
         x = torch.full((4096,), float(st.rank + 1), dtype=torch.float32, device=dev)
@@ -145,6 +145,7 @@ def preflight(st, world: int, tp: int, dev, eng) -> dict:
         ar = getattr(eng, "custom_ar", None)
         lib = "rccl" if info["backend"] == "nccl" else info["backend"]  # the library collective
         info["custom_ar_selftest"] = getattr(ar, "verified", None)
+        info["custom_ar_selftest_passes"] = getattr(ar, "verified_counts", None)  # launches checked vs RCCL
         # every rank must agree on the protocol (a refusal below is collective)
         mine = torch.tensor([1 if ar is not None else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(mine, op=dist.ReduceOp.MIN)

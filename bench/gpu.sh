@@ -21,6 +21,7 @@
 #   r4b/r4c  round-4 passes: AR + TP + prefetch A/B; Mixtral + profiles
 #   r4d      in-launch residual reduce + decode-attention depth A/Bs at 64 rows (step logs)
 #   r5a      gemm_pf: tests, per-projection A/B at the mixed-step rows, headline on / off + profile
+#   r6a      GG_AR per-launch generations: custom all-reduce + TP engine tests, headline, 70B TP8 rank c1
 # Each GPU step has its own time limit; the first failure ends the suite.
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -70,6 +71,10 @@ ab)
     run "driver_$n" 200 env $s $B --steps 20 --warmup 5 "$@"
     run "w400_$n" 250 env $s $B --steps 400 --warmup 40 "$@"
   done ;;
+r6a)
+  pyt tp_tests 900 tests/test_custom_ar_gpu.py tests/test_tp_gpu.py
+  run bench_driver 200 $B --steps 20 --warmup 5 "$@"
+  run tp8_c1 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20 "$@" ;;
 tp)
   pyt tp_tests 600 tests/test_custom_ar_gpu.py tests/test_rccl_gpu.py tests/test_tp_gpu.py
   run tp8_c1 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20 "$@"

@@ -72,9 +72,11 @@ struct M64Epi {
 // unfused path) and pushes it to every peer as LL lines (comm/ll.h) at [parity]
 // [source rank][element / 4] of the peer's receive region, then polls its OWN region
 // for the peers' lines of the same tile and adds all contributions in rank order to
-// the residual (bit-identical on every rank), with the tile's statistics. Generation
-// per column tile (gens), so the pull-free double-buffering argument of the LL
-// all-reduce holds per tile. loop: one-process TP-shard simulation -- the "peers" are
+// the residual (bit-identical on every rank), with the tile's statistics. One
+// generation per launch, kept per AR_GRAN-column granule (gens): every GG_AR launch
+// covers all N columns, so each granule advances once per launch whatever the tile
+// width (the O and down launches of a layer may differ) and the pull-free
+// double-buffering argument of the LL all-reduce holds per line. loop: one-process TP-shard simulation -- the "peers" are
 // this rank's own region (lines pushed to source slot r, polled, not added): the
 // traffic and the waits of a `world`-rank group, the numerics of one rank; loop - 1 =
 // a simulated link latency in wall-clock ticks, waited once per tile between the
@@ -82,11 +84,12 @@ struct M64Epi {
 // tiles (the consumer combines <= 64 partial sums per row) -- each tile stores its row
 // sums to ss_tmp, the second of the pair to finish (ticket pair[tile / 2]) adds the
 // two in order.
+constexpr int AR_GRAN = 32;  // the narrowest GG_AR tile (16 x NW x WV columns)
 struct ArDesc {
   uint8_t* data[CAR_MAX_RANKS];  // each rank's LL receive region (loop: all this rank's own)
   int64_t region;
   int rank, world, loop, group;
-  uint32_t* gens;                // one generation per column tile
+  uint32_t* gens;                // one generation per AR_GRAN columns (all equal after a launch)
   uint32_t* err;                 // [timeouts, wait limit] (the custom all-reduce's ctl)
   float* ss_tmp;
   int* pair;
@@ -267,7 +270,11 @@ __device__ __forceinline__ void m64g_ar_tail(const float* __restrict__ part, int
   const int tid = threadIdx.x;
   const int n0 = bx * COLS;
   const int64_t slab = static_cast<int64_t>(M) * N;
-  const uint32_t gen = gens()[bx] + 1;
+  // One generation per LAUNCH, not per tile: the O and down launches share the LL
+  // region at different tile widths, so the words are kept per AR_GRAN-column granule
+  // and every launch advances each granule once -- all equal, whatever COLS is.
+  static_assert(COLS % AR_GRAN == 0, "GG_AR tiles cover whole granules");
+  const uint32_t gen = gens()[n0 / AR_GRAN] + 1;
   const int64_t src_bytes = region() / (2 * CAR_MAX_RANKS);  // per (parity, source)
   const int64_t par = static_cast<int64_t>(gen & 1) * (region() / 2);
   uint8_t* const own = peer(rank);
@@ -343,7 +350,7 @@ __device__ __forceinline__ void m64g_ar_tail(const float* __restrict__ part, int
       else st4_sc1(reinterpret_cast<float*>(d64(26)) + bx * M + m, sq);
     }
   }
-  if (tid == 0) gens()[bx] = gen;
+  if (tid < COLS / AR_GRAN) gens()[n0 / AR_GRAN + tid] = gen;
   if (static_cast<int>(d32(21)) == 1) return;
   // pair statistics: the later tile of the pair adds both row sums, in tile order
   if (!agent_ticket(reinterpret_cast<int*>(d64(28)) + bx / 2, 1, flag)) return;
@@ -1038,7 +1045,8 @@ int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, i
   const MoeResidEpi mre = mre_in ? *mre_in : MoeResidEpi{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
   if (mode == GG_MOE_RESID && (mre.dest == nullptr || mre.w == nullptr || mre.resid == nullptr ||
                                mre.ss_out == nullptr || mre.counters == nullptr || mre.T < 1 || mre.k < 1 ||
-                               max_rows > 256 || (16 * nw * m64g_cfg_waves(cfg)) % 4))
+                               max_rows > 256 || (16 * nw * m64g_cfg_waves(cfg)) % 4 ||
+                               N / (16 * nw * m64g_cfg_waves(cfg)) > 64))  // the next norm sums <= 64 per row
     return 1;
   const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
   if (K % (S * kc) || N % cols) return 1;
@@ -1110,6 +1118,8 @@ static int m64g_check(int M, int K, int N, const float* part, const uint16_t* ou
   if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 10) return 1;
   if (cfg >= 8 && M > 16) return 1;  // deep-ring configurations: one x tile only
   if (mode < GG_BF16 || mode > GG_AR || mode == GG_MOE_RESID) return 1;
+  // the consumer's statistics paths sum at most 64 partial sums per row (m64g prologue)
+  if (epi.ss_in != nullptr && (epi.ss_n < 1 || epi.ss_n > 64 || epi.ss_stride < M)) return 1;
   const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
   if (K % kc || S > K / kc || N % cols) return 1;
   // split-K SiLU: fp32 slabs + one zeroed arrival ticket per column tile (m64g_silu_tail)

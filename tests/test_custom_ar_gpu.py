@@ -259,16 +259,19 @@ def test_dead_peer_costs_one_limit_not_one_per_collective():
 
 def _selftest_worker(rank, world, port, q, ll_max):
     """maybe_enable's first-contact check on the ranks of this box: every protocol
-    agrees with the reference all-reduce, so nothing is switched off."""
-    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    agrees with the reference all-reduce, so nothing is switched off. GG_AR runs on
+    the 8B TP2 and 70B TP8 O / down shards (tile widths differ between the two)."""
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+                       "XGS_TUNE": "gemm_ar_shared=1"})
     import torch.distributed as dist
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
         from xgserve.parallel.custom_ar import CustomAllReduce
         ar = CustomAllReduce(rank, world, torch.device("cuda:0"), ll_max=ll_max)
-        res = ar.self_test(dist.group.WORLD, dist.group.WORLD)
-        q.put((rank, res, ar.protocol(), ar.timeouts()))
+        shapes = [(4096, 2048), (4096, 7168), (8192, 1024), (8192, 3584)]
+        res = ar.self_test(dist.group.WORLD, dist.group.WORLD, shapes)
+        q.put((rank, (res, ar.verified_counts), ar.protocol(), ar.timeouts()))
         dist.barrier()
         ar.close()
         dist.destroy_process_group()
@@ -278,12 +281,19 @@ def _selftest_worker(rank, world, port, q, ll_max):
 
 @pytest.mark.parametrize("world,ll_max", [(2, None), (2, 0), (4, None)])
 def test_custom_allreduce_self_test(world, ll_max):
-    for rank, res, proto, tmo in _run(_selftest_worker, world, ll_max):
-        assert isinstance(res, dict), res
+    from xgserve.parallel.custom_ar import CustomAllReduce
+    n = CustomAllReduce.SELF_TEST_ITERS
+    for rank, out, proto, tmo in _run(_selftest_worker, world, ll_max):
+        assert isinstance(out, tuple), out
+        res, counts = out
         assert res["pull"] and res["pull_resid"], res
         assert res["gemm_ar"], res  # the all-reduce inside the row-parallel GEMM launch
+        # every protocol ran its full repetition count on fresh data (GG_AR: per shape)
+        assert counts["pull"] == n and counts["pull_resid"] == n, counts
+        assert counts["gemm_ar"] == 4 * n, counts
         if ll_max == 0:
-            assert res["ll"] is None and proto == "pull"
+            assert res["ll"] is None and proto == "pull" and counts["ll"] is None
         else:
             assert res["ll"] and res["ll_resid"] and proto == "ll", res
+            assert counts["ll"] == n and counts["ll_resid"] == n, counts
         assert tmo == 0

@@ -75,3 +75,39 @@ def test_cli_exit_code_on_bad_url(tmp_path):
     p = subprocess.run([sys.executable, "-m", "xgserve", "check-config", "--checkpoint", "http://127.0.0.1:9/x"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     assert p.returncode == 2 and "cannot fetch" in p.stderr
+
+
+def test_index_server_error_is_not_read_as_unsharded(tmp_path, monkeypatch):
+    """Only a 404 on model.safetensors.index.json means "one file": a 5xx on the index
+    of a sharded checkpoint is reported as itself, and no .part file stays behind."""
+    import json as _json
+    d = tmp_path / "srv"
+    d.mkdir()
+    (d / "config.json").write_text(_json.dumps({"model_type": "llama"}))
+
+    class H(http.server.SimpleHTTPRequestHandler):
+        def __init__(self, *a, **k):
+            super().__init__(*a, directory=str(d), **k)
+
+        def log_message(self, *a, **k):
+            pass
+
+        def do_GET(self):  # noqa: N802
+            if self.path.endswith("model.safetensors.index.json"):
+                self.send_response(503)
+                self.send_header("Content-Length", "0")
+                self.end_headers()
+                return
+            super().do_GET()
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    from xgserve.models.fetch import FetchError, fetch_checkpoint
+    cache = tmp_path / "cache"
+    try:
+        with pytest.raises(FetchError, match="HTTP 503") as ei:
+            fetch_checkpoint(f"http://127.0.0.1:{srv.server_address[1]}/", root=str(cache))
+        assert ei.value.status == 503
+    finally:
+        srv.shutdown()
+    assert not list(cache.rglob("*.part"))

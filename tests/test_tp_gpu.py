@@ -69,6 +69,8 @@ def _rank_main(rank, world, port, ck, moe_comm, q, env=None):
                 outs = eng.generate(PROMPTS, sp)
             eng.stop_followers()
             mode = {"custom_ar": eng.custom_ar is not None, "graphs": bool(eng.runner.graphs), "async": eng._async,
+                    "gemm_ar": eng.custom_ar is not None and eng.custom_ar.gemm_ar is not None
+                    and eng.custom_ar.gemm_ar_allowed(),
                     "fused": eng.model._fused_ok, "samples": eng.runner.sample_log}
             q.put(("ok", outs, mode))
         else:
@@ -84,6 +86,7 @@ def _rank_main(rank, world, port, ck, moe_comm, q, env=None):
 
 
 _UNFUSED = {"XGS_TUNE": "fused_decode=0|async_sched=0"}
+_GG_AR = {"XGS_TUNE": "gemm_ar_shared=1"}
 
 
 @pytest.mark.parametrize("model,moe_comm,world,env", [
@@ -94,7 +97,12 @@ _UNFUSED = {"XGS_TUNE": "fused_decode=0|async_sched=0"}
     ("mixtral", "alltoall", 2, None), ("mixtral", "allreduce", 2, None), ("mixtral", "auto", 2, None),
     ("mixtral", "alltoall", 2, {"XGS_TUNE": "ep_exact_min_pairs=0"}),
     # an arrival while decoding: the asynchronous eager mixed step under TP
-    ("llama", "alltoall", 2, {"XGS_TEST_STAGGER": "1"}), ("llama", "alltoall", 4, {"XGS_TEST_STAGGER": "1"})])
+    ("llama", "alltoall", 2, {"XGS_TEST_STAGGER": "1"}), ("llama", "alltoall", 4, {"XGS_TEST_STAGGER": "1"}),
+    # the all-reduce inside the O / down GEMM launches (GG_AR; on separate GPUs the
+    # default, here forced on for ranks sharing the GPU): graphs + async scheduling,
+    # O and down at different tile widths over consecutive layers
+    ("llama", "alltoall", 2, _GG_AR), ("llama", "alltoall", 2, dict(_GG_AR, XGS_TEST_STAGGER="1")),
+    ("llama", "alltoall", 4, _GG_AR)])
 def test_tp2_on_one_gpu_matches_fp32_reference(tmp_path, model, moe_comm, world, env):
     """Llama: TP attention + MLP shards; by default the fused TP decode layer (one
     custom all-reduce launch per row-parallel projection reduces the split-K
@@ -130,8 +138,10 @@ def test_tp2_on_one_gpu_matches_fp32_reference(tmp_path, model, moe_comm, world,
     assert kind == "ok", outs
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert mode["custom_ar"], mode  # decode all-reduces on the IPC kernels
-    if model == "llama" and (env is None or "XGS_TEST_STAGGER" in env):
+    if model == "llama" and (env is None or "XGS_TEST_STAGGER" in env or env is _GG_AR):
         assert mode["graphs"] and mode["async"] and mode["fused"], mode
+    # GG_AR is engaged exactly when forced on (ranks share this box's GPU)
+    assert mode["gemm_ar"] == ("gemm_ar_shared=1" in (env or {}).get("XGS_TUNE", "")), mode
 
     base = None
     if model == "mixtral":

@@ -130,7 +130,14 @@ class LLMEngine:
         self.model.set_moe_comm(cfg.moe_comm)
         self.load_time = time.time() - t0
         from ..parallel.custom_ar import maybe_enable
-        self.custom_ar = maybe_enable(st, self.model.device)  # one-shot xGMI all-reduce for TP decode
+        m = self.mcfg
+        ar_shapes = None
+        if st.tp_size > 1 and m.arch != "gpt2":  # the row-parallel shards GG_AR serves: O, then down
+            ar_shapes = [(m.hidden_size, m.num_heads * m.head_dim // st.tp_size)]
+            if not m.num_experts:
+                ar_shapes.append((m.hidden_size, m.intermediate_size // st.tp_size))
+        # one-shot xGMI all-reduce for TP decode
+        self.custom_ar = maybe_enable(st, self.model.device, ar_shapes)
         self.device = self.model.device
         self.max_model_len = min(cfg.max_model_len or self.mcfg.max_position, self.mcfg.max_position)
         self.tokenizer = load_tokenizer(self.mcfg, cfg.checkpoint)

@@ -31,7 +31,9 @@ CHUNK = 8 << 20
 
 
 class FetchError(RuntimeError):
-    pass
+    def __init__(self, msg: str, status: Optional[int] = None):
+        super().__init__(msg)
+        self.status = status  # the HTTP status when the server answered with an error
 
 
 def is_url(spec: Optional[str]) -> bool:
@@ -50,22 +52,29 @@ def _join(base: str, name: str) -> str:
 def _get(url: str, dest: str, timeout: float) -> int:
     tmp = dest + ".part"
     try:
-        with urllib.request.urlopen(url, timeout=timeout) as r:  # noqa: S310 - http(s) only (is_url)
-            want = r.headers.get("Content-Length")
-            n = 0
-            with open(tmp, "wb") as f:
-                while True:
-                    b = r.read(CHUNK)
-                    if not b:
-                        break
-                    f.write(b)
-                    n += len(b)
-    except urllib.error.HTTPError as e:
-        raise FetchError(f"{url}: HTTP {e.code} {e.reason}") from None
-    except (urllib.error.URLError, OSError, ValueError) as e:
-        raise FetchError(f"{url}: {getattr(e, 'reason', e)}") from None
-    if want is not None and int(want) != n:
-        raise FetchError(f"{url}: truncated ({n} of {want} bytes)")
+        try:
+            with urllib.request.urlopen(url, timeout=timeout) as r:  # noqa: S310 - http(s) only (is_url)
+                want = r.headers.get("Content-Length")
+                n = 0
+                with open(tmp, "wb") as f:
+                    while True:
+                        b = r.read(CHUNK)
+                        if not b:
+                            break
+                        f.write(b)
+                        n += len(b)
+        except urllib.error.HTTPError as e:
+            raise FetchError(f"{url}: HTTP {e.code} {e.reason}", status=e.code) from None
+        except (urllib.error.URLError, OSError, ValueError) as e:
+            raise FetchError(f"{url}: {getattr(e, 'reason', e)}") from None
+        if want is not None and int(want) != n:
+            raise FetchError(f"{url}: truncated ({n} of {want} bytes)")
+    except FetchError:
+        try:  # a failed download leaves no partial file behind
+            os.remove(tmp)
+        except OSError:
+            pass
+        raise
     os.replace(tmp, dest)
     return n
 
@@ -86,7 +95,11 @@ def fetch_checkpoint(url: str, root: Optional[str] = None, timeout: float = 60.0
         _get(_join(url, "model.safetensors.index.json"), os.path.join(d, "model.safetensors.index.json"), timeout)
         with open(os.path.join(d, "model.safetensors.index.json")) as f:
             shards = sorted(set(json.load(f)["weight_map"].values()))
-    except FetchError:
+    except FetchError as e:
+        # only a missing index means "unsharded": a timeout, 5xx or truncation of the
+        # index of a sharded checkpoint is reported as itself
+        if e.status != 404:
+            raise
         shards = ["model.safetensors"]
     except (ValueError, KeyError) as e:
         raise FetchError(f"{url}: bad model.safetensors.index.json ({e})") from None

@@ -220,7 +220,8 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
         # workgroups on 256 CUs): 2 K splits fill the chip
         S = 2
     part = torch.empty(S, P, H, dtype=torch.float32, device=x.device)
-    if (resid is not None and counters is not None and max_rows <= MOE_PREFILL_PAIRS and H // cols2 <= counters.numel()
+    if (resid is not None and counters is not None and max_rows <= MOE_PREFILL_PAIRS and H // cols2 <= 64
+            and H // cols2 <= counters.numel()
             and (H // cols2) * T <= ss.numel()):
         kn.moe_gemm_m64g_resid(act.data_ptr(), 0, offs.data_ptr(), E, F, w2.data_ptr(), H, P, part.data_ptr(), S, nw2,
                                cfg2, max_rows, stream_ptr(), valid, dest.data_ptr(),

@@ -137,7 +137,7 @@ def gemm_ar_args(layer_tp: int, T: int, H: int, device) -> Optional[GemmArArgs]:
     s = get_state()
     if s.tp_size == 1:
         return _loopback_args(layer_tp, device) if layer_tp > 1 else None
-    if _CUSTOM_AR is None or not getattr(_CUSTOM_AR, "gemm_ar", None) or _CUSTOM_AR.shared_device:
+    if _CUSTOM_AR is None or not getattr(_CUSTOM_AR, "gemm_ar", None) or not _CUSTOM_AR.gemm_ar_allowed():
         return None
     return _CUSTOM_AR.gemm_ar
 

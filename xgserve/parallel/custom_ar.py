@@ -181,6 +181,7 @@ class CustomAllReduce:
         self.timeout_s = 0.0
         self.set_timeout(self.serve_timeout())
         self.verified = None  # self_test() outcome
+        self.verified_counts = None  # launches that passed per protocol
         # operands of the all-reduce inside the row-parallel GEMMs (comm.gemm_ar_args);
         # None until self_test() has verified it against RCCL
         from .comm import GemmArArgs
@@ -252,86 +253,127 @@ class CustomAllReduce:
                                          self.err.data_ptr(), stream_ptr())
         return out
 
-    def self_test(self, group, cpu_group) -> dict:
+    # first-contact repetitions: each protocol runs this many times on fresh data (an
+    # intermittent fault -- a torn 16-byte line over xGMI -- would not show in one trial)
+    SELF_TEST_ITERS = 50
+    LL_SIZES = (16 << 10, 32 << 10, 64 << 10, 128 << 10, 256 << 10)
+
+    def gemm_ar_allowed(self) -> bool:
+        """GG_AR (the all-reduce inside the row-parallel GEMM) spins on its peers from
+        a GEMM-sized grid: on separate GPUs always; on ranks sharing one GPU only
+        under the test-only XGS_TUNE gemm_ar_shared=1, for <= 4 ranks (whose grids are
+        co-resident there), so the engine path can be exercised on one-GPU boxes."""
+        from .. import tune
+        if not self.shared_device:
+            return True
+        return self.world <= 4 and tune.get_bool("gemm_ar_shared", False)
+
+    def self_test(self, group, cpu_group, ar_shapes=None) -> dict:
         """Run every protocol this instance would use against RCCL on the real links
-        (module docstring, "First contact"); switch off the ones that disagree on any
-        rank. Returns {"ll", "ll_resid", "pull", "pull_resid", "two_shot", "gemm_ar"} -> bool
-        (None: protocol not in use)."""
+        (module docstring, "First contact"), SELF_TEST_ITERS times each on fresh data;
+        switch off the ones that disagree on any rank. ar_shapes: the model's
+        row-parallel (N, K) shapes in layer order (O, down), replayed for GG_AR at
+        T = 1..4 rows -- the serving sequence, whose tile widths may differ between the
+        two launches. Returns {"ll", "ll_resid", "pull", "pull_resid", "two_shot",
+        "gemm_ar"} -> bool (None: protocol not in use); the passing launch counts are
+        kept in self.verified_counts."""
+        from .comm import GEMM_AR_MAX_T
         dev = self.device
         g = torch.Generator(device=dev).manual_seed(4321 + self.rank)
         res = {"ll": None, "ll_resid": None, "pull": None, "pull_resid": None, "two_shot": None, "gemm_ar": None}
+        counts = {k: 0 for k in res}
+        iters = self.SELF_TEST_ITERS
 
         def close_enough(got: torch.Tensor, ref: torch.Tensor) -> bool:
             return bool(torch.isfinite(got).all()) and float((got.float() - ref).abs().max()) <= \
                 2e-2 * max(1e-3, float(ref.abs().max()))
 
-        def plain(nbytes: int, ll: bool) -> bool:
-            x = (torch.randn(nbytes // 2, generator=g, device=dev) * 0.5).bfloat16()
-            ref = x.float()
-            dist.all_reduce(ref, group=group)
+        def plain(name: str, sizes, ll: bool) -> bool:
             keep = self.ll_max
-            if not ll:
-                self.ll_max = 0
-            try:
-                y = self.all_reduce(x.clone())
-            finally:
-                self.ll_max = keep
-            torch.cuda.synchronize(dev)
-            return close_enough(y, ref)
+            for i in range(iters):
+                nbytes = sizes[i % len(sizes)]
+                x = (torch.randn(nbytes // 2, generator=g, device=dev) * 0.5).bfloat16()
+                ref = x.float()
+                dist.all_reduce(ref, group=group)
+                if not ll:
+                    self.ll_max = 0
+                try:
+                    y = self.all_reduce(x.clone())
+                finally:
+                    self.ll_max = keep
+                torch.cuda.synchronize(dev)
+                if not close_enough(y, ref):
+                    return False
+                counts[name] += 1
+            return True
 
-        def resid(ll: bool) -> bool:
-            T, H, S = 8, 4096, 2
-            part = torch.randn(S, T, H, generator=g, device=dev) * 0.25
-            base = torch.randn(T, H, generator=torch.Generator(device=dev).manual_seed(99), device=dev).bfloat16()
-            ref = part.sum(0)
-            dist.all_reduce(ref, group=group)
-            ref = base.float() + ref
-            r = base.clone()
-            ss = torch.zeros(T * (H // 1024), dtype=torch.float32, device=dev)
+        def resid(name: str, ll: bool) -> bool:
+            H = 4096
             keep = self.resid_ll
-            self.resid_ll = ll
-            try:
-                self.all_reduce_resid(part, r, ss)
-            finally:
-                self.resid_ll = keep
-            torch.cuda.synchronize(dev)
-            ss_ref = (r.float().view(T, H // 1024, 1024) ** 2).sum(-1).t().reshape(-1)
-            return close_enough(r, ref) and bool(torch.allclose(ss, ss_ref, rtol=2e-2, atol=1e-2))
-
-        def gemm_ar() -> bool:
-            from ..ops.linear import ResidWorkspace, m64_ar_resid_linear
-            ok_all = True
-            for T, N, K in ((8, 4096, 1024), (1, 8192, 1024)):
-                x = (torch.randn(T, K, generator=g, device=dev) * 0.5).bfloat16()
-                w = (torch.randn(N, K, generator=g, device=dev) * 0.05).bfloat16()
-                base = torch.randn(T, N, generator=torch.Generator(device=dev).manual_seed(77), device=dev).bfloat16()
-                mine = (x.float() @ w.float().t()).bfloat16().float()
-                ref = mine.clone()
+            for i in range(iters):
+                T, S = (1, 2, 3, 4, 8, 16, 64)[i % 7], 1 + i % 4
+                part = torch.randn(S, T, H, generator=g, device=dev) * 0.25
+                base = torch.randn(T, H, generator=torch.Generator(device=dev).manual_seed(99 + i),
+                                   device=dev).bfloat16()
+                ref = part.sum(0)
                 dist.all_reduce(ref, group=group)
                 ref = base.float() + ref
-                ws = ResidWorkspace(1, 64, N, dev)
-                for _ in range(2):  # a second launch on the advanced generations
-                    r = base.clone()
-                    st = m64_ar_resid_linear(x, w, r, ws, 0, self._gemm_ar)
-                    torch.cuda.synchronize(dev)
-                    n = st.n
-                    ss_ref = (r.float().view(T, n, N // n) ** 2).sum(-1).t().reshape(-1)
-                    ok_all = ok_all and close_enough(r, ref) and bool(
-                        torch.allclose(st.ss[: n * T], ss_ref, rtol=2e-2, atol=1e-2))
-            return ok_all
+                r = base.clone()
+                ss = torch.zeros(T * (H // 1024), dtype=torch.float32, device=dev)
+                self.resid_ll = ll
+                try:
+                    self.all_reduce_resid(part, r, ss)
+                finally:
+                    self.resid_ll = keep
+                torch.cuda.synchronize(dev)
+                ss_ref = (r.float().view(T, H // 1024, 1024) ** 2).sum(-1).t().reshape(-1)
+                if not (close_enough(r, ref) and bool(torch.allclose(ss, ss_ref, rtol=2e-2, atol=1e-2))):
+                    return False
+                counts[name] += 1
+            return True
 
-        checks = {"pull": lambda: plain(16 << 10, False) and plain(min(self.slot, 256 << 10), False),
-                  "pull_resid": lambda: resid(False)}
-        # (ranks sharing one GPU never use it: a GEMM-sized grid spinning on its peers
-        # need not be co-resident with theirs there -- see shared_device)
-        if not self.shared_device or self.world <= 4:
+        def gemm_ar() -> bool:
+            from ..ops.linear import ResidWorkspace, m64_ar_resid_linear, m64_plan
+            # default: the Llama-3-8B TP2 O / down shards (64- and 32-column tiles)
+            shapes = [(n, k) for n, k in (ar_shapes or [(4096, 2048), (4096, 7168)])
+                      if m64_plan(1, n, k) is not None]
+            if not shapes:
+                return True
+            ws = ResidWorkspace(len(shapes), 64, max(n for n, _ in shapes), dev)
+            wts = [(torch.randn(n, k, generator=g, device=dev) * (0.5 / k ** 0.5)).bfloat16() for n, k in shapes]
+            for i in range(iters):
+                T = 1 + i % GEMM_AR_MAX_T
+                outs = []
+                for site, ((n, k), w) in enumerate(zip(shapes, wts)):  # one layer's O then down
+                    x = (torch.randn(T, k, generator=g, device=dev) * 0.5).bfloat16()
+                    base = (torch.randn(T, n, generator=g, device=dev)).bfloat16()
+                    r = base.clone()
+                    st = m64_ar_resid_linear(x, w, r, ws, site, self._gemm_ar)
+                    outs.append((x, w, base, r, st))
+                torch.cuda.synchronize(dev)
+                for x, w, base, r, st in outs:
+                    ref = (x.float() @ w.float().t()).bfloat16().float()
+                    dist.all_reduce(ref, group=group)
+                    ref = base.float() + ref
+                    n = st.n
+                    N = w.shape[0]
+                    ss_ref = (r.float().view(T, n, N // n) ** 2).sum(-1).t().reshape(-1)
+                    if not (close_enough(r, ref) and bool(torch.allclose(st.ss[: n * T], ss_ref, rtol=2e-2,
+                                                                         atol=1e-2))):
+                        return False
+                    counts["gemm_ar"] += 1
+            return True
+
+        checks = {"pull": lambda: plain("pull", (16 << 10, min(self.slot, 256 << 10)), False),
+                  "pull_resid": lambda: resid("pull_resid", False)}
+        if self.gemm_ar_allowed():
             checks["gemm_ar"] = gemm_ar
         if self.ll_max > 0:
-            checks["ll"] = lambda: plain(min(self.ll_max, 16 << 10), True) and plain(self.ll_max, True)
+            checks["ll"] = lambda: plain("ll", [n for n in self.LL_SIZES if n <= self.ll_max] or [self.ll_max], True)
         if self.resid_ll:
-            checks["ll_resid"] = lambda: resid(True)
+            checks["ll_resid"] = lambda: resid("ll_resid", True)
         if self.world >= 4 and self._two_shot(1 << 20):
-            checks["two_shot"] = lambda: plain(1 << 20, False)
+            checks["two_shot"] = lambda: plain("two_shot", (1 << 20,), False)
         self.set_timeout(self.WARMUP_TIMEOUT_S)
         for name, fn in checks.items():
             try:
@@ -356,6 +398,7 @@ class CustomAllReduce:
         if res["gemm_ar"] is False:
             log.warning("custom all-reduce: the GEMM-fused all-reduce disagreed with RCCL; separate launches")
         self.verified = res
+        self.verified_counts = {k: (counts[k] if res[k] is not None else None) for k in res}
         return res
 
     def protocol(self) -> str:
@@ -406,9 +449,10 @@ class CustomAllReduce:
         self.data = self.sig = 0
 
 
-def maybe_enable(state, device: torch.device) -> Optional[CustomAllReduce]:
+def maybe_enable(state, device: torch.device, ar_shapes=None) -> Optional[CustomAllReduce]:
     """Register the custom all-reduce for this TP group (GPU, 2..8 ranks), unless
-    XGS_CUSTOM_AR=0. Falls back to RCCL on any setup failure."""
+    XGS_CUSTOM_AR=0. Falls back to RCCL on any setup failure. ar_shapes: the model's
+    row-parallel (N, K) projection shards (self_test replays them)."""
     import os
     from . import comm
     if state.tp_size < 2 or device.type != "cuda" or os.environ.get("XGS_CUSTOM_AR", "1") == "0":
@@ -418,7 +462,7 @@ def maybe_enable(state, device: torch.device) -> Optional[CustomAllReduce]:
     except Exception as e:  # noqa: BLE001 - RCCL remains correct
         log.warning("custom all-reduce unavailable (%s); using RCCL", e)
         return None
-    res = ar.self_test(state.tp_group, state.tp_cpu_group)
+    res = ar.self_test(state.tp_group, state.tp_cpu_group, ar_shapes)
     if not (res["pull"] and res["pull_resid"]):
         log.warning("custom all-reduce: pull kernels disagreed with RCCL (%s); using RCCL", res)
         ar.close()

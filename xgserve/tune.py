@@ -20,6 +20,7 @@ Keys (default in brackets; every default is the production setting):
   decode_depth [2]         decode attention K/V register pipeline depth
   decode_max_splits [16]   split-K cap of decode attention
   gemm_ar [1]              TP decode: all-reduce inside the row-parallel O / down GEMM launches
+  gemm_ar_shared [0]       test-only: GG_AR also for <= 4 ranks sharing one GPU (one-GPU boxes)
   ar_ll_max [262144]       push (LL) all-reduce up to this many bytes (0: pull kernels)
   sim_ar_us [0]            --tp-shard simulation: stand-in all-reduce latency
   tp_overlap_chunks [2]    TP prefill: all-reduces pipelined over this many chunks
@@ -32,7 +33,7 @@ from __future__ import annotations
 import os
 from typing import Dict
 
-KEYS = {"fused_decode", "async_sched", "early_release", "spin_wait", "pf", "pf_m", "moe_pf", "gemm_ar", "krot", "m64_plans", "mw_plans",
+KEYS = {"fused_decode", "async_sched", "early_release", "spin_wait", "pf", "pf_m", "moe_pf", "gemm_ar", "gemm_ar_shared", "krot", "m64_plans", "mw_plans",
         "mw_max_tokens", "resid_inlaunch_kb", "decode_depth", "decode_max_splits", "ar_ll_max", "sim_ar_us",
         "tp_overlap_chunks", "tp_overlap_min_tokens", "ep_exact_min_pairs"}
 
