@@ -185,6 +185,15 @@ def _replica_delta(s0, s1, win) -> list:
     return out
 
 
+def _replica_requests(s0, s1) -> dict:
+    """Requests the router sent to each replica during the window (id -> count) and
+    the spread of that split: max / mean - 1 (0 = perfectly even)."""
+    r0 = {r["id"]: r.get("requests_dispatched", 0) for r in s0.get("replicas", [])}
+    per = {str(r["id"]): r.get("requests_dispatched", 0) - r0.get(r["id"], 0) for r in s1.get("replicas", [])}
+    mean = sum(per.values()) / max(1, len(per))
+    return {"per_replica": per, "imbalance": round(max(per.values()) / mean - 1, 4) if per and mean > 0 else None}
+
+
 def _report(a, st, s0, s1) -> dict:
     win = st["t1"] - st["t0"]
     m0, m1 = s0["metrics"], s1["metrics"]
@@ -203,6 +212,7 @@ def _report(a, st, s0, s1) -> dict:
         "server_prompt_tokens_per_sec": round(dp / win, 2), "server_generation_tokens_per_sec": round(dg / win, 2),
         "event_loop_lag_ms": m1.get("event_loop_lag_ms"), "client_procs": a.procs,
         "replica_window": _replica_delta(s0, s1, win),
+        "replica_requests": _replica_requests(s0, s1),
         "model": s1.get("model"),
     }
 
@@ -219,6 +229,7 @@ def main() -> int:
     ap.add_argument("--ready-timeout", type=float, default=900.0)
     ap.add_argument("--procs", type=int, default=4, help="client processes")
     ap.add_argument("--out", help="also append the JSON line to this file")
+    ap.add_argument("--label", help="added to the JSON line (bench/scale.sh)")
     a = ap.parse_args()
     if bool(a.url) == bool(a.launch):
         ap.error("give exactly one of --url / --launch")
@@ -233,6 +244,8 @@ def main() -> int:
             url = f"http://127.0.0.1:{port}"
         asyncio.run(_wait_ready(url, a.ready_timeout))
         res = run(a, url)
+        if a.label:
+            res["label"] = a.label
         line = json.dumps(res)
         print(line, flush=True)
         if a.out:

@@ -198,6 +198,7 @@ class InferenceServer:
         self._swap_lock: Optional[asyncio.Lock] = None
         self._reduced = False
         self.swaps = 0
+        self.dispatched: Dict[int, int] = {}  # requests sent per replica id (first sends and re-dispatches)
         self.hub = None  # FrontendHub when HTTP runs in front-end processes (api.frontends > 1)
         trace.configure(cfg.observability.tracing, cfg.observability.trace_sample_rate)
 
@@ -469,6 +470,7 @@ class InferenceServer:
         self.inflight[sreq.id] = sreq
         r.inflight[sreq.id] = sreq
         self.router.add_active(rid, 1)
+        self.dispatched[rid] = self.dispatched.get(rid, 0) + 1
         trace.end_span(sreq.qspan, replica=rid)
         sreq.espan = trace.start_span("engine", parent=sreq.qspan, request_id=sreq.id, replica=rid)
         r.submit(sreq.id, sreq.prompt_ids, copy.copy(sreq.params), sreq.priority, sreq.kind.value, sreq.sse_native)
@@ -982,6 +984,7 @@ class InferenceServer:
             reps.append({"id": s["id"], "healthy": s["healthy"], "active_requests": len(r.inflight) if r else 0,
                          "memory_used": s["memory_used"], "memory_available": s["memory_available"],
                          "kind": r.kind if r else None, "restarts": r.restarts if r else 0,
+                         "requests_dispatched": self.dispatched.get(s["id"], 0),
                          "heartbeat_age_s": r.heartbeat_age() if r else None, "engine": st})
         return {"model": self.model_name, "metrics": snap,
                 "queue_depth": {"high": h, "normal": n, "low": l, "total": t},
