@@ -50,8 +50,9 @@ def parse():
     ap.add_argument("--coalesce-max-wait", type=int, default=4, help="admission window bound, in steps")
     ap.add_argument("--moe-comm", default="auto", choices=["auto", "alltoall", "allreduce"])
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--weight-dtype", default=None, choices=["fp8"],
-                    help="fp8: E4M3 weight copies for batch <= 16 decode (not the bf16 headline)")
+    ap.add_argument("--weight-dtype", default=None, choices=["fp8", "int8", "int4"],
+                    help="weight-only copies for decode batches <= 64: fp8 (E4M3), int8 (per-channel) or int4 "
+                         "(per 128-k group) -- not the bf16 headline")
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--temperature", type=float, default=0.0,
                     help="sampling temperature of every request (0 = greedy, the headline)")
@@ -353,7 +354,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": ("bf16" if on_gpu else "fp32") if a.weight_dtype is None else "bf16 activations, fp8 (E4M3) decode weights",
+            "dtype": ("bf16" if on_gpu else "fp32") if a.weight_dtype is None else f"bf16 activations, {a.weight_dtype} decode weights",
             "data": "synthetic (random-token prompts, random-init weights)",
             "ttft_p50_ms": round(1000 * p50, 2) if p50 == p50 else None,
             "config": {"model": a.model, "global_batch": a.concurrency * dp,

@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--mw-sweep", action="store_true",
                     help="sweep gemm_mw (split, cfg) configurations at 64 < M <= 320 against hipBLASLt")
     ap.add_argument("--top", type=int, default=6, help="--mw-sweep: configurations printed per (shape, M)")
+    ap.add_argument("--splits", type=int, nargs="+", default=[1, 2, 3, 4, 5, 6, 8],
+                    help="--m64g-sweep: split-K values of the partial-sum mode")
     a = ap.parse_args()
     kernels()
     if a.m64g_sweep:
@@ -182,7 +184,7 @@ def m64g_sweep(a):
                     continue
                 for nw in ((2,) if mode == L.MODE_SILU else (1, 2)):
                     for S in ((1, 2, 4) if mode == L.MODE_SILU else (1,) if mode != L.MODE_PARTIAL else
-                              (1, 2, 3, 4, 5, 6, 8)):
+                              tuple(a.splits)):
                         cols = 16 * nw * waves[cfg]
                         if N % cols or K % kcs[cfg] or S > K // kcs[cfg] or (mode == L.MODE_SILU and K % (S * kcs[cfg])):
                             continue

@@ -21,6 +21,7 @@
 #   r4b/r4c  round-4 passes: AR + TP + prefetch A/B; Mixtral + profiles
 #   r4d      in-launch residual reduce + decode-attention depth A/Bs at 64 rows (step logs)
 #   r5a      gemm_pf: tests, per-projection A/B at the mixed-step rows, headline on / off + profile
+#   r6q      int8 / int4 / fp8 weight-only decode: kernel + engine tests, batch 1 and 64 concurrent
 #   r6a      GG_AR per-launch generations: custom all-reduce + TP engine tests, headline, 70B TP8 rank c1
 # Each GPU step has its own time limit; the first failure ends the suite.
 set -o pipefail
@@ -70,6 +71,12 @@ ab)
     n=$(echo "$s" | tr -c 'A-Za-z0-9_=\n' '_')
     run "driver_$n" 200 env $s $B --steps 20 --warmup 5 "$@"
     run "w400_$n" 250 env $s $B --steps 400 --warmup 40 "$@"
+  done ;;
+r6q)
+  pyt wq_tests 600 tests/test_wq_gpu.py tests/test_fp8_gpu.py
+  for q in int4 int8 fp8; do
+    run "c1_$q" 200 $B --concurrency 1 --steps 200 --warmup 20 --weight-dtype $q "$@"
+    run "c64_$q" 200 $B --steps 20 --warmup 5 --weight-dtype $q "$@"
   done ;;
 r6a)
   pyt tp_tests 900 tests/test_custom_ar_gpu.py tests/test_tp_gpu.py

@@ -17,11 +17,52 @@
 //   modes: W8_PARTIAL -> fp32 split-K partials [S, M, N] (reduced by the consumer
 //   kernel, like gemm_m64g's); W8_SILU -> bf16 silu(gate) * up from block-16
 //   interleaved gate|up rows (split 1).
+//
+// Weight formats (FMT; Req 10.3 quantization levels, weight-only, bf16 activations):
+//   WQ_FP8   E4M3 codes, fp32 scale per output channel (above);
+//   WQ_INT8  symmetric int8 codes, fp32 scale per output channel: each byte widened
+//            exactly (|q| <= 127 is a bf16 integer), scale in the epilogue as for FP8;
+//   WQ_INT4  symmetric 4-bit codes in groups of WQ_GROUP = 128 k per output channel,
+//            fp32 scale per (group, channel) [K / 128][N]. Stored offset-binary
+//            (u = q + 8) and packed so that one 32-bit word holds 8 consecutive k
+//            with element 2j at bits 4j and element 2j + 1 at bits 16 + 4j: one
+//            v_and_or per bf16 PAIR builds 0x4300 | u = 128 + u = 136 + q (exact
+//            bf16). The MFMA accumulates sum x (136 + q) per group; an all-ones
+//            MFMA gives sum x over the same group, and at each group end
+//            acc += s_group (acc_group - 136 sum x). Rows are KC / 2 bytes; the
+//            workgroup's scales are staged in LDS before the DMA pipeline starts
+//            (no VGPR-destination global load beside the in-flight LDS-DMA).
 #include "glds.h"
 
 namespace xgk {
 
 enum : int { W8_PARTIAL = 1, W8_SILU = 2 };
+enum : int { WQ_FP8 = 0, WQ_INT8 = 1, WQ_INT4 = 2 };
+constexpr int WQ_GROUP = 128;
+constexpr int WQ_SC_FLOATS = 4096;  // int4 scales staged per workgroup (groups x columns)
+
+// 8 int8 codes (k order) -> bf16x8 A fragment (exact)
+__device__ __forceinline__ bf16x8_t int8x8_to_bf16(uint2 v) {
+  uint32_t o[4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const uint32_t wv = j ? v.y : v.x;
+    const float a = static_cast<float>(static_cast<int8_t>(wv & 0xFF));
+    const float b = static_cast<float>(static_cast<int8_t>((wv >> 8) & 0xFF));
+    const float c = static_cast<float>(static_cast<int8_t>((wv >> 16) & 0xFF));
+    const float d = static_cast<float>(static_cast<int8_t>(wv >> 24));
+    // exact integers: the bf16 of each is its top 16 bits
+    o[2 * j] = (__float_as_uint(a) >> 16) | (__float_as_uint(b) & 0xFFFF0000u);
+    o[2 * j + 1] = (__float_as_uint(c) >> 16) | (__float_as_uint(d) & 0xFFFF0000u);
+  }
+  return as_frag(make_uint4(o[0], o[1], o[2], o[3]));
+}
+
+// 8 offset-binary nibbles (pair-interleaved, see WQ_INT4) -> bf16x8 of 136 + q
+__device__ __forceinline__ bf16x8_t u4x8_to_bf16(uint32_t v) {
+  return as_frag(make_uint4((v & 0x000F000Fu) | 0x43004300u, ((v >> 4) & 0x000F000Fu) | 0x43004300u,
+                            ((v >> 8) & 0x000F000Fu) | 0x43004300u, ((v >> 12) & 0x000F000Fu) | 0x43004300u));
+}
 
 // 8 E4M3 bytes (k order) -> bf16x8 A fragment
 __device__ __forceinline__ bf16x8_t fp8x8_to_bf16(uint2 v) {
@@ -40,13 +81,14 @@ __device__ __forceinline__ bf16x8_t fp8x8_to_bf16(uint2 v) {
 //   NW  16-column MFMA tiles per wave (SiLU needs 2: one gate + one up tile)
 //   WV  waves per workgroup
 //   KC  k per chunk (fp8 row = KC bytes, bf16 x row = 2 KC bytes)
-template <int NW, int WV, int KC, int MT>
+template <int NW, int WV, int KC, int MT, int FMT = WQ_FP8>
 __global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __restrict__ x, int M, int K,
                                                              const uint8_t* __restrict__ w,
                                                              const float* __restrict__ wscale, int N,
                                                              float* __restrict__ part, uint16_t* __restrict__ out,
                                                              int mode) {
-  constexpr int XRB = KC * 2, WRB = KC;          // bytes per LDS row
+  constexpr bool I4 = FMT == WQ_INT4;
+  constexpr int XRB = KC * 2, WRB = I4 ? KC / 2 : KC;  // bytes per LDS row
   constexpr int XG = XRB / 16, WG = WRB / 16;    // 16-B granules per row
   constexpr int XRPI = 1024 / XRB, WRPI = 1024 / WRB;  // rows per DMA instruction
   constexpr int XROWS = 16 * MT;
@@ -61,6 +103,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __r
   __shared__ __attribute__((aligned(1024))) uint8_t lds0[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds1[SLOT];
   __shared__ __attribute__((aligned(1024))) uint8_t lds2[SLOT];
+  // int4: this workgroup's group scales [group][column] (unused otherwise)
+  __shared__ __attribute__((aligned(16))) float sc_lds[I4 ? WQ_SC_FLOATS : 4];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -76,7 +120,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __r
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
       const int r = WRPI * i + dr;
-      wsrc[i] = w + static_cast<int64_t>(nbase + r) * K + k0 + 16 * (dj ^ (r & (WG - 1)));
+      wsrc[i] = w + static_cast<int64_t>(nbase + r) * (I4 ? K / 2 : K) + (I4 ? k0 / 2 : k0) +
+                16 * (dj ^ (r & (WG - 1)));
     }
   }
   const uint16_t* xsrc[XI];
@@ -94,7 +139,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __r
 #pragma unroll
     for (int i = 0; i < XI; ++i) glds16(xsrc[i] + kk, slot + XRPI * (wid * XI + i) * XRB);
 #pragma unroll
-    for (int i = 0; i < WI; ++i) glds16_nt(wsrc[i] + kk, slot + XBYTES + wid * WBYTES + i * 1024);
+    for (int i = 0; i < WI; ++i) glds16_nt(wsrc[i] + (I4 ? kk / 2 : kk), slot + XBYTES + wid * WBYTES + i * 1024);
   };
 
   f32x4_t acc[NW][MT];
@@ -102,9 +147,45 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __r
   for (int nt = 0; nt < NW; ++nt)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // int4: the open group's sum x (136 + q) and sum x (every row of an all-ones MFMA)
+  f32x4_t accg[I4 ? NW : 1][I4 ? MT : 1];
+  f32x4_t xs[I4 ? MT : 1];
+  constexpr int COLS = 16 * NW * WV;
+  const int g0 = k0 / WQ_GROUP;  // first group of this split
+  if constexpr (I4) {
+#pragma unroll
+    for (int nt = 0; nt < NW; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) accg[nt][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) xs[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // stage the scales before any LDS-DMA is in flight (host: groups x COLS <= WQ_SC_FLOATS)
+    const int ng = kws / WQ_GROUP, col0 = blockIdx.x * COLS;
+    for (int i = tid; i < ng * COLS; i += 64 * WV) sc_lds[i] = wscale[static_cast<int64_t>(g0 + i / COLS) * N + col0 +
+                                                                      i % COLS];
+    __syncthreads();
+  }
+  const bf16x8_t ones = as_frag(make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
+  // fold the group that ends at chunk c, k step t (int4)
+  auto fold = [&](int gi) {
+#pragma unroll
+    for (int nt = 0; nt < NW; ++nt) {
+      const float4 sc = *reinterpret_cast<const float4*>(sc_lds + gi * COLS + wid * WROWS + 16 * nt + 4 * g);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        acc[nt][mt][0] += sc.x * (accg[nt][mt][0] - 136.f * xs[mt][0]);
+        acc[nt][mt][1] += sc.y * (accg[nt][mt][1] - 136.f * xs[mt][1]);
+        acc[nt][mt][2] += sc.z * (accg[nt][mt][2] - 136.f * xs[mt][2]);
+        acc[nt][mt][3] += sc.w * (accg[nt][mt][3] - 136.f * xs[mt][3]);
+        accg[nt][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) xs[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  };
 
-  auto compute = [&](const uint8_t* slot) {
-    const uint8_t* xs = slot;
+  auto compute = [&](const uint8_t* slot, int c) {
+    const uint8_t* xsl = slot;
     const uint8_t* ws = slot + XBYTES + wid * WBYTES;
 #pragma unroll
     for (int t = 0; t < KC / 32; ++t) {
@@ -113,18 +194,33 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __r
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int xr = 16 * mt + li;
-        b[mt] = *reinterpret_cast<const uint4*>(xs + xr * XRB + (((4 * t + g) ^ (xr & (XG - 1))) * 16));
+        b[mt] = *reinterpret_cast<const uint4*>(xsl + xr * XRB + (((4 * t + g) ^ (xr & (XG - 1))) * 16));
       }
 #pragma unroll
       for (int nt = 0; nt < NW; ++nt) {
-        // W (A operand): row 16 nt + li, k = 32t + 8g.. -> fp8 granule 2t + g/2, byte (g & 1) * 8
         const int row = 16 * nt + li;
-        const uint2 a8 = *reinterpret_cast<const uint2*>(ws + row * WRB +
-                                                         (((2 * t + (g >> 1)) ^ (row & (WG - 1))) * 16) +
-                                                         (g & 1) * 8);
-        const bf16x8_t a = fp8x8_to_bf16(a8);
+        bf16x8_t a;
+        if constexpr (I4) {
+          // W row 16 nt + li, k = 32t + 8g.. -> 4-bit granule t, bytes 4g .. 4g + 3
+          a = u4x8_to_bf16(*reinterpret_cast<const uint32_t*>(ws + row * WRB + ((t ^ (row & (WG - 1))) * 16) +
+                                                              4 * g));
+        } else {
+          // W (A operand): row 16 nt + li, k = 32t + 8g.. -> byte granule 2t + g/2, byte (g & 1) * 8
+          const uint2 a8 = *reinterpret_cast<const uint2*>(ws + row * WRB +
+                                                           (((2 * t + (g >> 1)) ^ (row & (WG - 1))) * 16) +
+                                                           (g & 1) * 8);
+          a = FMT == WQ_INT8 ? int8x8_to_bf16(a8) : fp8x8_to_bf16(a8);
+        }
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = mfma16x16x32(a, as_frag(b[mt]), acc[nt][mt]);
+        for (int mt = 0; mt < MT; ++mt) {
+          if constexpr (I4) accg[nt][mt] = mfma16x16x32(a, as_frag(b[mt]), accg[nt][mt]);
+          else acc[nt][mt] = mfma16x16x32(a, as_frag(b[mt]), acc[nt][mt]);
+        }
+      }
+      if constexpr (I4) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) xs[mt] = mfma16x16x32(ones, as_frag(b[mt]), xs[mt]);
+        if ((t + 1) % (WQ_GROUP / 32) == 0) fold((c * KC + 32 * t) / WQ_GROUP);
       }
     }
   };
@@ -134,7 +230,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __r
     else wait_vmcnt<0>();
     raw_barrier();
     if (c + 2 < nchunks) issue(nxt2, c + 2);
-    compute(cur);
+    compute(cur, c);
   };
 
   issue(lds0, 0);
@@ -149,8 +245,9 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_w8_kernel(const uint16_t* __r
   if (c + 1 < nchunks) step(lds1, lds0, c + 1);
 
   // acc[nt][mt][r] = out[m = 16 mt + li][n = nbase + 16 nt + 4 g + r] / scale[n]
+  // (int4: the group scales are already folded in)
 #pragma unroll
-  for (int nt = 0; nt < NW; ++nt) {
+  for (int nt = 0; nt < (I4 ? 0 : NW); ++nt) {
     const float4 sc = *reinterpret_cast<const float4*>(wscale + nbase + 16 * nt + 4 * g);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -200,20 +297,12 @@ static int w8_cfg_cols(int cfg) {
 static int w8_cfg_kc(int cfg) { return cfg >= 3 ? 256 : 128; }
 static int w8_cfg_nw(int cfg) { return cfg == 2 ? 1 : 2; }
 
-int gemm_w8(const uint16_t* x, int M, int K, const uint8_t* w, const float* scale, int N, float* part,
-            uint16_t* out, int S, int mode, int cfg, hipStream_t st) {
-  if (M < 1 || M > 64 || S < 1 || cfg < 0 || cfg > 4) return 1;
-  if (M > 16 && cfg >= 3) return 1;  // KC 256 with four x tiles exceeds the LDS
-  if (mode != W8_PARTIAL && mode != W8_SILU) return 1;
-  const int cols = w8_cfg_cols(cfg), kc = w8_cfg_kc(cfg);
-  if (N % cols || K % (S * kc)) return 1;
-  if (mode == W8_SILU && (w8_cfg_nw(cfg) != 2 || S != 1 || out == nullptr)) return 1;
-  if (mode == W8_PARTIAL && part == nullptr) return 1;
-  const dim3 grid(N / cols, S);
-#define XGK_W8(NW, WV, KC, MT)                                                                               \
-  hipLaunchKernelGGL((gemm_w8_kernel<NW, WV, KC, MT>), grid, dim3(64 * WV), 0, st, x, M, K, w, scale, N, part, out, \
-                     mode)
-  const bool mt1 = M <= 16;
+template <int FMT>
+static void launch_w8(int cfg, bool mt1, dim3 grid, hipStream_t st, const uint16_t* x, int M, int K, const uint8_t* w,
+                      const float* scale, int N, float* part, uint16_t* out, int mode) {
+#define XGK_W8(NW, WV, KC, MT)                                                                                 \
+  hipLaunchKernelGGL((gemm_w8_kernel<NW, WV, KC, MT, FMT>), grid, dim3(64 * WV), 0, st, x, M, K, w, scale, N, part, \
+                     out, mode)
   switch (cfg) {
     case 0: if (mt1) XGK_W8(2, 4, 128, 1); else XGK_W8(2, 4, 128, 4); break;
     case 1: if (mt1) XGK_W8(2, 2, 128, 1); else XGK_W8(2, 2, 128, 4); break;
@@ -222,6 +311,25 @@ int gemm_w8(const uint16_t* x, int M, int K, const uint8_t* w, const float* scal
     default: XGK_W8(2, 4, 256, 1); break;
   }
 #undef XGK_W8
+}
+
+// fmt: WQ_FP8 / WQ_INT8 (scale [N]) or WQ_INT4 (w [N, K / 2] packed, scale [K / 128, N])
+int gemm_w8(const uint16_t* x, int M, int K, const uint8_t* w, const float* scale, int N, float* part,
+            uint16_t* out, int S, int mode, int cfg, hipStream_t st, int fmt) {
+  if (M < 1 || M > 64 || S < 1 || cfg < 0 || cfg > 4 || fmt < WQ_FP8 || fmt > WQ_INT4) return 1;
+  if (M > 16 && cfg >= 3) return 1;  // KC 256 with four x tiles exceeds the LDS
+  if (mode != W8_PARTIAL && mode != W8_SILU) return 1;
+  const int cols = w8_cfg_cols(cfg), kc = w8_cfg_kc(cfg);
+  if (N % cols || K % (S * kc)) return 1;
+  if (mode == W8_SILU && (w8_cfg_nw(cfg) != 2 || S != 1 || out == nullptr)) return 1;
+  if (mode == W8_PARTIAL && part == nullptr) return 1;
+  // int4: whole groups per split, and the workgroup's scales fit its LDS stage
+  if (fmt == WQ_INT4 && ((K / S) % WQ_GROUP || (K / S / WQ_GROUP) * cols > WQ_SC_FLOATS)) return 1;
+  const dim3 grid(N / cols, S);
+  const bool mt1 = M <= 16;
+  if (fmt == WQ_FP8) launch_w8<WQ_FP8>(cfg, mt1, grid, st, x, M, K, w, scale, N, part, out, mode);
+  else if (fmt == WQ_INT8) launch_w8<WQ_INT8>(cfg, mt1, grid, st, x, M, K, w, scale, N, part, out, mode);
+  else launch_w8<WQ_INT4>(cfg, mt1, grid, st, x, M, K, w, scale, N, part, out, mode);
   return 0;
 }
 

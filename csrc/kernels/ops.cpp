@@ -70,7 +70,7 @@ size_t sample_ws_row_bytes();
 void segment_sum(const uint16_t*, int, const int32_t*, const int32_t*, float*, int, hipStream_t);
 void subst_tokens(int32_t*, const int32_t*, const int32_t*, int, hipStream_t);
 int gemm_w8(const uint16_t*, int, int, const uint8_t*, const float*, int, float*, uint16_t*, int, int, int,
-            hipStream_t);
+            hipStream_t, int);
 void moe_topk_softmax(const void*, int, int, int, int, int, float*, int32_t*, hipStream_t);
 void moe_align(const int32_t*, int, int, int, int, int, int32_t*, int32_t*, int32_t*, hipStream_t);
 int moe_combine(const void*, int, int, const int32_t*, const float*, void*, int, int, int, hipStream_t, int);
@@ -220,11 +220,12 @@ PYBIND11_MODULE(_kernels, m) {
      py::arg("st"), py::arg("ws") = 0, py::arg("ws_rows") = 0);
   m.def("sample_ws_row_bytes", []() { return static_cast<int64_t>(xgk::sample_ws_row_bytes()); });
   m.def("gemm_w8", [](uintptr_t x, int M, int K, uintptr_t w, uintptr_t scale, int N, uintptr_t part, uintptr_t out,
-                      int splits, int mode, int cfg, uintptr_t st) {
+                      int splits, int mode, int cfg, uintptr_t st, int fmt) {
     check(xgk::gemm_w8(P<const uint16_t>(x), M, K, P<const uint8_t>(w), P<const float>(scale), N, P<float>(part),
-                       P<uint16_t>(out), splits, mode, cfg, S(st)),
+                       P<uint16_t>(out), splits, mode, cfg, S(st), fmt),
           "gemm_w8");
-  });
+  }, py::arg("x"), py::arg("M"), py::arg("K"), py::arg("w"), py::arg("scale"), py::arg("N"), py::arg("part"),
+     py::arg("out"), py::arg("splits"), py::arg("mode"), py::arg("cfg"), py::arg("st"), py::arg("fmt") = 0);
   m.def("subst_tokens", [](uintptr_t ids, uintptr_t src, uintptr_t prev, int n, uintptr_t st) {
     xgk::subst_tokens(P<int32_t>(ids), P<const int32_t>(src), P<const int32_t>(prev), n, S(st));
     check(0, "subst_tokens");

@@ -504,3 +504,26 @@ def test_priority_parse():
     assert Priority.parse("High") == Priority.High and Priority.parse("low") == Priority.Low
     with pytest.raises(ValueError):
         Priority.parse("URGENT")
+
+
+def test_weight_quantizers_roundtrip():
+    """INT8 / INT4 weight-only quantizers (Req 10.3): codes in range, dequantisation
+    within half a step of the input, and the int4 pair-interleaved packing (element
+    2j at bits 4j, element 2j + 1 at bits 16 + 4j of each word) decodes by hand."""
+    import torch
+    from xgserve.ops.linear import (WQ_INT4, WQ_INT8, dequantize_weight, quantize_weight)
+    g = torch.Generator().manual_seed(3)
+    w = torch.randn(48, 384, generator=g)
+    q, s = quantize_weight(w, WQ_INT8)
+    assert q.dtype == torch.uint8 and s.shape == (48,) and int(q.view(torch.int8).abs().max()) <= 127
+    assert float(((dequantize_weight(q, s, WQ_INT8) - w).abs() - s[:, None] / 2).max()) <= 1e-6
+    q4, s4 = quantize_weight(w, WQ_INT4)
+    assert q4.shape == (48, 192) and s4.shape == (3, 48)
+    d = dequantize_weight(q4, s4, WQ_INT4)
+    step = s4.t().repeat_interleave(128, dim=1)
+    assert float(((d - w).abs() - step / 2).max()) <= 1e-5
+    word = int(q4[5, 4:8].view(torch.int32)[0]) & 0xFFFFFFFF  # k = 8 .. 15 of row 5
+    for j in range(4):
+        for h in range(2):
+            u = (word >> (4 * j + 16 * h)) & 15
+            assert abs((u - 8) * float(s4[0, 5]) - float(d[5, 8 + 2 * j + h])) < 1e-6

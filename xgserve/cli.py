@@ -31,7 +31,7 @@ def _common(p: argparse.ArgumentParser) -> None:
     p.add_argument("--replicas", type=int, help="data-parallel replicas")
     p.add_argument("--gpus", help="comma-separated GPU ids, e.g. 0,1,2,3")
     p.add_argument("--device", help="force a device, e.g. cpu")
-    p.add_argument("--quantization", choices=["bf16", "fp16", "fp32", "fp8"],
+    p.add_argument("--quantization", choices=["bf16", "fp16", "fp32", "fp8", "int8", "int4"],
                    help="fp8: E4M3 weights (per-channel scales) for batch <= 16 decode, bf16 activations")
     p.add_argument("--strategy", choices=["round_robin", "least_loaded", "memory_aware"])
     p.add_argument("--batch-mode", choices=["continuous", "static"])

@@ -222,6 +222,13 @@ class LLMEngine:
             self.spec = SpeculativeDecoder(self, cfg.draft_model, cfg.num_speculative_tokens,
                                            cfg.spec_min_acceptance_rate)
         self._inflight = None  # (plan, handle): launched by the previous step() (async scheduling)
+        # Speculative decoding keeps the synchronous loop: asynchronous scheduling plans
+        # step N+1 before step N's tokens reach the host, which needs every row's next
+        # position and KV slot in advance -- exactly what verification leaves open (a
+        # row advances by 1..k+1 tokens, known only after the acceptance test), and the
+        # draft model's next proposal depends on those accepted tokens too. Planning for
+        # every acceptance length (k+1 plans per row) would defeat the point, so a
+        # speculating engine runs step by step.
         self._async = (cfg.async_schedule and tune.get_bool("async_sched", True)
                        and self.device.type == "cuda" and self.spec is None and bool(self.runner.graphs))
         log.info("engine ready: model=%s tp=%d blocks=%d (%.1f GiB KV) load=%.1fs", self.mcfg.name, get_state().tp_size,

@@ -38,7 +38,8 @@ from ..ops.linear import (MODE_PARTIAL, MODE_SILU, MW_MAX_M, W8_MAX_M, W8_MIN_EL
                           lm_head_linear, m64_ar_resid_linear, m64_linear, m64_norm_linear, m64_plan,
                           m64_resid_linear,
                           mw_linear, mw_plan, pf_linear, pf_plan, pick_split,
-                          quantize_fp8, skinny_linear, splitk_linear, splitk_prefill_ok, w8_linear, w8_plan)
+                          quantize_fp8, quantize_weight, skinny_linear, splitk_linear, splitk_prefill_ok, w8_linear,
+                          w8_plan, WQ_FORMATS)
 from .base import AttnMeta, PagedAttention, init_weight, kv_head_range, local_heads, shard
 from .config import ModelConfig
 
@@ -167,7 +168,7 @@ class LlamaLayer(nn.Module):
         self.pf_ok = self.fast_ok and bool(PF_SET) and tp == 1 and all(
             pf_plan(PF_MAX_M, n, k, mode) is not None for n, k, mode in mw_shapes)
         # M <= 16 too, when every projection has a measured small-M plan
-        self.w8 = None  # FP8 weight copies for batch <= 16 decode (LlamaForCausalLM.quantize_fp8)
+        self.w8 = None  # fp8 / int8 / int4 weight copies for decode (LlamaForCausalLM.quantize_weights)
         self.m64_small_ok = self.m64_ok and all(
             m64_plan(1, n, k, MODE_PARTIAL) is not None
             for n, k in ((Nqkv, H), (H, Hq * D)) + (() if self.moe else ((H, cfg.intermediate_size // tp),))) and (
@@ -178,7 +179,7 @@ class LlamaLayer(nn.Module):
         one, else the bf16 weight on gemm_m64g (same PendingSum / SiLU outputs)."""
         q = self.w8.get(name)
         if q is not None:
-            return w8_linear(x, q[0], q[1], mode)
+            return w8_linear(x, q[0], q[1], mode, fmt=q[2])
         return m64_linear(x, getattr(self, name), mode)
 
     def _ar(self, x: torch.Tensor) -> torch.Tensor:
@@ -555,29 +556,37 @@ class LlamaForCausalLM(nn.Module):
 
     @torch.no_grad()
     def quantize_fp8(self) -> bool:
-        """Weight-only FP8 for batch <= 16 decode: per dense layer, E4M3 copies of the
-        QKV / O / gate_up / down weights with per-output-channel scales (after the
-        RMSNorm folding). Prefill and larger batches keep the bf16 weights (MFMA-
-        bound there); the fused bf16 decode layer is disabled. Returns False (and
-        changes nothing) when a shape has no gemm_w8 plan or the model is MoE."""
+        return self.quantize_weights("fp8")
+
+    @torch.no_grad()
+    def quantize_weights(self, kind: str = "fp8") -> bool:
+        """Weight-only quantization for decode batches <= 64 (Req 10.3): per dense
+        layer, copies of the QKV / O / gate_up / down weights (after the RMSNorm
+        folding) as fp8 (E4M3, per-channel scale), int8 (per-channel scale) or int4
+        (per 128-k group scales), run by gemm_w8. Prefill and larger batches keep
+        the bf16 weights (MFMA-bound there); the fused bf16 decode layer is
+        disabled. Returns False (and changes nothing) when a shape has no gemm_w8
+        plan or the model is MoE."""
+        fmt = WQ_FORMATS[kind]
         if self.device.type != "cuda" or any(l.moe for l in self.layers):
             return False
         l0 = self.layers[0]
         names = ("qkv", "o", "gate_up", "down")
         for n in names:
             w = getattr(l0, n)
-            if w8_plan(1, w.shape[0], w.shape[1], MODE_SILU if n == "gate_up" else MODE_PARTIAL) is None:
+            mode = MODE_SILU if n == "gate_up" else MODE_PARTIAL
+            if any(w8_plan(m, w.shape[0], w.shape[1], mode, fmt) is None for m in (1, W8_MAX_M)):
                 return False
-        def use_fp8(n):  # small projections stay bf16 where gemm_m64g has a plan
+        def use_q(n):  # small projections stay bf16 where gemm_m64g has a plan
             w = getattr(l0, n)
             mode = MODE_SILU if n == "gate_up" else MODE_PARTIAL
             return w.numel() >= W8_MIN_ELEMS or not (l0.m64_small_ok and
                                                      m64_plan(1, w.shape[0], w.shape[1], mode) is not None)
-        chosen = [n for n in names if use_fp8(n)]
+        chosen = [n for n in names if use_q(n)]
         for l in self.layers:
-            l.w8 = {n: quantize_fp8(getattr(l, n)) for n in chosen}
+            l.w8 = {n: quantize_weight(getattr(l, n), fmt) + (fmt,) for n in chosen}
         self._fused_ok = self._fused_small_ok = False
-        self.weight_dtype = "fp8"
+        self.weight_dtype = kind
         return True
 
     def fused_decode_ok(self, meta: AttnMeta) -> bool:

@@ -30,8 +30,9 @@ def model_class(cfg: ModelConfig):
 def build_model(cfg: ModelConfig, device="cpu", dtype: Optional[torch.dtype] = None,
                 checkpoint: Optional[str] = None, seed: int = 0, tp: Optional[int] = None,
                 rank: Optional[int] = None, weight_dtype: Optional[str] = None):
-    """weight_dtype "fp8": also keep E4M3 weight copies for batch <= 16 decode
-    (LlamaForCausalLM.quantize_fp8); activations and everything else stay `dtype`."""
+    """weight_dtype "fp8" / "int8" / "int4": also keep quantized weight copies for
+    decode batches <= 64 (LlamaForCausalLM.quantize_weights); activations and
+    everything else stay `dtype`."""
     if dtype is None:
         dtype = torch.float32 if (cfg.dtype == "float32" and torch.device(device).type == "cpu") else torch.bfloat16
     m = model_class(cfg)(cfg, device=device, dtype=dtype, tp=tp, rank=rank)
@@ -41,9 +42,9 @@ def build_model(cfg: ModelConfig, device="cpu", dtype: Optional[torch.dtype] = N
         m.random_init(seed)
     if hasattr(m, "fold_norms"):
         m.fold_norms()  # RMSNorm weights into the projections (fused decode layer)
-    if weight_dtype == "fp8":
-        if not (hasattr(m, "quantize_fp8") and m.quantize_fp8()):
-            raise ValueError(f"fp8 weights are not supported for {cfg.name} on {device}")
+    if weight_dtype in ("fp8", "int8", "int4"):
+        if not (hasattr(m, "quantize_weights") and m.quantize_weights(weight_dtype)):
+            raise ValueError(f"{weight_dtype} weights are not supported for {cfg.name} on {device}")
     elif weight_dtype not in (None, "bf16", "fp16", "fp32"):
         raise ValueError(f"unknown weight_dtype {weight_dtype!r}")
     m.eval()

@@ -681,48 +681,131 @@ def dequantize_fp8(q: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
     return q.view(torch.float8_e4m3fn).float() * scale.float()[:, None]
 
 
-def w8_plan(M: int, N: int, K: int, mode: int):
+# ---------------------------------------------------------------------------- INT8 / INT4 weights
+# Req 10.3 quantization levels (the reference's Q8_0 / Q4_0 of llama.cpp, design.md:326-332),
+# weight-only on the same gemm_w8 pipeline (csrc/kernels/gemm_w8.hip, FMT):
+#   int8: symmetric, one fp32 scale per output channel (scale = max|w_row| / 127);
+#   int4: symmetric, one fp32 scale per 128-k group and output channel
+#         (scale = max|w_group| / 7, codes -8..7), packed two per byte.
+WQ_FP8, WQ_INT8, WQ_INT4 = 0, 1, 2
+WQ_FORMATS = {"fp8": WQ_FP8, "int8": WQ_INT8, "int4": WQ_INT4}
+WQ_GROUP = 128
+WQ_SC_FLOATS = 4096  # int4 scales one workgroup stages in LDS (groups x columns)
+
+
+def quantize_int8(w: torch.Tensor):
+    """[N, K] -> (int8 codes as uint8 [N, K], fp32 per-row scales [N])."""
+    wf = w.float()
+    scale = (wf.abs().amax(dim=1) / 127.0).clamp_min(1e-12)
+    q = torch.round(wf / scale[:, None]).clamp(-127, 127).to(torch.int8)
+    return q.view(torch.uint8).contiguous(), scale.contiguous()
+
+
+def dequantize_int8(q: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    return q.view(torch.int8).float() * scale.float()[:, None]
+
+
+def quantize_int4(w: torch.Tensor):
+    """[N, K] -> (packed uint8 [N, K / 2], fp32 group scales [K / 128, N]). Codes
+    q = round(w / s) in -8..7 are stored offset-binary (u = q + 8); each 32-bit word
+    holds 8 consecutive k, element 2j at bits 4j and element 2j + 1 at bits 16 + 4j
+    (the pair layout the kernel widens with one and_or per bf16 pair)."""
+    N, K = w.shape
+    if K % WQ_GROUP:
+        raise ValueError(f"int4 weights need K % {WQ_GROUP} == 0, got K={K}")
+    wf = w.float().view(N, K // WQ_GROUP, WQ_GROUP)
+    scale = (wf.abs().amax(dim=2) / 7.0).clamp_min(1e-12)  # [N, G]
+    u = (torch.round(wf / scale[:, :, None]).clamp(-8, 7) + 8).to(torch.int32).view(N, K // 8, 4, 2)
+    word = torch.zeros(N, K // 8, dtype=torch.int32, device=w.device)
+    for j in range(4):
+        word |= u[:, :, j, 0] << (4 * j)
+        word |= u[:, :, j, 1] << (16 + 4 * j)
+    packed = word.view(torch.uint8).view(N, K // 2)  # little-endian words
+    return packed.contiguous(), scale.t().contiguous()
+
+
+def dequantize_int4(packed: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    N = packed.shape[0]
+    K = packed.shape[1] * 2
+    word = packed.contiguous().view(torch.int32).view(N, K // 8)
+    u = torch.empty(N, K // 8, 4, 2, dtype=torch.int32, device=packed.device)
+    for j in range(4):
+        u[:, :, j, 0] = (word >> (4 * j)) & 15
+        u[:, :, j, 1] = (word >> (16 + 4 * j)) & 15
+    q = (u.view(N, K) - 8).float()
+    return q * scale.t().repeat_interleave(WQ_GROUP, dim=1).float()
+
+
+def quantize_weight(w: torch.Tensor, fmt: int):
+    return {WQ_FP8: quantize_fp8, WQ_INT8: quantize_int8, WQ_INT4: quantize_int4}[fmt](w)
+
+
+def dequantize_weight(q: torch.Tensor, scale: torch.Tensor, fmt: int) -> torch.Tensor:
+    return {WQ_FP8: dequantize_fp8, WQ_INT8: dequantize_int8, WQ_INT4: dequantize_int4}[fmt](q, scale)
+
+
+def _w8_fits(N: int, K: int, mode: int, S: int, cfg: int, M: int, fmt: int) -> bool:
+    cols, kc = W8_CFGS[cfg]
+    if N % cols or K % (S * kc) or (M > 16 and cfg >= 3) or (mode == MODE_SILU and (S != 1 or cfg == 2)):
+        return False
+    return fmt != WQ_INT4 or ((K // S) % WQ_GROUP == 0 and (K // S // WQ_GROUP) * cols <= WQ_SC_FLOATS)
+
+
+def w8_plan(M: int, N: int, K: int, mode: int, fmt: int = WQ_FP8):
     """(split_k, cfg) for gemm_w8, or None. SiLU needs split 1 and two 16-column
-    tiles per wave; otherwise the smallest split-K giving >= 256 workgroups."""
+    tiles per wave; otherwise the smallest split-K giving >= 256 workgroups. int4:
+    the measured plan with the split raised (or the tile narrowed) until the
+    workgroup's group scales fit its LDS stage."""
     if not (1 <= M <= W8_MAX_M):
         return None
     t = (_W8_TUNED if M <= 16 else _W8_TUNED64).get((N, K, mode))
-    if t is not None:
+    if t is None:
+        cfg = 1
+        cols, kc = W8_CFGS[cfg]
+        if N % cols or K % kc:
+            return None
+        if mode == MODE_SILU:
+            t = (1, cfg)
+        else:
+            S = 1
+            for s in (1, 2, 4, 8, 16):
+                if K % (s * kc):
+                    break
+                S = s
+                if (N // cols) * s >= 256:
+                    break
+            t = (S, cfg)
+    if _w8_fits(N, K, mode, t[0], t[1], M, fmt):
         return t
-    cfg = 1
-    cols, kc = W8_CFGS[cfg]
-    if N % cols or K % kc:
-        return None
-    if mode == MODE_SILU:
-        return 1, cfg
-    S = 1
-    for s in (1, 2, 4, 8, 16):
-        if K % (s * kc):
-            break
-        S = s
-        if (N // cols) * s >= 256:
-            break
-    return S, cfg
+    S0, cfg0 = t
+    for cfg in (cfg0, 1, 3, 0, 4, 2):
+        for S in ((S0, 2 * S0, 4 * S0, 8 * S0) if mode != MODE_SILU else (1,)):
+            if _w8_fits(N, K, mode, S, cfg, M, fmt):
+                return S, cfg
+    return None
 
 
 def w8_linear(x: torch.Tensor, q: torch.Tensor, scale: torch.Tensor, mode: int = MODE_PARTIAL,
-              plan=None, out: Optional[torch.Tensor] = None):
-    """x [M <= 16, K] bf16 . (diag(scale) q)^T: PendingSum (MODE_PARTIAL) or bf16
+              plan=None, out: Optional[torch.Tensor] = None, fmt: int = WQ_FP8):
+    """x [M <= 64, K] bf16 . W^T with W the dequantized weight (fmt WQ_FP8 / WQ_INT8:
+    diag(scale) q; WQ_INT4: group scales): PendingSum (MODE_PARTIAL) or bf16
     silu(gate) * up [M, N/2] from block-16 interleaved gate|up rows (MODE_SILU)."""
     M, K = x.shape
     N = q.shape[0]
-    p = plan or w8_plan(M, N, K, mode)
-    if p is None or not x.is_contiguous() or q.dtype != torch.uint8 or scale.dtype != torch.float32:
-        raise ValueError(f"gemm_w8: unsupported M={M} N={N} K={K} mode={mode}")
+    p = plan or w8_plan(M, N, K, mode, fmt)
+    kq = K // 2 if fmt == WQ_INT4 else K
+    if (p is None or not x.is_contiguous() or q.dtype != torch.uint8 or scale.dtype != torch.float32
+            or tuple(q.shape) != (N, kq) or scale.numel() != (N * (K // WQ_GROUP) if fmt == WQ_INT4 else N)):
+        raise ValueError(f"gemm_w8: unsupported M={M} N={N} K={K} mode={mode} fmt={fmt}")
     S, cfg = p
     k = kernels()
     if mode == MODE_PARTIAL:
         part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
         k.gemm_w8(x.data_ptr(), M, K, q.data_ptr(), scale.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, cfg,
-                  stream_ptr())
+                  stream_ptr(), fmt)
         return PendingSum(part, S)
     if out is None:
         out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=x.device)
     k.gemm_w8(x.data_ptr(), M, K, q.data_ptr(), scale.data_ptr(), N, 0, out.data_ptr(), 1, MODE_SILU, cfg,
-              stream_ptr())
+              stream_ptr(), fmt)
     return out

@@ -98,7 +98,10 @@ class WorkerSection:
     tp: int = 1                       # tensor-parallel degree per replica
     gpus: Optional[str] = None        # e.g. "0,1,2,3"; default 0..replicas*tp-1
     device: Optional[str] = None      # "cpu" forces the CPU path
-    quantization: str = "bf16"        # bf16 | fp16 | fp32 | fp8 (fp8 = E4M3 weights for decode batches <= 64, bf16 activations)
+    # bf16 | fp16 | fp32 | fp8 | int8 | int4: fp8 (E4M3, per-channel scale), int8 (per-channel)
+    # and int4 (per 128-k group scales) are weight-only copies for decode batches <= 64,
+    # bf16 activations (Req 10.3; the reference's Q8_0 / Q4_0 levels)
+    quantization: str = "bf16"
     block_size: int = 16
     max_num_seqs: int = 256
     max_num_batched_tokens: int = 8192
@@ -196,8 +199,8 @@ class ServerConfig:
         w = self.worker
         if w.replicas <= 0 or w.tp <= 0:
             e.append("worker.replicas and worker.tp must be > 0")
-        if w.quantization not in ("bf16", "fp16", "fp32", "fp8"):
-            e.append(f"worker.quantization {w.quantization!r} not supported (bf16|fp16|fp32|fp8)")
+        if w.quantization not in ("bf16", "fp16", "fp32", "fp8", "int8", "int4"):
+            e.append(f"worker.quantization {w.quantization!r} not supported (bf16|fp16|fp32|fp8|int8|int4)")
         if not (0.0 < w.gpu_memory_utilization <= 1.0):
             e.append("worker.gpu_memory_utilization must be in (0, 1]")
         if w.block_size % 16:

@@ -41,8 +41,9 @@ HEARTBEAT_S = 0.5
 def engine_spec(worker, cache=None, spec=None, fault: Optional[dict] = None, batcher=None) -> dict:
     """Plain-dict (picklable) description of one replica's engine. `fault` holds
     MockEngine fault-injection knobs (crash_after_steps, eos_every)."""
-    dt = {"bf16": "bfloat16", "fp16": "float16", "fp32": "float32", "fp8": "bfloat16"}[worker.quantization]
-    wdt = "fp8" if worker.quantization == "fp8" else None
+    dt = {"bf16": "bfloat16", "fp16": "float16", "fp32": "float32", "fp8": "bfloat16", "int8": "bfloat16",
+          "int4": "bfloat16"}[worker.quantization]
+    wdt = worker.quantization if worker.quantization in ("fp8", "int8", "int4") else None
     return dict(mock=worker.mock, mock_latency_ms=worker.mock_latency_ms, mock_kv_seqs=worker.mock_kv_seqs, model=worker.model,
                 checkpoint=worker.checkpoint, tp=worker.tp, device=worker.device, dtype=dt, weight_dtype=wdt,
                 block_size=worker.block_size, max_num_seqs=worker.max_num_seqs,
