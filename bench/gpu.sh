@@ -72,6 +72,11 @@ ab)
     run "driver_$n" 200 env $s $B --steps 20 --warmup 5 "$@"
     run "w400_$n" 250 env $s $B --steps 400 --warmup 40 "$@"
   done ;;
+r6s)  # m64g sweeps: deep four-x-tile rings at the 8B decode shapes (M 64), deep splits at M 1
+  pyt pf_tests 300 tests/test_pf_gpu.py
+  run sweep64 500 python -u bench/gemm_bench.py --m64g-sweep --M 64 --shapes qkv o down gate_up
+  run sweep1 600 python -u bench/gemm_bench.py --m64g-sweep --M 1 --shapes qkv70t8 o70t8 down70t8 gate_up70t8 qkv o down \
+      --splits 1 2 3 4 6 8 10 12 16 20 24 32 ;;
 r6q)
   pyt wq_tests 600 tests/test_wq_gpu.py tests/test_fp8_gpu.py
   for q in int4 int8 fp8; do

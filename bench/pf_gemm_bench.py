@@ -67,7 +67,6 @@ def main():
     ap.add_argument("--M", type=int, nargs="+", default=[575, 1024, 2048])
     ap.add_argument("--cfgs", type=int, nargs="+", default=None, help="gemm_pf cfgs to time (default: the plan's)")
     ap.add_argument("--splits", type=int, nargs="+", default=None)
-    ap.add_argument("--sk", type=int, nargs="+", default=None, help="stream-K grids to time (0 = data-parallel)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-check", action="store_true")
@@ -94,18 +93,14 @@ def main():
             cfgs = a.cfgs if a.cfgs is not None else [plan[1]]
             splits = a.splits if (a.splits is not None and mode == L.MODE_PARTIAL) else [plan[0]]
             variants = {}
-            sks = a.sk if a.sk is not None else [plan[2]]
             for cfg in cfgs:
                 for S in splits:
-                    for skg in (sks if S == 1 else [0]):
-                        if skg and L.PF_CFG_BM[cfg % 16] > L.PF_SK_MAX_BM:
-                            continue
-                        variants[f"pf_c{cfg}_s{S}" + (f"_sk{skg}" if skg else "")] = (S, cfg, skg)
+                    variants[f"pf_c{cfg}_s{S}"] = (S, cfg)
             probes = {}
             if a.probe:
-                for k, (S, cfg, skg) in list(variants.items()):
-                    probes[k + "_nodma"] = (S, cfg % 16 + 16, skg)
-                    probes[k + "_nomfma"] = (S, cfg % 16 + 32, skg)
+                for k, (S, cfg) in list(variants.items()):
+                    probes[k + "_nodma"] = (S, cfg % 16 + 16)
+                    probes[k + "_nomfma"] = (S, cfg % 16 + 32)
             if not a.no_check:
                 r = ref(x, ws[0], mode)
                 for k, p in variants.items():

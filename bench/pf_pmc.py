@@ -24,7 +24,7 @@ x = torch.randn(a.M, a.K, device="cuda").bfloat16()
 w = (torch.randn(a.N, a.K, device="cuda") * 0.02).bfloat16()
 for cfg in a.cfgs:
     for _ in range(a.iters):
-        L.pf_linear(x, w, L.MODE_SILU, plan=(1, cfg, 0))
+        L.pf_linear(x, w, L.MODE_SILU, plan=(1, cfg))
 for _ in range(a.iters):
     F.linear(x, w)
 torch.cuda.synchronize()

@@ -138,24 +138,6 @@ __device__ __forceinline__ void pf_wait(bool steady) {
   else wait_vmcnt<0>();
 }
 
-// Stream-K (sk_grid > 0): `sk_grid` persistent workgroups split the TM x TN x nk
-// K-tile iterations evenly, so a grid whose tile count is not a multiple of the CU
-// count (336 tiles of the 8B gate_up at M = 575 on 256 CUs) runs ~1.3 tile-times
-// instead of 2. Workgroup g owns iterations [start(g), start(g+1)), start(g) =
-// floor(g I / G): a suffix of one tile, whole tiles, a prefix of another. A tile
-// finished by several workgroups is combined by the last arriver: every other
-// contributor writes its fp32 accumulators (lane-major, write-through sc1) to its
-// workspace slot (g, 0) if the tile holds the START of its range, else (g, 1), then
-// adds its iteration count to the tile's ticket (relaxed, agent scope); the one
-// whose add completes nk acquires, adds every other contributor's slot into its
-// registers and runs the epilogue (Guideline 16 / §5 "In-launch split-K
-// reduction", sc1 form). Tickets re-arm themselves (the last arriver zeroes them).
-struct PfSk {
-  float* ws;      // [sk_grid][2][512 threads x ACC floats]
-  int* tickets;   // [tiles], zero between launches
-  int grid;       // 0: data-parallel (grid = tiles x S)
-};
-
 // Grouped (MoE expert) form, GRP: the M dimension is moe_align's expert-sorted,
 // 64-padded row space [P]; expert e owns rows [offs[e], offs[e + 1]) and its own
 // weight w + e * w_stride. Tile slot mi of a column tile walks the experts' tiles in
@@ -170,11 +152,11 @@ struct PfGrp {
   int64_t w_stride;  // elements between two experts' [N, K] weights
 };
 
-template <int BM, int MTP, bool NT, int PR = 0, bool SKM = false, int LAG = 1, bool GRP = false>
+template <int BM, int MTP, bool NT, int PR = 0, int LAG = 1, bool GRP = false>
 __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restrict__ x, int M, int K,
                                                           const uint16_t* __restrict__ w, int N, int S,
                                                           float* __restrict__ part, uint16_t* __restrict__ out,
-                                                          int mode, int krot, PfSk sk, PfGrp grp) {
+                                                          int mode, int krot, PfGrp grp) {
   // MTP: 16-row m tiles per wave per phase -> a phase is MTP x 4 x 2 MFMAs per wave
   // and releases 32 MTP A rows = 4 MTP DMA pieces of 8 rows; wave w issues pieces
   // w, w + 8, ... (MTP = 3: 12 pieces -> waves 0-3 two, waves 4-7 one; NA0 / NA1 are
@@ -190,11 +172,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
   constexpr int SLOT = ASZ + BN * 128;     // + the W image
   constexpr int NACC = P * MTP * 4;        // f32x4 accumulators per lane
   static_assert(P >= 2 && P * 32 * MTP == BM && MTP >= 2 && MTP <= 4 && NA1 >= 1, "gemm_pf geometry");
-  static_assert(2 * SLOT + 16 <= 160 * 1024, "LDS");
-  // ONE __shared__ object (cdna_hip_programming.md §5 "Three .s-level traps" (a));
-  // the last 16 bytes hold the stream-K "last arriver" flag
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * SLOT + 16];
-  int* const sk_flag = reinterpret_cast<int*>(smem + 2 * SLOT);
+  static_assert(2 * SLOT <= 160 * 1024, "LDS");
+  // ONE __shared__ object (cdna_hip_programming.md §5 "Three .s-level traps" (a))
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * SLOT];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -425,7 +405,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
     }
   };
 
-  if constexpr (!SKM) {  // data-parallel: one (tile, split) per workgroup
+  // data-parallel: one (tile, split) per workgroup
+  {
     // GRP: the tile slots past the experts' last tile are empty and sit at the end of
     // the order, so the dispatch order itself (block b on XCD b % 8) spreads the real
     // tiles over every XCD; the XCD-contiguous order v would leave whole XCDs idle
@@ -455,87 +436,15 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const uint16_t* __restr
     const int kt_lo = s * nk_all / S;
     compute(m0, n0, kt_lo, (s + 1) * nk_all / S - kt_lo, m_hi, wb);
     epilogue(m0, n0, s, m_hi);
-  } else {  // stream-K
-    const int64_t I = static_cast<int64_t>(per_split) * nk_all;
-    const int G = sk.grid;
-    auto start = [&](int gg) { return static_cast<int64_t>(gg) * I / G; };
-    auto slot_of = [&](int gg, int tile) {  // workspace slot of contributor gg to `tile`
-      return sk.ws + (static_cast<int64_t>(gg) * 2 + (start(gg) >= static_cast<int64_t>(tile) * nk_all ? 0 : 1)) *
-                         (512 * NACC * 4);
-    };
-    const int64_t it_hi = start(v + 1);
-    for (int64_t it = start(v); it < it_hi;) {
-      const int tile = static_cast<int>(it / nk_all);
-      const int k0 = static_cast<int>(it - static_cast<int64_t>(tile) * nk_all);
-      const int k1 = static_cast<int>(min(static_cast<int64_t>(nk_all), k0 + (it_hi - it)));
-      it += k1 - k0;
-      int m0, n0;
-      tile_mn(tile, m0, n0);
-      compute(m0, n0, k0, k1 - k0, M, w);
-      if (k0 != 0 || k1 != nk_all) {
-        // a shared tile: publish, then the last arriver combines
-        float* mine = slot_of(v, tile) + tid * 4;
-#pragma unroll
-        for (int q = 0; q < P; ++q)
-#pragma unroll
-          for (int mt = 0; mt < MTP; ++mt)
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) st16_sc1(mine + ((q * MTP + mt) * 4 + nt) * 512 * 4, acc[q][mt][nt]);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains (write-through)
-        __syncthreads();
-        if (tid == 0) {
-          const int prev = __hip_atomic_fetch_add(sk.tickets + tile, k1 - k0, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-          const int last = prev + (k1 - k0) == nk_all;
-          if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(sk.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          *sk_flag = last;
-        }
-        __syncthreads();
-        if (*sk_flag == 0) continue;
-        // contributors: the workgroups owning iterations [tile nk, tile nk + nk)
-        // (grid > iterations: workgroups between them may own none and never stored)
-        const int64_t t_lo = static_cast<int64_t>(tile) * nk_all;
-        const int g_lo = static_cast<int>(((t_lo + 1) * G - 1) / I);
-        const int g_hi = static_cast<int>(((t_lo + nk_all) * G - 1) / I);
-        for (int gg = g_lo; gg <= g_hi; ++gg) {
-          if (gg == v || start(gg) == start(gg + 1)) continue;
-          const float* other = slot_of(gg, tile) + tid * 4;
-#pragma unroll
-          for (int q = 0; q < P; ++q)
-#pragma unroll
-            for (int mt = 0; mt < MTP; ++mt)
-#pragma unroll
-              for (int nt = 0; nt < 4; ++nt) {
-                const float4 o = *reinterpret_cast<const float4*>(other + ((q * MTP + mt) * 4 + nt) * 512 * 4);
-                acc[q][mt][nt] += f32x4_t{o.x, o.y, o.z, o.w};
-              }
-        }
-      }
-      epilogue(m0, n0, 0, M);
-    }
   }
 }
 
 template <int BM, int MTP, bool NT, int PR = 0, int LAG = 1>
 static int launch_pf(int tiles, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N, int S,
-                     float* part, uint16_t* out, int mode, PfSk sk) {
+                     float* part, uint16_t* out, int mode) {
   const PfGrp ng{nullptr, nullptr, 0, 0, 0};
-  // stream-K: tiles up to 256 rows (the 288-row variant spills the combine's registers)
-  if constexpr (BM <= 256) {
-    if (sk.grid) {
-      hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, true, LAG>), dim3(sk.grid), dim3(512), 0, st, x, M, K, w, N, S,
-                         part, out, mode, pf_krot, sk, ng);
-      return static_cast<int>(hipGetLastError());
-    }
-  } else if (sk.grid) {
-    return 1;
-  }
-  hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, false, LAG>), dim3(tiles * S), dim3(512), 0, st, x, M, K, w, N, S,
-                     part, out, mode, pf_krot, sk, ng);
+  hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, NT, PR, LAG>), dim3(tiles * S), dim3(512), 0, st, x, M, K, w, N, S, part,
+                     out, mode, pf_krot, ng);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -556,31 +465,27 @@ int pf_cfg_bm(int cfg) {
 
 template <int PR>
 static int launch_pf_cfg(int c, int tiles, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N,
-                         int S, float* part, uint16_t* out, int mode, PfSk sk) {
+                         int S, float* part, uint16_t* out, int mode) {
   switch (c) {
-    case 0: return launch_pf<256, 2, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    case 1: return launch_pf<192, 2, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    case 2: return launch_pf<128, 2, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    case 3: return launch_pf<256, 4, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    case 4: return launch_pf<192, 3, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    case 5: return launch_pf<288, 3, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    case 6: return launch_pf<288, 3, false, PR, 2>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    case 7: return launch_pf<256, 2, false, PR, 2>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    case 8: return launch_pf<192, 2, false, PR, 2>(tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 0: return launch_pf<256, 2, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode);
+    case 1: return launch_pf<192, 2, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode);
+    case 2: return launch_pf<128, 2, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode);
+    case 3: return launch_pf<256, 4, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode);
+    case 4: return launch_pf<192, 3, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode);
+    case 5: return launch_pf<288, 3, false, PR>(tiles, st, x, M, K, w, N, S, part, out, mode);
+    case 6: return launch_pf<288, 3, false, PR, 2>(tiles, st, x, M, K, w, N, S, part, out, mode);
+    case 7: return launch_pf<256, 2, false, PR, 2>(tiles, st, x, M, K, w, N, S, part, out, mode);
+    case 8: return launch_pf<192, 2, false, PR, 2>(tiles, st, x, M, K, w, N, S, part, out, mode);
     default: return 1;
   }
 }
-
-// sk_grid > 0: stream-K over sk_grid persistent workgroups (S must be 1); ws holds
-// sk_grid x 2 x pf_sk_slot_floats(cfg) floats, tickets one zeroed int per tile
-int pf_sk_slot_floats(int cfg) { return 512 * (pf_cfg_bm(cfg) / 32) * 4 * 4; }
 
 // grouped (MoE): data-parallel only, no K rotation
 template <int BM, int MTP, int LAG>
 static int launch_pf_grp(int tiles, hipStream_t st, const uint16_t* x, int M, int K, const uint16_t* w, int N, int S,
                          float* part, uint16_t* out, int mode, const PfGrp& grp) {
-  hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, false, 0, false, LAG, true>), dim3(tiles * S), dim3(512), 0, st, x, M, K,
-                     w, N, S, part, out, mode, 0, PfSk{nullptr, nullptr, 0}, grp);
+  hipLaunchKernelGGL((gemm_pf_kernel<BM, MTP, false, 0, LAG, true>), dim3(tiles * S), dim3(512), 0, st, x, M, K, w, N,
+                     S, part, out, mode, 0, grp);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -613,10 +518,9 @@ int gemm_pf_grouped(const uint16_t* x, const int32_t* rows, const int32_t* offs,
 }
 
 int gemm_pf(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* part, uint16_t* out, int S, int mode,
-            int cfg, int sk_grid, float* sk_ws, int* sk_tickets, hipStream_t st) {
+            int cfg, hipStream_t st) {
   if (M < 1 || K < 64 || K % 64 || N < pf::BN || N % pf::BN || S < 1 || S > K / 64 || cfg < 0 || cfg >= 48)
     return 1;
-  if (sk_grid < 0 || (sk_grid > 0 && (S != 1 || sk_ws == nullptr || sk_tickets == nullptr))) return 1;
   if (mode == PF_PARTIAL) {
     if (part == nullptr) return 1;
   } else if (mode == PF_BF16 || mode == PF_SILU) {
@@ -626,12 +530,11 @@ int gemm_pf(const uint16_t* x, int M, int K, const uint16_t* w, int N, float* pa
   }
   const int bm = pf_cfg_bm(cfg);
   const int tiles = ((M + bm - 1) / bm) * (N / pf::BN);
-  const PfSk sk{sk_ws, sk_tickets, sk_grid};
   switch (cfg / 16) {
-    case 0: return launch_pf_cfg<0>(cfg % 16, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 0: return launch_pf_cfg<0>(cfg % 16, tiles, st, x, M, K, w, N, S, part, out, mode);
 #ifdef XGK_PROBES  // anatomy probes (no DMA / no MFMA): measurement builds only (xgserve/_build.py --probes)
-    case 1: return launch_pf_cfg<1>(cfg % 16, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
-    default: return launch_pf_cfg<2>(cfg % 16, tiles, st, x, M, K, w, N, S, part, out, mode, sk);
+    case 1: return launch_pf_cfg<1>(cfg % 16, tiles, st, x, M, K, w, N, S, part, out, mode);
+    default: return launch_pf_cfg<2>(cfg % 16, tiles, st, x, M, K, w, N, S, part, out, mode);
 #else
     default: return 1;
 #endif

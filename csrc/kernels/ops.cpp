@@ -29,9 +29,7 @@ int gemm_m64g_ar(const uint16_t*, int, int, const uint16_t*, int, float*, int, i
 int m64g_ar_desc_bytes();
 int gemm_pf_grouped(const uint16_t*, const int32_t*, const int32_t*, int, int, int, const uint16_t*, int, int, float*,
                     uint16_t*, int, int, int, hipStream_t);
-int gemm_pf(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, int, float*, int*,
-            hipStream_t);
-int pf_sk_slot_floats(int);
+int gemm_pf(const uint16_t*, int, int, const uint16_t*, int, float*, uint16_t*, int, int, int, hipStream_t);
 void set_pf_krot(int);
 void set_k_rotation(int mode);
 void add_partials_resid(const float*, int, int, uint16_t*, float*, int, hipStream_t, uint64_t);
@@ -268,9 +266,9 @@ PYBIND11_MODULE(_kernels, m) {
   });
   // prompt-sized MFMA GEMM (gemm_pf.hip): mixed steps above gemm_mw's range, prefill
   m.def("gemm_pf", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,
-                      int mode, int cfg, int sk_grid, uintptr_t sk_ws, uintptr_t sk_tickets, uintptr_t st) {
+                      int mode, int cfg, uintptr_t st) {
     check(xgk::gemm_pf(P<uint16_t>(x), M, K, P<uint16_t>(w), N, P<float>(part), P<uint16_t>(out), splits, mode, cfg,
-                       sk_grid, P<float>(sk_ws), P<int>(sk_tickets), S(st)),
+                       S(st)),
           "gemm_pf");
   });
   // grouped form over moe_align's expert-sorted rows (the prompt-sized expert GEMMs)
@@ -281,7 +279,6 @@ PYBIND11_MODULE(_kernels, m) {
                                max_pairs, P<float>(part), P<uint16_t>(out), splits, mode, cfg, S(st)),
           "gemm_pf_grouped");
   });
-  m.def("pf_sk_slot_floats", &xgk::pf_sk_slot_floats);
   m.def("set_pf_krot", [](int on) { xgk::set_pf_krot(on); });
   m.def("set_k_rotation", [](int mode) { xgk::set_k_rotation(mode); });
   m.def("gemm_m64g_ex", [](uintptr_t x, int M, int K, uintptr_t w, int N, uintptr_t part, uintptr_t out, int splits,

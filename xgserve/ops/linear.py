@@ -89,7 +89,9 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, split_k: Optional[int] = Non
 # 8-10: deep LDS rings (5 / 4 / 6 slots) for M <= 16 -- more weight bytes in flight per CU
 M64G_CFGS = {0: (4, 128, False), 1: (4, 128, True), 2: (4, 64, False), 3: (4, 64, True),
              4: (2, 64, False), 5: (2, 64, True), 6: (2, 128, True), 7: (8, 64, True),
-             8: (2, 128, True), 9: (4, 128, True), 10: (2, 64, True)}
+             8: (2, 128, True), 9: (4, 128, True), 10: (2, 64, True),
+             # deep rings with four x tiles (16 < M <= 64): 6 / 6 / 4 slots of KC 64
+             11: (4, 64, True), 12: (2, 64, True), 13: (4, 64, True)}
 M64G_SMALL_ONLY = (8, 9, 10)
 
 # Measured on MI355X with cold weights (bench/gemm_bench.py --m64g-sweep,
@@ -299,7 +301,8 @@ def mw_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, plan=N
 # ---------------------------------------------------------------------------- gemm_pf (prompt-sized M)
 # csrc/kernels/gemm_pf.hip: BM x 256 output tiles on 8 waves, 64-deep K tiles consumed
 # in phases with the next tiles' LDS-DMA in flight across the barriers, waves 4-7 one
-# barrier behind waves 0-3 (MFMA / load ping-pong per SIMD), stream-K option.
+# barrier behind waves 0-3 (MFMA / load ping-pong per SIMD). (A stream-K form measured
+# 164 vs 121 us at the 575-row gate_up and was removed, profiles/r5_pf_gemm.md.)
 # cfg -> (BM, m tiles per wave per phase): 0 (256, 2) 1 (192, 2) 2 (128, 2) 3 (256, 4)
 # 4 (192, 3) 5 (288, 3).
 PF_CFG_BM = {0: 256, 1: 192, 2: 128, 3: 256, 4: 192, 5: 288, 6: 288, 7: 256, 8: 192}
@@ -312,8 +315,6 @@ _PF_CFG_KT_US = {2: 1.07, 4: 1.34, 8: 1.37, 3: 1.75, 7: 1.51, 6: 1.77}   # cfg -
 _PF_CFG_BM_ = {2: 128, 4: 192, 8: 192, 3: 256, 7: 256, 6: 288}
 PF_WG_US = 5.0
 PF_WG_OUT_GBS = 60.0
-PF_SK_OVERHEAD = 1.45    # stream-K (shared tiles: partial slots, pipeline restarts, lost W reuse)
-PF_SK_MAX_BM = 256       # the 288-row tile has no register room for the stream-K loop
 
 
 def pf_bm(M: int) -> int:
@@ -334,10 +335,10 @@ def cu_count(device=None) -> int:
 
 @functools.lru_cache(maxsize=4096)  # (eager mixed steps call it per projection: ~10 us of host time)
 def pf_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL, cus: int = 256):
-    """(split_k, cfg, sk_grid) for gemm_pf, or None when the shape is unsupported.
-    Every cfg of _PF_CFG_KT_US is priced with the model above: data-parallel (PARTIAL:
-    with split-K up to one round of workgroups; the fp32 partials' round trip through
-    the consumer is added), or stream-K over `cus` workgroups (bf16 / SiLU)."""
+    """(split_k, cfg) for gemm_pf, or None when the shape is unsupported. Every cfg of
+    _PF_CFG_KT_US is priced with the model above (PARTIAL: with split-K up to one
+    round of workgroups; the fp32 partials' round trip through the consumer is
+    added)."""
     if M < 1 or N % 256 or K % 64 or K < 64:
         return None
     nk = K // 64
@@ -353,41 +354,13 @@ def pf_plan(M: int, N: int, K: int, mode: int = MODE_PARTIAL, cus: int = 256):
             while tiles * (S + 1) <= cus and (S + 1) <= K // 256:
                 S += 1
             # + the consumer's read of the extra fp32 slabs (~7 TB/s; their writes are in wg)
-            cands.append(((-(-tiles * S // cus)) * (wg + -(-nk // S) * kt) + (S - 1) * M * N * 4 / 7e6, S, 0))
+            cands.append(((-(-tiles * S // cus)) * (wg + -(-nk // S) * kt) + (S - 1) * M * N * 4 / 7e6, S))
         else:
-            cands.append((-(-tiles // cus) * (wg + nk * kt), 1, 0))
-            if bm <= PF_SK_MAX_BM and tiles % cus:
-                cands.append((wg + tiles * nk / cus * kt * PF_SK_OVERHEAD, 1, cus))
-        for c in cands:
-            t, S_, skg = c[0], c[1], c[2]
+            cands.append((-(-tiles // cus) * (wg + nk * kt), 1))
+        for t, S_ in cands:
             if best is None or t < best[0]:
-                best = (t, S_, cfg, skg)
-    return best[1], best[2], best[3]
-
-
-class _SkWorkspace:
-    def __init__(self):
-        self.ws = {}
-        self.tickets = {}
-        self.retired = []
-
-    def get(self, device, grid: int, cfg: int, tiles: int):
-        key = str(device)
-        need = grid * 2 * kernels().pf_sk_slot_floats(cfg)
-        w = self.ws.get(key)
-        if w is None or w.numel() < need:
-            if w is not None:
-                self.retired.append(w)  # captured graphs may still point at it
-            w = self.ws[key] = torch.empty(need, dtype=torch.float32, device=device)
-        t = self.tickets.get(key)
-        if t is None or t.numel() < tiles:
-            if t is not None:
-                self.retired.append(t)
-            t = self.tickets[key] = torch.zeros(max(tiles, 4096), dtype=torch.int32, device=device)
-        return w, t
-
-
-_PF_SK = _SkWorkspace()
+                best = (t, S_, cfg)
+    return best[1], best[2]
 
 
 def pf_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_BF16, plan=None,
@@ -400,21 +373,15 @@ def pf_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_BF16, plan=None
     p = plan or pf_plan(M, N, K, mode, cu_count(x.device) if x.is_cuda else 256)
     if p is None or not x.is_contiguous() or not w.is_contiguous():
         raise ValueError(f"gemm_pf: unsupported M={M} N={N} K={K} mode={mode}")
-    S, cfg, skg = p if len(p) == 3 else (p[0], p[1], 0)
+    S, cfg = p[0], p[1]
     k = kernels()
-    wsp = tk = 0
-    if skg:
-        bm = PF_CFG_BM[cfg % 16]
-        wt, tt = _PF_SK.get(x.device, skg, cfg, -(-M // bm) * (N // 256))
-        wsp, tk = wt.data_ptr(), tt.data_ptr()
     if mode == MODE_PARTIAL:
         part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
-        k.gemm_pf(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, cfg, skg, wsp, tk,
-                  stream_ptr())
+        k.gemm_pf(x.data_ptr(), M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_PARTIAL, cfg, stream_ptr())
         return PendingSum(part, S)
     if out is None:
         out = torch.empty(M, N // 2 if mode == MODE_SILU else N, dtype=torch.bfloat16, device=x.device)
-    k.gemm_pf(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), S, mode, cfg, skg, wsp, tk, stream_ptr())
+    k.gemm_pf(x.data_ptr(), M, K, w.data_ptr(), N, 0, out.data_ptr(), S, mode, cfg, stream_ptr())
     return out
 
 
