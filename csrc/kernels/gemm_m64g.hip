@@ -1089,10 +1089,6 @@ static void launch_m64g(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, i
 #define XGK_M64G_DEEP(WV, KC, NT, NSV)                                                                             \
   hipLaunchKernelGGL((gemm_m64g_kernel<NW, WV, KC, NT, 1, NSV>), grid, dim3(64 * WV), 0, st, x, M, K, w, N, part, \
                      out, mode, epi)
-// deep-ring four-x-tile configurations (KC 64: 16-24 KB slots, 4-5 chunks in flight)
-#define XGK_M64G4_DEEP(WV, KC, NT, NSV)                                                                            \
-  hipLaunchKernelGGL((gemm_m64g_kernel<NW, WV, KC, NT, 4, NSV>), grid, dim3(64 * WV), 0, st, x, M, K, w, N, part, \
-                     out, mode, epi)
   switch (cfg) {
     case 1: XGK_M64G(4, 128, true); break;
     case 2: XGK_M64G4(4, 64, false); break;
@@ -1104,29 +1100,23 @@ static void launch_m64g(int cfg, dim3 grid, hipStream_t st, const uint16_t* x, i
     case 8: XGK_M64G_DEEP(2, 128, true, 5); break;
     case 9: XGK_M64G_DEEP(4, 128, true, 4); break;
     case 10: XGK_M64G_DEEP(2, 64, true, 6); break;
-    case 11: XGK_M64G4_DEEP(4, 64, true, 6); break;
-    case 12: XGK_M64G4_DEEP(2, 64, true, 6); break;
-    case 13: XGK_M64G4_DEEP(4, 64, true, 4); break;
     default: XGK_M64G(4, 128, false); break;
   }
 #undef XGK_M64G
 #undef XGK_M64G4
 #undef XGK_M64G_DEEP
-#undef XGK_M64G4_DEEP
 }
 
-int m64g_cfg_waves(int cfg) {
-  return (cfg == 7) ? 8 : (cfg == 9 || cfg == 11 || cfg == 13) ? 4 : (cfg >= 4 ? 2 : 4);
-}
+int m64g_cfg_waves(int cfg) { return cfg == 7 ? 8 : cfg == 9 ? 4 : (cfg >= 4 ? 2 : 4); }
 int m64g_cfg_kc(int cfg) {
-  return (cfg == 2 || cfg == 3 || cfg == 4 || cfg == 5 || cfg == 7 || cfg >= 10) ? 64 : 128;
+  return (cfg == 2 || cfg == 3 || cfg == 4 || cfg == 5 || cfg == 7 || cfg == 10) ? 64 : 128;
 }
 
 // Host-side shape / operand checks shared by both entry points (0 = valid).
 static int m64g_check(int M, int K, int N, const float* part, const uint16_t* out, int S, int mode, int nw, int cfg,
                       const M64Epi& epi) {
-  if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 13) return 1;
-  if (cfg >= 8 && cfg <= 10 && M > 16) return 1;  // deep-ring one-x-tile configurations
+  if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 10) return 1;
+  if (cfg >= 8 && M > 16) return 1;  // deep-ring configurations: one x tile only
   if (mode < GG_BF16 || mode > GG_AR || mode == GG_MOE_RESID) return 1;
   // the consumer's statistics paths sum at most 64 partial sums per row (m64g prologue)
   if (epi.ss_in != nullptr && (epi.ss_n < 1 || epi.ss_n > 64 || epi.ss_stride < M)) return 1;

@@ -89,9 +89,10 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor, split_k: Optional[int] = Non
 # 8-10: deep LDS rings (5 / 4 / 6 slots) for M <= 16 -- more weight bytes in flight per CU
 M64G_CFGS = {0: (4, 128, False), 1: (4, 128, True), 2: (4, 64, False), 3: (4, 64, True),
              4: (2, 64, False), 5: (2, 64, True), 6: (2, 128, True), 7: (8, 64, True),
-             8: (2, 128, True), 9: (4, 128, True), 10: (2, 64, True),
-             # deep rings with four x tiles (16 < M <= 64): 6 / 6 / 4 slots of KC 64
-             11: (4, 64, True), 12: (2, 64, True), 13: (4, 64, True)}
+             8: (2, 128, True), 9: (4, 128, True), 10: (2, 64, True)}
+# (Deep four-x-tile rings -- KC 64, 4-6 slots at M = 64 -- ran the 8B gate_up at 38.1
+# vs 41.7 us in isolation but +0.1 % end to end (10,756 vs 10,742 tok/s, 400 steps,
+# profiles/r6/r6s_m64g_sweep.md), and were not kept.)
 M64G_SMALL_ONLY = (8, 9, 10)
 
 # Measured on MI355X with cold weights (bench/gemm_bench.py --m64g-sweep,
