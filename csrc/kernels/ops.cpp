@@ -422,6 +422,22 @@ PYBIND11_MODULE(_kernels, m) {
 
   // ---- custom one-shot xGMI all-reduce (csrc/comm/custom_allreduce.hip)
   m.def("car_wallclock_khz", []() { return xgk::car_wallclock_khz(); });
+  // CU-partitioned streams (engine/partition.py): a HIP stream whose dispatches -- kernels
+  // and graph launches alike -- run only on the CUs set in `mask` (32 CUs per word)
+  m.def("cu_mask_stream_create", [](std::vector<uint32_t> mask) {
+    hipStream_t st = nullptr;
+    const hipError_t e = hipExtStreamCreateWithCUMask(&st, static_cast<uint32_t>(mask.size()), mask.data());
+    if (e != hipSuccess) throw std::runtime_error(std::string("hipExtStreamCreateWithCUMask: ") + hipGetErrorString(e));
+    return reinterpret_cast<uintptr_t>(st);
+  });
+  m.def("cu_mask_stream_get", [](uintptr_t st, int words) {
+    std::vector<uint32_t> mask(static_cast<size_t>(words), 0u);
+    const hipError_t e = hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>(st), static_cast<uint32_t>(words),
+                                               mask.data());
+    if (e != hipSuccess) throw std::runtime_error(std::string("hipExtStreamGetCUMask: ") + hipGetErrorString(e));
+    return mask;
+  });
+  m.def("stream_destroy", [](uintptr_t st) { (void)hipStreamDestroy(reinterpret_cast<hipStream_t>(st)); });
   m.def("car_limits", []() { return py::make_tuple(xgk::car_max_ranks(), xgk::car_max_blocks(), xgk::car_chunk()); });
   m.def("car_alloc_uncached", [](int64_t bytes) {
     void* p = nullptr;
