@@ -114,7 +114,8 @@ def prompt_gemm(eng) -> str:
     if layers is None or not getattr(layers[0], "pf_ok", False):
         return "library"
     from xgserve.models import llama
-    return f"gemm_pf[{','.join(sorted(llama.PF_SET))}] for {llama.PF_MIN_M}-{llama.PF_MAX_M} tokens"
+    return "gemm_pf " + ", ".join(f"{k} {'+'.join(f'{lo}-{hi}' for lo, hi in ws)}"
+                                  for k, ws in sorted(llama.PF_WINDOWS.items()) if ws) + " tokens"
 
 
 def preflight(st, world: int, tp: int, dev, eng) -> dict:

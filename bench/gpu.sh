@@ -72,6 +72,15 @@ ab)
     run "driver_$n" 200 env $s $B --steps 20 --warmup 5 "$@"
     run "w400_$n" 250 env $s $B --steps 400 --warmup 40 "$@"
   done ;;
+r6b)  # 128-tile statistics (no GG_AR pair combine at TP8), measured pf windows: tests + A/Bs
+  pyt b_tests 900 tests/test_fused_decode_gpu.py tests/test_custom_ar_gpu.py tests/test_pf_gpu.py tests/test_engine_gpu.py
+  run tp8_c1 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+  run driver 200 $B --steps 20 --warmup 5
+  run p384_new 250 $B --steps 400 --warmup 40 --prompt-len 384
+  run p384_old 250 env XGS_TUNE=pf_windows=gate_up:513-576 $B --steps 400 --warmup 40 --prompt-len 384 ;;
+r6p)  # gemm_pf vs the tuned library GEMMs over the prompt-sized step range (the pf decision table)
+  run pfsweep 900 python -u bench/pf_gemm_bench.py --no-check --rounds 3 --iters 10 --cfgs 2 4 8 3 7 6 \
+      --shapes gate_up down_p qkv_p o_p --M 320 384 448 512 575 640 768 896 1024 1280 1536 2048 3072 4096 8192 ;;
 r6s)  # m64g sweeps: deep four-x-tile rings at the 8B decode shapes (M 64), deep splits at M 1
   pyt pf_tests 300 tests/test_pf_gpu.py
   run sweep64 500 python -u bench/gemm_bench.py --m64g-sweep --M 64 --shapes qkv o down gate_up

@@ -45,9 +45,11 @@ enum : int { GG_BF16 = 0, GG_PARTIAL = 1, GG_SILU = 2, GG_RESID = 3, GG_MOE_RESI
 //           partial sums of squares per row, ss_in[j * ss_stride + m], added in a
 //           fixed order; output row m is scaled by rsqrt(sum / K + eps).
 //           ss_n <= 8: any M (lane group g of row m sums j = g, g + 4);
-//           8 < ss_n <= 64: M <= 16: wave w, group g sums j = 4w + g + 4 WV q, q < 8;
-//           M > 16 (MT = 4): lane m of wave w sums j = w + WV q (64 / WV loads), the
-//           waves' sums added through LDS in wave order (deterministic).
+//           8 < ss_n <= 128, M <= 16: wave w, group g sums j = 4w + g + 4 WV q,
+//           q < 32 / WV (a 128-tile producer -- the 70B TP8 O / down at 64-column
+//           tiles -- needs no pair combine);
+//           8 < ss_n <= 64, M > 16 (MT = 4): lane m of wave w sums j = w + WV q (64 / WV
+//           loads), the waves' sums added through LDS in wave order (deterministic).
 //   GG_RESID: resid[m, n] += sum_s part[s, m, n] (bf16 residual stream, in place);
 //           ss_out[tile * M + m] = sum over the tile's columns of resid[m, n]^2
 //           (the next GEMM's ss_in with ss_n = gridDim.x). counters: gridDim.x tile
@@ -514,7 +516,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   const bool tall_ss = MT > 1 && has_ss && epi.ss_n > 8 && M > 16;
   const bool wide_ss = has_ss && epi.ss_n > 8 && !tall_ss;
   constexpr int TQ = MT > 1 ? 64 / WV : 1;
-  float ssv[8];
+  constexpr int WQ = 32 / WV;  // wide statistics loads per lane (4 WV groups x WQ = 128 sums)
+  float ssv[WQ > 8 ? WQ : 8];
   float ssb[TQ];
   // ring prologue: chunks 0 .. NS - 2 into their slots
   auto slot_of = [&](int j) -> uint8_t* {
@@ -527,8 +530,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
     for (int q = 0; q < TQ; ++q) ssb[q] = ld_ss(min(wid + WV * q, epi.ss_n - 1) * epi.ss_stride + min(lane, M - 1));
   } else if (has_ss) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (!wide_ss && (i >> 1) >= MT) break;
+    for (int i = 0; i < (WQ > 8 ? WQ : 8); ++i) {
+      if (wide_ss ? i >= WQ : (i >> 1) >= MT || i >= 8) break;
       const int mt = wide_ss ? 0 : i >> 1, q = wide_ss ? i : i & 1;
       const int j = wide_ss ? 4 * wid + g + 4 * WV * q : g + 4 * q;
       ssv[i] = ld_ss(min(j, epi.ss_n - 1) * epi.ss_stride + min(16 * mt + li, M - 1));
@@ -597,7 +600,7 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
     } else {
       float v = 0.f;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v += 4 * wid + g + 4 * WV * q < epi.ss_n ? ssv[q] : 0.f;
+      for (int q = 0; q < WQ; ++q) v += 4 * wid + g + 4 * WV * q < epi.ss_n ? ssv[q] : 0.f;
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
       float* red = reinterpret_cast<float*>(lds0);
@@ -1119,7 +1122,7 @@ static int m64g_check(int M, int K, int N, const float* part, const uint16_t* ou
   if (cfg >= 8 && M > 16) return 1;  // deep-ring configurations: one x tile only
   if (mode < GG_BF16 || mode > GG_AR || mode == GG_MOE_RESID) return 1;
   // the consumer's statistics paths sum at most 64 partial sums per row (m64g prologue)
-  if (epi.ss_in != nullptr && (epi.ss_n < 1 || epi.ss_n > 64 || epi.ss_stride < M)) return 1;
+  if (epi.ss_in != nullptr && (epi.ss_n < 1 || epi.ss_n > (M <= 16 ? 128 : 64) || epi.ss_stride < M)) return 1;
   const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
   if (K % kc || S > K / kc || N % cols) return 1;
   // split-K SiLU: fp32 slabs + one zeroed arrival ticket per column tile (m64g_silu_tail)

@@ -50,6 +50,28 @@ def test_norm_linear_row_scale(M, n_parts):
     assert rel_err(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("M", [1, 4, 16])
+@pytest.mark.parametrize("n_parts", [72, 128])
+@pytest.mark.parametrize("N,K,mode", [(1280, 8192, MODE_PARTIAL), (7168, 8192, MODE_SILU), (6144, 4096, MODE_PARTIAL),
+                                      (28672, 4096, MODE_SILU)])
+def test_norm_linear_128_partial_sums(M, n_parts, N, K, mode):
+    """M <= 16 consumers combine up to 128 per-tile statistics (the wide path at 2 / 4
+    waves: 70B TP8 and 8B decode plans), so a 128-tile GG_AR / GG_RESID producer needs
+    no pair combine."""
+    x = rnd(M, K)
+    sq = x.float() ** 2
+    st = RowStats(sq.view(M, n_parts, -1).sum(-1).t().contiguous(), n_parts, M)
+    h = x.float() * torch.rsqrt(sq.sum(-1, keepdim=True) / K + 1e-5)
+    if mode == MODE_PARTIAL:
+        w = rnd(N, K, scale=0.02)
+        pend = m64_norm_linear(x, w, MODE_PARTIAL, st, 1e-5)
+        assert rel_err(pend.part.sum(0), h @ w.float().t()) < 2e-3
+    else:
+        g, u = rnd(N // 2, K, scale=0.02), rnd(N // 2, K, scale=0.02)
+        y = m64_norm_linear(x, interleave_gate_up(g, u), MODE_SILU, st, 1e-5)
+        assert rel_err(y, F.silu(h @ g.float().t()) * (h @ u.float().t())) < 1e-2
+
+
 @pytest.mark.parametrize("M", [1, 17, 64])
 @pytest.mark.parametrize("S,cfg", [(1, 7), (2, 7), (4, 7), (2, 1), (2, 5), (2, 6), (4, 6), (4, 0), (4, 1), (4, 3)])
 @pytest.mark.parametrize("normed", [False, True])

@@ -62,20 +62,46 @@ FUSED_DECODE = tune.get_bool("fused_decode", True)
 # MFMA GEMMs whose split-K partials go to the consumers, SiLU-gate in gate_up.
 # 0 = hipBLASLt for every step above 64 tokens.
 MW_MAX_TOKENS = min(MW_MAX_M, tune.get_int("mw_max_tokens", MW_MAX_M))
-# PF_MIN_M <= T <= PF_MAX_M tokens (a mixed step carrying a whole 512-token prompt
-# chunk) on TP = 1: the projections named by XGS_TUNE pf (comma list of qkv, o,
-# gate_up, down; "1" = PF_DEFAULT, "0" = none) on gemm_pf (csrc/kernels/gemm_pf.hip)
-# -- QKV / O / down as split-K partials into their consumers, gate_up with the SiLU
-# gate in its epilogue. The window is where two 288-row tiles cover the step: one
-# round of workgroups on 256 CUs, where gemm_pf beats the tuned library GEMMs
-# (gate_up 121 vs 124 + 10 us at M = 575); above and below it the tuned library
-# tiles are ahead (profiles/r5_pf_gemm.md) and keep those steps.
-PF_DEFAULT = "gate_up,down"
+# Prompt-sized mixed steps on TP = 1: each projection takes gemm_pf
+# (csrc/kernels/gemm_pf.hip) for the step sizes where it measured faster than the
+# tuned library GEMM (profiles/r6/r6p_pf_vs_library.md, cold weights, the engine's
+# library forms) -- QKV / O / down as split-K partials into their consumers, gate_up
+# with the SiLU gate in its epilogue:
+#   gate_up 513-576 rows: the library's tile-quantisation cliff (103 us at 512 rows,
+#     135 at 575), where two 288-row tiles cover the step (pf 110 us); 2-17 % behind
+#     the library at every other measured size;
+#   down 321-576 rows: 5-11 % ahead of the library's split-4 GEMM at every measured
+#     size (<= 320 rows run on gemm_mw);
+#   QKV / O: never -- pf's isolated lead is smaller than the fp32 partial slabs it adds
+#     to their consumers (r5: -0.5 % end to end with every projection on pf).
+# XGS_TUNE pf: "1" = these windows, "0" = library everywhere, or a comma list of
+# projections to allow; pf_windows overrides the table ("gate_up:513-576/down:321-576").
+PF_WINDOWS_DEFAULT = "gate_up:513-576/down:321-576"
+
+
+def _parse_pf_windows(spec: str):
+    out = {"qkv": (), "o": (), "gate_up": (), "down": ()}
+    for item in filter(None, (t.strip() for t in spec.split("/"))):
+        name, rng = item.split(":")
+        assert name in out, f"XGS_TUNE pf_windows: {name!r}"
+        out[name] = tuple(tuple(int(v) for v in r.split("-")) for r in rng.split("+"))
+    return out
+
+
 _pf_spec = tune.get_str("pf", "1")
 PF_SET = frozenset() if _pf_spec in ("0", "") else frozenset(
-    (PF_DEFAULT if _pf_spec == "1" else _pf_spec).replace("+", ",").split(","))
+    ("qkv,o,gate_up,down" if _pf_spec == "1" else _pf_spec).replace("+", ",").split(","))
 assert PF_SET <= {"qkv", "o", "gate_up", "down"}, f"XGS_TUNE pf: {sorted(PF_SET)}"
-PF_MIN_M, PF_MAX_M = (int(v) for v in tune.get_str("pf_m", "513-576").split("-"))
+PF_WINDOWS = {k: (v if k in PF_SET else ())
+              for k, v in _parse_pf_windows(tune.get_str("pf_windows", PF_WINDOWS_DEFAULT)).items()}
+PF_MAX_M = max([hi for ws in PF_WINDOWS.values() for _, hi in ws] or [0])
+
+
+def pf_projections(T: int) -> frozenset:
+    """The projections that run on gemm_pf at a T-token step."""
+    return frozenset(k for k, ws in PF_WINDOWS.items() if any(lo <= T <= hi for lo, hi in ws))
+
+
 # TP > 1 prefill-sized steps: the row-parallel all-reduces are pipelined over this
 # many token chunks and overlapped with the next chunk's GEMMs (RCCL stream); a
 # 2k-token 8B step moves 16 MiB per all-reduce -- ~100 us on 7 xGMI links, a
@@ -165,7 +191,7 @@ class LlamaLayer(nn.Module):
             mw_plan(MW_MAX_TOKENS, n, k, mode) is not None and mw_plan(FAST_M_SLAB + 1, n, k, mode) is not None
             for n, k, mode in mw_shapes)
         # T > MW_MAX_TOKENS on TP = 1: gemm_pf for every projection (MoE layers: attention)
-        self.pf_ok = self.fast_ok and bool(PF_SET) and tp == 1 and all(
+        self.pf_ok = self.fast_ok and PF_MAX_M > 0 and tp == 1 and all(
             pf_plan(PF_MAX_M, n, k, mode) is not None for n, k, mode in mw_shapes)
         # M <= 16 too, when every projection has a measured small-M plan
         self.w8 = None  # fp8 / int8 / int4 weight copies for decode (LlamaForCausalLM.quantize_weights)
@@ -374,23 +400,24 @@ class LlamaLayer(nn.Module):
             act = mw_linear(h, self.gate_up, MODE_SILU)
             d = mw_linear(act, self.down, MODE_PARTIAL)
             return (d if self.tp == 1 else self._ar(d.materialize())), residual
-        if self.pf_ok and PF_MIN_M <= T <= PF_MAX_M:
-            # prompt-sized mixed steps: gemm_pf for the projections of PF_SET (split-K
-            # partials into the consumers: rope_cache_partials / add + rmsnorm; the SiLU
-            # gate in the gate_up epilogue), the library GEMMs for the others
-            if "qkv" in PF_SET:
+        use_pf = pf_projections(T) if self.pf_ok else frozenset()
+        if use_pf:
+            # prompt-sized mixed steps: gemm_pf for the projections whose measured window
+            # holds T (split-K partials into the consumers: rope_cache_partials / add +
+            # rmsnorm; the SiLU gate in the gate_up epilogue), the library GEMMs for the others
+            if "qkv" in use_pf:
                 a = self.attn.from_partials(pf_linear(h, self.qkv, MODE_PARTIAL), meta, kv, cos_sin)
             else:
                 a = self.attn(F.linear(h, self.qkv), meta, kv, cos_sin)
-            o = pf_linear(a, self.o, MODE_PARTIAL) if "o" in PF_SET else F.linear(a, self.o)
+            o = pf_linear(a, self.o, MODE_PARTIAL) if "o" in use_pf else F.linear(a, self.o)
             h, residual = ops.fused_add_rmsnorm(o, residual, self.post_norm, eps)
             if self.moe:
                 return self.mlp(h), residual
-            if "gate_up" in PF_SET:
+            if "gate_up" in use_pf:
                 act = pf_linear(h, self.gate_up, MODE_SILU)
             else:
                 act = ops.silu_and_mul(F.linear(h, self.gate_up), interleave16=True)
-            if "down" in PF_SET:
+            if "down" in use_pf:
                 return pf_linear(act, self.down, MODE_PARTIAL), residual
             if splitk_prefill_ok(act, self.down):
                 return splitk_linear(act, self.down, linear_mod.SPLITK_PREFILL_S), residual

@@ -307,7 +307,6 @@ def mw_linear(x: torch.Tensor, w: torch.Tensor, mode: int = MODE_PARTIAL, plan=N
 # cfg -> (BM, m tiles per wave per phase): 0 (256, 2) 1 (192, 2) 2 (128, 2) 3 (256, 4)
 # 4 (192, 3) 5 (288, 3).
 PF_CFG_BM = {0: 256, 1: 192, 2: 128, 3: 256, 4: 192, 5: 288, 6: 288, 7: 256, 8: 192}
-PF_MIN_M = 65
 # The planner's cost model, fitted to bench/pf_gemm_bench.py at the 8B mixed-step
 # shapes (profiles/r5_pf_gemm.md): a workgroup costs PF_WG_US + its output bytes at
 # PF_WG_OUT_GBS (fp32 partials or bf16) + K tiles x the per-K-tile time of its cfg;
@@ -437,7 +436,8 @@ class ResidWorkspace:
     Statistics site 0 is the embedding; sites 2i+1 / 2i+2 follow layer i's
     attention / MLP residual adds."""
 
-    MAX_TILES = 64  # per-tile statistics a consumer can combine (ss_n <= 64)
+    MAX_TILES = 64  # per-tile statistics a consumer can combine (ss_n <= 64) at any M
+    MAX_TILES_SMALL_M = 128  # ... and at M <= 16 (gemm_m64g's wide statistics path)
     IN_LAUNCH_MAX_M = 64
 
     def __init__(self, n_sites: int, max_m: int, H: int, device):
@@ -452,6 +452,9 @@ class ResidWorkspace:
         self.ar_pair = torch.zeros(self.MAX_TILES, dtype=torch.int32, device=device)
         self.ar_ss_tmp = torch.zeros(2 * self.MAX_TILES * self.IN_LAUNCH_MAX_M, dtype=torch.float32, device=device)
         self._ar_descs = {}
+
+    def max_tiles(self, M: int) -> int:
+        return self.MAX_TILES_SMALL_M if M <= 16 else self.MAX_TILES
 
     def ar_desc(self, ar, group: int) -> torch.Tensor:
         """Device copy of gemm_m64g's ArDesc for these all-reduce operands (built once;
@@ -560,7 +563,7 @@ def m64_resid_linear(x, w: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace
     ss = ws.ss[site]
     cols = 16 * nw * M64G_CFGS[cfg][0]
     ntiles = N // cols
-    if (S * M * cols * 4 <= RESID_INLAUNCH_MAX_BYTES and ntiles <= ws.MAX_TILES
+    if (S * M * cols * 4 <= RESID_INLAUNCH_MAX_BYTES and ntiles <= ws.max_tiles(M)
             and M <= ws.IN_LAUNCH_MAX_M):
         k.gemm_m64g_ex(xp, M, K, w.data_ptr(), N, part.data_ptr(), 0, S, MODE_RESID, nw, cfg, 0, 0, 0,
                        float(eps), resid.data_ptr(), ss.data_ptr(), ws.counters[site].data_ptr(), stream_ptr())
@@ -585,7 +588,8 @@ def m64_ar_resid_linear(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor, w
         raise ValueError(f"gemm_m64g_ar: unsupported shape M={M} N={N} K={K}")
     nw, S, cfg = plan
     ntiles = N // (16 * nw * M64G_CFGS[cfg][0])
-    group = 1 if ntiles <= ws.MAX_TILES else 2
+    # more column tiles than the consumer combines: statistics per pair of tiles
+    group = 1 if ntiles <= ws.max_tiles(M) else 2
     if ntiles > 2 * ws.MAX_TILES:
         raise ValueError(f"gemm_m64g_ar: {ntiles} column tiles")
     part = torch.empty(S, M, N, dtype=torch.float32, device=resid.device)

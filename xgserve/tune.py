@@ -9,9 +9,9 @@ Keys (default in brackets; every default is the production setting):
   async_sched [1]          plan + launch step N+1 before step N's tokens reach the host
   early_release [config]   release length-finishing rows at lookahead
   spin_wait [1]            host polls the step event instead of blocking
-  pf [1]                   gemm_pf projections of prompt-sized mixed steps: 1 = the default set,
-                           0 = library GEMMs, or a list "qkv,o,gate_up,down"
-  pf_m [513-576]           the step sizes (tokens) that take gemm_pf
+  pf [1]                   gemm_pf projections of prompt-sized mixed steps: 1 = the measured windows,
+                           0 = library GEMMs, or a list "qkv,o,gate_up,down" of those allowed
+  pf_windows [gate_up:513-576/down:321-576]   step sizes (tokens) per projection that take gemm_pf
   moe_pf [1]               prompt-sized expert GEMMs (> 256 token-expert pairs) on gemm_pf's grouped form
   krot [1]                 K-chunk rotation of the weight-streaming GEMMs (0 / 1 / 2)
   m64_plans / mw_plans     gemm_m64g / gemm_mw plan overrides, "NxKxMODE@BUCKET=...;..."
@@ -33,7 +33,7 @@ from __future__ import annotations
 import os
 from typing import Dict
 
-KEYS = {"fused_decode", "async_sched", "early_release", "spin_wait", "pf", "pf_m", "moe_pf", "gemm_ar", "gemm_ar_shared", "krot", "m64_plans", "mw_plans",
+KEYS = {"fused_decode", "async_sched", "early_release", "spin_wait", "pf", "pf_windows", "moe_pf", "gemm_ar", "gemm_ar_shared", "krot", "m64_plans", "mw_plans",
         "mw_max_tokens", "resid_inlaunch_kb", "decode_depth", "decode_max_splits", "ar_ll_max", "sim_ar_us",
         "tp_overlap_chunks", "tp_overlap_min_tokens", "ep_exact_min_pairs"}
 
