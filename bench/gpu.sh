@@ -72,6 +72,11 @@ ab)
     run "driver_$n" 200 env $s $B --steps 20 --warmup 5 "$@"
     run "w400_$n" 250 env $s $B --steps 400 --warmup 40 "$@"
   done ;;
+r6f)  # closing kernel profiles: 8B c64 / c1, Mixtral c1, one 70B TP8 rank c1
+  bash bench/profile.sh "$o/c64"
+  bash bench/profile.sh "$o/c1" --concurrency 1
+  bash bench/profile.sh "$o/mix_c1" --model mixtral-8x7b --concurrency 1
+  bash bench/profile.sh "$o/tp8_c1" --model llama3-70b --tp-shard 8 --concurrency 1 ;;
 r6b)  # 128-tile statistics (no GG_AR pair combine at TP8), measured pf windows: tests + A/Bs
   pyt b_tests 900 tests/test_fused_decode_gpu.py tests/test_custom_ar_gpu.py tests/test_pf_gpu.py tests/test_engine_gpu.py
   run tp8_c1 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
