@@ -33,6 +33,8 @@
 
 #include <cstddef>
 
+#include <algorithm>
+
 #include "glds.h"
 #include "../comm/ll.h"
 
@@ -1040,9 +1042,14 @@ int m64g_cfg_kc(int cfg);
 // max_rows: a bound on the real rows of any expert (<= 16 selects the one-x-tile
 // kernel; rows 16..63 of each padded tile are then left unwritten -- pads only).
 // valid: the sorted rows (-1 = pad) for the row-occupancy dispatch, or nullptr (all 64 rows).
+// pairs > 0: a bound on the (token, choice) rows over ALL local experts. The real
+// 64-row tiles lead the padded layout (segments are packed, 64-aligned), and there are
+// at most ceil(pairs / 64) + min(E, pairs) of them, so the grid stops there instead of
+// at the capacity P / 64 (batch 1, Mixtral: 3 row tiles instead of 8 -- the empty
+// workgroups each paid an offsets read before exiting).
 int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, int E, int K, const uint16_t* w, int N,
                   int P, float* part, uint16_t* out, int S, int mode, int nw, int cfg, int max_rows, hipStream_t st,
-                  const int32_t* valid, const MoeResidEpi* mre_in) {
+                  const int32_t* valid, const MoeResidEpi* mre_in, int pairs) {
   if (E < 1 || P < 0 || P % 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 6) return 1;
   if (mode != GG_BF16 && mode != GG_PARTIAL && mode != GG_SILU && mode != GG_MOE_RESID) return 1;
   const MoeResidEpi mre = mre_in ? *mre_in : MoeResidEpi{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
@@ -1057,7 +1064,8 @@ int moe_gemm_m64g(const uint16_t* x, const int32_t* rows, const int32_t* offs, i
   if ((mode == GG_PARTIAL || mode == GG_MOE_RESID) && part == nullptr) return 1;
   if (mode != GG_PARTIAL && mode != GG_MOE_RESID && out == nullptr) return 1;
   if (P == 0) return 0;
-  const dim3 grid(N / cols, S, P / 64);
+  const int ztiles = pairs > 0 ? std::min(P / 64, (pairs + 63) / 64 + std::min(E, pairs)) : P / 64;
+  const dim3 grid(N / cols, S, ztiles);
   const bool mt1 = max_rows <= 16 && cfg != 2 && cfg != 3;  // 16 x rows >= one DMA per wave
   // 128-row pairs for prefill-sized steps (> 256 pairs; decode keeps the 48 KB-slot
   // kernel and its occupancy), KC 64 configs only

@@ -49,7 +49,8 @@ struct MoeResidEpi {
   int k;
 };
 int moe_gemm_m64g(const uint16_t*, const int32_t*, const int32_t*, int, int, const uint16_t*, int, int, float*,
-                  uint16_t*, int, int, int, int, int, hipStream_t, const int32_t*, const MoeResidEpi* = nullptr);
+                  uint16_t*, int, int, int, int, int, hipStream_t, const int32_t*, const MoeResidEpi* = nullptr,
+                  int pairs = 0);
 void add_partials_rmsnorm(const float*, int, int, uint16_t*, const uint16_t*, uint16_t*, int, float, hipStream_t);
 void reduce_partials(const float*, int, int64_t, uint16_t*, hipStream_t);
 int rope_cache_partials(const float*, int, uint16_t*, int64_t, const int32_t*, const float*, uint16_t*, uint16_t*,
@@ -347,31 +348,31 @@ PYBIND11_MODULE(_kernels, m) {
   // valid: the sorted rows (-1 = pad) -> per-workgroup 16/32/64-row body; 0: all rows
   m.def("moe_gemm_m64g_rows", [](uintptr_t x, uintptr_t rows, uintptr_t offs, int E, int K, uintptr_t w, int N, int P_,
                                  uintptr_t part, uintptr_t out, int splits, int mode, int nw, int cfg, int max_rows,
-                                 uintptr_t st, uintptr_t valid) {
+                                 uintptr_t st, uintptr_t valid, int pairs) {
     check(xgk::moe_gemm_m64g(P<const uint16_t>(x), P<const int32_t>(rows), P<const int32_t>(offs), E, K,
                              P<const uint16_t>(w), N, P_, P<float>(part), P<uint16_t>(out), splits, mode, nw, cfg,
-                             max_rows, S(st), P<const int32_t>(valid)),
+                             max_rows, S(st), P<const int32_t>(valid), nullptr, pairs),
           "moe_gemm_m64g_rows");
   }, py::arg("x"), py::arg("rows"), py::arg("offs"), py::arg("E"), py::arg("K"), py::arg("w"), py::arg("N"),
      py::arg("P"), py::arg("part"), py::arg("out"), py::arg("splits"), py::arg("mode"), py::arg("nw"), py::arg("cfg"),
-     py::arg("max_rows"), py::arg("st"), py::arg("valid") = 0);
+     py::arg("max_rows"), py::arg("st"), py::arg("valid") = 0, py::arg("pairs") = 0);
   // w2 of the fused MoE decode layer with the weighted combine + residual add in the
   // launch (GG_MOE_RESID = 4): resid[T, N] += sum_j w[t, j] * (sum_s part[s, dest[t, j]]),
   // ss_out[N / cols, T] = per-column-tile sum of squares of the new residual
   m.def("moe_gemm_m64g_resid", [](uintptr_t x, uintptr_t rows, uintptr_t offs, int E, int K, uintptr_t w, int N,
                                   int P_, uintptr_t part, int splits, int nw, int cfg, int max_rows, uintptr_t st,
                                   uintptr_t valid, uintptr_t dest, uintptr_t wts, uintptr_t resid, uintptr_t ss_out,
-                                  uintptr_t counters, int T, int k) {
+                                  uintptr_t counters, int T, int k, int pairs) {
     const xgk::MoeResidEpi e{P<const int32_t>(dest), P<const float>(wts), P<uint16_t>(resid), P<float>(ss_out),
                              P<int>(counters), T, k};
     check(xgk::moe_gemm_m64g(P<const uint16_t>(x), P<const int32_t>(rows), P<const int32_t>(offs), E, K,
                              P<const uint16_t>(w), N, P_, P<float>(part), nullptr, splits, 4, nw, cfg, max_rows,
-                             S(st), P<const int32_t>(valid), &e),
+                             S(st), P<const int32_t>(valid), &e, pairs),
           "moe_gemm_m64g_resid");
   }, py::arg("x"), py::arg("rows"), py::arg("offs"), py::arg("E"), py::arg("K"), py::arg("w"), py::arg("N"),
      py::arg("P"), py::arg("part"), py::arg("splits"), py::arg("nw"), py::arg("cfg"), py::arg("max_rows"),
      py::arg("st"), py::arg("valid"), py::arg("dest"), py::arg("wts"), py::arg("resid"), py::arg("ss_out"),
-     py::arg("counters"), py::arg("T"), py::arg("k"));
+     py::arg("counters"), py::arg("T"), py::arg("k"), py::arg("pairs") = 0);
   m.def("moe_route", [](uintptr_t h, uintptr_t wr, int T, int H, int E, int k, int renorm, uintptr_t w, uintptr_t ids,
                         uintptr_t st, uintptr_t norm_w, float eps, uintptr_t hn, uintptr_t al_rows, uintptr_t al_offs,
                         uintptr_t al_dest, int al_E, int al_eoff, int al_bm) {

@@ -199,8 +199,10 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
                            S, 1, cfg, stream_ptr())
         return _moe_combine(kn, part, S, P, dest, topk_w, resid, ss, T, k, H, x, out_f32)
 
+    # pairs = T * k bounds the real row tiles (they lead the padded layout): the grid
+    # stops there instead of at the capacity P / 64
     def gemm(*a, cfg=0):
-        kn.moe_gemm_m64g_rows(*a[:-1], cfg, max_rows, a[-1], valid)
+        kn.moe_gemm_m64g_rows(*a[:-1], cfg, max_rows, a[-1], valid, T * k)
     cfg13 = ((MOE_CFG_W13_PREFILL if T * k > MOE_PREFILL_PAIRS else MOE_CFG_W13)
              if (H % 64 == 0 and F2 % 128 == 0) else 0)
     gemm(x.contiguous().data_ptr(), sorted_rows.data_ptr(), offs.data_ptr(), E, H, w13.data_ptr(), F2, P, 0,
@@ -226,7 +228,7 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
         kn.moe_gemm_m64g_resid(act.data_ptr(), 0, offs.data_ptr(), E, F, w2.data_ptr(), H, P, part.data_ptr(), S, nw2,
                                cfg2, max_rows, stream_ptr(), valid, dest.data_ptr(),
                                topk_w.float().contiguous().data_ptr(), resid.data_ptr(), ss.data_ptr(),
-                               counters.data_ptr(), T, k)
+                               counters.data_ptr(), T, k, T * k)
         return H // cols2
     gemm(act.data_ptr(), 0, offs.data_ptr(), E, F, w2.data_ptr(), H, P, part.data_ptr(), 0, S, 1, nw2, stream_ptr(),
          cfg=cfg2)
