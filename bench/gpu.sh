@@ -77,8 +77,19 @@ r6f)  # closing kernel profiles: 8B c64 / c1, Mixtral c1, one 70B TP8 rank c1
   bash bench/profile.sh "$o/c1" --concurrency 1
   bash bench/profile.sh "$o/mix_c1" --model mixtral-8x7b --concurrency 1
   bash bench/profile.sh "$o/tp8_c1" --model llama3-70b --tp-shard 8 --concurrency 1 ;;
+r6t)  # same-box A/B: 128-tile statistics at M <= 16 vs the pair combine (70B TP8 rank, 8B batch 1)
+  for r in 1 2; do
+    for v in 64 128; do
+      run "tp8_c1_t${v}_$r" 300 env XGS_TUNE=small_m_tiles=$v $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+    done
+  done
+  for v in 64 128; do
+    run "c1_t$v" 200 env XGS_TUNE=small_m_tiles=$v $B --concurrency 1 --steps 300 --warmup 30
+  done ;;
 r6b)  # 128-tile statistics (no GG_AR pair combine at TP8), measured pf windows: tests + A/Bs
   pyt b_tests 900 tests/test_fused_decode_gpu.py tests/test_custom_ar_gpu.py tests/test_pf_gpu.py tests/test_engine_gpu.py
+  pyt moe_tests 400 tests/test_kernels_gpu.py -k "moe or mixtral or expert"
+  run mix_c1 300 $B --model mixtral-8x7b --concurrency 1 --steps 100 --warmup 10
   run tp8_c1 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
   run driver 200 $B --steps 20 --warmup 5
   run p384_new 250 $B --steps 400 --warmup 40 --prompt-len 384

@@ -437,7 +437,8 @@ class ResidWorkspace:
     attention / MLP residual adds."""
 
     MAX_TILES = 64  # per-tile statistics a consumer can combine (ss_n <= 64) at any M
-    MAX_TILES_SMALL_M = 128  # ... and at M <= 16 (gemm_m64g's wide statistics path)
+    # ... and at M <= 16 (gemm_m64g's wide statistics path; XGS_TUNE small_m_tiles A/B)
+    MAX_TILES_SMALL_M = tune.get_int("small_m_tiles", 128)
     IN_LAUNCH_MAX_M = 64
 
     def __init__(self, n_sites: int, max_m: int, H: int, device):

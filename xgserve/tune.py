@@ -11,7 +11,7 @@ Keys (default in brackets; every default is the production setting):
   spin_wait [1]            host polls the step event instead of blocking
   pf [1]                   gemm_pf projections of prompt-sized mixed steps: 1 = the measured windows,
                            0 = library GEMMs, or a list "qkv,o,gate_up,down" of those allowed
-  pf_windows [gate_up:513-576/down:321-576]   step sizes (tokens) per projection that take gemm_pf
+  pf_windows [gate_up:513-576/down:513-576]   step sizes (tokens) per projection that take gemm_pf
   moe_pf [1]               prompt-sized expert GEMMs (> 256 token-expert pairs) on gemm_pf's grouped form
   krot [1]                 K-chunk rotation of the weight-streaming GEMMs (0 / 1 / 2)
   m64_plans / mw_plans     gemm_m64g / gemm_mw plan overrides, "NxKxMODE@BUCKET=...;..."
@@ -21,6 +21,7 @@ Keys (default in brackets; every default is the production setting):
   decode_max_splits [16]   split-K cap of decode attention
   gemm_ar [1]              TP decode: all-reduce inside the row-parallel O / down GEMM launches
   gemm_ar_shared [0]       test-only: GG_AR also for <= 4 ranks sharing one GPU (one-GPU boxes)
+  small_m_tiles [128]      column-tile statistics a M <= 16 consumer combines (64: pair combine above)
   ar_ll_max [262144]       push (LL) all-reduce up to this many bytes (0: pull kernels)
   sim_ar_us [0]            --tp-shard simulation: stand-in all-reduce latency
   tp_overlap_chunks [2]    TP prefill: all-reduces pipelined over this many chunks
@@ -33,7 +34,7 @@ from __future__ import annotations
 import os
 from typing import Dict
 
-KEYS = {"fused_decode", "async_sched", "early_release", "spin_wait", "pf", "pf_windows", "moe_pf", "gemm_ar", "gemm_ar_shared", "krot", "m64_plans", "mw_plans",
+KEYS = {"fused_decode", "async_sched", "early_release", "spin_wait", "pf", "pf_windows", "moe_pf", "gemm_ar", "gemm_ar_shared", "small_m_tiles", "krot", "m64_plans", "mw_plans",
         "mw_max_tokens", "resid_inlaunch_kb", "decode_depth", "decode_max_splits", "ar_ll_max", "sim_ar_us",
         "tp_overlap_chunks", "tp_overlap_min_tokens", "ep_exact_min_pairs"}
 
