@@ -44,6 +44,9 @@ def main():
     ap.add_argument("--iters", type=int, default=70)
     ap.add_argument("--bs", type=int, default=16)
     ap.add_argument("--depth", type=int, nargs="+", default=[2])
+    ap.add_argument("--arrange", default="random", choices=["random", "pair", "sorted"],
+                    help="sequence order: random lengths; pair = seq b and b + B/2 complement each other "
+                         "(short + long); sorted = ascending")
     ap.add_argument("--probe", action="store_true",
                     help="anatomy: also time the kernel without its prologue (11), key loop (12), both (13)")
     a = ap.parse_args()
@@ -54,6 +57,12 @@ def main():
     B = a.B
     g = torch.Generator().manual_seed(0)
     lens = (a.L - torch.randint(0, max(a.stagger, 1), (B,), generator=g)).int()
+    if a.arrange != "random":
+        srt = torch.sort(lens).values
+        if a.arrange == "sorted":
+            lens = srt
+        else:  # b < B/2 takes the i-th shortest, b + B/2 the i-th longest
+            lens = torch.cat([srt[: B // 2], srt[B // 2:].flip(0)]).int()
     caches = [make_cache(B, lens, Hkv, D, bs, dev, g) for _ in range(a.caches)]
     lens = lens.to(dev)
     pos = (lens - 1).int()
@@ -87,7 +96,7 @@ def main():
             torch.cuda.synchronize()
             us = s.elapsed_time(e) / a.iters * 1000.0
             print(json.dumps({"op": "decode_attention_fq", "cache": mode, "B": B, "L": a.L, "stagger": a.stagger, "bs": bs,
-                              "splits": S, "depth": dp, "us": round(us, 2), "TB/s": round(nbytes / us / 1e6, 3)}), flush=True)
+                              "splits": S, "depth": dp, "arrange": a.arrange, "us": round(us, 2), "TB/s": round(nbytes / us / 1e6, 3)}), flush=True)
 
 
 if __name__ == "__main__":
