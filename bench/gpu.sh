@@ -72,6 +72,16 @@ ab)
     run "driver_$n" 200 env $s $B --steps 20 --warmup 5 "$@"
     run "w400_$n" 250 env $s $B --steps 400 --warmup 40 "$@"
   done ;;
+r6g1)  # closing gate, part 1: every GPU test + smoke()
+  pyt gputests 1100 tests -m gpu
+  run smoke 150 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+r6g2)  # closing gate, part 2: the driver-form headline twice, 3000 steps, batch 1, the serving path at DP 1
+  run driver_a 200 $B --steps 20 --warmup 5
+  run driver_b 200 $B --steps 20 --warmup 5
+  run long 300 $B --steps 3000 --warmup 100
+  run c1 200 $B --concurrency 1 --steps 300 --warmup 30
+  run serve_dp1 400 python -u bench/serve_bench.py --launch "--model llama3-8b --max-num-seqs 64 --replicas 1 --frontends 2" \
+      --concurrency 64 --prompt-len 512 --output-len 256 --warmup 40 --duration 40 --procs 4 --label serve_dp1 ;;
 r6f)  # closing kernel profiles: 8B c64 / c1, Mixtral c1, one 70B TP8 rank c1
   bash bench/profile.sh "$o/c64"
   bash bench/profile.sh "$o/c1" --concurrency 1
