@@ -87,6 +87,12 @@ r6f)  # closing kernel profiles: 8B c64 / c1, Mixtral c1, one 70B TP8 rank c1
   bash bench/profile.sh "$o/c1" --concurrency 1
   bash bench/profile.sh "$o/mix_c1" --model mixtral-8x7b --concurrency 1
   bash bench/profile.sh "$o/tp8_c1" --model llama3-70b --tp-shard 8 --concurrency 1 ;;
+r6d)  # 70B TP8 rank, batch 1: down-projection plans under GG_AR (same box)
+  for pl in base "8192x3584x1@16=1,1,9" "8192x3584x1@16=1,2,9" "8192x3584x1@16=2,2,6" "8192x3584x1@16=1,2,5"; do
+    n=$(echo "$pl" | tr -c 'A-Za-z0-9_\n' '_')
+    if [ "$pl" = base ]; then e="XGS_TUNE=krot=1"; else e="XGS_TUNE=m64_plans=$pl"; fi
+    run "tp8_$n" 300 env $e $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+  done ;;
 r6t)  # same-box A/B: 128-tile statistics at M <= 16 vs the pair combine (70B TP8 rank, 8B batch 1)
   for r in 1 2; do
     for v in 64 128; do
