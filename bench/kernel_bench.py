@@ -133,6 +133,40 @@ def bench_small(res, T=64, H=4096, F=14336):
     res.append({"op": "silu_and_mul", "T": T, "us": round(timeit(lambda: ops.silu_and_mul(gu)), 2)})
 
 
+def bench_moe_route(res, H=4096, E=8, k=2, layers=32):
+    """Mixtral batch-1 router (RMSNorm + router GEMV + top-k + align, one launch) next to a
+    trivial one-workgroup kernel at the same shape (the launch floor); router weights
+    rotate over `layers` copies as in a decode step."""
+    dev = "cuda"
+    resid = torch.randn(1, H, device=dev).bfloat16()
+    nw = torch.ones(H, device=dev).bfloat16()
+    routers = [(torch.randn(E, H, device=dev) * 0.02).bfloat16() for _ in range(layers)]
+    i = [0]
+
+    def route():
+        i[0] += 1
+        return ops.moe.moe_route_norm(resid, nw, 1e-5, routers[i[0] % layers], k, align=(E, 0))
+
+    def graphed(fn, n=64):
+        """device time per call: n calls captured in one HIP graph (no host launch cost)"""
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(n):
+                    fn()
+        torch.cuda.synchronize()
+        return timeit(g.replay, iters=20, warm=3) / n
+
+    res.append({"op": "moe_route_norm+align", "T": 1, "E": E, "us_graph": round(graphed(route), 2)})
+    res.append({"op": "moe_route(no norm, no align)", "T": 1, "E": E,
+                "us_graph": round(graphed(lambda: ops.moe.moe_route(resid, routers[0], k)), 2)})
+    res.append({"op": "rmsnorm (launch floor)", "T": 1, "us_graph": round(graphed(lambda: ops.rmsnorm(resid, nw, 1e-5)), 2)})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="all")
@@ -158,6 +192,8 @@ def main():
             bench_sampling(res, B)
     if a.what in ("all", "small"):
         bench_small(res)
+    if a.what in ("all", "moe"):
+        bench_moe_route(res)
     for r in res:
         print(json.dumps(r))
 

@@ -182,53 +182,58 @@ struct RouteAlign {
   int E_local, expert_offset, block_m, cap;
 };
 
-// Thread 0 of route2_kernel: softmax over the E router sums (red[wave][e]), top-k,
-// optional renormalisation -> w / ids of token t; with ra.sorted_rows (one token) also
-// align_kernel's layout offsets s_off / rows s_pos, published by the caller.
+// Wave 0 of route2_kernel: the same selection with lane e holding expert e (E <= 64):
+// the router sums (fixed order over the waves), the softmax max / denominator and each
+// of the k argmax rounds are wave reductions instead of thread 0's serial loops (about
+// 2 us of dependent LDS reads and branches per launch at Mixtral batch 1). Ties go to
+// the lowest expert index (as the reference top-k); the softmax denominator is a tree sum.
 template <int EM, int NWV>
-__device__ __forceinline__ void route_select(const float (*red)[EM + 1], int E, int k, int renorm, int t,
-                                             float* __restrict__ w, int32_t* __restrict__ ids, const RouteAlign& ra,
-                                             bool align, int* s_off, int* s_pos) {
-  float v[EM];
-  float mx = -INFINITY;
-  for (int e = 0; e < E; ++e) {
-    float sum = 0.f;
+__device__ __forceinline__ void route_select_wave(const float (*red)[EM + 1], int E, int k, int renorm, int t,
+                                                  float* __restrict__ w, int32_t* __restrict__ ids,
+                                                  const RouteAlign& ra, bool align, int* s_off, int* s_pos) {
+  const int lane = threadIdx.x & 63;
+  float v = -INFINITY;
+  if (lane < E) {
+    v = 0.f;
 #pragma unroll
-    for (int q = 0; q < NWV; ++q) sum += red[q][e];
-    v[e] = sum;
-    mx = fmaxf(mx, v[e]);
+    for (int q = 0; q < NWV; ++q) v += red[q][lane];
   }
-  float den = 0.f;
-  for (int e = 0; e < E; ++e) den += __expf(v[e] - mx);
-  unsigned long long used = 0;
-  float sel[16];
-  int sid[16];
-  float ssum = 0.f;
+  const float mx = wave_max(v);
+  const float den = wave_sum(lane < E ? __expf(v - mx) : 0.f);
+  bool used = false;
+  float ssum = 0.f, my_sel = 0.f;
+  int my_id = 0;
   for (int j = 0; j < k; ++j) {
-    int best = -1;
-    float bv = -INFINITY;
-    for (int e = 0; e < E; ++e)
-      if (!((used >> e) & 1ull) && (best < 0 || v[e] > bv)) { best = e; bv = v[e]; }
-    used |= 1ull << best;
-    sid[j] = best;
-    sel[j] = __expf(bv - mx) / den;
-    ssum += sel[j];
+    // argmax over the unused experts, lowest index on ties
+    float bv = (lane < E && !used) ? v : -INFINITY;
+    int bi = (lane < E && !used) ? lane : 64;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    const float sel = __expf(bv - mx) / den;
+    ssum += sel;
+    if (lane == bi) used = true;
+    if (lane == j) { my_sel = sel; my_id = bi; }
+    if (align && lane == 0) s_pos[j] = bi;  // expert ids for now; rows below
   }
-  for (int j = 0; j < k; ++j) {
-    w[static_cast<int64_t>(t) * k + j] = renorm ? sel[j] / ssum : sel[j];
-    ids[static_cast<int64_t>(t) * k + j] = sid[j];
+  if (lane < k) {
+    w[static_cast<int64_t>(t) * k + lane] = renorm ? my_sel / ssum : my_sel;
+    ids[static_cast<int64_t>(t) * k + lane] = my_id;
   }
-  if (align) {  // align_kernel's layout for the k pairs of this one token
+  if (align && lane == 0) {  // align_kernel's layout for the k pairs of this one token
     int cnt[EM];
     for (int e = 0; e < ra.E_local; ++e) cnt[e] = 0;
     for (int j = 0; j < k; ++j) {
-      const int e = sid[j] - ra.expert_offset;
+      const int e = s_pos[j] - ra.expert_offset;
       if (e >= 0 && e < ra.E_local) ++cnt[e];
     }
     s_off[0] = 0;
     for (int e = 0; e < ra.E_local; ++e) s_off[e + 1] = s_off[e] + (cnt[e] + ra.block_m - 1) / ra.block_m * ra.block_m;
     for (int j = 0; j < k; ++j) {
-      const int e = sid[j] - ra.expert_offset;
+      const int e = s_pos[j] - ra.expert_offset;
       s_pos[j] = (e >= 0 && e < ra.E_local) ? s_off[e] : -1;  // distinct experts: one row each
     }
   }
@@ -307,7 +312,7 @@ __global__ void __launch_bounds__(512) route2_kernel(const uint16_t* __restrict_
   }
   __syncthreads();
   const bool align = ra.sorted_rows != nullptr;  // T == 1 (host-checked)
-  if (threadIdx.x == 0) route_select<EM, NWV>(red, E, k, renorm, t, w, ids, ra, align, s_off, s_pos);
+  if (wid == 0) route_select_wave<EM, NWV>(red, E, k, renorm, t, w, ids, ra, align, s_off, s_pos);
   if (!align) return;
   __syncthreads();
   for (int e = threadIdx.x; e <= ra.E_local; e += blockDim.x) ra.offsets[e] = s_off[e];
