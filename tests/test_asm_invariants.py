@@ -205,3 +205,24 @@ def test_gemm_m64g_waits_are_counted(tmp_path):
 def test_prefill_attention_has_no_clobber_warning(tmp_path):
     _, log = _compile("prefill_attention", tmp_path)
     assert "reserved registers on the clobber list" not in log
+
+
+def test_gemm_w8_waits_are_counted(tmp_path):
+    """gemm_w8 (fp8 / int8 / int4 weights): inside the LDS-DMA pipeline every vmcnt wait
+    is the steady count G = x + weight DMAs per chunk (chunk c + 1 stays in flight) or the
+    drain; the int4 form's group-scale staging (ordinary loads, before the first DMA) keeps
+    its own compiler waits outside that span. No spills."""
+    asm, log = _compile("gemm_w8", tmp_path)
+    assert "reserved registers on the clobber list" not in log
+    ks = _kernels(asm, "_ZN3xgk14gemm_w8_kernel")
+    assert len(ks) >= 24, len(ks)  # 8 geometries x 3 weight formats
+    for name, body in ks.items():
+        NW, WV, KC, MT, FMT = _targs(name)
+        wrb = KC // 2 if FMT == 2 else KC
+        XI = 16 * MT // (1024 // (2 * KC)) // WV
+        WI = 16 * NW // (1024 // wrb)
+        G = XI + WI
+        got = _vmcnts(_without_epilogue_blocks(_pipeline(body)))
+        assert got <= {0, G}, (name, sorted(got), G)
+        assert G in got, (name, sorted(got), G)
+    _no_spills(asm)
