@@ -80,14 +80,14 @@ struct M64Epi {
 // generation per launch, kept per AR_GRAN-column granule (gens): every GG_AR launch
 // covers all N columns, so each granule advances once per launch whatever the tile
 // width (the O and down launches of a layer may differ) and the pull-free
-// double-buffering argument of the LL all-reduce holds per line. loop: one-process TP-shard simulation -- the "peers" are
-// this rank's own region (lines pushed to source slot r, polled, not added): the
-// traffic and the waits of a `world`-rank group, the numerics of one rank; loop - 1 =
-// a simulated link latency in wall-clock ticks, waited once per tile between the
-// pushes and the polls. More than 64 column tiles (group 2): statistics per PAIR of
-// tiles (the consumer combines <= 64 partial sums per row) -- each tile stores its row
-// sums to ss_tmp, the second of the pair to finish (ticket pair[tile / 2]) adds the
-// two in order.
+// double-buffering argument of the LL all-reduce holds per line. loop: one-process
+// TP-shard simulation -- the "peers" are this rank's own region (lines pushed to source
+// slot r, polled, not added): the traffic and the waits of a `world`-rank group, the
+// numerics of one rank; loop - 1 = a simulated link latency in wall-clock ticks, waited
+// once per tile between the pushes and the polls. More column tiles than the consumer
+// combines (64 per row, 128 at M <= 16; group 2): statistics per PAIR of tiles -- each
+// tile stores its row sums to ss_tmp, the second of the pair to finish (ticket
+// pair[tile / 2]) adds the two in order.
 constexpr int AR_GRAN = 32;  // the narrowest GG_AR tile (16 x NW x WV columns)
 struct ArDesc {
   uint8_t* data[CAR_MAX_RANKS];  // each rank's LL receive region (loop: all this rank's own)
@@ -1129,7 +1129,7 @@ static int m64g_check(int M, int K, int N, const float* part, const uint16_t* ou
   if (M < 1 || M > 64 || S < 1 || (nw != 1 && nw != 2) || cfg < 0 || cfg > 10) return 1;
   if (cfg >= 8 && M > 16) return 1;  // deep-ring configurations: one x tile only
   if (mode < GG_BF16 || mode > GG_AR || mode == GG_MOE_RESID) return 1;
-  // the consumer's statistics paths sum at most 64 partial sums per row (m64g prologue)
+  // the consumer's statistics paths sum at most 64 partial sums per row, 128 at M <= 16
   if (epi.ss_in != nullptr && (epi.ss_n < 1 || epi.ss_n > (M <= 16 ? 128 : 64) || epi.ss_stride < M)) return 1;
   const int cols = 16 * nw * m64g_cfg_waves(cfg), kc = m64g_cfg_kc(cfg);
   if (K % kc || S > K / kc || N % cols) return 1;
