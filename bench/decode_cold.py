@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--arrange", default="random", choices=["random", "pair", "sorted"],
                     help="sequence order: random lengths; pair = seq b and b + B/2 complement each other "
                          "(short + long); sorted = ascending")
+    ap.add_argument("--graph", action="store_true",
+                    help="time `iters` calls captured in one HIP graph (device time; an eager Python loop is "
+                         "host-bound below ~10 us per call)")
     ap.add_argument("--probe", action="store_true",
                     help="anatomy: also time the kernel without its prologue (11), key loop (12), both (13)")
     a = ap.parse_args()
@@ -88,15 +91,25 @@ def main():
             for i in range(2 * len(caches)):
                 f(i)
             torch.cuda.synchronize()
+            body = lambda: [f(i) for i in range(a.iters)]  # noqa: E731
+            if a.graph:
+                gs = torch.cuda.Stream()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.stream(gs):
+                    with torch.cuda.graph(g, stream=gs):
+                        body()
+                torch.cuda.synchronize()
+                body = g.replay
+                body()
+                torch.cuda.synchronize()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-            for i in range(a.iters):
-                f(i)
+            body()
             e.record()
             torch.cuda.synchronize()
             us = s.elapsed_time(e) / a.iters * 1000.0
             print(json.dumps({"op": "decode_attention_fq", "cache": mode, "B": B, "L": a.L, "stagger": a.stagger, "bs": bs,
-                              "splits": S, "depth": dp, "arrange": a.arrange, "us": round(us, 2), "TB/s": round(nbytes / us / 1e6, 3)}), flush=True)
+                              "splits": S, "depth": dp, "arrange": a.arrange, "graph": a.graph, "us": round(us, 2), "TB/s": round(nbytes / us / 1e6, 3)}), flush=True)
 
 
 if __name__ == "__main__":
