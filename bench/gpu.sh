@@ -87,6 +87,11 @@ r6f)  # closing kernel profiles: 8B c64 / c1, Mixtral c1, one 70B TP8 rank c1
   bash bench/profile.sh "$o/c1" --concurrency 1
   bash bench/profile.sh "$o/mix_c1" --model mixtral-8x7b --concurrency 1
   bash bench/profile.sh "$o/tp8_c1" --model llama3-70b --tp-shard 8 --concurrency 1 ;;
+r6w)  # gate_up on gemm_pf at 448-512-row mixed steps: same-box A/B at --prompt-len 416 (479-row steps)
+  for r in 1 2; do
+    run "p416_new_$r" 250 $B --steps 400 --warmup 40 --prompt-len 416
+    run "p416_old_$r" 250 env XGS_TUNE=pf_windows=gate_up:513-576/down:513-576 $B --steps 400 --warmup 40 --prompt-len 416
+  done ;;
 r6d)  # 70B TP8 rank, batch 1: down-projection plans under GG_AR (same box)
   for pl in base "8192x3584x1@16=1,1,9" "8192x3584x1@16=1,2,9" "8192x3584x1@16=2,2,6" "8192x3584x1@16=1,2,5"; do
     n=$(echo "$pl" | tr -c 'A-Za-z0-9_\n' '_')

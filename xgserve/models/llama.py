@@ -67,9 +67,9 @@ MW_MAX_TOKENS = min(MW_MAX_M, tune.get_int("mw_max_tokens", MW_MAX_M))
 # tuned library GEMM (profiles/r6/r6p_pf_vs_library.md, cold weights, the engine's
 # library forms) -- QKV / O / down as split-K partials into their consumers, gate_up
 # with the SiLU gate in its epilogue:
-#   gate_up 513-576 rows: the library's tile-quantisation cliff (103 us at 512 rows,
-#     135 at 575), where two 288-row tiles cover the step (pf 110 us); 2-17 % behind
-#     the library at every other measured size;
+#   gate_up 448-576 rows: 4-5 % ahead of the library's GEMM + SiLU-gate pair at 448 / 512
+#     rows, 22 % at 575 -- its tile-quantisation cliff (GEMM 103 us at 512 rows, 135 at
+#     575), where two 288-row tiles cover the step; within +-1 % or behind elsewhere;
 #   down 513-576 rows: 5-11 % ahead of the library's split-4 GEMM in isolation at every
 #     measured size from 320 to 576 rows, but its 8 fp32 slabs (vs the library's 4) cost
 #     the consumer more than that below 513: 447-row steps (--prompt-len 384) ran 11,603
@@ -78,7 +78,7 @@ MW_MAX_TOKENS = min(MW_MAX_M, tune.get_int("mw_max_tokens", MW_MAX_M))
 #     to their consumers (r5: -0.5 % end to end with every projection on pf).
 # XGS_TUNE pf: "1" = these windows, "0" = library everywhere, or a comma list of
 # projections to allow; pf_windows overrides the table ("gate_up:513-576/down:321-576").
-PF_WINDOWS_DEFAULT = "gate_up:513-576/down:513-576"
+PF_WINDOWS_DEFAULT = "gate_up:448-576/down:513-576"
 
 
 def _parse_pf_windows(spec: str):

@@ -11,7 +11,7 @@ Keys (default in brackets; every default is the production setting):
   spin_wait [1]            host polls the step event instead of blocking
   pf [1]                   gemm_pf projections of prompt-sized mixed steps: 1 = the measured windows,
                            0 = library GEMMs, or a list "qkv,o,gate_up,down" of those allowed
-  pf_windows [gate_up:513-576/down:513-576]   step sizes (tokens) per projection that take gemm_pf
+  pf_windows [gate_up:448-576/down:513-576]   step sizes (tokens) per projection that take gemm_pf
   moe_pf [1]               prompt-sized expert GEMMs (> 256 token-expert pairs) on gemm_pf's grouped form
   krot [1]                 K-chunk rotation of the weight-streaming GEMMs (0 / 1 / 2)
   m64_plans / mw_plans     gemm_m64g / gemm_mw plan overrides, "NxKxMODE@BUCKET=...;..."
