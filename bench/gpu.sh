@@ -87,6 +87,16 @@ r6f)  # closing kernel profiles: 8B c64 / c1, Mixtral c1, one 70B TP8 rank c1
   bash bench/profile.sh "$o/c1" --concurrency 1
   bash bench/profile.sh "$o/mix_c1" --model mixtral-8x7b --concurrency 1
   bash bench/profile.sh "$o/tp8_c1" --model llama3-70b --tp-shard 8 --concurrency 1 ;;
+r6e)  # split QKV prologue in decode attention (partials issued ahead of the K/V preloads): tests + same-box A/B vs depth 4 (classic)
+  pyt e_tests 600 tests/test_fused_decode_gpu.py
+  run e_cold 200 python -u bench/decode_cold.py --graph --depth 2 4 3 --splits 1 2 4
+  run e_cold_b1 200 python -u bench/decode_cold.py --graph --B 1 --L 768 --depth 2 4 --splits 4 8 16
+  for r in 1 2; do
+    run "c64_split_$r" 250 $B --steps 300 --warmup 30
+    run "c64_classic_$r" 250 env XGS_TUNE=decode_depth=4 $B --steps 300 --warmup 30
+    run "c1_split_$r" 200 $B --concurrency 1 --steps 300 --warmup 30
+    run "c1_classic_$r" 200 env XGS_TUNE=decode_depth=4 $B --concurrency 1 --steps 300 --warmup 30
+  done ;;
 r6w)  # gate_up on gemm_pf at 448-512-row mixed steps: same-box A/B at --prompt-len 416 (479-row steps)
   for r in 1 2; do
     run "p416_new_$r" 250 $B --steps 400 --warmup 40 --prompt-len 416

@@ -153,6 +153,109 @@ __device__ __forceinline__ void decode_qkv_prologue(const QkvFuse& fq, int b, in
   if (wkv) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the cache row lands before any wave reads it
 }
 
+// The same prologue in two halves for S <= 8 (every decode QKV plan): qkv_issue puts
+// this thread's work item's partial loads (all 8 clamped splits) and RoPE factors in
+// flight, the kernel then issues its K/V preloads, and qkv_finish waits only for the
+// older prologue loads (in-order vmcnt) -- the prologue's L2 round trip, RoPE and
+// cache append overlap the K/V HBM latency instead of queueing behind it.
+template <int D>
+struct QkvItem {
+  float4 a[8], e[8];   // split partials: rotation-pair first / second halves (v item: e = a's address)
+  float4 cv, sv;       // RoPE cos / sin of the 4 pairs
+  int kind;            // 0 none, 1 q head (index hh), 2 k head, 3 v values
+  int hh, c;
+  int64_t dst;
+};
+
+template <int D, int G>
+__device__ __forceinline__ void qkv_issue(const QkvFuse& fq, int b, int kvh, int Hq, int Hkv, int bs, bool owns_last,
+                                          QkvItem<D>& w) {
+  constexpr int HALF = D / 2, CPH = HALF / 4, NR = (G + 1) * CPH;
+  static_assert(NR + D / 4 <= 256, "one prologue work item per thread");
+  const int64_t width = static_cast<int64_t>(Hq + 2 * Hkv) * D;
+  const int64_t slab = static_cast<int64_t>(gridDim.y) * width;
+  const int64_t row = static_cast<int64_t>(b) * width;
+  const int slot = fq.slot_mapping[b];
+  const bool wkv = owns_last && slot >= 0;
+  w.dst = wkv ? ((static_cast<int64_t>(slot / bs) * Hkv + kvh) * bs + slot % bs) * D : 0;
+  const int it = threadIdx.x;
+  int64_t col = 0;
+  w.kind = 0;
+  if (it < NR) {
+    w.hh = it / CPH;
+    w.c = it % CPH;
+    if (w.hh < G || wkv) {
+      w.kind = w.hh < G ? 1 : 2;
+      col = static_cast<int64_t>(w.hh < G ? kvh * G + w.hh : Hq + kvh) * D + w.c * 4;
+    }
+  } else if (it < NR + D / 4 && wkv) {
+    w.kind = 3;
+    w.c = it - NR;
+    col = static_cast<int64_t>(Hq + Hkv + kvh) * D + w.c * 4;
+  }
+  // unconditional loads (threads without an item re-read the slab's first line, a
+  // v item its own line for the second half): loads under a branch make the
+  // compiler's wait at the join conservative (a small vmcnt that drains the K/V
+  // preloads issued after them)
+  const float* p = fq.part + (w.kind == 0 ? 0 : row + col);
+  const int eo = w.kind == 1 || w.kind == 2 ? HALF : 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    w.a[i] = *reinterpret_cast<const float4*>(p);
+    w.e[i] = *reinterpret_cast<const float4*>(p + eo);
+    if (i + 1 < fq.S) p += slab;
+  }
+  const int pos = fq.apply_rope ? fq.positions[b] : 0;
+  const float* cs = (fq.apply_rope ? fq.cos_sin : fq.part) + static_cast<int64_t>(pos) * D;
+  const int cc = w.kind == 1 || w.kind == 2 ? w.c * 4 : 0;
+  w.cv = *reinterpret_cast<const float4*>(cs + cc);
+  w.sv = *reinterpret_cast<const float4*>(cs + HALF + cc);
+  asm volatile("" ::: "memory");  // keep these loads ahead of the K/V preloads
+}
+
+template <int D, int G>
+__device__ __forceinline__ void qkv_finish(const QkvFuse& fq, QkvItem<D>& w, uint16_t* q_lds) {
+  constexpr int HALF = D / 2;
+  if (w.kind != 0) {
+    float a[4] = {0.f, 0.f, 0.f, 0.f}, e[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float k = i < fq.S ? 1.f : 0.f;
+      a[0] += k * w.a[i].x; a[1] += k * w.a[i].y; a[2] += k * w.a[i].z; a[3] += k * w.a[i].w;
+      e[0] += k * w.e[i].x; e[1] += k * w.e[i].y; e[2] += k * w.e[i].z; e[3] += k * w.e[i].w;
+    }
+    if (w.kind == 3) {
+      *reinterpret_cast<uint2*>(fq.v_cache + w.dst + w.c * 4) = pack4(a);
+    } else {
+      if (fq.apply_rope) {
+        const float cc[4] = {w.cv.x, w.cv.y, w.cv.z, w.cv.w}, ss[4] = {w.sv.x, w.sv.y, w.sv.z, w.sv.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float x1 = a[i], x2 = e[i];
+          a[i] = x1 * cc[i] - x2 * ss[i];
+          e[i] = x2 * cc[i] + x1 * ss[i];
+        }
+      }
+      // q rows through an LDS-qualified pointer: the compiler cannot merge them with the
+      // k-cache stores into one flat store, which would make the barrier wait on vmcnt(0)
+      if (w.kind == 1) {
+        typedef __attribute__((address_space(3))) uint64_t lds_u64;
+        lds_u64* o = (lds_u64*)(q_lds + w.hh * D);
+        const uint2 pa = pack4(a), pe = pack4(e);
+        o[w.c] = (static_cast<uint64_t>(pa.y) << 32) | pa.x;
+        o[HALF / 4 + w.c] = (static_cast<uint64_t>(pe.y) << 32) | pe.x;
+      } else {
+        uint16_t* o = fq.k_cache + w.dst;
+        *reinterpret_cast<uint2*>(o + w.c * 4) = pack4(a);
+        *reinterpret_cast<uint2*>(o + HALF + w.c * 4) = pack4(e);
+      }
+    }
+  }
+  // the cache row lands before any wave reads it (waits for the K/V preloads too,
+  // which by now have had the prologue's latency to arrive)
+  if (w.kind >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Per 16-key tile and wave:
 //   S^T[16 keys][16 heads] = K . Q^T     4 x v_mfma_f32_16x16x32_bf16 (K frags straight from HBM)
 //   online softmax per head (lane&15 = head): 2 xor-shuffles per reduction,
@@ -211,7 +314,9 @@ __device__ __forceinline__ float combine_splits(const float* __restrict__ lse, c
 // PR (anatomy probes, bench/decode_cold.py --probe; output garbage): 0 = the kernel;
 // 1 = no fused prologue (no QKV-partial reads / RoPE / KV append); 2 = no key loop;
 // 3 = neither (launch + merge + store only); 4 = the kernel with cached (temporal) K/V loads.
-template <int D, int G, bool FQ, bool KL = false, int NB = 2, int PR = 0>
+// SPRO (FQ): the split prologue (qkv_issue before the K/V preloads, qkv_finish
+// after; QKV plans with S <= 8 -- all of them today); false: the classic prologue.
+template <int D, int G, bool FQ, bool KL = false, int NB = 2, int PR = 0, bool SPRO = true>
 __global__ void __launch_bounds__(256) decode_attn_kernel(
     const uint16_t* __restrict__ q, int64_t q_stride, const uint16_t* kc, const uint16_t* vc,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ seq_lens,
@@ -219,7 +324,9 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
     int Hq, int Hkv, int bs, float scale, int num_splits, QkvFuse fq) {
   using C = DecodeCfg<D, G>;
   const int kvh = blockIdx.x, b = blockIdx.y, split = blockIdx.z;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // wid through readfirstlane: wave-uniform to the compiler, so the page-table reads of
+  // load_tile are scalar loads (lgkmcnt) and do not wait behind the prologue's vector loads
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int L = seq_lens[b];
   const int ntiles = (L + 15) >> 4;
@@ -240,10 +347,12 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   // flight while tile t is processed (one tile of lookahead left HBM idle between
   // a wave's tiles at 64 concurrent sequences)
   uint4 kf[NB][C::KK], vr[NB][C::VLD];
+  // t < 0: a discarded load of the cache's first tile (keeps the preload count static)
   auto load_tile = [&](int t, uint4 (&kf)[C::KK], uint4 (&vr)[C::VLD]) {
     const int key0 = t * 16;
-    const int page = bt[key0 / bs];
-    const int64_t base = (static_cast<int64_t>(page) * Hkv + kvh) * head_stride + static_cast<int64_t>(key0 % bs) * D;
+    const int64_t base = t < 0 ? 0
+                               : (static_cast<int64_t>(bt[key0 / bs]) * Hkv + kvh) * head_stride +
+                                     static_cast<int64_t>(key0 % bs) * D;
     // K/V are read once per step and a step's cache (GBs at 64 sequences) never fits the
     // L2 / Infinity Cache: non-temporal loads, 5.3 -> 6.1 TB/s at 2K keys (r4_decode_nt.md)
     auto ldkv = [](const uint16_t* p) { return PR == 4 ? ld16(p) : ld16_nt(p); };
@@ -271,15 +380,28 @@ __global__ void __launch_bounds__(256) decode_attn_kernel(
   // except the tile holding the key the prologue appends (the last one), which is
   // loaded after the prologue's barrier as before
   constexpr bool LOOP = PR != 2 && PR != 3;
+  constexpr bool PRO = FQ && PR != 1 && PR != 3;
+  // S <= 8 (SPRO): the prologue's own loads go out first (qkv_issue / qkv_finish). A
+  // template choice, not a runtime branch, and the issue runs for every workgroup
+  // (its loads stay in bounds for any L): loads under a branch, or registers the
+  // other arm reuses, make the compiler's wait at the join drain everything after them
+  constexpr bool SPLIT = PRO && SPRO;
+  QkvItem<D> qi;
+  if constexpr (SPLIT) qkv_issue<D, G>(fq, b, kvh, Hq, Hkv, bs, split == (ntiles - 1) / tps, qi);
+  // every wave issues all NB preloads (skipped tiles as discarded loads): a static
+  // count lets the compiler wait for the older prologue loads with vmcnt(NB * 8)
+  // instead of vmcnt(0) at a control-flow join
   bool pre[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int tj = t0 + j * C::WAVES;
     pre[j] = LOOP && FQ && tj < t_end && tj != ntiles - 1;
-    if (pre[j]) load_tile(tj, kf[j], vr[j]);
+    if constexpr (LOOP && FQ) load_tile(pre[j] ? tj : -1, kf[j], vr[j]);
   }
   if constexpr (FQ) {
-    if constexpr (PR != 1 && PR != 3) {
+    if constexpr (SPLIT) {
+      if (L > 0) qkv_finish<D, G>(fq, qi, q_lds);
+    } else if constexpr (PRO) {
       if (L > 0) decode_qkv_prologue<D, G>(fq, b, kvh, Hq, Hkv, bs, split == (ntiles - 1) / tps, q_lds);
     }
     __syncthreads();
@@ -464,19 +586,30 @@ static void launch_decode(const uint16_t* q, int64_t qs, const uint16_t* kc, con
       return;
     }
 #endif
-    if (depth == 3) {
-      hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, true, 3>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc,
-                         bt, bts, sl, po, pl, out, os, Hq, Hkv, bs, scale, S, fq);
-      if (S > 1) hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
-      return;
-    }
   }
-  if constexpr (D == 128 && G <= 4)
-    hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, true>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt,
-                       bts, sl, po, pl, out, os, Hq, Hkv, bs, scale, S, fq);
-  else
-    hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, bt, bts, sl,
-                       po, pl, out, os, Hq, Hkv, bs, scale, S, fq);
+  // the split prologue handles QKV plans of <= 8 splits; depth 4 = the classic
+  // prologue at depth 2 (A/B)
+  const bool classic = FQ && (fq.S > 8 || depth == 4);
+#define XGK_DEC(KL, NB, SP)                                                                                          \
+  hipLaunchKernelGGL((decode_attn_kernel<D, G, FQ, KL, NB, 0, SP>), dim3(Hkv, B, S), dim3(256), 0, st, q, qs, kc, vc, \
+                     bt, bts, sl, po, pl, out, os, Hq, Hkv, bs, scale, S, fq)
+  if constexpr (D == 128 && G <= 4 && FQ) {
+    if (depth == 3) {
+      if (classic) XGK_DEC(true, 3, false);
+      else XGK_DEC(true, 3, true);
+    } else {
+      if (classic) XGK_DEC(true, 2, false);
+      else XGK_DEC(true, 2, true);
+    }
+  } else if constexpr (D == 128 && G <= 4) {
+    XGK_DEC(true, 2, true);
+  } else if constexpr (FQ) {
+    if (classic) XGK_DEC(false, 2, false);
+    else XGK_DEC(false, 2, true);
+  } else {
+    XGK_DEC(false, 2, true);
+  }
+#undef XGK_DEC
   if (S > 1) hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(B * Hq), dim3(D), 0, st, po, pl, out, os, Hq, S);
 }
 
@@ -511,9 +644,9 @@ int decode_attention_fq(const float* part, int S_qkv, const int32_t* positions, 
   if (part == nullptr || S_qkv < 1 || bs % 16 != 0 || Hq % Hkv != 0 || D != 128 || num_splits < 1) return -1;
   if (num_splits > 1 && (part_out == nullptr || part_lse == nullptr)) return -1;
 #ifdef XGK_PROBES
-  if (out == nullptr || depth < 2 || (depth > 3 && (depth < 11 || depth > 14))) return -1;
+  if (out == nullptr || depth < 2 || (depth > 4 && (depth < 11 || depth > 14))) return -1;
 #else
-  if (out == nullptr || depth < 2 || depth > 3) return -1;
+  if (out == nullptr || depth < 2 || depth > 4) return -1;
 #endif
   const QkvFuse fq{part, S_qkv, positions, cos_sin, slots, kc, vc, apply_rope};
   const int G = Hq / Hkv;

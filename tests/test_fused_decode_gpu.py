@@ -171,10 +171,12 @@ def _paged(lens, Hkv, D, bs, extra_pages=8):
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 8)])
-@pytest.mark.parametrize("S", [1, 4, 8])
+@pytest.mark.parametrize("S", [1, 4, 8, 12])
 @pytest.mark.parametrize("splits", [1, 3, 16])
-@pytest.mark.parametrize("depth", [2, 3])
+@pytest.mark.parametrize("depth", [2, 3, 4])
 def test_decode_attention_fused_prologue(Hq, Hkv, S, splits, depth):
+    """S <= 8 runs the split prologue (partial loads issued ahead of the K/V
+    preloads), S = 12 and depth 4 the classic one."""
     import xgserve.ops.attention as A
     D, bs = 128, 16
     lens = [1, 17, 300, 64, 0, 129]  # row 4: a graph padding row (no KV write, no attention)

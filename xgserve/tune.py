@@ -17,7 +17,7 @@ Keys (default in brackets; every default is the production setting):
   m64_plans / mw_plans     gemm_m64g / gemm_mw plan overrides, "NxKxMODE@BUCKET=...;..."
   mw_max_tokens [320]      largest step on gemm_mw
   resid_inlaunch_kb [32]   in-launch residual reduce bound of the fused decode GEMMs
-  decode_depth [2]         decode attention K/V register pipeline depth
+  decode_depth [2]         decode attention K/V register pipeline depth (4: depth 2 with the classic QKV prologue)
   decode_max_splits [16]   split-K cap of decode attention
   gemm_ar [1]              TP decode: all-reduce inside the row-parallel O / down GEMM launches
   gemm_ar_shared [0]       test-only: GG_AR also for <= 4 ranks sharing one GPU (one-GPU boxes)
