@@ -87,6 +87,17 @@ r6f)  # closing kernel profiles: 8B c64 / c1, Mixtral c1, one 70B TP8 rank c1
   bash bench/profile.sh "$o/c1" --concurrency 1
   bash bench/profile.sh "$o/mix_c1" --model mixtral-8x7b --concurrency 1
   bash bench/profile.sh "$o/tp8_c1" --model llama3-70b --tp-shard 8 --concurrency 1 ;;
+r6l)  # static-count K/V refills in the decode key loop (exact vmcnt per register tile): tests + same-box A/B vs depth 5
+  pyt l_tests 900 tests/test_fused_decode_gpu.py tests/test_kernels_gpu.py -k "decode or attention"
+  run l_cold 200 python -u bench/decode_cold.py --graph --depth 2 5 --splits 1 2 4
+  run l_cold_2k 200 python -u bench/decode_cold.py --graph --L 2048 --caches 3 --depth 2 5 --splits 1 2
+  for r in 1 2; do
+    run "c64_sl_$r" 250 $B --steps 300 --warmup 30
+    run "c64_nosl_$r" 250 env XGS_TUNE=decode_depth=5 $B --steps 300 --warmup 30
+    run "c1_sl_$r" 200 $B --concurrency 1 --steps 300 --warmup 30
+    run "c1_nosl_$r" 200 env XGS_TUNE=decode_depth=5 $B --concurrency 1 --steps 300 --warmup 30
+  done
+  run tp8_c1 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20 ;;
 r6e)  # split QKV prologue in decode attention (partials issued ahead of the K/V preloads): tests + same-box A/B vs depth 4 (classic)
   pyt e_tests 600 tests/test_fused_decode_gpu.py
   run e_cold 200 python -u bench/decode_cold.py --graph --depth 2 4 3 --splits 1 2 4
