@@ -87,6 +87,12 @@ r6f)  # closing kernel profiles: 8B c64 / c1, Mixtral c1, one 70B TP8 rank c1
   bash bench/profile.sh "$o/c1" --concurrency 1
   bash bench/profile.sh "$o/mix_c1" --model mixtral-8x7b --concurrency 1
   bash bench/profile.sh "$o/tp8_c1" --model llama3-70b --tp-shard 8 --concurrency 1 ;;
+r6pp)  # prefill attention ping-pong form (waves 4-7 half a tile behind): tests + kernel A/B at 2K / 8K + 8K TTFT
+  pyt pp_tests 600 tests/test_kernels_gpu.py -k "prefill"
+  run pp_attn 300 python -u bench/prefill_bench.py --lens 2048 8192 --gh 0 -382 -482 -384 -484 --no-ttft ;;
+r6po)  # prefill attention OPT variants (K 8-ahead, softmax split, page prefetch), alternating order at 8K
+  pyt po_tests 600 tests/test_kernels_gpu.py -k "prefill"
+  run po_attn 400 python -u bench/prefill_bench.py --lens 8192 --no-ttft --gh -382 -10382 -20382 -40382 -70382 -382 -10382 -20382 -40382 -70382 -384 -70384 -384 -70384 ;;
 r6l)  # static-count K/V refills in the decode key loop (exact vmcnt per register tile): tests + same-box A/B vs depth 5
   pyt l_tests 900 tests/test_fused_decode_gpu.py tests/test_kernels_gpu.py -k "decode or attention"
   run l_cold 200 python -u bench/decode_cold.py --graph --depth 2 5 --splits 1 2 4
