@@ -87,6 +87,35 @@ r6f)  # closing kernel profiles: 8B c64 / c1, Mixtral c1, one 70B TP8 rank c1
   bash bench/profile.sh "$o/c1" --concurrency 1
   bash bench/profile.sh "$o/mix_c1" --model mixtral-8x7b --concurrency 1
   bash bench/profile.sh "$o/tp8_c1" --model llama3-70b --tp-shard 8 --concurrency 1 ;;
+r6fg)  # fused decode-GEMM forms vs plain forms, graph-timed, cold weights (70B TP8 / TP1 shard, 8B)
+  run fg_70t8 200 python -u bench/fused_gemm_bench.py --model llama3-70b --tp 8 --M 1 4
+  run fg_8b 200 python -u bench/fused_gemm_bench.py --model llama3-8b --tp 1 --M 1 64 ;;
+r6fs)  # fused-form plan sweeps (norm128 / GG_RESID), graph-timed, cold weights
+  run fs_70t8 400 python -u bench/fused_gemm_bench.py --model llama3-70b --tp 8 --M 1 --sweep
+  run fs_8b 400 python -u bench/fused_gemm_bench.py --model llama3-8b --tp 1 --M 1 64 --sweep ;;
+r6fp)  # fused-form plans from the r6fs sweep: same-box end-to-end A/B
+  for r in 1 2; do
+    run "tp8_base_$r" 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+    run "tp8_new_$r" 300 env "XGS_TUNE=m64_plans=1280x8192x1@16=1,8,0;8192x1024x1@16=1,1,0" $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+    run "c1_base_$r" 200 $B --concurrency 1 --steps 300 --warmup 30
+    run "c1_gu3_$r" 200 env "XGS_TUNE=m64_plans=28672x4096x2@16=2,1,3" $B --concurrency 1 --steps 300 --warmup 30
+    run "c64_base_$r" 250 $B --steps 300 --warmup 30
+    run "c64_dn141_$r" 250 env "XGS_TUNE=m64_plans=4096x14336x1@64=1,4,1" $B --steps 300 --warmup 30
+  done ;;
+r6rt)  # tests after the S=1 GG_RESID LDS tail + fused-form plans
+  pyt rt_tests 1100 tests/test_fused_decode_gpu.py tests/test_gemm_ar_gpu.py tests/test_tp_gpu.py tests/test_custom_ar_gpu.py tests/test_engine_gpu.py tests/test_skinny_gpu.py ;;
+r6g8)  # 70B TP8 rank, batch 1: per-GEMM (by grid) kernel times under the fused decode layer (and A/B knobs)
+  for v in base "fused_decode=0" "krot=0" "krot=2"; do
+    n=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')
+    raw=$(mktemp -d "${TMPDIR:-/tmp}/xgs_g8.XXXXXX")
+    if [ "$v" = base ]; then e="XGS_TUNE="; else e="XGS_TUNE=$v"; fi
+    env $e timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$raw" -o run -- \
+        python3 bench.py --steps 60 --warmup 20 --model llama3-70b --tp-shard 8 --concurrency 1 > "$o/bench_$n.log" 2>&1
+    tr=$(find "$raw" -name '*kernel_trace.csv' | sort | tail -n 1)
+    python3 bench/prof_summary.py "$tr" --window-ms 200 --by-grid > "$o/grid_$n.md"
+    rm -rf "$raw"
+    tail -n 1 "$o/bench_$n.log" | cut -c1-200
+  done ;;
 r6pp)  # prefill attention ping-pong form (waves 4-7 half a tile behind): tests + kernel A/B at 2K / 8K + 8K TTFT
   pyt pp_tests 600 tests/test_kernels_gpu.py -k "prefill"
   run pp_attn 300 python -u bench/prefill_bench.py --lens 2048 8192 --gh 0 -382 -482 -384 -484 --no-ttft ;;

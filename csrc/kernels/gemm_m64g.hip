@@ -159,9 +159,13 @@ __device__ __forceinline__ bool agent_ticket(int* cnt, int last_value, int* flag
 // of loads (IB x 4 slab reads + IB residual reads in flight before the first add):
 // the slabs were written by other XCDs, so every read is a MALL round trip and a
 // pass-by-pass loop paid one per NTHR x 16 B (~1 us per 16 KB at M = 64).
+// ys (S == 1): the tile staged in LDS [M][COLS] by this workgroup instead of its slab
+// (no store -> drain -> reload round trip). 4 < S <= 8: all S slab reads of an item in
+// one batch (a 4-wide batch loop paid two MALL round trips per pass).
 template <int COLS, int NTHR>
 __device__ __forceinline__ void m64g_resid_reduce(const float* __restrict__ part, int S, int M, int N, int tile,
-                                                  const M64Epi& epi, int r0 = 0, int r1 = -1) {
+                                                  const M64Epi& epi, int r0 = 0, int r1 = -1,
+                                                  const float* ys = nullptr) {
   constexpr int C4 = COLS / 4;
   constexpr int IB = 4;
   static_assert(64 % C4 == 0 && NTHR % C4 == 0, "row groups must not straddle waves");
@@ -187,22 +191,49 @@ __device__ __forceinline__ void m64g_resid_reduce(const float* __restrict__ part
 #pragma unroll
       for (int j = 0; j < 4; ++j) y[i][j] = 0.f;
     }
-    for (int s0 = 0; s0 < S; s0 += 4) {
-      float4 v[IB][4];
+    if (ys != nullptr) {
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        const float4 v = *reinterpret_cast<const float4*>(ys + (m[i] - r0) * COLS + 4 * c[i]);
+        y[i][0] = v.x;
+        y[i][1] = v.y;
+        y[i][2] = v.z;
+        y[i][3] = v.w;
+      }
+    } else if (S > 4 && S <= 8) {
+      float4 v[IB][8];
 #pragma unroll
       for (int i = 0; i < IB; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[i][j] = *reinterpret_cast<const float4*>(part + min(s0 + j, S - 1) * slab + off[i]);
+        for (int j = 0; j < 8; ++j) v[i][j] = *reinterpret_cast<const float4*>(part + min(j, S - 1) * slab + off[i]);
 #pragma unroll
       for (int i = 0; i < IB; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float k = s0 + j < S ? 1.f : 0.f;
+        for (int j = 0; j < 8; ++j) {
+          const float k = j < S ? 1.f : 0.f;
           y[i][0] += k * v[i][j].x;
           y[i][1] += k * v[i][j].y;
           y[i][2] += k * v[i][j].z;
           y[i][3] += k * v[i][j].w;
         }
+    } else {
+      for (int s0 = 0; s0 < S; s0 += 4) {
+        float4 v[IB][4];
+#pragma unroll
+        for (int i = 0; i < IB; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[i][j] = *reinterpret_cast<const float4*>(part + min(s0 + j, S - 1) * slab + off[i]);
+#pragma unroll
+        for (int i = 0; i < IB; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float k = s0 + j < S ? 1.f : 0.f;
+            y[i][0] += k * v[i][j].x;
+            y[i][1] += k * v[i][j].y;
+            y[i][2] += k * v[i][j].z;
+            y[i][3] += k * v[i][j].w;
+          }
+      }
     }
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
@@ -231,14 +262,16 @@ __device__ __forceinline__ void m64g_resid_reduce(const float* __restrict__ part
 // GG_RESID tail: tile ticket -> the last arriver reduces the tile.
 template <int COLS, int NTHR>
 __device__ __forceinline__ void m64g_resid_tail(const float* __restrict__ part, int S, int M, int N,
-                                                const M64Epi& epi, int* flag, int bx) {
+                                                const M64Epi& epi, int* flag, int bx, const float* ys = nullptr) {
   if (S > 1) {
     if (!agent_ticket(epi.counters + bx, S - 1, flag)) return;
+  } else if (ys != nullptr) {
+    __syncthreads();  // every wave's LDS stage
   } else {  // one split: the tile's own slab, written by every wave, read back in another layout
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  m64g_resid_reduce<COLS, NTHR>(part, S, M, N, bx, epi);
+  m64g_resid_reduce<COLS, NTHR>(part, S, M, N, bx, epi, 0, -1, ys);
 }
 
 // GG_AR tail (M64Epi::ar_*): tile ticket -> the last arriver reduces the S slabs,
@@ -635,8 +668,9 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
   // acc[nt][mt][r] = out[m = 16 mt + li][n = nbase + 16 nt + 4 g + r]
   const bool silu_split = NW == 2 && mode == GG_SILU && S > 1;
   constexpr int TCOLS = 16 * NW * WV;
-  if (mode == GG_AR && S == 1 && 256 + M * TCOLS * 4 <= static_cast<int>(sizeof(lds0))) {
-    // one split: the tile goes through LDS to the all-reduce tail (no slab store + reload)
+  if ((mode == GG_AR || mode == GG_RESID) && S == 1 && 256 + M * TCOLS * 4 <= static_cast<int>(sizeof(lds0))) {
+    // one split: the tile goes through LDS to the residual / all-reduce tail (no slab
+    // store + drain + reload)
     __syncthreads();  // every wave is past its last ring read
     float* ys = reinterpret_cast<float*>(lds0 + 256);
 #pragma unroll
@@ -648,7 +682,8 @@ __global__ void __launch_bounds__(64 * WV, 1) gemm_m64g_kernel(const uint16_t* _
         *reinterpret_cast<float4*>(ys + m * TCOLS + (nbase - bx * TCOLS) + 16 * nt + 4 * g) =
             make_float4(acc[nt][mt][0], acc[nt][mt][1], acc[nt][mt][2], acc[nt][mt][3]);
     }
-    m64g_ar_tail<TCOLS, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0), bx, ar_dv, ys);
+    if (mode == GG_AR) m64g_ar_tail<TCOLS, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0), bx, ar_dv, ys);
+    else m64g_resid_tail<TCOLS, 64 * WV>(part, S, M, N, epi, reinterpret_cast<int*>(lds0), bx, ys);
   } else if (mode == GG_PARTIAL || mode == GG_RESID || mode == GG_AR || silu_split) {
     float* pp = part + static_cast<int64_t>(s) * M * N;
 #pragma unroll

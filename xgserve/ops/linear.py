@@ -106,7 +106,8 @@ _M64_TUNED = {
     # 16 / 32 re-swept with K rotation in round 4 (profiles/r4_m64g_sweep_m1.jsonl; 64: r4_m64g_sweep_rot.jsonl)
     (6144, 4096, MODE_PARTIAL): {64: (2, 5, 3), 32: (1, 5, 7), 16: (1, 2, 9)},
     (4096, 4096, MODE_PARTIAL): {64: (1, 4, 0), 32: (1, 4, 0), 16: (1, 3, 0)},
-    (28672, 4096, MODE_SILU): {64: (2, 1, 1), 32: (2, 1, 3), 16: (2, 1, 5)},
+    # bucket 16: the fused (row-scaled) form's sweep, r6/r6_fused_plans.md (batch 1 +3 %)
+    (28672, 4096, MODE_SILU): {64: (2, 1, 1), 32: (2, 1, 3), 16: (2, 1, 3)},
     (4096, 14336, MODE_PARTIAL): {64: (2, 8, 3), 32: (1, 4, 1), 16: (1, 4, 9)},
     # Llama-3-70B TP1
     (10240, 8192, MODE_PARTIAL): {64: (2, 2, 1), 16: (2, 8, 5)},
@@ -131,13 +132,13 @@ _M64_TUNED = {
     (3584, 4096, MODE_SILU): {64: (2, 4, 6), 32: (2, 4, 0), 16: (2, 4, 0)},  # gate_up8t8
     (8192, 4096, MODE_PARTIAL): {64: (2, 4, 3), 32: (2, 4, 3), 16: (2, 4, 1)},  # o70t2
     (8192, 2048, MODE_PARTIAL): {64: (1, 2, 0), 32: (1, 2, 0), 16: (1, 2, 0)},  # o70t4
-    (8192, 1024, MODE_PARTIAL): {64: (1, 2, 2), 32: (2, 2, 4), 16: (1, 1, 9)},  # o70t8
+    (8192, 1024, MODE_PARTIAL): {64: (1, 2, 2), 32: (2, 2, 4), 16: (1, 1, 0)},  # o70t8 (16: fused-form sweep)
     (4096, 2048, MODE_PARTIAL): {64: (1, 4, 2), 32: (1, 4, 4), 16: (1, 2, 0)},  # o8t2
     (4096, 1024, MODE_PARTIAL): {64: (1, 4, 2), 32: (2, 4, 4), 16: (1, 4, 5)},  # o8t4
     (4096, 512, MODE_PARTIAL): {64: (2, 2, 6), 32: (1, 2, 3), 16: (2, 1, 6)},  # o8t8
     (5120, 8192, MODE_PARTIAL): {64: (2, 6, 1), 32: (2, 8, 5), 16: (1, 6, 6)},  # qkv70t2
     (2560, 8192, MODE_PARTIAL): {64: (1, 6, 1), 32: (2, 8, 1), 16: (1, 6, 0)},  # qkv70t4
-    (1280, 8192, MODE_PARTIAL): {64: (1, 8, 0), 32: (1, 8, 0), 16: (2, 8, 4)},  # qkv70t8
+    (1280, 8192, MODE_PARTIAL): {64: (1, 8, 0), 32: (1, 8, 0), 16: (1, 8, 0)},  # qkv70t8 (16: fused-form sweep)
     (3072, 4096, MODE_PARTIAL): {64: (1, 8, 4), 32: (1, 4, 2), 16: (1, 8, 6)},  # qkv8t2
     (1536, 4096, MODE_PARTIAL): {64: (1, 8, 2), 32: (1, 4, 1), 16: (1, 8, 4)},  # qkv8t4
     (768, 4096, MODE_PARTIAL): {64: (1, 8, 5), 32: (1, 8, 2), 16: (2, 8, 0)},  # qkv8t8
@@ -517,13 +518,14 @@ def tile_counters(device, n: int) -> torch.Tensor:
 
 
 def m64_norm_linear(x: torch.Tensor, w: torch.Tensor, mode: int, stats: RowStats, eps: float,
-                    out: Optional[torch.Tensor] = None):
+                    out: Optional[torch.Tensor] = None, plan=None):
     """gemm_m64g on the raw residual stream x with its RMSNorm applied as a per-row
     epilogue scale rsqrt(sum_sq / K + eps) (norm weight folded into w): PendingSum
-    (MODE_PARTIAL) or bf16 silu(gate) * up (MODE_SILU)."""
+    (MODE_PARTIAL) or bf16 silu(gate) * up (MODE_SILU). plan: (nw, S, cfg) override
+    (sweeps)."""
     M, K = x.shape
     N = w.shape[0]
-    plan = m64_plan(M, N, K, mode)
+    plan = plan or m64_plan(M, N, K, mode)
     if plan is None:
         raise ValueError(f"gemm_m64g: unsupported shape M={M} N={N} K={K} mode={mode}")
     nw, S, cfg = plan
@@ -547,7 +549,7 @@ def m64_norm_linear(x: torch.Tensor, w: torch.Tensor, mode: int, stats: RowStats
 
 
 def m64_resid_linear(x, w: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace, site: int,
-                     eps: float) -> RowStats:
+                     eps: float, plan=None) -> RowStats:
     """resid += x . w^T (bf16 residual stream, in place) on gemm_m64g; returns the
     new residual's RMSNorm statistics. Small split-K slabs are reduced inside the
     GEMM launch (GG_RESID), large ones by the wide add_partials_resid kernel.
@@ -555,7 +557,7 @@ def m64_resid_linear(x, w: torch.Tensor, resid: torch.Tensor, ws: ResidWorkspace
     M, K = x.shape
     xp = x.data_ptr()
     N = w.shape[0]
-    plan = m64_plan(M, N, K, MODE_PARTIAL)
+    plan = plan or m64_plan(M, N, K, MODE_PARTIAL)
     if plan is None or N % 1024 or tuple(resid.shape) != (M, N):
         raise ValueError(f"gemm_m64g resid: unsupported shape M={M} N={N} K={K}")
     nw, S, cfg = plan
