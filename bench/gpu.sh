@@ -104,6 +104,40 @@ r6fp)  # fused-form plans from the r6fs sweep: same-box end-to-end A/B
   done ;;
 r6rt)  # tests after the S=1 GG_RESID LDS tail + fused-form plans
   pyt rt_tests 1100 tests/test_fused_decode_gpu.py tests/test_gemm_ar_gpu.py tests/test_tp_gpu.py tests/test_custom_ar_gpu.py tests/test_engine_gpu.py tests/test_skinny_gpu.py ;;
+r6fs2)  # fused-form plan sweeps, 70B TP8 at M 16 / 64, 8B at M 16
+  run fs2_70t8 600 python -u bench/fused_gemm_bench.py --model llama3-70b --tp 8 --M 16 64 --sweep
+  run fs2_8b 400 python -u bench/fused_gemm_bench.py --model llama3-8b --tp 1 --M 16 --sweep ;;
+r6fp2)  # 70B TP8 rank: down plans from the r6fs2 sweep, same-box end-to-end A/B (c1 and c64)
+  for r in 1 2; do
+    run "tp8c1_base_$r" 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+    run "tp8c1_dn129_$r" 300 env "XGS_TUNE=m64_plans=8192x3584x1@16=1,2,9" $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+    run "tp8c64_base_$r" 400 $B --model llama3-70b --tp-shard 8 --steps 60 --warmup 20
+    run "tp8c64_dn120_$r" 400 env "XGS_TUNE=m64_plans=8192x3584x1@64=1,2,0" $B --model llama3-70b --tp-shard 8 --steps 60 --warmup 20
+  done ;;
+r6g64)  # 70B TP8 rank, 64 concurrent: per-kernel (by grid) times
+  raw=$(mktemp -d "${TMPDIR:-/tmp}/xgs_g64.XXXXXX")
+  timeout -k 10 500 rocprofv3 --kernel-trace --output-format csv -d "$raw" -o run -- \
+      python3 bench.py --steps 40 --warmup 20 --model llama3-70b --tp-shard 8 > "$o/bench.log" 2>&1
+  tr=$(find "$raw" -name '*kernel_trace.csv' | sort | tail -n 1)
+  python3 bench/prof_summary.py "$tr" --window-ms 300 --by-grid --top 30 > "$o/grid.md"
+  rm -rf "$raw" ;;
+r6ri)  # in-launch residual reduce bound at 64 rows (8B o / down): fused microbench + end to end
+  for kb in 32 64 256; do
+    run "ri_fg_$kb" 200 env XGS_TUNE=resid_inlaunch_kb=$kb python -u bench/fused_gemm_bench.py --model llama3-8b --tp 1 --M 64
+  done
+  for r in 1 2; do
+    for kb in 32 64 256; do
+      run "ri_c64_${kb}_$r" 250 env XGS_TUNE=resid_inlaunch_kb=$kb $B --steps 300 --warmup 30
+    done
+  done ;;
+r6c1)  # 8B batch 1: runner-up fused-form plans (r6fs) end to end, same box
+  for r in 1 2; do
+    run "c1_base_$r" 200 $B --concurrency 1 --steps 300 --warmup 30
+    run "c1_dn246_$r" 200 env "XGS_TUNE=m64_plans=4096x14336x1@16=2,4,6" $B --concurrency 1 --steps 300 --warmup 30
+    run "c1_o141_$r" 200 env "XGS_TUNE=m64_plans=4096x4096x1@16=1,4,1" $B --concurrency 1 --steps 300 --warmup 30
+    run "c1_qkv241_$r" 200 env "XGS_TUNE=m64_plans=6144x4096x1@16=2,4,1" $B --concurrency 1 --steps 300 --warmup 30
+    run "c1_gu219_$r" 200 env "XGS_TUNE=m64_plans=28672x4096x2@16=2,1,9" $B --concurrency 1 --steps 300 --warmup 30
+  done ;;
 r6g8)  # 70B TP8 rank, batch 1: per-GEMM (by grid) kernel times under the fused decode layer (and A/B knobs)
   for v in base "fused_decode=0" "krot=0" "krot=2"; do
     n=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')
