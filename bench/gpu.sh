@@ -138,6 +138,16 @@ r6c1)  # 8B batch 1: runner-up fused-form plans (r6fs) end to end, same box
     run "c1_qkv241_$r" 200 env "XGS_TUNE=m64_plans=6144x4096x1@16=2,4,1" $B --concurrency 1 --steps 300 --warmup 30
     run "c1_gu219_$r" 200 env "XGS_TUNE=m64_plans=28672x4096x2@16=2,1,9" $B --concurrency 1 --steps 300 --warmup 30
   done ;;
+r6mo)  # Mixtral decode expert GEMMs in the fused forms (w13 SiLU, w2 + combine into the residual): sweep
+  run mo_sweep 400 python -u bench/moe_fused_bench.py --T 1 4 16 ;;
+r6mw)  # Mixtral: decode-sized w2 on 64-column tiles (moe_w2_small) -- tests + same-box end-to-end A/B
+  pyt mw_tests 600 tests/test_fused_decode_gpu.py tests/test_kernels_gpu.py -k "moe or mixtral or expert"
+  for r in 1 2; do
+    run "mix_c1_new_$r" 250 $B --model mixtral-8x7b --concurrency 1 --steps 100 --warmup 20
+    run "mix_c1_old_$r" 250 env XGS_TUNE=moe_w2_small=0 $B --model mixtral-8x7b --concurrency 1 --steps 100 --warmup 20
+  done
+  run "mix_c8_new" 250 $B --model mixtral-8x7b --concurrency 8 --steps 100 --warmup 20
+  run "mix_c8_old" 250 env XGS_TUNE=moe_w2_small=0 $B --model mixtral-8x7b --concurrency 8 --steps 100 --warmup 20 ;;
 r6g8)  # 70B TP8 rank, batch 1: per-GEMM (by grid) kernel times under the fused decode layer (and A/B knobs)
   for v in base "fused_decode=0" "krot=0" "krot=2"; do
     n=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')

@@ -29,6 +29,14 @@ MOE_CFG_W13_PREFILL = 3
 # gemm_pf_grouped): one MFMA tile of 192-288 rows covers an expert's rows, so each
 # expert's weights stream once per step (profiles/r5_moe_pf.md). XGS_TUNE moe_pf=0: off.
 MOE_PF = __import__("xgserve.tune", fromlist=["get_bool"]).get_bool("moe_pf", True)
+# decode-sized w2 (<= 8 token-expert pairs) in its fused form (combine into the
+# residual in the launch): 64-column tiles on the 4-wave nt config, 2 K splits --
+# bench/moe_fused_bench.py, profiles/r6/r6_moe_w2.md (T = 1 / 4: 39.1 / 109.3 us vs
+# 40.5 / 114+ for the 128-column tiles; Mixtral batch 1 5.12 -> 5.07 ms; 16 pairs
+# (batch 8) measured no gain end to end, so larger steps keep the 128-column tiles).
+# XGS_TUNE moe_w2_small=0 restores the 128-column tiles and their splits (A/B).
+MOE_W2_SMALL = __import__("xgserve.tune", fromlist=["get_bool"]).get_bool("moe_w2_small", True)
+MOE_W2_SMALL_PAIRS = 8
 
 
 def _moe_pf_cfg(pairs: int, E: int) -> int:
@@ -212,7 +220,10 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     cfg2 = (MOE_CFG_W2_PREFILL if T * k > MOE_PREFILL_PAIRS else MOE_CFG_W2) if nw2 == 2 else 0
     kc2 = 128
     S = 1
-    for sk in ((4, 2) if T * k <= 4 else (2,) if T * k <= 16 else ()):
+    small = MOE_W2_SMALL and T * k <= MOE_W2_SMALL_PAIRS and H % 64 == 0 and H // 64 <= 64
+    if small:
+        nw2, cfg2 = 1, MOE_CFG_W2
+    for sk in ((2,) if small else (4, 2) if T * k <= 4 else (2,) if T * k <= 16 else ()):
         if F % (sk * kc2) == 0 and F % (sk * 256) == 0:
             S = sk
             break
