@@ -148,6 +148,18 @@ r6mw)  # Mixtral: decode-sized w2 on 64-column tiles (moe_w2_small) -- tests + s
   done
   run "mix_c8_new" 250 $B --model mixtral-8x7b --concurrency 8 --steps 100 --warmup 20
   run "mix_c8_old" 250 env XGS_TUNE=moe_w2_small=0 $B --model mixtral-8x7b --concurrency 8 --steps 100 --warmup 20 ;;
+r6fs3)  # fused-form plan sweeps: 70B TP1 at M 1, 8B TP2 (Mixtral TP2 attention) at M 1 / 64
+  run fs3_70t1 900 python -u bench/fused_gemm_bench.py --model llama3-70b --tp 1 --M 1 --sweep
+  run fs3_8t2 500 python -u bench/fused_gemm_bench.py --model llama3-8b --tp 2 --M 1 64 --sweep ;;
+r6fp3)  # fused-form plans from r6fs3: 70B TP1 batch 1 and Mixtral TP2 rank batch 1, same box
+  P70="10240x8192x1@16=1,1,9;8192x8192x1@16=1,1,9;8192x28672x1@16=1,2,1"
+  P8T2="3072x4096x1@16=1,4,0;4096x2048x1@16=1,1,0"
+  for r in 1 2; do
+    run "t1_base_$r" 300 $B --model llama3-70b --concurrency 1 --steps 40 --warmup 10
+    run "t1_new_$r" 300 env "XGS_TUNE=m64_plans=$P70" $B --model llama3-70b --concurrency 1 --steps 40 --warmup 10
+    run "mx2_base_$r" 300 $B --model mixtral-8x7b --tp-shard 2 --concurrency 1 --steps 100 --warmup 20
+    run "mx2_new_$r" 300 env "XGS_TUNE=m64_plans=$P8T2" $B --model mixtral-8x7b --tp-shard 2 --concurrency 1 --steps 100 --warmup 20
+  done ;;
 r6g8)  # 70B TP8 rank, batch 1: per-GEMM (by grid) kernel times under the fused decode layer (and A/B knobs)
   for v in base "fused_decode=0" "krot=0" "krot=2"; do
     n=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')
