@@ -160,6 +160,14 @@ r6fp3)  # fused-form plans from r6fs3: 70B TP1 batch 1 and Mixtral TP2 rank batc
     run "mx2_base_$r" 300 $B --model mixtral-8x7b --tp-shard 2 --concurrency 1 --steps 100 --warmup 20
     run "mx2_new_$r" 300 env "XGS_TUNE=m64_plans=$P8T2" $B --model mixtral-8x7b --tp-shard 2 --concurrency 1 --steps 100 --warmup 20
   done ;;
+r6sp)  # decode attention split cap at batch 1 (8B and one 70B TP8 rank), same box (SPLITS="16 8 4 2 1")
+  SPLITS=${SPLITS:-16 8 4 2 1}
+  for r in 1 2; do
+    for m in $SPLITS; do
+      run "c1_s${m}_$r" 200 env XGS_TUNE=decode_max_splits=$m $B --concurrency 1 --steps 300 --warmup 30
+      run "tp8_s${m}_$r" 300 env XGS_TUNE=decode_max_splits=$m $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
+    done
+  done ;;
 r6g8)  # 70B TP8 rank, batch 1: per-GEMM (by grid) kernel times under the fused decode layer (and A/B knobs)
   for v in base "fused_decode=0" "krot=0" "krot=2"; do
     n=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')
