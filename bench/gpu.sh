@@ -168,6 +168,22 @@ r6sp)  # decode attention split cap at batch 1 (8B and one 70B TP8 rank), same b
       run "tp8_s${m}_$r" 300 env XGS_TUNE=decode_max_splits=$m $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
     done
   done ;;
+r6rf)  # Mixtral batch 1: router inside the O launch (moe_route_fold) -- tests + same-box A/B
+  pyt rf_tests 900 tests/test_fused_decode_gpu.py tests/test_asm_invariants.py -k "route or mixtral or moe or m64g or gemm"
+  for r in 1 2; do
+    run "mix_c1_fold_$r" 250 $B --model mixtral-8x7b --concurrency 1 --steps 100 --warmup 20
+    run "mix_c1_nofold_$r" 250 env XGS_TUNE=moe_route_fold=0 $B --model mixtral-8x7b --concurrency 1 --steps 100 --warmup 20
+  done ;;
+r6rfp)  # Mixtral batch 1 kernel times with / without the router in the O launch
+  for v in "moe_route_fold=1" "moe_route_fold=0"; do
+    n=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')
+    raw=$(mktemp -d "${TMPDIR:-/tmp}/xgs_rf.XXXXXX")
+    XGS_TUNE=$v timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$raw" -o run -- \
+        python3 bench.py --steps 60 --warmup 20 --model mixtral-8x7b --concurrency 1 > "$o/bench_$n.log" 2>&1
+    tr=$(find "$raw" -name '*kernel_trace.csv' | sort | tail -n 1)
+    python3 bench/prof_summary.py "$tr" --window-ms 200 --by-grid > "$o/grid_$n.md"
+    rm -rf "$raw"
+  done ;;
 r6g8)  # 70B TP8 rank, batch 1: per-GEMM (by grid) kernel times under the fused decode layer (and A/B knobs)
   for v in base "fused_decode=0" "krot=0" "krot=2"; do
     n=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')
