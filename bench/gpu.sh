@@ -184,6 +184,14 @@ r6rfp)  # Mixtral batch 1 kernel times with / without the router in the O launch
     python3 bench/prof_summary.py "$tr" --window-ms 200 --by-grid > "$o/grid_$n.md"
     rm -rf "$raw"
   done ;;
+r6am)  # split-row greedy argmax: tests + end to end at batch 1 and 64 (before/after on one box is the next suite)
+  pyt am_tests 600 tests/test_kernels_gpu.py tests/test_engine_gpu.py -k "argmax or greedy or async or sample"
+  for r in 1 2; do
+    run "c1_$r" 200 $B --concurrency 1 --steps 300 --warmup 30
+    run "c1_old_$r" 200 env XGS_TUNE=argmax_split=0 $B --concurrency 1 --steps 300 --warmup 30
+    run "c64_$r" 250 $B --steps 300 --warmup 30
+    run "c64_old_$r" 250 env XGS_TUNE=argmax_split=0 $B --steps 300 --warmup 30
+  done ;;
 r6g8)  # 70B TP8 rank, batch 1: per-GEMM (by grid) kernel times under the fused decode layer (and A/B knobs)
   for v in base "fused_decode=0" "krot=0" "krot=2"; do
     n=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')

@@ -62,7 +62,9 @@ int decode_attention(const uint16_t*, int64_t, const uint16_t*, const uint16_t*,
                      float*, float*, uint16_t*, int64_t, int, int, int, int, int, float, int, hipStream_t);
 int prefill_attention(const uint16_t*, int64_t, const uint16_t*, const uint16_t*, const int32_t*, int, const int32_t*,
                       const int32_t*, uint16_t*, int64_t, int, int, int, int, int, int, float, hipStream_t, int);
-void argmax_logprob(const void*, int, int64_t, int, int, int32_t*, float*, hipStream_t);
+void argmax_logprob(const void*, int, int64_t, int, int, int32_t*, float*, hipStream_t, float* ws = nullptr,
+                    int* cnt = nullptr);
+int argmax_ws_floats_per_row();
 void sample_tokens(const void*, int, int64_t, int, int, const float*, const float*, const int32_t*, const uint64_t*,
                    uint64_t, int32_t*, float*, void*, hipStream_t);
 size_t sample_ws_row_bytes();
@@ -201,11 +203,16 @@ PYBIND11_MODULE(_kernels, m) {
   }, py::arg("q"), py::arg("qs"), py::arg("kc"), py::arg("vc"), py::arg("bt"), py::arg("bts"), py::arg("qsl"),
      py::arg("sl"), py::arg("out"), py::arg("os"), py::arg("ns"), py::arg("maxq"), py::arg("Hq"), py::arg("Hkv"),
      py::arg("D"), py::arg("bs"), py::arg("scale"), py::arg("st"), py::arg("gh") = 0);
+  // ws / cnt (optional): the split-row form -- B x argmax_ws_floats_per_row() floats and B zeroed
+  // ints (re-armed by every launch)
   m.def("argmax_logprob", [](uintptr_t logits, int is_f32, int64_t stride, int B, int V, uintptr_t tok, uintptr_t lp,
-                             uintptr_t st) {
-    xgk::argmax_logprob(P<const void>(logits), is_f32, stride, B, V, P<int32_t>(tok), P<float>(lp), S(st));
+                             uintptr_t st, uintptr_t ws, uintptr_t cnt) {
+    xgk::argmax_logprob(P<const void>(logits), is_f32, stride, B, V, P<int32_t>(tok), P<float>(lp), S(st), P<float>(ws),
+                        P<int>(cnt));
     check(0, "argmax_logprob");
-  });
+  }, py::arg("logits"), py::arg("is_f32"), py::arg("stride"), py::arg("B"), py::arg("V"), py::arg("tok"), py::arg("lp"),
+     py::arg("st"), py::arg("ws") = 0, py::arg("cnt") = 0);
+  m.def("argmax_ws_floats_per_row", []() { return xgk::argmax_ws_floats_per_row(); });
   m.def("sample_tokens", [](uintptr_t logits, int is_f32, int64_t stride, int B, int V, uintptr_t temps,
                             uintptr_t top_ps, uintptr_t top_ks, uintptr_t seeds, uint64_t step, uintptr_t tok,
                             uintptr_t lp, uintptr_t st, uintptr_t ws, int ws_rows) {

@@ -659,9 +659,106 @@ static void launch_sample_v2(const T* logits, int64_t stride, int B, int V, cons
                      seeds, step, ws, tok, lp);
 }
 
+// Split-row greedy path: ARG_PARTS workgroups of 256 threads per row each reduce a
+// contiguous slice (one batch of loads per thread at V = 128K), publish their (max,
+// argmax, log-sum-exp) write-through and take a ticket on the row; the row's last
+// arriver merges the slices in slice order (deterministic) and writes the token and its
+// logprob. One 1024-thread workgroup per row was latency-bound: 13.7 us per step at
+// batch 1 for a 256 KB row (128 exps per thread, two dependent load rounds).
+constexpr int ARG_PARTS = 8;
+template <typename T>
+__global__ void __launch_bounds__(256) argmax_split_kernel(const T* __restrict__ logits, int64_t stride, int V,
+                                                           int32_t* __restrict__ out_tok, float* __restrict__ out_lp,
+                                                           float4* __restrict__ ws, int* __restrict__ cnt) {
+  constexpr int W = VecW<T>::W;
+  constexpr int U = 8;
+  const int row = blockIdx.x / ARG_PARTS, part = blockIdx.x % ARG_PARTS;
+  const T* rp = logits + row * stride;
+  const int nv = V / W;
+  const int v0 = static_cast<int>(static_cast<int64_t>(nv) * part / ARG_PARTS);
+  const int v1 = static_cast<int>(static_cast<int64_t>(nv) * (part + 1) / ARG_PARTS);
+  ArgLse a{-INFINITY, 0x7fffffff, -INFINITY, 0.f};
+  for (int c0 = v0 + threadIdx.x; c0 < v1; c0 += U * blockDim.x) {
+    uint4 raw[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) raw[u] = ld16(rp + static_cast<int64_t>(min(c0 + u * (int)blockDim.x, v1 - 1)) * W);
+    float f[U][W];
+    float bm = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (W == 8) {
+        unpack8(raw[u], f[u]);
+      } else {
+        f[u][0] = __uint_as_float(raw[u].x); f[u][1] = __uint_as_float(raw[u].y);
+        f[u][2] = __uint_as_float(raw[u].z); f[u][3] = __uint_as_float(raw[u].w);
+      }
+      const bool ok = c0 + u * (int)blockDim.x < v1;
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        if (!ok) f[u][k] = -INFINITY;
+        const float x = f[u][k];
+        if (x > a.v) { a.v = x; a.i = (c0 + u * (int)blockDim.x) * W + k; }
+        bm = fmaxf(bm, x);
+      }
+    }
+    if (bm == -INFINITY) continue;
+    const float mn = fmaxf(a.m, bm);
+    float bs = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < W; ++k) bs += __expf(f[u][k] - mn);
+    a.s = (a.m == -INFINITY ? 0.f : a.s * __expf(a.m - mn)) + bs;
+    a.m = mn;
+  }
+  if (part == ARG_PARTS - 1) {  // the scalar tail past the last full vector
+    for (int i = nv * W + threadIdx.x; i < V; i += blockDim.x) {
+      const float x = scalar_at<T>(rp, i);
+      if (x > a.v) { a.v = x; a.i = i; }
+      if (x > a.m) { a.s = a.s * __expf(a.m - x) + 1.f; a.m = x; } else { a.s += __expf(x - a.m); }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ArgLse b{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64), __shfl_xor(a.m, o, 64), __shfl_xor(a.s, o, 64)};
+    a = merge(a, b);
+  }
+  __shared__ ArgLse red[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = a;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  ArgLse r = red[0];
+  for (int w = 1; w < 4; ++w) r = merge(r, red[w]);
+  st16_sc1(reinterpret_cast<float*>(ws + row * ARG_PARTS + part),
+           f32x4_t{r.v, __int_as_float(r.i), r.m, r.s});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (__hip_atomic_fetch_add(cnt + row, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ARG_PARTS - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  ArgLse m{-INFINITY, 0x7fffffff, -INFINITY, 0.f};
+  for (int q = 0; q < ARG_PARTS; ++q) {
+    const float4 v = ws[row * ARG_PARTS + q];
+    m = merge(m, ArgLse{v.x, __float_as_int(v.y), v.z, v.w});
+  }
+  __hip_atomic_store(cnt + row, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next launch
+  out_tok[row] = m.i;
+  if (out_lp) out_lp[row] = m.v - (m.m + __logf(m.s));
+}
+
+int argmax_ws_floats_per_row() { return 4 * ARG_PARTS; }
+
 void argmax_logprob(const void* logits, int is_f32, int64_t stride, int B, int V, int32_t* tok, float* lp,
-                    hipStream_t st) {
+                    hipStream_t st, float* ws, int* cnt) {
   if (B <= 0) return;
+  if (ws != nullptr && cnt != nullptr) {  // ws: B x ARG_PARTS float4; cnt: B zeroed ints
+    if (is_f32)
+      hipLaunchKernelGGL(argmax_split_kernel<float>, dim3(B * ARG_PARTS), dim3(256), 0, st, (const float*)logits,
+                         stride, V, tok, lp, reinterpret_cast<float4*>(ws), cnt);
+    else
+      hipLaunchKernelGGL(argmax_split_kernel<uint16_t>, dim3(B * ARG_PARTS), dim3(256), 0, st,
+                         (const uint16_t*)logits, stride, V, tok, lp, reinterpret_cast<float4*>(ws), cnt);
+    return;
+  }
   if (is_f32)
     hipLaunchKernelGGL(argmax_kernel<float>, dim3(B), dim3(1024), 0, st, (const float*)logits, stride, V, tok, lp);
   else

@@ -209,13 +209,22 @@ def test_prefill_attention_spike_forces_rescale():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("V", [128256, 50257, 32000])
+@pytest.mark.parametrize("V", [128256, 50257, 32000, 1000, 16387])
 def test_argmax_logprob(dtype, V):
-    logits = rnd(9, V, scale=3.0, dtype=dtype)
-    tok, lp = ops.argmax_logprob(logits)
-    rt, rl = ops.argmax_logprob_ref(logits.cpu())
-    assert torch.equal(tok.cpu(), rt)
-    torch.testing.assert_close(lp.cpu(), rl, atol=1e-3, rtol=1e-3)
+    """V >= 16K: the split-row kernel (8 slices, last arriver merges); three launches in
+    a row (the per-row tickets must re-arm); ties go to the lowest index."""
+    from xgserve.ops import sampling as SP
+    for it in range(3):
+        logits = rnd(9, V, scale=3.0, dtype=dtype)
+        if it == 2:  # a tie across two slices: the lower index wins
+            logits[3, V // 3] = logits[3, V - 2] = logits[3].max() + 1
+        tok, lp = ops.argmax_logprob(logits)
+        rt, rl = ops.argmax_logprob_ref(logits.cpu())
+        assert torch.equal(tok.cpu(), rt)
+        torch.testing.assert_close(lp.cpu(), rl, atol=1e-3, rtol=1e-3)
+    if V >= SP.ARGMAX_SPLIT_MIN_V:
+        torch.cuda.synchronize()
+        assert int(SP._argmax_ws(logits.device, 9)[1].abs().sum()) == 0
 
 
 def test_sample_tokens_greedy_and_distribution():

@@ -15,9 +15,32 @@ def argmax_logprob_ref(logits: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor
     return tok.to(torch.int32), lp
 
 
+_ARGMAX_WS = {}
+_ARGMAX_WS_RETIRED = []
+# below this a row is one workgroup's work anyway; XGS_TUNE argmax_split=0: always the
+# one-workgroup-per-row kernel (A/B)
+ARGMAX_SPLIT_MIN_V = 16384 if __import__("xgserve.tune", fromlist=["get_bool"]).get_bool("argmax_split", True) else 1 << 62
+
+
+def _argmax_ws(device, B: int):
+    """Split-row argmax scratch: per-slice partials and zeroed per-row tickets (every
+    launch's last arriver re-arms its row), grown on demand, kept alive for captured graphs."""
+    key = str(device)
+    ws = _ARGMAX_WS.get(key)
+    if ws is None or ws[1].numel() < B:
+        if ws is not None:
+            _ARGMAX_WS_RETIRED.append(ws)
+        n = max(B, 64)
+        ws = _ARGMAX_WS[key] = (torch.empty(n * kernels().argmax_ws_floats_per_row(), dtype=torch.float32,
+                                            device=device),
+                                torch.zeros(n, dtype=torch.int32, device=device))
+    return ws
+
+
 def argmax_logprob(logits: torch.Tensor, out_tok: Optional[torch.Tensor] = None,
                    out_lp: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Greedy token + its log-probability per row of a [B, V] logits matrix."""
+    """Greedy token + its log-probability per row of a [B, V] logits matrix. Large
+    vocabularies take the split-row kernel (8 workgroups per row, last arriver merges)."""
     if not use_native(logits):
         t, lp = argmax_logprob_ref(logits)
         return t, lp
@@ -27,8 +50,12 @@ def argmax_logprob(logits: torch.Tensor, out_tok: Optional[torch.Tensor] = None,
         out_tok = torch.empty(B, dtype=torch.int32, device=logits.device)
     if out_lp is None:
         out_lp = torch.empty(B, dtype=torch.float32, device=logits.device)
+    ws = cnt = 0
+    if V >= ARGMAX_SPLIT_MIN_V:
+        w, c = _argmax_ws(logits.device, B)
+        ws, cnt = w.data_ptr(), c.data_ptr()
     kernels().argmax_logprob(logits.data_ptr(), 1 if logits.dtype == torch.float32 else 0, logits.stride(0), B, V,
-                             out_tok.data_ptr(), out_lp.data_ptr(), stream_ptr())
+                             out_tok.data_ptr(), out_lp.data_ptr(), stream_ptr(), ws, cnt)
     return out_tok, out_lp
 
 

@@ -13,6 +13,7 @@ Keys (default in brackets; every default is the production setting):
                            0 = library GEMMs, or a list "qkv,o,gate_up,down" of those allowed
   pf_windows [gate_up:448-576/down:513-576]   step sizes (tokens) per projection that take gemm_pf
   moe_pf [1]               prompt-sized expert GEMMs (> 256 token-expert pairs) on gemm_pf's grouped form
+  argmax_split [1]         greedy argmax over large vocabularies: 8 workgroups per row
   moe_w2_small [1]         decode-sized w2 (<= 8 token-expert pairs) on 64-column tiles, 2 splits
   krot [1]                 K-chunk rotation of the weight-streaming GEMMs (0 / 1 / 2)
   m64_plans / mw_plans     gemm_m64g / gemm_mw plan overrides, "NxKxMODE@BUCKET=...;..."
@@ -35,7 +36,7 @@ from __future__ import annotations
 import os
 from typing import Dict
 
-KEYS = {"fused_decode", "async_sched", "early_release", "spin_wait", "pf", "pf_windows", "moe_pf", "moe_w2_small", "gemm_ar", "gemm_ar_shared", "small_m_tiles", "krot", "m64_plans", "mw_plans",
+KEYS = {"fused_decode", "async_sched", "early_release", "spin_wait", "pf", "pf_windows", "moe_pf", "moe_w2_small", "argmax_split", "gemm_ar", "gemm_ar_shared", "small_m_tiles", "krot", "m64_plans", "mw_plans",
         "mw_max_tokens", "resid_inlaunch_kb", "decode_depth", "decode_max_splits", "ar_ll_max", "sim_ar_us",
         "tp_overlap_chunks", "tp_overlap_min_tokens", "ep_exact_min_pairs"}
 
