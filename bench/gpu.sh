@@ -192,6 +192,23 @@ r6am)  # split-row greedy argmax: tests + end to end at batch 1 and 64 (before/a
     run "c64_$r" 250 $B --steps 300 --warmup 30
     run "c64_old_$r" 250 env XGS_TUNE=argmax_split=0 $B --steps 300 --warmup 30
   done ;;
+r6lm)  # LM head at batch 1 / 64: hipBLASLt vs gemm_m64g (bf16 logits), cold weights
+  run lm 200 python -u bench/gemm_bench.py --shapes lm_head --M 1 16 64 ;;
+r6lh)  # decode LM head on gemm_m64g vs hipBLASLt, same box
+  pyt lh_tests 600 tests/test_engine_gpu.py tests/test_skinny_gpu.py -k "logits or greedy or lm_head or reference"
+  for r in 1 2; do
+    run "c1_m64_$r" 200 $B --concurrency 1 --steps 300 --warmup 30
+    run "c1_lib_$r" 200 env XGS_TUNE=lm_head_m64=0 $B --concurrency 1 --steps 300 --warmup 30
+    run "c64_m64_$r" 250 $B --steps 300 --warmup 30
+    run "c64_lib_$r" 250 env XGS_TUNE=lm_head_m64=0 $B --steps 300 --warmup 30
+  done ;;
+r6lhp)  # batch 1 with the LM head on gemm_m64g: kernel times by grid
+  raw=$(mktemp -d "${TMPDIR:-/tmp}/xgs_lh.XXXXXX")
+  timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$raw" -o run -- \
+      python3 bench.py --steps 60 --warmup 20 --concurrency 1 > "$o/bench.log" 2>&1
+  tr=$(find "$raw" -name '*kernel_trace.csv' | sort | tail -n 1)
+  python3 bench/prof_summary.py "$tr" --window-ms 200 --by-grid > "$o/grid.md"
+  rm -rf "$raw" ;;
 r6g8)  # 70B TP8 rank, batch 1: per-GEMM (by grid) kernel times under the fused decode layer (and A/B knobs)
   for v in base "fused_decode=0" "krot=0" "krot=2"; do
     n=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')
