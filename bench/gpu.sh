@@ -209,6 +209,14 @@ r6lhp)  # batch 1 with the LM head on gemm_m64g: kernel times by grid
   tr=$(find "$raw" -name '*kernel_trace.csv' | sort | tail -n 1)
   python3 bench/prof_summary.py "$tr" --window-ms 200 --by-grid > "$o/grid.md"
   rm -rf "$raw" ;;
+r6qo)  # mixed steps: QKV / O on gemm_pf at 513-576 rows (fp32 partials into their consumers), same box
+  W0="gate_up:448-576/down:513-576"
+  for r in 1 2; do
+    run "base_$r" 250 $B --steps 300 --warmup 30
+    run "o_$r" 250 env "XGS_TUNE=pf_windows=$W0/o:513-576" $B --steps 300 --warmup 30
+    run "qkv_$r" 250 env "XGS_TUNE=pf_windows=$W0/qkv:513-576" $B --steps 300 --warmup 30
+    run "qkvo_$r" 250 env "XGS_TUNE=pf_windows=$W0/qkv:513-576/o:513-576" $B --steps 300 --warmup 30
+  done ;;
 r6g8)  # 70B TP8 rank, batch 1: per-GEMM (by grid) kernel times under the fused decode layer (and A/B knobs)
   for v in base "fused_decode=0" "krot=0" "krot=2"; do
     n=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')
