@@ -139,7 +139,7 @@ r6c1)  # 8B batch 1: runner-up fused-form plans (r6fs) end to end, same box
     run "c1_gu219_$r" 200 env "XGS_TUNE=m64_plans=28672x4096x2@16=2,1,9" $B --concurrency 1 --steps 300 --warmup 30
   done ;;
 r6mo)  # Mixtral decode expert GEMMs in the fused forms (w13 SiLU, w2 + combine into the residual): sweep
-  run mo_sweep 400 python -u bench/moe_fused_bench.py --T 1 4 16 ;;
+  run mo_sweep 600 python -u bench/moe_fused_bench.py --T ${MO_T:-1 4 16} ;;
 r6mw)  # Mixtral: decode-sized w2 on 64-column tiles (moe_w2_small) -- tests + same-box end-to-end A/B
   pyt mw_tests 600 tests/test_fused_decode_gpu.py tests/test_kernels_gpu.py -k "moe or mixtral or expert"
   for r in 1 2; do
@@ -216,6 +216,23 @@ r6qo)  # mixed steps: QKV / O on gemm_pf at 513-576 rows (fp32 partials into the
     run "o_$r" 250 env "XGS_TUNE=pf_windows=$W0/o:513-576" $B --steps 300 --warmup 30
     run "qkv_$r" 250 env "XGS_TUNE=pf_windows=$W0/qkv:513-576" $B --steps 300 --warmup 30
     run "qkvo_$r" 250 env "XGS_TUNE=pf_windows=$W0/qkv:513-576/o:513-576" $B --steps 300 --warmup 30
+  done ;;
+r6mx)  # Mixtral 64 / 8 concurrent: w2 64-column tiles up to 128 pairs, w13 cfg 3 from 64 pairs (same box)
+  for r in 1 2; do
+    run "c64_base_$r" 300 $B --model mixtral-8x7b --steps 60 --warmup 20
+    run "c64_w2_$r" 300 env XGS_TUNE=moe_w2_small_pairs=128 $B --model mixtral-8x7b --steps 60 --warmup 20
+    run "c64_w13_$r" 300 env XGS_TUNE=moe_w13_big_pairs=64 $B --model mixtral-8x7b --steps 60 --warmup 20
+    run "c64_both_$r" 300 env "XGS_TUNE=moe_w2_small_pairs=128|moe_w13_big_pairs=64" $B --model mixtral-8x7b --steps 60 --warmup 20
+    run "c8_base_$r" 250 $B --model mixtral-8x7b --concurrency 8 --steps 100 --warmup 20
+    run "c8_w2_$r" 250 env XGS_TUNE=moe_w2_small_pairs=128 $B --model mixtral-8x7b --concurrency 8 --steps 100 --warmup 20
+  done ;;
+r6mx2)  # MoE decode plans as adopted: tests + Mixtral TP1 c64 / c1 and one Mixtral TP2/EP2 rank c64, same box
+  pyt mx_tests 900 tests/test_fused_decode_gpu.py tests/test_kernels_gpu.py tests/test_tp_gpu.py -k "moe or mixtral or expert or ep"
+  for r in 1 2; do
+    run "c64_new_$r" 300 $B --model mixtral-8x7b --steps 60 --warmup 20
+    run "c64_old_$r" 300 env XGS_TUNE=moe_w2_small=0 $B --model mixtral-8x7b --steps 60 --warmup 20
+    run "ep2_new_$r" 300 $B --model mixtral-8x7b --tp-shard 2 --steps 60 --warmup 20
+    run "ep2_old_$r" 300 env XGS_TUNE=moe_w2_small=0 $B --model mixtral-8x7b --tp-shard 2 --steps 60 --warmup 20
   done ;;
 r6g8)  # 70B TP8 rank, batch 1: per-GEMM (by grid) kernel times under the fused decode layer (and A/B knobs)
   for v in base "fused_decode=0" "krot=0" "krot=2"; do

@@ -289,7 +289,9 @@ def test_moe_route_norm_and_combine_resid(T):
             ss = torch.full((64 * T,), -1.0, device=DEV)
             n = ops.fused_moe(hn, w13, w2, w, ids, resid=r, ss=ss, counters=counters if use_ctr else None)
             from xgserve.ops import moe as MO
-            tile = 64 if (MO.MOE_W2_SMALL and T * k <= MO.MOE_W2_SMALL_PAIRS) else 128  # decode-sized w2 tiles
+            pairs = T * k
+            small = pairs <= MO.MOE_W2_SMALL_LOW or MO.MOE_W2_SMALL_HIGH <= pairs <= MO.MOE_PREFILL_PAIRS
+            tile = 64 if (MO.MOE_W2_SMALL and small) else 128  # decode-sized w2 tiles
             assert n == (H // tile if use_ctr else H // 1024)
             want = (resid.float() + out.float()).bfloat16()
             assert rel_err(r, want) < 1e-2

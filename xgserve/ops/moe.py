@@ -29,14 +29,21 @@ MOE_CFG_W13_PREFILL = 3
 # gemm_pf_grouped): one MFMA tile of 192-288 rows covers an expert's rows, so each
 # expert's weights stream once per step (profiles/r5_moe_pf.md). XGS_TUNE moe_pf=0: off.
 MOE_PF = __import__("xgserve.tune", fromlist=["get_bool"]).get_bool("moe_pf", True)
-# decode-sized w2 (<= 8 token-expert pairs) in its fused form (combine into the
-# residual in the launch): 64-column tiles on the 4-wave nt config, 2 K splits --
-# bench/moe_fused_bench.py, profiles/r6/r6_moe_w2.md (T = 1 / 4: 39.1 / 109.3 us vs
-# 40.5 / 114+ for the 128-column tiles; Mixtral batch 1 5.12 -> 5.07 ms; 16 pairs
-# (batch 8) measured no gain end to end, so larger steps keep the 128-column tiles).
-# XGS_TUNE moe_w2_small=0 restores the 128-column tiles and their splits (A/B).
+# decode-sized w2 in its fused form (combine into the residual in the launch) on 64-column
+# tiles with the 4-wave nt config: steps of <= 8 token-expert pairs (2 K splits) and of
+# 64-256 pairs (1 split). bench/moe_fused_bench.py, profiles/r6/r6_moe_w2.md: T = 1 / 4 /
+# 32 / 64 at 39.1 / 109.3 / 144.8 / 156.6 us vs 40.5 / 114+ / 153.0 / 166.6 for the
+# 128-column tiles; end to end Mixtral batch 1 5.12 -> 5.07 ms, 64 concurrent 19.83 ->
+# 19.53 ms (with w13 on cfg 3 from 64 pairs: 19.41 ms). 16 pairs (batch 8) measured
+# 0.4 % slower, so 9-63 pairs keep the 128-column tiles. XGS_TUNE moe_w2_small=0:
+# the 128-column tiles everywhere and w13 on cfg 5 (A/B).
 MOE_W2_SMALL = __import__("xgserve.tune", fromlist=["get_bool"]).get_bool("moe_w2_small", True)
-MOE_W2_SMALL_PAIRS = 8
+MOE_W2_SMALL_LOW = 8     # <= this many pairs
+MOE_W2_SMALL_HIGH = 64   # >= this many pairs (and <= MOE_PREFILL_PAIRS)
+# w13 of decode-sized steps from this many pairs up on cfg 3 (swept fastest at T = 64:
+# 290.5 vs 297.0 us for cfg 5)
+MOE_W13_BIG_PAIRS = 64
+MOE_CFG_W13_BIG = 3
 
 
 def _moe_pf_cfg(pairs: int, E: int) -> int:
@@ -211,7 +218,8 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     # stops there instead of at the capacity P / 64
     def gemm(*a, cfg=0):
         kn.moe_gemm_m64g_rows(*a[:-1], cfg, max_rows, a[-1], valid, T * k)
-    cfg13 = ((MOE_CFG_W13_PREFILL if T * k > MOE_PREFILL_PAIRS else MOE_CFG_W13)
+    cfg13 = ((MOE_CFG_W13_PREFILL if T * k > MOE_PREFILL_PAIRS else
+              MOE_CFG_W13_BIG if MOE_W2_SMALL and T * k >= MOE_W13_BIG_PAIRS else MOE_CFG_W13)
              if (H % 64 == 0 and F2 % 128 == 0) else 0)
     gemm(x.contiguous().data_ptr(), sorted_rows.data_ptr(), offs.data_ptr(), E, H, w13.data_ptr(), F2, P, 0,
          act.data_ptr(), 1, 2, 2, stream_ptr(), cfg=cfg13)
@@ -220,10 +228,11 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     cfg2 = (MOE_CFG_W2_PREFILL if T * k > MOE_PREFILL_PAIRS else MOE_CFG_W2) if nw2 == 2 else 0
     kc2 = 128
     S = 1
-    small = MOE_W2_SMALL and T * k <= MOE_W2_SMALL_PAIRS and H % 64 == 0 and H // 64 <= 64
+    small = (MOE_W2_SMALL and (T * k <= MOE_W2_SMALL_LOW or MOE_W2_SMALL_HIGH <= T * k <= MOE_PREFILL_PAIRS)
+             and H % 64 == 0 and H // 64 <= 64)
     if small:
         nw2, cfg2 = 1, MOE_CFG_W2
-    for sk in ((2,) if small else (4, 2) if T * k <= 4 else (2,) if T * k <= 16 else ()):
+    for sk in (((2,) if T * k <= 8 else ()) if small else (4, 2) if T * k <= 4 else (2,) if T * k <= 16 else ()):
         if F % (sk * kc2) == 0 and F % (sk * 256) == 0:
             S = sk
             break

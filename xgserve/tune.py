@@ -14,7 +14,7 @@ Keys (default in brackets; every default is the production setting):
   pf_windows [gate_up:448-576/down:513-576]   step sizes (tokens) per projection that take gemm_pf
   moe_pf [1]               prompt-sized expert GEMMs (> 256 token-expert pairs) on gemm_pf's grouped form
   argmax_split [1]         greedy argmax over large vocabularies: 8 workgroups per row
-  moe_w2_small [1]         decode-sized w2 (<= 8 token-expert pairs) on 64-column tiles, 2 splits
+  moe_w2_small [1]         decode-sized w2 on 64-column tiles (<= 8 and 64-256 token-expert pairs)
   krot [1]                 K-chunk rotation of the weight-streaming GEMMs (0 / 1 / 2)
   m64_plans / mw_plans     gemm_m64g / gemm_mw plan overrides, "NxKxMODE@BUCKET=...;..."
   mw_max_tokens [320]      largest step on gemm_mw
