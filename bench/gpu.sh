@@ -234,6 +234,14 @@ r6mx2)  # MoE decode plans as adopted: tests + Mixtral TP1 c64 / c1 and one Mixt
     run "ep2_new_$r" 300 $B --model mixtral-8x7b --tp-shard 2 --steps 60 --warmup 20
     run "ep2_old_$r" 300 env XGS_TUNE=moe_w2_small=0 $B --model mixtral-8x7b --tp-shard 2 --steps 60 --warmup 20
   done ;;
+r6p512)  # prefill attention at 512 / 576-token prompts: every configuration (8B heads)
+  run p512 300 python -u bench/prefill_bench.py --lens 512 576 1024 --no-ttft --gh 0 -1282 -1284 -1281 -242 -241 -244 -82 -81 -84 -42 -41 -44 ;;
+r6t1c64)  # 70B TP1, 64 concurrent: bucket-64 plans from the fused-form sweep (r6fs4), same box
+  P="10240x8192x1@64=1,3,7;8192x8192x1@64=1,2,1;8192x28672x1@64=2,4,1"
+  for r in 1 2; do
+    run "base_$r" 400 $B --model llama3-70b --steps 40 --warmup 10
+    run "new_$r" 400 env "XGS_TUNE=m64_plans=$P" $B --model llama3-70b --steps 40 --warmup 10
+  done ;;
 r6g8)  # 70B TP8 rank, batch 1: per-GEMM (by grid) kernel times under the fused decode layer (and A/B knobs)
   for v in base "fused_decode=0" "krot=0" "krot=2"; do
     n=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')

@@ -110,11 +110,12 @@ _M64_TUNED = {
     (28672, 4096, MODE_SILU): {64: (2, 1, 1), 32: (2, 1, 3), 16: (2, 1, 3)},
     (4096, 14336, MODE_PARTIAL): {64: (2, 8, 3), 32: (1, 4, 1), 16: (1, 4, 9)},
     # Llama-3-70B TP1
-    # bucket 16 of qkv / o / down: the fused-form sweep (r6/r6_fused_plans.md; batch 1 23.2 -> 22.5 ms)
-    (10240, 8192, MODE_PARTIAL): {64: (2, 2, 1), 16: (1, 1, 9)},
-    (8192, 8192, MODE_PARTIAL): {64: (2, 8, 7), 32: (2, 8, 7), 16: (1, 1, 9)},  # 8-wave tile: 23.3 vs 24.8-25.7 us
+    # buckets 16 / 64 of qkv / o / down: the fused-form sweep (r6/r6_fused_plans.md; batch 1 23.2 -> 22.5 ms,
+    # 64 concurrent 38.1 -> 37.9 ms)
+    (10240, 8192, MODE_PARTIAL): {64: (1, 3, 7), 16: (1, 1, 9)},
+    (8192, 8192, MODE_PARTIAL): {64: (1, 2, 1), 32: (2, 8, 7), 16: (1, 1, 9)},  # 8-wave tile: 23.3 vs 24.8-25.7 us
     (57344, 8192, MODE_SILU): {64: (2, 1, 7), 32: (2, 1, 7), 16: (2, 1, 7)},  # 8-wave tile: 148 vs 166-178 us
-    (8192, 28672, MODE_PARTIAL): {64: (2, 4, 3), 16: (1, 2, 1)},
+    (8192, 28672, MODE_PARTIAL): {64: (2, 4, 1), 16: (1, 2, 1)},
     # 70B shards re-swept with K rotation in round 4 at M = 1 / 64 (profiles/r4_m64g_sweep_tp.jsonl)
     # TP shards (Llama-3-8B / Mixtral attention TP2/4/8, Llama-3-70B TP2/4/8), re-swept at
     # M = 1 / 16 (bucket 16: best sum), 32, 64 (profiles/r2_tp_shard_sweep.jsonl); gate_up
