@@ -168,22 +168,6 @@ r6sp)  # decode attention split cap at batch 1 (8B and one 70B TP8 rank), same b
       run "tp8_s${m}_$r" 300 env XGS_TUNE=decode_max_splits=$m $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20
     done
   done ;;
-r6rf)  # Mixtral batch 1: router inside the O launch (moe_route_fold) -- tests + same-box A/B
-  pyt rf_tests 900 tests/test_fused_decode_gpu.py tests/test_asm_invariants.py -k "route or mixtral or moe or m64g or gemm"
-  for r in 1 2; do
-    run "mix_c1_fold_$r" 250 $B --model mixtral-8x7b --concurrency 1 --steps 100 --warmup 20
-    run "mix_c1_nofold_$r" 250 env XGS_TUNE=moe_route_fold=0 $B --model mixtral-8x7b --concurrency 1 --steps 100 --warmup 20
-  done ;;
-r6rfp)  # Mixtral batch 1 kernel times with / without the router in the O launch
-  for v in "moe_route_fold=1" "moe_route_fold=0"; do
-    n=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')
-    raw=$(mktemp -d "${TMPDIR:-/tmp}/xgs_rf.XXXXXX")
-    XGS_TUNE=$v timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$raw" -o run -- \
-        python3 bench.py --steps 60 --warmup 20 --model mixtral-8x7b --concurrency 1 > "$o/bench_$n.log" 2>&1
-    tr=$(find "$raw" -name '*kernel_trace.csv' | sort | tail -n 1)
-    python3 bench/prof_summary.py "$tr" --window-ms 200 --by-grid > "$o/grid_$n.md"
-    rm -rf "$raw"
-  done ;;
 r6am)  # split-row greedy argmax: tests + end to end at batch 1 and 64 (before/after on one box is the next suite)
   pyt am_tests 600 tests/test_kernels_gpu.py tests/test_engine_gpu.py -k "argmax or greedy or async or sample"
   for r in 1 2; do
@@ -194,21 +178,6 @@ r6am)  # split-row greedy argmax: tests + end to end at batch 1 and 64 (before/a
   done ;;
 r6lm)  # LM head at batch 1 / 64: hipBLASLt vs gemm_m64g (bf16 logits), cold weights
   run lm 200 python -u bench/gemm_bench.py --shapes lm_head --M 1 16 64 ;;
-r6lh)  # decode LM head on gemm_m64g vs hipBLASLt, same box
-  pyt lh_tests 600 tests/test_engine_gpu.py tests/test_skinny_gpu.py -k "logits or greedy or lm_head or reference"
-  for r in 1 2; do
-    run "c1_m64_$r" 200 $B --concurrency 1 --steps 300 --warmup 30
-    run "c1_lib_$r" 200 env XGS_TUNE=lm_head_m64=0 $B --concurrency 1 --steps 300 --warmup 30
-    run "c64_m64_$r" 250 $B --steps 300 --warmup 30
-    run "c64_lib_$r" 250 env XGS_TUNE=lm_head_m64=0 $B --steps 300 --warmup 30
-  done ;;
-r6lhp)  # batch 1 with the LM head on gemm_m64g: kernel times by grid
-  raw=$(mktemp -d "${TMPDIR:-/tmp}/xgs_lh.XXXXXX")
-  timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$raw" -o run -- \
-      python3 bench.py --steps 60 --warmup 20 --concurrency 1 > "$o/bench.log" 2>&1
-  tr=$(find "$raw" -name '*kernel_trace.csv' | sort | tail -n 1)
-  python3 bench/prof_summary.py "$tr" --window-ms 200 --by-grid > "$o/grid.md"
-  rm -rf "$raw" ;;
 r6qo)  # mixed steps: QKV / O on gemm_pf at 513-576 rows (fp32 partials into their consumers), same box
   W0="gate_up:448-576/down:513-576"
   for r in 1 2; do
@@ -216,15 +185,6 @@ r6qo)  # mixed steps: QKV / O on gemm_pf at 513-576 rows (fp32 partials into the
     run "o_$r" 250 env "XGS_TUNE=pf_windows=$W0/o:513-576" $B --steps 300 --warmup 30
     run "qkv_$r" 250 env "XGS_TUNE=pf_windows=$W0/qkv:513-576" $B --steps 300 --warmup 30
     run "qkvo_$r" 250 env "XGS_TUNE=pf_windows=$W0/qkv:513-576/o:513-576" $B --steps 300 --warmup 30
-  done ;;
-r6mx)  # Mixtral 64 / 8 concurrent: w2 64-column tiles up to 128 pairs, w13 cfg 3 from 64 pairs (same box)
-  for r in 1 2; do
-    run "c64_base_$r" 300 $B --model mixtral-8x7b --steps 60 --warmup 20
-    run "c64_w2_$r" 300 env XGS_TUNE=moe_w2_small_pairs=128 $B --model mixtral-8x7b --steps 60 --warmup 20
-    run "c64_w13_$r" 300 env XGS_TUNE=moe_w13_big_pairs=64 $B --model mixtral-8x7b --steps 60 --warmup 20
-    run "c64_both_$r" 300 env "XGS_TUNE=moe_w2_small_pairs=128|moe_w13_big_pairs=64" $B --model mixtral-8x7b --steps 60 --warmup 20
-    run "c8_base_$r" 250 $B --model mixtral-8x7b --concurrency 8 --steps 100 --warmup 20
-    run "c8_w2_$r" 250 env XGS_TUNE=moe_w2_small_pairs=128 $B --model mixtral-8x7b --concurrency 8 --steps 100 --warmup 20
   done ;;
 r6mx2)  # MoE decode plans as adopted: tests + Mixtral TP1 c64 / c1 and one Mixtral TP2/EP2 rank c64, same box
   pyt mx_tests 900 tests/test_fused_decode_gpu.py tests/test_kernels_gpu.py tests/test_tp_gpu.py -k "moe or mixtral or expert or ep"
@@ -254,23 +214,6 @@ r6g8)  # 70B TP8 rank, batch 1: per-GEMM (by grid) kernel times under the fused 
     rm -rf "$raw"
     tail -n 1 "$o/bench_$n.log" | cut -c1-200
   done ;;
-r6pp)  # prefill attention ping-pong form (waves 4-7 half a tile behind): tests + kernel A/B at 2K / 8K + 8K TTFT
-  pyt pp_tests 600 tests/test_kernels_gpu.py -k "prefill"
-  run pp_attn 300 python -u bench/prefill_bench.py --lens 2048 8192 --gh 0 -382 -482 -384 -484 --no-ttft ;;
-r6po)  # prefill attention OPT variants (K 8-ahead, softmax split, page prefetch), alternating order at 8K
-  pyt po_tests 600 tests/test_kernels_gpu.py -k "prefill"
-  run po_attn 400 python -u bench/prefill_bench.py --lens 8192 --no-ttft --gh -382 -10382 -20382 -40382 -70382 -382 -10382 -20382 -40382 -70382 -384 -70384 -384 -70384 ;;
-r6l)  # static-count K/V refills in the decode key loop (exact vmcnt per register tile): tests + same-box A/B vs depth 5
-  pyt l_tests 900 tests/test_fused_decode_gpu.py tests/test_kernels_gpu.py -k "decode or attention"
-  run l_cold 200 python -u bench/decode_cold.py --graph --depth 2 5 --splits 1 2 4
-  run l_cold_2k 200 python -u bench/decode_cold.py --graph --L 2048 --caches 3 --depth 2 5 --splits 1 2
-  for r in 1 2; do
-    run "c64_sl_$r" 250 $B --steps 300 --warmup 30
-    run "c64_nosl_$r" 250 env XGS_TUNE=decode_depth=5 $B --steps 300 --warmup 30
-    run "c1_sl_$r" 200 $B --concurrency 1 --steps 300 --warmup 30
-    run "c1_nosl_$r" 200 env XGS_TUNE=decode_depth=5 $B --concurrency 1 --steps 300 --warmup 30
-  done
-  run tp8_c1 300 $B --model llama3-70b --tp-shard 8 --concurrency 1 --steps 100 --warmup 20 ;;
 r6e)  # split QKV prologue in decode attention (partials issued ahead of the K/V preloads): tests + same-box A/B vs depth 4 (classic)
   pyt e_tests 600 tests/test_fused_decode_gpu.py
   run e_cold 200 python -u bench/decode_cold.py --graph --depth 2 4 3 --splits 1 2 4
