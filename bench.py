@@ -273,12 +273,15 @@ def main():
     def run_step():
         if step_log is not None:
             t0, c0 = time.perf_counter(), dict(eng.stats_counters)
+            p0 = dict(eng._timing) if eng._timing is not None else None
         outs = eng.step()
         now = time.perf_counter()
         if step_log is not None:
             c1 = eng.stats_counters
             step_log.append((round(1000 * (now - t0), 3), c1["prefill_tokens_computed"] - c0["prefill_tokens_computed"],
-                             c1["decode_steps"] - c0["decode_steps"], c1["generation_tokens"] - c0["generation_tokens"]))
+                             c1["decode_steps"] - c0["decode_steps"], c1["generation_tokens"] - c0["generation_tokens"],
+                             None if p0 is None else {k: round(1000 * (v - p0.get(k, 0.0)), 3)
+                                                      for k, v in eng._timing.items()}))
         n_tok = 0
         for o in outs:
             n_tok += len(o.new_token_ids)
@@ -326,7 +329,7 @@ def main():
         with open(os.environ["XGS_STEP_LOG"], "w") as f:
             for i, e in enumerate(step_log):
                 f.write(json.dumps({"i": i, "timed": i >= a.warmup, "ms": e[0], "prefill_tokens": e[1],
-                                    "decode_step": e[2], "gen_tokens": e[3]}) + "\n")
+                                    "decode_step": e[2], "gen_tokens": e[3], "phases_ms": e[4]}) + "\n")
     ttfts = [first_tok[r] - arrival[r] for r in first_tok if r not in first_before]
     p50_local = float(np.median(ttfts)) if ttfts else float("nan")
 
